@@ -1,0 +1,272 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident Reed-Solomon encode on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): 4 data + 2 parity shards, 1 MiB per shard,
+4096 stripes per GPU, all resident in HBM ([stripe][shard][1 MiB], 24 GiB per
+GPU) before timing starts.  One step = one rs_encode_batch_dev call over the
+whole batch (one kernel launch).  N GPUs = N independent processes, each
+encoding its own 4096 stripes (stripes are independent: no collective on the
+data path; torch.distributed is used only for the timing barrier and the max
+over ranks).  value = user data protected per second over all GPUs =
+N * k * S * B * steps / t  (GiB/s).
+
+Also reported (rank 0): decode rates for 1 and 2 erasures, the device copy
+kernel rate, the roofline of the encode kernel (HIP events on the launch
+stream), and the CPU baseline -- the oracle's scalar restatement of the
+reference loop (InputOutputByteTableCodingLoop.java:12-44) timed on a bounded
+sample on this host.
+
+Run:  python bench.py [--gpus N --steps K --warmup W]
+      (N > 1 is launched by torch.distributed.run, one rank per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.join(ROOT, "java-reed-solomon-distributed-file-system_amd")
+sys.path.insert(0, PKG_DIR)
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+SEED = 0x5EED
+METRIC = "RS encode/decode GiB/s device-resident, 4+2×1 MiB stripes, at 1/2/4/8 GPU"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--k", type=int, default=4)
+    ap.add_argument("--m", type=int, default=2)
+    ap.add_argument("--shard-bytes", type=int, default=1 << 20)
+    ap.add_argument("--stripes", type=int, default=4096, help="stripes per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-extras", action="store_true", help="skip decode/copy/host-inclusive/CPU legs")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    import rsamd
+    from rsamd import device as rdev
+    from rsamd.device import StripeLayout
+
+    k, m, S, B = args.k, args.m, args.shard_bytes, args.stripes
+    rs = rsamd.ReedSolomon.create(k, m)
+    lay = StripeLayout.packed(B, k + m, S)
+    buf = torch.empty(lay.nbytes, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream()
+    rdev.fill_synthetic(buf.data_ptr(), k, lay, SEED, stripe0=rank * B, stream=stream)
+    torch.cuda.synchronize()
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    def step():
+        rdev.encode(rs, buf.data_ptr(), lay, stream)
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    # Per-launch HIP events on the launch stream (the kernel's own duration).
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for s, e in evs:
+        s.record(stream)
+        step()
+        e.record(stream)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    launch_ms = sum(s.elapsed_time(e) for s, e in evs) / len(evs)
+
+    # Verify the timed result before reporting (a wrong fast kernel is not done).
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    rdev.verify(rs, buf.data_ptr(), lay, flag.data_ptr(), stream)
+    ok = int(flag.item()) == 0
+    if world > 1:
+        okt = torch.tensor([0 if ok else 1], dtype=torch.int32, device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MAX)
+        ok = int(okt.item()) == 0
+
+    user_bytes = k * S * B  # per GPU per step
+    value = world * user_bytes * args.steps / elapsed / 2**30
+    alg_bytes = (k + m) * S * B  # per launch: each data byte read once, each parity byte written once
+    achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
+
+    extra = {}
+    cpu = None
+    if rank == 0 and not args.no_extras:
+        extra = device_extras(torch, rs, rdev, buf, lay, stream, k, m, S, B)
+        if world == 1:
+            cpu = cpu_baseline(k, m, S, args.cpu_seconds)
+            extra.update(host_inclusive(rsamd, k, m))
+    traffic = pmc_traffic(k, m, S, B)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (splitmix64 bytes generated in HBM)",
+            "config": {
+                "workload": f"encode {k}+{m} x {S // 1024} KiB shards x {B} stripes per GPU (BASELINE configs[1])",
+                "k": k, "m": m, "shard_bytes": S, "stripes_per_gpu": B, "global_stripes": B * world,
+                "parallelism": f"stripe-partitioned x{world} (no collective)",
+            },
+            "verified": ok,
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": traffic,
+                "kernel": f"gf_vec_kernel<{k},{m},...> (rs_encode_batch_dev)",
+                "alg_bytes_per_launch": alg_bytes,
+                "avg_launch_ms": round(launch_ms, 4),
+            },
+            "cpu_baseline": cpu,
+            "extra": extra,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def timed(torch, stream, fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    s.record(stream)
+    for _ in range(iters):
+        fn()
+    e.record(stream)
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e-3
+
+
+def device_extras(torch, rs, rdev, buf, lay, stream, k, m, S, B):
+    out = {}
+    for miss in [(0,), (0, 1), (0, 5)]:
+        present = [i not in miss for i in range(k + m)]
+        t = timed(torch, stream, lambda: rdev.decode(rs, buf.data_ptr(), present, lay, stream), 5)
+        e = len(miss)
+        key = "decode_" + "_".join(map(str, miss))
+        out[key + "_GiBps"] = round(k * S * B / t / 2**30, 2)
+        out[key + "_hbm_frac"] = round((k + e) * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
+    # restore parity (decode rewrote the "missing" shards with identical bytes)
+    n = min(buf.numel() // 2, 8 << 30)
+    t = timed(torch, stream, lambda: rdev.copy(buf.data_ptr() + n, buf.data_ptr(), n, stream), 5)
+    out["copy_kernel_GBps"] = round(2 * n / t / 1e9, 1)
+    out["copy_kernel_hbm_frac"] = round(2 * n / t / 1e9 / HBM_PEAK_GBPS, 4)
+    return out
+
+
+def cpu_baseline(k, m, S, budget_s):
+    """The oracle's scalar InputOutputByteTable loop (the reference's default
+    coding loop, -O2 -fno-tree-vectorize) on host-resident stripes."""
+    import numpy as np
+    from oracle import c_ref
+    c_ref.build()
+    codec = c_ref.Codec(k, m)
+    n = 8
+    stride = S
+    host = np.zeros(n * (k + m) * stride, dtype=np.uint8)
+    for t in range(n):
+        host[t * (k + m) * S: t * (k + m) * S + k * S] = c_ref.fill_synthetic(k * S, SEED, t)
+    done, t0 = 0, time.perf_counter()
+    while True:
+        codec.code_stripes(host, n, S, stride, (k + m) * stride, None, 1)
+        done += n
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    rate = k * S * done / el / 2**30
+    threads = min(16, os.cpu_count() or 1)
+    done_mt, t1 = 0, time.perf_counter()
+    nm = threads * 2
+    host_mt = np.zeros(nm * (k + m) * S, dtype=np.uint8)
+    while time.perf_counter() - t1 < budget_s / 2:
+        codec.code_stripes(host_mt, nm, S, S, (k + m) * S, None, threads)
+        done_mt += nm
+    rate_mt = k * S * done_mt / (time.perf_counter() - t1) / 2**30
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(rate, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{done} stripes of {k}+{m} x {S // 1024} KiB encoded by the scalar restatement of "
+                      f"InputOutputByteTableCodingLoop (oracle/rs_oracle.c, -O2 -fno-tree-vectorize), "
+                      f"{el:.1f} s, host-resident",
+            "multi_thread": {"value": round(rate_mt, 4), "threads": threads, "stripes": done_mt},
+            "cpu_model": model}
+
+
+def host_inclusive(rsamd, k, m):
+    """Rate of the JNI-facing host API (H2D + kernel + D2H, pageable buffers)."""
+    import numpy as np
+    n = 64 << 20
+    rng = np.random.default_rng(5)
+    sh = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)] + [np.zeros(n, np.uint8) for _ in range(m)]
+    rs = rsamd.ReedSolomon.create(k, m)
+    rs.encodeParity(sh, 0, n)
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        rs.encodeParity(sh, 0, n)
+    t = (time.perf_counter() - t0) / reps
+    return {"host_inclusive_encode_GiBps": round(k * n / t / 2**30, 3),
+            "host_inclusive_note": f"rs_encode_parity on {k}x64 MiB pageable host shards (H2D + kernel + D2H)"}
+
+
+def pmc_traffic(k, m, S, B):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary for this
+    exact workload (profiles/pmc_traffic.json), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(p))
+        key = f"encode_{k}_{m}_{S}_{B}"
+        return d[key]["hbm_bytes_per_launch"] if key in d else None
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+if __name__ == "__main__":
+    main()

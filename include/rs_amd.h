@@ -1,0 +1,176 @@
+/*
+ * rs_amd.h -- C-ABI of the MI355X Reed-Solomon engine (librsamd.so).
+ *
+ * Drop-in boundary for the reference codec (Backblaze JavaReedSolomon as
+ * vendored in /root/reference/src/main/java/edu/cmu/reedsolomon/).  Every
+ * byte of shard data is coded on the GPU by hand-written HIP kernels for
+ * gfx950; the host code here only validates arguments, builds GF(2^8)
+ * matrices (k x k inversions, as the reference does on the host) and moves
+ * bytes.  There is no CPU coding path: with no usable GPU every coding call
+ * returns RS_E_HIP / RS_E_NO_DEVICE.
+ *
+ * Conventions
+ *  - Return 0 on success or a negative RS_E_* code.  rs_last_error_message()
+ *    then holds the text the Java code would have put in its
+ *    IllegalArgumentException (thread-local), so a JNI shim can ThrowNew.
+ *  - Argument checks run in the reference's order
+ *    (ReedSolomon.java:277-302) and nothing is written on an error path.
+ *  - Host entry points are synchronous and use the calling thread's current
+ *    HIP device.  *_dev entry points are asynchronous on `stream` (a
+ *    hipStream_t passed as void*, NULL = the null stream).
+ *  - A codec handle is immutable after rs_codec_create and safe to share
+ *    between threads (the Java codec is one static final instance:
+ *    ReedSolomonEncoder.java:17).
+ */
+#ifndef RS_AMD_H
+#define RS_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Error codes.  Java exception each one maps to, and its text. */
+enum {
+    RS_OK = 0,
+    RS_E_WRONG_NSHARDS = -1,    /* IAE "wrong number of shards: <n>"          ReedSolomon.java:281 */
+    RS_E_SIZE_MISMATCH = -2,    /* IAE "Shards are different sizes"           ReedSolomon.java:288 */
+    RS_E_NEG_OFFSET = -3,       /* IAE "offset is negative: <off>"            ReedSolomon.java:294 */
+    RS_E_NEG_COUNT = -4,        /* IAE "byteCount is negative: <n>"           ReedSolomon.java:297 */
+    RS_E_TOO_SMALL = -5,        /* IAE "buffers to small: <n><off>"           ReedSolomon.java:300 */
+    RS_E_NOT_ENOUGH = -6,       /* IAE "Not enough shards present"            ReedSolomon.java:198 */
+    RS_E_TOO_MANY_SHARDS = -7,  /* IAE "too many shards - max is 256"         ReedSolomon.java:45  */
+    RS_E_SINGULAR = -8,         /* IAE "Matrix is singular"                   Matrix.java:310      */
+    RS_E_HIP = -9,              /* HIP runtime failure (message has the HIP error string)          */
+    RS_E_INVALID = -10,         /* bad argument the Java API cannot express (NULL, k<1, layout)    */
+    RS_E_TEMP_TOO_SMALL = -11,  /* IAE "tempBuffer is not big enough"         ReedSolomon.java:150 */
+    RS_E_NO_DEVICE = -12        /* no HIP device visible                                           */
+};
+
+#if defined(__GNUC__)
+#define RS_API __attribute__((visibility("default")))
+#else
+#define RS_API
+#endif
+
+typedef struct rs_codec rs_codec;
+
+/* ---------------------------------------------------------------------------
+ * Codec lifetime -- replaces ReedSolomon.create / the 3-arg constructor
+ * (ReedSolomon.java:30-57).  Builds the systematic generator matrix
+ * G = vandermonde(k+m, k) * inverse(top k x k) exactly as buildMatrix
+ * (ReedSolomon.java:312-343).  No device work happens here.
+ * ------------------------------------------------------------------------- */
+RS_API int rs_codec_create(int data_shards, int parity_shards, rs_codec **out);
+RS_API void rs_codec_destroy(rs_codec *codec);
+RS_API int rs_codec_data_shard_count(const rs_codec *codec);   /* getDataShardCount   ReedSolomon.java:62 */
+RS_API int rs_codec_parity_shard_count(const rs_codec *codec); /* getParityShardCount ReedSolomon.java:69 */
+RS_API int rs_codec_total_shard_count(const rs_codec *codec);  /* getTotalShardCount  ReedSolomon.java:76 */
+/* Copy G ((k+m) x k, row-major) to out_rows. */
+RS_API int rs_codec_matrix(const rs_codec *codec, uint8_t *out_rows);
+/* The single fused decode matrix for a presence pattern (see rs_decode_missing):
+ * survivors[k] = first k present shard indices, missing[] = absent indices in
+ * ascending order, rows (n_missing x k) maps survivors -> each missing shard. */
+RS_API int rs_codec_decode_matrix(const rs_codec *codec, const uint8_t *present, int nshards,
+                           int *survivors, int *missing, int *n_missing, uint8_t *rows);
+
+RS_API const char *rs_last_error_message(void);
+/* Free the calling thread's device contexts (streams, staging buffers). */
+RS_API void rs_thread_release(void);
+/* Number of visible HIP devices (0 when none). */
+RS_API int rs_device_count(void);
+
+/* ---------------------------------------------------------------------------
+ * Host-buffer API (JNI-facing).  Shards are caller-owned host arrays,
+ * mutated in place.  Each call stages [offset, offset+byte_count) of the
+ * shards to the GPU, codes them there and copies the outputs back.
+ * shard_lens[i] is the Java array length of shards[i] (for the size checks).
+ * ------------------------------------------------------------------------- */
+
+/* ReedSolomon.encodeParity(byte[][] shards, int offset, int byteCount)
+ * (ReedSolomon.java:90-104): parity shards k..k+m-1 := G[k..] * data. */
+RS_API int rs_encode_parity(const rs_codec *codec, uint8_t *const *shards, int nshards,
+                     const int64_t *shard_lens, int32_t offset, int32_t byte_count);
+
+/* ReedSolomon.decodeMissing(byte[][] shards, boolean[] shardPresent, int offset,
+ * int byteCount) (ReedSolomon.java:175-272).  present[i] != 0 marks shard i
+ * present.  All present -> returns without touching anything (:190-194).
+ * Survivors are the first k present shards in index order (:210-223); every
+ * missing shard (data and parity) is produced in ONE GPU pass from them with
+ * the matrix rs_codec_decode_matrix reports (bit-identical to Java's two
+ * passes).  Missing buffers must be allocated; their contents
+ * are overwritten. */
+RS_API int rs_decode_missing(const rs_codec *codec, uint8_t *const *shards, int nshards,
+                      const int64_t *shard_lens, const uint8_t *present,
+                      int32_t offset, int32_t byte_count);
+
+/* ReedSolomon.isParityCorrect(shards, firstByte, byteCount[, tempBuffer])
+ * (ReedSolomon.java:115-164).  temp may be NULL; when given, temp_len is its
+ * length and only its size is checked (the GPU needs no scratch; the Java
+ * tempBuffer is scratch and its contents are not part of the contract).
+ * *result = 1 when every parity byte matches, else 0. */
+RS_API int rs_is_parity_correct(const rs_codec *codec, uint8_t *const *shards, int nshards,
+                         const int64_t *shard_lens, int32_t first_byte, int32_t byte_count,
+                         const uint8_t *temp, int64_t temp_len, int *result);
+
+/* CodingLoop.codeSomeShards(matrixRows, inputs, inputCount, outputs, outputCount,
+ * offset, byteCount) (CodingLoop.java:79-85; default impl
+ * InputOutputByteTableCodingLoop.java:12-44): outputs[o][b] =
+ * XOR_i mul(matrix_rows[o][i], inputs[i][b]) for b in [offset, offset+byte_count).
+ * matrix_rows[o] has input_count entries.  Outputs must not alias inputs. */
+RS_API int rs_code_some_shards(const uint8_t *const *matrix_rows, const uint8_t *const *inputs,
+                        int input_count, uint8_t *const *outputs, int output_count,
+                        int32_t offset, int32_t byte_count);
+
+/* CodingLoop.checkSomeShards(...) (CodingLoop.java:110-117, CodingLoopBase.java:17-41):
+ * *result = 1 iff to_check[o][b] equals the product for every o, b. */
+RS_API int rs_check_some_shards(const uint8_t *const *matrix_rows, const uint8_t *const *inputs,
+                         int input_count, const uint8_t *const *to_check, int check_count,
+                         int32_t offset, int32_t byte_count, int *result);
+
+/* ---------------------------------------------------------------------------
+ * Device-resident batched API (the benchmark path; no Java counterpart --
+ * it is what a stripe-batching caller uses).  Layout: shard s of stripe t
+ * starts at dev_base + t*stripe_stride + s*shard_stride; shard_len bytes are
+ * coded per shard.  Fast path when dev_base, both strides are multiples of 16
+ * (any shard_len); otherwise a byte-granular kernel is used.
+ * ------------------------------------------------------------------------- */
+
+/* Encode parity for n_stripes stripes. */
+RS_API int rs_encode_batch_dev(const rs_codec *codec, uint8_t *dev_base, size_t n_stripes,
+                        size_t shard_len, size_t shard_stride, size_t stripe_stride, void *stream);
+
+/* Reconstruct the shards absent from present[0..k+m) in every stripe (one
+ * presence pattern for the whole batch). */
+RS_API int rs_decode_batch_dev(const rs_codec *codec, uint8_t *dev_base, const uint8_t *present,
+                        size_t n_stripes, size_t shard_len, size_t shard_stride,
+                        size_t stripe_stride, void *stream);
+
+/* Verify parity of every stripe: dev_mismatch (a device int) is OR-ed with 1
+ * when any parity byte differs.  The caller zeroes it first. */
+RS_API int rs_verify_batch_dev(const rs_codec *codec, const uint8_t *dev_base, size_t n_stripes,
+                        size_t shard_len, size_t shard_stride, size_t stripe_stride,
+                        int *dev_mismatch, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Benchmark/test support (not part of the reference API).
+ * ------------------------------------------------------------------------- */
+
+/* Fill the k data shards of stripes [0, n_stripes) with synthetic bytes:
+ * the k*shard_len data bytes of global stripe g = stripe0 + t, read as
+ * consecutive little-endian 64-bit words w = 0,1,..., are
+ * splitmix64(seed ^ g) outputs 1,2,...  shard_len % 8 == 0. */
+RS_API int rs_fill_synthetic_dev(uint8_t *dev_base, int data_shards, size_t n_stripes, size_t shard_len,
+                          size_t shard_stride, size_t stripe_stride, uint64_t seed,
+                          uint64_t stripe0, void *stream);
+
+/* dst := src, n bytes, with the same 16-byte streaming kernel style (the
+ * "measured device copy" the roofline is also quoted against). */
+RS_API int rs_copy_dev(uint8_t *dst, const uint8_t *src, size_t n, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RS_AMD_H */

@@ -1,0 +1,426 @@
+// capi.cpp -- the extern "C" boundary (include/rs_amd.h).
+//
+// Host-buffer entry points mirror ReedSolomon.java / CodingLoop.java one for
+// one (argument meaning, check order, exception text); they stage the byte
+// range to the GPU, run the kernels of kernels.hip and copy results back.
+// Device entry points enqueue the same kernels on a caller's stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/rs_amd.h"
+#include "codec.hpp"
+#include "gf256.hpp"
+#include "kernels.hpp"
+
+struct rs_codec {
+    rsamd::Codec *impl;
+};
+
+namespace {
+
+using rsamd::Codec;
+using rsamd::DevPlan;
+using rsamd::Geometry;
+using rsamd::Mode;
+using rsamd::Plan;
+
+thread_local std::string t_err;
+
+int fail(int code, const std::string &msg) {
+    t_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char *where) {
+    char buf[256];
+    std::snprintf(buf, sizeof buf, "HIP error %s (%s) in %s", hipGetErrorName(e), hipGetErrorString(e), where);
+    t_err = buf;
+    return RS_E_HIP;
+}
+
+#define RS_HIP(call)                                         \
+    do {                                                     \
+        hipError_t e_ = (call);                              \
+        if (e_ != hipSuccess) return hip_fail(e_, #call);    \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// Per-(thread, device) staging context for the host-buffer API.
+// ---------------------------------------------------------------------------
+struct ThreadCtx {
+    hipStream_t stream = nullptr;
+    uint8_t *stage = nullptr;  // nslots x slot_stride device bytes
+    size_t stage_cap = 0;
+    uint8_t *plan = nullptr;   // per-call plan images (rs_code_some_shards)
+    size_t plan_cap = 0;
+    int *flag = nullptr;       // verify result
+};
+
+thread_local std::map<int, ThreadCtx *> t_ctx;
+
+int need_device() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(RS_E_NO_DEVICE, "no HIP device available");
+    return RS_OK;
+}
+
+int thread_ctx(ThreadCtx **out) {
+    int dev = 0;
+    RS_HIP(hipGetDevice(&dev));
+    auto it = t_ctx.find(dev);
+    if (it == t_ctx.end()) {
+        auto *c = new ThreadCtx;
+        hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&c->flag), 256);
+        if (e != hipSuccess) {
+            delete c;
+            return hip_fail(e, "thread context");
+        }
+        it = t_ctx.emplace(dev, c).first;
+    }
+    *out = it->second;
+    return RS_OK;
+}
+
+int grow(uint8_t **buf, size_t *cap, size_t want) {
+    if (*cap >= want) return RS_OK;
+    if (*buf) RS_HIP(hipFree(*buf));
+    *buf = nullptr;
+    *cap = 0;
+    RS_HIP(hipMalloc(reinterpret_cast<void **>(buf), want));
+    *cap = want;
+    return RS_OK;
+}
+
+// Bytes per shard staged per round trip.  Bounds device staging to
+// nslots * kChunk and keeps each H2D/D2H large.
+constexpr size_t kChunk = size_t(64) << 20;
+
+size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Stage [offset, offset+count) of the host shards (slot-indexed), run every
+// launch group of `plans`, copy results back.
+//   in_slots:  slots copied host -> device (coding inputs, plus the checked
+//              shards in Verify mode)
+//   out_slots: slots copied device -> host afterwards (Code mode)
+int run_host(const std::vector<DevPlan> &plans, int nslots, const std::vector<int> &in_slots,
+             const std::vector<int> &out_slots, uint8_t *const *host, size_t offset, size_t count, Mode mode,
+             int *result) {
+    ThreadCtx *ctx = nullptr;
+    int rc = thread_ctx(&ctx);
+    if (rc) return rc;
+    const size_t chunk = std::min(count, kChunk);
+    const size_t slot_stride = round_up(std::max<size_t>(chunk, 1), 256);
+    rc = grow(&ctx->stage, &ctx->stage_cap, slot_stride * size_t(nslots));
+    if (rc) return rc;
+    if (mode == Mode::Verify) RS_HIP(hipMemsetAsync(ctx->flag, 0, sizeof(int), ctx->stream));
+    for (size_t done = 0; done < count; done += chunk) {
+        const size_t n = std::min(chunk, count - done);
+        for (int s : in_slots)
+            RS_HIP(hipMemcpyAsync(ctx->stage + size_t(s) * slot_stride, host[s] + offset + done, n,
+                                  hipMemcpyHostToDevice, ctx->stream));
+        Geometry g;
+        g.base = ctx->stage;
+        g.n_stripes = 1;
+        g.col0 = 0;
+        g.len = n;
+        g.shard_stride = slot_stride;
+        g.stripe_stride = slot_stride * size_t(nslots);
+        for (const DevPlan &p : plans) RS_HIP(rsamd::launch_gf(g, p, mode, ctx->flag, ctx->stream));
+        if (mode == Mode::Code)
+            for (int s : out_slots)
+                RS_HIP(hipMemcpyAsync(host[s] + offset + done, ctx->stage + size_t(s) * slot_stride, n,
+                                      hipMemcpyDeviceToHost, ctx->stream));
+    }
+    if (mode == Mode::Verify) {
+        int h = 0;
+        RS_HIP(hipMemcpyAsync(&h, ctx->flag, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        RS_HIP(hipStreamSynchronize(ctx->stream));
+        *result = h ? 0 : 1;
+    } else {
+        RS_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    return RS_OK;
+}
+
+// ReedSolomon.checkBuffersAndSizes (ReedSolomon.java:277-302), same order and text.
+int check_buffers_and_sizes(const Codec &c, uint8_t *const *shards, int nshards, const int64_t *lens,
+                            int64_t offset, int64_t count) {
+    if (nshards != c.total()) return fail(RS_E_WRONG_NSHARDS, "wrong number of shards: " + std::to_string(nshards));
+    if (!shards || !lens) return fail(RS_E_INVALID, "shards and shard_lens must not be NULL");
+    for (int i = 1; i < nshards; ++i)
+        if (lens[i] != lens[0]) return fail(RS_E_SIZE_MISMATCH, "Shards are different sizes");
+    if (offset < 0) return fail(RS_E_NEG_OFFSET, "offset is negative: " + std::to_string(offset));
+    if (count < 0) return fail(RS_E_NEG_COUNT, "byteCount is negative: " + std::to_string(count));
+    if (lens[0] < offset + count)  // Java concatenates the two ints (ReedSolomon.java:300)
+        return fail(RS_E_TOO_SMALL, "buffers to small: " + std::to_string(count) + std::to_string(offset));
+    for (int i = 0; i < nshards; ++i)
+        if (!shards[i] && lens[i] > 0) return fail(RS_E_INVALID, "shard " + std::to_string(i) + " is NULL");
+    return RS_OK;
+}
+
+int code_with_plan(const Plan &plan, int nslots, uint8_t *const *host, size_t offset, size_t count, Mode mode,
+                   int *result) {
+    int rc = need_device();
+    if (rc) return rc;
+    std::vector<DevPlan> plans;
+    RS_HIP(plan.device_plans(&plans));
+    std::vector<int> in = plan.in_idx();
+    if (mode == Mode::Verify) in.insert(in.end(), plan.out_idx().begin(), plan.out_idx().end());
+    return run_host(plans, nslots, in, plan.out_idx(), host, offset, count, mode, result);
+}
+
+// Plan for explicit rows (CodingLoop API): slots 0..nin-1 inputs, nin.. outputs.
+// Uploaded per call to the thread context (rows change per call).
+int code_rows(const uint8_t *const *rows, const uint8_t *const *inputs, int nin, uint8_t *const *outputs, int nout,
+              int32_t offset, int32_t count, Mode mode, int *result) {
+    if (nout <= 0 || count <= 0) {  // the Java loops do nothing
+        if (result) *result = 1;
+        return RS_OK;
+    }
+    if (!rows || !inputs || !outputs || nin < 1)
+        return fail(RS_E_INVALID, "matrix_rows, inputs and outputs must not be NULL; input_count >= 1");
+    if (offset < 0) return fail(RS_E_INVALID, "offset is negative: " + std::to_string(offset));
+    for (int p = 0; p < nout; ++p)
+        if (!rows[p] || !outputs[p]) return fail(RS_E_INVALID, "NULL matrix row or output");
+    for (int i = 0; i < nin; ++i)
+        if (!inputs[i]) return fail(RS_E_INVALID, "NULL input");
+    int rc = need_device();
+    if (rc) return rc;
+    rsamd::GfMatrix m(nout, nin);
+    for (int p = 0; p < nout; ++p)
+        for (int i = 0; i < nin; ++i) m.at(p, i) = rows[p][i];
+    std::vector<int> in_idx(nin), out_idx(nout);
+    for (int i = 0; i < nin; ++i) in_idx[i] = i;
+    for (int p = 0; p < nout; ++p) out_idx[p] = nin + p;
+    Plan plan(in_idx, out_idx, m);
+
+    ThreadCtx *ctx = nullptr;
+    rc = thread_ctx(&ctx);
+    if (rc) return rc;
+    std::vector<std::vector<uint8_t>> images;
+    size_t total = 0;
+    for (int g = 0; g < plan.groups(); ++g) {
+        images.push_back(plan.image(g));
+        total += images.back().size();
+    }
+    rc = grow(&ctx->plan, &ctx->plan_cap, total);
+    if (rc) return rc;
+    std::vector<DevPlan> plans;
+    size_t off = 0;
+    for (int g = 0; g < plan.groups(); ++g) {
+        RS_HIP(hipMemcpyAsync(ctx->plan + off, images[g].data(), images[g].size(), hipMemcpyHostToDevice,
+                              ctx->stream));
+        plans.push_back(rsamd::dev_plan_at(ctx->plan + off, nin, std::min(rsamd::kMaxOut, nout - g * rsamd::kMaxOut)));
+        off += images[g].size();
+    }
+    std::vector<uint8_t *> slots(size_t(nin) + nout);
+    for (int i = 0; i < nin; ++i) slots[i] = const_cast<uint8_t *>(inputs[i]);
+    for (int p = 0; p < nout; ++p) slots[nin + p] = outputs[p];
+    std::vector<int> in_slots = in_idx;
+    if (mode == Mode::Verify) in_slots.insert(in_slots.end(), out_idx.begin(), out_idx.end());
+    return run_host(plans, nin + nout, in_slots, out_idx, slots.data(), size_t(offset), size_t(count), mode, result);
+}
+
+const Codec *impl(const rs_codec *c) { return c ? c->impl : nullptr; }
+
+}  // namespace
+
+extern "C" {
+
+int rs_codec_create(int data_shards, int parity_shards, rs_codec **out) {
+    if (!out) return fail(RS_E_INVALID, "out must not be NULL");
+    Codec *c = nullptr;
+    std::string err;
+    int rc = Codec::create(data_shards, parity_shards, &c, &err);
+    if (rc) return fail(rc, err);
+    *out = new rs_codec{c};
+    return RS_OK;
+}
+
+void rs_codec_destroy(rs_codec *codec) {
+    if (!codec) return;
+    delete codec->impl;  // device plan copies are leaked with the process (no HIP calls at teardown)
+    delete codec;
+}
+
+int rs_codec_data_shard_count(const rs_codec *c) { return impl(c) ? impl(c)->k() : RS_E_INVALID; }
+int rs_codec_parity_shard_count(const rs_codec *c) { return impl(c) ? impl(c)->m() : RS_E_INVALID; }
+int rs_codec_total_shard_count(const rs_codec *c) { return impl(c) ? impl(c)->total() : RS_E_INVALID; }
+
+int rs_codec_matrix(const rs_codec *c, uint8_t *out_rows) {
+    if (!impl(c) || !out_rows) return fail(RS_E_INVALID, "NULL argument");
+    const auto &d = impl(c)->matrix().data();
+    std::memcpy(out_rows, d.data(), d.size());
+    return RS_OK;
+}
+
+int rs_codec_decode_matrix(const rs_codec *c, const uint8_t *present, int nshards, int *survivors, int *missing,
+                           int *n_missing, uint8_t *rows) {
+    if (!impl(c) || !present || !survivors || !missing || !n_missing || !rows)
+        return fail(RS_E_INVALID, "NULL argument");
+    if (nshards != impl(c)->total()) return fail(RS_E_WRONG_NSHARDS, "wrong number of shards: " + std::to_string(nshards));
+    std::shared_ptr<const Plan> plan;
+    int rc = impl(c)->decode_plan(present, &plan);
+    if (rc == RS_E_NOT_ENOUGH) return fail(rc, "Not enough shards present");
+    if (rc == RS_E_SINGULAR) return fail(rc, "Matrix is singular");
+    const int k = impl(c)->k();
+    for (int i = 0; i < k; ++i) survivors[i] = plan->in_idx()[i];
+    *n_missing = int(plan->out_idx().size());
+    for (int j = 0; j < *n_missing; ++j) missing[j] = plan->out_idx()[j];
+    std::memcpy(rows, plan->rows().data().data(), plan->rows().data().size());
+    return RS_OK;
+}
+
+const char *rs_last_error_message(void) { return t_err.c_str(); }
+
+void rs_thread_release(void) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (auto &kv : t_ctx) {
+        ThreadCtx *c = kv.second;
+        (void)hipSetDevice(kv.first);
+        if (c->stream) (void)hipStreamDestroy(c->stream);
+        if (c->stage) (void)hipFree(c->stage);
+        if (c->plan) (void)hipFree(c->plan);
+        if (c->flag) (void)hipFree(c->flag);
+        delete c;
+    }
+    t_ctx.clear();
+    (void)hipSetDevice(cur);
+}
+
+int rs_device_count(void) {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
+int rs_encode_parity(const rs_codec *codec, uint8_t *const *shards, int nshards, const int64_t *shard_lens,
+                     int32_t offset, int32_t byte_count) {
+    const Codec *c = impl(codec);
+    if (!c) return fail(RS_E_INVALID, "codec is NULL");
+    int rc = check_buffers_and_sizes(*c, shards, nshards, shard_lens, offset, byte_count);
+    if (rc) return rc;
+    if (byte_count == 0 || c->m() == 0) return RS_OK;
+    return code_with_plan(c->encode_plan(), c->total(), shards, size_t(offset), size_t(byte_count), Mode::Code,
+                          nullptr);
+}
+
+int rs_decode_missing(const rs_codec *codec, uint8_t *const *shards, int nshards, const int64_t *shard_lens,
+                      const uint8_t *present, int32_t offset, int32_t byte_count) {
+    const Codec *c = impl(codec);
+    if (!c) return fail(RS_E_INVALID, "codec is NULL");
+    int rc = check_buffers_and_sizes(*c, shards, nshards, shard_lens, offset, byte_count);
+    if (rc) return rc;
+    if (!present) return fail(RS_E_INVALID, "present must not be NULL");
+    int n_present = 0;
+    for (int i = 0; i < c->total(); ++i) n_present += present[i] ? 1 : 0;
+    if (n_present == c->total()) return RS_OK;  // ReedSolomon.java:190-194
+    if (n_present < c->k()) return fail(RS_E_NOT_ENOUGH, "Not enough shards present");
+    std::shared_ptr<const Plan> plan;
+    rc = c->decode_plan(present, &plan);
+    if (rc == RS_E_SINGULAR) return fail(rc, "Matrix is singular");
+    if (rc) return fail(rc, "Not enough shards present");
+    if (byte_count == 0) return RS_OK;
+    return code_with_plan(*plan, c->total(), shards, size_t(offset), size_t(byte_count), Mode::Code, nullptr);
+}
+
+int rs_is_parity_correct(const rs_codec *codec, uint8_t *const *shards, int nshards, const int64_t *shard_lens,
+                         int32_t first_byte, int32_t byte_count, const uint8_t *temp, int64_t temp_len,
+                         int *result) {
+    const Codec *c = impl(codec);
+    if (!c || !result) return fail(RS_E_INVALID, "codec and result must not be NULL");
+    int rc = check_buffers_and_sizes(*c, shards, nshards, shard_lens, first_byte, byte_count);
+    if (rc) return rc;
+    if (temp && temp_len < int64_t(first_byte) + byte_count)
+        return fail(RS_E_TEMP_TOO_SMALL, "tempBuffer is not big enough");
+    if (byte_count == 0 || c->m() == 0) {
+        *result = 1;
+        return RS_OK;
+    }
+    return code_with_plan(c->verify_plan(), c->total(), shards, size_t(first_byte), size_t(byte_count),
+                          Mode::Verify, result);
+}
+
+int rs_code_some_shards(const uint8_t *const *matrix_rows, const uint8_t *const *inputs, int input_count,
+                        uint8_t *const *outputs, int output_count, int32_t offset, int32_t byte_count) {
+    return code_rows(matrix_rows, inputs, input_count, outputs, output_count, offset, byte_count, Mode::Code,
+                     nullptr);
+}
+
+int rs_check_some_shards(const uint8_t *const *matrix_rows, const uint8_t *const *inputs, int input_count,
+                         const uint8_t *const *to_check, int check_count, int32_t offset, int32_t byte_count,
+                         int *result) {
+    if (!result) return fail(RS_E_INVALID, "result must not be NULL");
+    return code_rows(matrix_rows, inputs, input_count, const_cast<uint8_t *const *>(to_check), check_count, offset,
+                     byte_count, Mode::Verify, result);
+}
+
+int rs_encode_batch_dev(const rs_codec *codec, uint8_t *dev_base, size_t n_stripes, size_t shard_len,
+                        size_t shard_stride, size_t stripe_stride, void *stream) {
+    const Codec *c = impl(codec);
+    if (!c || (!dev_base && n_stripes && shard_len)) return fail(RS_E_INVALID, "NULL codec or device base");
+    std::vector<DevPlan> plans;
+    RS_HIP(c->encode_plan().device_plans(&plans));
+    Geometry g{dev_base, n_stripes, 0, shard_len, shard_stride, stripe_stride};
+    for (const DevPlan &p : plans)
+        RS_HIP(rsamd::launch_gf(g, p, Mode::Code, nullptr, static_cast<hipStream_t>(stream)));
+    return RS_OK;
+}
+
+int rs_decode_batch_dev(const rs_codec *codec, uint8_t *dev_base, const uint8_t *present, size_t n_stripes,
+                        size_t shard_len, size_t shard_stride, size_t stripe_stride, void *stream) {
+    const Codec *c = impl(codec);
+    if (!c || !present || (!dev_base && n_stripes && shard_len))
+        return fail(RS_E_INVALID, "NULL codec, presence pattern or device base");
+    int n_present = 0;
+    for (int i = 0; i < c->total(); ++i) n_present += present[i] ? 1 : 0;
+    if (n_present == c->total()) return RS_OK;
+    if (n_present < c->k()) return fail(RS_E_NOT_ENOUGH, "Not enough shards present");
+    std::shared_ptr<const Plan> plan;
+    int rc = c->decode_plan(present, &plan);
+    if (rc) return fail(rc, rc == RS_E_SINGULAR ? "Matrix is singular" : "Not enough shards present");
+    std::vector<DevPlan> plans;
+    RS_HIP(plan->device_plans(&plans));
+    Geometry g{dev_base, n_stripes, 0, shard_len, shard_stride, stripe_stride};
+    for (const DevPlan &p : plans)
+        RS_HIP(rsamd::launch_gf(g, p, Mode::Code, nullptr, static_cast<hipStream_t>(stream)));
+    return RS_OK;
+}
+
+int rs_verify_batch_dev(const rs_codec *codec, const uint8_t *dev_base, size_t n_stripes, size_t shard_len,
+                        size_t shard_stride, size_t stripe_stride, int *dev_mismatch, void *stream) {
+    const Codec *c = impl(codec);
+    if (!c || !dev_mismatch || (!dev_base && n_stripes && shard_len))
+        return fail(RS_E_INVALID, "NULL codec, device base or mismatch flag");
+    std::vector<DevPlan> plans;
+    RS_HIP(c->verify_plan().device_plans(&plans));
+    Geometry g{const_cast<uint8_t *>(dev_base), n_stripes, 0, shard_len, shard_stride, stripe_stride};
+    for (const DevPlan &p : plans)
+        RS_HIP(rsamd::launch_gf(g, p, Mode::Verify, dev_mismatch, static_cast<hipStream_t>(stream)));
+    return RS_OK;
+}
+
+int rs_fill_synthetic_dev(uint8_t *dev_base, int data_shards, size_t n_stripes, size_t shard_len, size_t shard_stride,
+                          size_t stripe_stride, uint64_t seed, uint64_t stripe0, void *stream) {
+    if (!dev_base || data_shards < 1) return fail(RS_E_INVALID, "NULL device base or data_shards < 1");
+    if (shard_len % 8) return fail(RS_E_INVALID, "shard_len must be a multiple of 8");
+    RS_HIP(rsamd::launch_fill_synthetic(dev_base, data_shards, n_stripes, shard_len, shard_stride, stripe_stride,
+                                        seed, stripe0, static_cast<hipStream_t>(stream)));
+    return RS_OK;
+}
+
+int rs_copy_dev(uint8_t *dst, const uint8_t *src, size_t n, void *stream) {
+    if ((!dst || !src) && n) return fail(RS_E_INVALID, "NULL pointer");
+    RS_HIP(rsamd::launch_copy(dst, src, n, static_cast<hipStream_t>(stream)));
+    return RS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,155 @@
+// codec.cpp -- see codec.hpp.
+#include "codec.hpp"
+
+#include <cstring>
+
+#include "../../include/rs_amd.h"
+
+namespace rsamd {
+
+PlanLayout plan_layout(int nin, int nout) {
+    PlanLayout l;
+    l.tabs = 0;
+    l.in_idx = size_t(nin) * nout * sizeof(PermTable);
+    l.out_idx = l.in_idx + size_t(nin) * sizeof(int32_t);
+    l.bytes = (l.out_idx + size_t(nout) * sizeof(int32_t) + 255) & ~size_t(255);
+    return l;
+}
+
+DevPlan dev_plan_at(const void *base, int nin, int nout) {
+    const PlanLayout l = plan_layout(nin, nout);
+    const uint8_t *b = static_cast<const uint8_t *>(base);
+    DevPlan p;
+    p.tabs = reinterpret_cast<const uint32_t *>(b + l.tabs);
+    p.in_idx = reinterpret_cast<const int32_t *>(b + l.in_idx);
+    p.out_idx = reinterpret_cast<const int32_t *>(b + l.out_idx);
+    p.nin = nin;
+    p.nout = nout;
+    return p;
+}
+
+Plan::Plan(std::vector<int> in_idx, std::vector<int> out_idx, GfMatrix rows)
+    : in_idx_(std::move(in_idx)), out_idx_(std::move(out_idx)), rows_(std::move(rows)) {}
+
+std::vector<uint8_t> Plan::image(int g) const {
+    const int nin = int(in_idx_.size());
+    const int p0 = g * kMaxOut;
+    const int nout = std::min<int>(kMaxOut, int(out_idx_.size()) - p0);
+    const PlanLayout l = plan_layout(nin, nout);
+    std::vector<uint8_t> img(l.bytes, 0);
+    // tabs[i][p] (input-major so one input's tables are contiguous)
+    for (int i = 0; i < nin; ++i)
+        for (int p = 0; p < nout; ++p) {
+            const PermTable t = perm_table(rows_.at(p0 + p, i));
+            std::memcpy(img.data() + l.tabs + (size_t(i) * nout + p) * sizeof(PermTable), &t, sizeof t);
+        }
+    for (int i = 0; i < nin; ++i) {
+        const int32_t v = in_idx_[i];
+        std::memcpy(img.data() + l.in_idx + i * sizeof(int32_t), &v, sizeof v);
+    }
+    for (int p = 0; p < nout; ++p) {
+        const int32_t v = out_idx_[p0 + p];
+        std::memcpy(img.data() + l.out_idx + p * sizeof(int32_t), &v, sizeof v);
+    }
+    return img;
+}
+
+hipError_t Plan::device_plans(std::vector<DevPlan> *out) const {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const int nin = int(in_idx_.size());
+    std::lock_guard<std::mutex> lock(mu_);
+    auto it = dev_.find(dev);
+    std::vector<size_t> offs;
+    size_t total = 0;
+    for (int g = 0; g < groups(); ++g) {
+        offs.push_back(total);
+        total += plan_layout(nin, std::min<int>(kMaxOut, int(out_idx_.size()) - g * kMaxOut)).bytes;
+    }
+    if (it == dev_.end()) {
+        void *buf = nullptr;
+        e = hipMalloc(&buf, total ? total : 256);
+        if (e != hipSuccess) return e;
+        for (int g = 0; g < groups(); ++g) {
+            const std::vector<uint8_t> img = image(g);
+            e = hipMemcpy(static_cast<uint8_t *>(buf) + offs[g], img.data(), img.size(), hipMemcpyHostToDevice);
+            if (e != hipSuccess) {
+                (void)hipFree(buf);
+                return e;
+            }
+        }
+        it = dev_.emplace(dev, buf).first;
+    }
+    out->clear();
+    for (int g = 0; g < groups(); ++g) {
+        const int nout = std::min<int>(kMaxOut, int(out_idx_.size()) - g * kMaxOut);
+        out->push_back(dev_plan_at(static_cast<uint8_t *>(it->second) + offs[g], nin, nout));
+    }
+    return hipSuccess;
+}
+
+Codec::Codec(int k, int m) : k_(k), m_(m), matrix_(build_generator(k, k + m)) {
+    std::vector<int> in(k), out(m);
+    for (int i = 0; i < k; ++i) in[i] = i;
+    for (int p = 0; p < m; ++p) out[p] = k + p;
+    std::vector<int> parity(m);
+    for (int p = 0; p < m; ++p) parity[p] = k + p;
+    encode_.reset(new Plan(in, out, matrix_.select_rows(parity)));  // parityRows, ReedSolomon.java:53-56
+}
+
+int Codec::create(int k, int m, Codec **out, std::string *err) {
+    if (256 < k + m) {  // ReedSolomon.java:44-46
+        *err = "too many shards - max is 256";
+        return RS_E_TOO_MANY_SHARDS;
+    }
+    if (k < 1 || m < 0) {
+        *err = "shard counts must satisfy data >= 1 and parity >= 0";
+        return RS_E_INVALID;
+    }
+    *out = new Codec(k, m);
+    return RS_OK;
+}
+
+int Codec::decode_plan(const uint8_t *present, std::shared_ptr<const Plan> *out) const {
+    std::vector<uint8_t> key(total());
+    for (int i = 0; i < total(); ++i) key[i] = present[i] ? 1 : 0;
+    {
+        std::lock_guard<std::mutex> lock(mu_);
+        auto it = decode_cache_.find(key);
+        if (it != decode_cache_.end()) {
+            *out = it->second;
+            return RS_OK;
+        }
+    }
+    std::vector<int> surv, missing;
+    for (int i = 0; i < total(); ++i) {
+        if (key[i] && int(surv.size()) < k_) surv.push_back(i);
+        if (!key[i]) missing.push_back(i);
+    }
+    if (int(surv.size()) < k_) return RS_E_NOT_ENOUGH;
+    GfMatrix dinv;
+    if (!matrix_.select_rows(surv).invert(&dinv)) return RS_E_SINGULAR;
+    // One row per missing shard over the survivors.  Java's second pass codes
+    // missing parity from ALL data shards (ReedSolomon.java:259-271); every
+    // present data shard is a survivor and Dinv's row for it is the unit vector
+    // selecting it, so parityRow * Dinv reproduces that pass bit for bit.
+    GfMatrix rows(int(missing.size()), k_);
+    for (size_t r = 0; r < missing.size(); ++r) {
+        const int j = missing[r];
+        if (j < k_) {
+            for (int c = 0; c < k_; ++c) rows.at(int(r), c) = dinv.at(j, c);
+        } else {
+            GfMatrix prow = matrix_.select_rows({j});
+            GfMatrix fused = prow.times(dinv);
+            for (int c = 0; c < k_; ++c) rows.at(int(r), c) = fused.at(0, c);
+        }
+    }
+    auto plan = std::make_shared<const Plan>(surv, missing, std::move(rows));
+    std::lock_guard<std::mutex> lock(mu_);
+    auto ins = decode_cache_.emplace(key, plan);
+    *out = ins.first->second;
+    return RS_OK;
+}
+
+}  // namespace rsamd

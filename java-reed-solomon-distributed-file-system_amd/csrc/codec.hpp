@@ -1,0 +1,78 @@
+// codec.hpp -- the host-side mirror of ReedSolomon.java: generator matrix,
+// encode plan, cached fused decode plans, and their device-resident copies.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "gf256.hpp"
+#include "kernels.hpp"
+
+namespace rsamd {
+
+// A coding plan: out[idx_out[p]] = XOR_i rows[p][i] * in[idx_in[i]], split into
+// launch groups of at most kMaxOut outputs.  Host-only until uploaded.
+class Plan {
+public:
+    Plan(std::vector<int> in_idx, std::vector<int> out_idx, GfMatrix rows);
+    const std::vector<int> &in_idx() const { return in_idx_; }
+    const std::vector<int> &out_idx() const { return out_idx_; }
+    const GfMatrix &rows() const { return rows_; }
+    int groups() const { return int((out_idx_.size() + kMaxOut - 1) / kMaxOut); }
+
+    // Per-group device plans on the calling thread's current device; uploaded
+    // once per device (blocking hipMemcpy on first use) and then immutable.
+    hipError_t device_plans(std::vector<DevPlan> *out) const;
+
+    // The flat image uploaded for group g (exposed for per-call uploads).
+    std::vector<uint8_t> image(int g) const;
+
+private:
+    std::vector<int> in_idx_, out_idx_;
+    GfMatrix rows_;
+    mutable std::mutex mu_;
+    mutable std::map<int, void *> dev_;  // device id -> allocation of all groups
+};
+
+// Offsets of one group's image: tabs, then in_idx, then out_idx.
+struct PlanLayout {
+    size_t tabs, in_idx, out_idx, bytes;
+};
+PlanLayout plan_layout(int nin, int nout);
+DevPlan dev_plan_at(const void *base, int nin, int nout);
+
+class Codec {
+public:
+    static int create(int k, int m, Codec **out, std::string *err);
+
+    int k() const { return k_; }
+    int m() const { return m_; }
+    int total() const { return k_ + m_; }
+    const GfMatrix &matrix() const { return matrix_; }
+    const Plan &encode_plan() const { return *encode_; }
+    const Plan &verify_plan() const { return *encode_; }
+
+    // Fused decode plan for a presence pattern (cached, thread-safe).  Inputs =
+    // the first k present shards (ReedSolomon.java:210-223); outputs = every
+    // absent shard in ascending order; rows: Dinv[j] for a missing data shard j,
+    // parityRow[p] * Dinv for a missing parity shard.
+    // Returns 0, RS_E_NOT_ENOUGH-style negative code, or RS_E_SINGULAR.
+    int decode_plan(const uint8_t *present, std::shared_ptr<const Plan> *out) const;
+
+private:
+    Codec(int k, int m);
+    int k_, m_;
+    GfMatrix matrix_;
+    std::unique_ptr<Plan> encode_;
+    mutable std::mutex mu_;
+    mutable std::map<std::vector<uint8_t>, std::shared_ptr<const Plan>> decode_cache_;
+};
+
+}  // namespace rsamd

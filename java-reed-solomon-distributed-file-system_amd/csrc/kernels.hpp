@@ -1,0 +1,49 @@
+// kernels.hpp -- launchers for the gfx950 kernels in kernels.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+
+namespace rsamd {
+
+// A device-resident coding plan for ONE launch: nout <= kMaxOut outputs, each
+// the GF dot product of a coefficient row with the nin input shards.
+// Device memory layout (one allocation, see Codec::device_plan):
+//   uint32 tabs[nin][nout][5]   PermTable of coefficient row[p][i]
+//   int32  in_idx[nin]          shard index of input i inside a stripe
+//   int32  out_idx[nout]        shard index of output p inside a stripe
+constexpr int kMaxOut = 4;
+struct DevPlan {
+    const uint32_t *tabs = nullptr;
+    const int32_t *in_idx = nullptr;
+    const int32_t *out_idx = nullptr;
+    int nin = 0, nout = 0;
+};
+
+// Stripe-batched layout: shard s of stripe t at base + t*stripe_stride + s*shard_stride,
+// bytes [col0, col0 + len) of every shard take part.
+struct Geometry {
+    uint8_t *base = nullptr;
+    size_t n_stripes = 0;
+    size_t col0 = 0;
+    size_t len = 0;
+    size_t shard_stride = 0;
+    size_t stripe_stride = 0;
+};
+
+enum class Mode { Code, Verify };
+
+// Codes (or, with Mode::Verify, checks into *mismatch) every stripe of g with plan p.
+// Returns hipSuccess or the first launch error.
+hipError_t launch_gf(const Geometry &g, const DevPlan &p, Mode mode, int *mismatch, hipStream_t s);
+
+hipError_t launch_fill_synthetic(uint8_t *base, int k, size_t n_stripes, size_t shard_len,
+                                 size_t shard_stride, size_t stripe_stride, uint64_t seed,
+                                 uint64_t stripe0, hipStream_t s);
+
+hipError_t launch_copy(uint8_t *dst, const uint8_t *src, size_t n, hipStream_t s);
+
+}  // namespace rsamd

@@ -1,0 +1,83 @@
+"""Device-resident batched API (the benchmark path) over the C-ABI.
+
+Stripes live in HBM as ``[stripe][shard][shard_stride]``; every call is
+asynchronous on the given HIP stream.  ``torch`` is only plumbing here (device
+allocation and streams); the byte work is done by the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Sequence
+
+import numpy as np
+
+from . import _lib
+from .codec import ReedSolomon, _bools, check
+
+
+@dataclass(frozen=True)
+class StripeLayout:
+    """Byte layout of a stripe batch in device memory."""
+
+    n_stripes: int
+    shard_len: int
+    shard_stride: int
+    stripe_stride: int
+
+    @staticmethod
+    def packed(n_stripes: int, total_shards: int, shard_len: int, align: int = 256) -> "StripeLayout":
+        stride = (shard_len + align - 1) // align * align
+        return StripeLayout(n_stripes, shard_len, stride, stride * total_shards)
+
+    @property
+    def nbytes(self) -> int:
+        return self.n_stripes * self.stripe_stride
+
+
+def _stream_handle(stream) -> int:
+    if stream is None:
+        return 0
+    if isinstance(stream, int):
+        return stream
+    return int(stream.cuda_stream)  # torch.cuda.Stream
+
+
+def encode(codec: ReedSolomon, dev_base: int, lay: StripeLayout, stream=None) -> None:
+    check(_lib.load().rs_encode_batch_dev(codec.handle, C.c_void_p(dev_base), lay.n_stripes, lay.shard_len,
+                                          lay.shard_stride, lay.stripe_stride, C.c_void_p(_stream_handle(stream))))
+
+
+def decode(codec: ReedSolomon, dev_base: int, present: Sequence, lay: StripeLayout, stream=None) -> None:
+    p = _bools(present)
+    check(_lib.load().rs_decode_batch_dev(codec.handle, C.c_void_p(dev_base), p.ctypes.data_as(_lib.u8p),
+                                          lay.n_stripes, lay.shard_len, lay.shard_stride, lay.stripe_stride,
+                                          C.c_void_p(_stream_handle(stream))))
+
+
+def verify(codec: ReedSolomon, dev_base: int, lay: StripeLayout, dev_flag: int, stream=None) -> None:
+    check(_lib.load().rs_verify_batch_dev(codec.handle, C.c_void_p(dev_base), lay.n_stripes, lay.shard_len,
+                                          lay.shard_stride, lay.stripe_stride, C.c_void_p(dev_flag),
+                                          C.c_void_p(_stream_handle(stream))))
+
+
+def fill_synthetic(dev_base: int, data_shards: int, lay: StripeLayout, seed: int, stripe0: int = 0,
+                   stream=None) -> None:
+    check(_lib.load().rs_fill_synthetic_dev(C.c_void_p(dev_base), data_shards, lay.n_stripes, lay.shard_len,
+                                            lay.shard_stride, lay.stripe_stride, seed, stripe0,
+                                            C.c_void_p(_stream_handle(stream))))
+
+
+def copy(dst: int, src: int, n: int, stream=None) -> None:
+    check(_lib.load().rs_copy_dev(C.c_void_p(dst), C.c_void_p(src), n, C.c_void_p(_stream_handle(stream))))
+
+
+def device_count() -> int:
+    return _lib.load().rs_device_count()
+
+
+def view_shards(buf: np.ndarray, lay: StripeLayout, total: int) -> np.ndarray:
+    """Host view (n_stripes, total, shard_len) of a host copy of the batch."""
+    v = buf[: lay.nbytes].reshape(lay.n_stripes, lay.stripe_stride)
+    v = v[:, : total * lay.shard_stride].reshape(lay.n_stripes, total, lay.shard_stride)
+    return v[:, :, : lay.shard_len]

@@ -1,0 +1,54 @@
+"""pytest configuration.
+
+Markers:
+  gpu  -- needs a visible MI355X (gfx950) and the built librsamd.so; these are
+          the parity tests proper and call the engine through the C-ABI.
+Everything unmarked runs on CPU (oracle pinning, golden fixtures, host-side
+matrix logic and argument checks of the C-ABI, gloo multi-process tests).
+"""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG_DIR = os.path.join(ROOT, "java-reed-solomon-distributed-file-system_amd")
+for p in (ROOT, PKG_DIR):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: requires an MI355X GPU and the HIP extension")
+
+
+@pytest.fixture(scope="session")
+def golden_dir():
+    return GOLDEN
+
+
+@pytest.fixture(scope="session")
+def oracle_lib():
+    from oracle import c_ref
+    c_ref.build()
+    return c_ref
+
+
+@pytest.fixture(scope="session")
+def native():
+    """The product library; fails loudly when it is not built."""
+    from rsamd import _lib
+    return _lib.load()
+
+
+@pytest.fixture(scope="session")
+def gpu(native):
+    """Skip-free GPU gate: a gpu-marked test on a box without a device is an error."""
+    n = native.rs_device_count()
+    if n < 1:
+        pytest.fail("no HIP device visible to librsamd.so (gpu tests need an MI355X)")
+    import torch
+    assert torch.cuda.is_available(), "torch sees no GPU"
+    return torch.device("cuda:0")

@@ -1,0 +1,143 @@
+"""CPU tests of the product library's host side, through the C-ABI.
+
+No compute calls: these cover that librsamd.so loads, exports exactly what
+include/rs_amd.h declares, builds the same generator / fused decode matrices as
+the oracle, and returns the reference's argument errors (ReedSolomon.java:277-302)
+before touching any device.  Without a GPU every coding call must fail loudly
+(GpuError), never fall back to a CPU path.
+"""
+import itertools
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "rs_amd.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"RS_API\s+[\w\s\*]*?\b(rs_\w+)\s*\(", text)))
+
+
+def test_header_symbols_exported(native):
+    from rsamd import _lib
+    names = header_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(native, n), n
+    assert sorted(_lib.SIGNATURES) == names
+
+
+def test_header_error_codes_match_oracle():
+    text = open(HEADER).read()
+    codes = dict((k, int(v)) for k, v in re.findall(r"(RS_E_\w+)\s*=\s*(-?\d+)", text))
+    oracle_src = open(os.path.join(ROOT, "oracle", "rs_oracle.c")).read()
+    orc = dict((k, int(v)) for k, v in re.findall(r"ORC_(E_\w+)\s*=\s*(-?\d+)", oracle_src))
+    for k, v in orc.items():
+        if "RS_" + k in codes:
+            assert codes["RS_" + k] == v, k
+    from rsamd import codec
+    for k, v in codes.items():
+        assert getattr(codec, k) == v
+
+
+@pytest.mark.parametrize("k,m", [(4, 2), (10, 4), (17, 3), (1, 1), (5, 5), (3, 0), (128, 128)])
+def test_generator_matrix_matches_oracle(native, oracle_lib, k, m):
+    import rsamd
+    rs = rsamd.ReedSolomon.create(k, m)
+    assert (rs.getDataShardCount(), rs.getParityShardCount(), rs.getTotalShardCount()) == (k, m, k + m)
+    assert np.array_equal(rs.matrix(), oracle_lib.build_matrix(k, k + m))
+
+
+def test_codec_create_errors(native):
+    import rsamd
+    with pytest.raises(rsamd.IllegalArgumentException, match="^too many shards - max is 256$"):
+        rsamd.ReedSolomon.create(250, 7)
+    with pytest.raises(rsamd.IllegalArgumentException):
+        rsamd.ReedSolomon.create(0, 2)
+
+
+@pytest.mark.parametrize("k,m,maxe", [(4, 2, 2), (10, 4, 4), (5, 5, 3)])
+def test_fused_decode_matrix_matches_oracle(native, oracle_lib, k, m, maxe):
+    import rsamd
+    rs = rsamd.ReedSolomon.create(k, m)
+    oc = oracle_lib.Codec(k, m)
+    for e in range(1, maxe + 1):
+        for miss in itertools.combinations(range(k + m), e):
+            present = [i not in miss for i in range(k + m)]
+            assert _eq(rs.decode_matrix(present), oc.decode_rows(present)), miss
+
+
+def _eq(a, b):
+    return a[0] == b[0] and a[1] == b[1] and np.array_equal(a[2], b[2])
+
+
+def test_decode_matrix_survey_appendix(native):
+    import rsamd
+    rs = rsamd.ReedSolomon.create(4, 2)
+    s, mi, r = rs.decode_matrix([0, 1, 1, 1, 1, 1])
+    assert s == [1, 2, 3, 4] and mi == [0] and r.tolist() == [[166, 245, 210, 128]]
+    s, mi, r = rs.decode_matrix([1, 1, 0, 0, 1, 1])
+    assert s == [0, 1, 4, 5] and r.tolist() == [[141, 246, 123, 1], [246, 141, 1, 123]]
+    rs10 = rsamd.ReedSolomon.create(10, 4)
+    s, mi, r = rs10.decode_matrix([0] * 4 + [1] * 10)
+    assert s == list(range(4, 14)) and r[0].tolist() == [29, 239, 227, 16, 49, 195, 195, 48, 13, 12]
+
+
+def test_argument_errors_before_device(native):
+    """Every IllegalArgumentException of ReedSolomon.java, in its check order,
+    with its exact text -- returned before any device work (so also on CPU)."""
+    import rsamd
+    rs = rsamd.ReedSolomon.create(4, 2)
+    sh = [np.zeros(10, np.uint8) for _ in range(6)]
+    IAE = rsamd.IllegalArgumentException
+    with pytest.raises(IAE, match="^wrong number of shards: 7$") as ei:
+        rs.encodeParity(sh + [np.zeros(10, np.uint8)], 0, 10)
+    assert ei.value.code == -1
+    # shard count is checked before sizes (ReedSolomon.java:280 before :285)
+    with pytest.raises(IAE, match="^wrong number of shards: 5$"):
+        rs.encodeParity(sh[:4] + [np.zeros(3, np.uint8)], 0, 10)
+    with pytest.raises(IAE, match="^Shards are different sizes$"):
+        rs.encodeParity(sh[:5] + [np.zeros(3, np.uint8)], -5, -5)
+    with pytest.raises(IAE, match="^offset is negative: -5$"):
+        rs.encodeParity(sh, -5, -5)
+    with pytest.raises(IAE, match="^byteCount is negative: -5$"):
+        rs.encodeParity(sh, 0, -5)
+    with pytest.raises(IAE, match="^buffers to small: 101$"):  # "10" + "1", as Java prints it
+        rs.encodeParity(sh, 1, 10)
+    with pytest.raises(IAE, match="^buffers to small: 65$"):  # checks run even when all are present
+        rs.decodeMissing(sh, [True] * 6, 5, 6)
+    with pytest.raises(IAE, match="^buffers to small: 65$"):
+        rs.isParityCorrect(sh, 5, 6)
+    with pytest.raises(IAE, match="^Not enough shards present$"):
+        rs.decodeMissing(sh, [True, True, False, False, True, False], 0, 10)
+    with pytest.raises(IAE, match="^tempBuffer is not big enough$"):
+        rs.isParityCorrect(sh, 2, 8, np.zeros(9, np.uint8))
+    # nothing was written on the error paths
+    assert all((s == 0).all() for s in sh)
+
+
+def test_all_present_and_empty_are_no_ops_without_device(native):
+    """decodeMissing with every shard present returns before any coding
+    (ReedSolomon.java:190-194), and zero-length work needs no device."""
+    import rsamd
+    rs = rsamd.ReedSolomon.create(4, 2)
+    sh = [np.full(10, 7, np.uint8) for _ in range(6)]
+    rs.decodeMissing(sh, [True] * 6, 0, 10)
+    rs.encodeParity(sh, 4, 0)
+    assert all((s == 7).all() for s in sh)
+
+
+def test_coding_without_device_fails_loudly(native):
+    import rsamd
+    if native.rs_device_count() > 0:
+        pytest.skip("a device is visible; covered by the gpu tests")
+    rs = rsamd.ReedSolomon.create(4, 2)
+    sh = [np.ones(16, np.uint8) for _ in range(6)]
+    with pytest.raises(rsamd.GpuError):
+        rs.encodeParity(sh, 0, 16)
+    assert all((s == 1).all() for s in sh)

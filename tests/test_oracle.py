@@ -1,0 +1,195 @@
+"""Pins the CPU oracle (oracle/) to the reference before anything is compared
+against it.
+
+Evidence used:
+  * the literal LOG/EXP tables of Galois.java:58-169 (tests/golden/galois_tables.json);
+  * the upstream Backblaze 5+5 known-answer vector;
+  * the reference's own round-trip tests, ReedSolomonTest.java:70-93 (0 erasures
+    and erasures {0 (DataDiskOne), 5 (ParityDiskTwo)}), on seeded data instead
+    of 200 MB of unseeded java.util.Random;
+  * the reference's committed fixture ClientClusterCommTestFiles/Files/test.txt
+    through pad -> split -> encode -> erase -> decode -> merge -> trim;
+  * the C and numpy restatements against each other, and all 12 coding loops of
+    CodingLoop.java:42-56 against each other.
+"""
+import hashlib
+import itertools
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import numpy_ref as nr
+
+
+def test_tables_match_reference_literals(oracle_lib, golden_dir):
+    d = json.load(open(os.path.join(golden_dir, "galois_tables.json")))
+    assert np.array_equal(np.array(d["log_table"], dtype=np.int16), oracle_lib.log_table())
+    assert np.array_equal(np.array(d["exp_table"], dtype=np.uint8), oracle_lib.exp_table())
+    assert np.array_equal(np.array(d["log_table"], dtype=np.int16), nr.LOG_TABLE)
+    assert np.array_equal(np.array(d["exp_table"], dtype=np.uint8), nr.EXP_TABLE)
+    assert np.array_equal(oracle_lib.mul_table(), nr.MUL_TABLE)
+
+
+def test_galois_scalar_semantics(oracle_lib):
+    L = oracle_lib.lib()
+    # Galois.java:198-253 edge cases
+    assert L.orc_gal_multiply(0, 7) == 0 and L.orc_gal_multiply(7, 0) == 0
+    assert L.orc_gal_exp(0, 0) == 1 and L.orc_gal_exp(0, 3) == 0
+    assert L.orc_gal_divide(0, 0) == 0  # a == 0 short-circuits before the divisor check
+    assert L.orc_gal_divide(5, 0) < 0
+    assert oracle_lib.lib().orc_last_error() == b"Argument 'divisor' is 0"
+    for a in range(1, 256):
+        for b in (1, 2, 3, 29, 255):
+            q = L.orc_gal_divide(a, b)
+            assert L.orc_gal_multiply(q, b) == a
+    # the 16 generating polynomials listed at Galois.java:38-39
+    import ctypes as C
+    out = (C.c_int * 256)()
+    n = L.orc_all_possible_polynomials(out)
+    assert list(out)[:n] == [29, 43, 45, 77, 95, 99, 101, 105, 113, 135, 141, 169, 195, 207, 231, 245]
+
+
+def test_known_answer_5_5(oracle_lib):
+    c = oracle_lib.Codec(5, 5)
+    data = [[0, 1], [4, 5], [2, 3], [6, 7], [8, 9]]
+    shards = [np.array(d, np.uint8) for d in data] + [np.zeros(2, np.uint8) for _ in range(5)]
+    c.encode_parity(shards, 0, 2)
+    assert [s.tolist() for s in shards[5:]] == [[12, 13], [10, 11], [14, 15], [90, 91], [94, 95]]
+
+
+@pytest.mark.parametrize("k,m", [(4, 2), (10, 4), (17, 3), (5, 5), (1, 1), (3, 0), (2, 6)])
+def test_c_and_numpy_restatements_agree(oracle_lib, k, m):
+    assert np.array_equal(oracle_lib.build_matrix(k, k + m), nr.build_matrix(k, k + m))
+    g = nr.build_matrix(k, k + m)
+    assert np.array_equal(g[:k], np.eye(k, dtype=np.uint8))  # systematic
+
+
+def test_generator_rows_survey_appendix(golden_dir):
+    d = json.load(open(os.path.join(golden_dir, "rs_small.json")))
+    assert d["generator_4_2"][4:] == [[27, 28, 18, 20], [28, 27, 20, 18]]
+    assert d["generator_10_4"][10] == [129, 150, 175, 184, 210, 196, 254, 232, 3, 2]
+    assert d["generator_17_3_row0"] == [148, 148, 115, 115, 221, 221, 48, 48, 227, 227, 238, 238, 87, 87, 81, 81, 1]
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 1000, 4097])
+def test_all_twelve_coding_loops_agree(oracle_lib, n):
+    rng = np.random.default_rng(n)
+    rows = rng.integers(0, 256, size=(3, 5), dtype=np.uint8)
+    inputs = [rng.integers(0, 256, size=n + 9, dtype=np.uint8) for _ in range(5)]
+    results = []
+    for loop_id in range(12):
+        outs = [np.full(n + 9, 0xAB, np.uint8) for _ in range(3)]
+        oracle_lib.code_some_shards(loop_id, rows, inputs, outs, 4, n)
+        results.append(outs)
+        assert all((o[:4] == 0xAB).all() and (o[4 + n:] == 0xAB).all() for o in outs)  # range respected
+    for r in results[1:]:
+        assert all(np.array_equal(a, b) for a, b in zip(results[0], r))
+    ref = [np.zeros(n + 9, np.uint8) for _ in range(3)]
+    nr.code_some_shards(rows, inputs, ref, 4, n)
+    assert all(np.array_equal(a[4:4 + n], b[4:4 + n]) for a, b in zip(ref, results[7]))
+
+
+def test_check_some_shards_both_variants(oracle_lib):
+    rng = np.random.default_rng(1)
+    rows = nr.build_matrix(4, 6)[4:]
+    inputs = [rng.integers(0, 256, 64, dtype=np.uint8) for _ in range(4)]
+    outs = [np.zeros(64, np.uint8) for _ in range(2)]
+    nr.code_some_shards(rows, inputs, outs, 0, 64)
+    tmp = np.zeros(64, np.uint8)
+    assert oracle_lib.check_some_shards(rows, inputs, outs, 0, 64)
+    assert oracle_lib.check_some_shards(rows, inputs, outs, 0, 64, tmp)
+    outs[1][63] ^= 1
+    assert not oracle_lib.check_some_shards(rows, inputs, outs, 0, 64)
+    assert not oracle_lib.check_some_shards(rows, inputs, outs, 0, 64, tmp)
+    assert oracle_lib.check_some_shards(rows, inputs, outs, 0, 63)
+
+
+def erasure_sets(total, m):
+    for e in range(0, m + 1):
+        yield from itertools.combinations(range(total), e)
+
+
+@pytest.mark.parametrize("k,m", [(4, 2), (10, 4), (3, 3)])
+def test_round_trip_every_erasure_subset(oracle_lib, k, m):
+    c = oracle_lib.Codec(k, m)
+    rs = nr.ReedSolomonRef(k, m)
+    S = 64
+    data = nr.synthetic_stripe(0x5EED, 3, k, S)
+    base = [data[i].copy() for i in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
+    c.encode_parity(base, 0, S)
+    assert c.is_parity_correct(base, 0, S)
+    for miss in erasure_sets(k + m, m):
+        sh = [b.copy() for b in base]
+        for j in miss:
+            sh[j][:] = 0
+        present = [i not in miss for i in range(k + m)]
+        c.decode_missing(sh, present, 0, S)
+        assert all(np.array_equal(a, b) for a, b in zip(sh, base)), miss
+        sh2 = [b.copy() for b in base]
+        for j in miss:
+            sh2[j][:] = 0
+        rs.decode_missing(sh2, present, 0, S)
+        assert all(np.array_equal(a, b) for a, b in zip(sh2, base)), miss
+
+
+def test_reference_round_trip_tests_seeded(oracle_lib):
+    """ReedSolomonTest.testBasicEncodingAndDecoding / testDecodeMissingShards
+    (ReedSolomonTest.java:70-93) on a 2 MB seeded file (the reference uses 200 MB
+    of unseeded java.util.Random)."""
+    rng = np.random.default_rng(2023)
+    data = rng.integers(0, 256, 2_000_000, dtype=np.uint8).tobytes()
+    c = oracle_lib.Codec(4, 2)
+    shards = c.file_encode(data)
+    assert c.file_decode(shards, [True] * 6, len(data)) == data
+    erased = shards.copy()
+    erased[5] = 0  # ParityDiskTwo
+    erased[0] = 0  # DataDiskOne
+    assert c.file_decode(erased, [False, True, True, True, True, False], len(data)) == data
+
+
+def test_reference_fixture_test_txt(oracle_lib, golden_dir):
+    raw = open(os.path.join(golden_dir, "reference_test.txt"), "rb").read()
+    exp = json.load(open(os.path.join(golden_dir, "rs_small.json")))["reference_test_txt"]
+    assert hashlib.sha256(raw).hexdigest() == exp["sha256"]
+    c = oracle_lib.Codec(4, 2)
+    shards = c.file_encode(raw)
+    assert shards.shape[1] == exp["shard_len"] == 23000
+    assert [hashlib.sha256(shards[i].tobytes()).hexdigest() for i in range(6)] == exp["shard_sha256"]
+    # SURVEY.md 8c digests (prefixes)
+    assert [hashlib.sha256(shards[i].tobytes()).hexdigest()[:16] for i in range(6)] == [
+        "1801edd458223445", "1801edd458223445", "377336b103dbb41b", "082d5bd597c83de1",
+        "e729eb68ab0edff9", "5873e6fec2830015"]
+    for miss in erasure_sets(6, 2):
+        er = shards.copy()
+        for j in miss:
+            er[j] = 0
+        assert c.file_decode(er, [i not in miss for i in range(6)], len(raw)) == raw
+
+
+def test_layout_pad_split_merge_edges():
+    for n in (0, 1, 999, 1000, 3999, 4000, 4001, 12345):
+        data = bytes((i * 7 + 3) & 0xFF for i in range(n))
+        sh = nr.split_file(data, 4, 2)
+        assert sh.shape[1] == nr.padded_size(n) // 4
+        assert nr.merge_file(sh, 4, n) == data
+
+
+def test_error_contract(oracle_lib):
+    c = oracle_lib.Codec(4, 2)
+    sh = [np.zeros(10, np.uint8) for _ in range(6)]
+    with pytest.raises(ValueError, match="^wrong number of shards: 5$"):
+        c.encode_parity(sh[:5], 0, 10)
+    with pytest.raises(ValueError, match="^Shards are different sizes$"):
+        c.encode_parity(sh[:5] + [np.zeros(11, np.uint8)], 0, 10)
+    with pytest.raises(ValueError, match="^offset is negative: -1$"):
+        c.encode_parity(sh, -1, 10)
+    with pytest.raises(ValueError, match="^byteCount is negative: -2$"):
+        c.encode_parity(sh, 0, -2)
+    with pytest.raises(ValueError, match="^buffers to small: 83$"):  # "8" + "3"
+        c.encode_parity(sh, 3, 8)
+    with pytest.raises(ValueError, match="^Not enough shards present$"):
+        c.decode_missing(sh, [True, True, True, False, False, False], 0, 10)
+    with pytest.raises(ValueError, match="^too many shards - max is 256$"):
+        oracle_lib.Codec(200, 57)
