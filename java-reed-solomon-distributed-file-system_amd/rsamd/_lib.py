@@ -55,6 +55,15 @@ def load():
     """Return the loaded library (raises OSError if it has not been built)."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: torch bundles its own libamdhip64 (soname
+        # libamdhip64.so.7, loaded by file name "libamdhip64.so").  If torch is
+        # loaded first, librsamd's DT_NEEDED libamdhip64.so.7 binds to that same
+        # runtime; loaded the other way round the process would get two runtimes
+        # and torch would see no GPU.  Without torch, /opt/rocm's runtime is used.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise OSError(f"librsamd.so not built at {LIB_PATH}; run __graft_entry__.build() "
                           f"(make -C {CSRC})")
