@@ -122,6 +122,9 @@ def main():
     cpu = None
     if rank == 0 and not args.no_extras:
         extra = device_extras(torch, rs, rdev, buf, lay, stream, k, m, S, B)
+        del buf
+        torch.cuda.empty_cache()
+        extra.update(other_configs(torch, rsamd, rdev, dev, stream))
         if world == 1:
             cpu = cpu_baseline(k, m, S, args.cpu_seconds)
             extra.update(host_inclusive(rsamd, k, m))
@@ -154,7 +157,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
-                "kernel": f"gf_vec_kernel<{k},{m},...> (rs_encode_batch_dev)",
+                "kernel": f"gf_vec_kernel<{k},{m},false> (rs_encode_batch_dev)",
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_ms": round(launch_ms, 4),
             },
@@ -187,11 +190,36 @@ def device_extras(torch, rs, rdev, buf, lay, stream, k, m, S, B):
         key = "decode_" + "_".join(map(str, miss))
         out[key + "_GiBps"] = round(k * S * B / t / 2**30, 2)
         out[key + "_hbm_frac"] = round((k + e) * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
-    # restore parity (decode rewrote the "missing" shards with identical bytes)
     n = min(buf.numel() // 2, 8 << 30)
     t = timed(torch, stream, lambda: rdev.copy(buf.data_ptr() + n, buf.data_ptr(), n, stream), 5)
     out["copy_kernel_GBps"] = round(2 * n / t / 1e9, 1)
     out["copy_kernel_hbm_frac"] = round(2 * n / t / 1e9 / HBM_PEAK_GBPS, 4)
+    return out
+
+
+def other_configs(torch, rsamd, rdev, dev, stream):
+    """BASELINE configs[3] (10+4 x 4 MiB; the per-GPU share of 1024 stripes over
+    8 GPUs) and configs[4] (4+2 x 4 KiB x 1 M stripes), encode and decode."""
+    from rsamd.device import StripeLayout
+    out = {}
+    for name, k, m, S, B, miss in [("cfg3_10p4_4MiB_x128", 10, 4, 4 << 20, 128, (0, 1, 2, 3)),
+                                   ("cfg4_4p2_4KiB_x1M", 4, 2, 4096, 1 << 20, (0, 1))]:
+        rs = rsamd.ReedSolomon.create(k, m)
+        lay = StripeLayout.packed(B, k + m, S)
+        buf = torch.empty(lay.nbytes, dtype=torch.uint8, device=dev)
+        rdev.fill_synthetic(buf.data_ptr(), k, lay, SEED, 0, stream)
+        t = timed(torch, stream, lambda: rdev.encode(rs, buf.data_ptr(), lay, stream), 10)
+        out[name + "_encode_GiBps"] = round(k * S * B / t / 2**30, 2)
+        out[name + "_encode_hbm_frac"] = round((k + m) * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
+        present = [i not in miss for i in range(k + m)]
+        t = timed(torch, stream, lambda: rdev.decode(rs, buf.data_ptr(), present, lay, stream), 10)
+        out[name + "_decode_" + "_".join(map(str, miss)) + "_GiBps"] = round(k * S * B / t / 2**30, 2)
+        out[name + "_decode_hbm_frac"] = round((k + len(miss)) * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
+        flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        rdev.verify(rs, buf.data_ptr(), lay, flag.data_ptr(), stream)
+        out[name + "_verified"] = int(flag.item()) == 0
+        del buf
+        torch.cuda.empty_cache()
     return out
 
 
