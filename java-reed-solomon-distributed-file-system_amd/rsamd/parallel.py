@@ -1,0 +1,93 @@
+"""Stripe partitioning across GPUs (one process per GPU).
+
+Stripes are independent: GPU g owns a contiguous range
+of stripe indices and codes it with no data-path collective.  torch.distributed
+is used only to line ranks up for timing and to reduce a few scalars (elapsed
+time, verification flags).  The backend is RCCL ("nccl") on GPU nodes; set
+RSAMD_DIST_BACKEND=gloo to run several ranks on one GPU or on CPU.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+
+@dataclass(frozen=True)
+class Rank:
+    rank: int
+    world: int
+    local: int
+    backend: str
+
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1
+
+
+def stripe_partition(total_stripes: int, world: int, rank: int):
+    """Contiguous [start, start+count) share of `total_stripes` for `rank`;
+    shares differ by at most one stripe and cover every stripe exactly once."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} of world {world}")
+    base, extra = divmod(total_stripes, world)
+    start = rank * base + min(rank, extra)
+    return start, base + (1 if rank < extra else 0)
+
+
+def init_from_env(use_gpu: bool = True) -> Rank:
+    """Read RANK / WORLD_SIZE / LOCAL_RANK (torch.distributed.run), select the
+    local GPU and initialise the process group when world > 1."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("RSAMD_DIST_BACKEND", "nccl" if use_gpu else "gloo")
+    import torch
+    if use_gpu:
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+    if world > 1:
+        import torch.distributed as dist
+        if not dist.is_initialized():
+            kw = {}
+            if backend == "nccl":
+                kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
+            dist.init_process_group(backend, **kw)
+    return Rank(rank, world, local, backend)
+
+
+def _reduce(r: Rank, value: float, op: str, dtype=None) -> float:
+    if not r.distributed:
+        return value
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", torch.cuda.current_device()) if r.backend == "nccl" else torch.device("cpu")
+    t = torch.tensor([value], dtype=dtype or torch.float64, device=dev)
+    dist.all_reduce(t, op=getattr(dist.ReduceOp, op))
+    return float(t.item())
+
+
+def max_over_ranks(r: Rank, value: float) -> float:
+    return _reduce(r, value, "MAX")
+
+
+def sum_over_ranks(r: Rank, value: float) -> float:
+    return _reduce(r, value, "SUM")
+
+
+def all_ranks_true(r: Rank, flag: bool) -> bool:
+    return _reduce(r, 0.0 if flag else 1.0, "MAX") == 0.0
+
+
+def barrier(r: Rank, sync_gpu: bool = True) -> None:
+    if sync_gpu:
+        import torch
+        torch.cuda.synchronize()
+    if r.distributed:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def shutdown(r: Rank) -> None:
+    if r.distributed:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()

@@ -22,6 +22,12 @@ echo "== bench $(date +%T)"
 timeout -k 10 400 python3 bench.py > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err" || { tail -30 "$OUT/bench_$TAG.err"; exit 1; }
 cat "$OUT/bench_$TAG.json"
 
+echo "== 2-rank bench on one GPU (gloo; exercises the multi-rank path) $(date +%T)"
+RSAMD_DIST_BACKEND=gloo timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+    --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --stripes 512 --steps 5 --warmup 2 --no-extras \
+    > "$OUT/bench2rank_$TAG.json" 2> "$OUT/bench2rank_$TAG.err" || { tail -30 "$OUT/bench2rank_$TAG.err"; exit 1; }
+cat "$OUT/bench2rank_$TAG.json"
+
 echo "== rocprofv3 kernel trace $(date +%T)"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- \
     python3 "$R/bench.py" --steps 10 --warmup 2 --no-extras > "$OUT/prof_$TAG.log" 2>&1 || { tail -30 "$OUT/prof_$TAG.log"; exit 1; }
