@@ -155,6 +155,47 @@ RS_API int rs_verify_batch_dev(const rs_codec *codec, const uint8_t *dev_base, s
                         int *dev_mismatch, void *stream);
 
 /* ---------------------------------------------------------------------------
+ * Client file layout: ReedSolomonEncoder /
+ * ReedSolomonDecoder (client/ReedSolomonEncoder.java:56-85,
+ * client/ReedSolomonDecoder.java:33-39,62-103, ConfigVariables.java:4-9).
+ * The file is zero-padded to a multiple of k*block; file block b goes to data
+ * shard b % k at offset (b / k) * block; shard_len = padded / k.  The DFS uses
+ * block = 1000, k = 4, m = 2.  For k == 4, block % 8 == 0 and aligned
+ * buffers, encode reads the file and decode writes it inside the coding
+ * kernels (no separate split / merge pass).
+ * ------------------------------------------------------------------------- */
+
+/* pad() geometry (ReedSolomonEncoder.java:76-85): padded length and shard length. */
+RS_API int rs_file_layout(const rs_codec *codec, int64_t file_len, int32_t block, int64_t *padded_len,
+                          int64_t *shard_len);
+
+/* ReedSolomonEncoder.encode() (ReedSolomonEncoder.java:56-74) on host buffers:
+ * pad + split + encodeParity.  shards_out[0..k+m) must each hold shard_len
+ * bytes (rs_file_layout); data shards and parity are written. */
+RS_API int rs_file_encode(const rs_codec *codec, const uint8_t *file, int64_t file_len, int32_t block,
+                          uint8_t *const *shards_out, int nshards, const int64_t *shard_lens);
+
+/* new ReedSolomonDecoder(shards, shardPresent, byteCntInShard, fileSize)
+ * (ReedSolomonDecoder.java:33-39): decodeMissing(shards, present, 0,
+ * byteCntInShard) -- missing shards are filled in place, as in the Java --
+ * then merge the data shards and trim to file_size into file_out.
+ * shard_lens[0] % block must be 0 and file_size <= k * shard_lens[0]
+ * (the Java would throw ArrayIndexOutOfBounds otherwise): RS_E_INVALID. */
+RS_API int rs_file_decode(const rs_codec *codec, uint8_t *const *shards, int nshards, const int64_t *shard_lens,
+                          const uint8_t *present, int32_t byte_cnt_in_shard, int32_t block, uint8_t *file_out,
+                          int64_t file_size);
+
+/* Device versions.  dev_shards holds k+m shards of shard_len bytes at
+ * dev_shards + s*shard_stride.  Encode: file -> all k+m shards.  Decode:
+ * survivors -> the trimmed file; with write_missing != 0 the absent shards
+ * are also reconstructed in dev_shards (otherwise only the file is written). */
+RS_API int rs_file_encode_dev(const rs_codec *codec, const uint8_t *dev_file, size_t file_len, size_t block,
+                              uint8_t *dev_shards, size_t shard_stride, void *stream);
+RS_API int rs_file_decode_dev(const rs_codec *codec, uint8_t *dev_shards, size_t shard_len, size_t shard_stride,
+                              const uint8_t *present, size_t block, uint8_t *dev_file_out, size_t file_size,
+                              int write_missing, void *stream);
+
+/* ---------------------------------------------------------------------------
  * Benchmark/test support (not part of the reference API).
  * ------------------------------------------------------------------------- */
 

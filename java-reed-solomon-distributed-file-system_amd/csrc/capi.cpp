@@ -18,6 +18,7 @@
 #include "codec.hpp"
 #include "gf256.hpp"
 #include "kernels.hpp"
+#include "layout.hpp"
 
 struct rs_codec {
     rsamd::Codec *impl;
@@ -61,6 +62,8 @@ struct ThreadCtx {
     uint8_t *plan = nullptr;   // per-call plan images (rs_code_some_shards)
     size_t plan_cap = 0;
     int *flag = nullptr;       // verify result
+    uint8_t *file = nullptr;   // file staging (rs_file_encode / rs_file_decode)
+    size_t file_cap = 0;
 };
 
 thread_local std::map<int, ThreadCtx *> t_ctx;
@@ -229,6 +232,100 @@ int code_rows(const uint8_t *const *rows, const uint8_t *const *inputs, int nin,
     return run_host(plans, nin + nout, in_slots, out_idx, slots.data(), size_t(offset), size_t(count), mode, result);
 }
 
+
+// ---------------------------------------------------------------------------
+// Client file layout (ReedSolomonEncoder / ReedSolomonDecoder).
+// ---------------------------------------------------------------------------
+int file_layout(const Codec &c, int64_t file_len, int64_t block, int64_t *padded, int64_t *S) {
+    if (file_len < 0) return fail(RS_E_INVALID, "file length is negative: " + std::to_string(file_len));
+    if (block < 1) return fail(RS_E_INVALID, "block size must be positive");
+    const int64_t mult = int64_t(c.k()) * block;  // ConfigVariables.FILE_SIZE_MULTIPLE
+    *padded = file_len % mult == 0 ? file_len : file_len / mult * mult + mult;  // ReedSolomonEncoder.java:76-85
+    *S = *padded / c.k();
+    return RS_OK;
+}
+
+int file_encode_dev(const Codec &c, const uint8_t *file, size_t file_len, size_t block, uint8_t *shards,
+                    size_t stride, hipStream_t s) {
+    int64_t padded = 0, S = 0;
+    int rc = file_layout(c, int64_t(file_len), int64_t(block), &padded, &S);
+    if (rc) return rc;
+    if (S == 0) return RS_OK;
+    if (!shards || (!file && file_len)) return fail(RS_E_INVALID, "NULL device buffer");
+    if (stride < size_t(S)) return fail(RS_E_INVALID, "shard_stride is smaller than the shard length");
+    rsamd::FileGeom g;
+    g.file = file;
+    g.file_len = file_len;
+    g.block = block;
+    g.k = c.k();
+    g.S = size_t(S);
+    g.shards = shards;
+    g.shard_stride = stride;
+    std::vector<DevPlan> plans;
+    RS_HIP(c.encode_plan().device_plans(&plans));
+    Geometry sg{shards, 1, 0, size_t(S), stride, stride * size_t(c.total())};
+    size_t first = 0;
+    if (rsamd::file_fusable(g, true)) {
+        RS_HIP(rsamd::launch_file_encode_fused(g, plans.empty() ? nullptr : &plans[0], s));
+        first = plans.empty() ? 0 : 1;
+    } else {
+        RS_HIP(rsamd::launch_split(g, s));
+    }
+    for (size_t i = first; i < plans.size(); ++i) RS_HIP(rsamd::launch_gf(sg, plans[i], Mode::Code, nullptr, s));
+    return RS_OK;
+}
+
+int file_decode_dev(const Codec &c, uint8_t *shards, size_t S, size_t stride, const uint8_t *present, size_t block,
+                    uint8_t *file_out, size_t file_size, bool write_missing, hipStream_t s) {
+    if (!present) return fail(RS_E_INVALID, "present must not be NULL");
+    if (block < 1) return fail(RS_E_INVALID, "block size must be positive");
+    if (S % block) return fail(RS_E_INVALID, "shard length " + std::to_string(S) + " is not a multiple of the block size");
+    if (file_size > S * size_t(c.k())) return fail(RS_E_INVALID, "file size exceeds k * shard length");
+    if (stride < S) return fail(RS_E_INVALID, "shard_stride is smaller than the shard length");
+    int n_present = 0;
+    for (int i = 0; i < c.total(); ++i) n_present += present[i] ? 1 : 0;
+    if (n_present < c.k()) return fail(RS_E_NOT_ENOUGH, "Not enough shards present");
+    if (S == 0 || (file_size == 0 && !write_missing)) return RS_OK;
+    if (!shards || (!file_out && file_size)) return fail(RS_E_INVALID, "NULL device buffer");
+    rsamd::FileGeom g;
+    g.file_out = file_out;
+    g.file_len = file_size;
+    g.block = block;
+    g.k = c.k();
+    g.S = S;
+    g.shards = shards;
+    g.shard_stride = stride;
+    std::shared_ptr<const Plan> plan;
+    int n_missing_data = 0;
+    for (int i = 0; i < c.k(); ++i) n_missing_data += present[i] ? 0 : 1;
+    const bool fused = rsamd::file_fusable(g, false) && n_missing_data <= rsamd::kMaxOut;
+    if (write_missing || !fused) {
+        if (n_present < c.total()) {  // reconstruct every absent shard in place, then merge
+            int rc = c.decode_plan(present, &plan);
+            if (rc) return fail(rc, rc == RS_E_SINGULAR ? "Matrix is singular" : "Not enough shards present");
+            std::vector<DevPlan> plans;
+            RS_HIP(plan->device_plans(&plans));
+            Geometry sg{shards, 1, 0, S, stride, stride * size_t(c.total())};
+            for (const DevPlan &p : plans) RS_HIP(rsamd::launch_gf(sg, p, Mode::Code, nullptr, s));
+        }
+        if (file_size == 0) return RS_OK;
+        if (!rsamd::file_fusable(g, false)) {
+            RS_HIP(rsamd::launch_merge(g, s));
+            return RS_OK;
+        }
+        std::vector<uint8_t> all(c.total(), 1);  // every shard now holds its bytes: pure merge
+        int rc = c.decode_plan(all.data(), &plan, true);
+        if (rc) return fail(rc, "decode plan");
+    } else {
+        int rc = c.decode_plan(present, &plan, true);
+        if (rc) return fail(rc, rc == RS_E_SINGULAR ? "Matrix is singular" : "Not enough shards present");
+    }
+    rsamd::FileDecodePlan fp;
+    RS_HIP(plan->device_file_plan(c.k(), &fp));
+    RS_HIP(rsamd::launch_file_decode_fused(g, fp, s));
+    return RS_OK;
+}
+
 const Codec *impl(const rs_codec *c) { return c ? c->impl : nullptr; }
 
 }  // namespace
@@ -291,6 +388,7 @@ void rs_thread_release(void) {
         if (c->stage) (void)hipFree(c->stage);
         if (c->plan) (void)hipFree(c->plan);
         if (c->flag) (void)hipFree(c->flag);
+        if (c->file) (void)hipFree(c->file);
         delete c;
     }
     t_ctx.clear();
@@ -405,6 +503,94 @@ int rs_verify_batch_dev(const rs_codec *codec, const uint8_t *dev_base, size_t n
     Geometry g{const_cast<uint8_t *>(dev_base), n_stripes, 0, shard_len, shard_stride, stripe_stride};
     for (const DevPlan &p : plans)
         RS_HIP(rsamd::launch_gf(g, p, Mode::Verify, dev_mismatch, static_cast<hipStream_t>(stream)));
+    return RS_OK;
+}
+
+int rs_file_layout(const rs_codec *codec, int64_t file_len, int32_t block, int64_t *padded_len, int64_t *shard_len) {
+    const Codec *c = impl(codec);
+    if (!c || !padded_len || !shard_len) return fail(RS_E_INVALID, "NULL argument");
+    return file_layout(*c, file_len, block, padded_len, shard_len);
+}
+
+int rs_file_encode_dev(const rs_codec *codec, const uint8_t *dev_file, size_t file_len, size_t block,
+                       uint8_t *dev_shards, size_t shard_stride, void *stream) {
+    const Codec *c = impl(codec);
+    if (!c) return fail(RS_E_INVALID, "codec is NULL");
+    return file_encode_dev(*c, dev_file, file_len, block, dev_shards, shard_stride, static_cast<hipStream_t>(stream));
+}
+
+int rs_file_decode_dev(const rs_codec *codec, uint8_t *dev_shards, size_t shard_len, size_t shard_stride,
+                       const uint8_t *present, size_t block, uint8_t *dev_file_out, size_t file_size,
+                       int write_missing, void *stream) {
+    const Codec *c = impl(codec);
+    if (!c) return fail(RS_E_INVALID, "codec is NULL");
+    return file_decode_dev(*c, dev_shards, shard_len, shard_stride, present, block, dev_file_out, file_size,
+                           write_missing != 0, static_cast<hipStream_t>(stream));
+}
+
+int rs_file_encode(const rs_codec *codec, const uint8_t *file, int64_t file_len, int32_t block,
+                   uint8_t *const *shards_out, int nshards, const int64_t *shard_lens) {
+    const Codec *c = impl(codec);
+    if (!c) return fail(RS_E_INVALID, "codec is NULL");
+    int64_t padded = 0, S = 0;
+    int rc = file_layout(*c, file_len, block, &padded, &S);
+    if (rc) return rc;
+    if (nshards != c->total()) return fail(RS_E_WRONG_NSHARDS, "wrong number of shards: " + std::to_string(nshards));
+    if (!shards_out || !shard_lens || (!file && file_len)) return fail(RS_E_INVALID, "NULL argument");
+    for (int i = 0; i < nshards; ++i)
+        if (shard_lens[i] < S || (!shards_out[i] && S)) return fail(RS_E_INVALID, "shard " + std::to_string(i) + " is shorter than " + std::to_string(S));
+    if (S == 0) return RS_OK;
+    rc = need_device();
+    if (rc) return rc;
+    ThreadCtx *ctx = nullptr;
+    rc = thread_ctx(&ctx);
+    if (rc) return rc;
+    const size_t stride = round_up(size_t(S), 256);
+    const size_t file_bytes = round_up(size_t(file_len), 256);
+    rc = grow(&ctx->file, &ctx->file_cap, file_bytes + stride * size_t(c->total()));
+    if (rc) return rc;
+    uint8_t *dfile = ctx->file, *dsh = ctx->file + file_bytes;
+    if (file_len) RS_HIP(hipMemcpyAsync(dfile, file, size_t(file_len), hipMemcpyHostToDevice, ctx->stream));
+    rc = file_encode_dev(*c, dfile, size_t(file_len), size_t(block), dsh, stride, ctx->stream);
+    if (rc) return rc;
+    for (int i = 0; i < c->total(); ++i)
+        RS_HIP(hipMemcpyAsync(shards_out[i], dsh + size_t(i) * stride, size_t(S), hipMemcpyDeviceToHost, ctx->stream));
+    RS_HIP(hipStreamSynchronize(ctx->stream));
+    return RS_OK;
+}
+
+int rs_file_decode(const rs_codec *codec, uint8_t *const *shards, int nshards, const int64_t *shard_lens,
+                   const uint8_t *present, int32_t byte_cnt_in_shard, int32_t block, uint8_t *file_out,
+                   int64_t file_size) {
+    const Codec *c = impl(codec);
+    if (!c) return fail(RS_E_INVALID, "codec is NULL");
+    // decodeMissing(shards, shardPresent, 0, byteCntInShard)  (ReedSolomonDecoder.java:36)
+    int rc = rs_decode_missing(codec, shards, nshards, shard_lens, present, 0, byte_cnt_in_shard);
+    if (rc) return rc;
+    // mergeShardsToFile + trimPadding (ReedSolomonDecoder.java:92-103, 62-66) over shards[0].length
+    const int64_t S = shard_lens[0];
+    if (block < 1 || S % block) return fail(RS_E_INVALID, "shard length " + std::to_string(S) + " is not a multiple of the block size");
+    if (file_size < 0 || file_size > S * c->k()) return fail(RS_E_INVALID, "file size exceeds k * shard length");
+    if (file_size == 0) return RS_OK;
+    if (!file_out) return fail(RS_E_INVALID, "file_out is NULL");
+    rc = need_device();
+    if (rc) return rc;
+    ThreadCtx *ctx = nullptr;
+    rc = thread_ctx(&ctx);
+    if (rc) return rc;
+    const size_t stride = round_up(size_t(S), 256);
+    const size_t file_bytes = round_up(size_t(file_size), 256);
+    rc = grow(&ctx->file, &ctx->file_cap, file_bytes + stride * size_t(c->total()));
+    if (rc) return rc;
+    uint8_t *dfile = ctx->file, *dsh = ctx->file + file_bytes;
+    for (int i = 0; i < c->k(); ++i)
+        RS_HIP(hipMemcpyAsync(dsh + size_t(i) * stride, shards[i], size_t(S), hipMemcpyHostToDevice, ctx->stream));
+    std::vector<uint8_t> all(c->total(), 1);  // shards are complete now: merge only
+    rc = file_decode_dev(*c, dsh, size_t(S), stride, all.data(), size_t(block), dfile, size_t(file_size), false,
+                         ctx->stream);
+    if (rc) return rc;
+    RS_HIP(hipMemcpyAsync(file_out, dfile, size_t(file_size), hipMemcpyDeviceToHost, ctx->stream));
+    RS_HIP(hipStreamSynchronize(ctx->stream));
     return RS_OK;
 }
 

@@ -89,6 +89,52 @@ hipError_t Plan::device_plans(std::vector<DevPlan> *out) const {
     return hipSuccess;
 }
 
+hipError_t Plan::device_file_plan(int k, FileDecodePlan *out) const {
+    const int E = int(out_idx_.size());
+    if (E > kMaxOut || int(in_idx_.size()) != k) return hipErrorInvalidValue;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const size_t tabs_bytes = size_t(k) * E * sizeof(PermTable);
+    std::lock_guard<std::mutex> lock(mu_);
+    auto it = dev_file_.find(dev);
+    if (it == dev_file_.end()) {
+        std::vector<uint8_t> img(tabs_bytes + 2 * size_t(k) * sizeof(int32_t));
+        for (int j = 0; j < k; ++j)
+            for (int r = 0; r < E; ++r) {
+                const PermTable t = perm_table(rows_.at(r, j));
+                std::memcpy(img.data() + (size_t(j) * E + r) * sizeof(PermTable), &t, sizeof t);
+            }
+        for (int j = 0; j < k; ++j) {
+            const int32_t v = in_idx_[j];
+            std::memcpy(img.data() + tabs_bytes + j * sizeof(int32_t), &v, sizeof v);
+        }
+        for (int i = 0; i < k; ++i) {  // data shard i: survivor position, or -(row + 1)
+            int32_t src = 0;
+            for (int j = 0; j < k; ++j)
+                if (in_idx_[j] == i) src = j;
+            for (int r = 0; r < E; ++r)
+                if (out_idx_[r] == i) src = -(r + 1);
+            std::memcpy(img.data() + tabs_bytes + (k + i) * sizeof(int32_t), &src, sizeof src);
+        }
+        void *buf = nullptr;
+        e = hipMalloc(&buf, img.size());
+        if (e != hipSuccess) return e;
+        e = hipMemcpy(buf, img.data(), img.size(), hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            (void)hipFree(buf);
+            return e;
+        }
+        it = dev_file_.emplace(dev, buf).first;
+    }
+    const uint8_t *b = static_cast<const uint8_t *>(it->second);
+    out->tabs = reinterpret_cast<const uint32_t *>(b);
+    out->in_idx = reinterpret_cast<const int32_t *>(b + tabs_bytes);
+    out->dsrc = reinterpret_cast<const int32_t *>(b + tabs_bytes + size_t(k) * sizeof(int32_t));
+    out->n_missing_data = E;
+    return hipSuccess;
+}
+
 Codec::Codec(int k, int m) : k_(k), m_(m), matrix_(build_generator(k, k + m)) {
     std::vector<int> in(k), out(m);
     for (int i = 0; i < k; ++i) in[i] = i;
@@ -111,9 +157,10 @@ int Codec::create(int k, int m, Codec **out, std::string *err) {
     return RS_OK;
 }
 
-int Codec::decode_plan(const uint8_t *present, std::shared_ptr<const Plan> *out) const {
-    std::vector<uint8_t> key(total());
+int Codec::decode_plan(const uint8_t *present, std::shared_ptr<const Plan> *out, bool data_only) const {
+    std::vector<uint8_t> key(total() + 1);
     for (int i = 0; i < total(); ++i) key[i] = present[i] ? 1 : 0;
+    key[total()] = data_only ? 1 : 0;
     {
         std::lock_guard<std::mutex> lock(mu_);
         auto it = decode_cache_.find(key);
@@ -125,7 +172,7 @@ int Codec::decode_plan(const uint8_t *present, std::shared_ptr<const Plan> *out)
     std::vector<int> surv, missing;
     for (int i = 0; i < total(); ++i) {
         if (key[i] && int(surv.size()) < k_) surv.push_back(i);
-        if (!key[i]) missing.push_back(i);
+        if (!key[i] && (!data_only || i < k_)) missing.push_back(i);
     }
     if (int(surv.size()) < k_) return RS_E_NOT_ENOUGH;
     GfMatrix dinv;

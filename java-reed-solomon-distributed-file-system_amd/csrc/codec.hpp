@@ -14,6 +14,7 @@
 
 #include "gf256.hpp"
 #include "kernels.hpp"
+#include "layout.hpp"
 
 namespace rsamd {
 
@@ -34,11 +35,16 @@ public:
     // The flat image uploaded for group g (exposed for per-call uploads).
     std::vector<uint8_t> image(int g) const;
 
+    // Device image of a data-only decode plan for the fused decode-to-file
+    // kernel (layout.hpp FileDecodePlan); k data shards, <= kMaxOut missing.
+    hipError_t device_file_plan(int k, FileDecodePlan *out) const;
+
 private:
     std::vector<int> in_idx_, out_idx_;
     GfMatrix rows_;
     mutable std::mutex mu_;
-    mutable std::map<int, void *> dev_;  // device id -> allocation of all groups
+    mutable std::map<int, void *> dev_;       // device id -> allocation of all groups
+    mutable std::map<int, void *> dev_file_;  // device id -> FileDecodePlan image
 };
 
 // Offsets of one group's image: tabs, then in_idx, then out_idx.
@@ -63,8 +69,10 @@ public:
     // the first k present shards (ReedSolomon.java:210-223); outputs = every
     // absent shard in ascending order; rows: Dinv[j] for a missing data shard j,
     // parityRow[p] * Dinv for a missing parity shard.
-    // Returns 0, RS_E_NOT_ENOUGH-style negative code, or RS_E_SINGULAR.
-    int decode_plan(const uint8_t *present, std::shared_ptr<const Plan> *out) const;
+    // With data_only, outputs are the absent DATA shards only (the fused
+    // decode-to-file path needs no parity).  Returns 0, RS_E_NOT_ENOUGH or
+    // RS_E_SINGULAR.
+    int decode_plan(const uint8_t *present, std::shared_ptr<const Plan> *out, bool data_only = false) const;
 
 private:
     Codec(int k, int m);

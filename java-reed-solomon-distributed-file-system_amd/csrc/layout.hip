@@ -1,0 +1,315 @@
+// layout.hip -- the client's file <-> shard layout fused into the codec kernels
+// (SURVEY.md section 8 row f1).
+//
+// Reference layout (ReedSolomonEncoder.java:56-85, ReedSolomonDecoder.java:62-103,
+// ConfigVariables.java:4-9): the file is zero-padded to a multiple of k*block;
+// block b (block bytes) goes to data shard b % k at offset (b / k) * block, so a
+// shard is S = padded / k bytes; the decoder merges the blocks back and trims
+// to the file size.  Equivalently, shard column c = r*block + w of data shard i
+// holds file byte (r*k + i)*block + w.
+//
+// The fused kernels read the file (or write it) directly:
+//   file_encode_kernel<K,M>: file -> K data shards + M parity shards, one pass,
+//     traffic k*S read + (k+m)*S written (instead of split + encode: (3k+m)*S).
+//   file_decode_kernel<K,E>: K survivors -> file, the E missing data shards
+//     computed in registers, traffic k*S read + file_size written.
+// block % 8 == 0 (the DFS uses 1000), so every 8-byte half of a lane's 16-byte
+// column vector maps to one contiguous 8-byte run of the file.  Any other
+// block size, alignment or k uses the generic split / merge kernels plus the
+// stripe kernels of kernels.hip.
+#include "layout.hpp"
+
+#include <algorithm>
+#include <climits>
+
+#include "gf_device.hpp"
+
+namespace rsamd {
+namespace {
+
+using namespace dev;
+
+constexpr int kWave = 64;
+constexpr int kThreads = 256;
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+struct FileArgs {
+    const uint8_t *file;  // encode: source file
+    uint8_t *file_out;    // decode: destination file
+    uint64_t file_len;    // encode: unpadded length; decode: trimmed file size
+    uint8_t *shards;
+    uint64_t shard_stride;
+    uint64_t S;           // shard length (a multiple of block)
+    uint32_t block;
+    uint32_t nvec;        // ceil(S / 16)
+    const uint32_t *tabs; // [K][M or E][5]
+    const int32_t *in_idx;  // decode: survivor shard indices [K]
+    const int32_t *dsrc;    // decode: data shard i -> survivor position (>= 0) or -(row + 1)
+};
+
+// File byte runs of 8: [f, f+8) clipped to len, zero beyond (the padding).
+__device__ __forceinline__ u32x2 load8(const uint8_t *file, uint64_t len, uint64_t f) {
+    if (f + 8 <= len) return __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(file + f));
+    uint64_t v = 0;
+    for (uint64_t b = f; b < len && b < f + 8; ++b) v |= uint64_t(file[b]) << (8 * (b - f));
+    return u32x2{uint32_t(v), uint32_t(v >> 32)};
+}
+
+__device__ __forceinline__ void store8(uint8_t *file, uint64_t len, uint64_t f, u32x2 v) {
+    if (f + 8 <= len) {
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x2 *>(file + f));
+        return;
+    }
+    const uint64_t x = uint64_t(v[0]) | uint64_t(v[1]) << 32;
+    for (uint64_t b = f; b < len && b < f + 8; ++b) file[b] = uint8_t(x >> (8 * (b - f)));
+}
+
+// Row r and in-row offset w of shard column cc = c0 + d, given the
+// block-uniform (r0, w0) of c0 and 0 <= d < 1024.
+__device__ __forceinline__ void row_of(uint64_t r0, uint32_t w0, uint32_t d, uint32_t block, uint64_t &r,
+                                       uint32_t &w) {
+    r = r0;
+    w = w0 + d;
+    while (w >= block) {
+        w -= block;
+        ++r;
+    }
+}
+
+template <int K, int M>
+__global__ void __launch_bounds__(kWave) file_encode_kernel(FileArgs a) {
+    const uint32_t v = blockIdx.x * kWave + threadIdx.x;
+    const uint64_t c0 = uint64_t(blockIdx.x) * kWave * 16;  // block-uniform first column
+    const uint64_t r0 = c0 / a.block;
+    const uint32_t w0 = uint32_t(c0 - r0 * a.block);
+    if (v >= a.nvec) return;
+    const uint64_t c = uint64_t(v) * 16;
+    const bool hi = c + 16 <= a.S;  // the last vector of a shard may be a single 8-byte half
+    uint64_t rr[2];
+    uint32_t ww[2];
+    row_of(r0, w0, threadIdx.x * 16, a.block, rr[0], ww[0]);
+    row_of(r0, w0, threadIdx.x * 16 + 8, a.block, rr[1], ww[1]);
+
+    u32x4 x[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const u32x2 lo = load8(a.file, a.file_len, (rr[0] * K + i) * a.block + ww[0]);
+        const u32x2 up = hi ? load8(a.file, a.file_len, (rr[1] * K + i) * a.block + ww[1]) : u32x2{0, 0};
+        x[i] = u32x4{lo[0], lo[1], up[0], up[1]};
+    }
+    uint8_t *col = a.shards + c;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        uint8_t *dst = col + uint64_t(i) * a.shard_stride;
+        if (hi)
+            __builtin_nontemporal_store(x[i], reinterpret_cast<u32x4 *>(dst));
+        else
+            __builtin_nontemporal_store(u32x2{x[i][0], x[i][1]}, reinterpret_cast<u32x2 *>(dst));
+    }
+    if (M == 0) return;
+    u32x4 acc[M > 0 ? M : 1];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        Sel s[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) s[i] = selectors(x[i][w]);
+#pragma unroll
+        for (int p = 0; p < M; ++p) {
+            uint32_t T[K][5];
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+#pragma unroll
+                for (int j = 0; j < 5; ++j) T[i][j] = a.tabs[(i * M + p) * 5 + j];
+            acc[p][w] = dot_dword<K>(T, s);
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < M; ++p) {
+        uint8_t *dst = col + uint64_t(K + p) * a.shard_stride;
+        if (hi)
+            __builtin_nontemporal_store(acc[p], reinterpret_cast<u32x4 *>(dst));
+        else
+            __builtin_nontemporal_store(u32x2{acc[p][0], acc[p][1]}, reinterpret_cast<u32x2 *>(dst));
+    }
+}
+
+template <int N>
+__device__ __forceinline__ u32x4 pick(const u32x4 (&v)[N], int idx) {
+    u32x4 r = v[0];
+#pragma unroll
+    for (int j = 1; j < N; ++j)
+        if (idx == j) r = v[j];
+    return r;
+}
+
+template <int K, int E>
+__global__ void __launch_bounds__(kWave) file_decode_kernel(FileArgs a) {
+    const uint32_t v = blockIdx.x * kWave + threadIdx.x;
+    const uint64_t c0 = uint64_t(blockIdx.x) * kWave * 16;
+    const uint64_t r0 = c0 / a.block;
+    const uint32_t w0 = uint32_t(c0 - r0 * a.block);
+    int dsrc[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) dsrc[i] = a.dsrc[i];
+    if (v >= a.nvec) return;
+    const uint64_t c = uint64_t(v) * 16;
+    const bool hi = c + 16 <= a.S;
+    u32x4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const uint8_t *src = a.shards + uint64_t(a.in_idx[j]) * a.shard_stride + c;
+        if (hi) {
+            x[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src));
+        } else {
+            const u32x2 h = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(src));
+            x[j] = u32x4{h[0], h[1], 0, 0};
+        }
+    }
+    u32x4 y[E > 0 ? E : 1];
+    if (E > 0) {
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            Sel s[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) s[j] = selectors(x[j][w]);
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                uint32_t T[K][5];
+#pragma unroll
+                for (int j = 0; j < K; ++j)
+#pragma unroll
+                    for (int q = 0; q < 5; ++q) T[j][q] = a.tabs[(j * E + e) * 5 + q];
+                y[e][w] = dot_dword<K>(T, s);
+            }
+        }
+    }
+    uint64_t rr[2];
+    uint32_t ww[2];
+    row_of(r0, w0, threadIdx.x * 16, a.block, rr[0], ww[0]);
+    row_of(r0, w0, threadIdx.x * 16 + 8, a.block, rr[1], ww[1]);
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        constexpr int EY = E > 0 ? E : 1;
+        const u32x4 d = dsrc[i] >= 0 ? pick<K>(x, dsrc[i]) : pick<EY>(y, -dsrc[i] - 1);
+        store8(a.file_out, a.file_len, (rr[0] * K + i) * a.block + ww[0], u32x2{d[0], d[1]});
+        if (hi) store8(a.file_out, a.file_len, (rr[1] * K + i) * a.block + ww[1], u32x2{d[2], d[3]});
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Generic split (file -> k data shards) and merge (k data shards -> file):
+// one thread per W-byte word of one shard, W = 8 when block % 8 == 0 and the
+// buffers are 8-aligned, else 1.
+// ---------------------------------------------------------------------------
+struct CopyArgs {
+    const uint8_t *file;
+    uint8_t *file_out;
+    uint64_t file_len;
+    uint8_t *shards;
+    uint64_t shard_stride;
+    uint64_t S;
+    uint64_t block;
+    uint64_t words_per_shard;  // ceil(S / W)
+    uint64_t total;            // k * words_per_shard
+    int k;
+};
+
+template <int W, bool SPLIT>
+__global__ void __launch_bounds__(kThreads) split_merge_kernel(CopyArgs a) {
+    const uint64_t step = uint64_t(gridDim.x) * kThreads;
+    for (uint64_t idx = uint64_t(blockIdx.x) * kThreads + threadIdx.x; idx < a.total; idx += step) {
+        const uint64_t i = idx / a.words_per_shard;
+        const uint64_t c = (idx - i * a.words_per_shard) * W;
+        const uint64_t r = c / a.block;
+        const uint64_t f = (r * a.k + i) * a.block + (c - r * a.block);
+        uint8_t *sh = a.shards + i * a.shard_stride + c;
+        const uint64_t n = a.S - c < W ? a.S - c : W;  // bytes of this word inside the shard
+        if (SPLIT) {
+            if (W == 8 && n == 8) {
+                *reinterpret_cast<u32x2 *>(sh) = load8(a.file, a.file_len, f);
+            } else {
+                for (uint64_t b = 0; b < n; ++b) sh[b] = f + b < a.file_len ? a.file[f + b] : 0;
+            }
+        } else {
+            if (W == 8 && n == 8) {
+                store8(a.file_out, a.file_len, f, *reinterpret_cast<const u32x2 *>(sh));
+            } else {
+                for (uint64_t b = 0; b < n; ++b)
+                    if (f + b < a.file_len) a.file_out[f + b] = sh[b];
+            }
+        }
+    }
+}
+
+template <int K, int M>
+hipError_t launch_enc_t(const FileArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL((file_encode_kernel<K, M>), dim3((a.nvec + kWave - 1) / kWave), dim3(kWave), 0, s, a);
+    return hipGetLastError();
+}
+
+template <int K, int E>
+hipError_t launch_dec_t(const FileArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL((file_decode_kernel<K, E>), dim3((a.nvec + kWave - 1) / kWave), dim3(kWave), 0, s, a);
+    return hipGetLastError();
+}
+
+bool aligned(const void *p, size_t a) { return reinterpret_cast<uintptr_t>(p) % a == 0; }
+
+hipError_t launch_split_merge(const FileGeom &g, bool split, hipStream_t s) {
+    const bool w8 = g.block % 8 == 0 && g.S % 8 == 0 && g.shard_stride % 8 == 0 && aligned(g.shards, 8) &&
+                    aligned(split ? static_cast<const void *>(g.file) : static_cast<const void *>(g.file_out), 8);
+    const int W = w8 ? 8 : 1;
+    CopyArgs a{g.file, g.file_out, g.file_len, g.shards, g.shard_stride, g.S, g.block, (g.S + W - 1) / W, 0, g.k};
+    a.total = uint64_t(g.k) * a.words_per_shard;
+    if (a.total == 0) return hipSuccess;
+    const unsigned grid = unsigned(std::min<uint64_t>((a.total + kThreads - 1) / kThreads, 1u << 20));
+    if (w8 && split) hipLaunchKernelGGL((split_merge_kernel<8, true>), dim3(grid), dim3(kThreads), 0, s, a);
+    if (w8 && !split) hipLaunchKernelGGL((split_merge_kernel<8, false>), dim3(grid), dim3(kThreads), 0, s, a);
+    if (!w8 && split) hipLaunchKernelGGL((split_merge_kernel<1, true>), dim3(grid), dim3(kThreads), 0, s, a);
+    if (!w8 && !split) hipLaunchKernelGGL((split_merge_kernel<1, false>), dim3(grid), dim3(kThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+bool file_fusable(const FileGeom &g, bool encode) {
+    return g.k == 4 && g.block % 8 == 0 && g.block >= 8 && g.S % g.block == 0 && g.shard_stride % 16 == 0 &&
+           aligned(g.shards, 16) &&
+           aligned(encode ? static_cast<const void *>(g.file) : static_cast<const void *>(g.file_out), 8) &&
+           (g.S + 15) / 16 <= uint64_t(INT32_MAX) * kWave;
+}
+
+hipError_t launch_file_encode_fused(const FileGeom &g, const DevPlan *parity0, hipStream_t s) {
+    if (g.S == 0) return hipSuccess;
+    FileArgs a{g.file, nullptr, g.file_len, g.shards, g.shard_stride, g.S, uint32_t(g.block),
+               uint32_t((g.S + 15) / 16), parity0 ? parity0->tabs : nullptr, nullptr, nullptr};
+    const int m = parity0 ? parity0->nout : 0;
+    switch (m) {
+    case 0: return launch_enc_t<4, 0>(a, s);
+    case 1: return launch_enc_t<4, 1>(a, s);
+    case 2: return launch_enc_t<4, 2>(a, s);
+    case 3: return launch_enc_t<4, 3>(a, s);
+    case 4: return launch_enc_t<4, 4>(a, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_file_decode_fused(const FileGeom &g, const FileDecodePlan &p, hipStream_t s) {
+    if (g.S == 0 || g.file_len == 0) return hipSuccess;
+    FileArgs a{nullptr, g.file_out, g.file_len, g.shards, g.shard_stride, g.S, uint32_t(g.block),
+               uint32_t((g.S + 15) / 16), p.tabs, p.in_idx, p.dsrc};
+    switch (p.n_missing_data) {
+    case 0: return launch_dec_t<4, 0>(a, s);
+    case 1: return launch_dec_t<4, 1>(a, s);
+    case 2: return launch_dec_t<4, 2>(a, s);
+    case 3: return launch_dec_t<4, 3>(a, s);
+    case 4: return launch_dec_t<4, 4>(a, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_split(const FileGeom &g, hipStream_t s) { return launch_split_merge(g, true, s); }
+hipError_t launch_merge(const FileGeom &g, hipStream_t s) { return launch_split_merge(g, false, s); }
+
+}  // namespace rsamd

@@ -43,6 +43,14 @@ SIGNATURES = {
                                       C.c_void_p]),
     "rs_verify_batch_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t,
                                       C.c_void_p, C.c_void_p]),
+    "rs_file_layout": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    "rs_file_encode": (C.c_int, [C.c_void_p, u8p, C.c_int64, C.c_int32, u8pp, C.c_int, C.POINTER(C.c_int64)]),
+    "rs_file_decode": (C.c_int, [C.c_void_p, u8pp, C.c_int, C.POINTER(C.c_int64), u8p, C.c_int32, C.c_int32, u8p,
+                                 C.c_int64]),
+    "rs_file_encode_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p, C.c_size_t,
+                                     C.c_void_p]),
+    "rs_file_decode_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, u8p, C.c_size_t, C.c_void_p,
+                                     C.c_size_t, C.c_int, C.c_void_p]),
     "rs_fill_synthetic_dev": (C.c_int, [C.c_void_p, C.c_int, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t,
                                         C.c_uint64, C.c_uint64, C.c_void_p]),
     "rs_copy_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),

@@ -141,3 +141,31 @@ def test_coding_without_device_fails_loudly(native):
     with pytest.raises(rsamd.GpuError):
         rs.encodeParity(sh, 0, 16)
     assert all((s == 1).all() for s in sh)
+
+
+def test_file_layout_geometry(native, oracle_lib):
+    """ReedSolomonEncoder.pad (ReedSolomonEncoder.java:76-85): round up to k*block."""
+    import rsamd
+    from rsamd.layout import file_layout
+    rs = rsamd.ReedSolomon.create(4, 2)
+    for n in (0, 1, 3999, 4000, 4001, 90999, 200_000_000):
+        padded, S = file_layout(rs, n)
+        assert padded == oracle_lib.lib().orc_padded_size(n, 4, 1000) and S == padded // 4
+    assert file_layout(rsamd.ReedSolomon.create(10, 4), 12345, 512) == (15360, 1536)
+    with pytest.raises(rsamd.IllegalArgumentException):
+        file_layout(rs, 10, 0)
+
+
+def test_file_decode_contract_without_device(native):
+    """ReedSolomonDecoder checks run before any device work: decodeMissing's
+    argument checks, then the merge's shard-length / file-size limits."""
+    import rsamd
+    from rsamd.layout import ReedSolomonDecoder
+    sh = [np.zeros(1500, np.uint8) for _ in range(6)]
+    with pytest.raises(rsamd.IllegalArgumentException, match="^Not enough shards present$"):
+        ReedSolomonDecoder(sh, [1, 1, 1, 0, 0, 0], 1500, 10)
+    with pytest.raises(rsamd.IllegalArgumentException, match="not a multiple of the block size"):
+        ReedSolomonDecoder(sh, [1] * 6, 1500, 10)
+    sh = [np.zeros(1000, np.uint8) for _ in range(6)]
+    with pytest.raises(rsamd.IllegalArgumentException, match="exceeds"):
+        ReedSolomonDecoder(sh, [1] * 6, 1000, 4001)
