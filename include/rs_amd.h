@@ -148,6 +148,19 @@ RS_API int rs_decode_batch_dev(const rs_codec *codec, uint8_t *dev_base, const u
                         size_t n_stripes, size_t shard_len, size_t shard_stride,
                         size_t stripe_stride, void *stream);
 
+/* Reconstruct with a presence pattern PER STRIPE (the
+ * master's per-chunk-group recovery, MasterImpl.java:794-839 with
+ * ChunkserverDiskRecoveryMachine.java:34-48, and client reads with different
+ * missing shards per stripe).  present is a HOST array of n_stripes x (k+m)
+ * flags.  One launch per group of <= 4 outputs; each stripe reads its own
+ * first-k-present survivors and writes its own absent shards.  Every stripe
+ * needs >= k present shards (else RS_E_NOT_ENOUGH before any launch).
+ * Asynchronous on stream; the call's small plan tables live in a per-thread
+ * staging slot that the next masked call on the same thread waits for. */
+RS_API int rs_decode_batch_masked_dev(const rs_codec *codec, uint8_t *dev_base, const uint8_t *present,
+                                      size_t n_stripes, size_t shard_len, size_t shard_stride,
+                                      size_t stripe_stride, void *stream);
+
 /* Verify parity of every stripe: dev_mismatch (a device int) is OR-ed with 1
  * when any parity byte differs.  The caller zeroes it first. */
 RS_API int rs_verify_batch_dev(const rs_codec *codec, const uint8_t *dev_base, size_t n_stripes,
@@ -188,7 +201,9 @@ RS_API int rs_file_decode(const rs_codec *codec, uint8_t *const *shards, int nsh
 /* Device versions.  dev_shards holds k+m shards of shard_len bytes at
  * dev_shards + s*shard_stride.  Encode: file -> all k+m shards.  Decode:
  * survivors -> the trimmed file; with write_missing != 0 the absent shards
- * are also reconstructed in dev_shards (otherwise only the file is written). */
+ * are also reconstructed in dev_shards.  With write_missing == 0 the absent
+ * shard buffers are scratch: the fused k == 4 path leaves them untouched, the
+ * generic path reconstructs them in place before merging. */
 RS_API int rs_file_encode_dev(const rs_codec *codec, const uint8_t *dev_file, size_t file_len, size_t block,
                               uint8_t *dev_shards, size_t shard_stride, void *stream);
 RS_API int rs_file_decode_dev(const rs_codec *codec, uint8_t *dev_shards, size_t shard_len, size_t shard_stride,

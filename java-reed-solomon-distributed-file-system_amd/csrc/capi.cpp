@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -64,6 +65,14 @@ struct ThreadCtx {
     int *flag = nullptr;       // verify result
     uint8_t *file = nullptr;   // file staging (rs_file_encode / rs_file_decode)
     size_t file_cap = 0;
+    // rs_decode_batch_masked_dev: per-call plan records (device + pinned host),
+    // reused by the next call only after `masked_done` (recorded on the
+    // caller's stream behind the kernels) has completed.
+    uint8_t *masked_dev = nullptr;
+    size_t masked_dev_cap = 0;
+    uint8_t *masked_host = nullptr;
+    size_t masked_host_cap = 0;
+    hipEvent_t masked_done = nullptr;
 };
 
 thread_local std::map<int, ThreadCtx *> t_ctx;
@@ -326,6 +335,98 @@ int file_decode_dev(const Codec &c, uint8_t *shards, size_t S, size_t stride, co
     return RS_OK;
 }
 
+
+int decode_masked_dev(const Codec &c, uint8_t *base, const uint8_t *present, size_t n_stripes, size_t shard_len,
+                      size_t shard_stride, size_t stripe_stride, hipStream_t stream) {
+    const int T = c.total(), k = c.k();
+    if (!present) return fail(RS_E_INVALID, "present must not be NULL");
+    if (n_stripes == 0 || shard_len == 0) return RS_OK;
+    if (!base) return fail(RS_E_INVALID, "NULL device base");
+    if (n_stripes > size_t(INT32_MAX)) return fail(RS_E_INVALID, "too many stripes");
+    // Distinct presence patterns -> record ids.
+    std::map<std::vector<uint8_t>, int32_t> ids;
+    std::vector<std::vector<uint8_t>> pats;
+    std::vector<int32_t> pid(n_stripes);
+    std::vector<uint8_t> key(T);
+    for (size_t t = 0; t < n_stripes; ++t) {
+        int np = 0;
+        for (int i = 0; i < T; ++i) np += (key[i] = present[t * T + i] ? 1 : 0);
+        if (np < k) return fail(RS_E_NOT_ENOUGH, "Not enough shards present");
+        auto it = ids.find(key);
+        if (it == ids.end()) {
+            it = ids.emplace(key, int32_t(pats.size())).first;
+            pats.push_back(key);
+        }
+        pid[t] = it->second;
+    }
+    std::vector<std::shared_ptr<const Plan>> plans(pats.size());
+    size_t max_missing = 0;
+    for (size_t q = 0; q < pats.size(); ++q) {
+        int rc = c.decode_plan(pats[q].data(), &plans[q]);
+        if (rc) return fail(rc, rc == RS_E_SINGULAR ? "Matrix is singular" : "Not enough shards present");
+        max_missing = std::max(max_missing, plans[q]->out_idx().size());
+    }
+    if (max_missing == 0) return RS_OK;
+    const int ms = std::min<int>(c.m(), rsamd::kMaxOut);
+    const size_t groups = (max_missing + ms - 1) / ms;
+    const rsamd::MaskedRecordLayout L = rsamd::masked_record_layout(k, ms);
+    const size_t npat = pats.size();
+    const size_t ids_off = groups * npat * L.bytes;
+    const size_t bytes = ids_off + n_stripes * sizeof(int32_t);
+
+    ThreadCtx *ctx = nullptr;
+    int rc = thread_ctx(&ctx);
+    if (rc) return rc;
+    if (!ctx->masked_done) RS_HIP(hipEventCreateWithFlags(&ctx->masked_done, hipEventDisableTiming));
+    else RS_HIP(hipEventSynchronize(ctx->masked_done));  // the previous call's kernels are done with the slot
+    if (ctx->masked_host_cap < bytes) {
+        if (ctx->masked_host) RS_HIP(hipHostFree(ctx->masked_host));
+        ctx->masked_host = nullptr;
+        ctx->masked_host_cap = 0;
+        RS_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->masked_host), bytes, hipHostMallocDefault));
+        ctx->masked_host_cap = bytes;
+    }
+    rc = grow(&ctx->masked_dev, &ctx->masked_dev_cap, bytes);
+    if (rc) return rc;
+    uint8_t *img = ctx->masked_host;
+    std::memset(img, 0, ids_off);
+    for (size_t g = 0; g < groups; ++g)
+        for (size_t q = 0; q < npat; ++q) {
+            const Plan &pl = *plans[q];
+            uint8_t *r = img + (g * npat + q) * L.bytes;
+            const int nm = int(pl.out_idx().size());
+            const int32_t nout = std::max(0, std::min<int>(ms, nm - int(g) * ms));
+            std::memcpy(r, &nout, sizeof nout);
+            for (int i = 0; i < k; ++i) {
+                const int32_t v = pl.in_idx()[i];
+                std::memcpy(r + L.in_idx + i * 4, &v, 4);
+            }
+            for (int p = 0; p < nout; ++p) {
+                const int row = int(g) * ms + p;
+                const int32_t v = pl.out_idx()[row];
+                std::memcpy(r + L.out_idx + p * 4, &v, 4);
+                for (int i = 0; i < k; ++i) {
+                    const rsamd::PermTable t = rsamd::perm_table(pl.rows().at(row, i));
+                    std::memcpy(r + L.tabs + (size_t(i) * ms + p) * sizeof t, &t, sizeof t);
+                }
+            }
+        }
+    std::memcpy(img + ids_off, pid.data(), n_stripes * sizeof(int32_t));
+    RS_HIP(hipMemcpyAsync(ctx->masked_dev, img, bytes, hipMemcpyHostToDevice, stream));
+    Geometry geo{base, n_stripes, 0, shard_len, shard_stride, stripe_stride};
+    for (size_t g = 0; g < groups; ++g) {
+        rsamd::MaskedPlan mp;
+        mp.records = ctx->masked_dev + g * npat * L.bytes;
+        mp.rec_stride = L.bytes;
+        mp.plan_ids = reinterpret_cast<const int32_t *>(ctx->masked_dev + ids_off);
+        mp.nin = k;
+        mp.mslots = ms;
+        RS_HIP(rsamd::launch_gf_masked(geo, mp, stream));
+    }
+    RS_HIP(hipEventRecord(ctx->masked_done, stream));
+    return RS_OK;
+}
+
 const Codec *impl(const rs_codec *c) { return c ? c->impl : nullptr; }
 
 }  // namespace
@@ -389,6 +490,10 @@ void rs_thread_release(void) {
         if (c->plan) (void)hipFree(c->plan);
         if (c->flag) (void)hipFree(c->flag);
         if (c->file) (void)hipFree(c->file);
+        if (c->masked_done) (void)hipEventSynchronize(c->masked_done);
+        if (c->masked_dev) (void)hipFree(c->masked_dev);
+        if (c->masked_host) (void)hipHostFree(c->masked_host);
+        if (c->masked_done) (void)hipEventDestroy(c->masked_done);
         delete c;
     }
     t_ctx.clear();
@@ -491,6 +596,14 @@ int rs_decode_batch_dev(const rs_codec *codec, uint8_t *dev_base, const uint8_t 
     for (const DevPlan &p : plans)
         RS_HIP(rsamd::launch_gf(g, p, Mode::Code, nullptr, static_cast<hipStream_t>(stream)));
     return RS_OK;
+}
+
+int rs_decode_batch_masked_dev(const rs_codec *codec, uint8_t *dev_base, const uint8_t *present, size_t n_stripes,
+                               size_t shard_len, size_t shard_stride, size_t stripe_stride, void *stream) {
+    const Codec *c = impl(codec);
+    if (!c) return fail(RS_E_INVALID, "codec is NULL");
+    return decode_masked_dev(*c, dev_base, present, n_stripes, shard_len, shard_stride, stripe_stride,
+                             static_cast<hipStream_t>(stream));
 }
 
 int rs_verify_batch_dev(const rs_codec *codec, const uint8_t *dev_base, size_t n_stripes, size_t shard_len,

@@ -190,6 +190,147 @@ __global__ void __launch_bounds__(kWave) gf_vec_generic_kernel(VecArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Masked vector kernel: the coding plan is chosen PER STRIPE from a table of
+// records (one per distinct presence pattern).  The record index, shard
+// indices, output count and tables are block-uniform scalar loads; stripes
+// whose record has nout == 0 return at once.  Same wave shape as
+// gf_vec_kernel; up to MS outputs per launch.
+// ---------------------------------------------------------------------------
+struct MaskedArgs {
+    uint8_t *base;
+    const uint8_t *records;
+    uint64_t rec_stride;
+    const int32_t *plan_ids;
+    uint64_t stripe_stride;
+    uint64_t shard_stride;
+    uint32_t nvec, chunks, n_items;
+    uint32_t rec_in_idx, rec_out_idx, rec_tabs;  // byte offsets inside a record
+    int nin;                                     // generic kernel only
+};
+
+template <int K, int MS>
+__global__ void __launch_bounds__(kWave) gf_masked_kernel(MaskedArgs a) {
+    const uint32_t item = blockIdx.x;
+    const uint32_t stripe = item / a.chunks;
+    const uint32_t v = (item - stripe * a.chunks) * uint32_t(kWave) + threadIdx.x;
+    const uint8_t *rec = a.records + uint64_t(a.plan_ids[stripe]) * a.rec_stride;
+    const int nout = *reinterpret_cast<const int32_t *>(rec);
+    if (nout == 0 || v >= a.nvec) return;
+    const int32_t *in_idx = reinterpret_cast<const int32_t *>(rec + a.rec_in_idx);
+    const int32_t *out_idx = reinterpret_cast<const int32_t *>(rec + a.rec_out_idx);
+    const uint32_t *tabs = reinterpret_cast<const uint32_t *>(rec + a.rec_tabs);
+    uint8_t *sb = a.base + uint64_t(stripe) * a.stripe_stride + uint64_t(v) * 16;
+    uint64_t out_off[MS];
+#pragma unroll
+    for (int p = 0; p < MS; ++p) out_off[p] = uint64_t(out_idx[p]) * a.shard_stride;
+    u32x4 x[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) x[i] = load_stream(sb + uint64_t(in_idx[i]) * a.shard_stride);
+    u32x4 acc[MS];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        uint32_t T[MS][5];
+#pragma unroll
+        for (int p = 0; p < MS; ++p)
+#pragma unroll
+            for (int j = 0; j < 5; ++j) T[p][j] = tabs[(i * MS + p) * 5 + j];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const Sel s = selectors(x[i][w]);
+#pragma unroll
+            for (int p = 0; p < MS; ++p) {
+                uint32_t t0, t1, t2;
+                terms(T[p], s, t0, t1, t2);
+                acc[p][w] = i == 0 ? xor3(t0, t1, t2) : xor3(acc[p][w], t0, t1) ^ t2;
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int p = 0; p < MS; ++p)
+        if (p < nout) __builtin_nontemporal_store(acc[p], reinterpret_cast<u32x4 *>(sb + out_off[p]));
+}
+
+template <int MS>
+__global__ void __launch_bounds__(kWave) gf_masked_generic_kernel(MaskedArgs a) {
+    const uint32_t item = blockIdx.x;
+    const uint32_t stripe = item / a.chunks;
+    const uint32_t v = (item - stripe * a.chunks) * uint32_t(kWave) + threadIdx.x;
+    const uint8_t *rec = a.records + uint64_t(a.plan_ids[stripe]) * a.rec_stride;
+    const int nout = *reinterpret_cast<const int32_t *>(rec);
+    if (nout == 0 || v >= a.nvec) return;
+    const int32_t *in_idx = reinterpret_cast<const int32_t *>(rec + a.rec_in_idx);
+    const int32_t *out_idx = reinterpret_cast<const int32_t *>(rec + a.rec_out_idx);
+    const uint32_t *tabs = reinterpret_cast<const uint32_t *>(rec + a.rec_tabs);
+    uint8_t *sb = a.base + uint64_t(stripe) * a.stripe_stride + uint64_t(v) * 16;
+    uint64_t out_off[MS];
+#pragma unroll
+    for (int p = 0; p < MS; ++p) out_off[p] = uint64_t(out_idx[p]) * a.shard_stride;
+    u32x4 acc[MS];
+#pragma unroll
+    for (int p = 0; p < MS; ++p) acc[p] = u32x4{0, 0, 0, 0};
+    u32x4 next = load_stream(sb + uint64_t(in_idx[0]) * a.shard_stride);
+    for (int i = 0; i < a.nin; ++i) {
+        const u32x4 x = next;
+        if (i + 1 < a.nin) next = load_stream(sb + uint64_t(in_idx[i + 1]) * a.shard_stride);
+        uint32_t T[MS][5];
+#pragma unroll
+        for (int p = 0; p < MS; ++p)
+#pragma unroll
+            for (int j = 0; j < 5; ++j) T[p][j] = tabs[(i * MS + p) * 5 + j];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const Sel s = selectors(x[w]);
+#pragma unroll
+            for (int p = 0; p < MS; ++p) {
+                uint32_t t0, t1, t2;
+                terms(T[p], s, t0, t1, t2);
+                acc[p][w] = xor3(acc[p][w], t0, t1) ^ t2;
+            }
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < MS; ++p)
+        if (p < nout) __builtin_nontemporal_store(acc[p], reinterpret_cast<u32x4 *>(sb + out_off[p]));
+}
+
+// Masked byte kernel: any alignment, and the <16-byte tails.
+struct MaskedByteArgs {
+    uint8_t *base;
+    const uint8_t *records;
+    uint64_t rec_stride;
+    const int32_t *plan_ids;
+    uint64_t stripe_stride, shard_stride, col0, ncols, total;
+    uint32_t rec_in_idx, rec_out_idx, rec_tabs;
+    int nin, mslots;
+};
+
+__global__ void __launch_bounds__(kThreads) gf_masked_byte_kernel(MaskedByteArgs a) {
+    const uint64_t step = uint64_t(gridDim.x) * kThreads;
+    for (uint64_t idx = uint64_t(blockIdx.x) * kThreads + threadIdx.x; idx < a.total; idx += step) {
+        const uint64_t stripe = idx / a.ncols;
+        const uint64_t col = a.col0 + (idx - stripe * a.ncols);
+        const uint8_t *rec = a.records + uint64_t(a.plan_ids[stripe]) * a.rec_stride;
+        const int nout = *reinterpret_cast<const int32_t *>(rec);
+        if (nout == 0) continue;
+        const int32_t *in_idx = reinterpret_cast<const int32_t *>(rec + a.rec_in_idx);
+        const int32_t *out_idx = reinterpret_cast<const int32_t *>(rec + a.rec_out_idx);
+        const uint32_t *tabs = reinterpret_cast<const uint32_t *>(rec + a.rec_tabs);
+        uint8_t *sb = a.base + stripe * a.stripe_stride + col;
+        uint32_t acc[kMaxOut] = {0, 0, 0, 0};
+        for (int i = 0; i < a.nin; ++i) {
+            const Sel s = selectors(sb[uint64_t(in_idx[i]) * a.shard_stride]);
+            for (int p = 0; p < nout; ++p) {
+                uint32_t t0, t1, t2;
+                terms(tabs + (i * a.mslots + p) * 5, s, t0, t1, t2);
+                acc[p] = xor3(acc[p], t0, t1) ^ t2;
+            }
+        }
+        for (int p = 0; p < nout; ++p) sb[uint64_t(out_idx[p]) * a.shard_stride] = uint8_t(acc[p]);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Byte kernel: any alignment; also the <16-byte tail of aligned shards.
 // One thread per (stripe, column byte).
 // ---------------------------------------------------------------------------
@@ -310,6 +451,82 @@ hipError_t launch_bytes(const Geometry &g, const DevPlan &p, size_t col0, size_t
     return hipGetLastError();
 }
 
+template <int K, int MS>
+hipError_t launch_masked_t(const MaskedArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL((gf_masked_kernel<K, MS>), dim3(a.n_items), dim3(kWave), 0, s, a);
+    return hipGetLastError();
+}
+
+template <int MS>
+hipError_t launch_masked_generic_t(const MaskedArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL((gf_masked_generic_kernel<MS>), dim3(a.n_items), dim3(kWave), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t dispatch_masked(const MaskedArgs &a, int ms, hipStream_t s) {
+#define RSAMD_CASE(K, M) \
+    if (a.nin == K && ms == M) return launch_masked_t<K, M>(a, s);
+    RSAMD_CASE(4, 1) RSAMD_CASE(4, 2) RSAMD_CASE(4, 3) RSAMD_CASE(4, 4)
+    RSAMD_CASE(10, 1) RSAMD_CASE(10, 2) RSAMD_CASE(10, 3) RSAMD_CASE(10, 4)
+#undef RSAMD_CASE
+    switch (ms) {
+    case 1: return launch_masked_generic_t<1>(a, s);
+    case 2: return launch_masked_generic_t<2>(a, s);
+    case 3: return launch_masked_generic_t<3>(a, s);
+    case 4: return launch_masked_generic_t<4>(a, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_masked_bytes(const Geometry &g, const MaskedPlan &p, const MaskedRecordLayout &l, size_t col0,
+                               size_t ncols, hipStream_t s) {
+    MaskedByteArgs a{g.base, p.records, p.rec_stride, p.plan_ids, g.stripe_stride, g.shard_stride, col0, ncols,
+                     uint64_t(g.n_stripes) * ncols, uint32_t(l.in_idx), uint32_t(l.out_idx), uint32_t(l.tabs),
+                     p.nin, p.mslots};
+    if (a.total == 0) return hipSuccess;
+    const unsigned grid = unsigned(std::min<uint64_t>((a.total + kThreads - 1) / kThreads, 65536));
+    hipLaunchKernelGGL(gf_masked_byte_kernel, dim3(grid), dim3(kThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+MaskedRecordLayout masked_record_layout(int nin, int mslots) {
+    MaskedRecordLayout l;
+    l.in_idx = 16;
+    l.out_idx = l.in_idx + size_t(nin) * 4;
+    l.tabs = (l.out_idx + size_t(mslots) * 4 + 15) / 16 * 16;
+    l.bytes = (l.tabs + size_t(nin) * mslots * 20 + 15) / 16 * 16;
+    return l;
+}
+
+hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t s) {
+    if (g.n_stripes == 0 || g.len == 0) return hipSuccess;
+    if (p.mslots < 1 || p.mslots > kMaxOut || p.nin < 1) return hipErrorInvalidValue;
+    const MaskedRecordLayout l = masked_record_layout(p.nin, p.mslots);
+    uint8_t *base = g.base + g.col0;
+    const bool aligned = (reinterpret_cast<uintptr_t>(base) % 16 == 0) && g.shard_stride % 16 == 0 &&
+                         g.stripe_stride % 16 == 0;
+    if (!aligned || g.len / 16 > UINT32_MAX - kWave) return launch_masked_bytes(g, p, l, g.col0, g.len, s);
+    const uint32_t nvec = uint32_t(g.len / 16);
+    if (nvec > 0) {
+        const uint32_t chunks = (nvec + kWave - 1) / kWave;
+        const size_t stripes_per_launch = std::max<size_t>(1, size_t(INT32_MAX) / chunks);
+        for (size_t t0 = 0; t0 < g.n_stripes; t0 += stripes_per_launch) {
+            const size_t nst = std::min(stripes_per_launch, g.n_stripes - t0);
+            MaskedArgs a{base + t0 * g.stripe_stride, p.records, p.rec_stride, p.plan_ids + t0, g.stripe_stride,
+                         g.shard_stride, nvec, chunks, uint32_t(nst * chunks), uint32_t(l.in_idx),
+                         uint32_t(l.out_idx), uint32_t(l.tabs), p.nin};
+            hipError_t e = dispatch_masked(a, p.mslots, s);
+            if (e != hipSuccess) return e;
+        }
+    }
+    const size_t tail = g.len % 16;
+    if (tail) return launch_masked_bytes(g, p, l, g.col0 + size_t(nvec) * 16, tail, s);
+    return hipSuccess;
+}
+
+namespace {
 }  // namespace
 
 hipError_t launch_gf(const Geometry &g, const DevPlan &p, Mode mode, int *mismatch, hipStream_t s) {

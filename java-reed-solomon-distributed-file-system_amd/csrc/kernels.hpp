@@ -40,6 +40,24 @@ enum class Mode { Code, Verify };
 // Returns hipSuccess or the first launch error.
 hipError_t launch_gf(const Geometry &g, const DevPlan &p, Mode mode, int *mismatch, hipStream_t s);
 
+// Per-stripe presence patterns (rs_decode_batch_masked_dev).  records holds one
+// fixed-size record per distinct pattern (masked_record_layout); plan_ids[t]
+// selects stripe t's record.  A record with nout == 0 leaves its stripes alone.
+struct MaskedRecordLayout {
+    size_t in_idx, out_idx, tabs, bytes;  // byte offsets inside a record; nout is an int32 at 0
+};
+MaskedRecordLayout masked_record_layout(int nin, int mslots);
+
+struct MaskedPlan {
+    const uint8_t *records = nullptr;
+    size_t rec_stride = 0;
+    const int32_t *plan_ids = nullptr;
+    int nin = 0;
+    int mslots = 0;  // output slots per record (<= kMaxOut)
+};
+
+hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t s);
+
 hipError_t launch_fill_synthetic(uint8_t *base, int k, size_t n_stripes, size_t shard_len,
                                  size_t shard_stride, size_t stripe_stride, uint64_t seed,
                                  uint64_t stripe0, hipStream_t s);

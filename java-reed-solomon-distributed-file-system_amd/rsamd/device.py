@@ -55,6 +55,16 @@ def decode(codec: ReedSolomon, dev_base: int, present: Sequence, lay: StripeLayo
                                           C.c_void_p(_stream_handle(stream))))
 
 
+def decode_masked(codec: ReedSolomon, dev_base: int, present, lay: StripeLayout, stream=None) -> None:
+    """Per-stripe presence patterns: present is (n_stripes, k+m) of bools/0-1."""
+    p = np.ascontiguousarray(np.asarray(present, dtype=bool).astype(np.uint8))
+    if p.ndim != 2 or p.shape[0] != lay.n_stripes or p.shape[1] != codec.getTotalShardCount():
+        raise ValueError(f"present must be ({lay.n_stripes}, {codec.getTotalShardCount()}), got {p.shape}")
+    check(_lib.load().rs_decode_batch_masked_dev(codec.handle, C.c_void_p(dev_base), p.ctypes.data_as(_lib.u8p),
+                                                 lay.n_stripes, lay.shard_len, lay.shard_stride, lay.stripe_stride,
+                                                 C.c_void_p(_stream_handle(stream))))
+
+
 def verify(codec: ReedSolomon, dev_base: int, lay: StripeLayout, dev_flag: int, stream=None) -> None:
     check(_lib.load().rs_verify_batch_dev(codec.handle, C.c_void_p(dev_base), lay.n_stripes, lay.shard_len,
                                           lay.shard_stride, lay.stripe_stride, C.c_void_p(dev_flag),

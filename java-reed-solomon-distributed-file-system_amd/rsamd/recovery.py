@@ -1,0 +1,72 @@
+"""Chunkserver recovery: the reference's per-chunk-group decode, on the GPU.
+
+ChunkserverDiskRecoveryMachine mirrors
+server/Chunkserver/ChunkserverDiskRecoveryMachine.java:14-57 one call at a
+time (same checks, messages and quirks; decodeMissing runs on the GPU).  The
+master drives it once per 6 x 1000-byte chunk group (MasterImpl.java:794-839);
+recover_chunk_groups_dev does all of a server's chunk groups in one batched
+launch, each group with its own presence pattern (rs_decode_batch_masked_dev).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .codec import IllegalArgumentException, RS_E_INVALID, RS_E_NOT_ENOUGH
+from .device import StripeLayout, decode_masked
+from .layout import DATA_SHARD_COUNT, PARITY_SHARD_COUNT, TOTAL_SHARD_COUNT, _codec
+
+
+class ChunkserverDiskRecoveryMachine:
+    """ChunkserverDiskRecoveryMachine.java:14-57."""
+
+    def __init__(self):
+        self._data = [None] * TOTAL_SHARD_COUNT
+        self._present = [False] * TOTAL_SHARD_COUNT
+        self._present_cnt = 0
+        self._byte_cnt = 0
+        self._rs = _codec(DATA_SHARD_COUNT, PARITY_SHARD_COUNT)
+
+    def addChunkserverDisksData(self, serverIdx: int, chunkserverDiskData) -> None:
+        """:22-32 (adding an index twice counts twice, as in the Java)."""
+        if serverIdx < 0 or serverIdx >= TOTAL_SHARD_COUNT:
+            raise IllegalArgumentException(RS_E_INVALID, "Given server index does not exist")
+        data = np.frombuffer(bytes(chunkserverDiskData), dtype=np.uint8)
+        if self._byte_cnt != 0 and len(data) != self._byte_cnt:
+            raise IllegalArgumentException(RS_E_INVALID, "Number of bytes in different chunkserver disks mismatch")
+        self._byte_cnt = len(data)
+        self._data[serverIdx] = data.copy()
+        self._present[serverIdx] = True
+        self._present_cnt += 1
+
+    def recoverChunkserverDiskData(self) -> None:
+        """:34-48."""
+        if self._present_cnt < DATA_SHARD_COUNT:
+            raise IllegalArgumentException(RS_E_NOT_ENOUGH, "There is not enough disk data to perform the recovery")
+        if self._byte_cnt == 0:
+            raise IllegalArgumentException(RS_E_INVALID, "There is no data to recover")
+        if self._present_cnt == TOTAL_SHARD_COUNT:
+            return
+        for i in range(TOTAL_SHARD_COUNT):
+            if not self._present[i]:
+                self._data[i] = np.zeros(self._byte_cnt, dtype=np.uint8)
+        self._rs.decodeMissing(self._data, self._present, 0, self._byte_cnt)
+        for i in range(TOTAL_SHARD_COUNT):
+            self._present[i] = True
+
+    def retrieveRecoveredDiskData(self, serverIdx: int) -> bytes:
+        """:50-57."""
+        if serverIdx < 0 or serverIdx >= TOTAL_SHARD_COUNT:
+            raise IllegalArgumentException(RS_E_INVALID, "Given server index does not exist")
+        if not self._present[serverIdx]:
+            self.recoverChunkserverDiskData()
+        return self._data[serverIdx].tobytes()
+
+
+def recover_chunk_groups_dev(dev_base: int, present, lay: StripeLayout, stream=None,
+                             data_shards: int = DATA_SHARD_COUNT, parity_shards: int = PARITY_SHARD_COUNT) -> None:
+    """Reconstruct every absent chunk of every chunk group in one batched call.
+
+    The groups are stripes of a [group][server][chunk] device layout (chunk =
+    ConfigVariables.BLOCK_SIZE bytes in the DFS); present is (groups, k+m).
+    """
+    decode_masked(_codec(data_shards, parity_shards), dev_base, present, lay, stream)

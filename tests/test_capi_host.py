@@ -169,3 +169,30 @@ def test_file_decode_contract_without_device(native):
     sh = [np.zeros(1000, np.uint8) for _ in range(6)]
     with pytest.raises(rsamd.IllegalArgumentException, match="exceeds"):
         ReedSolomonDecoder(sh, [1] * 6, 1000, 4001)
+
+
+def test_recovery_machine_contract_without_device(native):
+    """ChunkserverDiskRecoveryMachine.java:22-57 checks, messages and quirks."""
+    import rsamd
+    from rsamd.recovery import ChunkserverDiskRecoveryMachine
+    m = ChunkserverDiskRecoveryMachine()
+    with pytest.raises(rsamd.IllegalArgumentException, match="^Given server index does not exist$"):
+        m.addChunkserverDisksData(6, b"x")
+    m.addChunkserverDisksData(0, b"abc")
+    with pytest.raises(rsamd.IllegalArgumentException, match="^Number of bytes in different chunkserver disks mismatch$"):
+        m.addChunkserverDisksData(1, b"abcd")
+    with pytest.raises(rsamd.IllegalArgumentException, match="^There is not enough disk data to perform the recovery$"):
+        m.recoverChunkserverDiskData()
+    with pytest.raises(rsamd.IllegalArgumentException, match="^Given server index does not exist$"):
+        m.retrieveRecoveredDiskData(-1)
+    assert m.retrieveRecoveredDiskData(0) == b"abc"
+    e = ChunkserverDiskRecoveryMachine()
+    for i in range(4):
+        e.addChunkserverDisksData(i, b"")
+    with pytest.raises(rsamd.IllegalArgumentException, match="^There is no data to recover$"):
+        e.recoverChunkserverDiskData()
+    # the Java counts a re-added index twice: 6 adds of 5 servers look "complete" and return early
+    q = ChunkserverDiskRecoveryMachine()
+    for i in (0, 1, 2, 3, 4, 4):
+        q.addChunkserverDisksData(i, b"zz")
+    q.recoverChunkserverDiskData()

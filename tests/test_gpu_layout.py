@@ -68,18 +68,19 @@ def _dev(arr_or_n, pad=0):
     return t
 
 
-@pytest.mark.parametrize("k,m,block,n,file_off,stride_pad", [
-    (4, 2, 1000, 1_234_567, 0, 0),     # fused kernels (the DFS shape)
-    (4, 2, 1000, 4000 * 37, 0, 256),   # fused, exact multiple, padded stride
-    (4, 2, 1000, 9_999, 8, 0),         # fused, 8-aligned file offset
-    (4, 2, 1000, 77_777, 3, 0),        # misaligned file -> generic split/merge
-    (4, 2, 512, 100_000, 0, 0),        # another block size, fused
-    (4, 2, 7, 5_000, 0, 0),            # block % 8 != 0 -> byte split/merge
-    (5, 3, 1000, 200_001, 0, 0),       # k != 4 -> generic
-    (10, 4, 1000, 500_000, 0, 0),      # config-4 shape
-    (4, 6, 1000, 60_000, 0, 0),        # m > 4: fused first parity group + stripe kernel
+@pytest.mark.parametrize("k,m,block,n,file_off,stride_mode", [
+    (4, 2, 1000, 1_234_567, 0, "aligned"),   # fused kernels (the DFS shape)
+    (4, 2, 1000, 1_234_567, 0, "exact"),     # stride = S = 8 mod 16 -> generic split/merge + stripe kernels
+    (4, 2, 1000, 4000 * 37, 0, "aligned"),   # fused, exact multiple of k*block
+    (4, 2, 1000, 9_999, 8, "aligned"),       # fused, 8-aligned file offset
+    (4, 2, 1000, 77_777, 3, "aligned"),      # misaligned file -> generic split/merge
+    (4, 2, 512, 100_000, 0, "exact"),        # another block size (S % 16 == 0: fused)
+    (4, 2, 7, 5_000, 0, "aligned"),          # block % 8 != 0 -> byte split/merge
+    (5, 3, 1000, 200_001, 0, "aligned"),     # k != 4 -> generic
+    (10, 4, 1000, 500_000, 0, "aligned"),    # config-4 shape
+    (4, 6, 1000, 60_000, 0, "aligned"),      # m > 4: fused first parity group + stripe kernel
 ])
-def test_device_layout_paths(gpu, oracle_lib, k, m, block, n, file_off, stride_pad):
+def test_device_layout_paths(gpu, oracle_lib, k, m, block, n, file_off, stride_mode):
     import torch
     import rsamd
     from rsamd.layout import decode_file_dev, encode_file_dev, file_layout
@@ -91,7 +92,7 @@ def test_device_layout_paths(gpu, oracle_lib, k, m, block, n, file_off, stride_p
     fdev = _dev(data, pad=file_off + 16)
     if file_off:
         fdev[file_off: file_off + n] = fdev[:n].clone()
-    stride = S + stride_pad
+    stride = S if stride_mode == "exact" else (S + 255) // 256 * 256
     sdev = _dev((k + m) * stride)
     encode_file_dev(rs, fdev.data_ptr() + file_off, n, sdev.data_ptr(), stride, block, torch.cuda.current_stream())
     got = sdev.cpu().numpy().reshape(k + m, stride)[:, :S]

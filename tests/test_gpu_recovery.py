@@ -1,0 +1,142 @@
+"""GPU tests of batched recovery with a presence pattern per stripe
+(ChunkserverDiskRecoveryMachine.java:14-57 driven per
+chunk group by MasterImpl.java:794-839).  Bit-exact against the golden
+fixtures and the oracle."""
+import itertools
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _golden(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name), allow_pickle=False)["shards"]
+
+
+def _run_masked(rs, batch, present, stride=None):
+    import torch
+    from rsamd import device
+    from rsamd.device import StripeLayout
+    B, T, S = batch.shape
+    stride = stride or S
+    host = np.zeros((B, T, stride), np.uint8)
+    host[:, :, :S] = batch
+    for t in range(B):
+        for j in range(T):
+            if not present[t][j]:
+                host[t, j, :S] = 0x3C  # garbage the decode must overwrite
+    dev = torch.from_numpy(host.reshape(-1).copy()).to("cuda:0")
+    device.decode_masked(rs, dev.data_ptr(), present, StripeLayout(B, S, stride, stride * T),
+                         torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    return dev.cpu().numpy().reshape(B, T, stride)[:, :, :S]
+
+
+def test_masked_4_2_every_pattern_mixed(gpu, golden_dir):
+    import rsamd
+    g = _golden(golden_dir, "rs_4_2_s4096_b8.npz")
+    pats = [tuple(i not in miss for i in range(6))
+            for e in range(3) for miss in itertools.combinations(range(6), e)]  # 22 patterns
+    batch = np.concatenate([g] * 3)[: len(pats)]
+    rs = rsamd.ReedSolomon.create(4, 2)
+    out = _run_masked(rs, batch, pats)
+    assert np.array_equal(out, batch)
+
+
+def test_masked_10_4_and_generic_17_3(gpu, golden_dir):
+    import rsamd
+    g = _golden(golden_dir, "rs_10_4_s1024_b4.npz")
+    pats = [[i not in miss for i in range(14)] for miss in [(0, 1, 2, 3), (), (13,), (2, 7, 11)]]
+    assert np.array_equal(_run_masked(rsamd.ReedSolomon.create(10, 4), g, pats), g)
+    g = _golden(golden_dir, "rs_17_3_s512_b2.npz")
+    pats = [[i not in miss for i in range(20)] for miss in [(0, 5, 19), (17, 18)]]
+    assert np.array_equal(_run_masked(rsamd.ReedSolomon.create(17, 3), g, pats), g)
+
+
+def test_masked_more_than_four_outputs(gpu, oracle_lib):
+    """m = 6: patterns with 5-6 erasures need two output groups."""
+    import rsamd
+    k, m, S, B = 4, 6, 256, 6
+    rng = np.random.default_rng(6)
+    batch = np.zeros((B, k + m, S), np.uint8)
+    c = oracle_lib.Codec(k, m)
+    for t in range(B):
+        batch[t, :k] = rng.integers(0, 256, (k, S), dtype=np.uint8)
+        c.encode_parity([batch[t, i] for i in range(k + m)], 0, S)
+    misses = [(0, 1, 2, 3, 4, 5), (1,), (4, 5, 6, 7, 8), (), (0, 9), (3, 4, 5, 6, 7, 8)]
+    pats = [[i not in mi for i in range(k + m)] for mi in misses]
+    assert np.array_equal(_run_masked(rsamd.ReedSolomon.create(k, m), batch, pats), batch)
+
+
+@pytest.mark.parametrize("S,stride", [(1000, 1000), (1000, 1008), (4096, 4099)])
+def test_masked_chunk_groups_like_the_master(gpu, oracle_lib, S, stride):
+    """The DFS recovers 6 x 1000-byte chunk groups (S % 16 != 0: tail kernel);
+    odd strides take the byte kernel."""
+    import rsamd
+    rng = np.random.default_rng(S + stride)
+    B = 500
+    batch = np.zeros((B, 6, S), np.uint8)
+    batch[:, :4] = rng.integers(0, 256, (B, 4, S), dtype=np.uint8)
+    c = oracle_lib.Codec(4, 2)
+    for t in range(B):
+        c.encode_parity([batch[t, i] for i in range(6)], 0, S)
+    allp = [tuple(i not in miss for i in range(6)) for e in range(3) for miss in itertools.combinations(range(6), e)]
+    pats = [allp[int(x)] for x in rng.integers(0, len(allp), B)]
+    assert np.array_equal(_run_masked(rsamd.ReedSolomon.create(4, 2), batch, pats, stride), batch)
+
+
+def test_masked_not_enough_fails_before_launch(gpu):
+    import torch
+    import rsamd
+    from rsamd import device
+    from rsamd.device import StripeLayout
+    rs = rsamd.ReedSolomon.create(4, 2)
+    buf = torch.full((2 * 6 * 64,), 7, dtype=torch.uint8, device="cuda:0")
+    with pytest.raises(rsamd.IllegalArgumentException, match="^Not enough shards present$"):
+        device.decode_masked(rs, buf.data_ptr(), [[1] * 6, [1, 1, 1, 0, 0, 0]], StripeLayout(2, 64, 64, 384))
+    assert int((buf != 7).sum().item()) == 0
+
+
+def test_masked_full_size_small_objects(gpu):
+    """BASELINE configs[4] shape: 1 M stripes of 4 KiB, a random pattern per stripe."""
+    import torch
+    import rsamd
+    from rsamd import device
+    from rsamd.device import StripeLayout
+    rs = rsamd.ReedSolomon.create(4, 2)
+    B, S = 1 << 20, 4096
+    lay = StripeLayout.packed(B, 6, S)
+    buf = torch.empty(lay.nbytes, dtype=torch.uint8, device="cuda:0")
+    st = torch.cuda.current_stream()
+    device.fill_synthetic(buf.data_ptr(), 4, lay, 0x5EED, 0, st)
+    device.encode(rs, buf.data_ptr(), lay, st)
+    ref = buf.clone()
+    rng = np.random.default_rng(1)
+    allp = np.array([[i not in miss for i in range(6)] for e in range(3)
+                     for miss in itertools.combinations(range(6), e)], dtype=bool)
+    pats = allp[rng.integers(0, len(allp), B)]
+    v = buf.view(B, 6, S)
+    mask = torch.from_numpy(~pats).to("cuda:0")
+    v.masked_fill_(mask[:, :, None], 0)
+    device.decode_masked(rs, buf.data_ptr(), pats, lay, st)
+    assert torch.equal(buf, ref)
+    del buf, ref, v
+    torch.cuda.empty_cache()
+
+
+def test_recovery_machine_mirror(gpu, oracle_lib):
+    from rsamd.recovery import ChunkserverDiskRecoveryMachine
+    rng = np.random.default_rng(9)
+    S = 1000
+    shards = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(4)] + [np.zeros(S, np.uint8)] * 2
+    shards = [s.copy() for s in shards]
+    oracle_lib.Codec(4, 2).encode_parity(shards, 0, S)
+    for miss in [(0,), (0, 5), (2, 3), (4,)]:
+        mach = ChunkserverDiskRecoveryMachine()
+        for i in range(6):
+            if i not in miss:
+                mach.addChunkserverDisksData(i, shards[i].tobytes())
+        for j in miss:
+            assert mach.retrieveRecoveredDiskData(j) == shards[j].tobytes()
