@@ -112,6 +112,7 @@ def main():
         del buf
         torch.cuda.empty_cache()
         extra.update(other_configs(torch, rsamd, rdev, dev, stream))
+        extra.update(layout_legs(torch, rsamd, dev, stream))
         if world == 1:
             cpu = cpu_baseline(k, m, S, args.cpu_seconds)
             extra.update(host_inclusive(rsamd, k, m))
@@ -204,8 +205,50 @@ def other_configs(torch, rsamd, rdev, dev, stream):
         flag = torch.zeros(1, dtype=torch.int32, device=dev)
         rdev.verify(rs, buf.data_ptr(), lay, flag.data_ptr(), stream)
         out[name + "_verified"] = int(flag.item()) == 0
+        if name.startswith("cfg4"):
+            # row f2: a random presence pattern per stripe (<= 2 erasures), one launch
+            import itertools
+            import numpy as np
+            pats = np.array([[i not in miss for i in range(k + m)] for e in range(3)
+                             for miss in itertools.combinations(range(k + m), e)], dtype=bool)
+            present = pats[np.random.default_rng(0).integers(0, len(pats), B)]
+            t = timed(torch, stream, lambda: rdev.decode_masked(rs, buf.data_ptr(), present, lay, stream), 5)
+            miss_frac = float((~present).sum()) / B
+            out[name + "_decode_masked_GiBps"] = round(k * S * B / t / 2**30, 2)
+            out[name + "_decode_masked_hbm_frac"] = round((k + miss_frac) * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
+            rdev.verify(rs, buf.data_ptr(), lay, flag.data_ptr(), stream)
+            out[name + "_decode_masked_verified"] = int(flag.item()) == 0
         del buf
         torch.cuda.empty_cache()
+    return out
+
+
+def layout_legs(torch, rsamd, dev, stream):
+    """Row f1: the client layout fused into the kernels -- a 4 GiB file encoded
+    straight into 4+2 shards, and decoded back with 2 erasures."""
+    from rsamd.layout import decode_file_dev, encode_file_dev, file_layout
+    rs = rsamd.ReedSolomon.create(4, 2)
+    n = 4 << 30
+    _, S = file_layout(rs, n)
+    stride = (S + 255) // 256 * 256
+    f = torch.empty(n, dtype=torch.uint8, device=dev)
+    from rsamd import device as rdev
+    from rsamd.device import StripeLayout
+    rdev.fill_synthetic(f.data_ptr(), 1, StripeLayout(1, n, n, n), SEED, 0, stream)
+    sh = torch.empty(6 * stride, dtype=torch.uint8, device=dev)
+    out = {}
+    t = timed(torch, stream, lambda: encode_file_dev(rs, f.data_ptr(), n, sh.data_ptr(), stride, stream=stream), 5)
+    out["file_encode_4GiB_GiBps"] = round(n / t / 2**30, 2)
+    out["file_encode_hbm_frac"] = round((n + 6 * S) / t / 1e9 / HBM_PEAK_GBPS, 4)
+    g = torch.empty(n, dtype=torch.uint8, device=dev)
+    present = [False, True, True, True, True, False]
+    t = timed(torch, stream, lambda: decode_file_dev(rs, sh.data_ptr(), S, stride, present, g.data_ptr(), n,
+                                                     stream=stream), 5)
+    out["file_decode_0_5_4GiB_GiBps"] = round(n / t / 2**30, 2)
+    out["file_decode_hbm_frac"] = round((4 * S + n) / t / 1e9 / HBM_PEAK_GBPS, 4)
+    out["file_round_trip_ok"] = bool(torch.equal(f, g))
+    del f, g, sh
+    torch.cuda.empty_cache()
     return out
 
 

@@ -343,21 +343,45 @@ int decode_masked_dev(const Codec &c, uint8_t *base, const uint8_t *present, siz
     if (n_stripes == 0 || shard_len == 0) return RS_OK;
     if (!base) return fail(RS_E_INVALID, "NULL device base");
     if (n_stripes > size_t(INT32_MAX)) return fail(RS_E_INVALID, "too many stripes");
-    // Distinct presence patterns -> record ids.
-    std::map<std::vector<uint8_t>, int32_t> ids;
+    // Distinct presence patterns -> record ids.  Patterns of <= 20 shards are
+    // keyed by their bitmask in a direct table (one pass, no allocation per
+    // stripe); wider codes use an ordered map of the flag vector.
     std::vector<std::vector<uint8_t>> pats;
     std::vector<int32_t> pid(n_stripes);
     std::vector<uint8_t> key(T);
-    for (size_t t = 0; t < n_stripes; ++t) {
-        int np = 0;
-        for (int i = 0; i < T; ++i) np += (key[i] = present[t * T + i] ? 1 : 0);
-        if (np < k) return fail(RS_E_NOT_ENOUGH, "Not enough shards present");
-        auto it = ids.find(key);
-        if (it == ids.end()) {
-            it = ids.emplace(key, int32_t(pats.size())).first;
-            pats.push_back(key);
+    auto add_pattern = [&]() {
+        pats.push_back(key);
+        return int32_t(pats.size() - 1);
+    };
+    if (T <= 20) {
+        std::vector<int32_t> table(size_t(1) << T, -1);
+        for (size_t t = 0; t < n_stripes; ++t) {
+            const uint8_t *row = present + t * T;
+            uint32_t bits = 0;
+            int np = 0;
+            for (int i = 0; i < T; ++i)
+                if (row[i]) {
+                    bits |= 1u << i;
+                    ++np;
+                }
+            if (np < k) return fail(RS_E_NOT_ENOUGH, "Not enough shards present");
+            int32_t &slot = table[bits];
+            if (slot < 0) {
+                for (int i = 0; i < T; ++i) key[i] = (bits >> i) & 1;
+                slot = add_pattern();
+            }
+            pid[t] = slot;
         }
-        pid[t] = it->second;
+    } else {
+        std::map<std::vector<uint8_t>, int32_t> ids;
+        for (size_t t = 0; t < n_stripes; ++t) {
+            int np = 0;
+            for (int i = 0; i < T; ++i) np += (key[i] = present[t * T + i] ? 1 : 0);
+            if (np < k) return fail(RS_E_NOT_ENOUGH, "Not enough shards present");
+            auto it = ids.find(key);
+            if (it == ids.end()) it = ids.emplace(key, add_pattern()).first;
+            pid[t] = it->second;
+        }
     }
     std::vector<std::shared_ptr<const Plan>> plans(pats.size());
     size_t max_missing = 0;

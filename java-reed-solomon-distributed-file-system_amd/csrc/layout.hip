@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 
 #include "gf_device.hpp"
 
@@ -48,21 +49,50 @@ struct FileArgs {
     const int32_t *dsrc;    // decode: data shard i -> survivor position (>= 0) or -(row + 1)
 };
 
+// How the fused kernels touch the FILE side (the shard side is always 16-byte
+// non-temporal): IO_NT8 = 8-byte non-temporal, IO_PLAIN8 = 8-byte plain (the
+// two halves of a 16-byte column vector meet in L2), IO_PAIR16 = one 16-byte
+// access when both halves fall in the same block row (8-byte aligned), else
+// two 8-byte accesses.  Chosen at launch (RSAMD_LAYOUT_IO); default IO_PLAIN8,
+// measured best (profiles/r1/layout_io_sweep.txt: file encode 0.78 / decode 0.50
+// of HBM peak vs 0.68 / 0.38 non-temporal and 0.77 / 0.47 paired).
+enum FileIo { IO_NT8 = 0, IO_PLAIN8 = 1, IO_PAIR16 = 2 };
+
 // File byte runs of 8: [f, f+8) clipped to len, zero beyond (the padding).
+template <int IO>
 __device__ __forceinline__ u32x2 load8(const uint8_t *file, uint64_t len, uint64_t f) {
-    if (f + 8 <= len) return __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(file + f));
+    if (f + 8 <= len)
+        return IO == IO_NT8 ? __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(file + f))
+                            : *reinterpret_cast<const u32x2 *>(file + f);
     uint64_t v = 0;
     for (uint64_t b = f; b < len && b < f + 8; ++b) v |= uint64_t(file[b]) << (8 * (b - f));
     return u32x2{uint32_t(v), uint32_t(v >> 32)};
 }
 
+template <int IO>
 __device__ __forceinline__ void store8(uint8_t *file, uint64_t len, uint64_t f, u32x2 v) {
     if (f + 8 <= len) {
-        __builtin_nontemporal_store(v, reinterpret_cast<u32x2 *>(file + f));
+        if (IO == IO_NT8)
+            __builtin_nontemporal_store(v, reinterpret_cast<u32x2 *>(file + f));
+        else
+            *reinterpret_cast<u32x2 *>(file + f) = v;
         return;
     }
     const uint64_t x = uint64_t(v[0]) | uint64_t(v[1]) << 32;
     for (uint64_t b = f; b < len && b < f + 8; ++b) file[b] = uint8_t(x >> (8 * (b - f)));
+}
+
+// 16 file bytes [f, f+16) when both halves are contiguous (same block row),
+// f 8-byte aligned: one dwordx4 access (the hardware splits it if needed).
+struct alignas(8) u32x4_a8 {
+    uint32_t v[4];
+};
+__device__ __forceinline__ u32x4 load16_a8(const uint8_t *p) {
+    const u32x4_a8 t = *reinterpret_cast<const u32x4_a8 *>(p);
+    return u32x4{t.v[0], t.v[1], t.v[2], t.v[3]};
+}
+__device__ __forceinline__ void store16_a8(uint8_t *p, const u32x4 &v) {
+    *reinterpret_cast<u32x4_a8 *>(p) = u32x4_a8{{v[0], v[1], v[2], v[3]}};
 }
 
 // Row r and in-row offset w of shard column cc = c0 + d, given the
@@ -77,7 +107,7 @@ __device__ __forceinline__ void row_of(uint64_t r0, uint32_t w0, uint32_t d, uin
     }
 }
 
-template <int K, int M>
+template <int K, int M, int IO>
 __global__ void __launch_bounds__(kWave) file_encode_kernel(FileArgs a) {
     const uint32_t v = blockIdx.x * kWave + threadIdx.x;
     const uint64_t c0 = uint64_t(blockIdx.x) * kWave * 16;  // block-uniform first column
@@ -91,12 +121,26 @@ __global__ void __launch_bounds__(kWave) file_encode_kernel(FileArgs a) {
     row_of(r0, w0, threadIdx.x * 16, a.block, rr[0], ww[0]);
     row_of(r0, w0, threadIdx.x * 16 + 8, a.block, rr[1], ww[1]);
 
+    // Tables first: read before any store, so they stay scalar loads.
+    uint32_t T[M > 0 ? M : 1][K][5];
+#pragma unroll
+    for (int p = 0; p < M; ++p)
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+#pragma unroll
+            for (int j = 0; j < 5; ++j) T[p][i][j] = a.tabs[(i * M + p) * 5 + j];
     u32x4 x[K];
+    const bool pair = IO == IO_PAIR16 && hi && rr[0] == rr[1];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-        const u32x2 lo = load8(a.file, a.file_len, (rr[0] * K + i) * a.block + ww[0]);
-        const u32x2 up = hi ? load8(a.file, a.file_len, (rr[1] * K + i) * a.block + ww[1]) : u32x2{0, 0};
-        x[i] = u32x4{lo[0], lo[1], up[0], up[1]};
+        const uint64_t f0 = (rr[0] * K + i) * a.block + ww[0];
+        if (pair && f0 + 16 <= a.file_len) {
+            x[i] = load16_a8(a.file + f0);
+        } else {
+            const u32x2 lo = load8<IO>(a.file, a.file_len, f0);
+            const u32x2 up = hi ? load8<IO>(a.file, a.file_len, (rr[1] * K + i) * a.block + ww[1]) : u32x2{0, 0};
+            x[i] = u32x4{lo[0], lo[1], up[0], up[1]};
+        }
     }
     uint8_t *col = a.shards + c;
 #pragma unroll
@@ -115,14 +159,7 @@ __global__ void __launch_bounds__(kWave) file_encode_kernel(FileArgs a) {
 #pragma unroll
         for (int i = 0; i < K; ++i) s[i] = selectors(x[i][w]);
 #pragma unroll
-        for (int p = 0; p < M; ++p) {
-            uint32_t T[K][5];
-#pragma unroll
-            for (int i = 0; i < K; ++i)
-#pragma unroll
-                for (int j = 0; j < 5; ++j) T[i][j] = a.tabs[(i * M + p) * 5 + j];
-            acc[p][w] = dot_dword<K>(T, s);
-        }
+        for (int p = 0; p < M; ++p) acc[p][w] = dot_dword<K>(T[p], s);
     }
 #pragma unroll
     for (int p = 0; p < M; ++p) {
@@ -143,7 +180,7 @@ __device__ __forceinline__ u32x4 pick(const u32x4 (&v)[N], int idx) {
     return r;
 }
 
-template <int K, int E>
+template <int K, int E, int IO>
 __global__ void __launch_bounds__(kWave) file_decode_kernel(FileArgs a) {
     const uint32_t v = blockIdx.x * kWave + threadIdx.x;
     const uint64_t c0 = uint64_t(blockIdx.x) * kWave * 16;
@@ -192,8 +229,13 @@ __global__ void __launch_bounds__(kWave) file_decode_kernel(FileArgs a) {
     for (int i = 0; i < K; ++i) {
         constexpr int EY = E > 0 ? E : 1;
         const u32x4 d = dsrc[i] >= 0 ? pick<K>(x, dsrc[i]) : pick<EY>(y, -dsrc[i] - 1);
-        store8(a.file_out, a.file_len, (rr[0] * K + i) * a.block + ww[0], u32x2{d[0], d[1]});
-        if (hi) store8(a.file_out, a.file_len, (rr[1] * K + i) * a.block + ww[1], u32x2{d[2], d[3]});
+        const uint64_t f0 = (rr[0] * K + i) * a.block + ww[0];
+        if (IO == IO_PAIR16 && hi && rr[0] == rr[1] && f0 + 16 <= a.file_len) {
+            store16_a8(a.file_out + f0, d);
+        } else {
+            store8<IO>(a.file_out, a.file_len, f0, u32x2{d[0], d[1]});
+            if (hi) store8<IO>(a.file_out, a.file_len, (rr[1] * K + i) * a.block + ww[1], u32x2{d[2], d[3]});
+        }
     }
 }
 
@@ -227,13 +269,13 @@ __global__ void __launch_bounds__(kThreads) split_merge_kernel(CopyArgs a) {
         const uint64_t n = a.S - c < W ? a.S - c : W;  // bytes of this word inside the shard
         if (SPLIT) {
             if (W == 8 && n == 8) {
-                *reinterpret_cast<u32x2 *>(sh) = load8(a.file, a.file_len, f);
+                *reinterpret_cast<u32x2 *>(sh) = load8<IO_PLAIN8>(a.file, a.file_len, f);
             } else {
                 for (uint64_t b = 0; b < n; ++b) sh[b] = f + b < a.file_len ? a.file[f + b] : 0;
             }
         } else {
             if (W == 8 && n == 8) {
-                store8(a.file_out, a.file_len, f, *reinterpret_cast<const u32x2 *>(sh));
+                store8<IO_PLAIN8>(a.file_out, a.file_len, f, *reinterpret_cast<const u32x2 *>(sh));
             } else {
                 for (uint64_t b = 0; b < n; ++b)
                     if (f + b < a.file_len) a.file_out[f + b] = sh[b];
@@ -242,15 +284,33 @@ __global__ void __launch_bounds__(kThreads) split_merge_kernel(CopyArgs a) {
     }
 }
 
+int file_io_mode() {
+    static const int v = [] {
+        const char *e = std::getenv("RSAMD_LAYOUT_IO");
+        return e ? std::atoi(e) : int(IO_PLAIN8);
+    }();
+    return v;
+}
+
 template <int K, int M>
 hipError_t launch_enc_t(const FileArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL((file_encode_kernel<K, M>), dim3((a.nvec + kWave - 1) / kWave), dim3(kWave), 0, s, a);
+    const dim3 grid((a.nvec + kWave - 1) / kWave);
+    switch (file_io_mode()) {
+    case IO_NT8: hipLaunchKernelGGL((file_encode_kernel<K, M, IO_NT8>), grid, dim3(kWave), 0, s, a); break;
+    case IO_PLAIN8: hipLaunchKernelGGL((file_encode_kernel<K, M, IO_PLAIN8>), grid, dim3(kWave), 0, s, a); break;
+    default: hipLaunchKernelGGL((file_encode_kernel<K, M, IO_PAIR16>), grid, dim3(kWave), 0, s, a); break;
+    }
     return hipGetLastError();
 }
 
 template <int K, int E>
 hipError_t launch_dec_t(const FileArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL((file_decode_kernel<K, E>), dim3((a.nvec + kWave - 1) / kWave), dim3(kWave), 0, s, a);
+    const dim3 grid((a.nvec + kWave - 1) / kWave);
+    switch (file_io_mode()) {
+    case IO_NT8: hipLaunchKernelGGL((file_decode_kernel<K, E, IO_NT8>), grid, dim3(kWave), 0, s, a); break;
+    case IO_PLAIN8: hipLaunchKernelGGL((file_decode_kernel<K, E, IO_PLAIN8>), grid, dim3(kWave), 0, s, a); break;
+    default: hipLaunchKernelGGL((file_decode_kernel<K, E, IO_PAIR16>), grid, dim3(kWave), 0, s, a); break;
+    }
     return hipGetLastError();
 }
 
