@@ -189,10 +189,11 @@ def other_configs(torch, rsamd, rdev, dev, stream):
     8 GPUs) and configs[4] (4+2 x 4 KiB x 1 M stripes), encode and decode."""
     from rsamd.device import StripeLayout
     out = {}
-    for name, k, m, S, B, miss in [("cfg3_10p4_4MiB_x128", 10, 4, 4 << 20, 128, (0, 1, 2, 3)),
-                                   ("cfg4_4p2_4KiB_x1M", 4, 2, 4096, 1 << 20, (0, 1))]:
+    for name, k, m, S, B, miss, pad in [("cfg3_10p4_4MiB_x128", 10, 4, 4 << 20, 128, (0, 1, 2, 3), 0),
+                                        ("cfg3_10p4_4MiB_x128_pad4K", 10, 4, 4 << 20, 128, (0, 1, 2, 3), 4096),
+                                        ("cfg4_4p2_4KiB_x1M", 4, 2, 4096, 1 << 20, (0, 1), 0)]:
         rs = rsamd.ReedSolomon.create(k, m)
-        lay = StripeLayout.packed(B, k + m, S)
+        lay = StripeLayout.packed(B, k + m, S, pad=pad)
         buf = torch.empty(lay.nbytes, dtype=torch.uint8, device=dev)
         rdev.fill_synthetic(buf.data_ptr(), k, lay, SEED, 0, stream)
         t = timed(torch, stream, lambda: rdev.encode(rs, buf.data_ptr(), lay, stream), 10)

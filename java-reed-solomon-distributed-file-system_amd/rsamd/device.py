@@ -26,8 +26,11 @@ class StripeLayout:
     stripe_stride: int
 
     @staticmethod
-    def packed(n_stripes: int, total_shards: int, shard_len: int, align: int = 256) -> "StripeLayout":
-        stride = (shard_len + align - 1) // align * align
+    def packed(n_stripes: int, total_shards: int, shard_len: int, align: int = 256, pad: int = 0) -> "StripeLayout":
+        """Shards back to back at `align`-rounded strides, plus `pad` bytes
+        between shards (a 4 KiB pad spreads the 14 streams of 10+4 x 4 MiB
+        stripes over more HBM channels)."""
+        stride = (shard_len + align - 1) // align * align + pad
         return StripeLayout(n_stripes, shard_len, stride, stride * total_shards)
 
     @property

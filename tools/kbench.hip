@@ -186,6 +186,8 @@ __global__ void fill_kernel(uint64_t *p, uint64_t n, uint64_t seed) {
 }
 
 struct Ctx {
+    size_t pad = 0;  // extra bytes between shards (shard_stride = S + pad)
+    size_t cap = 0;  // bytes allocated at buf: every shape is checked against it on the host
     uint8_t *buf;
     uint32_t *tabs;
     size_t S, B, total;
@@ -197,7 +199,9 @@ std::vector<uint8_t> sample_parity(Ctx &c, int K, int M) {
     std::vector<uint8_t> out;
     for (size_t t : {size_t(0), size_t(1), c.B - 2, c.B - 1}) {
         std::vector<uint8_t> h(M * c.S);
-        CHECK(hipMemcpy(h.data(), c.buf + t * c.total * c.S + K * c.S, M * c.S, hipMemcpyDeviceToHost));
+        const size_t sh = c.S + c.pad;
+        for (int p = 0; p < M; ++p)
+            CHECK(hipMemcpy(h.data() + p * c.S, c.buf + t * c.total * sh + (K + p) * sh, c.S, hipMemcpyDeviceToHost));
         out.insert(out.end(), h.begin(), h.end());
     }
     return out;
@@ -208,7 +212,8 @@ void run_enc(Ctx &c, const char *name, unsigned grid_cap, int reps) {
     const uint32_t nvec = uint32_t(c.S / 16);
     const uint32_t per = BLK * U;
     const uint32_t chunks = (nvec + per - 1) / per;
-    Args a{c.buf, c.tabs, uint64_t(c.total * c.S), uint64_t(c.S), nvec, chunks, uint32_t(c.B * chunks)};
+    const uint64_t sh = c.S + c.pad;
+    Args a{c.buf, c.tabs, uint64_t(c.total * sh), sh, nvec, chunks, uint32_t(c.B * chunks)};
     unsigned grid = a.n_items;
     if (grid_cap && grid > grid_cap) grid = grid_cap;
     CHECK(hipMemset(c.buf + K * c.S, 0, M * c.S));  // poison stripe 0 parity so a no-op variant shows
@@ -233,7 +238,7 @@ void run_enc(Ctx &c, const char *name, unsigned grid_cap, int reps) {
         if (c.ref_parity.empty()) c.ref_parity = p;
         ok = (p == c.ref_parity) ? "ok" : "MISMATCH";
     }
-    std::printf("%-44s grid=%8u  %8.3f ms  %7.1f GB/s  %5.1f%% of 8 TB/s  %s\n", name, grid, ms, bytes / ms / 1e6,
+    std::printf("%-44s pad=%6zu  %8.3f ms  %7.1f GB/s  %5.1f%% of 8 TB/s  %s\n", name, c.pad, ms, bytes / ms / 1e6,
                 bytes / ms / 1e6 / 80.0, ok);
     std::fflush(stdout);
 }
@@ -243,7 +248,8 @@ template <int K, int M, int BLK, bool NTL, bool NTS>
 void run_staged(Ctx &c, const char *name, int reps) {
     const uint32_t nvec = uint32_t(c.S / 16);
     const uint32_t chunks = (nvec + BLK - 1) / BLK;
-    Args a{c.buf, c.tabs, uint64_t(c.total * c.S), uint64_t(c.S), nvec, chunks, uint32_t(c.B * chunks)};
+    const uint64_t sh = c.S + c.pad;
+    Args a{c.buf, c.tabs, uint64_t(c.total * sh), sh, nvec, chunks, uint32_t(c.B * chunks)};
     const unsigned grid = a.n_items;
     CHECK(hipMemset(c.buf + K * c.S, 0, M * c.S));
     hipLaunchKernelGGL((enc_staged_kernel<K, M, BLK, NTL, NTS>), dim3(grid), dim3(BLK), 0, 0, a);
@@ -263,7 +269,74 @@ void run_staged(Ctx &c, const char *name, int reps) {
     const double bytes = double(K + M) * c.S * c.B;
     auto p = sample_parity(c, K, M);
     if (c.ref_parity.empty()) c.ref_parity = p;
-    std::printf("%-44s grid=%8u  %8.3f ms  %7.1f GB/s  %5.1f%% of 8 TB/s  %s\n", name, grid, ms, bytes / ms / 1e6,
+    std::printf("%-44s pad=%6zu  %8.3f ms  %7.1f GB/s  %5.1f%% of 8 TB/s  %s\n", name, c.pad, ms, bytes / ms / 1e6,
+                bytes / ms / 1e6 / 80.0, p == c.ref_parity ? "ok" : "MISMATCH");
+    std::fflush(stdout);
+}
+
+// Same shape, loads/stores through buffer intrinsics with explicit cache-policy
+// bits (gfx950 CPol: sc0 = 1, nt = 2, sc1 = 16).
+template <int K, int M, int LAUX, int SAUX>
+__global__ void __launch_bounds__(64) enc_buf_kernel(Args a) {
+    uint32_t T[M][K][5];
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int p = 0; p < M; ++p)
+#pragma unroll
+            for (int j = 0; j < 5; ++j) T[p][i][j] = a.tabs[(i * M + p) * 5 + j];
+    const uint32_t item = blockIdx.x;
+    const uint32_t stripe = item / a.chunks;
+    const uint32_t v = (item - stripe * a.chunks) * 64u + threadIdx.x;
+    if (v >= a.nvec) return;
+    uint8_t *sb = a.base + uint64_t(stripe) * a.stripe_stride;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(sb, 0, 0x7fffffff, 0x00020000);
+    u32x4 x[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const uint32_t off = uint32_t(i * a.shard_stride + uint64_t(v) * 16);
+        x[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, LAUX));
+    }
+    u32x4 acc[M];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        Sel s[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) s[i] = selectors(x[i][w]);
+#pragma unroll
+        for (int p = 0; p < M; ++p) acc[p][w] = dot_dword<K>(T[p], s);
+    }
+#pragma unroll
+    for (int p = 0; p < M; ++p) {
+        const uint32_t off = uint32_t((K + p) * a.shard_stride + uint64_t(v) * 16);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, acc[p]), rs, off, 0, SAUX);
+    }
+}
+
+template <int K, int M, int LAUX, int SAUX>
+void run_buf(Ctx &c, const char *name, int reps) {
+    const uint32_t nvec = uint32_t(c.S / 16);
+    const uint32_t chunks = (nvec + 63) / 64;
+    const uint64_t sh = c.S + c.pad;
+    Args a{c.buf, c.tabs, uint64_t(c.total * sh), sh, nvec, chunks, uint32_t(c.B * chunks)};
+    hipLaunchKernelGGL((enc_buf_kernel<K, M, LAUX, SAUX>), dim3(a.n_items), dim3(64), 0, 0, a);
+    CHECK(hipDeviceSynchronize());
+    std::vector<float> ts;
+    for (int r = 0; r < reps; ++r) {
+        CHECK(hipEventRecord(c.e0, 0));
+        hipLaunchKernelGGL((enc_buf_kernel<K, M, LAUX, SAUX>), dim3(a.n_items), dim3(64), 0, 0, a);
+        CHECK(hipEventRecord(c.e1, 0));
+        CHECK(hipEventSynchronize(c.e1));
+        float ms = 0;
+        CHECK(hipEventElapsedTime(&ms, c.e0, c.e1));
+        ts.push_back(ms);
+    }
+    std::sort(ts.begin(), ts.end());
+    const double ms = ts[ts.size() / 2];
+    const double bytes = double(K + M) * c.S * c.B;
+    auto p = sample_parity(c, K, M);
+    if (c.ref_parity.empty()) c.ref_parity = p;
+    std::printf("%-44s pad=%6zu  %8.3f ms  %7.1f GB/s  %5.1f%% of 8 TB/s  %s\n", name, c.pad, ms, bytes / ms / 1e6,
                 bytes / ms / 1e6 / 80.0, p == c.ref_parity ? "ok" : "MISMATCH");
     std::fflush(stdout);
 }
@@ -290,12 +363,18 @@ void run_copy(Ctx &c, const char *name, unsigned grid, int reps) {
     std::fflush(stdout);
 }
 
-void setup_shape(Ctx &c, int K, int M, size_t S, size_t B) {
+bool setup_shape(Ctx &c, int K, int M, size_t S, size_t B) {
+    const size_t need = B * size_t(K + M) * (S + c.pad);
+    if (need > c.cap || size_t(K) * M * 20 > 64 * 1024) {  // never launch past the allocation
+        std::printf("--- skip %d+%d S=%zu B=%zu pad=%zu: needs %zu bytes > %zu allocated\n", K, M, S, B, c.pad, need,
+                    c.cap);
+        return false;
+    }
     c.S = S;
     c.B = B;
     c.total = K + M;
     c.ref_parity.clear();
-    const size_t bytes = c.B * c.total * c.S;
+    const size_t bytes = c.B * c.total * (c.S + c.pad);
     hipLaunchKernelGGL(fill_kernel, dim3(65536), dim3(256), 0, 0, reinterpret_cast<uint64_t *>(c.buf), bytes / 8,
                        0x5EEDull + K);
     GfMatrix g = build_generator(K, K + M);
@@ -308,40 +387,34 @@ void setup_shape(Ctx &c, int K, int M, size_t S, size_t B) {
     CHECK(hipMemcpy(c.tabs, tabs.data(), tabs.size() * 4, hipMemcpyHostToDevice));
     CHECK(hipDeviceSynchronize());
     std::printf("--- %d+%d x %zu KiB x %zu stripes (%.1f GiB)\n", K, M, S >> 10, B, bytes / 1073741824.0);
+    return true;
 }
 
 int main(int argc, char **argv) {
     const int reps = argc > 1 ? std::atoi(argv[1]) : 7;
     Ctx c;
-    CHECK(hipMalloc(&c.buf, size_t(24) << 30));
+    c.cap = size_t(24) << 30;
+    CHECK(hipMalloc(&c.buf, c.cap));
     CHECK(hipMalloc(&c.tabs, 64 * 1024));
     CHECK(hipEventCreate(&c.e0));
     CHECK(hipEventCreate(&c.e1));
 
-    setup_shape(c, 4, 2, size_t(1) << 20, 4096);
-    run_enc<4, 2, 1, 64, true, true, GF>(c, "gf U1 B64 ntl+nts", 0, reps);
-    run_enc<4, 2, 1, 256, true, true, GF>(c, "gf U1 B256 ntl+nts", 0, reps);
-    run_enc<4, 2, 2, 64, true, true, GF>(c, "gf U2 B64 ntl+nts", 0, reps);
-    run_enc<4, 2, 1, 64, false, false, GF>(c, "gf U1 B64", 0, reps);
-    run_enc<4, 2, 1, 64, false, true, GF>(c, "gf U1 B64 nts", 0, reps);
-    run_enc<4, 2, 1, 128, true, true, GF>(c, "gf U1 B128 ntl+nts", 0, reps);
-    run_staged<4, 2, 64, true, true>(c, "staged 4+2 B64 ntl+nts", reps);
-    run_enc<4, 2, 1, 64, true, true, XOR>(c, "xor U1 B64 ntl+nts (memory ref)", 0, reps);
-    for (unsigned g : {524288u, 2097152u}) run_copy<64, true, true>(c, "copy B64 nt/nt", g, reps);
-
-    setup_shape(c, 4, 1, size_t(1) << 20, 4096);  // decode e=1 shape
-    run_enc<4, 1, 1, 64, true, true, GF>(c, "gf 4->1 U1 B64 ntl+nts", 0, reps);
-    run_enc<4, 1, 1, 256, true, true, GF>(c, "gf 4->1 U1 B256 ntl+nts", 0, reps);
-
-    setup_shape(c, 10, 4, size_t(4) << 20, 128);  // config-4 per-GPU share
-    run_staged<10, 4, 64, true, true>(c, "staged 10+4 B64 ntl+nts", reps);
-    run_staged<10, 4, 128, true, true>(c, "staged 10+4 B128 ntl+nts", reps);
-    run_staged<10, 4, 256, true, true>(c, "staged 10+4 B256 ntl+nts", reps);
-    run_enc<10, 4, 1, 64, true, true, GF>(c, "gf 10+4 U1 B64 ntl+nts", 0, reps);
-    run_enc<10, 4, 1, 64, true, true, XOR>(c, "xor 10+4 U1 B64 ntl+nts (memory ref)", 0, reps);
-
-    setup_shape(c, 4, 2, 4096, 1 << 20);  // config-5 small objects
-    run_enc<4, 2, 1, 64, true, true, GF>(c, "gf 4K U1 B64 ntl+nts", 0, reps);
-    run_enc<4, 2, 1, 256, true, true, GF>(c, "gf 4K U1 B256 ntl+nts", 0, reps);
+    for (size_t pad : {size_t(0), size_t(512), size_t(1024), size_t(2048), size_t(4096), size_t(8192),
+                       size_t(12288), size_t(16384), size_t(65536)}) {
+        c.pad = pad;
+        if (!setup_shape(c, 10, 4, size_t(4) << 20, 120)) continue;
+        run_enc<10, 4, 1, 64, true, true, GF>(c, "gf 10+4 staged? (enc_kernel) B64", 0, reps);
+        run_staged<10, 4, 64, true, true>(c, "staged 10+4 B64", reps);
+    }
+    for (size_t pad : {size_t(0), size_t(256), size_t(512), size_t(1024), size_t(2048), size_t(4096)}) {
+        c.pad = pad;
+        if (!setup_shape(c, 4, 2, 4096, 900000)) continue;
+        run_enc<4, 2, 1, 64, true, true, GF>(c, "gf 4+2 4KiB B64", 0, reps);
+    }
+    for (size_t pad : {size_t(0), size_t(2048), size_t(8192), size_t(16384)}) {
+        c.pad = pad;
+        if (!setup_shape(c, 4, 2, size_t(1) << 20, 3900)) continue;
+        run_enc<4, 2, 1, 64, true, true, GF>(c, "gf 4+2 1MiB B64", 0, reps);
+    }
     return 0;
 }
