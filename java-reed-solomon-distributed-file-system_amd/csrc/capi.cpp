@@ -58,7 +58,9 @@ int hip_fail(hipError_t e, const char *where) {
 // ---------------------------------------------------------------------------
 struct ThreadCtx {
     hipStream_t stream = nullptr;
-    uint8_t *stage = nullptr;  // nslots x slot_stride device bytes
+    hipStream_t stream2 = nullptr;  // second ping-pong stream of run_host
+    hipEvent_t ready = nullptr;     // orders stream2 behind stream's verify-flag memset
+    uint8_t *stage = nullptr;       // 2 x nslots x slot_stride device bytes (ping-pong halves)
     size_t stage_cap = 0;
     uint8_t *plan = nullptr;   // per-call plan images (rs_code_some_shards)
     size_t plan_cap = 0;
@@ -90,6 +92,8 @@ int thread_ctx(ThreadCtx **out) {
     if (it == t_ctx.end()) {
         auto *c = new ThreadCtx;
         hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ready, hipEventDisableTiming);
         if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&c->flag), 256);
         if (e != hipSuccess) {
             delete c;
@@ -111,9 +115,10 @@ int grow(uint8_t **buf, size_t *cap, size_t want) {
     return RS_OK;
 }
 
-// Bytes per shard staged per round trip.  Bounds device staging to
-// nslots * kChunk and keeps each H2D/D2H large.
-constexpr size_t kChunk = size_t(64) << 20;
+// Bytes per shard staged per round trip.  Chunks alternate between two
+// streams with their own staging halves, so chunk j's D2H overlaps chunk
+// j+1's H2D (PCIe is full duplex) and the kernels hide under both.
+constexpr size_t kChunk = size_t(32) << 20;
 
 size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -130,26 +135,40 @@ int run_host(const std::vector<DevPlan> &plans, int nslots, const std::vector<in
     if (rc) return rc;
     const size_t chunk = std::min(count, kChunk);
     const size_t slot_stride = round_up(std::max<size_t>(chunk, 1), 256);
-    rc = grow(&ctx->stage, &ctx->stage_cap, slot_stride * size_t(nslots));
+    const size_t half = slot_stride * size_t(nslots);
+    const int nbuf = count > chunk ? 2 : 1;
+    rc = grow(&ctx->stage, &ctx->stage_cap, half * size_t(nbuf));
     if (rc) return rc;
-    if (mode == Mode::Verify) RS_HIP(hipMemsetAsync(ctx->flag, 0, sizeof(int), ctx->stream));
-    for (size_t done = 0; done < count; done += chunk) {
+    hipStream_t streams[2] = {ctx->stream, ctx->stream2};
+    if (mode == Mode::Verify) {
+        RS_HIP(hipMemsetAsync(ctx->flag, 0, sizeof(int), ctx->stream));
+        RS_HIP(hipEventRecord(ctx->ready, ctx->stream));
+        RS_HIP(hipStreamWaitEvent(ctx->stream2, ctx->ready, 0));
+    }
+    size_t j = 0;
+    for (size_t done = 0; done < count; done += chunk, ++j) {
         const size_t n = std::min(chunk, count - done);
+        hipStream_t st = streams[j % nbuf];
+        uint8_t *stage = ctx->stage + (j % nbuf) * half;
         for (int s : in_slots)
-            RS_HIP(hipMemcpyAsync(ctx->stage + size_t(s) * slot_stride, host[s] + offset + done, n,
-                                  hipMemcpyHostToDevice, ctx->stream));
+            RS_HIP(hipMemcpyAsync(stage + size_t(s) * slot_stride, host[s] + offset + done, n, hipMemcpyHostToDevice,
+                                  st));
         Geometry g;
-        g.base = ctx->stage;
+        g.base = stage;
         g.n_stripes = 1;
         g.col0 = 0;
         g.len = n;
         g.shard_stride = slot_stride;
-        g.stripe_stride = slot_stride * size_t(nslots);
-        for (const DevPlan &p : plans) RS_HIP(rsamd::launch_gf(g, p, mode, ctx->flag, ctx->stream));
+        g.stripe_stride = half;
+        for (const DevPlan &p : plans) RS_HIP(rsamd::launch_gf(g, p, mode, ctx->flag, st));
         if (mode == Mode::Code)
             for (int s : out_slots)
-                RS_HIP(hipMemcpyAsync(host[s] + offset + done, ctx->stage + size_t(s) * slot_stride, n,
-                                      hipMemcpyDeviceToHost, ctx->stream));
+                RS_HIP(hipMemcpyAsync(host[s] + offset + done, stage + size_t(s) * slot_stride, n,
+                                      hipMemcpyDeviceToHost, st));
+    }
+    if (nbuf == 2) {  // join: stream waits for everything stream2 issued
+        RS_HIP(hipEventRecord(ctx->ready, ctx->stream2));
+        RS_HIP(hipStreamWaitEvent(ctx->stream, ctx->ready, 0));
     }
     if (mode == Mode::Verify) {
         int h = 0;
@@ -510,6 +529,8 @@ void rs_thread_release(void) {
         ThreadCtx *c = kv.second;
         (void)hipSetDevice(kv.first);
         if (c->stream) (void)hipStreamDestroy(c->stream);
+        if (c->stream2) (void)hipStreamDestroy(c->stream2);
+        if (c->ready) (void)hipEventDestroy(c->ready);
         if (c->stage) (void)hipFree(c->stage);
         if (c->plan) (void)hipFree(c->plan);
         if (c->flag) (void)hipFree(c->flag);

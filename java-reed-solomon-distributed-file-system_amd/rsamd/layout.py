@@ -44,6 +44,14 @@ def file_layout(codec: ReedSolomon, file_len: int, block: int = BLOCK_SIZE):
     return p.value, s.value
 
 
+def file_encode_into(codec: ReedSolomon, file_data: np.ndarray, shards_out: Sequence, block: int = BLOCK_SIZE) -> None:
+    """rs_file_encode into caller-provided shard buffers (no allocation)."""
+    src = file_data if len(file_data) else np.zeros(1, np.uint8)
+    b = _Buffers(shards_out)
+    check(_lib.load().rs_file_encode(codec.handle, src.ctypes.data_as(_lib.u8p), len(file_data), block, b.ptrs,
+                                     len(shards_out), b.lens))
+
+
 class ReedSolomonEncoder:
     """client/ReedSolomonEncoder.java (the in-memory constructor, :27-30)."""
 
