@@ -171,13 +171,18 @@ __global__ void __launch_bounds__(kWave) file_encode_kernel(FileArgs a) {
     }
 }
 
-template <int N>
-__device__ __forceinline__ u32x4 pick(const u32x4 (&v)[N], int idx) {
-    u32x4 r = v[0];
+// Data shard held by register vector j of a decode (j < K: survivor j, else
+// rebuilt vector j - K), or -1: the inverse of the uniform dsrc map by scalar
+// selects.  Kernels scatter each vector to its data shard instead of
+// gathering x[dsrc[i]]: a run-time index into a register array (even as a
+// select chain, which the compiler folds back into one) puts it in scratch.
+template <int K>
+__device__ __forceinline__ int data_row(const int (&dsrc)[K], int j) {
+    int row = -1;
 #pragma unroll
-    for (int j = 1; j < N; ++j)
-        if (idx == j) r = v[j];
-    return r;
+    for (int i = 0; i < K; ++i)
+        if (dsrc[i] == (j < K ? j : K - 1 - j)) row = i;
+    return row;
 }
 
 template <int K, int E, int IO>
@@ -226,15 +231,159 @@ __global__ void __launch_bounds__(kWave) file_decode_kernel(FileArgs a) {
     row_of(r0, w0, threadIdx.x * 16, a.block, rr[0], ww[0]);
     row_of(r0, w0, threadIdx.x * 16 + 8, a.block, rr[1], ww[1]);
 #pragma unroll
-    for (int i = 0; i < K; ++i) {
-        constexpr int EY = E > 0 ? E : 1;
-        const u32x4 d = dsrc[i] >= 0 ? pick<K>(x, dsrc[i]) : pick<EY>(y, -dsrc[i] - 1);
+    for (int j = 0; j < K + E; ++j) {
+        const int i = data_row<K>(dsrc, j);
+        if (i < 0) continue;
+        const u32x4 d = j < K ? x[j] : y[j < K ? 0 : j - K];
         const uint64_t f0 = (rr[0] * K + i) * a.block + ww[0];
         if (IO == IO_PAIR16 && hi && rr[0] == rr[1] && f0 + 16 <= a.file_len) {
             store16_a8(a.file_out + f0, d);
         } else {
             store8<IO>(a.file_out, a.file_len, f0, u32x2{d[0], d[1]});
             if (hi) store8<IO>(a.file_out, a.file_len, (rr[1] * K + i) * a.block + ww[1], u32x2{d[2], d[3]});
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Tiled decode-to-file.  A 256-thread workgroup owns R whole block rows
+// (R * block columns of every shard; R even so every offset stays 16-byte
+// aligned).  Phase 1: each thread loads the K survivors' 16-byte column
+// vectors, rebuilds the E missing data shards in registers and parks the K
+// data vectors in an LDS tile [data shard][R * block].  Phase 2: the tile's
+// file bytes are ONE contiguous run [r0*K*block, (r0+R)*K*block) -- written
+// as aligned 16-byte stores, each assembled from two 8-byte LDS reads (a
+// 16-byte chunk may straddle two blocks when block % 16 == 8).  This replaces
+// the per-lane 8-byte file stores of file_decode_kernel (0.49 of HBM peak).
+// ---------------------------------------------------------------------------
+constexpr int kTileThreads = 256;
+constexpr int kTileSlots = 2;  // 16-byte column vectors per thread and shard in phase 1
+
+struct TileArgs {
+    uint8_t *file_out;
+    uint64_t file_size;
+    const uint8_t *shards;
+    uint64_t shard_stride;
+    uint64_t n_rows;       // S / block
+    uint32_t block;
+    uint32_t rows;         // R rows per tile (even)
+    uint32_t inv_block;    // floor(2^32 / block) + 1: t / block for t < 2^16
+    uint32_t inv_kblock;   // same for K * block
+    const uint32_t *tabs;  // [K][E][5]
+    const int32_t *in_idx;
+    const int32_t *dsrc;
+};
+
+__device__ __forceinline__ uint32_t div_small(uint32_t t, uint32_t inv) {
+    return uint32_t((uint64_t(t) * inv) >> 32);
+}
+
+// One 16-byte column vector of each survivor (8 bytes at the ragged end).
+template <int K>
+__device__ __forceinline__ void tile_load(u32x4 (&x)[K], const uint8_t *shards, const uint64_t (&in_off)[K],
+                                          uint32_t c, uint32_t span) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const uint8_t *src = shards + in_off[j] + c;
+        if (c + 16 <= span) {
+            x[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src));
+        } else if (c < span) {
+            const u32x2 h = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(src));
+            x[j] = u32x4{h[0], h[1], 0, 0};
+        }
+    }
+}
+
+// Rebuild the E missing data vectors from x and park all K data vectors of
+// column c in the LDS tile [data shard][pitch].
+template <int K, int E>
+__device__ __forceinline__ void tile_park(const u32x4 (&x)[K], const uint32_t (&T)[E > 0 ? E : 1][K][5],
+                                          const int (&dsrc)[K], uint8_t *tile, uint32_t pitch, uint32_t c,
+                                          uint32_t span) {
+    if (c >= span) return;
+    constexpr int EY = E > 0 ? E : 1;
+    u32x4 y[EY];
+    if (E > 0) {
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            Sel sl[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) sl[j] = selectors(x[j][w]);
+#pragma unroll
+            for (int e = 0; e < E; ++e) y[e][w] = dot_dword<K>(T[e], sl);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < K + E; ++j) {
+        const int row = data_row<K>(dsrc, j);
+        if (row < 0) continue;
+        const u32x4 d = j < K ? x[j] : y[j < K ? 0 : j - K];
+        uint8_t *dst = tile + row * pitch + c;
+        if (c + 16 <= span)
+            *reinterpret_cast<u32x4 *>(dst) = d;
+        else
+            *reinterpret_cast<u32x2 *>(dst) = u32x2{d[0], d[1]};
+    }
+}
+
+template <int K, int E>
+__global__ void __launch_bounds__(kTileThreads) file_decode_tiled_kernel(TileArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
+    const uint64_t r0 = uint64_t(blockIdx.x) * a.rows;
+    const uint32_t rows = uint32_t(min(uint64_t(a.rows), a.n_rows - r0));
+    const uint32_t span = rows * a.block;      // columns of this tile (a multiple of 16 unless last)
+    const uint32_t pitch = a.rows * a.block;   // LDS bytes per data shard
+    const uint64_t col0 = r0 * a.block;
+    int dsrc[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) dsrc[i] = a.dsrc[i];
+    uint32_t T[E > 0 ? E : 1][K][5];
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+#pragma unroll
+            for (int q = 0; q < 5; ++q) T[e][j][q] = a.tabs[(j * E + e) * 5 + q];
+    uint64_t in_off[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) in_off[j] = uint64_t(a.in_idx[j]) * a.shard_stride + col0;
+
+    // Phase 1: survivors -> data vectors -> LDS.  span % 8 == 0 (block % 8 == 0)
+    // and span <= 2 * 256 * 16: both slots' loads are issued before any
+    // compute, then each slot is folded and parked.  One named register array
+    // per slot: an x[slot][shard] array indexed through the slot loop stays
+    // an alloca and spills the vectors to scratch (2x the HBM traffic).
+    const uint32_t c0 = threadIdx.x * 16, c1 = c0 + kTileThreads * 16;
+    u32x4 x0[K], x1[K];
+    tile_load<K>(x0, a.shards, in_off, c0, span);
+    tile_load<K>(x1, a.shards, in_off, c1, span);
+    tile_park<K, E>(x0, T, dsrc, tile, pitch, c0, span);
+    tile_park<K, E>(x1, T, dsrc, tile, pitch, c1, span);
+    __syncthreads();
+
+    // Phase 2: the tile's contiguous file run, 16-byte aligned chunks.
+    const uint32_t kblock = uint32_t(K) * a.block;
+    const uint64_t f0 = r0 * kblock;
+    const uint32_t run = rows * kblock;
+    for (uint32_t t = threadIdx.x * 16; t < run; t += kTileThreads * 16) {
+        const uint64_t f = f0 + t;
+        if (f >= a.file_size) break;
+        u32x2 half[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t u = t + 8 * h;               // byte of the run
+            const uint32_t row = div_small(u, a.inv_kblock);
+            const uint32_t rem = u - row * kblock;
+            const uint32_t i = div_small(rem, a.inv_block);
+            const uint32_t w = rem - i * a.block;
+            half[h] = *reinterpret_cast<const u32x2 *>(tile + i * pitch + row * a.block + w);
+        }
+        const u32x4 v{half[0][0], half[0][1], half[1][0], half[1][1]};
+        if (f + 16 <= a.file_size) {
+            __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(a.file_out + f));
+        } else {
+            for (uint32_t b = 0; b < 16 && f + b < a.file_size; ++b)
+                a.file_out[f + b] = uint8_t(v[b / 4] >> (8 * (b % 4)));
         }
     }
 }
@@ -355,8 +504,45 @@ hipError_t launch_file_encode_fused(const FileGeom &g, const DevPlan *parity0, h
     return hipErrorInvalidValue;
 }
 
+namespace {
+
+template <int K, int E>
+hipError_t launch_tiled_t(const TileArgs &a, uint64_t tiles, hipStream_t s) {
+    const size_t lds = size_t(K) * a.rows * a.block;
+    hipLaunchKernelGGL((file_decode_tiled_kernel<K, E>), dim3(unsigned(tiles)), dim3(kTileThreads), lds, s,
+                       a);
+    return hipGetLastError();
+}
+
+// A tile spans R * block <= kTileSlots * 256 * 16 columns (R even, >= 2), so
+// LDS per workgroup is <= K * 8 KiB = 32 KiB at K = 4.
+uint32_t tile_rows(const FileGeom &g) {
+    if (g.block >= (1u << 15)) return 0;
+    uint64_t R = uint64_t(kTileSlots) * kTileThreads * 16 / g.block;
+    if (R % 2) --R;
+    return R >= 2 ? uint32_t(R) : 0;
+}
+
+}  // namespace
+
 hipError_t launch_file_decode_fused(const FileGeom &g, const FileDecodePlan &p, hipStream_t s) {
     if (g.S == 0 || g.file_len == 0) return hipSuccess;
+    const uint32_t R = tile_rows(g);
+    const char *mode = std::getenv("RSAMD_FILE_DECODE");
+    if (R && !(mode && mode[0] == '0')) {  // RSAMD_FILE_DECODE=0 selects the untiled kernel (A/B only)
+        TileArgs a{g.file_out, g.file_len, g.shards, g.shard_stride, g.S / g.block, uint32_t(g.block), R,
+                   uint32_t((uint64_t(1) << 32) / g.block + 1), uint32_t((uint64_t(1) << 32) / (uint64_t(g.k) * g.block) + 1),
+                   p.tabs, p.in_idx, p.dsrc};
+        const uint64_t tiles = (a.n_rows + R - 1) / R;
+        switch (p.n_missing_data) {
+        case 0: return launch_tiled_t<4, 0>(a, tiles, s);
+        case 1: return launch_tiled_t<4, 1>(a, tiles, s);
+        case 2: return launch_tiled_t<4, 2>(a, tiles, s);
+        case 3: return launch_tiled_t<4, 3>(a, tiles, s);
+        case 4: return launch_tiled_t<4, 4>(a, tiles, s);
+        }
+        return hipErrorInvalidValue;
+    }
     FileArgs a{nullptr, g.file_out, g.file_len, g.shards, g.shard_stride, g.S, uint32_t(g.block),
                uint32_t((g.S + 15) / 16), p.tabs, p.in_idx, p.dsrc};
     switch (p.n_missing_data) {

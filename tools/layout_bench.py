@@ -35,22 +35,30 @@ def main():
     out = {"io": os.environ.get("RSAMD_LAYOUT_IO", "default")}
     rs = rsamd.ReedSolomon.create(4, 2)
     n = 4 << 30
-    _, S = file_layout(rs, n)
-    stride = (S + 255) // 256 * 256
+    blk = int(os.environ.get("RSAMD_BENCH_BLOCK", "1000"))
+    out["block"] = blk
+    n = n // (4 * blk) * (4 * blk)
+    _, S = file_layout(rs, n, blk)
+    pad = int(os.environ.get("RSAMD_BENCH_PAD", "0"))
+    out["pad"] = pad
+    stride = (S + 255) // 256 * 256 + pad
     f = torch.empty(n, dtype=torch.uint8, device="cuda:0")
     rdev.fill_synthetic(f.data_ptr(), 1, StripeLayout(1, n, n, n), 0x5EED, 0, st)
     sh = torch.empty(6 * stride, dtype=torch.uint8, device="cuda:0")
-    t = timed(torch, st, lambda: encode_file_dev(rs, f.data_ptr(), n, sh.data_ptr(), stride, stream=st))
+    t = timed(torch, st, lambda: encode_file_dev(rs, f.data_ptr(), n, sh.data_ptr(), stride, blk, stream=st))
     out["file_encode_hbm_frac"] = round((n + 6 * S) / t / 8e12, 4)
     g = torch.empty(n, dtype=torch.uint8, device="cuda:0")
     for present in ([1] * 6, [0, 1, 1, 1, 1, 0], [0, 0, 1, 1, 1, 1]):
         t = timed(torch, st, lambda: decode_file_dev(rs, sh.data_ptr(), S, stride, present, g.data_ptr(), n,
-                                                     stream=st))
+                                                     blk, stream=st))
         key = "file_decode_" + "".join(map(str, present))
         out[key + "_hbm_frac"] = round((4 * S + n) / t / 8e12, 4)
         out[key + "_ok"] = bool(torch.equal(f, g))
     del f, g, sh
     torch.cuda.empty_cache()
+    if os.environ.get("RSAMD_BENCH_SKIP_MASKED"):
+        print(json.dumps(out), flush=True)
+        return
     B, S = 1 << 20, 4096
     lay = StripeLayout.packed(B, 6, S)
     buf = torch.empty(lay.nbytes, dtype=torch.uint8, device="cuda:0")
