@@ -155,11 +155,28 @@ RS_API int rs_decode_batch_dev(const rs_codec *codec, uint8_t *dev_base, const u
  * flags.  One launch per group of <= 4 outputs; each stripe reads its own
  * first-k-present survivors and writes its own absent shards.  Every stripe
  * needs >= k present shards (else RS_E_NOT_ENOUGH before any launch).
- * Asynchronous on stream; the call's small plan tables live in a per-thread
- * staging slot that the next masked call on the same thread waits for. */
+ * Asynchronous on stream.  For k+m <= 20 (and at most 65536 decodable
+ * patterns) the flags become per-stripe bitmasks looked up in the codec's
+ * pattern table (see below); wider codes get per-call records.  The per-call
+ * bytes live in one of two per-thread staging slots used in turn: a call
+ * waits only for the kernels of the masked call two before it. */
 RS_API int rs_decode_batch_masked_dev(const rs_codec *codec, uint8_t *dev_base, const uint8_t *present,
                                       size_t n_stripes, size_t shard_len, size_t shard_stride,
                                       size_t stripe_stride, void *stream);
+
+/* The same with the presence patterns already in HBM: dev_present_bits[t]
+ * has bit i set when shard i of stripe t is present (no host work per call,
+ * graph-capturable).  The codec's pattern table -- a record for every
+ * bitmask with >= k bits set and a 2^(k+m) id table -- is built and uploaded
+ * on the first call per device (blocking); RS_E_INVALID when k+m > 20 or the
+ * code has more than 65536 decodable patterns.  Stripes with fewer than k
+ * present shards (or bits >= 2^(k+m)) are left untouched and, when
+ * dev_bad_count is not NULL, counted into that device int32 (atomic adds;
+ * the caller zeroes it).  A stripe with every shard present is untouched. */
+RS_API int rs_decode_batch_masked_bits_dev(const rs_codec *codec, uint8_t *dev_base,
+                                           const uint32_t *dev_present_bits, size_t n_stripes,
+                                           size_t shard_len, size_t shard_stride, size_t stripe_stride,
+                                           int32_t *dev_bad_count, void *stream);
 
 /* Verify parity of every stripe: dev_mismatch (a device int) is OR-ed with 1
  * when any parity byte differs.  The caller zeroes it first. */

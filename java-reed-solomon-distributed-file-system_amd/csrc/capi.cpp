@@ -13,6 +13,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rs_amd.h"
@@ -56,6 +57,18 @@ int hip_fail(hipError_t e, const char *where) {
 // ---------------------------------------------------------------------------
 // Per-(thread, device) staging context for the host-buffer API.
 // ---------------------------------------------------------------------------
+// Per-call staging of rs_decode_batch_masked_dev (stripe pattern ids or
+// bitmasks, plus records on the dedupe path): pinned host + device bytes,
+// reused only after `done` (recorded on the caller's stream behind the
+// call's kernels) has completed.
+struct MaskedSlot {
+    uint8_t *dev = nullptr;
+    size_t dev_cap = 0;
+    uint8_t *host = nullptr;
+    size_t host_cap = 0;
+    hipEvent_t done = nullptr;
+};
+
 struct ThreadCtx {
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;  // second ping-pong stream of run_host
@@ -67,14 +80,10 @@ struct ThreadCtx {
     int *flag = nullptr;       // verify result
     uint8_t *file = nullptr;   // file staging (rs_file_encode / rs_file_decode)
     size_t file_cap = 0;
-    // rs_decode_batch_masked_dev: per-call plan records (device + pinned host),
-    // reused by the next call only after `masked_done` (recorded on the
-    // caller's stream behind the kernels) has completed.
-    uint8_t *masked_dev = nullptr;
-    size_t masked_dev_cap = 0;
-    uint8_t *masked_host = nullptr;
-    size_t masked_host_cap = 0;
-    hipEvent_t masked_done = nullptr;
+    // rs_decode_batch_masked_dev: two staging slots used in turn, so a call's
+    // host-side preparation overlaps the previous call's kernels.
+    MaskedSlot masked[2];
+    int masked_next = 0;
 };
 
 thread_local std::map<int, ThreadCtx *> t_ctx;
@@ -355,6 +364,81 @@ int file_decode_dev(const Codec &c, uint8_t *shards, size_t S, size_t stride, co
 }
 
 
+// Next staging slot of this thread with >= bytes on both sides, once the
+// kernels of the call that last used it have completed.
+int masked_slot(size_t bytes, MaskedSlot **out) {
+    ThreadCtx *ctx = nullptr;
+    int rc = thread_ctx(&ctx);
+    if (rc) return rc;
+    MaskedSlot &sl = ctx->masked[ctx->masked_next];
+    ctx->masked_next ^= 1;
+    if (!sl.done) RS_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    else RS_HIP(hipEventSynchronize(sl.done));
+    if (sl.host_cap < bytes) {
+        if (sl.host) RS_HIP(hipHostFree(sl.host));
+        sl.host = nullptr;
+        sl.host_cap = 0;
+        RS_HIP(hipHostMalloc(reinterpret_cast<void **>(&sl.host), bytes, hipHostMallocDefault));
+        sl.host_cap = bytes;
+    }
+    rc = grow(&sl.dev, &sl.dev_cap, bytes);
+    if (rc) return rc;
+    *out = &sl;
+    return RS_OK;
+}
+
+// One launch per output group over the pattern tables; plan_ids holds the
+// stripes' presence bitmasks.
+int launch_pattern_groups(const Codec &c, const rsamd::PatternTables &pt, const Geometry &geo, const int32_t *bits,
+                          int32_t *bad, hipStream_t stream) {
+    for (int g = 0; g < pt.groups; ++g) {
+        rsamd::MaskedPlan mp;
+        mp.records = pt.records + size_t(g) * pt.npat * pt.rec_stride;
+        mp.rec_stride = pt.rec_stride;
+        mp.plan_ids = bits;
+        mp.nin = c.k();
+        mp.mslots = pt.mslots;
+        mp.mask_table = pt.mask_table;
+        mp.mask_bits = c.total();
+        mp.bad = g == 0 ? bad : nullptr;
+        RS_HIP(rsamd::launch_gf_masked(geo, mp, stream));
+    }
+    return RS_OK;
+}
+
+// Presence bitmasks of present[0 .. n) rows into bits.  RS_OK, or
+// RS_E_NOT_ENOUGH when a row has fewer than k flags set, or RS_E_SINGULAR when
+// a row's pattern has no record in table.  Large batches use host threads.
+int presence_bits(const uint8_t *present, size_t n, int T, int k, const int32_t *table, uint32_t *bits) {
+    auto run = [&](size_t t0, size_t t1) {
+        int rc = RS_OK;
+        for (size_t t = t0; t < t1; ++t) {
+            const uint8_t *row = present + t * T;
+            uint32_t b = 0;
+            for (int i = 0; i < T; ++i) b |= uint32_t(row[i] != 0) << i;
+            bits[t] = b;
+            if (table[b] < 0) rc = __builtin_popcount(b) < k ? RS_E_NOT_ENOUGH : (rc ? rc : RS_E_SINGULAR);
+        }
+        return rc;
+    };
+    const size_t nthreads =
+        n >= (size_t(1) << 18) ? std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency())) : 1;
+    if (nthreads <= 1) return run(0, n);
+    std::vector<std::thread> pool;
+    std::vector<int> rcs(nthreads, RS_OK);
+    const size_t per = (n + nthreads - 1) / nthreads;
+    for (size_t w = 1; w < nthreads; ++w)
+        pool.emplace_back([&, w] { rcs[w] = run(std::min(n, w * per), std::min(n, (w + 1) * per)); });
+    rcs[0] = run(0, std::min(n, per));
+    for (auto &th : pool) th.join();
+    int rc = RS_OK;
+    for (int r : rcs) {
+        if (r == RS_E_NOT_ENOUGH) return r;
+        if (r) rc = r;
+    }
+    return rc;
+}
+
 int decode_masked_dev(const Codec &c, uint8_t *base, const uint8_t *present, size_t n_stripes, size_t shard_len,
                       size_t shard_stride, size_t stripe_stride, hipStream_t stream) {
     const int T = c.total(), k = c.k();
@@ -362,45 +446,42 @@ int decode_masked_dev(const Codec &c, uint8_t *base, const uint8_t *present, siz
     if (n_stripes == 0 || shard_len == 0) return RS_OK;
     if (!base) return fail(RS_E_INVALID, "NULL device base");
     if (n_stripes > size_t(INT32_MAX)) return fail(RS_E_INVALID, "too many stripes");
-    // Distinct presence patterns -> record ids.  Patterns of <= 20 shards are
-    // keyed by their bitmask in a direct table (one pass, no allocation per
-    // stripe); wider codes use an ordered map of the flag vector.
+    const Geometry geo{base, n_stripes, 0, shard_len, shard_stride, stripe_stride};
+
+    // Codes with a pattern table: upload the stripes' presence bitmasks, the
+    // kernels look their records up (no per-call plan building).
+    rsamd::PatternTables pt;
+    std::string err;
+    if (c.pattern_tables(&pt, &err) == RS_OK) {
+        MaskedSlot *sl = nullptr;
+        int rc = masked_slot(n_stripes * sizeof(uint32_t), &sl);
+        if (rc) return rc;
+        uint32_t *bits = reinterpret_cast<uint32_t *>(sl->host);
+        rc = presence_bits(present, n_stripes, T, k, pt.host_mask_table, bits);
+        if (rc) return fail(rc, rc == RS_E_SINGULAR ? "Matrix is singular" : "Not enough shards present");
+        RS_HIP(hipMemcpyAsync(sl->dev, bits, n_stripes * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+        rc = launch_pattern_groups(c, pt, geo, reinterpret_cast<const int32_t *>(sl->dev), nullptr, stream);
+        if (rc) return rc;
+        RS_HIP(hipEventRecord(sl->done, stream));
+        return RS_OK;
+    }
+
+    // Wide codes: distinct presence patterns -> per-call record ids (ordered
+    // map of the flag vector).
     std::vector<std::vector<uint8_t>> pats;
     std::vector<int32_t> pid(n_stripes);
     std::vector<uint8_t> key(T);
-    auto add_pattern = [&]() {
-        pats.push_back(key);
-        return int32_t(pats.size() - 1);
-    };
-    if (T <= 20) {
-        std::vector<int32_t> table(size_t(1) << T, -1);
-        for (size_t t = 0; t < n_stripes; ++t) {
-            const uint8_t *row = present + t * T;
-            uint32_t bits = 0;
-            int np = 0;
-            for (int i = 0; i < T; ++i)
-                if (row[i]) {
-                    bits |= 1u << i;
-                    ++np;
-                }
-            if (np < k) return fail(RS_E_NOT_ENOUGH, "Not enough shards present");
-            int32_t &slot = table[bits];
-            if (slot < 0) {
-                for (int i = 0; i < T; ++i) key[i] = (bits >> i) & 1;
-                slot = add_pattern();
-            }
-            pid[t] = slot;
+    std::map<std::vector<uint8_t>, int32_t> ids;
+    for (size_t t = 0; t < n_stripes; ++t) {
+        int np = 0;
+        for (int i = 0; i < T; ++i) np += (key[i] = present[t * T + i] ? 1 : 0);
+        if (np < k) return fail(RS_E_NOT_ENOUGH, "Not enough shards present");
+        auto it = ids.find(key);
+        if (it == ids.end()) {
+            pats.push_back(key);
+            it = ids.emplace(key, int32_t(pats.size() - 1)).first;
         }
-    } else {
-        std::map<std::vector<uint8_t>, int32_t> ids;
-        for (size_t t = 0; t < n_stripes; ++t) {
-            int np = 0;
-            for (int i = 0; i < T; ++i) np += (key[i] = present[t * T + i] ? 1 : 0);
-            if (np < k) return fail(RS_E_NOT_ENOUGH, "Not enough shards present");
-            auto it = ids.find(key);
-            if (it == ids.end()) it = ids.emplace(key, add_pattern()).first;
-            pid[t] = it->second;
-        }
+        pid[t] = it->second;
     }
     std::vector<std::shared_ptr<const Plan>> plans(pats.size());
     size_t max_missing = 0;
@@ -416,58 +497,38 @@ int decode_masked_dev(const Codec &c, uint8_t *base, const uint8_t *present, siz
     const size_t npat = pats.size();
     const size_t ids_off = groups * npat * L.bytes;
     const size_t bytes = ids_off + n_stripes * sizeof(int32_t);
-
-    ThreadCtx *ctx = nullptr;
-    int rc = thread_ctx(&ctx);
+    MaskedSlot *sl = nullptr;
+    int rc = masked_slot(bytes, &sl);
     if (rc) return rc;
-    if (!ctx->masked_done) RS_HIP(hipEventCreateWithFlags(&ctx->masked_done, hipEventDisableTiming));
-    else RS_HIP(hipEventSynchronize(ctx->masked_done));  // the previous call's kernels are done with the slot
-    if (ctx->masked_host_cap < bytes) {
-        if (ctx->masked_host) RS_HIP(hipHostFree(ctx->masked_host));
-        ctx->masked_host = nullptr;
-        ctx->masked_host_cap = 0;
-        RS_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->masked_host), bytes, hipHostMallocDefault));
-        ctx->masked_host_cap = bytes;
-    }
-    rc = grow(&ctx->masked_dev, &ctx->masked_dev_cap, bytes);
-    if (rc) return rc;
-    uint8_t *img = ctx->masked_host;
-    std::memset(img, 0, ids_off);
     for (size_t g = 0; g < groups; ++g)
-        for (size_t q = 0; q < npat; ++q) {
-            const Plan &pl = *plans[q];
-            uint8_t *r = img + (g * npat + q) * L.bytes;
-            const int nm = int(pl.out_idx().size());
-            const int32_t nout = std::max(0, std::min<int>(ms, nm - int(g) * ms));
-            std::memcpy(r, &nout, sizeof nout);
-            for (int i = 0; i < k; ++i) {
-                const int32_t v = pl.in_idx()[i];
-                std::memcpy(r + L.in_idx + i * 4, &v, 4);
-            }
-            for (int p = 0; p < nout; ++p) {
-                const int row = int(g) * ms + p;
-                const int32_t v = pl.out_idx()[row];
-                std::memcpy(r + L.out_idx + p * 4, &v, 4);
-                for (int i = 0; i < k; ++i) {
-                    const rsamd::PermTable t = rsamd::perm_table(pl.rows().at(row, i));
-                    std::memcpy(r + L.tabs + (size_t(i) * ms + p) * sizeof t, &t, sizeof t);
-                }
-            }
-        }
-    std::memcpy(img + ids_off, pid.data(), n_stripes * sizeof(int32_t));
-    RS_HIP(hipMemcpyAsync(ctx->masked_dev, img, bytes, hipMemcpyHostToDevice, stream));
-    Geometry geo{base, n_stripes, 0, shard_len, shard_stride, stripe_stride};
+        for (size_t q = 0; q < npat; ++q) rsamd::fill_masked_record(*plans[q], int(g), ms, L, sl->host + (g * npat + q) * L.bytes);
+    std::memcpy(sl->host + ids_off, pid.data(), n_stripes * sizeof(int32_t));
+    RS_HIP(hipMemcpyAsync(sl->dev, sl->host, bytes, hipMemcpyHostToDevice, stream));
     for (size_t g = 0; g < groups; ++g) {
         rsamd::MaskedPlan mp;
-        mp.records = ctx->masked_dev + g * npat * L.bytes;
+        mp.records = sl->dev + g * npat * L.bytes;
         mp.rec_stride = L.bytes;
-        mp.plan_ids = reinterpret_cast<const int32_t *>(ctx->masked_dev + ids_off);
+        mp.plan_ids = reinterpret_cast<const int32_t *>(sl->dev + ids_off);
         mp.nin = k;
         mp.mslots = ms;
         RS_HIP(rsamd::launch_gf_masked(geo, mp, stream));
     }
-    RS_HIP(hipEventRecord(ctx->masked_done, stream));
+    RS_HIP(hipEventRecord(sl->done, stream));
     return RS_OK;
+}
+
+int decode_masked_bits_dev(const Codec &c, uint8_t *base, const uint32_t *dev_bits, size_t n_stripes,
+                           size_t shard_len, size_t shard_stride, size_t stripe_stride, int32_t *dev_bad,
+                           hipStream_t stream) {
+    if (n_stripes == 0 || shard_len == 0) return RS_OK;
+    if (!base || !dev_bits) return fail(RS_E_INVALID, "NULL device buffer");
+    if (n_stripes > size_t(INT32_MAX)) return fail(RS_E_INVALID, "too many stripes");
+    rsamd::PatternTables pt;
+    std::string err;
+    int rc = c.pattern_tables(&pt, &err);
+    if (rc) return fail(rc, err);
+    const Geometry geo{base, n_stripes, 0, shard_len, shard_stride, stripe_stride};
+    return launch_pattern_groups(c, pt, geo, reinterpret_cast<const int32_t *>(dev_bits), dev_bad, stream);
 }
 
 const Codec *impl(const rs_codec *c) { return c ? c->impl : nullptr; }
@@ -535,10 +596,12 @@ void rs_thread_release(void) {
         if (c->plan) (void)hipFree(c->plan);
         if (c->flag) (void)hipFree(c->flag);
         if (c->file) (void)hipFree(c->file);
-        if (c->masked_done) (void)hipEventSynchronize(c->masked_done);
-        if (c->masked_dev) (void)hipFree(c->masked_dev);
-        if (c->masked_host) (void)hipHostFree(c->masked_host);
-        if (c->masked_done) (void)hipEventDestroy(c->masked_done);
+        for (MaskedSlot &sl : c->masked) {
+            if (sl.done) (void)hipEventSynchronize(sl.done);
+            if (sl.dev) (void)hipFree(sl.dev);
+            if (sl.host) (void)hipHostFree(sl.host);
+            if (sl.done) (void)hipEventDestroy(sl.done);
+        }
         delete c;
     }
     t_ctx.clear();
@@ -649,6 +712,15 @@ int rs_decode_batch_masked_dev(const rs_codec *codec, uint8_t *dev_base, const u
     if (!c) return fail(RS_E_INVALID, "codec is NULL");
     return decode_masked_dev(*c, dev_base, present, n_stripes, shard_len, shard_stride, stripe_stride,
                              static_cast<hipStream_t>(stream));
+}
+
+int rs_decode_batch_masked_bits_dev(const rs_codec *codec, uint8_t *dev_base, const uint32_t *dev_present_bits,
+                                    size_t n_stripes, size_t shard_len, size_t shard_stride, size_t stripe_stride,
+                                    int32_t *dev_bad_count, void *stream) {
+    const Codec *c = impl(codec);
+    if (!c) return fail(RS_E_INVALID, "codec is NULL");
+    return decode_masked_bits_dev(*c, dev_base, dev_present_bits, n_stripes, shard_len, shard_stride, stripe_stride,
+                                  dev_bad_count, static_cast<hipStream_t>(stream));
 }
 
 int rs_verify_batch_dev(const rs_codec *codec, const uint8_t *dev_base, size_t n_stripes, size_t shard_len,

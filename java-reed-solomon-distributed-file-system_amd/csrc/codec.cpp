@@ -199,4 +199,96 @@ int Codec::decode_plan(const uint8_t *present, std::shared_ptr<const Plan> *out,
     return RS_OK;
 }
 
+void fill_masked_record(const Plan &p, int g, int ms, const MaskedRecordLayout &L, uint8_t *rec) {
+    const int k = int(p.in_idx().size());
+    const int nm = int(p.out_idx().size());
+    const int32_t nout = std::max(0, std::min(ms, nm - g * ms));
+    std::memset(rec, 0, L.bytes);
+    std::memcpy(rec, &nout, sizeof nout);
+    for (int i = 0; i < k; ++i) {
+        const int32_t v = p.in_idx()[i];
+        std::memcpy(rec + L.in_idx + i * 4, &v, 4);
+    }
+    for (int q = 0; q < nout; ++q) {
+        const int row = g * ms + q;
+        const int32_t v = p.out_idx()[row];
+        std::memcpy(rec + L.out_idx + q * 4, &v, 4);
+        for (int i = 0; i < k; ++i) {
+            const PermTable t = perm_table(p.rows().at(row, i));
+            std::memcpy(rec + L.tabs + (size_t(i) * ms + q) * sizeof t, &t, sizeof t);
+        }
+    }
+}
+
+int Codec::pattern_tables(PatternTables *out, std::string *err) const {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        *err = "hipGetDevice failed";
+        return RS_E_HIP;
+    }
+    std::lock_guard<std::mutex> lock(pat_mu_);
+    auto it = patterns_.find(dev);
+    if (it != patterns_.end()) {
+        *out = it->second;
+        return RS_OK;
+    }
+    const int T = total();
+    if (pattern_refusal_.empty() && T > kMaxPatternBits)
+        pattern_refusal_ =
+            "presence bitmasks need k + m <= " + std::to_string(kMaxPatternBits) + " (got " + std::to_string(T) + ")";
+    const uint32_t n = T > kMaxPatternBits ? 0 : 1u << T;
+    size_t npat = 0;
+    for (uint32_t bits = 0; pattern_refusal_.empty() && bits < n; ++bits) npat += __builtin_popcount(bits) >= k_ ? 1 : 0;
+    if (pattern_refusal_.empty() && npat > kMaxPatterns)
+        pattern_refusal_ = "code has " + std::to_string(npat) + " decodable presence patterns (> " +
+                           std::to_string(kMaxPatterns) + "); use rs_decode_batch_masked_dev";
+    if (!pattern_refusal_.empty()) {
+        *err = pattern_refusal_;
+        return RS_E_INVALID;
+    }
+    std::vector<int32_t> table(n, -1);
+    std::vector<std::shared_ptr<const Plan>> plans;
+    plans.reserve(npat);
+    std::vector<uint8_t> present(T);
+    size_t max_missing = 0;
+    for (uint32_t bits = 0; bits < n; ++bits) {
+        if (__builtin_popcount(bits) < k_) continue;
+        for (int i = 0; i < T; ++i) present[i] = (bits >> i) & 1;
+        std::shared_ptr<const Plan> p;
+        const int rc = decode_plan(present.data(), &p);
+        if (rc == RS_E_SINGULAR) continue;  // stays -1: such stripes are skipped and counted
+        if (rc) {
+            *err = "decode plan";
+            return rc;
+        }
+        table[bits] = int32_t(plans.size());
+        max_missing = std::max(max_missing, p->out_idx().size());
+        plans.push_back(std::move(p));
+    }
+    PatternTables t;
+    t.npat = plans.size();
+    t.mslots = std::max(1, std::min(m_, kMaxOut));
+    t.groups = int(std::max<size_t>(1, (max_missing + t.mslots - 1) / t.mslots));
+    const MaskedRecordLayout L = masked_record_layout(k_, t.mslots);
+    t.rec_stride = L.bytes;
+    const size_t rec_bytes = size_t(t.groups) * t.npat * L.bytes;
+    std::vector<uint8_t> img(rec_bytes + size_t(n) * sizeof(int32_t));
+    for (int g = 0; g < t.groups; ++g)
+        for (size_t q = 0; q < t.npat; ++q) fill_masked_record(*plans[q], g, t.mslots, L, img.data() + (g * t.npat + q) * L.bytes);
+    std::memcpy(img.data() + rec_bytes, table.data(), size_t(n) * sizeof(int32_t));
+    void *buf = nullptr;
+    if (hipMalloc(&buf, img.size()) != hipSuccess || hipMemcpy(buf, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        if (buf) (void)hipFree(buf);
+        *err = "pattern table upload failed";
+        return RS_E_HIP;
+    }
+    if (host_mask_table_.empty()) host_mask_table_ = std::move(table);  // same ids on every device; never resized after
+    t.host_mask_table = host_mask_table_.data();
+    t.records = static_cast<const uint8_t *>(buf);
+    t.mask_table = reinterpret_cast<const int32_t *>(static_cast<const uint8_t *>(buf) + rec_bytes);
+    patterns_.emplace(dev, t);
+    *out = t;
+    return RS_OK;
+}
+
 }  // namespace rsamd

@@ -54,6 +54,22 @@ struct PlanLayout {
 PlanLayout plan_layout(int nin, int nout);
 DevPlan dev_plan_at(const void *base, int nin, int nout);
 
+// Fill one masked record (kernels.hpp MaskedRecordLayout) with output group g
+// (at most ms outputs) of plan p.
+void fill_masked_record(const Plan &p, int g, int ms, const MaskedRecordLayout &L, uint8_t *rec);
+
+// Every decodable presence pattern of a code as device-resident masked
+// records, looked up by presence bitmask (rs_decode_batch_masked_bits_dev).
+struct PatternTables {
+    const uint8_t *records = nullptr;     // groups blocks of npat records each
+    size_t rec_stride = 0, npat = 0;
+    const int32_t *mask_table = nullptr;       // [2^total]: pattern id, or -1 (not decodable)
+    const int32_t *host_mask_table = nullptr;  // the same ids in host memory
+    int groups = 0, mslots = 0;
+};
+constexpr int kMaxPatternBits = 20;        // k + m for a bitmask table (4 MiB of ids)
+constexpr size_t kMaxPatterns = 1u << 16;  // decodable patterns in one table
+
 class Codec {
 public:
     static int create(int k, int m, Codec **out, std::string *err);
@@ -74,6 +90,13 @@ public:
     // RS_E_SINGULAR.
     int decode_plan(const uint8_t *present, std::shared_ptr<const Plan> *out, bool data_only = false) const;
 
+    // The pattern tables on the calling thread's current device, built on
+    // first use (every bitmask with >= k present bits gets decode_plan's
+    // record; blocking upload) and then immutable.  RS_E_INVALID when
+    // k + m > kMaxPatternBits or the code has more than kMaxPatterns decodable
+    // patterns (use the host-pattern call), RS_E_HIP on a HIP error.
+    int pattern_tables(PatternTables *out, std::string *err) const;
+
 private:
     Codec(int k, int m);
     int k_, m_;
@@ -81,6 +104,10 @@ private:
     std::unique_ptr<Plan> encode_;
     mutable std::mutex mu_;
     mutable std::map<std::vector<uint8_t>, std::shared_ptr<const Plan>> decode_cache_;
+    mutable std::mutex pat_mu_;
+    mutable std::map<int, PatternTables> patterns_;  // device id -> tables (leaked with the process)
+    mutable std::vector<int32_t> host_mask_table_;
+    mutable std::string pattern_refusal_;  // set once the code is found too wide for a table
 };
 
 }  // namespace rsamd

@@ -206,14 +206,36 @@ struct MaskedArgs {
     uint32_t nvec, chunks, n_items;
     uint32_t rec_in_idx, rec_out_idx, rec_tabs;  // byte offsets inside a record
     int nin;                                     // generic kernel only
+    const int32_t *mask_table;                   // MaskedPlan::mask_table
+    int mask_bits;
+    int32_t *bad;
 };
+
+// Stripe t's record, or nullptr when its presence bitmask is not decodable
+// (counted into bad by the thread that owns the stripe's column 0).
+__device__ __forceinline__ const uint8_t *masked_record(const uint8_t *records, uint64_t rec_stride,
+                                                        const int32_t *plan_ids, const int32_t *mask_table,
+                                                        int mask_bits, int32_t *bad, uint64_t t, bool col0) {
+    int32_t id = plan_ids[t];
+    if (mask_table) {
+        const uint32_t bits = uint32_t(id);
+        id = (bits >> mask_bits) ? -1 : mask_table[bits];
+        if (id < 0) {
+            if (bad && col0) atomicAdd(bad, 1);
+            return nullptr;
+        }
+    }
+    return records + uint64_t(id) * rec_stride;
+}
 
 template <int K, int MS>
 __global__ void __launch_bounds__(kWave) gf_masked_kernel(MaskedArgs a) {
     const uint32_t item = blockIdx.x;
     const uint32_t stripe = item / a.chunks;
     const uint32_t v = (item - stripe * a.chunks) * uint32_t(kWave) + threadIdx.x;
-    const uint8_t *rec = a.records + uint64_t(a.plan_ids[stripe]) * a.rec_stride;
+    const uint8_t *rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, a.bad, stripe,
+                                       v == 0);
+    if (!rec) return;
     const int nout = *reinterpret_cast<const int32_t *>(rec);
     if (nout == 0 || v >= a.nvec) return;
     const int32_t *in_idx = reinterpret_cast<const int32_t *>(rec + a.rec_in_idx);
@@ -256,7 +278,9 @@ __global__ void __launch_bounds__(kWave) gf_masked_generic_kernel(MaskedArgs a) 
     const uint32_t item = blockIdx.x;
     const uint32_t stripe = item / a.chunks;
     const uint32_t v = (item - stripe * a.chunks) * uint32_t(kWave) + threadIdx.x;
-    const uint8_t *rec = a.records + uint64_t(a.plan_ids[stripe]) * a.rec_stride;
+    const uint8_t *rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, a.bad, stripe,
+                                       v == 0);
+    if (!rec) return;
     const int nout = *reinterpret_cast<const int32_t *>(rec);
     if (nout == 0 || v >= a.nvec) return;
     const int32_t *in_idx = reinterpret_cast<const int32_t *>(rec + a.rec_in_idx);
@@ -303,6 +327,9 @@ struct MaskedByteArgs {
     uint64_t stripe_stride, shard_stride, col0, ncols, total;
     uint32_t rec_in_idx, rec_out_idx, rec_tabs;
     int nin, mslots;
+    const int32_t *mask_table;
+    int mask_bits;
+    int32_t *bad;
 };
 
 __global__ void __launch_bounds__(kThreads) gf_masked_byte_kernel(MaskedByteArgs a) {
@@ -310,7 +337,9 @@ __global__ void __launch_bounds__(kThreads) gf_masked_byte_kernel(MaskedByteArgs
     for (uint64_t idx = uint64_t(blockIdx.x) * kThreads + threadIdx.x; idx < a.total; idx += step) {
         const uint64_t stripe = idx / a.ncols;
         const uint64_t col = a.col0 + (idx - stripe * a.ncols);
-        const uint8_t *rec = a.records + uint64_t(a.plan_ids[stripe]) * a.rec_stride;
+        const uint8_t *rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, a.bad,
+                                           stripe, col == 0);
+        if (!rec) continue;
         const int nout = *reinterpret_cast<const int32_t *>(rec);
         if (nout == 0) continue;
         const int32_t *in_idx = reinterpret_cast<const int32_t *>(rec + a.rec_in_idx);
@@ -482,7 +511,7 @@ hipError_t launch_masked_bytes(const Geometry &g, const MaskedPlan &p, const Mas
                                size_t ncols, hipStream_t s) {
     MaskedByteArgs a{g.base, p.records, p.rec_stride, p.plan_ids, g.stripe_stride, g.shard_stride, col0, ncols,
                      uint64_t(g.n_stripes) * ncols, uint32_t(l.in_idx), uint32_t(l.out_idx), uint32_t(l.tabs),
-                     p.nin, p.mslots};
+                     p.nin, p.mslots, p.mask_table, p.mask_bits, p.bad};
     if (a.total == 0) return hipSuccess;
     const unsigned grid = unsigned(std::min<uint64_t>((a.total + kThreads - 1) / kThreads, 65536));
     hipLaunchKernelGGL(gf_masked_byte_kernel, dim3(grid), dim3(kThreads), 0, s, a);
@@ -516,7 +545,7 @@ hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t 
             const size_t nst = std::min(stripes_per_launch, g.n_stripes - t0);
             MaskedArgs a{base + t0 * g.stripe_stride, p.records, p.rec_stride, p.plan_ids + t0, g.stripe_stride,
                          g.shard_stride, nvec, chunks, uint32_t(nst * chunks), uint32_t(l.in_idx),
-                         uint32_t(l.out_idx), uint32_t(l.tabs), p.nin};
+                         uint32_t(l.out_idx), uint32_t(l.tabs), p.nin, p.mask_table, p.mask_bits, p.bad};
             hipError_t e = dispatch_masked(a, p.mslots, s);
             if (e != hipSuccess) return e;
         }

@@ -48,12 +48,20 @@ struct MaskedRecordLayout {
 };
 MaskedRecordLayout masked_record_layout(int nin, int mslots);
 
+//
+// With mask_table set, plan_ids[t] is instead stripe t's presence bitmask
+// (bit i = shard i present) and its record is mask_table[bits] (-1: not
+// decodable; bits >= 2^mask_bits is never looked up).  Such stripes are left
+// alone and, when bad is set, counted there once (atomicAdd per stripe).
 struct MaskedPlan {
     const uint8_t *records = nullptr;
     size_t rec_stride = 0;
     const int32_t *plan_ids = nullptr;
     int nin = 0;
     int mslots = 0;  // output slots per record (<= kMaxOut)
+    const int32_t *mask_table = nullptr;
+    int mask_bits = 0;
+    int32_t *bad = nullptr;
 };
 
 hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t s);

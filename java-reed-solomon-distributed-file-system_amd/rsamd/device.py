@@ -59,13 +59,33 @@ def decode(codec: ReedSolomon, dev_base: int, present: Sequence, lay: StripeLayo
 
 
 def decode_masked(codec: ReedSolomon, dev_base: int, present, lay: StripeLayout, stream=None) -> None:
-    """Per-stripe presence patterns: present is (n_stripes, k+m) of bools/0-1."""
-    p = np.ascontiguousarray(np.asarray(present, dtype=bool).astype(np.uint8))
+    """Per-stripe presence patterns: present is (n_stripes, k+m) of bools/0-1
+    (a C-contiguous bool or uint8 array is passed without a copy)."""
+    p = present if isinstance(present, np.ndarray) and present.dtype in (np.bool_, np.uint8) else \
+        np.asarray(present, dtype=bool)
+    p = np.ascontiguousarray(p).view(np.uint8)
     if p.ndim != 2 or p.shape[0] != lay.n_stripes or p.shape[1] != codec.getTotalShardCount():
         raise ValueError(f"present must be ({lay.n_stripes}, {codec.getTotalShardCount()}), got {p.shape}")
     check(_lib.load().rs_decode_batch_masked_dev(codec.handle, C.c_void_p(dev_base), p.ctypes.data_as(_lib.u8p),
                                                  lay.n_stripes, lay.shard_len, lay.shard_stride, lay.stripe_stride,
                                                  C.c_void_p(_stream_handle(stream))))
+
+
+def decode_masked_bits(codec: ReedSolomon, dev_base: int, dev_bits: int, lay: StripeLayout, dev_bad: int = 0,
+                       stream=None) -> None:
+    """Per-stripe presence bitmasks already in device memory: dev_bits points
+    at n_stripes uint32 words, bit i = shard i present.  Undecodable stripes
+    are skipped and counted into the device int32 at dev_bad (when given)."""
+    check(_lib.load().rs_decode_batch_masked_bits_dev(codec.handle, C.c_void_p(dev_base), C.c_void_p(dev_bits),
+                                                      lay.n_stripes, lay.shard_len, lay.shard_stride,
+                                                      lay.stripe_stride, C.c_void_p(dev_bad or None),
+                                                      C.c_void_p(_stream_handle(stream))))
+
+
+def presence_bits(present) -> np.ndarray:
+    """(n_stripes, k+m) presence flags -> uint32 bitmask per stripe (bit i = shard i)."""
+    p = np.asarray(present, dtype=bool)
+    return (p.astype(np.uint32) << np.arange(p.shape[1], dtype=np.uint32)).sum(axis=1, dtype=np.uint32)
 
 
 def verify(codec: ReedSolomon, dev_base: int, lay: StripeLayout, dev_flag: int, stream=None) -> None:

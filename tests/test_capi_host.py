@@ -196,3 +196,10 @@ def test_recovery_machine_contract_without_device(native):
     for i in (0, 1, 2, 3, 4, 4):
         q.addChunkserverDisksData(i, b"zz")
     q.recoverChunkserverDiskData()
+
+
+def test_presence_bits_helper():
+    from rsamd.device import presence_bits
+    p = np.array([[1, 1, 1, 1, 0, 0], [0, 1, 1, 1, 1, 1], [1] * 6], dtype=bool)
+    assert presence_bits(p).tolist() == [0b001111, 0b111110, 0b111111]
+    assert presence_bits(p).dtype == np.uint32

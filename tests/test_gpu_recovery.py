@@ -140,3 +140,111 @@ def test_recovery_machine_mirror(gpu, oracle_lib):
                 mach.addChunkserverDisksData(i, shards[i].tobytes())
         for j in miss:
             assert mach.retrieveRecoveredDiskData(j) == shards[j].tobytes()
+
+
+def _run_bits(rs, batch, words, stride=None):
+    """Device-resident presence bitmasks (rs_decode_batch_masked_bits_dev);
+    returns (shards, bad count)."""
+    import torch
+    from rsamd import device
+    from rsamd.device import StripeLayout
+    B, T, S = batch.shape
+    stride = stride or S
+    host = np.zeros((B, T, stride), np.uint8)
+    host[:, :, :S] = batch
+    for t in range(B):
+        for j in range(T):
+            if not (int(words[t]) >> j) & 1:
+                host[t, j, :S] = 0x3C
+    dev = torch.from_numpy(host.reshape(-1).copy()).to("cuda:0")
+    bits = torch.from_numpy(np.asarray(words, dtype=np.uint32).view(np.int32)).to("cuda:0")
+    bad = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    device.decode_masked_bits(rs, dev.data_ptr(), bits.data_ptr(), StripeLayout(B, S, stride, stride * T),
+                              bad.data_ptr(), torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    return dev.cpu().numpy().reshape(B, T, stride)[:, :, :S], int(bad.item()), host[:, :, :S]
+
+
+@pytest.mark.parametrize("S,stride", [(4096, 4096), (1000, 1008), (999, 1001)])
+def test_bits_every_bitmask_4_2(gpu, oracle_lib, S, stride):
+    """All 64 bitmasks of 4+2 plus out-of-range words: decodable stripes are
+    rebuilt bit-exact, the rest are left untouched and counted."""
+    import rsamd
+    words = list(range(64)) + [64, 0xFFFFFFFF, 1 << 31]
+    B = len(words)
+    rng = np.random.default_rng(S)
+    batch = np.zeros((B, 6, S), np.uint8)
+    batch[:, :4] = rng.integers(0, 256, (B, 4, S), dtype=np.uint8)
+    c = oracle_lib.Codec(4, 2)
+    for t in range(B):
+        c.encode_parity([batch[t, i] for i in range(6)], 0, S)
+    out, bad, before = _run_bits(rsamd.ReedSolomon.create(4, 2), batch, words, stride)
+    ok = np.array([w < 64 and bin(w).count("1") >= 4 for w in words])
+    assert bad == int((~ok).sum())
+    assert np.array_equal(out[ok], batch[ok])
+    assert np.array_equal(out[~ok], before[~ok])
+
+
+def test_bits_10_4_and_17_3(gpu, golden_dir):
+    import rsamd
+    from rsamd.device import presence_bits
+    g = _golden(golden_dir, "rs_10_4_s1024_b4.npz")
+    pats = [[i not in miss for i in range(14)] for miss in [(0, 1, 2, 3), (), (13,), (2, 7, 11)]]
+    out, bad, _ = _run_bits(rsamd.ReedSolomon.create(10, 4), g, presence_bits(pats))
+    assert bad == 0 and np.array_equal(out, g)
+    g = _golden(golden_dir, "rs_17_3_s512_b2.npz")
+    pats = [[i not in miss for i in range(20)] for miss in [(0, 5, 19), (17, 18)]]
+    out, bad, _ = _run_bits(rsamd.ReedSolomon.create(17, 3), g, presence_bits(pats))
+    assert bad == 0 and np.array_equal(out, g)
+
+
+@pytest.mark.parametrize("k,m", [(12, 9), (10, 10)])
+def test_bits_rejects_wide_codes_host_path_still_decodes(gpu, oracle_lib, k, m):
+    """k+m > 20 or > 65536 decodable patterns: the bitmask call refuses before
+    any launch; the host-flag call falls back to per-call records."""
+    import torch
+    import rsamd
+    from rsamd import device
+    from rsamd.device import StripeLayout
+    rs = rsamd.ReedSolomon.create(k, m)
+    S, B, T = 64, 3, k + m
+    buf = torch.zeros(B * T * S, dtype=torch.uint8, device="cuda:0")
+    bits = torch.zeros(B, dtype=torch.int32, device="cuda:0")
+    with pytest.raises(rsamd.IllegalArgumentException):
+        device.decode_masked_bits(rs, buf.data_ptr(), bits.data_ptr(), StripeLayout(B, S, S, S * T))
+    rng = np.random.default_rng(k)
+    batch = np.zeros((B, T, S), np.uint8)
+    batch[:, :k] = rng.integers(0, 256, (B, k, S), dtype=np.uint8)
+    c = oracle_lib.Codec(k, m)
+    for t in range(B):
+        c.encode_parity([batch[t, i] for i in range(T)], 0, S)
+    pats = [[i not in miss for i in range(T)] for miss in [tuple(range(m)), (), (k - 1, k + m - 1)]]
+    assert np.array_equal(_run_masked(rs, batch, pats), batch)
+
+
+def test_bits_full_size_small_objects(gpu):
+    """1 M stripes of 4 KiB with device-resident bitmasks, against the host-flag call."""
+    import torch
+    import rsamd
+    from rsamd import device
+    from rsamd.device import StripeLayout, presence_bits
+    rs = rsamd.ReedSolomon.create(4, 2)
+    B, S = 1 << 20, 4096
+    lay = StripeLayout.packed(B, 6, S)
+    buf = torch.empty(lay.nbytes, dtype=torch.uint8, device="cuda:0")
+    st = torch.cuda.current_stream()
+    device.fill_synthetic(buf.data_ptr(), 4, lay, 0x5EED, 0, st)
+    device.encode(rs, buf.data_ptr(), lay, st)
+    ref = buf.clone()
+    rng = np.random.default_rng(2)
+    allp = np.array([[i not in miss for i in range(6)] for e in range(3)
+                     for miss in itertools.combinations(range(6), e)], dtype=bool)
+    pats = allp[rng.integers(0, len(allp), B)]
+    mask = torch.from_numpy(~pats).to("cuda:0")
+    buf.view(B, 6, S).masked_fill_(mask[:, :, None], 0)
+    bits = torch.from_numpy(presence_bits(pats).view(np.int32)).to("cuda:0")
+    bad = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    device.decode_masked_bits(rs, buf.data_ptr(), bits.data_ptr(), lay, bad.data_ptr(), st)
+    assert torch.equal(buf, ref) and int(bad.item()) == 0
+    del buf, ref, mask
+    torch.cuda.empty_cache()

@@ -67,9 +67,13 @@ def main():
     pats = np.array([[i not in miss for i in range(6)] for e in range(3)
                      for miss in itertools.combinations(range(6), e)], dtype=bool)
     present = pats[np.random.default_rng(0).integers(0, len(pats), B)]
+    alg = (4 * int((~present).any(axis=1).sum()) + int((~present).sum())) * S
     t = timed(torch, st, lambda: rdev.decode_masked(rs, buf.data_ptr(), present, lay, st))
     out["masked_decode_1Mx4KiB_GiBps"] = round(4 * S * B / t / 2**30, 1)
-    out["masked_decode_hbm_frac"] = round((4 + float((~present).sum()) / B) * S * B / t / 8e12, 4)
+    out["masked_decode_hbm_frac"] = round(alg / t / 8e12, 4)
+    bits = torch.from_numpy(rdev.presence_bits(present).view(np.int32)).to("cuda:0")
+    t = timed(torch, st, lambda: rdev.decode_masked_bits(rs, buf.data_ptr(), bits.data_ptr(), lay, 0, st))
+    out["masked_bits_decode_hbm_frac"] = round(alg / t / 8e12, 4)
     print(json.dumps(out), flush=True)
 
 
