@@ -148,6 +148,9 @@ def main():
                 "kernel": f"gf_vec_kernel<{k},{m},false> (rs_encode_batch_dev)",
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_ms": round(launch_ms, 4),
+                # also as a fraction of the measured device copy kernel
+                "frac_of_copy_kernel": (round(achieved / extra["copy_kernel_GBps"], 4)
+                                        if extra.get("copy_kernel_GBps") else None),
             },
             "cpu_baseline": cpu,
             "extra": extra,
@@ -332,8 +335,22 @@ def host_inclusive(rsamd, k, m):
     _, S = file_layout(rs, len(data))
     fsh = [np.zeros(S, np.uint8) for _ in range(k + m)]
     out["host_inclusive_file_encode_GiBps"] = rate(lambda: file_encode_into(rs, data, fsh), len(data))
-    out["host_inclusive_note"] = (f"{k}+{m}, {n >> 20} MiB pageable host shards per call (file encode: a "
-                                  f"{len(data) >> 20} MiB file); PCIe-bound, never the bench value")
+    from rsamd.layout import file_decode_into
+    fpresent = [False] + [True] * (k + m - 2) + [False]
+    fout = np.empty(len(data), np.uint8)
+    out["host_inclusive_file_decode_0_%d_GiBps" % (k + m - 1)] = rate(
+        lambda: file_decode_into(rs, fsh, fpresent, S, fout), len(data))
+    # the same calls on pinned (page-locked) host buffers, where
+    # the two streams' H2D and D2H overlap as DMA
+    import torch
+    pin = [torch.empty(n, dtype=torch.uint8, pin_memory=True).numpy() for _ in range(k + m)]
+    for a, b in zip(pin, sh):
+        a[:] = b
+    out["host_inclusive_pinned_encode_GiBps"] = rate(lambda: rs.encodeParity(pin, 0, n), k * n)
+    out["host_inclusive_pinned_decode_0_1_GiBps"] = rate(lambda: rs.decodeMissing(pin, present, 0, n), k * n)
+    del pin
+    out["host_inclusive_note"] = (f"{k}+{m}, {n >> 20} MiB host shards per call, pageable unless 'pinned' "
+                                  f"(file legs: a {len(data) >> 20} MiB file); PCIe-bound, never the bench value")
     return out
 
 

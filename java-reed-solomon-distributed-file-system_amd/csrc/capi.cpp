@@ -69,11 +69,15 @@ struct MaskedSlot {
     hipEvent_t done = nullptr;
 };
 
+constexpr int kStageBufs = 3;  // staging buffers of the host-buffer pipeline
+
 struct ThreadCtx {
-    hipStream_t stream = nullptr;
-    hipStream_t stream2 = nullptr;  // second ping-pong stream of run_host
-    hipEvent_t ready = nullptr;     // orders stream2 behind stream's verify-flag memset
-    uint8_t *stage = nullptr;       // 2 x nslots x slot_stride device bytes (ping-pong halves)
+    hipStream_t stream = nullptr;   // host pipeline: H2D copies + kernels, in chunk order
+    hipStream_t stream2 = nullptr;  // host pipeline: D2H copies, in chunk order
+    hipEvent_t ready = nullptr;     // joins stream2 back into stream
+    hipEvent_t coded[kStageBufs] = {};  // buffer b's kernels done (stream -> stream2)
+    hipEvent_t freed[kStageBufs] = {};  // buffer b's D2H done (stream2 -> stream)
+    uint8_t *stage = nullptr;       // kStageBufs x nslots x slot_stride device bytes
     size_t stage_cap = 0;
     uint8_t *plan = nullptr;   // per-call plan images (rs_code_some_shards)
     size_t plan_cap = 0;
@@ -103,6 +107,10 @@ int thread_ctx(ThreadCtx **out) {
         hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ready, hipEventDisableTiming);
+        for (int b = 0; b < kStageBufs && e == hipSuccess; ++b) {
+            e = hipEventCreateWithFlags(&c->coded[b], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&c->freed[b], hipEventDisableTiming);
+        }
         if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&c->flag), 256);
         if (e != hipSuccess) {
             delete c;
@@ -124,12 +132,52 @@ int grow(uint8_t **buf, size_t *cap, size_t want) {
     return RS_OK;
 }
 
-// Bytes per shard staged per round trip.  Chunks alternate between two
-// streams with their own staging halves, so chunk j's D2H overlaps chunk
-// j+1's H2D (PCIe is full duplex) and the kernels hide under both.
+// Host-buffer pipeline.  A call is cut into chunks staged through
+// kStageBufs device buffers.  `stream` carries every H2D copy and kernel in
+// chunk order, `stream2` every D2H copy in chunk order: chunk j's D2H runs
+// beside chunk j+1's H2D (pinned copies measured 57 GB/s one way, 97 GB/s
+// both ways on MI355X; two streams each doing H2D-kernel-D2H fall into
+// lockstep and never overlap the directions).  Events hand each buffer from
+// the kernels to its D2H and back to the next H2D that reuses it.
 constexpr size_t kChunk = size_t(32) << 20;
+constexpr size_t kMinChunk = size_t(4) << 20;
+
+// Bytes per shard per chunk: about 8 chunks per call, within [4, 32] MiB.
+size_t chunk_bytes(size_t total) { return std::min(kChunk, std::max(kMinChunk, (total / 8 + 255) / 256 * 256)); }
 
 size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+struct Pipeline {
+    ThreadCtx *ctx;
+    int nbuf;  // staging buffers in use (1 .. kStageBufs)
+    // Before chunk j's H2D: its buffer's previous D2H must be done.
+    int begin(size_t j) const {
+        if (j >= size_t(nbuf)) RS_HIP(hipStreamWaitEvent(ctx->stream, ctx->freed[j % nbuf], 0));
+        return RS_OK;
+    }
+    // After chunk j's kernels: D2H copies issued on out() follow them.
+    int coded(size_t j) const {
+        RS_HIP(hipEventRecord(ctx->coded[j % nbuf], ctx->stream));
+        RS_HIP(hipStreamWaitEvent(ctx->stream2, ctx->coded[j % nbuf], 0));
+        return RS_OK;
+    }
+    // After chunk j's D2H copies.
+    int done(size_t j) const {
+        RS_HIP(hipEventRecord(ctx->freed[j % nbuf], ctx->stream2));
+        return RS_OK;
+    }
+    hipStream_t in() const { return ctx->stream; }
+    hipStream_t out() const { return ctx->stream2; }
+    // stream waits for everything on stream2, then the host waits for stream.
+    int finish() const {
+        RS_HIP(hipEventRecord(ctx->ready, ctx->stream2));
+        RS_HIP(hipStreamWaitEvent(ctx->stream, ctx->ready, 0));
+        RS_HIP(hipStreamSynchronize(ctx->stream));
+        return RS_OK;
+    }
+};
+
+int n_bufs(size_t n_chunks) { return int(std::min<size_t>(kStageBufs, std::max<size_t>(1, n_chunks))); }
 
 // Stage [offset, offset+count) of the host shards (slot-indexed), run every
 // launch group of `plans`, copy results back.
@@ -142,52 +190,48 @@ int run_host(const std::vector<DevPlan> &plans, int nslots, const std::vector<in
     ThreadCtx *ctx = nullptr;
     int rc = thread_ctx(&ctx);
     if (rc) return rc;
-    const size_t chunk = std::min(count, kChunk);
+    const size_t chunk = std::min(count, chunk_bytes(count));
     const size_t slot_stride = round_up(std::max<size_t>(chunk, 1), 256);
-    const size_t half = slot_stride * size_t(nslots);
-    const int nbuf = count > chunk ? 2 : 1;
-    rc = grow(&ctx->stage, &ctx->stage_cap, half * size_t(nbuf));
+    const size_t buf_bytes = slot_stride * size_t(nslots);
+    const Pipeline pl{ctx, n_bufs((count + chunk - 1) / chunk)};
+    rc = grow(&ctx->stage, &ctx->stage_cap, buf_bytes * size_t(pl.nbuf));
     if (rc) return rc;
-    hipStream_t streams[2] = {ctx->stream, ctx->stream2};
-    if (mode == Mode::Verify) {
-        RS_HIP(hipMemsetAsync(ctx->flag, 0, sizeof(int), ctx->stream));
-        RS_HIP(hipEventRecord(ctx->ready, ctx->stream));
-        RS_HIP(hipStreamWaitEvent(ctx->stream2, ctx->ready, 0));
-    }
+    if (mode == Mode::Verify) RS_HIP(hipMemsetAsync(ctx->flag, 0, sizeof(int), pl.in()));
     size_t j = 0;
     for (size_t done = 0; done < count; done += chunk, ++j) {
         const size_t n = std::min(chunk, count - done);
-        hipStream_t st = streams[j % nbuf];
-        uint8_t *stage = ctx->stage + (j % nbuf) * half;
+        uint8_t *stage = ctx->stage + (j % pl.nbuf) * buf_bytes;
+        rc = pl.begin(j);
+        if (rc) return rc;
         for (int s : in_slots)
             RS_HIP(hipMemcpyAsync(stage + size_t(s) * slot_stride, host[s] + offset + done, n, hipMemcpyHostToDevice,
-                                  st));
+                                  pl.in()));
         Geometry g;
         g.base = stage;
         g.n_stripes = 1;
         g.col0 = 0;
         g.len = n;
         g.shard_stride = slot_stride;
-        g.stripe_stride = half;
-        for (const DevPlan &p : plans) RS_HIP(rsamd::launch_gf(g, p, mode, ctx->flag, st));
-        if (mode == Mode::Code)
+        g.stripe_stride = buf_bytes;
+        for (const DevPlan &p : plans) RS_HIP(rsamd::launch_gf(g, p, mode, ctx->flag, pl.in()));
+        if (mode == Mode::Code) {
+            rc = pl.coded(j);
+            if (rc) return rc;
             for (int s : out_slots)
                 RS_HIP(hipMemcpyAsync(host[s] + offset + done, stage + size_t(s) * slot_stride, n,
-                                      hipMemcpyDeviceToHost, st));
-    }
-    if (nbuf == 2) {  // join: stream waits for everything stream2 issued
-        RS_HIP(hipEventRecord(ctx->ready, ctx->stream2));
-        RS_HIP(hipStreamWaitEvent(ctx->stream, ctx->ready, 0));
+                                      hipMemcpyDeviceToHost, pl.out()));
+            rc = pl.done(j);
+            if (rc) return rc;
+        }
     }
     if (mode == Mode::Verify) {
         int h = 0;
-        RS_HIP(hipMemcpyAsync(&h, ctx->flag, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-        RS_HIP(hipStreamSynchronize(ctx->stream));
+        RS_HIP(hipMemcpyAsync(&h, ctx->flag, sizeof(int), hipMemcpyDeviceToHost, pl.in()));
+        RS_HIP(hipStreamSynchronize(pl.in()));
         *result = h ? 0 : 1;
-    } else {
-        RS_HIP(hipStreamSynchronize(ctx->stream));
+        return RS_OK;
     }
-    return RS_OK;
+    return pl.finish();
 }
 
 // ReedSolomon.checkBuffersAndSizes (ReedSolomon.java:277-302), same order and text.
@@ -363,6 +407,92 @@ int file_decode_dev(const Codec &c, uint8_t *shards, size_t S, size_t stride, co
     return RS_OK;
 }
 
+
+// Host file paths (rs_file_encode / rs_file_decode): block rows staged
+// through two device halves on two streams, chunk_bytes() of file per
+// chunk, so chunk j's copies overlap chunk j+1's and each pageable copy is a
+// chunk (whole-file pageable copies measured ~5x slower than PCIe rate).
+
+struct FileChunks {
+    size_t R = 0, rows = 0;          // block rows per chunk, rows in all
+    size_t fbytes = 0, sstride = 0;  // staged file bytes and shard stride per buffer
+    size_t buf_bytes = 0;
+    int nbuf = 1;
+};
+
+FileChunks file_chunks(int k, int total, size_t S, size_t block) {
+    FileChunks f;
+    f.rows = S / block;
+    f.R = std::min(f.rows, std::max<size_t>(1, chunk_bytes(S * size_t(k)) / (size_t(k) * block)));
+    f.nbuf = n_bufs((f.rows + f.R - 1) / f.R);
+    f.fbytes = round_up(f.R * size_t(k) * block, 256);
+    f.sstride = round_up(f.R * block, 256);
+    f.buf_bytes = f.fbytes + f.sstride * size_t(total);
+    return f;
+}
+
+// rs_file_decode when byteCntInShard is the whole shard: one pass per chunk
+// -- upload the first k present shards, rebuild every absent shard and merge
+// the data shards into the file chunk on the GPU, download the rebuilt shards
+// (decodeMissing fills them in, ReedSolomonDecoder.java:36) and the file bytes.
+// Same checks, order and messages as rs_decode_missing + the merge.
+int file_decode_chunked(const Codec &c, uint8_t *const *shards, const int64_t *lens, const uint8_t *present,
+                        int32_t block, uint8_t *file_out, int64_t file_size) {
+    const int T = c.total(), k = c.k();
+    const int64_t S = lens[0];
+    int rc = check_buffers_and_sizes(c, shards, T, lens, 0, S);
+    if (rc) return rc;
+    int n_present = 0;
+    for (int i = 0; i < T; ++i) n_present += present[i] ? 1 : 0;
+    if (n_present < k) return fail(RS_E_NOT_ENOUGH, "Not enough shards present");
+    if (n_present < T) {
+        std::shared_ptr<const Plan> plan;
+        rc = c.decode_plan(present, &plan);
+        if (rc) return fail(rc, rc == RS_E_SINGULAR ? "Matrix is singular" : "Not enough shards present");
+    }
+    if (file_size < 0 || file_size > S * k) return fail(RS_E_INVALID, "file size exceeds k * shard length");
+    if (file_size > 0 && !file_out) return fail(RS_E_INVALID, "file_out is NULL");
+    if (S == 0 || (file_size == 0 && n_present == T)) return RS_OK;
+    rc = need_device();
+    if (rc) return rc;
+    ThreadCtx *ctx = nullptr;
+    rc = thread_ctx(&ctx);
+    if (rc) return rc;
+    const size_t blk = size_t(block);
+    const FileChunks f = file_chunks(k, T, size_t(S), blk);
+    rc = grow(&ctx->file, &ctx->file_cap, f.buf_bytes * size_t(f.nbuf));
+    if (rc) return rc;
+    const Pipeline pl{ctx, f.nbuf};
+    std::vector<int> surv, missing;
+    for (int i = 0; i < T; ++i) {
+        if (present[i] && int(surv.size()) < k) surv.push_back(i);
+        if (!present[i]) missing.push_back(i);
+    }
+    for (size_t j = 0, r0 = 0; r0 < f.rows; ++j, r0 += f.R) {
+        const size_t rc_rows = std::min(f.R, f.rows - r0);
+        const size_t col0 = r0 * blk, n = rc_rows * blk;
+        const size_t fo = r0 * size_t(k) * blk;
+        const size_t flen = size_t(file_size) > fo ? std::min(rc_rows * size_t(k) * blk, size_t(file_size) - fo) : 0;
+        if (flen == 0 && missing.empty()) break;
+        uint8_t *dfile = ctx->file + (j % f.nbuf) * f.buf_bytes, *dsh = dfile + f.fbytes;
+        rc = pl.begin(j);
+        if (rc) return rc;
+        for (int sidx : surv)
+            RS_HIP(hipMemcpyAsync(dsh + size_t(sidx) * f.sstride, shards[sidx] + col0, n, hipMemcpyHostToDevice,
+                                  pl.in()));
+        rc = file_decode_dev(c, dsh, n, f.sstride, present, blk, dfile, flen, true, pl.in());
+        if (rc) return rc;
+        rc = pl.coded(j);
+        if (rc) return rc;
+        for (int sidx : missing)
+            RS_HIP(hipMemcpyAsync(shards[sidx] + col0, dsh + size_t(sidx) * f.sstride, n, hipMemcpyDeviceToHost,
+                                  pl.out()));
+        if (flen) RS_HIP(hipMemcpyAsync(file_out + fo, dfile, flen, hipMemcpyDeviceToHost, pl.out()));
+        rc = pl.done(j);
+        if (rc) return rc;
+    }
+    return pl.finish();
+}
 
 // Next staging slot of this thread with >= bytes on both sides, once the
 // kernels of the call that last used it have completed.
@@ -592,6 +722,10 @@ void rs_thread_release(void) {
         if (c->stream) (void)hipStreamDestroy(c->stream);
         if (c->stream2) (void)hipStreamDestroy(c->stream2);
         if (c->ready) (void)hipEventDestroy(c->ready);
+        for (int b = 0; b < kStageBufs; ++b) {
+            if (c->coded[b]) (void)hipEventDestroy(c->coded[b]);
+            if (c->freed[b]) (void)hipEventDestroy(c->freed[b]);
+        }
         if (c->stage) (void)hipFree(c->stage);
         if (c->plan) (void)hipFree(c->plan);
         if (c->flag) (void)hipFree(c->flag);
@@ -775,18 +909,30 @@ int rs_file_encode(const rs_codec *codec, const uint8_t *file, int64_t file_len,
     ThreadCtx *ctx = nullptr;
     rc = thread_ctx(&ctx);
     if (rc) return rc;
-    const size_t stride = round_up(size_t(S), 256);
-    const size_t file_bytes = round_up(size_t(file_len), 256);
-    rc = grow(&ctx->file, &ctx->file_cap, file_bytes + stride * size_t(c->total()));
+    const size_t k = size_t(c->k()), blk = size_t(block);
+    const FileChunks f = file_chunks(c->k(), c->total(), size_t(S), blk);
+    rc = grow(&ctx->file, &ctx->file_cap, f.buf_bytes * size_t(f.nbuf));
     if (rc) return rc;
-    uint8_t *dfile = ctx->file, *dsh = ctx->file + file_bytes;
-    if (file_len) RS_HIP(hipMemcpyAsync(dfile, file, size_t(file_len), hipMemcpyHostToDevice, ctx->stream));
-    rc = file_encode_dev(*c, dfile, size_t(file_len), size_t(block), dsh, stride, ctx->stream);
-    if (rc) return rc;
-    for (int i = 0; i < c->total(); ++i)
-        RS_HIP(hipMemcpyAsync(shards_out[i], dsh + size_t(i) * stride, size_t(S), hipMemcpyDeviceToHost, ctx->stream));
-    RS_HIP(hipStreamSynchronize(ctx->stream));
-    return RS_OK;
+    const Pipeline pl{ctx, f.nbuf};
+    for (size_t j = 0, r0 = 0; r0 < f.rows; ++j, r0 += f.R) {
+        const size_t rc_rows = std::min(f.R, f.rows - r0);
+        const size_t off = r0 * k * blk;  // < file_len: every row holds file bytes
+        const size_t flen = std::min(rc_rows * k * blk, size_t(file_len) - off);
+        uint8_t *dfile = ctx->file + (j % f.nbuf) * f.buf_bytes, *dsh = dfile + f.fbytes;
+        rc = pl.begin(j);
+        if (rc) return rc;
+        RS_HIP(hipMemcpyAsync(dfile, file + off, flen, hipMemcpyHostToDevice, pl.in()));
+        rc = file_encode_dev(*c, dfile, flen, blk, dsh, f.sstride, pl.in());
+        if (rc) return rc;
+        rc = pl.coded(j);
+        if (rc) return rc;
+        for (int i = 0; i < c->total(); ++i)
+            RS_HIP(hipMemcpyAsync(shards_out[i] + r0 * blk, dsh + size_t(i) * f.sstride, rc_rows * blk,
+                                  hipMemcpyDeviceToHost, pl.out()));
+        rc = pl.done(j);
+        if (rc) return rc;
+    }
+    return pl.finish();
 }
 
 int rs_file_decode(const rs_codec *codec, uint8_t *const *shards, int nshards, const int64_t *shard_lens,
@@ -794,6 +940,9 @@ int rs_file_decode(const rs_codec *codec, uint8_t *const *shards, int nshards, c
                    int64_t file_size) {
     const Codec *c = impl(codec);
     if (!c) return fail(RS_E_INVALID, "codec is NULL");
+    if (nshards == c->total() && shards && shard_lens && present && byte_cnt_in_shard == shard_lens[0] &&
+        block >= 1 && shard_lens[0] % block == 0)
+        return file_decode_chunked(*c, shards, shard_lens, present, block, file_out, file_size);
     // decodeMissing(shards, shardPresent, 0, byteCntInShard)  (ReedSolomonDecoder.java:36)
     int rc = rs_decode_missing(codec, shards, nshards, shard_lens, present, 0, byte_cnt_in_shard);
     if (rc) return rc;

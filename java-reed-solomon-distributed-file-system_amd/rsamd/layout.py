@@ -93,6 +93,19 @@ class ReedSolomonEncoder:
         return self._padded // self._block - 1
 
 
+def file_decode_into(codec: ReedSolomon, shards: Sequence, shardPresent: Sequence, byteCntInShard: int,
+                     file_out: np.ndarray, block: int = BLOCK_SIZE) -> None:
+    """ReedSolomonDecoder's work into a caller-owned uint8 buffer of fileSize =
+    len(file_out) bytes: absent shards filled in place, data merged and trimmed
+    (rs_file_decode; no per-call host allocation)."""
+    if not (isinstance(file_out, np.ndarray) and file_out.dtype == np.uint8 and file_out.flags.c_contiguous):
+        raise TypeError("file_out must be a C-contiguous uint8 numpy array")
+    b = _Buffers(shards)
+    p = _bools(shardPresent)
+    check(_lib.load().rs_file_decode(codec.handle, b.ptrs, len(shards), b.lens, p.ctypes.data_as(_lib.u8p),
+                                     byteCntInShard, block, file_out.ctypes.data_as(_lib.u8p), len(file_out)))
+
+
 class ReedSolomonDecoder:
     """client/ReedSolomonDecoder.java, the shards constructor (:33-39):
     decodeMissing fills the absent shards IN PLACE (as the Java does), then the
