@@ -111,9 +111,9 @@ def main():
         extra = device_extras(torch, rs, rdev, buf, lay, stream, k, m, S, B)
         del buf
         torch.cuda.empty_cache()
-        extra.update(other_configs(torch, rsamd, rdev, dev, stream))
-        extra.update(layout_legs(torch, rsamd, dev, stream))
-        if world == 1:
+        if world == 1:  # multi-GPU runs report the scaling line only (the other ranks wait)
+            extra.update(other_configs(torch, rsamd, rdev, dev, stream))
+            extra.update(layout_legs(torch, rsamd, dev, stream))
             cpu = cpu_baseline(k, m, S, args.cpu_seconds)
             extra.update(host_inclusive(rsamd, k, m))
     traffic = pmc_traffic(k, m, S, B)

@@ -142,8 +142,30 @@ int grow(uint8_t **buf, size_t *cap, size_t want) {
 constexpr size_t kChunk = size_t(32) << 20;
 constexpr size_t kMinChunk = size_t(4) << 20;
 
-// Bytes per shard per chunk: about 8 chunks per call, within [4, 32] MiB.
-size_t chunk_bytes(size_t total) { return std::min(kChunk, std::max(kMinChunk, (total / 8 + 255) / 256 * 256)); }
+// Bytes per shard per chunk.  Pinned host buffers: about 8 chunks per call,
+// within [4, 32] MiB, so little of the first H2D and the last D2H is exposed.
+// Pageable buffers: kChunk -- the runtime stages pageable copies through one
+// path (55.9 GB/s for both directions together, even from two host threads;
+// tools/pcie_probe.py), so there is no duplex to win and fewer, larger copies
+// cost less (34 vs 31 GiB/s for 4+2 x 64 MiB).
+size_t chunk_bytes(size_t total, bool pinned) {
+    if (!pinned) return kChunk;
+    return std::min(kChunk, std::max(kMinChunk, (total / 8 + 255) / 256 * 256));
+}
+
+// True when every non-null pointer is page-locked host memory known to HIP.
+bool all_pinned(const uint8_t *const *ptrs, int n) {
+    for (int i = 0; i < n; ++i) {
+        if (!ptrs[i]) continue;
+        hipPointerAttribute_t attr;
+        if (hipPointerGetAttributes(&attr, ptrs[i]) != hipSuccess) {
+            (void)hipGetLastError();  // pageable memory: clear the sticky error
+            return false;
+        }
+        if (attr.type != hipMemoryTypeHost) return false;
+    }
+    return true;
+}
 
 size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -190,7 +212,7 @@ int run_host(const std::vector<DevPlan> &plans, int nslots, const std::vector<in
     ThreadCtx *ctx = nullptr;
     int rc = thread_ctx(&ctx);
     if (rc) return rc;
-    const size_t chunk = std::min(count, chunk_bytes(count));
+    const size_t chunk = std::min(count, chunk_bytes(count, all_pinned(host, nslots)));
     const size_t slot_stride = round_up(std::max<size_t>(chunk, 1), 256);
     const size_t buf_bytes = slot_stride * size_t(nslots);
     const Pipeline pl{ctx, n_bufs((count + chunk - 1) / chunk)};
@@ -420,10 +442,10 @@ struct FileChunks {
     int nbuf = 1;
 };
 
-FileChunks file_chunks(int k, int total, size_t S, size_t block) {
+FileChunks file_chunks(int k, int total, size_t S, size_t block, bool pinned) {
     FileChunks f;
     f.rows = S / block;
-    f.R = std::min(f.rows, std::max<size_t>(1, chunk_bytes(S * size_t(k)) / (size_t(k) * block)));
+    f.R = std::min(f.rows, std::max<size_t>(1, chunk_bytes(S * size_t(k), pinned) / (size_t(k) * block)));
     f.nbuf = n_bufs((f.rows + f.R - 1) / f.R);
     f.fbytes = round_up(f.R * size_t(k) * block, 256);
     f.sstride = round_up(f.R * block, 256);
@@ -459,7 +481,9 @@ int file_decode_chunked(const Codec &c, uint8_t *const *shards, const int64_t *l
     rc = thread_ctx(&ctx);
     if (rc) return rc;
     const size_t blk = size_t(block);
-    const FileChunks f = file_chunks(k, T, size_t(S), blk);
+    std::vector<const uint8_t *> bufs(shards, shards + T);
+    bufs.push_back(file_out);
+    const FileChunks f = file_chunks(k, T, size_t(S), blk, all_pinned(bufs.data(), int(bufs.size())));
     rc = grow(&ctx->file, &ctx->file_cap, f.buf_bytes * size_t(f.nbuf));
     if (rc) return rc;
     const Pipeline pl{ctx, f.nbuf};
@@ -910,7 +934,9 @@ int rs_file_encode(const rs_codec *codec, const uint8_t *file, int64_t file_len,
     rc = thread_ctx(&ctx);
     if (rc) return rc;
     const size_t k = size_t(c->k()), blk = size_t(block);
-    const FileChunks f = file_chunks(c->k(), c->total(), size_t(S), blk);
+    std::vector<const uint8_t *> bufs(shards_out, shards_out + nshards);
+    bufs.push_back(file);
+    const FileChunks f = file_chunks(c->k(), c->total(), size_t(S), blk, all_pinned(bufs.data(), int(bufs.size())));
     rc = grow(&ctx->file, &ctx->file_cap, f.buf_bytes * size_t(f.nbuf));
     if (rc) return rc;
     const Pipeline pl{ctx, f.nbuf};

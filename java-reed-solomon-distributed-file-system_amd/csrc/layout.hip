@@ -389,6 +389,125 @@ __global__ void __launch_bounds__(kTileThreads) file_decode_tiled_kernel(TileArg
 }
 
 // ---------------------------------------------------------------------------
+// Tiled file encode, the mirror image of the tiled decode.  A 256-thread
+// workgroup owns R whole block rows.  Phase 1: the tile's file bytes -- ONE
+// contiguous run [r0*K*block, (r0+R)*K*block), zero past the file end (the
+// padding) -- come in as aligned 16-byte loads, all issued up front, and land
+// in LDS unchanged.  Phase 2: each thread gathers the K data shards' 16-byte
+// column vectors from LDS (two 8-byte reads each: a vector may straddle two
+// blocks when block % 16 == 8), computes the M parity vectors and stores all
+// K + M with 16-byte non-temporal stores.  This replaces file_encode_kernel's
+// 8-byte file loads, which fetch 1.2x the file at block 1000
+// (profiles/r1/file_decode_ab/).  Needs a 16-byte aligned file.  Opt-in
+// (RSAMD_FILE_ENCODE=1): not faster than file_encode_kernel on MI355X.
+// ---------------------------------------------------------------------------
+struct EncTileArgs {
+    const uint8_t *file;
+    uint64_t file_len;
+    uint8_t *shards;
+    uint64_t shard_stride;
+    uint64_t n_rows;
+    uint32_t block;
+    uint32_t rows;
+    uint32_t inv_block;
+    const uint32_t *tabs;  // [K][M][5]
+};
+
+template <int K, int M>
+__global__ void __launch_bounds__(kTileThreads) file_encode_tiled_kernel(EncTileArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
+    const uint64_t r0 = uint64_t(blockIdx.x) * a.rows;
+    const uint32_t rows = uint32_t(min(uint64_t(a.rows), a.n_rows - r0));
+    const uint32_t span = rows * a.block;
+    const uint32_t kblock = uint32_t(K) * a.block;
+    const uint32_t run = rows * kblock;  // a multiple of 16 (rows even, or the file's last tile)
+    const uint64_t f0 = r0 * kblock;
+    uint32_t T[M > 0 ? M : 1][K][5];
+#pragma unroll
+    for (int p = 0; p < M; ++p)
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+#pragma unroll
+            for (int j = 0; j < 5; ++j) T[p][i][j] = a.tabs[(i * M + p) * 5 + j];
+
+    // Phase 1: run <= kTileSlots * 256 * 16 * K bytes, so 2K loads per thread.
+    constexpr int NL = kTileSlots * K;
+    u32x4 v[NL];
+#pragma unroll
+    for (int u = 0; u < NL; ++u) {
+        const uint32_t t = (u * kTileThreads + threadIdx.x) * 16;
+        const uint64_t f = f0 + t;
+        v[u] = u32x4{0, 0, 0, 0};
+        if (t < run) {
+            if (f + 16 <= a.file_len) {
+                v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(a.file + f));
+            } else if (f < a.file_len) {
+                uint32_t w[4] = {0, 0, 0, 0};
+                for (uint64_t b = f; b < a.file_len; ++b) w[(b - f) / 4] |= uint32_t(a.file[b]) << (8 * ((b - f) % 4));
+                v[u] = u32x4{w[0], w[1], w[2], w[3]};
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < NL; ++u) {
+        const uint32_t t = (u * kTileThreads + threadIdx.x) * 16;
+        if (t < run) *reinterpret_cast<u32x4 *>(tile + t) = v[u];
+    }
+    __syncthreads();
+
+    // Phase 2: columns c of the tile's span, kTileSlots vectors per thread.
+    const uint64_t col0 = r0 * a.block;
+#pragma unroll
+    for (int u = 0; u < kTileSlots; ++u) {
+        const uint32_t c = (u * kTileThreads + threadIdx.x) * 16;
+        if (c >= span) continue;
+        const bool hi = c + 16 <= span;  // else only the 8-byte half [c, c+8) exists
+        u32x4 x[K];
+        uint32_t lo_off, hi_off;  // LDS offsets of data shard 0's two halves
+        {
+            const uint32_t r = div_small(c, a.inv_block);
+            lo_off = r * kblock + (c - r * a.block);
+            const uint32_t c8 = c + 8;
+            const uint32_t r8 = div_small(c8, a.inv_block);
+            hi_off = r8 * kblock + (c8 - r8 * a.block);
+        }
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            const u32x2 l = *reinterpret_cast<const u32x2 *>(tile + lo_off + i * a.block);
+            const u32x2 h = hi ? *reinterpret_cast<const u32x2 *>(tile + hi_off + i * a.block) : u32x2{0, 0};
+            x[i] = u32x4{l[0], l[1], h[0], h[1]};
+        }
+        uint8_t *col = a.shards + col0 + c;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            uint8_t *dst = col + uint64_t(i) * a.shard_stride;
+            if (hi)
+                __builtin_nontemporal_store(x[i], reinterpret_cast<u32x4 *>(dst));
+            else
+                __builtin_nontemporal_store(u32x2{x[i][0], x[i][1]}, reinterpret_cast<u32x2 *>(dst));
+        }
+        if (M == 0) continue;
+        u32x4 acc[M > 0 ? M : 1];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            Sel sl[K];
+#pragma unroll
+            for (int i = 0; i < K; ++i) sl[i] = selectors(x[i][w]);
+#pragma unroll
+            for (int p = 0; p < M; ++p) acc[p][w] = dot_dword<K>(T[p], sl);
+        }
+#pragma unroll
+        for (int p = 0; p < M; ++p) {
+            uint8_t *dst = col + uint64_t(K + p) * a.shard_stride;
+            if (hi)
+                __builtin_nontemporal_store(acc[p], reinterpret_cast<u32x4 *>(dst));
+            else
+                __builtin_nontemporal_store(u32x2{acc[p][0], acc[p][1]}, reinterpret_cast<u32x2 *>(dst));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Generic split (file -> k data shards) and merge (k data shards -> file):
 // one thread per W-byte word of one shard, W = 8 when block % 8 == 0 and the
 // buffers are 8-aligned, else 1.
@@ -489,20 +608,6 @@ bool file_fusable(const FileGeom &g, bool encode) {
            (g.S + 15) / 16 <= uint64_t(INT32_MAX) * kWave;
 }
 
-hipError_t launch_file_encode_fused(const FileGeom &g, const DevPlan *parity0, hipStream_t s) {
-    if (g.S == 0) return hipSuccess;
-    FileArgs a{g.file, nullptr, g.file_len, g.shards, g.shard_stride, g.S, uint32_t(g.block),
-               uint32_t((g.S + 15) / 16), parity0 ? parity0->tabs : nullptr, nullptr, nullptr};
-    const int m = parity0 ? parity0->nout : 0;
-    switch (m) {
-    case 0: return launch_enc_t<4, 0>(a, s);
-    case 1: return launch_enc_t<4, 1>(a, s);
-    case 2: return launch_enc_t<4, 2>(a, s);
-    case 3: return launch_enc_t<4, 3>(a, s);
-    case 4: return launch_enc_t<4, 4>(a, s);
-    }
-    return hipErrorInvalidValue;
-}
 
 namespace {
 
@@ -511,6 +616,13 @@ hipError_t launch_tiled_t(const TileArgs &a, uint64_t tiles, hipStream_t s) {
     const size_t lds = size_t(K) * a.rows * a.block;
     hipLaunchKernelGGL((file_decode_tiled_kernel<K, E>), dim3(unsigned(tiles)), dim3(kTileThreads), lds, s,
                        a);
+    return hipGetLastError();
+}
+
+template <int K, int M>
+hipError_t launch_enc_tiled_t(const EncTileArgs &a, uint64_t tiles, hipStream_t s) {
+    const size_t lds = size_t(K) * a.rows * a.block;
+    hipLaunchKernelGGL((file_encode_tiled_kernel<K, M>), dim3(unsigned(tiles)), dim3(kTileThreads), lds, s, a);
     return hipGetLastError();
 }
 
@@ -524,6 +636,40 @@ uint32_t tile_rows(const FileGeom &g) {
 }
 
 }  // namespace
+
+hipError_t launch_file_encode_fused(const FileGeom &g, const DevPlan *parity0, hipStream_t s) {
+    if (g.S == 0) return hipSuccess;
+    // The untiled kernel is the default: the tiled one has ideal traffic
+    // (1.00x vs 1.2x file reads at block 1000) but measured 0.67-0.78 of peak
+    // against 0.72-0.78 across boxes (profiles/r1/file_decode_ab/).
+    // RSAMD_FILE_ENCODE=1 selects it (A/B).
+    const char *mode = std::getenv("RSAMD_FILE_ENCODE");
+    const uint32_t R = tile_rows(g);
+    if (R && aligned(g.file, 16) && mode && mode[0] == '1') {
+        EncTileArgs a{g.file, g.file_len, g.shards, g.shard_stride, g.S / g.block, uint32_t(g.block), R,
+                      uint32_t((uint64_t(1) << 32) / g.block + 1), parity0 ? parity0->tabs : nullptr};
+        const uint64_t tiles = (a.n_rows + R - 1) / R;
+        switch (parity0 ? parity0->nout : 0) {
+        case 0: return launch_enc_tiled_t<4, 0>(a, tiles, s);
+        case 1: return launch_enc_tiled_t<4, 1>(a, tiles, s);
+        case 2: return launch_enc_tiled_t<4, 2>(a, tiles, s);
+        case 3: return launch_enc_tiled_t<4, 3>(a, tiles, s);
+        case 4: return launch_enc_tiled_t<4, 4>(a, tiles, s);
+        }
+        return hipErrorInvalidValue;
+    }
+    FileArgs a{g.file, nullptr, g.file_len, g.shards, g.shard_stride, g.S, uint32_t(g.block),
+               uint32_t((g.S + 15) / 16), parity0 ? parity0->tabs : nullptr, nullptr, nullptr};
+    const int m = parity0 ? parity0->nout : 0;
+    switch (m) {
+    case 0: return launch_enc_t<4, 0>(a, s);
+    case 1: return launch_enc_t<4, 1>(a, s);
+    case 2: return launch_enc_t<4, 2>(a, s);
+    case 3: return launch_enc_t<4, 3>(a, s);
+    case 4: return launch_enc_t<4, 4>(a, s);
+    }
+    return hipErrorInvalidValue;
+}
 
 hipError_t launch_file_decode_fused(const FileGeom &g, const FileDecodePlan &p, hipStream_t s) {
     if (g.S == 0 || g.file_len == 0) return hipSuccess;
