@@ -203,3 +203,38 @@ def test_presence_bits_helper():
     p = np.array([[1, 1, 1, 1, 0, 0], [0, 1, 1, 1, 1, 1], [1] * 6], dtype=bool)
     assert presence_bits(p).tolist() == [0b001111, 0b111110, 0b111111]
     assert presence_bits(p).dtype == np.uint32
+
+
+def test_kernels_use_no_scratch(native, tmp_path):
+    """Every gfx950 kernel in librsamd.so has a private segment of 0 and no
+    VGPR spills: a run-time index into a register array (or a VGPR spill)
+    sends vectors through scratch memory and doubles HBM traffic (DESIGN.md
+    3.4).  SGPR spills (the E/M = 3, 4 layout variants) go to VGPR lanes, not
+    memory.  Reads the code object's AMDGPU metadata notes."""
+    import shutil
+    import subprocess
+    llvm = "/opt/rocm/lib/llvm/bin"
+    if not os.path.exists(os.path.join(llvm, "llvm-readelf")):
+        pytest.skip("ROCm llvm tools not installed")
+    lib = os.path.join(ROOT, "java-reed-solomon-distributed-file-system_amd", "lib", "librsamd.so")
+    so = tmp_path / "librsamd.so"
+    shutil.copy(lib, so)
+    subprocess.run([os.path.join(llvm, "llvm-objdump"), "--offloading", str(so)], check=True, cwd=tmp_path,
+                   stdout=subprocess.DEVNULL)
+    objs = sorted(tmp_path.glob("librsamd.so.*gfx950"))
+    assert objs, "no gfx950 code object in librsamd.so"
+    kernels = {}
+    for o in objs:
+        notes = subprocess.run([os.path.join(llvm, "llvm-readelf"), "--notes", str(o)], check=True,
+                               capture_output=True, text=True).stdout
+        name = None
+        for line in notes.splitlines():
+            line = line.strip()
+            if line.startswith(".name:"):
+                name = line.split(":", 1)[1].strip()
+                kernels.setdefault(name, {})
+            elif name and line.split(":")[0] in (".private_segment_fixed_size", ".vgpr_spill_count"):
+                kernels[name][line.split(":")[0]] = int(line.split(":", 1)[1])
+    assert len(kernels) > 40
+    bad = {k: v for k, v in kernels.items() if any(v.values())}
+    assert not bad, bad
