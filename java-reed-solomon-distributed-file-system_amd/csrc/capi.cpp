@@ -10,6 +10,8 @@
 #include <climits>
 #include <cstdio>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <map>
 #include <memory>
 #include <string>
@@ -18,6 +20,7 @@
 
 #include "../../include/rs_amd.h"
 #include "codec.hpp"
+#include "copy_pool.hpp"
 #include "gf256.hpp"
 #include "kernels.hpp"
 #include "layout.hpp"
@@ -75,10 +78,13 @@ struct ThreadCtx {
     hipStream_t stream = nullptr;   // host pipeline: H2D copies + kernels, in chunk order
     hipStream_t stream2 = nullptr;  // host pipeline: D2H copies, in chunk order
     hipEvent_t ready = nullptr;     // joins stream2 back into stream
-    hipEvent_t coded[kStageBufs] = {};  // buffer b's kernels done (stream -> stream2)
-    hipEvent_t freed[kStageBufs] = {};  // buffer b's D2H done (stream2 -> stream)
-    uint8_t *stage = nullptr;       // kStageBufs x nslots x slot_stride device bytes
+    hipEvent_t coded[kStageBufs] = {};   // buffer b's kernels done (stream -> stream2)
+    hipEvent_t freed[kStageBufs] = {};   // buffer b's D2H done (stream2 -> stream, and the host)
+    hipEvent_t loaded[kStageBufs] = {};  // buffer b's H2D done (its pinned mirror may be refilled)
+    uint8_t *stage = nullptr;       // kStageBufs device staging buffers
     size_t stage_cap = 0;
+    uint8_t *mirror = nullptr;      // their pinned host mirrors (pageable callers only)
+    size_t mirror_cap = 0;
     uint8_t *plan = nullptr;   // per-call plan images (rs_code_some_shards)
     size_t plan_cap = 0;
     int *flag = nullptr;       // verify result
@@ -110,6 +116,7 @@ int thread_ctx(ThreadCtx **out) {
         for (int b = 0; b < kStageBufs && e == hipSuccess; ++b) {
             e = hipEventCreateWithFlags(&c->coded[b], hipEventDisableTiming);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&c->freed[b], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&c->loaded[b], hipEventDisableTiming);
         }
         if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&c->flag), 256);
         if (e != hipSuccess) {
@@ -132,25 +139,42 @@ int grow(uint8_t **buf, size_t *cap, size_t want) {
     return RS_OK;
 }
 
-// Host-buffer pipeline.  A call is cut into chunks staged through
-// kStageBufs device buffers.  `stream` carries every H2D copy and kernel in
-// chunk order, `stream2` every D2H copy in chunk order: chunk j's D2H runs
-// beside chunk j+1's H2D (pinned copies measured 57 GB/s one way, 97 GB/s
-// both ways on MI355X; two streams each doing H2D-kernel-D2H fall into
-// lockstep and never overlap the directions).  Events hand each buffer from
-// the kernels to its D2H and back to the next H2D that reuses it.
-constexpr size_t kChunk = size_t(32) << 20;
-constexpr size_t kMinChunk = size_t(4) << 20;
+int grow_pinned(uint8_t **buf, size_t *cap, size_t want) {
+    if (*cap >= want) return RS_OK;
+    if (*buf) RS_HIP(hipHostFree(*buf));
+    *buf = nullptr;
+    *cap = 0;
+    RS_HIP(hipHostMalloc(reinterpret_cast<void **>(buf), want, hipHostMallocDefault));
+    *cap = want;
+    return RS_OK;
+}
 
-// Bytes per shard per chunk.  Pinned host buffers: about 8 chunks per call,
-// within [4, 32] MiB, so little of the first H2D and the last D2H is exposed.
-// Pageable buffers: kChunk -- the runtime stages pageable copies through one
-// path (55.9 GB/s for both directions together, even from two host threads;
-// tools/pcie_probe.py), so there is no duplex to win and fewer, larger copies
-// cost less (34 vs 31 GiB/s for 4+2 x 64 MiB).
-size_t chunk_bytes(size_t total, bool pinned) {
-    if (!pinned) return kChunk;
-    return std::min(kChunk, std::max(kMinChunk, (total / 8 + 255) / 256 * 256));
+// ---------------------------------------------------------------------------
+// Host-buffer pipeline.  A call is cut into chunks staged through kStageBufs
+// device buffers.  `stream` carries every H2D copy and kernel in chunk order,
+// `stream2` every D2H copy in chunk order, so chunk j's D2H runs beside chunk
+// j+1's H2D; events hand each buffer from its kernels to its D2H and back to
+// the H2D that reuses it.  (Two streams that each ran H2D -> kernel -> D2H
+// fell into lockstep and never overlapped the directions.)
+//
+// The link is full duplex only for async copies from page-locked memory
+// (57 GB/s one way, 97 GB/s both ways; pageable copies share one staged path
+// at 56 GB/s in total, even from two host threads -- tools/pcie_probe.py).
+// Pinned callers are copied directly.  Pageable callers (JNI arrays) go
+// through a pinned mirror of each staging buffer: the pool of copy_pool.hpp
+// fills chunk j's inputs into the mirror while the GPU moves chunk j-1, and
+// drains chunk j-1's outputs once their D2H is done.
+// ---------------------------------------------------------------------------
+constexpr size_t kChunk = size_t(32) << 20;        // max bytes per slot per chunk
+constexpr size_t kMinChunk = size_t(4) << 20;      // min bytes per slot per chunk (~8 chunks per call)
+constexpr size_t kMirrorBytes = size_t(24) << 20;  // pinned mirror bytes per staging buffer
+
+// Bytes per slot per chunk for a call of `total` bytes per slot and `nslots`
+// slots per buffer.
+size_t chunk_bytes(size_t total, int nslots, bool pinned) {
+    size_t c = std::max(kMinChunk, (total / 8 + 255) / 256 * 256);
+    if (!pinned) c = std::min(c, std::max<size_t>(size_t(1) << 20, kMirrorBytes / size_t(std::max(1, nslots))));
+    return std::min(kChunk, c);
 }
 
 // True when every non-null pointer is page-locked host memory known to HIP.
@@ -169,37 +193,89 @@ bool all_pinned(const uint8_t *const *ptrs, int n) {
 
 size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-struct Pipeline {
-    ThreadCtx *ctx;
-    int nbuf;  // staging buffers in use (1 .. kStageBufs)
-    // Before chunk j's H2D: its buffer's previous D2H must be done.
-    int begin(size_t j) const {
-        if (j >= size_t(nbuf)) RS_HIP(hipStreamWaitEvent(ctx->stream, ctx->freed[j % nbuf], 0));
-        return RS_OK;
-    }
-    // After chunk j's kernels: D2H copies issued on out() follow them.
-    int coded(size_t j) const {
-        RS_HIP(hipEventRecord(ctx->coded[j % nbuf], ctx->stream));
-        RS_HIP(hipStreamWaitEvent(ctx->stream2, ctx->coded[j % nbuf], 0));
-        return RS_OK;
-    }
-    // After chunk j's D2H copies.
-    int done(size_t j) const {
-        RS_HIP(hipEventRecord(ctx->freed[j % nbuf], ctx->stream2));
-        return RS_OK;
-    }
-    hipStream_t in() const { return ctx->stream; }
-    hipStream_t out() const { return ctx->stream2; }
-    // stream waits for everything on stream2, then the host waits for stream.
-    int finish() const {
-        RS_HIP(hipEventRecord(ctx->ready, ctx->stream2));
-        RS_HIP(hipStreamWaitEvent(ctx->stream, ctx->ready, 0));
-        RS_HIP(hipStreamSynchronize(ctx->stream));
-        return RS_OK;
-    }
-};
-
 int n_bufs(size_t n_chunks) { return int(std::min<size_t>(kStageBufs, std::max<size_t>(1, n_chunks))); }
+
+// One host <-> device transfer of a chunk: host bytes [host, host + n) and
+// bytes [off, off + n) of the chunk's staging buffer.
+struct Xfer {
+    uint8_t *host;
+    size_t off;
+    size_t n;
+};
+using ChunkIo = std::function<void(size_t j, std::vector<Xfer> *in, std::vector<Xfer> *out)>;
+using ChunkCode = std::function<int(size_t j, uint8_t *buf, hipStream_t s)>;
+
+// Runs n_chunks chunks of buf_bytes each: io(j) names chunk j's inputs and
+// outputs, code(j) enqueues its kernels on the given stream.  Returns once
+// every output has reached host memory.
+int run_chunks(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinned, const ChunkIo &io,
+               const ChunkCode &code) {
+    const int nbuf = n_bufs(n_chunks);
+    int rc = grow(&ctx->stage, &ctx->stage_cap, buf_bytes * size_t(nbuf));
+    if (rc) return rc;
+    const bool staged = !pinned;
+    if (staged) {
+        rc = grow_pinned(&ctx->mirror, &ctx->mirror_cap, buf_bytes * size_t(nbuf));
+        if (rc) return rc;
+    }
+    hipStream_t in_s = ctx->stream, out_s = ctx->stream2;
+    rsamd::CopyPool &pool = rsamd::CopyPool::get();
+    // Staged outputs are drained nbuf - 1 chunks behind (their D2H is long
+    // done by then), in the same pool batch as the next chunk's inputs.  A
+    // mirror's output bytes are drained before the D2H that reuses it is issued.
+    const size_t lag = size_t(std::max(1, nbuf - 1));
+    std::deque<std::pair<size_t, std::vector<Xfer>>> pending;
+    std::vector<Xfer> in, out;
+    std::vector<rsamd::CopyJob> jobs;
+    auto queue_drain = [&]() -> int {  // the oldest pending chunk: mirror -> caller
+        const size_t pj = pending.front().first;
+        RS_HIP(hipEventSynchronize(ctx->freed[pj % nbuf]));
+        const uint8_t *mir = ctx->mirror + (pj % nbuf) * buf_bytes;
+        for (const Xfer &x : pending.front().second) jobs.push_back({x.host, mir + x.off, x.n});
+        pending.pop_front();
+        return RS_OK;
+    };
+    for (size_t j = 0; j < n_chunks; ++j) {
+        const size_t b = j % nbuf;
+        uint8_t *dev = ctx->stage + b * buf_bytes;
+        uint8_t *mir = staged ? ctx->mirror + b * buf_bytes : nullptr;
+        in.clear();
+        out.clear();
+        io(j, &in, &out);
+        if (staged) {
+            jobs.clear();
+            if (pending.size() >= lag) {
+                rc = queue_drain();
+                if (rc) return rc;
+            }
+            if (j >= size_t(nbuf)) RS_HIP(hipEventSynchronize(ctx->loaded[b]));  // chunk j - nbuf's H2D done
+            for (const Xfer &x : in) jobs.push_back({mir + x.off, x.host, x.n});
+            pool.copy(jobs);
+        }
+        if (j >= size_t(nbuf)) RS_HIP(hipStreamWaitEvent(in_s, ctx->freed[b], 0));  // device buffer free
+        for (const Xfer &x : in)
+            RS_HIP(hipMemcpyAsync(dev + x.off, staged ? mir + x.off : x.host, x.n, hipMemcpyHostToDevice, in_s));
+        if (staged) RS_HIP(hipEventRecord(ctx->loaded[b], in_s));
+        rc = code(j, dev, in_s);
+        if (rc) return rc;
+        RS_HIP(hipEventRecord(ctx->coded[b], in_s));
+        RS_HIP(hipStreamWaitEvent(out_s, ctx->coded[b], 0));
+        for (const Xfer &x : out)
+            RS_HIP(hipMemcpyAsync(staged ? mir + x.off : x.host, dev + x.off, x.n, hipMemcpyDeviceToHost, out_s));
+        RS_HIP(hipEventRecord(ctx->freed[b], out_s));
+        if (staged && !out.empty()) pending.emplace_back(j, out);
+    }
+    while (!pending.empty()) {
+        jobs.clear();
+        rc = queue_drain();
+        if (rc) return rc;
+        pool.copy(jobs);
+    }
+    RS_HIP(hipEventRecord(ctx->ready, out_s));
+    RS_HIP(hipStreamWaitEvent(in_s, ctx->ready, 0));
+    RS_HIP(hipStreamSynchronize(in_s));
+    return RS_OK;
+}
 
 // Stage [offset, offset+count) of the host shards (slot-indexed), run every
 // launch group of `plans`, copy results back.
@@ -212,48 +288,35 @@ int run_host(const std::vector<DevPlan> &plans, int nslots, const std::vector<in
     ThreadCtx *ctx = nullptr;
     int rc = thread_ctx(&ctx);
     if (rc) return rc;
-    const size_t chunk = std::min(count, chunk_bytes(count, all_pinned(host, nslots)));
+    const bool pinned = all_pinned(host, nslots);
+    const size_t chunk = std::min(count, chunk_bytes(count, nslots, pinned));
     const size_t slot_stride = round_up(std::max<size_t>(chunk, 1), 256);
-    const size_t buf_bytes = slot_stride * size_t(nslots);
-    const Pipeline pl{ctx, n_bufs((count + chunk - 1) / chunk)};
-    rc = grow(&ctx->stage, &ctx->stage_cap, buf_bytes * size_t(pl.nbuf));
-    if (rc) return rc;
-    if (mode == Mode::Verify) RS_HIP(hipMemsetAsync(ctx->flag, 0, sizeof(int), pl.in()));
-    size_t j = 0;
-    for (size_t done = 0; done < count; done += chunk, ++j) {
-        const size_t n = std::min(chunk, count - done);
-        uint8_t *stage = ctx->stage + (j % pl.nbuf) * buf_bytes;
-        rc = pl.begin(j);
-        if (rc) return rc;
-        for (int s : in_slots)
-            RS_HIP(hipMemcpyAsync(stage + size_t(s) * slot_stride, host[s] + offset + done, n, hipMemcpyHostToDevice,
-                                  pl.in()));
+    if (mode == Mode::Verify) RS_HIP(hipMemsetAsync(ctx->flag, 0, sizeof(int), ctx->stream));
+    auto io = [&](size_t j, std::vector<Xfer> *in, std::vector<Xfer> *out) {
+        const size_t done = j * chunk, n = std::min(chunk, count - done);
+        for (int s : in_slots) in->push_back({host[s] + offset + done, size_t(s) * slot_stride, n});
+        if (mode == Mode::Code)
+            for (int s : out_slots) out->push_back({host[s] + offset + done, size_t(s) * slot_stride, n});
+    };
+    auto code = [&](size_t j, uint8_t *buf, hipStream_t st) -> int {
         Geometry g;
-        g.base = stage;
+        g.base = buf;
         g.n_stripes = 1;
         g.col0 = 0;
-        g.len = n;
+        g.len = std::min(chunk, count - j * chunk);
         g.shard_stride = slot_stride;
-        g.stripe_stride = buf_bytes;
-        for (const DevPlan &p : plans) RS_HIP(rsamd::launch_gf(g, p, mode, ctx->flag, pl.in()));
-        if (mode == Mode::Code) {
-            rc = pl.coded(j);
-            if (rc) return rc;
-            for (int s : out_slots)
-                RS_HIP(hipMemcpyAsync(host[s] + offset + done, stage + size_t(s) * slot_stride, n,
-                                      hipMemcpyDeviceToHost, pl.out()));
-            rc = pl.done(j);
-            if (rc) return rc;
-        }
-    }
+        g.stripe_stride = slot_stride * size_t(nslots);
+        for (const DevPlan &p : plans) RS_HIP(rsamd::launch_gf(g, p, mode, ctx->flag, st));
+        return RS_OK;
+    };
+    rc = run_chunks(ctx, (count + chunk - 1) / chunk, slot_stride * size_t(nslots), pinned, io, code);
+    if (rc) return rc;
     if (mode == Mode::Verify) {
         int h = 0;
-        RS_HIP(hipMemcpyAsync(&h, ctx->flag, sizeof(int), hipMemcpyDeviceToHost, pl.in()));
-        RS_HIP(hipStreamSynchronize(pl.in()));
+        RS_HIP(hipMemcpy(&h, ctx->flag, sizeof(int), hipMemcpyDeviceToHost));
         *result = h ? 0 : 1;
-        return RS_OK;
     }
-    return pl.finish();
+    return RS_OK;
 }
 
 // ReedSolomon.checkBuffersAndSizes (ReedSolomon.java:277-302), same order and text.
@@ -430,23 +493,22 @@ int file_decode_dev(const Codec &c, uint8_t *shards, size_t S, size_t stride, co
 }
 
 
-// Host file paths (rs_file_encode / rs_file_decode): block rows staged
-// through two device halves on two streams, chunk_bytes() of file per
-// chunk, so chunk j's copies overlap chunk j+1's and each pageable copy is a
-// chunk (whole-file pageable copies measured ~5x slower than PCIe rate).
-
+// Host file paths (rs_file_encode / rs_file_decode): whole block rows per
+// chunk through run_chunks, each staging buffer laid out as [file bytes of
+// the rows][shard 0 .. total-1 columns of the rows].  (Whole-file pageable
+// copies ran ~5x below PCIe rate.)
 struct FileChunks {
-    size_t R = 0, rows = 0;          // block rows per chunk, rows in all
+    size_t R = 0, rows = 0, n = 0;   // block rows per chunk, rows in all, chunks
     size_t fbytes = 0, sstride = 0;  // staged file bytes and shard stride per buffer
     size_t buf_bytes = 0;
-    int nbuf = 1;
 };
 
 FileChunks file_chunks(int k, int total, size_t S, size_t block, bool pinned) {
     FileChunks f;
     f.rows = S / block;
-    f.R = std::min(f.rows, std::max<size_t>(1, chunk_bytes(S * size_t(k), pinned) / (size_t(k) * block)));
-    f.nbuf = n_bufs((f.rows + f.R - 1) / f.R);
+    const size_t per_shard = chunk_bytes(S, k + total, pinned);
+    f.R = std::min(f.rows, std::max<size_t>(1, per_shard / block));
+    f.n = (f.rows + f.R - 1) / f.R;
     f.fbytes = round_up(f.R * size_t(k) * block, 256);
     f.sstride = round_up(f.R * block, 256);
     f.buf_bytes = f.fbytes + f.sstride * size_t(total);
@@ -480,42 +542,35 @@ int file_decode_chunked(const Codec &c, uint8_t *const *shards, const int64_t *l
     ThreadCtx *ctx = nullptr;
     rc = thread_ctx(&ctx);
     if (rc) return rc;
-    const size_t blk = size_t(block);
+    const size_t blk = size_t(block), kb = size_t(k) * blk;
     std::vector<const uint8_t *> bufs(shards, shards + T);
     bufs.push_back(file_out);
-    const FileChunks f = file_chunks(k, T, size_t(S), blk, all_pinned(bufs.data(), int(bufs.size())));
-    rc = grow(&ctx->file, &ctx->file_cap, f.buf_bytes * size_t(f.nbuf));
-    if (rc) return rc;
-    const Pipeline pl{ctx, f.nbuf};
+    const bool pinned = all_pinned(bufs.data(), int(bufs.size()));
+    const FileChunks f = file_chunks(k, T, size_t(S), blk, pinned);
     std::vector<int> surv, missing;
     for (int i = 0; i < T; ++i) {
         if (present[i] && int(surv.size()) < k) surv.push_back(i);
         if (!present[i]) missing.push_back(i);
     }
-    for (size_t j = 0, r0 = 0; r0 < f.rows; ++j, r0 += f.R) {
-        const size_t rc_rows = std::min(f.R, f.rows - r0);
-        const size_t col0 = r0 * blk, n = rc_rows * blk;
-        const size_t fo = r0 * size_t(k) * blk;
-        const size_t flen = size_t(file_size) > fo ? std::min(rc_rows * size_t(k) * blk, size_t(file_size) - fo) : 0;
-        if (flen == 0 && missing.empty()) break;
-        uint8_t *dfile = ctx->file + (j % f.nbuf) * f.buf_bytes, *dsh = dfile + f.fbytes;
-        rc = pl.begin(j);
-        if (rc) return rc;
-        for (int sidx : surv)
-            RS_HIP(hipMemcpyAsync(dsh + size_t(sidx) * f.sstride, shards[sidx] + col0, n, hipMemcpyHostToDevice,
-                                  pl.in()));
-        rc = file_decode_dev(c, dsh, n, f.sstride, present, blk, dfile, flen, true, pl.in());
-        if (rc) return rc;
-        rc = pl.coded(j);
-        if (rc) return rc;
-        for (int sidx : missing)
-            RS_HIP(hipMemcpyAsync(shards[sidx] + col0, dsh + size_t(sidx) * f.sstride, n, hipMemcpyDeviceToHost,
-                                  pl.out()));
-        if (flen) RS_HIP(hipMemcpyAsync(file_out + fo, dfile, flen, hipMemcpyDeviceToHost, pl.out()));
-        rc = pl.done(j);
-        if (rc) return rc;
-    }
-    return pl.finish();
+    // Nothing to rebuild: only the rows holding file bytes are needed.
+    const size_t rows_needed = missing.empty() ? std::min(f.rows, (size_t(file_size) + kb - 1) / kb) : f.rows;
+    auto flen_of = [&](size_t r0, size_t rc_rows) {
+        const size_t fo = r0 * kb;
+        return size_t(file_size) > fo ? std::min(rc_rows * kb, size_t(file_size) - fo) : size_t(0);
+    };
+    auto io = [&](size_t j, std::vector<Xfer> *in, std::vector<Xfer> *out) {
+        const size_t r0 = j * f.R, rc_rows = std::min(f.R, f.rows - r0), n = rc_rows * blk;
+        for (int sidx : surv) in->push_back({shards[sidx] + r0 * blk, f.fbytes + size_t(sidx) * f.sstride, n});
+        for (int sidx : missing) out->push_back({shards[sidx] + r0 * blk, f.fbytes + size_t(sidx) * f.sstride, n});
+        const size_t flen = flen_of(r0, rc_rows);
+        if (flen) out->push_back({file_out + r0 * kb, 0, flen});
+    };
+    auto code = [&](size_t j, uint8_t *buf, hipStream_t st) -> int {
+        const size_t r0 = j * f.R, rc_rows = std::min(f.R, f.rows - r0);
+        return file_decode_dev(c, buf + f.fbytes, rc_rows * blk, f.sstride, present, blk, buf, flen_of(r0, rc_rows),
+                               true, st);
+    };
+    return run_chunks(ctx, (rows_needed + f.R - 1) / f.R, f.buf_bytes, pinned, io, code);
 }
 
 // Next staging slot of this thread with >= bytes on both sides, once the
@@ -749,7 +804,9 @@ void rs_thread_release(void) {
         for (int b = 0; b < kStageBufs; ++b) {
             if (c->coded[b]) (void)hipEventDestroy(c->coded[b]);
             if (c->freed[b]) (void)hipEventDestroy(c->freed[b]);
+            if (c->loaded[b]) (void)hipEventDestroy(c->loaded[b]);
         }
+        if (c->mirror) (void)hipHostFree(c->mirror);
         if (c->stage) (void)hipFree(c->stage);
         if (c->plan) (void)hipFree(c->plan);
         if (c->flag) (void)hipFree(c->flag);
@@ -936,29 +993,22 @@ int rs_file_encode(const rs_codec *codec, const uint8_t *file, int64_t file_len,
     const size_t k = size_t(c->k()), blk = size_t(block);
     std::vector<const uint8_t *> bufs(shards_out, shards_out + nshards);
     bufs.push_back(file);
-    const FileChunks f = file_chunks(c->k(), c->total(), size_t(S), blk, all_pinned(bufs.data(), int(bufs.size())));
-    rc = grow(&ctx->file, &ctx->file_cap, f.buf_bytes * size_t(f.nbuf));
-    if (rc) return rc;
-    const Pipeline pl{ctx, f.nbuf};
-    for (size_t j = 0, r0 = 0; r0 < f.rows; ++j, r0 += f.R) {
-        const size_t rc_rows = std::min(f.R, f.rows - r0);
-        const size_t off = r0 * k * blk;  // < file_len: every row holds file bytes
-        const size_t flen = std::min(rc_rows * k * blk, size_t(file_len) - off);
-        uint8_t *dfile = ctx->file + (j % f.nbuf) * f.buf_bytes, *dsh = dfile + f.fbytes;
-        rc = pl.begin(j);
-        if (rc) return rc;
-        RS_HIP(hipMemcpyAsync(dfile, file + off, flen, hipMemcpyHostToDevice, pl.in()));
-        rc = file_encode_dev(*c, dfile, flen, blk, dsh, f.sstride, pl.in());
-        if (rc) return rc;
-        rc = pl.coded(j);
-        if (rc) return rc;
+    const bool pinned = all_pinned(bufs.data(), int(bufs.size()));
+    const FileChunks f = file_chunks(c->k(), c->total(), size_t(S), blk, pinned);
+    auto flen_of = [&](size_t r0, size_t rc_rows) {  // every row holds file bytes
+        return std::min(rc_rows * k * blk, size_t(file_len) - r0 * k * blk);
+    };
+    auto io = [&](size_t j, std::vector<Xfer> *in, std::vector<Xfer> *out) {
+        const size_t r0 = j * f.R, rc_rows = std::min(f.R, f.rows - r0);
+        in->push_back({const_cast<uint8_t *>(file) + r0 * k * blk, 0, flen_of(r0, rc_rows)});
         for (int i = 0; i < c->total(); ++i)
-            RS_HIP(hipMemcpyAsync(shards_out[i] + r0 * blk, dsh + size_t(i) * f.sstride, rc_rows * blk,
-                                  hipMemcpyDeviceToHost, pl.out()));
-        rc = pl.done(j);
-        if (rc) return rc;
-    }
-    return pl.finish();
+            out->push_back({shards_out[i] + r0 * blk, f.fbytes + size_t(i) * f.sstride, rc_rows * blk});
+    };
+    auto code = [&](size_t j, uint8_t *buf, hipStream_t st) -> int {
+        const size_t r0 = j * f.R, rc_rows = std::min(f.R, f.rows - r0);
+        return file_encode_dev(*c, buf, flen_of(r0, rc_rows), blk, buf + f.fbytes, f.sstride, st);
+    };
+    return run_chunks(ctx, f.n, f.buf_bytes, pinned, io, code);
 }
 
 int rs_file_decode(const rs_codec *codec, uint8_t *const *shards, int nshards, const int64_t *shard_lens,

@@ -1,0 +1,54 @@
+// copy_pool.hpp -- parallel host memcpy for the host-buffer pipeline.
+//
+// Pageable caller buffers (what JNI hands us) are staged through pinned
+// mirrors so the PCIe copies run as async DMA in both directions at once; the
+// pageable <-> pinned memcpy is split over a small process-wide worker pool so
+// it keeps up with the link (measured on the MI355X host: one thread ~23 GB/s,
+// 8 threads ~71 GB/s, 16 threads 100-126 GB/s; the link moves ~57 GB/s each
+// way -- tools/memcpy_probe.cpp).
+#pragma once
+
+#include <condition_variable>
+#include <cstddef>
+#include <cstdint>
+#include <deque>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace rsamd {
+
+struct CopyJob {
+    void *dst;
+    const void *src;
+    size_t n;
+};
+
+class CopyPool {
+public:
+    // The process-wide pool (created on first use, never destroyed: its
+    // threads are detached so process exit never waits on them).
+    static CopyPool &get();
+
+    // Copy every job, split into pieces over the workers and the calling
+    // thread; returns when all bytes are copied.  Safe to call from several
+    // threads at once.
+    void copy(const std::vector<CopyJob> &jobs);
+
+    int workers() const { return int(threads_.size()); }
+
+private:
+    explicit CopyPool(int n);
+    void run();
+
+    struct Piece {
+        CopyJob job;
+        size_t *pending;  // the batch's counter (guarded by mu_)
+    };
+    std::mutex mu_;
+    std::condition_variable work_cv_, done_cv_;
+    std::deque<Piece> queue_;
+    std::vector<std::thread> threads_;
+};
+
+}  // namespace rsamd

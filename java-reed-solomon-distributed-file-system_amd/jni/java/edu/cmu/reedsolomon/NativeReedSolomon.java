@@ -49,6 +49,21 @@ public final class NativeReedSolomon implements AutoCloseable {
         nativeDecodeMissing(handle, shards, shardPresent, offset, byteCount);
     }
 
+    /**
+     * Device-resident per-stripe recovery (rs_decode_batch_masked_bits_dev):
+     * stripes [stripe][shard][shardStride] at device address devBase, one
+     * uint32 presence bitmask per stripe at devBits (bit i = shard i present),
+     * asynchronous on the HIP stream handle `stream` (0 = default).  Stripes
+     * with fewer than k present shards are skipped and counted into the device
+     * int at devBad when it is not 0.  For services that keep chunk groups in
+     * GPU memory; the master's host-side loop uses decodeMissing per group.
+     */
+    public void decodeMaskedBitsDevice(long devBase, long devBits, long nStripes, long shardLen, long shardStride,
+                                       long stripeStride, long devBad, long stream) {
+        nativeDecodeMaskedBitsDevice(handle, devBase, devBits, nStripes, shardLen, shardStride, stripeStride, devBad,
+                                     stream);
+    }
+
     @Override
     public synchronized void close() {
         if (handle != 0) {
@@ -62,4 +77,7 @@ public final class NativeReedSolomon implements AutoCloseable {
     private static native void nativeEncodeParity(long h, byte[][] shards, int offset, int byteCount);
     private static native void nativeDecodeMissing(long h, byte[][] shards, boolean[] present, int offset, int byteCount);
     private static native boolean nativeIsParityCorrect(long h, byte[][] shards, int first, int byteCount, byte[] temp);
+    private static native void nativeDecodeMaskedBitsDevice(long h, long devBase, long devBits, long nStripes,
+                                                            long shardLen, long shardStride, long stripeStride,
+                                                            long devBad, long stream);
 }

@@ -185,3 +185,20 @@ JNIEXPORT jboolean JNICALL Java_edu_cmu_reedsolomon_GpuCodingLoop_nativeCheckSom
     }
     return result ? JNI_TRUE : JNI_FALSE;
 }
+
+/* ---- Device-resident recovery (no Java counterpart): chunk groups kept in HBM
+ * by a GPU-side service, one presence bitmask per group (rs_amd.h). ---- */
+JNIEXPORT void JNICALL Java_edu_cmu_reedsolomon_NativeReedSolomon_nativeDecodeMaskedBitsDevice(
+        JNIEnv *env, jclass cls, jlong h, jlong devBase, jlong devBits, jlong nStripes, jlong shardLen,
+        jlong shardStride, jlong stripeStride, jlong devBad, jlong stream) {
+    if (nStripes < 0 || shardLen < 0 || shardStride < 0 || stripeStride < 0) {
+        jclass c = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
+        if (c) (*env)->ThrowNew(env, c, "negative size");
+        return;
+    }
+    int rc = rs_decode_batch_masked_bits_dev((const rs_codec *)(uintptr_t)h, (uint8_t *)(uintptr_t)devBase,
+                                             (const uint32_t *)(uintptr_t)devBits, (size_t)nStripes,
+                                             (size_t)shardLen, (size_t)shardStride, (size_t)stripeStride,
+                                             (int32_t *)(uintptr_t)devBad, (void *)(uintptr_t)stream);
+    if (rc) throw_rs(env, rc);
+}
