@@ -410,3 +410,49 @@ def test_host_file_paths_pinned(gpu, oracle_lib):
     file_decode_into(rs, sh, [True, False, True, True, False, True], S, out)
     assert np.array_equal(out, data)
     assert np.array_equal(np.stack(sh), ref)
+
+
+@pytest.mark.parametrize("k,m", [(1, 1), (1, 255), (255, 1), (128, 128), (200, 56)])
+def test_extreme_shard_counts(gpu, oracle_lib, k, m):
+    """k + m up to the reference's limit of 256 (ReedSolomon.java:44-46):
+    generic kernel with up to 255 inputs, up to 64 output groups, decode of the
+    most erasures the code allows -- host API, device batch API and the
+    per-stripe masked call, against the oracle."""
+    import torch
+    import rsamd
+    from rsamd import device
+    from rsamd.device import StripeLayout
+    T, S = k + m, 4096 + 13  # 16-B vectors plus a byte tail
+    rng = np.random.default_rng(T * 7 + k)
+    ref = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
+    oracle = oracle_lib.Codec(k, m)
+    oracle.encode_parity(ref, 0, S)
+    rs = rsamd.ReedSolomon.create(k, m)
+    sh = [a.copy() if i < k else np.zeros(S, np.uint8) for i, a in enumerate(ref)]
+    rs.encodeParity(sh, 0, S)
+    assert all(np.array_equal(a, b) for a, b in zip(sh, ref))
+    assert rs.isParityCorrect(sh, 0, S)
+    # erase as many shards as the code allows: the first min(k, m) data shards, then parity
+    miss = list(range(min(k, m))) + list(range(k, k + m - min(k, m)))
+    present = [i not in miss for i in range(T)]
+    for j in miss:
+        sh[j][:] = 0
+    rs.decodeMissing(sh, present, 0, S)
+    assert all(np.array_equal(a, b) for a, b in zip(sh, ref))
+    # device batch: 2 stripes, same pattern, then the masked call with another
+    lay = StripeLayout.packed(2, T, S)
+    host = np.zeros((2, T, lay.shard_stride), np.uint8)
+    host[:, :, :S] = np.stack(ref)
+    dev = torch.from_numpy(host.reshape(-1).copy()).to("cuda:0")
+    dev.view(2, T, lay.shard_stride)[:, k:, :] = 0
+    device.encode(rs, dev.data_ptr(), lay)
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy().reshape(2, T, -1)[:, :, :S], host[:, :, :S])
+    pats = np.array([present, [i != T - 1 for i in range(T)]], dtype=bool)
+    for t in range(2):
+        for j in range(T):
+            if not pats[t, j]:
+                dev.view(2, T, lay.shard_stride)[t, j, :S] = 0x5A
+    device.decode_masked(rs, dev.data_ptr(), pats, lay)
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy().reshape(2, T, -1)[:, :, :S], host[:, :, :S])
