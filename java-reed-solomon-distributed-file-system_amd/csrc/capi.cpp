@@ -205,11 +205,25 @@ struct Xfer {
 using ChunkIo = std::function<void(size_t j, std::vector<Xfer> *in, std::vector<Xfer> *out)>;
 using ChunkCode = std::function<int(size_t j, uint8_t *buf, hipStream_t s)>;
 
+int run_chunks_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinned, const ChunkIo &io,
+                    const ChunkCode &code);
+
 // Runs n_chunks chunks of buf_bytes each: io(j) names chunk j's inputs and
 // outputs, code(j) enqueues its kernels on the given stream.  Returns once
-// every output has reached host memory.
+// every output has reached host memory -- also on an error, so no copy into
+// or out of caller memory is still in flight when the caller gets control.
 int run_chunks(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinned, const ChunkIo &io,
                const ChunkCode &code) {
+    const int rc = run_chunks_impl(ctx, n_chunks, buf_bytes, pinned, io, code);
+    if (rc) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipStreamSynchronize(ctx->stream2);
+    }
+    return rc;
+}
+
+int run_chunks_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinned, const ChunkIo &io,
+                    const ChunkCode &code) {
     const int nbuf = n_bufs(n_chunks);
     int rc = grow(&ctx->stage, &ctx->stage_cap, buf_bytes * size_t(nbuf));
     if (rc) return rc;
