@@ -15,7 +15,8 @@ timeout -k 10 400 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/sm
 tail -2 "$OUT/smoke_$TAG.log"
 
 echo "== pytest -m gpu $(date +%T)"
-timeout -k 10 700 python3 -m pytest tests -x -q -m gpu > "$OUT/pytest_gpu_$TAG.log" 2>&1 || { tail -40 "$OUT/pytest_gpu_$TAG.log"; exit 1; }
+timeout -k 10 700 python3 -u -m pytest tests -x -v -m gpu --timeout 150 --timeout-method thread \
+    > "$OUT/pytest_gpu_$TAG.log" 2>&1 || { tail -40 "$OUT/pytest_gpu_$TAG.log"; exit 1; }
 tail -3 "$OUT/pytest_gpu_$TAG.log"
 
 echo "== bench $(date +%T)"
