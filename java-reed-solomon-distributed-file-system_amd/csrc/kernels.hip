@@ -82,17 +82,65 @@ __device__ __forceinline__ void emit(uint8_t *p, const u32x4 &v, int *mismatch) 
     }
 }
 
+// The staged coding loop of gf_vec_kernel and gf_masked_kernel, as a macro
+// so each kernel keeps it inline in its own body (moved into a device
+// function behind the kernel's early exits, the same code was scheduled with
+// every table load hoisted: 146 VGPRs and 3 waves per SIMD at 10+4).
+//
+// All K input vectors are loaded up front.  The tables are staged one input
+// at a time: the M*5 dwords of input i+1 are fetched while input i is folded
+// in, and sched_barrier stops the scheduler from hoisting all K*M*5 of them,
+// which overflows the SGPR file at 10+4 (it spills into VGPR lanes: 3x
+// slower).  For K <= 4 the terms are folded in pairs across inputs
+// (fold_terms: 1.5 v_bitop3_b32 per input and output dword instead of 2); the
+// carried term costs M*4 VGPRs, which at 10+4 would drop the kernel from 7 to
+// 6 waves per SIMD, so wider codes fold each input alone.
+//   in: sb, TABS, IN_IDX, OUT_IDX, SHARD_STRIDE; out: out_off[M], acc[M] (u32x4)
+#define RSAMD_CODE_VECTORS(K, M, TABS, IN_IDX, OUT_IDX, SHARD_STRIDE)                                     \
+    constexpr bool kCarry = (K) <= 4;                                                                     \
+    uint64_t out_off[M]; /* read before any store so these stay scalar loads */                          \
+    _Pragma("unroll") for (int p = 0; p < (M); ++p) out_off[p] = uint64_t((OUT_IDX)[p]) * (SHARD_STRIDE); \
+    u32x4 x[K];                                                                                           \
+    _Pragma("unroll") for (int i = 0; i < (K); ++i) x[i] = load_stream(sb + uint64_t((IN_IDX)[i]) * (SHARD_STRIDE)); \
+    uint32_t Tc[M][5];                                                                                    \
+    _Pragma("unroll") for (int p = 0; p < (M); ++p)                                                       \
+        _Pragma("unroll") for (int j = 0; j < 5; ++j) Tc[p][j] = (TABS)[p * 5 + j];                       \
+    uint32_t fa[M][4], fc[kCarry ? (M) : 1][4];                                                           \
+    _Pragma("unroll") for (int i = 0; i < (K); ++i) {                                                     \
+        uint32_t Tn[M][5];                                                                                \
+        if (i + 1 < (K)) {                                                                                \
+            _Pragma("unroll") for (int p = 0; p < (M); ++p)                                               \
+                _Pragma("unroll") for (int j = 0; j < 5; ++j) Tn[p][j] = (TABS)[((i + 1) * (M) + p) * 5 + j]; \
+        }                                                                                                 \
+        _Pragma("unroll") for (int w = 0; w < 4; ++w) {                                                   \
+            const Sel s = selectors(x[i][w]);                                                             \
+            _Pragma("unroll") for (int p = 0; p < (M); ++p) {                                             \
+                uint32_t t0, t1, t2;                                                                      \
+                terms(Tc[p], s, t0, t1, t2);                                                              \
+                if (kCarry)                                                                               \
+                    fold_terms(i, fa[p][w], fc[kCarry ? p : 0][w], t0, t1, t2);                           \
+                else                                                                                      \
+                    fa[p][w] = i == 0 ? xor3(t0, t1, t2) : xor3(fa[p][w], t0, t1) ^ t2;                  \
+            }                                                                                             \
+        }                                                                                                 \
+        __builtin_amdgcn_sched_barrier(0);                                                                \
+        if (i + 1 < (K)) {                                                                                \
+            _Pragma("unroll") for (int p = 0; p < (M); ++p)                                               \
+                _Pragma("unroll") for (int j = 0; j < 5; ++j) Tc[p][j] = Tn[p][j];                        \
+        }                                                                                                 \
+    }                                                                                                     \
+    u32x4 acc[M];                                                                                         \
+    _Pragma("unroll") for (int p = 0; p < (M); ++p)                                                       \
+        _Pragma("unroll") for (int w = 0; w < 4; ++w)                                                     \
+            acc[p][w] = kCarry ? fold_end((K), fa[p][w], fc[kCarry ? p : 0][w]) : fa[p][w];
+
 // ---------------------------------------------------------------------------
 // Vector kernel, compile-time shape: K inputs, M outputs.
 // Block = one wave = 64 consecutive 16-byte vectors of every shard of one
 // stripe: the 64-thread, one-vector-per-lane, non-temporal, one-shot-grid
 // shape measured fastest on MI355X (tools/kbench.hip).
 // With no grid-stride loop nothing stored by the launch can alias the
-// coefficient tables, so every table load is a scalar load.  All K input
-// vectors are loaded up front; the tables are staged one input at a time (the
-// M*5 dwords of input i+1 are fetched while input i is folded in) and
-// sched_barrier stops the scheduler from hoisting all K*M*5 of them, which
-// overflows the SGPR file at 10+4 (it spills into VGPR lanes: 3x slower).
+// coefficient tables, so every table load is a scalar load.
 // ---------------------------------------------------------------------------
 template <int K, int M, bool VERIFY>
 __global__ void __launch_bounds__(kWave) gf_vec_kernel(VecArgs a) {
@@ -102,47 +150,7 @@ __global__ void __launch_bounds__(kWave) gf_vec_kernel(VecArgs a) {
     const uint32_t v = (item - stripe * a.chunks) * uint32_t(kWave) + threadIdx.x;
     if (v >= a.nvec) return;
     uint8_t *sb = a.base + uint64_t(stripe) * a.stripe_stride + uint64_t(v) * 16;
-
-    uint64_t out_off[M];  // read before any store so these stay scalar loads
-#pragma unroll
-    for (int p = 0; p < M; ++p) out_off[p] = uint64_t(a.out_idx[p]) * a.shard_stride;
-    u32x4 x[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i) x[i] = load_stream(sb + uint64_t(a.in_idx[i]) * a.shard_stride);
-
-    uint32_t Tc[M][5];
-#pragma unroll
-    for (int p = 0; p < M; ++p)
-#pragma unroll
-        for (int j = 0; j < 5; ++j) Tc[p][j] = a.tabs[p * 5 + j];
-    u32x4 acc[M];
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-        uint32_t Tn[M][5];
-        if (i + 1 < K) {
-#pragma unroll
-            for (int p = 0; p < M; ++p)
-#pragma unroll
-                for (int j = 0; j < 5; ++j) Tn[p][j] = a.tabs[((i + 1) * M + p) * 5 + j];
-        }
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const Sel s = selectors(x[i][w]);
-#pragma unroll
-            for (int p = 0; p < M; ++p) {
-                uint32_t t0, t1, t2;
-                terms(Tc[p], s, t0, t1, t2);
-                acc[p][w] = i == 0 ? xor3(t0, t1, t2) : xor3(acc[p][w], t0, t1) ^ t2;
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (i + 1 < K) {
-#pragma unroll
-            for (int p = 0; p < M; ++p)
-#pragma unroll
-                for (int j = 0; j < 5; ++j) Tc[p][j] = Tn[p][j];
-        }
-    }
+    RSAMD_CODE_VECTORS(K, M, a.tabs, a.in_idx, a.out_idx, a.shard_stride)
 #pragma unroll
     for (int p = 0; p < M; ++p) emit<VERIFY>(sb + out_off[p], acc[p], a.mismatch);
 }
@@ -211,21 +219,27 @@ struct MaskedArgs {
     int32_t *bad;
 };
 
-// Stripe t's record, or nullptr when its presence bitmask is not decodable
-// (counted into bad by the thread that owns the stripe's column 0).
+// Stripe t's record, or nullptr when its presence bitmask is not decodable.
+// No side effects: the caller counts an undecodable stripe (count_undecodable)
+// on the path that returns.  A store that could reach the record loads would
+// make the compiler read the record -- tables included -- with per-lane
+// vector loads instead of scalar loads (97 VGPRs and 4 waves per SIMD for
+// 4+2, 256 VGPRs and 1 wave for 10+4).
 __device__ __forceinline__ const uint8_t *masked_record(const uint8_t *records, uint64_t rec_stride,
                                                         const int32_t *plan_ids, const int32_t *mask_table,
-                                                        int mask_bits, int32_t *bad, uint64_t t, bool col0) {
+                                                        int mask_bits, uint64_t t) {
     int32_t id = plan_ids[t];
     if (mask_table) {
         const uint32_t bits = uint32_t(id);
         id = (bits >> mask_bits) ? -1 : mask_table[bits];
-        if (id < 0) {
-            if (bad && col0) atomicAdd(bad, 1);
-            return nullptr;
-        }
+        if (id < 0) return nullptr;
     }
     return records + uint64_t(id) * rec_stride;
+}
+
+// One count per undecodable stripe: by the thread that owns its column 0.
+__device__ __forceinline__ void count_undecodable(int32_t *bad, bool col0) {
+    if (bad && col0) atomicAdd(bad, 1);
 }
 
 template <int K, int MS>
@@ -233,41 +247,18 @@ __global__ void __launch_bounds__(kWave) gf_masked_kernel(MaskedArgs a) {
     const uint32_t item = blockIdx.x;
     const uint32_t stripe = item / a.chunks;
     const uint32_t v = (item - stripe * a.chunks) * uint32_t(kWave) + threadIdx.x;
-    const uint8_t *rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, a.bad, stripe,
-                                       v == 0);
-    if (!rec) return;
+    const uint8_t *rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, stripe);
+    if (!rec) {
+        count_undecodable(a.bad, v == 0);
+        return;
+    }
     const int nout = *reinterpret_cast<const int32_t *>(rec);
     if (nout == 0 || v >= a.nvec) return;
     const int32_t *in_idx = reinterpret_cast<const int32_t *>(rec + a.rec_in_idx);
     const int32_t *out_idx = reinterpret_cast<const int32_t *>(rec + a.rec_out_idx);
     const uint32_t *tabs = reinterpret_cast<const uint32_t *>(rec + a.rec_tabs);
     uint8_t *sb = a.base + uint64_t(stripe) * a.stripe_stride + uint64_t(v) * 16;
-    uint64_t out_off[MS];
-#pragma unroll
-    for (int p = 0; p < MS; ++p) out_off[p] = uint64_t(out_idx[p]) * a.shard_stride;
-    u32x4 x[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i) x[i] = load_stream(sb + uint64_t(in_idx[i]) * a.shard_stride);
-    u32x4 acc[MS];
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-        uint32_t T[MS][5];
-#pragma unroll
-        for (int p = 0; p < MS; ++p)
-#pragma unroll
-            for (int j = 0; j < 5; ++j) T[p][j] = tabs[(i * MS + p) * 5 + j];
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const Sel s = selectors(x[i][w]);
-#pragma unroll
-            for (int p = 0; p < MS; ++p) {
-                uint32_t t0, t1, t2;
-                terms(T[p], s, t0, t1, t2);
-                acc[p][w] = i == 0 ? xor3(t0, t1, t2) : xor3(acc[p][w], t0, t1) ^ t2;
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
+    RSAMD_CODE_VECTORS(K, MS, tabs, in_idx, out_idx, a.shard_stride)
 #pragma unroll
     for (int p = 0; p < MS; ++p)
         if (p < nout) __builtin_nontemporal_store(acc[p], reinterpret_cast<u32x4 *>(sb + out_off[p]));
@@ -278,9 +269,11 @@ __global__ void __launch_bounds__(kWave) gf_masked_generic_kernel(MaskedArgs a) 
     const uint32_t item = blockIdx.x;
     const uint32_t stripe = item / a.chunks;
     const uint32_t v = (item - stripe * a.chunks) * uint32_t(kWave) + threadIdx.x;
-    const uint8_t *rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, a.bad, stripe,
-                                       v == 0);
-    if (!rec) return;
+    const uint8_t *rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, stripe);
+    if (!rec) {
+        count_undecodable(a.bad, v == 0);
+        return;
+    }
     const int nout = *reinterpret_cast<const int32_t *>(rec);
     if (nout == 0 || v >= a.nvec) return;
     const int32_t *in_idx = reinterpret_cast<const int32_t *>(rec + a.rec_in_idx);
@@ -337,9 +330,11 @@ __global__ void __launch_bounds__(kThreads) gf_masked_byte_kernel(MaskedByteArgs
     for (uint64_t idx = uint64_t(blockIdx.x) * kThreads + threadIdx.x; idx < a.total; idx += step) {
         const uint64_t stripe = idx / a.ncols;
         const uint64_t col = a.col0 + (idx - stripe * a.ncols);
-        const uint8_t *rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, a.bad,
-                                           stripe, col == 0);
-        if (!rec) continue;
+        const uint8_t *rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, stripe);
+        if (!rec) {
+            count_undecodable(a.bad, col == 0);
+            continue;
+        }
         const int nout = *reinterpret_cast<const int32_t *>(rec);
         if (nout == 0) continue;
         const int32_t *in_idx = reinterpret_cast<const int32_t *>(rec + a.rec_in_idx);
