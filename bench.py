@@ -116,6 +116,9 @@ def main():
             extra.update(layout_legs(torch, rsamd, dev, stream))
             cpu = cpu_baseline(k, m, S, args.cpu_seconds)
             extra.update(host_inclusive(rsamd, k, m))
+    if world > 1 and not args.no_extras:
+        # every rank at once: the node's aggregate host <-> device rate
+        extra.update(host_inclusive_all_ranks(rsamd, parallel, r, k, m))
     traffic = pmc_traffic(k, m, S, B)
 
     if rank == 0:
@@ -351,6 +354,34 @@ def host_inclusive(rsamd, k, m):
     del pin
     out["host_inclusive_note"] = (f"{k}+{m}, {n >> 20} MiB host shards per call, pageable unless 'pinned' "
                                   f"(file legs: a {len(data) >> 20} MiB file); PCIe-bound, never the bench value")
+    return out
+
+
+def host_inclusive_all_ranks(rsamd, parallel, r, k, m, n=64 << 20, reps=4):
+    """SURVEY 8(d) host-inclusive rate at N GPUs: every rank calls the
+    JNI-facing encodeParity on its own host shards at the same time (pinned,
+    then pageable), bracketed by barriers; aggregate user bytes over the
+    slowest rank's time.  Bound by the node's PCIe / host memory, not HBM."""
+    import numpy as np
+    import torch
+    rng = np.random.default_rng(100 + r.rank)
+    rs = rsamd.ReedSolomon.create(k, m)
+    pin = [torch.empty(n, dtype=torch.uint8, pin_memory=True).numpy() for _ in range(k + m)]
+    for a in pin[:k]:
+        a[:] = rng.integers(0, 256, n, dtype=np.uint8)
+    pageable = [a.copy() for a in pin]
+    out = {}
+    for name, sh in (("pinned", pin), ("pageable", pageable)):
+        rs.encodeParity(sh, 0, n)  # warm-up (staging buffers, pinned mirrors)
+        parallel.barrier(r)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            rs.encodeParity(sh, 0, n)
+        el = parallel.max_over_ranks(r, time.perf_counter() - t0)
+        out[f"host_inclusive_{name}_encode_all_ranks_GiBps"] = round(r.world * reps * k * n / el / 2**30, 2)
+    out["host_inclusive_all_ranks_note"] = (f"{r.world} ranks at once, {k}+{m} x {n >> 20} MiB host shards per "
+                                            f"call, {reps} calls per rank")
+    del pin, pageable
     return out
 
 

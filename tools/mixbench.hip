@@ -11,6 +11,7 @@
 //   gf42x             gf42 with an XCD-contiguous blockIdx remap (the XCD that
 //                     gets every 8th block codes one contiguous eighth)
 //   xor42r            xor42 with the 4 loads issued in a per-wave rotated order
+//   gf42p1 / gf42p3   gf42 at wave priority 1 / 3 until its loads are issued
 // plus the additive model R / rate(rd4) + W / rate(wr2) for the encode.
 //
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -Ijava-reed-solomon-distributed-file-system_amd/csrc \
@@ -75,8 +76,20 @@ __global__ void __launch_bounds__(64) flat_kernel(uint8_t *p, uint64_t nvec, uin
 // Stripe-shaped kernels.  OP: 0 rd4, 1 wr2, 2 xor42, 3 gf42.  XCD: remap
 // blockIdx so XCD x (blocks x, x+8, ...) codes items [x*n/8, (x+1)*n/8).
 // ROT (XOR only): the 4 loads are issued starting at shard (item % 4).
-template <int OP, bool XCD, bool ROT>
+template <int OP, bool XCD, bool ROT, int PRIO = 0>
 __global__ void __launch_bounds__(64) stripe_kernel(Geo a) {
+    // Tables first: s_setprio counts as a memory clobber, so loads placed
+    // after it could no longer be scalar loads.
+    uint32_t T[M][K][5];
+    if (OP == 3) {
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+#pragma unroll
+            for (int p = 0; p < M; ++p)
+#pragma unroll
+                for (int j = 0; j < 5; ++j) T[p][i][j] = a.tabs[(i * M + p) * 5 + j];
+    }
+    if (PRIO) __builtin_amdgcn_s_setprio(PRIO);  // issue this wave's loads ahead of computing waves
     uint32_t item = blockIdx.x;
     if (XCD) item = (item % 8u) * (a.n_items / 8u) + item / 8u;
     const uint32_t stripe = item / a.chunks;
@@ -98,6 +111,7 @@ __global__ void __launch_bounds__(64) stripe_kernel(Geo a) {
 #pragma unroll
         for (int i = 0; i < K; ++i) x[i] = ld(sb + uint64_t(i) * a.shard_stride);
     }
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
     if (OP == 0) {
         uint32_t s = 0;
 #pragma unroll
@@ -114,13 +128,6 @@ __global__ void __launch_bounds__(64) stripe_kernel(Geo a) {
             for (int i = 1; i < K; ++i) acc[p] ^= x[i];
         }
     } else {
-        uint32_t T[M][K][5];
-#pragma unroll
-        for (int i = 0; i < K; ++i)
-#pragma unroll
-            for (int p = 0; p < M; ++p)
-#pragma unroll
-                for (int j = 0; j < 5; ++j) T[p][i][j] = a.tabs[(i * M + p) * 5 + j];
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
             Sel s[K];
@@ -211,6 +218,12 @@ int main(int argc, char **argv) {
     report("gf42x encode, XCD-contiguous items", R + W, t_gx);
     const double t_xr = median_ms([&] { hipLaunchKernelGGL((stripe_kernel<2, false, true>), grid, dim3(64), 0, 0, g); }, reps);
     report("xor42r memory reference, rotated load order", R + W, t_xr);
+    const double t_p1 = median_ms([&] { hipLaunchKernelGGL((stripe_kernel<3, false, false, 1>), grid, dim3(64), 0, 0, g); }, reps);
+    report("gf42p1 encode, setprio 1 while issuing loads", R + W, t_p1);
+    const double t_p3 = median_ms([&] { hipLaunchKernelGGL((stripe_kernel<3, false, false, 3>), grid, dim3(64), 0, 0, g); }, reps);
+    report("gf42p3 encode, setprio 3 while issuing loads", R + W, t_p3);
+    const double t_g2 = median_ms([&] { hipLaunchKernelGGL((stripe_kernel<3, false, false>), grid, dim3(64), 0, 0, g); }, reps);
+    report("gf42  encode (again, drift check)", R + W, t_g2);
     report("model: rd4 time + wr2 time", R + W, t_rd4 + t_wr2);
     report("model: R/rate(rd1) + W/rate(wr1)", R + W, R / (total / t_rd1) + W / (total / t_wr1));
     return 0;
