@@ -50,6 +50,8 @@ struct VecArgs {
     uint32_t nvec;     // full 16-byte vectors per shard
     uint32_t chunks;   // blocks per stripe = ceil(nvec / 64)
     uint32_t n_items;  // blocks in this launch
+    uint32_t rot;      // block order (block_item): chunk rotation per stripe
+    uint32_t xcd_span; // block order: XCD-contiguous remap span (0 = off)
     int nin;           // generic kernel only
     int *mismatch;     // Mode::Verify only
 };
@@ -80,6 +82,29 @@ __device__ __forceinline__ void emit(uint8_t *p, const u32x4 &v, int *mismatch) 
     } else {
         __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
     }
+}
+
+// Block -> (stripe, chunk) of the one-shot grids.  Stripe-major: the blocks
+// of one stripe are its consecutive 1 KiB column chunks, with two
+// refinements whose use block_order() picks per geometry from measurements:
+//  * rot != 0: each stripe's chunk order is rotated by rot * stripe, so the
+//    stripes in flight no longer start at the same offsets modulo the shard
+//    stride;
+//  * xcd_span != 0: within each group of 8 * xcd_span blocks, XCD x (which
+//    gets every 8th block) walks items [x * xcd_span, (x+1) * xcd_span), one
+//    contiguous range per XCD instead of every 8th chunk.
+// Both are bijections on [0, n_items); a trailing partial group keeps the
+// identity map.
+__device__ __forceinline__ void block_item(uint32_t n_items, uint32_t chunks, uint32_t rot, uint32_t xcd_span,
+                                           uint32_t &stripe, uint32_t &chunk) {
+    uint32_t b = blockIdx.x;
+    if (xcd_span) {  // groups of 8 * xcd_span blocks; XCD x walks items [x * xcd_span, (x+1) * xcd_span) of each
+        const uint32_t g0 = b - b % (8u * xcd_span);
+        if (g0 + 8u * xcd_span <= n_items) b = g0 + (b % 8u) * xcd_span + (b - g0) / 8u;
+    }
+    stripe = b / chunks;
+    chunk = b - stripe * chunks;
+    if (rot) chunk = uint32_t((chunk + uint64_t(rot) * stripe) % chunks);
 }
 
 // The staged coding loop of gf_vec_kernel and gf_masked_kernel, as a macro
@@ -145,9 +170,9 @@ __device__ __forceinline__ void emit(uint8_t *p, const u32x4 &v, int *mismatch) 
 template <int K, int M, bool VERIFY>
 __global__ void __launch_bounds__(kWave) gf_vec_kernel(VecArgs a) {
     if (VERIFY && mismatch_seen(a.mismatch)) return;
-    const uint32_t item = blockIdx.x;
-    const uint32_t stripe = item / a.chunks;
-    const uint32_t v = (item - stripe * a.chunks) * uint32_t(kWave) + threadIdx.x;
+    uint32_t stripe, chunk;
+    block_item(a.n_items, a.chunks, a.rot, a.xcd_span, stripe, chunk);
+    const uint32_t v = chunk * uint32_t(kWave) + threadIdx.x;
     if (v >= a.nvec) return;
     uint8_t *sb = a.base + uint64_t(stripe) * a.stripe_stride + uint64_t(v) * 16;
     RSAMD_CODE_VECTORS(K, M, a.tabs, a.in_idx, a.out_idx, a.shard_stride)
@@ -162,9 +187,9 @@ __global__ void __launch_bounds__(kWave) gf_vec_kernel(VecArgs a) {
 template <int M, bool VERIFY>
 __global__ void __launch_bounds__(kWave) gf_vec_generic_kernel(VecArgs a) {
     if (VERIFY && mismatch_seen(a.mismatch)) return;
-    const uint32_t item = blockIdx.x;
-    const uint32_t stripe = item / a.chunks;
-    const uint32_t v = (item - stripe * a.chunks) * uint32_t(kWave) + threadIdx.x;
+    uint32_t stripe, chunk;
+    block_item(a.n_items, a.chunks, a.rot, a.xcd_span, stripe, chunk);
+    const uint32_t v = chunk * uint32_t(kWave) + threadIdx.x;
     if (v >= a.nvec) return;
     uint8_t *sb = a.base + uint64_t(stripe) * a.stripe_stride + uint64_t(v) * 16;
     uint64_t out_off[M];
@@ -212,6 +237,7 @@ struct MaskedArgs {
     uint64_t stripe_stride;
     uint64_t shard_stride;
     uint32_t nvec, chunks, n_items;
+    uint32_t rot, xcd_span;                      // block order (block_item)
     uint32_t rec_in_idx, rec_out_idx, rec_tabs;  // byte offsets inside a record
     int nin;                                     // generic kernel only
     const int32_t *mask_table;                   // MaskedPlan::mask_table
@@ -244,9 +270,9 @@ __device__ __forceinline__ void count_undecodable(int32_t *bad, bool col0) {
 
 template <int K, int MS>
 __global__ void __launch_bounds__(kWave) gf_masked_kernel(MaskedArgs a) {
-    const uint32_t item = blockIdx.x;
-    const uint32_t stripe = item / a.chunks;
-    const uint32_t v = (item - stripe * a.chunks) * uint32_t(kWave) + threadIdx.x;
+    uint32_t stripe, chunk;
+    block_item(a.n_items, a.chunks, a.rot, a.xcd_span, stripe, chunk);
+    const uint32_t v = chunk * uint32_t(kWave) + threadIdx.x;
     const uint8_t *rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, stripe);
     if (!rec) {
         count_undecodable(a.bad, v == 0);
@@ -266,9 +292,9 @@ __global__ void __launch_bounds__(kWave) gf_masked_kernel(MaskedArgs a) {
 
 template <int MS>
 __global__ void __launch_bounds__(kWave) gf_masked_generic_kernel(MaskedArgs a) {
-    const uint32_t item = blockIdx.x;
-    const uint32_t stripe = item / a.chunks;
-    const uint32_t v = (item - stripe * a.chunks) * uint32_t(kWave) + threadIdx.x;
+    uint32_t stripe, chunk;
+    block_item(a.n_items, a.chunks, a.rot, a.xcd_span, stripe, chunk);
+    const uint32_t v = chunk * uint32_t(kWave) + threadIdx.x;
     const uint8_t *rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, stripe);
     if (!rec) {
         count_undecodable(a.bad, v == 0);
@@ -461,6 +487,46 @@ hipError_t dispatch_vec(VecArgs a, int nout, Mode mode, hipStream_t s) {
     return hipErrorInvalidValue;
 }
 
+// Block order of a launch (block_item): a table tuned on MI355X with the real
+// encode kernel (tools/sweep_order.sh, tools/ab_order_encode.sh; results in
+// profiles/r1/block_order_sweep.txt), fraction of HBM peak:
+//
+//   shards x size     stripe-major   XCD-contiguous   rotation (~3/8 stripe)
+//   4+2  x 16 KiB         0.78           0.81              0.73
+//   4+2  x 256 KiB        0.78           0.81              0.75
+//   4+2  x 512 KiB        0.77           0.80              0.79
+//   4+2  x 1 MiB          0.78           0.79              0.81-0.82
+//   4+2  x 2 MiB          0.77           0.79              0.69-0.70
+//   4+2  x 4 MiB          0.76           0.77              0.76
+//   4+2  x 8 MiB          0.74           0.79              0.73
+//   10+4 x 1 MiB          0.73           0.73              0.77
+//   10+4 x 4 MiB          0.70           0.70              0.72
+//   4+2  x 4 KiB          0.72           0.80              --
+//
+// The XCD-contiguous remap is the default; rotation wins at 1 MiB shards and
+// for wide (>= 14-shard) stripes of >= 1 MiB, and loses badly elsewhere (2 MiB),
+// so it is used exactly there.  RSAMD_BLOCK_ROT (rotation in chunks, 0 = off)
+// and RSAMD_BLOCK_XCD (0 off, 1 whole launch, N > 1 groups of 8 * N blocks)
+// override the table for A/B runs.
+struct BlockOrder {
+    uint32_t rot, xcd_span;
+};
+BlockOrder block_order(uint32_t chunks, uint32_t total_shards, uint32_t n_items) {
+    static const int env_rot = [] {
+        const char *e = std::getenv("RSAMD_BLOCK_ROT");
+        return e ? std::atoi(e) : -1;
+    }();
+    static const int env_xcd = [] {
+        const char *e = std::getenv("RSAMD_BLOCK_XCD");
+        return e ? std::atoi(e) : -1;
+    }();
+    const bool rotate = chunks == 1024 || (total_shards >= 14 && chunks >= 1024);
+    const uint32_t rot = env_rot >= 0 ? uint32_t(env_rot) : (rotate ? 3u * chunks / 8u - 1u : 0u);
+    uint32_t span = env_xcd >= 0 ? (env_xcd == 1 ? n_items / 8u : uint32_t(env_xcd)) : (rotate ? 0u : n_items / 8u);
+    if (span && uint64_t(span) * 8u > n_items) span = n_items / 8u;
+    return BlockOrder{chunks > 1 ? rot % chunks : 0u, span};
+}
+
 hipError_t launch_bytes(const Geometry &g, const DevPlan &p, size_t col0, size_t ncols, Mode mode, int *mismatch,
                         hipStream_t s) {
     ByteArgs a{g.base, p.tabs, p.in_idx, p.out_idx, g.stripe_stride, g.shard_stride, col0, ncols,
@@ -538,9 +604,12 @@ hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t 
         const size_t stripes_per_launch = std::max<size_t>(1, size_t(INT32_MAX) / chunks);
         for (size_t t0 = 0; t0 < g.n_stripes; t0 += stripes_per_launch) {
             const size_t nst = std::min(stripes_per_launch, g.n_stripes - t0);
+            const BlockOrder o = block_order(chunks, uint32_t(g.stripe_stride / std::max<size_t>(1, g.shard_stride)),
+                                             uint32_t(nst * chunks));
             MaskedArgs a{base + t0 * g.stripe_stride, p.records, p.rec_stride, p.plan_ids + t0, g.stripe_stride,
-                         g.shard_stride, nvec, chunks, uint32_t(nst * chunks), uint32_t(l.in_idx),
-                         uint32_t(l.out_idx), uint32_t(l.tabs), p.nin, p.mask_table, p.mask_bits, p.bad};
+                         g.shard_stride, nvec, chunks, uint32_t(nst * chunks), o.rot, o.xcd_span,
+                         uint32_t(l.in_idx), uint32_t(l.out_idx), uint32_t(l.tabs), p.nin, p.mask_table,
+                         p.mask_bits, p.bad};
             hipError_t e = dispatch_masked(a, p.mslots, s);
             if (e != hipSuccess) return e;
         }
@@ -569,8 +638,10 @@ hipError_t launch_gf(const Geometry &g, const DevPlan &p, Mode mode, int *mismat
         const size_t stripes_per_launch = std::max<size_t>(1, size_t(INT32_MAX) / chunks);
         for (size_t t0 = 0; t0 < g.n_stripes; t0 += stripes_per_launch) {
             const size_t nst = std::min(stripes_per_launch, g.n_stripes - t0);
+            const BlockOrder o = block_order(chunks, uint32_t(g.stripe_stride / std::max<size_t>(1, g.shard_stride)),
+                                             uint32_t(nst * chunks));
             VecArgs a{base + t0 * g.stripe_stride, p.tabs, p.in_idx, p.out_idx, g.stripe_stride, g.shard_stride,
-                      nvec, chunks, uint32_t(nst * chunks), p.nin, mismatch};
+                      nvec, chunks, uint32_t(nst * chunks), o.rot, o.xcd_span, p.nin, mismatch};
             hipError_t e = dispatch_vec(a, p.nout, mode, s);
             if (e != hipSuccess) return e;
         }
