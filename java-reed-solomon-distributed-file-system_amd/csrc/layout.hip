@@ -47,6 +47,7 @@ struct FileArgs {
     const uint32_t *tabs; // [K][M or E][5]
     const int32_t *in_idx;  // decode: survivor shard indices [K]
     const int32_t *dsrc;    // decode: data shard i -> survivor position (>= 0) or -(row + 1)
+    uint32_t xcd_span;      // block order (file_block)
 };
 
 // How the fused kernels touch the FILE side (the shard side is always 16-byte
@@ -107,10 +108,21 @@ __device__ __forceinline__ void row_of(uint64_t r0, uint32_t w0, uint32_t d, uin
     }
 }
 
+// Block order of the file kernels: with xcd_span != 0, XCD x (which gets
+// every 8th block) walks blocks [x * xcd_span, (x+1) * xcd_span), one
+// contiguous range per XCD (kernels.hip block_item; measured in
+// profiles/r1/block_order_sweep.txt for the stripe kernels).
+__device__ __forceinline__ uint32_t file_block(uint32_t xcd_span) {
+    uint32_t b = blockIdx.x;
+    if (xcd_span && b < 8u * xcd_span) b = (b % 8u) * xcd_span + b / 8u;
+    return b;
+}
+
 template <int K, int M, int IO>
 __global__ void __launch_bounds__(kWave) file_encode_kernel(FileArgs a) {
-    const uint32_t v = blockIdx.x * kWave + threadIdx.x;
-    const uint64_t c0 = uint64_t(blockIdx.x) * kWave * 16;  // block-uniform first column
+    const uint32_t blk = file_block(a.xcd_span);
+    const uint32_t v = blk * kWave + threadIdx.x;
+    const uint64_t c0 = uint64_t(blk) * kWave * 16;  // block-uniform first column
     const uint64_t r0 = c0 / a.block;
     const uint32_t w0 = uint32_t(c0 - r0 * a.block);
     if (v >= a.nvec) return;
@@ -187,8 +199,9 @@ __device__ __forceinline__ int data_row(const int (&dsrc)[K], int j) {
 
 template <int K, int E, int IO>
 __global__ void __launch_bounds__(kWave) file_decode_kernel(FileArgs a) {
-    const uint32_t v = blockIdx.x * kWave + threadIdx.x;
-    const uint64_t c0 = uint64_t(blockIdx.x) * kWave * 16;
+    const uint32_t blk = file_block(a.xcd_span);
+    const uint32_t v = blk * kWave + threadIdx.x;
+    const uint64_t c0 = uint64_t(blk) * kWave * 16;
     const uint64_t r0 = c0 / a.block;
     const uint32_t w0 = uint32_t(c0 - r0 * a.block);
     int dsrc[K];
@@ -272,6 +285,7 @@ struct TileArgs {
     const uint32_t *tabs;  // [K][E][5]
     const int32_t *in_idx;
     const int32_t *dsrc;
+    uint32_t xcd_span;     // block order (file_block)
 };
 
 __device__ __forceinline__ uint32_t div_small(uint32_t t, uint32_t inv) {
@@ -329,7 +343,7 @@ __device__ __forceinline__ void tile_park(const u32x4 (&x)[K], const uint32_t (&
 template <int K, int E>
 __global__ void __launch_bounds__(kTileThreads) file_decode_tiled_kernel(TileArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
-    const uint64_t r0 = uint64_t(blockIdx.x) * a.rows;
+    const uint64_t r0 = uint64_t(file_block(a.xcd_span)) * a.rows;
     const uint32_t rows = uint32_t(min(uint64_t(a.rows), a.n_rows - r0));
     const uint32_t span = rows * a.block;      // columns of this tile (a multiple of 16 unless last)
     const uint32_t pitch = a.rows * a.block;   // LDS bytes per data shard
@@ -411,12 +425,13 @@ struct EncTileArgs {
     uint32_t rows;
     uint32_t inv_block;
     const uint32_t *tabs;  // [K][M][5]
+    uint32_t xcd_span;     // block order (file_block)
 };
 
 template <int K, int M>
 __global__ void __launch_bounds__(kTileThreads) file_encode_tiled_kernel(EncTileArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
-    const uint64_t r0 = uint64_t(blockIdx.x) * a.rows;
+    const uint64_t r0 = uint64_t(file_block(a.xcd_span)) * a.rows;
     const uint32_t rows = uint32_t(min(uint64_t(a.rows), a.n_rows - r0));
     const uint32_t span = rows * a.block;
     const uint32_t kblock = uint32_t(K) * a.block;
@@ -560,6 +575,16 @@ int file_io_mode() {
     return v;
 }
 
+// XCD span for a file-kernel grid of n blocks (RSAMD_FILE_XCD=0 turns the
+// remap off for A/B runs).
+uint32_t file_xcd_span(uint64_t n_blocks) {
+    static const bool on = [] {
+        const char *e = std::getenv("RSAMD_FILE_XCD");
+        return !(e && e[0] == '0');
+    }();
+    return on ? uint32_t(n_blocks / 8u) : 0u;
+}
+
 template <int K, int M>
 hipError_t launch_enc_t(const FileArgs &a, hipStream_t s) {
     const dim3 grid((a.nvec + kWave - 1) / kWave);
@@ -647,8 +672,9 @@ hipError_t launch_file_encode_fused(const FileGeom &g, const DevPlan *parity0, h
     const uint32_t R = tile_rows(g);
     if (R && aligned(g.file, 16) && mode && mode[0] == '1') {
         EncTileArgs a{g.file, g.file_len, g.shards, g.shard_stride, g.S / g.block, uint32_t(g.block), R,
-                      uint32_t((uint64_t(1) << 32) / g.block + 1), parity0 ? parity0->tabs : nullptr};
+                      uint32_t((uint64_t(1) << 32) / g.block + 1), parity0 ? parity0->tabs : nullptr, 0};
         const uint64_t tiles = (a.n_rows + R - 1) / R;
+        a.xcd_span = file_xcd_span(tiles);
         switch (parity0 ? parity0->nout : 0) {
         case 0: return launch_enc_tiled_t<4, 0>(a, tiles, s);
         case 1: return launch_enc_tiled_t<4, 1>(a, tiles, s);
@@ -659,7 +685,8 @@ hipError_t launch_file_encode_fused(const FileGeom &g, const DevPlan *parity0, h
         return hipErrorInvalidValue;
     }
     FileArgs a{g.file, nullptr, g.file_len, g.shards, g.shard_stride, g.S, uint32_t(g.block),
-               uint32_t((g.S + 15) / 16), parity0 ? parity0->tabs : nullptr, nullptr, nullptr};
+               uint32_t((g.S + 15) / 16), parity0 ? parity0->tabs : nullptr, nullptr, nullptr, 0};
+    a.xcd_span = file_xcd_span((a.nvec + kWave - 1) / kWave);
     const int m = parity0 ? parity0->nout : 0;
     switch (m) {
     case 0: return launch_enc_t<4, 0>(a, s);
@@ -678,8 +705,9 @@ hipError_t launch_file_decode_fused(const FileGeom &g, const FileDecodePlan &p, 
     if (R && !(mode && mode[0] == '0')) {  // RSAMD_FILE_DECODE=0 selects the untiled kernel (A/B only)
         TileArgs a{g.file_out, g.file_len, g.shards, g.shard_stride, g.S / g.block, uint32_t(g.block), R,
                    uint32_t((uint64_t(1) << 32) / g.block + 1), uint32_t((uint64_t(1) << 32) / (uint64_t(g.k) * g.block) + 1),
-                   p.tabs, p.in_idx, p.dsrc};
+                   p.tabs, p.in_idx, p.dsrc, 0};
         const uint64_t tiles = (a.n_rows + R - 1) / R;
+        a.xcd_span = file_xcd_span(tiles);
         switch (p.n_missing_data) {
         case 0: return launch_tiled_t<4, 0>(a, tiles, s);
         case 1: return launch_tiled_t<4, 1>(a, tiles, s);
@@ -690,7 +718,8 @@ hipError_t launch_file_decode_fused(const FileGeom &g, const FileDecodePlan &p, 
         return hipErrorInvalidValue;
     }
     FileArgs a{nullptr, g.file_out, g.file_len, g.shards, g.shard_stride, g.S, uint32_t(g.block),
-               uint32_t((g.S + 15) / 16), p.tabs, p.in_idx, p.dsrc};
+               uint32_t((g.S + 15) / 16), p.tabs, p.in_idx, p.dsrc, 0};
+    a.xcd_span = file_xcd_span((a.nvec + kWave - 1) / kWave);
     switch (p.n_missing_data) {
     case 0: return launch_dec_t<4, 0>(a, s);
     case 1: return launch_dec_t<4, 1>(a, s);
