@@ -116,6 +116,7 @@ def main():
             extra.update(layout_legs(torch, rsamd, dev, stream))
             cpu = cpu_baseline(k, m, S, args.cpu_seconds)
             extra.update(host_inclusive(rsamd, k, m))
+            extra.update(config0_single_stripe(rsamd, k, m))
     if world > 1 and not args.no_extras:
         # every rank at once: the node's aggregate host <-> device rate
         extra.update(host_inclusive_all_ranks(rsamd, parallel, r, k, m))
@@ -354,6 +355,49 @@ def host_inclusive(rsamd, k, m):
     del pin
     out["host_inclusive_note"] = (f"{k}+{m}, {n >> 20} MiB host shards per call, pageable unless 'pinned' "
                                   f"(file legs: a {len(data) >> 20} MiB file); PCIe-bound, never the bench value")
+    return out
+
+
+def config0_single_stripe(rsamd, k, m, S=64 << 10, reps=200):
+    """BASELINE configs[0]: one 4+2 stripe of 64 KiB shards, encode then a
+    1-erasure decode, through the JNI-facing host API (H2D + kernel + D2H per
+    call) -- a latency, not a throughput -- next to the oracle's scalar port of
+    the reference loop on the same host buffers."""
+    import numpy as np
+    from oracle import c_ref
+    rng = np.random.default_rng(0)
+    data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
+    sh = [a.copy() for a in data] + [np.zeros(S, np.uint8) for _ in range(m)]
+    rs = rsamd.ReedSolomon.create(k, m)
+    oc = c_ref.Codec(k, m)
+    ref = [a.copy() for a in data] + [np.zeros(S, np.uint8) for _ in range(m)]
+    present = [False] + [True] * (k + m - 1)
+
+    def per_call_us(fn):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        return round((time.perf_counter() - t0) / reps * 1e6, 1)
+
+    out = {"cfg0_gpu_host_api_encode_us": per_call_us(lambda: rs.encodeParity(sh, 0, S)),
+           "cfg0_cpu_port_encode_us": per_call_us(lambda: oc.encode_parity(ref, 0, S))}
+    ok = all(np.array_equal(a, b) for a, b in zip(sh, ref))
+
+    def gpu_decode():
+        sh[0][:] = 0
+        rs.decodeMissing(sh, present, 0, S)
+
+    def cpu_decode():
+        ref[0][:] = 0
+        oc.decode_missing(ref, present, 0, S)
+
+    out["cfg0_gpu_host_api_decode_0_us"] = per_call_us(gpu_decode)
+    out["cfg0_cpu_port_decode_0_us"] = per_call_us(cpu_decode)
+    out["cfg0_bit_exact"] = ok and all(np.array_equal(a, b) for a, b in zip(sh, ref)) and \
+        np.array_equal(sh[0], data[0])
+    out["cfg0_note"] = (f"one {k}+{m} stripe of {S >> 10} KiB shards per call, host buffers; GPU = host API "
+                        f"(H2D + kernel + D2H), CPU = oracle scalar port, 1 thread")
     return out
 
 
