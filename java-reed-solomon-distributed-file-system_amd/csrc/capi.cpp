@@ -359,7 +359,9 @@ int run_host(const std::vector<DevPlan> &plans, int nslots, const std::vector<in
     ThreadCtx *ctx = nullptr;
     int rc = thread_ctx(&ctx);
     if (rc) return rc;
-    const bool pinned = all_pinned(host, nslots);
+    // Calls of <= 1 MiB per shard are one chunk either way (zero-copy path):
+    // skip the per-buffer pointer queries.
+    const bool pinned = count > (size_t(1) << 20) && all_pinned(host, nslots);
     const size_t chunk = std::min(count, chunk_bytes(count, nslots, pinned));
     const size_t slot_stride = round_up(std::max<size_t>(chunk, 1), 256);
     if (mode == Mode::Verify) RS_HIP(hipMemsetAsync(ctx->flag, 0, sizeof(int), ctx->stream));

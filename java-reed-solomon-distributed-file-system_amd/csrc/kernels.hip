@@ -39,6 +39,7 @@ using namespace dev;
 
 constexpr int kThreads = 256;  // byte / fill / copy kernels
 constexpr int kWave = 64;      // vector kernels: one wave per block
+constexpr uint64_t kSmallBytes = 16384;  // columns below which a ragged launch uses the byte kernel alone
 
 struct VecArgs {
     uint8_t *base;
@@ -629,6 +630,10 @@ hipError_t launch_gf(const Geometry &g, const DevPlan &p, Mode mode, int *mismat
     const bool aligned = (reinterpret_cast<uintptr_t>(base) % 16 == 0) && g.shard_stride % 16 == 0 &&
                          g.stripe_stride % 16 == 0;
     if (!aligned || g.len / 16 > UINT32_MAX - kWave) return launch_bytes(g, p, g.col0, g.len, mode, mismatch, s);
+    // A few KiB of ragged columns: one byte-kernel launch instead of a vector
+    // launch plus a tail launch (small host calls are launch-latency bound).
+    if (g.len % 16 && uint64_t(g.n_stripes) * g.len <= kSmallBytes)
+        return launch_bytes(g, p, g.col0, g.len, mode, mismatch, s);
 
     const uint32_t nvec = uint32_t(g.len / 16);
     if (nvec > 0) {

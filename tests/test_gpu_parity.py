@@ -167,7 +167,9 @@ def test_misaligned_layouts_use_byte_path(gpu, golden_dir, stride_pad, base_off)
     assert np.array_equal(out, shards[:3])
 
 
-@pytest.mark.parametrize("S", [1, 3, 15, 16, 17, 31, 1000, 4097])
+# small ragged batches (<= 16 KiB of columns) take the byte kernel alone; larger
+# ones the vector kernel plus a tail launch
+@pytest.mark.parametrize("S", [1, 3, 15, 16, 17, 31, 1000, 4097, 5467, 20003, 70001])
 def test_tails_and_ragged_lengths(gpu, oracle_lib, S):
     import rsamd
     rng = np.random.default_rng(S)
