@@ -17,7 +17,7 @@ u8p = C.POINTER(C.c_uint8)
 u8pp = C.POINTER(u8p)
 
 # Every exported symbol with (restype, argtypes) -- kept in sync with include/rs_amd.h
-# (tests/test_capi_symbols.py parses the header and checks this table).
+# (tests/test_capi_host.py::test_header_symbols_exported parses the header and checks this table).
 SIGNATURES = {
     "rs_codec_create": (C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     "rs_codec_destroy": (None, [C.c_void_p]),
