@@ -198,6 +198,46 @@ bool all_pinned(const uint8_t *const *ptrs, int n) {
 
 size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// Page-locks pageable caller buffers for the duration of one pipelined call
+// (hipHostRegister: ~0.2 ms per 64 MiB the first time a range is seen,
+// microseconds after), so the pipeline DMAs them directly, full duplex,
+// instead of staging them through pinned mirrors with host memcpy
+// (tools/reg_probe.py: 4+2 x 64 MiB encode 35 -> 43.5 GiB/s).  All or
+// nothing: if any range cannot be registered the call uses the mirrors.  The
+// destructor unregisters; run_chunks has drained both streams by then, also
+// on its error paths.  RSAMD_HOST_REGISTER=0 turns it off (A/B).
+class HostRegistration {
+public:
+    bool lock(const std::vector<std::pair<const uint8_t *, size_t>> &ranges) {
+        static const bool enabled = [] {
+            const char *e = std::getenv("RSAMD_HOST_REGISTER");
+            return !(e && e[0] == '0');
+        }();
+        if (!enabled) return false;
+        for (const auto &r : ranges) {
+            if (!r.first || r.second == 0) continue;
+            void *p = const_cast<uint8_t *>(r.first);
+            if (hipHostRegister(p, r.second, hipHostRegisterDefault) != hipSuccess) {
+                (void)hipGetLastError();
+                release();
+                return false;
+            }
+            regs_.push_back(p);
+        }
+        return true;
+    }
+    ~HostRegistration() { release(); }
+
+private:
+    void release() {
+        for (void *p : regs_) (void)hipHostUnregister(p);
+        regs_.clear();
+    }
+    std::vector<void *> regs_;
+};
+
+
+
 int n_bufs(size_t n_chunks) { return int(std::min<size_t>(kStageBufs, std::max<size_t>(1, n_chunks))); }
 
 // One host <-> device transfer of a chunk: host bytes [host, host + n) and
@@ -361,7 +401,15 @@ int run_host(const std::vector<DevPlan> &plans, int nslots, const std::vector<in
     if (rc) return rc;
     // Calls of <= 1 MiB per shard are one chunk either way (zero-copy path):
     // skip the per-buffer pointer queries.
-    const bool pinned = count > (size_t(1) << 20) && all_pinned(host, nslots);
+    bool pinned = count > (size_t(1) << 20) && all_pinned(host, nslots);
+    HostRegistration reg;
+    if (!pinned && count > chunk_bytes(count, nslots, false)) {  // pipelined: lock the caller's ranges
+        std::vector<std::pair<const uint8_t *, size_t>> ranges;
+        for (int sl : in_slots) ranges.push_back({host[sl] + offset, count});
+        if (mode == Mode::Code)
+            for (int sl : out_slots) ranges.push_back({host[sl] + offset, count});
+        pinned = reg.lock(ranges);
+    }
     const size_t chunk = std::min(count, chunk_bytes(count, nslots, pinned));
     const size_t slot_stride = round_up(std::max<size_t>(chunk, 1), 256);
     if (mode == Mode::Verify) RS_HIP(hipMemsetAsync(ctx->flag, 0, sizeof(int), ctx->stream));
@@ -618,7 +666,14 @@ int file_decode_chunked(const Codec &c, uint8_t *const *shards, const int64_t *l
     const size_t blk = size_t(block), kb = size_t(k) * blk;
     std::vector<const uint8_t *> bufs(shards, shards + T);
     bufs.push_back(file_out);
-    const bool pinned = all_pinned(bufs.data(), int(bufs.size()));
+    bool pinned = all_pinned(bufs.data(), int(bufs.size()));
+    HostRegistration reg;
+    if (!pinned && file_chunks(k, T, size_t(S), blk, false).n > 1) {
+        std::vector<std::pair<const uint8_t *, size_t>> ranges;
+        for (int i = 0; i < T; ++i) ranges.push_back({shards[i], size_t(S)});
+        ranges.push_back({file_out, size_t(file_size)});
+        pinned = reg.lock(ranges);
+    }
     const FileChunks f = file_chunks(k, T, size_t(S), blk, pinned);
     std::vector<int> surv, missing;
     for (int i = 0; i < T; ++i) {
@@ -1067,7 +1122,14 @@ int rs_file_encode(const rs_codec *codec, const uint8_t *file, int64_t file_len,
     const size_t k = size_t(c->k()), blk = size_t(block);
     std::vector<const uint8_t *> bufs(shards_out, shards_out + nshards);
     bufs.push_back(file);
-    const bool pinned = all_pinned(bufs.data(), int(bufs.size()));
+    bool pinned = all_pinned(bufs.data(), int(bufs.size()));
+    HostRegistration reg;
+    if (!pinned && file_chunks(c->k(), c->total(), size_t(S), blk, false).n > 1) {
+        std::vector<std::pair<const uint8_t *, size_t>> ranges;
+        for (int i = 0; i < nshards; ++i) ranges.push_back({shards_out[i], size_t(S)});
+        ranges.push_back({file, size_t(file_len)});
+        pinned = reg.lock(ranges);
+    }
     const FileChunks f = file_chunks(c->k(), c->total(), size_t(S), blk, pinned);
     auto flen_of = [&](size_t r0, size_t rc_rows) {  // every row holds file bytes
         return std::min(rc_rows * k * blk, size_t(file_len) - r0 * k * blk);
