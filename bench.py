@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--m", type=int, default=2)
     ap.add_argument("--shard-bytes", type=int, default=1 << 20)
     ap.add_argument("--stripes", type=int, default=4096, help="stripes per GPU")
+    ap.add_argument("--pad", type=int, default=0, help="bytes of padding between shards (layout A/B only)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     ap.add_argument("--no-extras", action="store_true", help="skip decode/copy/host-inclusive/CPU legs")
     return ap.parse_args()
@@ -69,7 +70,7 @@ def main():
     stripe0, count = parallel.stripe_partition(B * world, world, rank)
     assert count == B
     rs = rsamd.ReedSolomon.create(k, m)
-    lay = StripeLayout.packed(B, k + m, S)
+    lay = StripeLayout.packed(B, k + m, S, pad=args.pad)
     buf = torch.empty(lay.nbytes, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream()
     rdev.fill_synthetic(buf.data_ptr(), k, lay, SEED, stripe0=stripe0, stream=stream)

@@ -503,16 +503,19 @@ hipError_t dispatch_vec(VecArgs a, int nout, Mode mode, hipStream_t s) {
 //   10+4 x 1 MiB          0.73           0.73              0.77
 //   10+4 x 4 MiB          0.70           0.70              0.72
 //   4+2  x 4 KiB          0.72           0.80              --
+//   4+2  x 1 MiB + 1 KiB pad   0.75      0.80              0.75
+//   4+2  x 1 MiB + 4 KiB pad   0.62      0.78              0.74
+//   10+4 x 4 MiB + 4 KiB pad   0.75      0.71              0.74
 //
-// The XCD-contiguous remap is the default; rotation wins at 1 MiB shards and
-// for wide (>= 14-shard) stripes of >= 1 MiB, and loses badly elsewhere (2 MiB),
-// so it is used exactly there.  RSAMD_BLOCK_ROT (rotation in chunks, 0 = off)
+// The XCD-contiguous remap is the default; rotation wins at 1 MiB shards on
+// 1 MiB-aligned strides and for wide (>= 14-shard) stripes of >= 1 MiB, and
+// loses badly elsewhere (2 MiB, padded strides), so it is used exactly there.  RSAMD_BLOCK_ROT (rotation in chunks, 0 = off)
 // and RSAMD_BLOCK_XCD (0 off, 1 whole launch, N > 1 groups of 8 * N blocks)
 // override the table for A/B runs.
 struct BlockOrder {
     uint32_t rot, xcd_span;
 };
-BlockOrder block_order(uint32_t chunks, uint32_t total_shards, uint32_t n_items) {
+BlockOrder block_order(uint32_t chunks, uint32_t total_shards, uint64_t shard_stride, uint32_t n_items) {
     static const int env_rot = [] {
         const char *e = std::getenv("RSAMD_BLOCK_ROT");
         return e ? std::atoi(e) : -1;
@@ -521,7 +524,8 @@ BlockOrder block_order(uint32_t chunks, uint32_t total_shards, uint32_t n_items)
         const char *e = std::getenv("RSAMD_BLOCK_XCD");
         return e ? std::atoi(e) : -1;
     }();
-    const bool rotate = chunks == 1024 || (total_shards >= 14 && chunks >= 1024);
+    const bool rotate = (chunks == 1024 && shard_stride % (uint64_t(1) << 20) == 0) ||
+                        (total_shards >= 14 && chunks >= 1024);
     const uint32_t rot = env_rot >= 0 ? uint32_t(env_rot) : (rotate ? 3u * chunks / 8u - 1u : 0u);
     uint32_t span = env_xcd >= 0 ? (env_xcd == 1 ? n_items / 8u : uint32_t(env_xcd)) : (rotate ? 0u : n_items / 8u);
     if (span && uint64_t(span) * 8u > n_items) span = n_items / 8u;
@@ -606,7 +610,7 @@ hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t 
         for (size_t t0 = 0; t0 < g.n_stripes; t0 += stripes_per_launch) {
             const size_t nst = std::min(stripes_per_launch, g.n_stripes - t0);
             const BlockOrder o = block_order(chunks, uint32_t(g.stripe_stride / std::max<size_t>(1, g.shard_stride)),
-                                             uint32_t(nst * chunks));
+                                             g.shard_stride, uint32_t(nst * chunks));
             MaskedArgs a{base + t0 * g.stripe_stride, p.records, p.rec_stride, p.plan_ids + t0, g.stripe_stride,
                          g.shard_stride, nvec, chunks, uint32_t(nst * chunks), o.rot, o.xcd_span,
                          uint32_t(l.in_idx), uint32_t(l.out_idx), uint32_t(l.tabs), p.nin, p.mask_table,
@@ -644,7 +648,7 @@ hipError_t launch_gf(const Geometry &g, const DevPlan &p, Mode mode, int *mismat
         for (size_t t0 = 0; t0 < g.n_stripes; t0 += stripes_per_launch) {
             const size_t nst = std::min(stripes_per_launch, g.n_stripes - t0);
             const BlockOrder o = block_order(chunks, uint32_t(g.stripe_stride / std::max<size_t>(1, g.shard_stride)),
-                                             uint32_t(nst * chunks));
+                                             g.shard_stride, uint32_t(nst * chunks));
             VecArgs a{base + t0 * g.stripe_stride, p.tabs, p.in_idx, p.out_idx, g.stripe_stride, g.shard_stride,
                       nvec, chunks, uint32_t(nst * chunks), o.rot, o.xcd_span, p.nin, mismatch};
             hipError_t e = dispatch_vec(a, p.nout, mode, s);
