@@ -40,6 +40,24 @@ using namespace dev;
 constexpr int kThreads = 256;  // byte / fill / copy kernels
 constexpr int kWave = 64;      // vector kernels: one wave per block
 constexpr uint64_t kSmallBytes = 16384;  // columns below which a ragged launch uses the byte kernel alone
+// Division by a launch-invariant divisor with a multiply-high (Granlund and
+// Montgomery): q = (t + ((n - t) >> s1)) >> s2, t = mulhi(n, m), exact for all
+// 32-bit n.  The block -> (stripe, chunk) map divides wave-uniform values, and
+// a plain `/` compiles to a float-reciprocal sequence on the VALU (21 of the
+// 4+2 encode's 288 VALU ops); this stays on the scalar unit.
+struct FastDiv {
+    uint32_t m, s1, s2;
+};
+FastDiv make_fastdiv(uint32_t d) {
+    uint32_t l = 0;
+    while ((uint64_t(1) << l) < d) ++l;
+    return FastDiv{uint32_t(((uint64_t(1) << 32) * ((uint64_t(1) << l) - d)) / d + 1), l < 1 ? l : 1u,
+                   l > 1 ? l - 1 : 0u};
+}
+__device__ __forceinline__ uint32_t fast_div(uint32_t n, const FastDiv &f) {
+    const uint32_t t = __umulhi(n, f.m);
+    return (t + ((n - t) >> f.s1)) >> f.s2;
+}
 
 struct VecArgs {
     uint8_t *base;
@@ -53,6 +71,7 @@ struct VecArgs {
     uint32_t n_items;  // blocks in this launch
     uint32_t rot;      // block order (block_item): chunk rotation per stripe
     uint32_t xcd_span; // block order: XCD-contiguous remap span (0 = off)
+    FastDiv cdiv;      // division by chunks
     int nin;           // generic kernel only
     int *mismatch;     // Mode::Verify only
 };
@@ -91,21 +110,22 @@ __device__ __forceinline__ void emit(uint8_t *p, const u32x4 &v, int *mismatch) 
 //  * rot != 0: each stripe's chunk order is rotated by rot * stripe, so the
 //    stripes in flight no longer start at the same offsets modulo the shard
 //    stride;
-//  * xcd_span != 0: within each group of 8 * xcd_span blocks, XCD x (which
-//    gets every 8th block) walks items [x * xcd_span, (x+1) * xcd_span), one
+//  * xcd_span != 0: over the first 8 * xcd_span blocks, XCD x (which gets
+//    every 8th block) walks items [x * xcd_span, (x+1) * xcd_span), one
 //    contiguous range per XCD instead of every 8th chunk.
-// Both are bijections on [0, n_items); a trailing partial group keeps the
+// Both are bijections on [0, n_items); blocks past 8 * xcd_span keep the
 // identity map.
-__device__ __forceinline__ void block_item(uint32_t n_items, uint32_t chunks, uint32_t rot, uint32_t xcd_span,
+__device__ __forceinline__ void block_item(uint32_t chunks, const FastDiv &cdiv, uint32_t rot, uint32_t xcd_span,
                                            uint32_t &stripe, uint32_t &chunk) {
     uint32_t b = blockIdx.x;
-    if (xcd_span) {  // groups of 8 * xcd_span blocks; XCD x walks items [x * xcd_span, (x+1) * xcd_span) of each
-        const uint32_t g0 = b - b % (8u * xcd_span);
-        if (g0 + 8u * xcd_span <= n_items) b = g0 + (b % 8u) * xcd_span + (b - g0) / 8u;
-    }
-    stripe = b / chunks;
+    if (xcd_span && b < 8u * xcd_span) b = (b & 7u) * xcd_span + (b >> 3);
+    stripe = fast_div(b, cdiv);
     chunk = b - stripe * chunks;
-    if (rot) chunk = uint32_t((chunk + uint64_t(rot) * stripe) % chunks);
+    if (rot) {  // stripe * rot < n_items: fits 32 bits
+        const uint32_t p = stripe * rot;
+        chunk += p - fast_div(p, cdiv) * chunks;
+        if (chunk >= chunks) chunk -= chunks;
+    }
 }
 
 // The staged coding loop of gf_vec_kernel and gf_masked_kernel, as a macro
@@ -128,37 +148,64 @@ __device__ __forceinline__ void block_item(uint32_t n_items, uint32_t chunks, ui
     _Pragma("unroll") for (int p = 0; p < (M); ++p) out_off[p] = uint64_t((OUT_IDX)[p]) * (SHARD_STRIDE); \
     u32x4 x[K];                                                                                           \
     _Pragma("unroll") for (int i = 0; i < (K); ++i) x[i] = load_stream(sb + uint64_t((IN_IDX)[i]) * (SHARD_STRIDE)); \
-    uint32_t Tc[M][5];                                                                                    \
-    _Pragma("unroll") for (int p = 0; p < (M); ++p)                                                       \
-        _Pragma("unroll") for (int j = 0; j < 5; ++j) Tc[p][j] = (TABS)[p * 5 + j];                       \
-    uint32_t fa[M][4], fc[kCarry ? (M) : 1][4];                                                           \
-    _Pragma("unroll") for (int i = 0; i < (K); ++i) {                                                     \
-        uint32_t Tn[M][5];                                                                                \
-        if (i + 1 < (K)) {                                                                                \
-            _Pragma("unroll") for (int p = 0; p < (M); ++p)                                               \
-                _Pragma("unroll") for (int j = 0; j < 5; ++j) Tn[p][j] = (TABS)[((i + 1) * (M) + p) * 5 + j]; \
-        }                                                                                                 \
-        _Pragma("unroll") for (int w = 0; w < 4; ++w) {                                                   \
-            const Sel s = selectors(x[i][w]);                                                             \
-            _Pragma("unroll") for (int p = 0; p < (M); ++p) {                                             \
-                uint32_t t0, t1, t2;                                                                      \
-                terms(Tc[p], s, t0, t1, t2);                                                              \
-                if (kCarry)                                                                               \
-                    fold_terms(i, fa[p][w], fc[kCarry ? p : 0][w], t0, t1, t2);                           \
-                else                                                                                      \
-                    fa[p][w] = i == 0 ? xor3(t0, t1, t2) : xor3(fa[p][w], t0, t1) ^ t2;                  \
+    uint32_t fa[M][4];                                                                                    \
+    if (kCarry) {                                                                                         \
+        uint32_t Tc[M][5], fc[M][4];                                                                      \
+        _Pragma("unroll") for (int p = 0; p < (M); ++p)                                                   \
+            _Pragma("unroll") for (int j = 0; j < 5; ++j) Tc[p][j] = (TABS)[p * 5 + j];                   \
+        _Pragma("unroll") for (int i = 0; i < (K); ++i) {                                                 \
+            uint32_t Tn[M][5];                                                                            \
+            if (i + 1 < (K)) {                                                                            \
+                _Pragma("unroll") for (int p = 0; p < (M); ++p)                                           \
+                    _Pragma("unroll") for (int j = 0; j < 5; ++j) Tn[p][j] = (TABS)[((i + 1) * (M) + p) * 5 + j]; \
+            }                                                                                             \
+            _Pragma("unroll") for (int w = 0; w < 4; ++w) {                                               \
+                const Sel s = selectors(x[i][w]);                                                         \
+                _Pragma("unroll") for (int p = 0; p < (M); ++p) {                                         \
+                    uint32_t t0, t1, t2;                                                                  \
+                    terms(Tc[p], s, t0, t1, t2);                                                          \
+                    fold_terms(i, fa[p][w], fc[p][w], t0, t1, t2);                                        \
+                }                                                                                         \
+            }                                                                                             \
+            __builtin_amdgcn_sched_barrier(0);                                                            \
+            if (i + 1 < (K)) {                                                                            \
+                _Pragma("unroll") for (int p = 0; p < (M); ++p)                                           \
+                    _Pragma("unroll") for (int j = 0; j < 5; ++j) Tc[p][j] = Tn[p][j];                    \
             }                                                                                             \
         }                                                                                                 \
-        __builtin_amdgcn_sched_barrier(0);                                                                \
-        if (i + 1 < (K)) {                                                                                \
-            _Pragma("unroll") for (int p = 0; p < (M); ++p)                                               \
-                _Pragma("unroll") for (int j = 0; j < 5; ++j) Tc[p][j] = Tn[p][j];                        \
+        _Pragma("unroll") for (int p = 0; p < (M); ++p)                                                   \
+            _Pragma("unroll") for (int w = 0; w < 4; ++w) fa[p][w] = fold_end((K), fa[p][w], fc[p][w]);   \
+    } else {                                                                                              \
+        /* wide codes: inputs in pairs, both tables loaded at the top of the pair */                      \
+        _Pragma("unroll") for (int i = 0; i < (K); i += 2) {                                              \
+            const int n2 = (i + 1 < (K)) ? 2 : 1;                                                         \
+            uint32_t T2[2][M][5];                                                                         \
+            _Pragma("unroll") for (int q = 0; q < 2; ++q)                                                 \
+                if (q < n2)                                                                               \
+                    _Pragma("unroll") for (int p = 0; p < (M); ++p)                                       \
+                        _Pragma("unroll") for (int j = 0; j < 5; ++j) T2[q][p][j] = (TABS)[((i + q) * (M) + p) * 5 + j]; \
+            _Pragma("unroll") for (int w = 0; w < 4; ++w) {                                               \
+                const Sel s0 = selectors(x[i][w]);                                                        \
+                const Sel s1 = selectors(x[n2 == 2 ? i + 1 : i][w]);                                      \
+                _Pragma("unroll") for (int p = 0; p < (M); ++p) {                                         \
+                    uint32_t t0, t1, t2;                                                                  \
+                    terms(T2[0][p], s0, t0, t1, t2);                                                      \
+                    if (n2 == 2) {                                                                        \
+                        uint32_t u0, u1, u2;                                                              \
+                        terms(T2[1][p], s1, u0, u1, u2);                                                  \
+                        const uint32_t h = i == 0 ? xor3(t0, t1, t2) : xor3(xor3(fa[p][w], t0, t1), t2, u0); \
+                        fa[p][w] = i == 0 ? xor3(h, u0, u1) ^ u2 : xor3(h, u1, u2);                       \
+                    } else {                                                                              \
+                        fa[p][w] = i == 0 ? xor3(t0, t1, t2) : xor3(fa[p][w], t0, t1) ^ t2;              \
+                    }                                                                                     \
+                }                                                                                         \
+            }                                                                                             \
+            __builtin_amdgcn_sched_barrier(0);                                                            \
         }                                                                                                 \
     }                                                                                                     \
     u32x4 acc[M];                                                                                         \
     _Pragma("unroll") for (int p = 0; p < (M); ++p)                                                       \
-        _Pragma("unroll") for (int w = 0; w < 4; ++w)                                                     \
-            acc[p][w] = kCarry ? fold_end((K), fa[p][w], fc[kCarry ? p : 0][w]) : fa[p][w];
+        _Pragma("unroll") for (int w = 0; w < 4; ++w) acc[p][w] = fa[p][w];
 
 // ---------------------------------------------------------------------------
 // Vector kernel, compile-time shape: K inputs, M outputs.
@@ -172,7 +219,7 @@ template <int K, int M, bool VERIFY>
 __global__ void __launch_bounds__(kWave) gf_vec_kernel(VecArgs a) {
     if (VERIFY && mismatch_seen(a.mismatch)) return;
     uint32_t stripe, chunk;
-    block_item(a.n_items, a.chunks, a.rot, a.xcd_span, stripe, chunk);
+    block_item(a.chunks, a.cdiv, a.rot, a.xcd_span, stripe, chunk);
     const uint32_t v = chunk * uint32_t(kWave) + threadIdx.x;
     if (v >= a.nvec) return;
     uint8_t *sb = a.base + uint64_t(stripe) * a.stripe_stride + uint64_t(v) * 16;
@@ -189,7 +236,7 @@ template <int M, bool VERIFY>
 __global__ void __launch_bounds__(kWave) gf_vec_generic_kernel(VecArgs a) {
     if (VERIFY && mismatch_seen(a.mismatch)) return;
     uint32_t stripe, chunk;
-    block_item(a.n_items, a.chunks, a.rot, a.xcd_span, stripe, chunk);
+    block_item(a.chunks, a.cdiv, a.rot, a.xcd_span, stripe, chunk);
     const uint32_t v = chunk * uint32_t(kWave) + threadIdx.x;
     if (v >= a.nvec) return;
     uint8_t *sb = a.base + uint64_t(stripe) * a.stripe_stride + uint64_t(v) * 16;
@@ -239,6 +286,7 @@ struct MaskedArgs {
     uint64_t shard_stride;
     uint32_t nvec, chunks, n_items;
     uint32_t rot, xcd_span;                      // block order (block_item)
+    FastDiv cdiv;                                // division by chunks
     uint32_t rec_in_idx, rec_out_idx, rec_tabs;  // byte offsets inside a record
     int nin;                                     // generic kernel only
     const int32_t *mask_table;                   // MaskedPlan::mask_table
@@ -272,7 +320,7 @@ __device__ __forceinline__ void count_undecodable(int32_t *bad, bool col0) {
 template <int K, int MS>
 __global__ void __launch_bounds__(kWave) gf_masked_kernel(MaskedArgs a) {
     uint32_t stripe, chunk;
-    block_item(a.n_items, a.chunks, a.rot, a.xcd_span, stripe, chunk);
+    block_item(a.chunks, a.cdiv, a.rot, a.xcd_span, stripe, chunk);
     const uint32_t v = chunk * uint32_t(kWave) + threadIdx.x;
     const uint8_t *rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, stripe);
     if (!rec) {
@@ -294,7 +342,7 @@ __global__ void __launch_bounds__(kWave) gf_masked_kernel(MaskedArgs a) {
 template <int MS>
 __global__ void __launch_bounds__(kWave) gf_masked_generic_kernel(MaskedArgs a) {
     uint32_t stripe, chunk;
-    block_item(a.n_items, a.chunks, a.rot, a.xcd_span, stripe, chunk);
+    block_item(a.chunks, a.cdiv, a.rot, a.xcd_span, stripe, chunk);
     const uint32_t v = chunk * uint32_t(kWave) + threadIdx.x;
     const uint8_t *rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, stripe);
     if (!rec) {
@@ -510,8 +558,8 @@ hipError_t dispatch_vec(VecArgs a, int nout, Mode mode, hipStream_t s) {
 // The XCD-contiguous remap is the default; rotation wins at 1 MiB shards on
 // 1 MiB-aligned strides and for wide (>= 14-shard) stripes of >= 1 MiB, and
 // loses badly elsewhere (2 MiB, padded strides), so it is used exactly there.  RSAMD_BLOCK_ROT (rotation in chunks, 0 = off)
-// and RSAMD_BLOCK_XCD (0 off, 1 whole launch, N > 1 groups of 8 * N blocks)
-// override the table for A/B runs.
+// and RSAMD_BLOCK_XCD (0 / 1) override the table for A/B runs.  (Remapping
+// within groups of 8 * N blocks instead of the whole launch measured worse.)
 struct BlockOrder {
     uint32_t rot, xcd_span;
 };
@@ -527,9 +575,8 @@ BlockOrder block_order(uint32_t chunks, uint32_t total_shards, uint64_t shard_st
     const bool rotate = (chunks == 1024 && shard_stride % (uint64_t(1) << 20) == 0) ||
                         (total_shards >= 14 && chunks >= 1024);
     const uint32_t rot = env_rot >= 0 ? uint32_t(env_rot) : (rotate ? 3u * chunks / 8u - 1u : 0u);
-    uint32_t span = env_xcd >= 0 ? (env_xcd == 1 ? n_items / 8u : uint32_t(env_xcd)) : (rotate ? 0u : n_items / 8u);
-    if (span && uint64_t(span) * 8u > n_items) span = n_items / 8u;
-    return BlockOrder{chunks > 1 ? rot % chunks : 0u, span};
+    const bool xcd = env_xcd >= 0 ? env_xcd != 0 : !rotate;
+    return BlockOrder{chunks > 1 ? rot % chunks : 0u, xcd ? n_items / 8u : 0u};
 }
 
 hipError_t launch_bytes(const Geometry &g, const DevPlan &p, size_t col0, size_t ncols, Mode mode, int *mismatch,
@@ -613,7 +660,7 @@ hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t 
                                              g.shard_stride, uint32_t(nst * chunks));
             MaskedArgs a{base + t0 * g.stripe_stride, p.records, p.rec_stride, p.plan_ids + t0, g.stripe_stride,
                          g.shard_stride, nvec, chunks, uint32_t(nst * chunks), o.rot, o.xcd_span,
-                         uint32_t(l.in_idx), uint32_t(l.out_idx), uint32_t(l.tabs), p.nin, p.mask_table,
+                         make_fastdiv(chunks), uint32_t(l.in_idx), uint32_t(l.out_idx), uint32_t(l.tabs), p.nin, p.mask_table,
                          p.mask_bits, p.bad};
             hipError_t e = dispatch_masked(a, p.mslots, s);
             if (e != hipSuccess) return e;
@@ -650,7 +697,8 @@ hipError_t launch_gf(const Geometry &g, const DevPlan &p, Mode mode, int *mismat
             const BlockOrder o = block_order(chunks, uint32_t(g.stripe_stride / std::max<size_t>(1, g.shard_stride)),
                                              g.shard_stride, uint32_t(nst * chunks));
             VecArgs a{base + t0 * g.stripe_stride, p.tabs, p.in_idx, p.out_idx, g.stripe_stride, g.shard_stride,
-                      nvec, chunks, uint32_t(nst * chunks), o.rot, o.xcd_span, p.nin, mismatch};
+                      nvec, chunks, uint32_t(nst * chunks), o.rot, o.xcd_span, make_fastdiv(chunks), p.nin,
+                      mismatch};
             hipError_t e = dispatch_vec(a, p.nout, mode, s);
             if (e != hipSuccess) return e;
         }
