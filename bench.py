@@ -185,6 +185,12 @@ def device_extras(torch, rs, rdev, buf, lay, stream, k, m, S, B):
         key = "decode_" + "_".join(map(str, miss))
         out[key + "_GiBps"] = round(k * S * B / t / 2**30, 2)
         out[key + "_hbm_frac"] = round((k + e) * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
+    # row f3: isParityCorrect over the batch (reads k+m shards, writes nothing)
+    flag = torch.zeros(1, dtype=torch.int32, device=buf.device)
+    t = timed(torch, stream, lambda: rdev.verify(rs, buf.data_ptr(), lay, flag.data_ptr(), stream), 5)
+    out["verify_GiBps"] = round(k * S * B / t / 2**30, 2)
+    out["verify_hbm_frac"] = round((k + m) * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
+    out["verify_clean"] = int(flag.item()) == 0
     n = min(buf.numel() // 2, 8 << 30)
     t = timed(torch, stream, lambda: rdev.copy(buf.data_ptr() + n, buf.data_ptr(), n, stream), 5)
     out["copy_kernel_GBps"] = round(2 * n / t / 1e9, 1)
