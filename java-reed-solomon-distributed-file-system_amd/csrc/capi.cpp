@@ -15,6 +15,7 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -202,10 +203,26 @@ size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // (hipHostRegister: ~0.2 ms per 64 MiB the first time a range is seen,
 // microseconds after), so the pipeline DMAs them directly, full duplex,
 // instead of staging them through pinned mirrors with host memcpy
-// (tools/reg_probe.py: 4+2 x 64 MiB encode 35 -> 43.5 GiB/s).  All or
-// nothing: if any range cannot be registered the call uses the mirrors.  The
-// destructor unregisters; run_chunks has drained both streams by then, also
-// on its error paths.  RSAMD_HOST_REGISTER=0 turns it off (A/B).
+// (tools/reg_probe.py: 4+2 x 64 MiB encode 35 -> 43.5 GiB/s).
+//
+// Registrations go through a process-wide registry of page ranges: calls on
+// the same caller buffers (several threads, or one array passed twice) share
+// one registration by reference count, and a range that partly overlaps a
+// registered one is not registered again -- registering the same pages twice
+// and unregistering one while the other is in use aborts inside the HIP
+// runtime.  All or nothing: if any range cannot be locked the call uses the
+// mirrors.  The destructor releases after run_chunks has drained both
+// streams, also on its error paths.  RSAMD_HOST_REGISTER=0 turns it off.
+struct HostRegistry {
+    std::mutex mu;
+    std::map<uintptr_t, std::pair<uintptr_t, int>> regs;  // page start -> (page end, references)
+};
+
+HostRegistry &host_registry() {
+    static HostRegistry *r = new HostRegistry;  // never destroyed: no HIP calls at exit
+    return *r;
+}
+
 class HostRegistration {
 public:
     bool lock(const std::vector<std::pair<const uint8_t *, size_t>> &ranges) {
@@ -214,29 +231,71 @@ public:
             return !(e && e[0] == '0');
         }();
         if (!enabled) return false;
+        // The call's page ranges, sorted and merged: shards that are slices of
+        // one allocation (sharing boundary pages) become one registration.
+        constexpr uintptr_t kPage = 4096;
+        std::vector<std::pair<uintptr_t, uintptr_t>> pages;
         for (const auto &r : ranges) {
             if (!r.first || r.second == 0) continue;
-            void *p = const_cast<uint8_t *>(r.first);
-            if (hipHostRegister(p, r.second, hipHostRegisterDefault) != hipSuccess) {
-                (void)hipGetLastError();
-                release();
-                return false;
+            const uintptr_t a = reinterpret_cast<uintptr_t>(r.first);
+            pages.push_back({a & ~(kPage - 1), (a + r.second + kPage - 1) & ~(kPage - 1)});
+        }
+        std::sort(pages.begin(), pages.end());
+        std::vector<std::pair<uintptr_t, uintptr_t>> merged;
+        for (const auto &pr : pages) {
+            if (!merged.empty() && pr.first <= merged.back().second)
+                merged.back().second = std::max(merged.back().second, pr.second);
+            else
+                merged.push_back(pr);
+        }
+        HostRegistry &reg = host_registry();
+        std::lock_guard<std::mutex> guard(reg.mu);
+        for (const auto &pr : merged) {
+            const uintptr_t ps = pr.first, pe = pr.second;
+            auto next = reg.regs.upper_bound(ps);  // first registration starting after ps
+            if (next != reg.regs.begin()) {
+                auto prev = std::prev(next);
+                if (prev->second.first >= pe) {  // already covered: share it
+                    ++prev->second.second;
+                    held_.push_back(prev->first);
+                    continue;
+                }
+                if (prev->second.first > ps) return fail_locked(reg);  // partial overlap
             }
-            regs_.push_back(p);
+            if (next != reg.regs.end() && next->first < pe) return fail_locked(reg);
+            if (hipHostRegister(reinterpret_cast<void *>(ps), pe - ps, hipHostRegisterDefault) != hipSuccess) {
+                (void)hipGetLastError();
+                return fail_locked(reg);
+            }
+            reg.regs.emplace(ps, std::make_pair(pe, 1));
+            held_.push_back(ps);
         }
         return true;
     }
-    ~HostRegistration() { release(); }
+    ~HostRegistration() {
+        if (held_.empty()) return;
+        HostRegistry &reg = host_registry();
+        std::lock_guard<std::mutex> guard(reg.mu);
+        release_locked(reg);
+    }
 
 private:
-    void release() {
-        for (void *p : regs_) (void)hipHostUnregister(p);
-        regs_.clear();
+    bool fail_locked(HostRegistry &reg) {
+        release_locked(reg);
+        return false;
     }
-    std::vector<void *> regs_;
+    void release_locked(HostRegistry &reg) {
+        for (uintptr_t ps : held_) {
+            auto it = reg.regs.find(ps);
+            if (it != reg.regs.end() && --it->second.second == 0) {
+                (void)hipHostUnregister(reinterpret_cast<void *>(ps));
+                reg.regs.erase(it);
+            }
+        }
+        held_.clear();
+    }
+    std::vector<uintptr_t> held_;  // registry keys this call references
 };
-
-
 
 int n_bufs(size_t n_chunks) { return int(std::min<size_t>(kStageBufs, std::max<size_t>(1, n_chunks))); }
 

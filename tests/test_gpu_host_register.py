@@ -1,0 +1,75 @@
+"""GPU tests of the host-buffer pipeline's per-call page-locking
+(capi.cpp HostRegistration): pageable caller ranges are registered with
+hipHostRegister for the duration of a pipelined call, all or nothing, with the
+pinned mirrors as the fallback.  Registration collisions must never change a
+byte: threads sharing the same input arrays, shards that are slices of one
+allocation (shared pages), and the same array passed twice.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+N = (12 << 20) + 3  # several pipeline chunks per call, ragged end
+
+
+def test_threads_share_input_arrays(gpu, oracle_lib):
+    import rsamd
+    rs = rsamd.ReedSolomon.create(4, 2)
+    rng = np.random.default_rng(31)
+    data = [rng.integers(0, 256, N, dtype=np.uint8) for _ in range(4)]
+    ref = [d.copy() for d in data] + [np.zeros(N, np.uint8) for _ in range(2)]
+    oracle_lib.Codec(4, 2).encode_parity(ref, 0, N)
+    errors = []
+
+    def work(seed):
+        try:
+            for _ in range(3):
+                par = [np.full(N, seed, np.uint8) for _ in range(2)]
+                rs.encodeParity(data + par, 0, N)  # the same data arrays in every thread
+                assert np.array_equal(par[0], ref[4]) and np.array_equal(par[1], ref[5])
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    ts = [threading.Thread(target=work, args=(s,)) for s in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+
+
+def test_shards_are_slices_of_one_allocation(gpu, oracle_lib):
+    """Six shards back to back in one array (neighbouring shards share pages)."""
+    import rsamd
+    rs = rsamd.ReedSolomon.create(4, 2)
+    big = np.zeros(6 * N, np.uint8)
+    big[: 4 * N] = np.random.default_rng(32).integers(0, 256, 4 * N, dtype=np.uint8)
+    sh = [big[i * N:(i + 1) * N] for i in range(6)]
+    ref = [s.copy() for s in sh]
+    oracle_lib.Codec(4, 2).encode_parity(ref, 0, N)
+    rs.encodeParity(sh, 0, N)
+    assert all(np.array_equal(a, b) for a, b in zip(sh, ref))
+    sh[1][:] = 0
+    sh[4][:] = 0
+    rs.decodeMissing(sh, [True, False, True, True, False, True], 0, N)
+    assert all(np.array_equal(a, b) for a, b in zip(sh, ref))
+    assert rs.isParityCorrect(sh, 0, N)
+
+
+def test_same_array_twice_as_input(gpu, oracle_lib):
+    """CodingLoop-level call with one input array passed twice: its range is
+    registered once and the second registration collides -- the call falls
+    back to the mirrors and the bytes are still right."""
+    import rsamd
+    rng = np.random.default_rng(33)
+    a = rng.integers(0, 256, N, dtype=np.uint8)
+    b = rng.integers(0, 256, N, dtype=np.uint8)
+    rows = np.array([[3, 7, 11]], dtype=np.uint8)
+    out = [np.zeros(N, np.uint8)]
+    ref = [np.zeros(N, np.uint8)]
+    oracle_lib.code_some_shards(7, rows, [a, b, a], ref, 0, N)
+    rsamd.codeSomeShards(rows, [a, b, a], 3, out, 1, 0, N)
+    assert np.array_equal(out[0], ref[0])
