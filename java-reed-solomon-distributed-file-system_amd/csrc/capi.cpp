@@ -77,12 +77,13 @@ struct MaskedSlot {
 constexpr int kStageBufs = 3;  // staging buffers of the host-buffer pipeline
 
 struct ThreadCtx {
-    hipStream_t stream = nullptr;   // host pipeline: H2D copies + kernels, in chunk order
+    hipStream_t stream = nullptr;   // host pipeline: kernels, in chunk order
     hipStream_t stream2 = nullptr;  // host pipeline: D2H copies, in chunk order
+    hipStream_t stream3 = nullptr;  // host pipeline: H2D copies, in chunk order
     hipEvent_t ready = nullptr;     // joins stream2 back into stream
     hipEvent_t coded[kStageBufs] = {};   // buffer b's kernels done (stream -> stream2)
-    hipEvent_t freed[kStageBufs] = {};   // buffer b's D2H done (stream2 -> stream, and the host)
-    hipEvent_t loaded[kStageBufs] = {};  // buffer b's H2D done (its pinned mirror may be refilled)
+    hipEvent_t freed[kStageBufs] = {};   // buffer b's D2H done (stream2 -> stream3, and the host)
+    hipEvent_t loaded[kStageBufs] = {};  // buffer b's H2D done (stream3 -> stream; its pinned mirror may be refilled)
     uint8_t *stage = nullptr;       // kStageBufs device staging buffers
     size_t stage_cap = 0;
     uint8_t *mirror = nullptr;      // their pinned host mirrors (pageable callers only)
@@ -117,6 +118,7 @@ int thread_ctx(ThreadCtx **out) {
         auto *c = new ThreadCtx;
         hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ready, hipEventDisableTiming);
         for (int b = 0; b < kStageBufs && e == hipSuccess; ++b) {
             e = hipEventCreateWithFlags(&c->coded[b], hipEventDisableTiming);
@@ -177,8 +179,18 @@ constexpr size_t kZeroCopyBytes = size_t(64) << 20; // single-chunk calls up to 
 
 // Bytes per slot per chunk for a call of `total` bytes per slot and `nslots`
 // slots per buffer.
+size_t chunks_per_call() {
+    static const size_t v = [] {
+        const char *e = std::getenv("RSAMD_CHUNKS");
+        const long n = e ? std::atol(e) : 0;
+        return n > 0 ? size_t(n) : size_t(8);
+    }();
+    return v;
+}
+
 size_t chunk_bytes(size_t total, int nslots, bool pinned) {
-    size_t c = std::max(kMinChunk, (total / 8 + 255) / 256 * 256);
+    const size_t per = chunks_per_call();
+    size_t c = std::max(kMinChunk * 8 / per, (total / per + 255) / 256 * 256);
     if (!pinned) c = std::min(c, std::max<size_t>(size_t(1) << 20, kMirrorBytes / size_t(std::max(1, nslots))));
     return std::min(kChunk, c);
 }
@@ -320,6 +332,7 @@ int run_chunks(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinned, c
                const ChunkCode &code) {
     const int rc = run_chunks_impl(ctx, n_chunks, buf_bytes, pinned, io, code);
     if (rc) {
+        (void)hipStreamSynchronize(ctx->stream3);
         (void)hipStreamSynchronize(ctx->stream);
         (void)hipStreamSynchronize(ctx->stream2);
     }
@@ -377,6 +390,18 @@ int run_zero_copy(ThreadCtx *ctx, size_t buf_bytes, const ChunkIo &io, const Chu
     return RS_OK;
 }
 
+// Stream of the pipeline's H2D copies: a stream of their own, so chunk j+1's
+// upload is not queued behind chunk j's kernels (file decode: 4 x 8 MiB of
+// uploads, then 90 us of kernels, per 1.05 ms chunk).  RSAMD_PIPE_STREAMS=2
+// puts them back on the kernel stream.
+hipStream_t upload_stream(const ThreadCtx *ctx) {
+    static const bool two = [] {
+        const char *e = std::getenv("RSAMD_PIPE_STREAMS");
+        return e && std::atoi(e) == 2;
+    }();
+    return two ? ctx->stream : ctx->stream3;
+}
+
 int run_chunks_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinned, const ChunkIo &io,
                     const ChunkCode &code) {
     if (n_chunks == 1 && buf_bytes <= zero_copy_limit()) return run_zero_copy(ctx, buf_bytes, io, code);
@@ -388,7 +413,7 @@ int run_chunks_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinn
         rc = grow_pinned(&ctx->mirror, &ctx->mirror_cap, buf_bytes * size_t(nbuf));
         if (rc) return rc;
     }
-    hipStream_t in_s = ctx->stream, out_s = ctx->stream2;
+    hipStream_t up_s = upload_stream(ctx), in_s = ctx->stream, out_s = ctx->stream2;
     rsamd::CopyPool &pool = rsamd::CopyPool::get();
     // Staged outputs are drained nbuf - 1 chunks behind (their D2H is long
     // done by then), in the same pool batch as the next chunk's inputs.  A
@@ -422,10 +447,11 @@ int run_chunks_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinn
             for (const Xfer &x : in) jobs.push_back({mir + x.off, x.host, x.n});
             pool.copy(jobs);
         }
-        if (j >= size_t(nbuf)) RS_HIP(hipStreamWaitEvent(in_s, ctx->freed[b], 0));  // device buffer free
+        if (j >= size_t(nbuf)) RS_HIP(hipStreamWaitEvent(up_s, ctx->freed[b], 0));  // device buffer free
         for (const Xfer &x : in)
-            RS_HIP(hipMemcpyAsync(dev + x.off, staged ? mir + x.off : x.host, x.n, hipMemcpyHostToDevice, in_s));
-        if (staged) RS_HIP(hipEventRecord(ctx->loaded[b], in_s));
+            RS_HIP(hipMemcpyAsync(dev + x.off, staged ? mir + x.off : x.host, x.n, hipMemcpyHostToDevice, up_s));
+        RS_HIP(hipEventRecord(ctx->loaded[b], up_s));
+        if (up_s != in_s) RS_HIP(hipStreamWaitEvent(in_s, ctx->loaded[b], 0));
         rc = code(j, dev, in_s);
         if (rc) return rc;
         RS_HIP(hipEventRecord(ctx->coded[b], in_s));
@@ -987,6 +1013,7 @@ void rs_thread_release(void) {
         (void)hipSetDevice(kv.first);
         if (c->stream) (void)hipStreamDestroy(c->stream);
         if (c->stream2) (void)hipStreamDestroy(c->stream2);
+        if (c->stream3) (void)hipStreamDestroy(c->stream3);
         if (c->ready) (void)hipEventDestroy(c->ready);
         for (int b = 0; b < kStageBufs; ++b) {
             if (c->coded[b]) (void)hipEventDestroy(c->coded[b]);
