@@ -259,10 +259,10 @@ __global__ void __launch_bounds__(kWave) file_decode_kernel(FileArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Tiled decode-to-file.  A 256-thread workgroup owns R whole block rows
-// (R * block columns of every shard; R even so every offset stays 16-byte
-// aligned).  Phase 1: each thread loads the K survivors' 16-byte column
-// vectors, rebuilds the E missing data shards in registers and parks the K
+// Tiled decode-to-file.  A workgroup (THREADS x SLOTS column vectors) owns R
+// whole block rows (R * block columns of every shard; R even so every offset
+// stays 16-byte aligned).  Phase 1: each thread loads the K survivors' 16-byte
+// column vectors, rebuilds the E missing data shards in registers and parks the K
 // data vectors in an LDS tile [data shard][R * block].  Phase 2: the tile's
 // file bytes are ONE contiguous run [r0*K*block, (r0+R)*K*block) -- written
 // as aligned 16-byte stores, each assembled from two 8-byte LDS reads (a
@@ -271,6 +271,11 @@ __global__ void __launch_bounds__(kWave) file_decode_kernel(FileArgs a) {
 // ---------------------------------------------------------------------------
 constexpr int kTileThreads = 256;
 constexpr int kTileSlots = 2;  // 16-byte column vectors per thread and shard in phase 1
+// The decode tile's default shape: 512 threads x 1 vector (8 rows at block
+// 1000, as 256 x 2) measured 0.750-0.755 of peak on {0,5} against 0.737-0.743
+// for 256 x 2 (profiles/r1/file_decode_ab/dec_tile_shapes.txt).
+constexpr int kDecTileThreads = 512;
+constexpr int kDecTileSlots = 1;
 
 struct TileArgs {
     uint8_t *file_out;
@@ -340,8 +345,8 @@ __device__ __forceinline__ void tile_park(const u32x4 (&x)[K], const uint32_t (&
     }
 }
 
-template <int K, int E>
-__global__ void __launch_bounds__(kTileThreads) file_decode_tiled_kernel(TileArgs a) {
+template <int K, int E, int THREADS, int SLOTS>
+__global__ void __launch_bounds__(THREADS) file_decode_tiled_kernel(TileArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
     const uint64_t r0 = uint64_t(file_block(a.xcd_span)) * a.rows;
     const uint32_t rows = uint32_t(min(uint64_t(a.rows), a.n_rows - r0));
@@ -367,19 +372,19 @@ __global__ void __launch_bounds__(kTileThreads) file_decode_tiled_kernel(TileArg
     // compute, then each slot is folded and parked.  One named register array
     // per slot: an x[slot][shard] array indexed through the slot loop stays
     // an alloca and spills the vectors to scratch (2x the HBM traffic).
-    const uint32_t c0 = threadIdx.x * 16, c1 = c0 + kTileThreads * 16;
+    const uint32_t c0 = threadIdx.x * 16, c1 = c0 + THREADS * 16;
     u32x4 x0[K], x1[K];
     tile_load<K>(x0, a.shards, in_off, c0, span);
-    tile_load<K>(x1, a.shards, in_off, c1, span);
+    if constexpr (SLOTS == 2) tile_load<K>(x1, a.shards, in_off, c1, span);
     tile_park<K, E>(x0, T, dsrc, tile, pitch, c0, span);
-    tile_park<K, E>(x1, T, dsrc, tile, pitch, c1, span);
+    if constexpr (SLOTS == 2) tile_park<K, E>(x1, T, dsrc, tile, pitch, c1, span);
     __syncthreads();
 
     // Phase 2: the tile's contiguous file run, 16-byte aligned chunks.
     const uint32_t kblock = uint32_t(K) * a.block;
     const uint64_t f0 = r0 * kblock;
     const uint32_t run = rows * kblock;
-    for (uint32_t t = threadIdx.x * 16; t < run; t += kTileThreads * 16) {
+    for (uint32_t t = threadIdx.x * 16; t < run; t += THREADS * 16) {
         const uint64_t f = f0 + t;
         if (f >= a.file_size) break;
         u32x2 half[2];
@@ -636,12 +641,43 @@ bool file_fusable(const FileGeom &g, bool encode) {
 
 namespace {
 
+// Decode tile shape: THREADS x SLOTS 16-byte columns per shard.
+struct DecTile {
+    int threads, slots;
+};
+
+DecTile dec_tile() {
+    static const DecTile v = [] {
+        const char *e = std::getenv("RSAMD_DEC_TILE");  // "threads,slots" (A/B)
+        DecTile d{kDecTileThreads, kDecTileSlots};
+        if (e) {
+            int t = 0, sl = 0;
+            if (std::sscanf(e, "%d,%d", &t, &sl) == 2 && (t == 128 || t == 256 || t == 512) && (sl == 1 || sl == 2))
+                d = {t, sl};
+        }
+        return d;
+    }();
+    return v;
+}
+
 template <int K, int E>
 hipError_t launch_tiled_t(const TileArgs &a, uint64_t tiles, hipStream_t s) {
     const size_t lds = size_t(K) * a.rows * a.block;
-    hipLaunchKernelGGL((file_decode_tiled_kernel<K, E>), dim3(unsigned(tiles)), dim3(kTileThreads), lds, s,
-                       a);
-    return hipGetLastError();
+    const DecTile d = dec_tile();
+    const dim3 grid{unsigned(tiles)}, blk{unsigned(d.threads)};
+#define RSAMD_DEC_TILE(T, SL)                                                                   \
+    if (d.threads == T && d.slots == SL) {                                                      \
+        hipLaunchKernelGGL((file_decode_tiled_kernel<K, E, T, SL>), grid, blk, lds, s, a);      \
+        return hipGetLastError();                                                               \
+    }
+    RSAMD_DEC_TILE(512, 1)
+    RSAMD_DEC_TILE(256, 2)
+    RSAMD_DEC_TILE(256, 1)
+    RSAMD_DEC_TILE(128, 2)
+    RSAMD_DEC_TILE(512, 2)
+    RSAMD_DEC_TILE(128, 1)
+#undef RSAMD_DEC_TILE
+    return hipErrorInvalidValue;
 }
 
 template <int K, int M>
@@ -651,11 +687,11 @@ hipError_t launch_enc_tiled_t(const EncTileArgs &a, uint64_t tiles, hipStream_t 
     return hipGetLastError();
 }
 
-// A tile spans R * block <= kTileSlots * 256 * 16 columns (R even, >= 2), so
-// LDS per workgroup is <= K * 8 KiB = 32 KiB at K = 4.
-uint32_t tile_rows(const FileGeom &g) {
+// A tile spans R * block <= slots * threads * 16 columns (R even, >= 2), so
+// LDS per workgroup is <= K * 8 KiB = 32 KiB at K = 4 with the default shape.
+uint32_t tile_rows(const FileGeom &g, int threads = kTileThreads, int slots = kTileSlots) {
     if (g.block >= (1u << 15)) return 0;
-    uint64_t R = uint64_t(kTileSlots) * kTileThreads * 16 / g.block;
+    uint64_t R = uint64_t(slots) * threads * 16 / g.block;
     if (R % 2) --R;
     return R >= 2 ? uint32_t(R) : 0;
 }
@@ -700,7 +736,7 @@ hipError_t launch_file_encode_fused(const FileGeom &g, const DevPlan *parity0, h
 
 hipError_t launch_file_decode_fused(const FileGeom &g, const FileDecodePlan &p, hipStream_t s) {
     if (g.S == 0 || g.file_len == 0) return hipSuccess;
-    const uint32_t R = tile_rows(g);
+    const uint32_t R = tile_rows(g, dec_tile().threads, dec_tile().slots);
     const char *mode = std::getenv("RSAMD_FILE_DECODE");
     if (R && !(mode && mode[0] == '0')) {  // RSAMD_FILE_DECODE=0 selects the untiled kernel (A/B only)
         TileArgs a{g.file_out, g.file_len, g.shards, g.shard_stride, g.S / g.block, uint32_t(g.block), R,
