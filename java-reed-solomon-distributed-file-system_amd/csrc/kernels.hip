@@ -39,6 +39,10 @@ using namespace dev;
 
 constexpr int kThreads = 256;  // byte / fill / copy kernels
 constexpr int kWave = 64;      // vector kernels: one wave per block
+// A dispatch's grid is at most 2^32 - 1 work-items per dimension (the AQL
+// packet's grid size is 32-bit), so one-shot grids of one-wave blocks are cut
+// into launches of at most this many blocks.
+constexpr size_t kMaxGridBlocks = size_t(UINT32_MAX) / kWave;
 constexpr uint64_t kSmallBytes = 16384;  // columns below which a ragged launch uses the byte kernel alone
 // Division by a launch-invariant divisor with a multiply-high (Granlund and
 // Montgomery): q = (t + ((n - t) >> s1)) >> s2, t = mulhi(n, m), exact for all
@@ -653,7 +657,7 @@ hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t 
     const uint32_t nvec = uint32_t(g.len / 16);
     if (nvec > 0) {
         const uint32_t chunks = (nvec + kWave - 1) / kWave;
-        const size_t stripes_per_launch = std::max<size_t>(1, size_t(INT32_MAX) / chunks);
+        const size_t stripes_per_launch = std::max<size_t>(1, kMaxGridBlocks / chunks);
         for (size_t t0 = 0; t0 < g.n_stripes; t0 += stripes_per_launch) {
             const size_t nst = std::min(stripes_per_launch, g.n_stripes - t0);
             const BlockOrder o = block_order(chunks, uint32_t(g.stripe_stride / std::max<size_t>(1, g.shard_stride)),
@@ -690,8 +694,8 @@ hipError_t launch_gf(const Geometry &g, const DevPlan &p, Mode mode, int *mismat
     if (nvec > 0) {
         const uint32_t chunks = (nvec + kWave - 1) / kWave;
         // One block per 64 vectors of a stripe; very large batches are split
-        // by stripe ranges so the grid stays within gridDim.x.
-        const size_t stripes_per_launch = std::max<size_t>(1, size_t(INT32_MAX) / chunks);
+        // by stripe ranges so the grid stays within kMaxGridBlocks.
+        const size_t stripes_per_launch = std::max<size_t>(1, kMaxGridBlocks / chunks);
         for (size_t t0 = 0; t0 < g.n_stripes; t0 += stripes_per_launch) {
             const size_t nst = std::min(stripes_per_launch, g.n_stripes - t0);
             const BlockOrder o = block_order(chunks, uint32_t(g.stripe_stride / std::max<size_t>(1, g.shard_stride)),
@@ -727,8 +731,8 @@ hipError_t launch_copy(uint8_t *dst, const uint8_t *src, size_t n, hipStream_t s
     size_t head = 0;
     if (reinterpret_cast<uintptr_t>(dst) % 16 == 0 && reinterpret_cast<uintptr_t>(src) % 16 == 0) {
         const uint64_t nvec = n / 16;
-        for (uint64_t v0 = 0; v0 < nvec;) {  // one-shot grids of at most INT32_MAX blocks
-            const uint64_t nv = std::min<uint64_t>(nvec - v0, uint64_t(INT32_MAX) * kWave);
+        for (uint64_t v0 = 0; v0 < nvec;) {  // one-shot grids of at most kMaxGridBlocks blocks
+            const uint64_t nv = std::min<uint64_t>(nvec - v0, uint64_t(kMaxGridBlocks) * kWave);
             hipLaunchKernelGGL(copy_kernel, dim3(unsigned((nv + kWave - 1) / kWave)), dim3(kWave), 0, s,
                                dst + v0 * 16, src + v0 * 16, nv);
             v0 += nv;

@@ -635,7 +635,7 @@ bool file_fusable(const FileGeom &g, bool encode) {
     return g.k == 4 && g.block % 8 == 0 && g.block >= 8 && g.S % g.block == 0 && g.shard_stride % 16 == 0 &&
            aligned(g.shards, 16) &&
            aligned(encode ? static_cast<const void *>(g.file) : static_cast<const void *>(g.file_out), 8) &&
-           (g.S + 15) / 16 <= uint64_t(INT32_MAX) * kWave;
+           (g.S + 15) / 16 <= uint64_t(UINT32_MAX) - kWave;  // grid work-items fit 32 bits
 }
 
 
@@ -705,7 +705,8 @@ hipError_t launch_file_encode_fused(const FileGeom &g, const DevPlan *parity0, h
     // against 0.72-0.78 across boxes (profiles/r1/file_decode_ab/).
     // RSAMD_FILE_ENCODE=1 selects it (A/B).
     const char *mode = std::getenv("RSAMD_FILE_ENCODE");
-    const uint32_t R = tile_rows(g);
+    uint32_t R = tile_rows(g);
+    if (R && (g.S / g.block + R - 1) / R * uint64_t(kTileThreads) > UINT32_MAX) R = 0;  // grid > 2^32 work-items
     if (R && aligned(g.file, 16) && mode && mode[0] == '1') {
         EncTileArgs a{g.file, g.file_len, g.shards, g.shard_stride, g.S / g.block, uint32_t(g.block), R,
                       uint32_t((uint64_t(1) << 32) / g.block + 1), parity0 ? parity0->tabs : nullptr, 0};
@@ -736,7 +737,8 @@ hipError_t launch_file_encode_fused(const FileGeom &g, const DevPlan *parity0, h
 
 hipError_t launch_file_decode_fused(const FileGeom &g, const FileDecodePlan &p, hipStream_t s) {
     if (g.S == 0 || g.file_len == 0) return hipSuccess;
-    const uint32_t R = tile_rows(g, dec_tile().threads, dec_tile().slots);
+    uint32_t R = tile_rows(g, dec_tile().threads, dec_tile().slots);
+    if (R && (g.S / g.block + R - 1) / R * uint64_t(dec_tile().threads) > UINT32_MAX) R = 0;  // grid > 2^32 work-items
     const char *mode = std::getenv("RSAMD_FILE_DECODE");
     if (R && !(mode && mode[0] == '0')) {  // RSAMD_FILE_DECODE=0 selects the untiled kernel (A/B only)
         TileArgs a{g.file_out, g.file_len, g.shards, g.shard_stride, g.S / g.block, uint32_t(g.block), R,
