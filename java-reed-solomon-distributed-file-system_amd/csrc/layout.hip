@@ -415,10 +415,11 @@ __global__ void __launch_bounds__(THREADS) file_decode_tiled_kernel(TileArgs a) 
 // in LDS unchanged.  Phase 2: each thread gathers the K data shards' 16-byte
 // column vectors from LDS (two 8-byte reads each: a vector may straddle two
 // blocks when block % 16 == 8), computes the M parity vectors and stores all
-// K + M with 16-byte non-temporal stores.  This replaces file_encode_kernel's
-// 8-byte file loads, which fetch 1.2x the file at block 1000
-// (profiles/r1/file_decode_ab/).  Needs a 16-byte aligned file.  Opt-in
-// (RSAMD_FILE_ENCODE=1): not faster than file_encode_kernel on MI355X.
+// K + M with 16-byte non-temporal stores, in place of file_encode_kernel's
+// 8-byte file loads (which fetched 1.2x the file at block 1000 before the
+// XCD-contiguous block order, and exactly 1.0x since: profiles/pmc_traffic_all.json).
+// Needs a 16-byte aligned file.  Opt-in (RSAMD_FILE_ENCODE=1): not faster
+// than file_encode_kernel on MI355X.
 // ---------------------------------------------------------------------------
 struct EncTileArgs {
     const uint8_t *file;
@@ -700,9 +701,9 @@ uint32_t tile_rows(const FileGeom &g, int threads = kTileThreads, int slots = kT
 
 hipError_t launch_file_encode_fused(const FileGeom &g, const DevPlan *parity0, hipStream_t s) {
     if (g.S == 0) return hipSuccess;
-    // The untiled kernel is the default: the tiled one has ideal traffic
-    // (1.00x vs 1.2x file reads at block 1000) but measured 0.67-0.78 of peak
-    // against 0.72-0.78 across boxes (profiles/r1/file_decode_ab/).
+    // The untiled kernel is the default: both have exact traffic, and the
+    // tiled one measured 0.67-0.78 of peak against 0.72-0.78 across boxes
+    // (profiles/r1/file_decode_ab/).
     // RSAMD_FILE_ENCODE=1 selects it (A/B).
     const char *mode = std::getenv("RSAMD_FILE_ENCODE");
     uint32_t R = tile_rows(g);

@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""One device workload per process, for rocprofv3 --pmc passes: prepares the
+data (fill + encode), then launches the measured kernel 3 times and prints
+{"workload", "kernel", "alg_bytes_per_launch"} as JSON.  tools/gpu_pmc_all.sh
+runs every workload under FETCH_SIZE and WRITE_SIZE and turns the median
+dispatch into HBM bytes per launch (tools/pmc_summary.py).
+
+Workloads (bench.py's configs):
+  dec42_01   4+2 x 1 MiB x 4096, decode {0,1}          alg (4+2) S B
+  enc104     10+4 x 4 MiB x 128, encode                 alg 14 S B
+  dec104     10+4 x 4 MiB x 128, decode {0,1,2,3}       alg 14 S B
+  enc42_4k   4+2 x 4 KiB x 1 M, encode                  alg 6 S B
+  maskbits   4+2 x 4 KiB x 1 M, per-stripe bitmasks      alg (4 * stripes with a loss + erased shards) S
+  fenc       4 GiB file -> 4+2 shards (fused)            alg file + 6 S
+  fdec_05    4+2 shards {0,5} -> 4 GiB file (tiled)      alg 4 S + file
+"""
+import itertools
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "java-reed-solomon-distributed-file-system_amd"))
+
+SEED = 0x5EED
+
+
+def main():
+    name = sys.argv[1]
+    import numpy as np
+    import torch
+    import rsamd
+    from rsamd import device as rdev
+    from rsamd.device import StripeLayout
+    from rsamd.layout import decode_file_dev, encode_file_dev, file_layout
+    st = torch.cuda.current_stream()
+
+    def stripes(k, m, S, B):
+        rs = rsamd.ReedSolomon.create(k, m)
+        lay = StripeLayout.packed(B, k + m, S)
+        buf = torch.empty(lay.nbytes, dtype=torch.uint8, device="cuda:0")
+        rdev.fill_synthetic(buf.data_ptr(), k, lay, SEED, 0, st)
+        rdev.encode(rs, buf.data_ptr(), lay, st)
+        return rs, lay, buf
+
+    if name in ("dec42_01", "dec104", "enc104", "enc42_4k"):
+        k, m, S, B = {"dec42_01": (4, 2, 1 << 20, 4096), "dec104": (10, 4, 4 << 20, 128),
+                      "enc104": (10, 4, 4 << 20, 128), "enc42_4k": (4, 2, 4096, 1 << 20)}[name]
+        rs, lay, buf = stripes(k, m, S, B)
+        if name.startswith("dec"):
+            miss = (0, 1) if k == 4 else (0, 1, 2, 3)
+            present = [i not in miss for i in range(k + m)]
+            fn = lambda: rdev.decode(rs, buf.data_ptr(), present, lay, st)  # noqa: E731
+            alg = (k + len(miss)) * S * B
+            kernel = f"gf_vec_kernel<{k}, {len(miss)}, false>"
+        else:
+            fn = lambda: rdev.encode(rs, buf.data_ptr(), lay, st)  # noqa: E731
+            alg = (k + m) * S * B
+            kernel = f"gf_vec_kernel<{k}, {m}, false>"
+    elif name == "maskbits":
+        k, m, S, B = 4, 2, 4096, 1 << 20
+        rs, lay, buf = stripes(k, m, S, B)
+        pats = np.array([[i not in miss for i in range(6)] for e in range(3)
+                         for miss in itertools.combinations(range(6), e)], dtype=bool)
+        present = pats[np.random.default_rng(0).integers(0, len(pats), B)]
+        bits = torch.from_numpy(rdev.presence_bits(present).view(np.int32)).to("cuda:0")
+        fn = lambda: rdev.decode_masked_bits(rs, buf.data_ptr(), bits.data_ptr(), lay, 0, st)  # noqa: E731
+        alg = (4 * int((~present).any(axis=1).sum()) + int((~present).sum())) * S
+        kernel = "gf_masked_kernel<4, 2>"
+    elif name in ("fenc", "fdec_05"):
+        rs = rsamd.ReedSolomon.create(4, 2)
+        n = (4 << 30) // 4000 * 4000
+        _, S = file_layout(rs, n, 1000)
+        stride = (S + 255) // 256 * 256
+        f = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+        rdev.fill_synthetic(f.data_ptr(), 1, StripeLayout(1, n, n, n), SEED, 0, st)
+        sh = torch.empty(6 * stride, dtype=torch.uint8, device="cuda:0")
+        enc = lambda: encode_file_dev(rs, f.data_ptr(), n, sh.data_ptr(), stride, 1000, stream=st)  # noqa: E731
+        enc()
+        if name == "fenc":
+            fn, alg, kernel = enc, n + 6 * S, "file_encode_kernel<4, 2"
+        else:
+            g = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+            present = [0, 1, 1, 1, 1, 0]
+            fn = lambda: decode_file_dev(rs, sh.data_ptr(), S, stride, present, g.data_ptr(), n, 1000, stream=st)  # noqa: E731
+            alg, kernel = 4 * S + n, "file_decode_tiled_kernel<4, 1"
+    else:
+        raise SystemExit(f"unknown workload {name}")
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    print(json.dumps({"workload": name, "kernel": kernel, "alg_bytes_per_launch": alg}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
