@@ -327,7 +327,7 @@ def cpu_baseline(k, m, S, budget_s):
 
 def host_inclusive(rsamd, k, m):
     """Rates of the JNI-facing host-buffer API: H2D + kernel + D2H on pageable
-    buffers, chunked and overlapped on two streams (capi.cpp run_host)."""
+    buffers, chunked and overlapped on three streams (host.cpp run_chunks)."""
     import numpy as np
     from rsamd.layout import file_encode_into, file_layout
     n = 64 << 20

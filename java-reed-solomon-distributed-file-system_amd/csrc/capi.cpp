@@ -2,7 +2,8 @@
 //
 // Host-buffer entry points mirror ReedSolomon.java / CodingLoop.java one for
 // one (argument meaning, check order, exception text); they stage the byte
-// range to the GPU, run the kernels of kernels.hip and copy results back.
+// range to the GPU through host.hpp's pipeline, run the kernels of
+// kernels.hip / layout.hip and copy results back.
 // Device entry points enqueue the same kernels on a caller's stream.
 #include <hip/hip_runtime.h>
 
@@ -24,6 +25,7 @@
 #include "codec.hpp"
 #include "copy_pool.hpp"
 #include "gf256.hpp"
+#include "host.hpp"
 #include "kernels.hpp"
 #include "layout.hpp"
 
@@ -38,440 +40,7 @@ using rsamd::DevPlan;
 using rsamd::Geometry;
 using rsamd::Mode;
 using rsamd::Plan;
-
-thread_local std::string t_err;
-
-int fail(int code, const std::string &msg) {
-    t_err = msg;
-    return code;
-}
-
-int hip_fail(hipError_t e, const char *where) {
-    char buf[256];
-    std::snprintf(buf, sizeof buf, "HIP error %s (%s) in %s", hipGetErrorName(e), hipGetErrorString(e), where);
-    t_err = buf;
-    return RS_E_HIP;
-}
-
-#define RS_HIP(call)                                         \
-    do {                                                     \
-        hipError_t e_ = (call);                              \
-        if (e_ != hipSuccess) return hip_fail(e_, #call);    \
-    } while (0)
-
-// ---------------------------------------------------------------------------
-// Per-(thread, device) staging context for the host-buffer API.
-// ---------------------------------------------------------------------------
-// Per-call staging of rs_decode_batch_masked_dev (stripe pattern ids or
-// bitmasks, plus records on the dedupe path): pinned host + device bytes,
-// reused only after `done` (recorded on the caller's stream behind the
-// call's kernels) has completed.
-struct MaskedSlot {
-    uint8_t *dev = nullptr;
-    size_t dev_cap = 0;
-    uint8_t *host = nullptr;
-    size_t host_cap = 0;
-    hipEvent_t done = nullptr;
-};
-
-constexpr int kStageBufs = 3;  // staging buffers of the host-buffer pipeline
-
-struct ThreadCtx {
-    hipStream_t stream = nullptr;   // host pipeline: kernels, in chunk order
-    hipStream_t stream2 = nullptr;  // host pipeline: D2H copies, in chunk order
-    hipStream_t stream3 = nullptr;  // host pipeline: H2D copies, in chunk order
-    hipEvent_t ready = nullptr;     // joins stream2 back into stream
-    hipEvent_t coded[kStageBufs] = {};   // buffer b's kernels done (stream -> stream2)
-    hipEvent_t freed[kStageBufs] = {};   // buffer b's D2H done (stream2 -> stream3, and the host)
-    hipEvent_t loaded[kStageBufs] = {};  // buffer b's H2D done (stream3 -> stream; its pinned mirror may be refilled)
-    uint8_t *stage = nullptr;       // kStageBufs device staging buffers
-    size_t stage_cap = 0;
-    uint8_t *mirror = nullptr;      // their pinned host mirrors (pageable callers only)
-    size_t mirror_cap = 0;
-    uint8_t *plan = nullptr;   // per-call plan images (rs_code_some_shards)
-    size_t plan_cap = 0;
-    int *flag = nullptr;       // verify result
-    uint8_t *file = nullptr;   // file staging (rs_file_encode / rs_file_decode)
-    size_t file_cap = 0;
-    uint8_t *zc = nullptr;      // small calls: coherent, device-mapped host buffer the kernels use directly
-    uint8_t *zc_dev = nullptr;  // its device address
-    size_t zc_cap = 0;
-    // rs_decode_batch_masked_dev: two staging slots used in turn, so a call's
-    // host-side preparation overlaps the previous call's kernels.
-    MaskedSlot masked[2];
-    int masked_next = 0;
-};
-
-thread_local std::map<int, ThreadCtx *> t_ctx;
-
-int need_device() {
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(RS_E_NO_DEVICE, "no HIP device available");
-    return RS_OK;
-}
-
-int thread_ctx(ThreadCtx **out) {
-    int dev = 0;
-    RS_HIP(hipGetDevice(&dev));
-    auto it = t_ctx.find(dev);
-    if (it == t_ctx.end()) {
-        auto *c = new ThreadCtx;
-        hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ready, hipEventDisableTiming);
-        for (int b = 0; b < kStageBufs && e == hipSuccess; ++b) {
-            e = hipEventCreateWithFlags(&c->coded[b], hipEventDisableTiming);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&c->freed[b], hipEventDisableTiming);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&c->loaded[b], hipEventDisableTiming);
-        }
-        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&c->flag), 256);
-        if (e != hipSuccess) {
-            delete c;
-            return hip_fail(e, "thread context");
-        }
-        it = t_ctx.emplace(dev, c).first;
-    }
-    *out = it->second;
-    return RS_OK;
-}
-
-int grow(uint8_t **buf, size_t *cap, size_t want) {
-    if (*cap >= want) return RS_OK;
-    if (*buf) RS_HIP(hipFree(*buf));
-    *buf = nullptr;
-    *cap = 0;
-    RS_HIP(hipMalloc(reinterpret_cast<void **>(buf), want));
-    *cap = want;
-    return RS_OK;
-}
-
-int grow_pinned(uint8_t **buf, size_t *cap, size_t want) {
-    if (*cap >= want) return RS_OK;
-    if (*buf) RS_HIP(hipHostFree(*buf));
-    *buf = nullptr;
-    *cap = 0;
-    RS_HIP(hipHostMalloc(reinterpret_cast<void **>(buf), want, hipHostMallocDefault));
-    *cap = want;
-    return RS_OK;
-}
-
-// ---------------------------------------------------------------------------
-// Host-buffer pipeline.  A call is cut into chunks staged through kStageBufs
-// device buffers.  `stream` carries every H2D copy and kernel in chunk order,
-// `stream2` every D2H copy in chunk order, so chunk j's D2H runs beside chunk
-// j+1's H2D; events hand each buffer from its kernels to its D2H and back to
-// the H2D that reuses it.  (Two streams that each ran H2D -> kernel -> D2H
-// fell into lockstep and never overlapped the directions.)
-//
-// The link is full duplex only for async copies from page-locked memory
-// (57 GB/s one way, 97 GB/s both ways; pageable copies share one staged path
-// at 56 GB/s in total, even from two host threads -- tools/pcie_probe.py).
-// Pinned callers are copied directly.  Pageable callers (JNI arrays) go
-// through a pinned mirror of each staging buffer: the pool of copy_pool.hpp
-// fills chunk j's inputs into the mirror while the GPU moves chunk j-1, and
-// drains chunk j-1's outputs once their D2H is done.
-// ---------------------------------------------------------------------------
-constexpr size_t kChunk = size_t(32) << 20;        // max bytes per slot per chunk
-constexpr size_t kMinChunk = size_t(4) << 20;      // min bytes per slot per chunk (~8 chunks per call)
-constexpr size_t kMirrorBytes = size_t(24) << 20;  // pinned mirror bytes per staging buffer
-constexpr size_t kZeroCopyBytes = size_t(64) << 20; // single-chunk calls up to this size run zero-copy
-
-// Bytes per slot per chunk for a call of `total` bytes per slot and `nslots`
-// slots per buffer.
-size_t chunks_per_call() {
-    static const size_t v = [] {
-        const char *e = std::getenv("RSAMD_CHUNKS");
-        const long n = e ? std::atol(e) : 0;
-        return n > 0 ? size_t(n) : size_t(8);
-    }();
-    return v;
-}
-
-size_t chunk_bytes(size_t total, int nslots, bool pinned) {
-    const size_t per = chunks_per_call();
-    size_t c = std::max(kMinChunk * 8 / per, (total / per + 255) / 256 * 256);
-    if (!pinned) c = std::min(c, std::max<size_t>(size_t(1) << 20, kMirrorBytes / size_t(std::max(1, nslots))));
-    return std::min(kChunk, c);
-}
-
-// True when every non-null pointer is page-locked host memory known to HIP.
-bool all_pinned(const uint8_t *const *ptrs, int n) {
-    for (int i = 0; i < n; ++i) {
-        if (!ptrs[i]) continue;
-        hipPointerAttribute_t attr;
-        if (hipPointerGetAttributes(&attr, ptrs[i]) != hipSuccess) {
-            (void)hipGetLastError();  // pageable memory: clear the sticky error
-            return false;
-        }
-        if (attr.type != hipMemoryTypeHost) return false;
-    }
-    return true;
-}
-
-size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
-
-// Page-locks pageable caller buffers for the duration of one pipelined call
-// (hipHostRegister: ~0.2 ms per 64 MiB the first time a range is seen,
-// microseconds after), so the pipeline DMAs them directly, full duplex,
-// instead of staging them through pinned mirrors with host memcpy
-// (tools/reg_probe.py: 4+2 x 64 MiB encode 35 -> 43.5 GiB/s).
-//
-// Registrations go through a process-wide registry of page ranges: calls on
-// the same caller buffers (several threads, or one array passed twice) share
-// one registration by reference count, and a range that partly overlaps a
-// registered one is not registered again -- registering the same pages twice
-// and unregistering one while the other is in use aborts inside the HIP
-// runtime.  All or nothing: if any range cannot be locked the call uses the
-// mirrors.  The destructor releases after run_chunks has drained both
-// streams, also on its error paths.  RSAMD_HOST_REGISTER=0 turns it off.
-struct HostRegistry {
-    std::mutex mu;
-    std::map<uintptr_t, std::pair<uintptr_t, int>> regs;  // page start -> (page end, references)
-};
-
-HostRegistry &host_registry() {
-    static HostRegistry *r = new HostRegistry;  // never destroyed: no HIP calls at exit
-    return *r;
-}
-
-class HostRegistration {
-public:
-    bool lock(const std::vector<std::pair<const uint8_t *, size_t>> &ranges) {
-        static const bool enabled = [] {
-            const char *e = std::getenv("RSAMD_HOST_REGISTER");
-            return !(e && e[0] == '0');
-        }();
-        if (!enabled) return false;
-        // The call's page ranges, sorted and merged: shards that are slices of
-        // one allocation (sharing boundary pages) become one registration.
-        constexpr uintptr_t kPage = 4096;
-        std::vector<std::pair<uintptr_t, uintptr_t>> pages;
-        for (const auto &r : ranges) {
-            if (!r.first || r.second == 0) continue;
-            const uintptr_t a = reinterpret_cast<uintptr_t>(r.first);
-            pages.push_back({a & ~(kPage - 1), (a + r.second + kPage - 1) & ~(kPage - 1)});
-        }
-        std::sort(pages.begin(), pages.end());
-        std::vector<std::pair<uintptr_t, uintptr_t>> merged;
-        for (const auto &pr : pages) {
-            if (!merged.empty() && pr.first <= merged.back().second)
-                merged.back().second = std::max(merged.back().second, pr.second);
-            else
-                merged.push_back(pr);
-        }
-        HostRegistry &reg = host_registry();
-        std::lock_guard<std::mutex> guard(reg.mu);
-        for (const auto &pr : merged) {
-            const uintptr_t ps = pr.first, pe = pr.second;
-            auto next = reg.regs.upper_bound(ps);  // first registration starting after ps
-            if (next != reg.regs.begin()) {
-                auto prev = std::prev(next);
-                if (prev->second.first >= pe) {  // already covered: share it
-                    ++prev->second.second;
-                    held_.push_back(prev->first);
-                    continue;
-                }
-                if (prev->second.first > ps) return fail_locked(reg);  // partial overlap
-            }
-            if (next != reg.regs.end() && next->first < pe) return fail_locked(reg);
-            if (hipHostRegister(reinterpret_cast<void *>(ps), pe - ps, hipHostRegisterDefault) != hipSuccess) {
-                (void)hipGetLastError();
-                return fail_locked(reg);
-            }
-            reg.regs.emplace(ps, std::make_pair(pe, 1));
-            held_.push_back(ps);
-        }
-        return true;
-    }
-    ~HostRegistration() {
-        if (held_.empty()) return;
-        HostRegistry &reg = host_registry();
-        std::lock_guard<std::mutex> guard(reg.mu);
-        release_locked(reg);
-    }
-
-private:
-    bool fail_locked(HostRegistry &reg) {
-        release_locked(reg);
-        return false;
-    }
-    void release_locked(HostRegistry &reg) {
-        for (uintptr_t ps : held_) {
-            auto it = reg.regs.find(ps);
-            if (it != reg.regs.end() && --it->second.second == 0) {
-                (void)hipHostUnregister(reinterpret_cast<void *>(ps));
-                reg.regs.erase(it);
-            }
-        }
-        held_.clear();
-    }
-    std::vector<uintptr_t> held_;  // registry keys this call references
-};
-
-int n_bufs(size_t n_chunks) { return int(std::min<size_t>(kStageBufs, std::max<size_t>(1, n_chunks))); }
-
-// One host <-> device transfer of a chunk: host bytes [host, host + n) and
-// bytes [off, off + n) of the chunk's staging buffer.
-struct Xfer {
-    uint8_t *host;
-    size_t off;
-    size_t n;
-};
-using ChunkIo = std::function<void(size_t j, std::vector<Xfer> *in, std::vector<Xfer> *out)>;
-using ChunkCode = std::function<int(size_t j, uint8_t *buf, hipStream_t s)>;
-
-int run_chunks_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinned, const ChunkIo &io,
-                    const ChunkCode &code);
-
-// Runs n_chunks chunks of buf_bytes each: io(j) names chunk j's inputs and
-// outputs, code(j) enqueues its kernels on the given stream.  Returns once
-// every output has reached host memory -- also on an error, so no copy into
-// or out of caller memory is still in flight when the caller gets control.
-int run_chunks(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinned, const ChunkIo &io,
-               const ChunkCode &code) {
-    const int rc = run_chunks_impl(ctx, n_chunks, buf_bytes, pinned, io, code);
-    if (rc) {
-        (void)hipStreamSynchronize(ctx->stream3);
-        (void)hipStreamSynchronize(ctx->stream);
-        (void)hipStreamSynchronize(ctx->stream2);
-    }
-    return rc;
-}
-
-// Single-chunk calls (<= 4 MiB per shard) skip the DMA pipeline: the inputs
-// are copied into a coherent, device-mapped host buffer, the kernels read and
-// write it over the link directly, and the outputs are copied back -- one
-// launch and one stream sync instead of an async copy per shard each way and
-// the event hand-offs.  Measured per call (tools/small_call_bench.py, 4+2,
-// pageable): 1000-B shards 130 -> 36 us, 64 KiB 180 -> 40 us, 1 MiB 390-500
-// -> 280-306 us, 4 MiB 810-1100 -> 660-725 us.  RSAMD_ZC_BYTES sets the size
-// limit of the staging buffer (0 disables).
-size_t zero_copy_limit() {
-    static const size_t v = [] {
-        const char *e = std::getenv("RSAMD_ZC_BYTES");
-        return e ? size_t(std::strtoull(e, nullptr, 10)) : kZeroCopyBytes;
-    }();
-    return v;
-}
-
-int run_zero_copy(ThreadCtx *ctx, size_t buf_bytes, const ChunkIo &io, const ChunkCode &code) {
-    if (ctx->zc_cap < buf_bytes) {
-        if (ctx->zc) RS_HIP(hipHostFree(ctx->zc));
-        ctx->zc = ctx->zc_dev = nullptr;
-        ctx->zc_cap = 0;
-        RS_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->zc), buf_bytes,
-                             hipHostMallocMapped | hipHostMallocCoherent));
-        ctx->zc_cap = buf_bytes;
-        RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->zc_dev), ctx->zc, 0));
-    }
-    std::vector<Xfer> in, out;
-    io(0, &in, &out);
-    // Host copies on the calling thread; the copy pool only above 2 MiB (its
-    // wake-up costs more than a small memcpy).
-    const bool use_pool = buf_bytes > (size_t(2) << 20);
-    std::vector<rsamd::CopyJob> jobs;
-    for (const Xfer &x : in) jobs.push_back({ctx->zc + x.off, x.host, x.n});
-    if (use_pool) {
-        rsamd::CopyPool::get().copy(jobs);
-    } else {
-        for (const rsamd::CopyJob &j : jobs) std::memcpy(j.dst, j.src, j.n);
-    }
-    int rc = code(0, ctx->zc_dev, ctx->stream);
-    if (rc) return rc;
-    RS_HIP(hipStreamSynchronize(ctx->stream));
-    jobs.clear();
-    for (const Xfer &x : out) jobs.push_back({x.host, ctx->zc + x.off, x.n});
-    if (use_pool) {
-        rsamd::CopyPool::get().copy(jobs);
-    } else {
-        for (const rsamd::CopyJob &j : jobs) std::memcpy(j.dst, j.src, j.n);
-    }
-    return RS_OK;
-}
-
-// Stream of the pipeline's H2D copies: a stream of their own, so chunk j+1's
-// upload is not queued behind chunk j's kernels (file decode: 4 x 8 MiB of
-// uploads, then 90 us of kernels, per 1.05 ms chunk).  RSAMD_PIPE_STREAMS=2
-// puts them back on the kernel stream.
-hipStream_t upload_stream(const ThreadCtx *ctx) {
-    static const bool two = [] {
-        const char *e = std::getenv("RSAMD_PIPE_STREAMS");
-        return e && std::atoi(e) == 2;
-    }();
-    return two ? ctx->stream : ctx->stream3;
-}
-
-int run_chunks_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinned, const ChunkIo &io,
-                    const ChunkCode &code) {
-    if (n_chunks == 1 && buf_bytes <= zero_copy_limit()) return run_zero_copy(ctx, buf_bytes, io, code);
-    const int nbuf = n_bufs(n_chunks);
-    int rc = grow(&ctx->stage, &ctx->stage_cap, buf_bytes * size_t(nbuf));
-    if (rc) return rc;
-    const bool staged = !pinned;
-    if (staged) {
-        rc = grow_pinned(&ctx->mirror, &ctx->mirror_cap, buf_bytes * size_t(nbuf));
-        if (rc) return rc;
-    }
-    hipStream_t up_s = upload_stream(ctx), in_s = ctx->stream, out_s = ctx->stream2;
-    rsamd::CopyPool &pool = rsamd::CopyPool::get();
-    // Staged outputs are drained nbuf - 1 chunks behind (their D2H is long
-    // done by then), in the same pool batch as the next chunk's inputs.  A
-    // mirror's output bytes are drained before the D2H that reuses it is issued.
-    const size_t lag = size_t(std::max(1, nbuf - 1));
-    std::deque<std::pair<size_t, std::vector<Xfer>>> pending;
-    std::vector<Xfer> in, out;
-    std::vector<rsamd::CopyJob> jobs;
-    auto queue_drain = [&]() -> int {  // the oldest pending chunk: mirror -> caller
-        const size_t pj = pending.front().first;
-        RS_HIP(hipEventSynchronize(ctx->freed[pj % nbuf]));
-        const uint8_t *mir = ctx->mirror + (pj % nbuf) * buf_bytes;
-        for (const Xfer &x : pending.front().second) jobs.push_back({x.host, mir + x.off, x.n});
-        pending.pop_front();
-        return RS_OK;
-    };
-    for (size_t j = 0; j < n_chunks; ++j) {
-        const size_t b = j % nbuf;
-        uint8_t *dev = ctx->stage + b * buf_bytes;
-        uint8_t *mir = staged ? ctx->mirror + b * buf_bytes : nullptr;
-        in.clear();
-        out.clear();
-        io(j, &in, &out);
-        if (staged) {
-            jobs.clear();
-            if (pending.size() >= lag) {
-                rc = queue_drain();
-                if (rc) return rc;
-            }
-            if (j >= size_t(nbuf)) RS_HIP(hipEventSynchronize(ctx->loaded[b]));  // chunk j - nbuf's H2D done
-            for (const Xfer &x : in) jobs.push_back({mir + x.off, x.host, x.n});
-            pool.copy(jobs);
-        }
-        if (j >= size_t(nbuf)) RS_HIP(hipStreamWaitEvent(up_s, ctx->freed[b], 0));  // device buffer free
-        for (const Xfer &x : in)
-            RS_HIP(hipMemcpyAsync(dev + x.off, staged ? mir + x.off : x.host, x.n, hipMemcpyHostToDevice, up_s));
-        RS_HIP(hipEventRecord(ctx->loaded[b], up_s));
-        if (up_s != in_s) RS_HIP(hipStreamWaitEvent(in_s, ctx->loaded[b], 0));
-        rc = code(j, dev, in_s);
-        if (rc) return rc;
-        RS_HIP(hipEventRecord(ctx->coded[b], in_s));
-        RS_HIP(hipStreamWaitEvent(out_s, ctx->coded[b], 0));
-        for (const Xfer &x : out)
-            RS_HIP(hipMemcpyAsync(staged ? mir + x.off : x.host, dev + x.off, x.n, hipMemcpyDeviceToHost, out_s));
-        RS_HIP(hipEventRecord(ctx->freed[b], out_s));
-        if (staged && !out.empty()) pending.emplace_back(j, out);
-    }
-    while (!pending.empty()) {
-        jobs.clear();
-        rc = queue_drain();
-        if (rc) return rc;
-        pool.copy(jobs);
-    }
-    RS_HIP(hipEventRecord(ctx->ready, out_s));
-    RS_HIP(hipStreamWaitEvent(in_s, ctx->ready, 0));
-    RS_HIP(hipStreamSynchronize(in_s));
-    return RS_OK;
-}
+using namespace rsamd::host;
 
 // Stage [offset, offset+count) of the host shards (slot-indexed), run every
 // launch group of `plans`, copy results back.
@@ -1003,40 +572,9 @@ int rs_codec_decode_matrix(const rs_codec *c, const uint8_t *present, int nshard
     return RS_OK;
 }
 
-const char *rs_last_error_message(void) { return t_err.c_str(); }
+const char *rs_last_error_message(void) { return rsamd::host::last_error(); }
 
-void rs_thread_release(void) {
-    int cur = 0;
-    (void)hipGetDevice(&cur);
-    for (auto &kv : t_ctx) {
-        ThreadCtx *c = kv.second;
-        (void)hipSetDevice(kv.first);
-        if (c->stream) (void)hipStreamDestroy(c->stream);
-        if (c->stream2) (void)hipStreamDestroy(c->stream2);
-        if (c->stream3) (void)hipStreamDestroy(c->stream3);
-        if (c->ready) (void)hipEventDestroy(c->ready);
-        for (int b = 0; b < kStageBufs; ++b) {
-            if (c->coded[b]) (void)hipEventDestroy(c->coded[b]);
-            if (c->freed[b]) (void)hipEventDestroy(c->freed[b]);
-            if (c->loaded[b]) (void)hipEventDestroy(c->loaded[b]);
-        }
-        if (c->mirror) (void)hipHostFree(c->mirror);
-        if (c->stage) (void)hipFree(c->stage);
-        if (c->plan) (void)hipFree(c->plan);
-        if (c->flag) (void)hipFree(c->flag);
-        if (c->file) (void)hipFree(c->file);
-        if (c->zc) (void)hipHostFree(c->zc);
-        for (MaskedSlot &sl : c->masked) {
-            if (sl.done) (void)hipEventSynchronize(sl.done);
-            if (sl.dev) (void)hipFree(sl.dev);
-            if (sl.host) (void)hipHostFree(sl.host);
-            if (sl.done) (void)hipEventDestroy(sl.done);
-        }
-        delete c;
-    }
-    t_ctx.clear();
-    (void)hipSetDevice(cur);
-}
+void rs_thread_release(void) { rsamd::host::release_thread_contexts(); }
 
 int rs_device_count(void) {
     int n = 0;

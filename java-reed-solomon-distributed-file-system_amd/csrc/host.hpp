@@ -1,0 +1,121 @@
+// host.hpp -- host side of the C-ABI's host-buffer entry points: error text,
+// the per-(thread, device) staging context, page-locking of caller buffers
+// and the chunked H2D -> kernels -> D2H pipeline (host.cpp).  capi.cpp builds
+// every host-buffer call of include/rs_amd.h on these.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <functional>
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace rsamd {
+namespace host {
+
+// ---- errors: the thread's last message (rs_last_error_message) ------------
+int fail(int code, const std::string &msg);
+int hip_fail(hipError_t e, const char *where);
+const char *last_error();
+
+#define RS_HIP(call)                                                  \
+    do {                                                              \
+        hipError_t e_ = (call);                                       \
+        if (e_ != hipSuccess) return ::rsamd::host::hip_fail(e_, #call); \
+    } while (0)
+
+// ---- per-(thread, device) context ------------------------------------------
+// Per-call staging of rs_decode_batch_masked_dev (stripe pattern ids or
+// bitmasks, plus records on the dedupe path): pinned host + device bytes,
+// reused only after `done` (recorded on the caller's stream behind the
+// call's kernels) has completed.
+struct MaskedSlot {
+    uint8_t *dev = nullptr;
+    size_t dev_cap = 0;
+    uint8_t *host = nullptr;
+    size_t host_cap = 0;
+    hipEvent_t done = nullptr;
+};
+
+constexpr int kStageBufs = 3;  // staging buffers of the host-buffer pipeline
+
+struct ThreadCtx {
+    hipStream_t stream = nullptr;   // host pipeline: kernels, in chunk order
+    hipStream_t stream2 = nullptr;  // host pipeline: D2H copies, in chunk order
+    hipStream_t stream3 = nullptr;  // host pipeline: H2D copies, in chunk order
+    hipEvent_t ready = nullptr;     // joins stream2 back into stream
+    hipEvent_t coded[kStageBufs] = {};   // buffer b's kernels done (stream -> stream2)
+    hipEvent_t freed[kStageBufs] = {};   // buffer b's D2H done (stream2 -> stream3, and the host)
+    hipEvent_t loaded[kStageBufs] = {};  // buffer b's H2D done (stream3 -> stream; its pinned mirror may be refilled)
+    uint8_t *stage = nullptr;       // kStageBufs device staging buffers
+    size_t stage_cap = 0;
+    uint8_t *mirror = nullptr;      // their pinned host mirrors (pageable callers only)
+    size_t mirror_cap = 0;
+    uint8_t *plan = nullptr;   // per-call plan images (rs_code_some_shards)
+    size_t plan_cap = 0;
+    int *flag = nullptr;       // verify result
+    uint8_t *file = nullptr;   // file staging (rs_file_encode / rs_file_decode)
+    size_t file_cap = 0;
+    uint8_t *zc = nullptr;      // small calls: coherent, device-mapped host buffer the kernels use directly
+    uint8_t *zc_dev = nullptr;  // its device address
+    size_t zc_cap = 0;
+    // rs_decode_batch_masked_dev: two staging slots used in turn, so a call's
+    // host-side preparation overlaps the previous call's kernels.
+    MaskedSlot masked[2];
+    int masked_next = 0;
+};
+
+int need_device();
+// The calling thread's context on its current device (created on first use).
+int thread_ctx(ThreadCtx **out);
+// Frees every context of the calling thread (rs_thread_release).
+void release_thread_contexts();
+// Device / pinned-host buffers that only grow.
+int grow(uint8_t **buf, size_t *cap, size_t want);
+int grow_pinned(uint8_t **buf, size_t *cap, size_t want);
+
+// ---- the chunked pipeline --------------------------------------------------
+// Bytes per slot per chunk for a call of `total` bytes per slot and `nslots`
+// slots per buffer.
+size_t chunk_bytes(size_t total, int nslots, bool pinned);
+// True when every non-null pointer is page-locked host memory known to HIP.
+bool all_pinned(const uint8_t *const *ptrs, int n);
+inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Page-locks pageable caller ranges for the duration of one pipelined call
+// (host.cpp: a process-wide, reference-counted registry of page ranges).
+class HostRegistration {
+public:
+    HostRegistration() = default;
+    HostRegistration(const HostRegistration &) = delete;
+    HostRegistration &operator=(const HostRegistration &) = delete;
+    ~HostRegistration();
+    // All or nothing: false (and nothing held) if any range cannot be locked.
+    bool lock(const std::vector<std::pair<const uint8_t *, size_t>> &ranges);
+
+private:
+    std::vector<uintptr_t> held_;  // registry keys this call references
+};
+
+// One host <-> device transfer of a chunk: host bytes [host, host + n) and
+// bytes [off, off + n) of the chunk's staging buffer.
+struct Xfer {
+    uint8_t *host;
+    size_t off;
+    size_t n;
+};
+using ChunkIo = std::function<void(size_t j, std::vector<Xfer> *in, std::vector<Xfer> *out)>;
+using ChunkCode = std::function<int(size_t j, uint8_t *buf, hipStream_t s)>;
+
+// Runs n_chunks chunks of buf_bytes each: io(j) names chunk j's inputs and
+// outputs, code(j) enqueues its kernels on the given stream.  Returns once
+// every output has reached host memory -- also on an error, so no copy into
+// or out of caller memory is still in flight when the caller gets control.
+int run_chunks(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinned, const ChunkIo &io,
+               const ChunkCode &code);
+
+}  // namespace host
+}  // namespace rsamd

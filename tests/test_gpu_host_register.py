@@ -1,5 +1,5 @@
 """GPU tests of the host-buffer pipeline's per-call page-locking
-(capi.cpp HostRegistration): pageable caller ranges are registered with
+(host.cpp HostRegistration): pageable caller ranges are registered with
 hipHostRegister for the duration of a pipelined call, all or nothing, with the
 pinned mirrors as the fallback.  Registration collisions must never change a
 byte: threads sharing the same input arrays, shards that are slices of one

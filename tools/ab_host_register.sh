@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of page-locking pageable caller buffers per call (capi.cpp
+# A/B of page-locking pageable caller buffers per call (host.cpp
 # HostRegistration): GPU tests, then bench.py's host-inclusive legs with
 # RSAMD_HOST_REGISTER=0 (pinned mirrors + host memcpy) and the default, twice.
 set -o pipefail

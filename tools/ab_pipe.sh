@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of the host pipeline's stream layout and chunk count (capi.cpp
+# A/B of the host pipeline's stream layout and chunk count (host.cpp
 # run_chunks): bench.py's host-inclusive legs under each setting, twice.
 # Usage (via gpurun):  bash tools/ab_pipe.sh
 set -o pipefail
