@@ -98,6 +98,7 @@ void release_thread_contexts() {
             if (sl.dev) (void)hipFree(sl.dev);
             if (sl.host) (void)hipHostFree(sl.host);
             if (sl.done) (void)hipEventDestroy(sl.done);
+            if (sl.uploaded) (void)hipEventDestroy(sl.uploaded);
         }
         delete c;
     }

@@ -31,13 +31,16 @@ const char *last_error();
 // Per-call staging of rs_decode_batch_masked_dev (stripe pattern ids or
 // bitmasks, plus records on the dedupe path): pinned host + device bytes,
 // reused only after `done` (recorded on the caller's stream behind the
-// call's kernels) has completed.
+// call's kernels) has completed.  The upload runs on the context's H2D
+// stream and the caller's stream waits for `uploaded`, so it overlaps the
+// previous call's kernels instead of queueing behind them.
 struct MaskedSlot {
     uint8_t *dev = nullptr;
     size_t dev_cap = 0;
     uint8_t *host = nullptr;
     size_t host_cap = 0;
     hipEvent_t done = nullptr;
+    hipEvent_t uploaded = nullptr;
 };
 
 constexpr int kStageBufs = 3;  // staging buffers of the host-buffer pipeline

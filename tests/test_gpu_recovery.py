@@ -45,6 +45,26 @@ def test_masked_4_2_every_pattern_mixed(gpu, golden_dir):
     assert np.array_equal(out, batch)
 
 
+@pytest.mark.parametrize("n", [1, 2, 22])
+def test_masked_flag_bytes_any_nonzero(gpu, golden_dir, n):
+    """Host flags are bytes, nonzero = present (capi.cpp presence_bits reads a
+    row of up to 8 flags as one word; the last rows, whose word would run past
+    the array, take the per-byte loop): 1 and 2 stripes stay inside one word,
+    22 stripes cover every 4+2 pattern."""
+    import rsamd
+    g = _golden(golden_dir, "rs_4_2_s4096_b8.npz")
+    pats = [tuple(i not in miss for i in range(6))
+            for e in range(3) for miss in itertools.combinations(range(6), e)][-n:]
+    vals = np.array([1, 2, 0x7F, 0x80, 0xFF, 0x41], np.uint8)
+    flags = np.where(np.array(pats, bool), np.resize(vals, (n, 6)), 0).astype(np.uint8)
+    batch = np.concatenate([g] * 3)[:n]
+    rs = rsamd.ReedSolomon.create(4, 2)
+    assert np.array_equal(_run_masked(rs, batch, flags), batch)
+    flags[-1] = [0x80, 0, 0, 0, 0, 0xFF]  # two present: refused before any launch
+    with pytest.raises(rsamd.IllegalArgumentException, match="^Not enough shards present$"):
+        _run_masked(rs, batch, flags)
+
+
 def test_masked_10_4_and_generic_17_3(gpu, golden_dir):
     import rsamd
     g = _golden(golden_dir, "rs_10_4_s1024_b4.npz")
