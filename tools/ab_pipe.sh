@@ -6,7 +6,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
 SETTINGS=${SETTINGS:-"RSAMD_PIPE_STREAMS=2 RSAMD_PIPE_STREAMS=3 RSAMD_CHUNKS=12 RSAMD_CHUNKS=16"}
-for r in 1 2; do
+for r in $(seq 1 ${ROUNDS:-2}); do
   for s in $SETTINGS; do
     line=$(env "$s" timeout -k 10 120 python3 tools/host_legs.py 2>/dev/null) || { echo "FAILED $s"; exit 1; }
     echo "round $r $s $line"
