@@ -1,9 +1,13 @@
 """Python mirror of the reference client's file <-> shard layout classes.
 
   ReedSolomonEncoder(fileData).encode(); getShards(); getPaddedFileSize() ...
+  ReedSolomonEncoder(filePath, diskPaths).encode(); store()
       client/ReedSolomonEncoder.java:13-109
   ReedSolomonDecoder(shards, shardPresent, byteCntInShard, fileSize).getFileData()
+  ReedSolomonDecoder(filePath, diskPaths, fileSize).decode(); store()
       client/ReedSolomonDecoder.java:13-103
+(Java's overloaded constructors are told apart by the type of the first
+argument: a path string or os.PathLike selects the disk-file form.)
   constants  ConfigVariables.java:4-9  (BLOCK_SIZE 1000, 4 data + 2 parity)
 
 pad + split + encode (and decode + merge + trim) run on the GPU through
@@ -13,12 +17,13 @@ the coding kernels.  Device-resident versions: encode_file_dev / decode_file_dev
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Sequence
 
 import numpy as np
 
 from . import _lib
-from .codec import ReedSolomon, _bools, _Buffers, check
+from .codec import RS_E_INVALID, IllegalArgumentException, ReedSolomon, _bools, _Buffers, check
 from .device import _stream_handle
 
 BLOCK_SIZE = 1000         # ConfigVariables.BLOCK_SIZE
@@ -52,11 +57,25 @@ def file_encode_into(codec: ReedSolomon, file_data: np.ndarray, shards_out: Sequ
                                      len(shards_out), b.lens))
 
 
-class ReedSolomonEncoder:
-    """client/ReedSolomonEncoder.java (the in-memory constructor, :27-30)."""
+def _is_path(x) -> bool:
+    return isinstance(x, (str, os.PathLike))
 
-    def __init__(self, fileData: bytes, data_shards: int = DATA_SHARD_COUNT,
-                 parity_shards: int = PARITY_SHARD_COUNT, block: int = BLOCK_SIZE):
+
+class ReedSolomonEncoder:
+    """client/ReedSolomonEncoder.java: ReedSolomonEncoder(byte[] fileData)
+    (:27-30), or ReedSolomonEncoder(String filePath, String[] diskPaths)
+    (:32-41), which reads the file and names the k+m shard files store()
+    writes (:43-54)."""
+
+    def __init__(self, fileData, data_shards=DATA_SHARD_COUNT, parity_shards: int = PARITY_SHARD_COUNT,
+                 block: int = BLOCK_SIZE, diskPaths: Sequence = None):
+        self._file_path, self._disk_paths = None, None
+        if _is_path(fileData):  # (filePath, diskPaths): Files.readAllBytes(Path.of(filePath))
+            if not isinstance(data_shards, int):  # diskPaths given positionally, as in the Java
+                diskPaths, data_shards = data_shards, DATA_SHARD_COUNT
+            self._file_path, self._disk_paths = fileData, list(diskPaths)
+            with open(fileData, "rb") as f:
+                fileData = f.read()
         self._file = bytes(fileData)
         self._k, self._m, self._block = data_shards, parity_shards, block
         self._shards = None
@@ -75,6 +94,16 @@ class ReedSolomonEncoder:
 
     def getShards(self):
         return self._shards
+
+    def store(self) -> None:
+        """Each shard to its disk path (ReedSolomonEncoder.java:43-54; the Java
+        prints and carries on when a write fails)."""
+        for path, shard in zip(self._disk_paths, self._shards):
+            try:
+                with open(path, "wb") as f:
+                    f.write(shard.tobytes())
+            except OSError as e:
+                print(e)
 
     def getPaddedFileSize(self) -> int:
         return self._padded
@@ -107,20 +136,66 @@ def file_decode_into(codec: ReedSolomon, shards: Sequence, shardPresent: Sequenc
 
 
 class ReedSolomonDecoder:
-    """client/ReedSolomonDecoder.java, the shards constructor (:33-39):
-    decodeMissing fills the absent shards IN PLACE (as the Java does), then the
-    data shards are merged and trimmed to fileSize."""
+    """client/ReedSolomonDecoder.java.
 
-    def __init__(self, shards: Sequence, shardPresent: Sequence, byteCntInShard: int, fileSize: int,
+    ReedSolomonDecoder(shards, shardPresent, byteCntInShard, fileSize) (:33-39)
+    decodes at once: decodeMissing fills the absent shards IN PLACE (as the
+    Java does), then the data shards are merged and trimmed to fileSize.
+
+    ReedSolomonDecoder(filePath, diskPaths, fileSize) (:41-48) decodes on
+    decode() (:70-81): every readable disk file is a present shard
+    (retrieveShards, :50-60), the others are zero-filled and rebuilt; store()
+    writes the file (:83-90)."""
+
+    def __init__(self, shards, shardPresent, byteCntInShard: int = None, fileSize: int = None,
                  data_shards: int = DATA_SHARD_COUNT, parity_shards: int = PARITY_SHARD_COUNT,
                  block: int = BLOCK_SIZE):
-        codec = _codec(data_shards, parity_shards)
+        self._k, self._m, self._block = data_shards, parity_shards, block
+        self._data = None
+        if _is_path(shards):  # (filePath, diskPaths, fileSize)
+            self._file_path, self._disk_paths, self._file_size = shards, list(shardPresent), byteCntInShard
+            self._shards, self._present, self._byte_cnt = [None] * len(self._disk_paths), [False] * len(
+                self._disk_paths), 0
+            return
+        self._decode(shards, shardPresent, byteCntInShard, fileSize)
+
+    def _decode(self, shards, shardPresent, byteCntInShard, fileSize):
+        codec = _codec(self._k, self._m)
         b = _Buffers(shards)
         p = _bools(shardPresent)
         out = np.zeros(max(1, fileSize), dtype=np.uint8)
         check(_lib.load().rs_file_decode(codec.handle, b.ptrs, len(shards), b.lens, p.ctypes.data_as(_lib.u8p),
-                                         byteCntInShard, block, out.ctypes.data_as(_lib.u8p), fileSize))
+                                         byteCntInShard, self._block, out.ctypes.data_as(_lib.u8p), fileSize))
         self._data = out[:fileSize].tobytes()
+
+    def retrieveShards(self) -> None:
+        """Read every disk file; a readable one is a present shard and sets
+        byteCntInShard (the last one read wins, as in the Java)."""
+        for i, path in enumerate(self._disk_paths):
+            try:
+                with open(path, "rb") as f:
+                    self._shards[i] = np.frombuffer(f.read(), dtype=np.uint8).copy()
+            except OSError:
+                continue
+            self._present[i] = True
+            self._byte_cnt = len(self._shards[i])
+
+    def decode(self) -> None:
+        self.retrieveShards()
+        if self._byte_cnt == 0:
+            raise IllegalArgumentException(RS_E_INVALID, "There is not enough data to decode")
+        for i in range(len(self._shards)):
+            if self._shards[i] is None:
+                self._shards[i] = np.zeros(self._byte_cnt, dtype=np.uint8)
+        self._decode(self._shards, self._present, self._byte_cnt, self._file_size)
+
+    def store(self) -> None:
+        """The decoded file to filePath (ReedSolomonDecoder.java:83-90)."""
+        try:
+            with open(self._file_path, "wb") as f:
+                f.write(self._data)
+        except OSError as e:
+            print(e)
 
     def getFileData(self) -> bytes:
         return self._data
