@@ -852,6 +852,30 @@ int rs_fill_synthetic_dev(uint8_t *dev_base, int data_shards, size_t n_stripes, 
     return RS_OK;
 }
 
+int rs_dev_alloc(void **out, size_t bytes, int contiguous, int *got_contiguous) {
+    if (!out) return fail(RS_E_INVALID, "out must not be NULL");
+    *out = nullptr;
+    if (got_contiguous) *got_contiguous = 0;
+    int rc = need_device();
+    if (rc) return rc;
+    const size_t n = std::max<size_t>(bytes, 1);
+    if (contiguous) {
+        if (hipExtMallocWithFlags(out, n, hipDeviceMallocContiguous) == hipSuccess) {
+            if (got_contiguous) *got_contiguous = 1;
+            return RS_OK;
+        }
+        (void)hipGetLastError();  // no contiguous range of that size: plain hipMalloc
+        *out = nullptr;
+    }
+    RS_HIP(hipMalloc(out, n));
+    return RS_OK;
+}
+
+int rs_dev_free(void *ptr) {
+    if (ptr) RS_HIP(hipFree(ptr));
+    return RS_OK;
+}
+
 int rs_copy_dev(uint8_t *dst, const uint8_t *src, size_t n, void *stream) {
     if ((!dst || !src) && n) return fail(RS_E_INVALID, "NULL pointer");
     RS_HIP(rsamd::launch_copy(dst, src, n, static_cast<hipStream_t>(stream)));

@@ -58,6 +58,8 @@ SIGNATURES = {
     "rs_fill_synthetic_dev": (C.c_int, [C.c_void_p, C.c_int, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t,
                                         C.c_uint64, C.c_uint64, C.c_void_p]),
     "rs_copy_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
+    "rs_dev_alloc": (C.c_int, [C.POINTER(C.c_void_p), C.c_size_t, C.c_int, C.POINTER(C.c_int)]),
+    "rs_dev_free": (C.c_int, [C.c_void_p]),
 }
 
 _lib = None

@@ -105,6 +105,38 @@ def copy(dst: int, src: int, n: int, stream=None) -> None:
     check(_lib.load().rs_copy_dev(C.c_void_p(dst), C.c_void_p(src), n, C.c_void_p(_stream_handle(stream))))
 
 
+class DeviceBuffer:
+    """HBM for a stripe pool from rs_dev_alloc: one physically contiguous
+    range when contiguous=True and the device has one (else hipMalloc memory;
+    `.contiguous` says which).  Exposes data_ptr() / numel() / device like the
+    torch tensors the other calls here take pointers from; freed by free() or
+    when collected."""
+
+    def __init__(self, nbytes: int, contiguous: bool = True):
+        import torch
+        p, got = C.c_void_p(), C.c_int(0)
+        check(_lib.load().rs_dev_alloc(C.byref(p), nbytes, int(contiguous), C.byref(got)))
+        self._ptr, self.nbytes, self.contiguous = p.value, nbytes, bool(got.value)
+        self.device = torch.device("cuda", torch.cuda.current_device())
+
+    def data_ptr(self) -> int:
+        return self._ptr
+
+    def numel(self) -> int:
+        return self.nbytes
+
+    def free(self) -> None:
+        if self._ptr:
+            check(_lib.load().rs_dev_free(C.c_void_p(self._ptr)))
+            self._ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:  # noqa: BLE001  (interpreter shutdown)
+            pass
+
+
 def device_count() -> int:
     return _lib.load().rs_device_count()
 

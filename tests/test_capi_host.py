@@ -143,6 +143,17 @@ def test_coding_without_device_fails_loudly(native):
     assert all((s == 1).all() for s in sh)
 
 
+def test_dev_alloc_without_device_fails_loudly(native):
+    import ctypes as C
+    if native.rs_device_count() > 0:
+        pytest.skip("a device is visible; covered by the gpu tests")
+    p, got = C.c_void_p(1), C.c_int(7)
+    assert native.rs_dev_alloc(C.byref(p), 1 << 20, 1, C.byref(got)) == -12  # RS_E_NO_DEVICE
+    assert p.value is None and got.value == 0
+    assert native.rs_dev_alloc(None, 16, 1, None) == -10  # RS_E_INVALID: out is NULL
+    assert native.rs_dev_free(None) == 0
+
+
 def test_file_layout_geometry(native, oracle_lib):
     """ReedSolomonEncoder.pad (ReedSolomonEncoder.java:76-85): round up to k*block."""
     import rsamd
