@@ -50,7 +50,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     ap.add_argument("--no-extras", action="store_true", help="skip decode/copy/host-inclusive/CPU legs")
     ap.add_argument("--alloc", choices=["contiguous", "hipmalloc"], default="contiguous",
-                    help="HBM for the stripe batches: rs_dev_alloc contiguous range (default) or torch/hipMalloc")
+                    help="HBM for the headline stripe batch: rs_dev_alloc contiguous range (default) or torch/hipMalloc "
+                         "(the other configs' pools stay hipMalloc: contiguous measured no better there)")
     return ap.parse_args()
 
 
@@ -118,7 +119,7 @@ def main():
         del buf
         torch.cuda.empty_cache()
         if world == 1:  # multi-GPU runs report the scaling line only (the other ranks wait)
-            extra.update(other_configs(torch, rsamd, rdev, dev, stream, args.alloc))
+            extra.update(other_configs(torch, rsamd, rdev, dev, stream))
             extra.update(layout_legs(torch, rsamd, dev, stream))
             cpu = cpu_baseline(k, m, S, args.cpu_seconds)
             extra.update(host_inclusive(rsamd, k, m))
@@ -221,7 +222,7 @@ def device_extras(torch, rs, rdev, buf, lay, stream, k, m, S, B):
     return out
 
 
-def other_configs(torch, rsamd, rdev, dev, stream, alloc="contiguous"):
+def other_configs(torch, rsamd, rdev, dev, stream, alloc="hipmalloc"):
     """BASELINE configs[3] (10+4 x 4 MiB; the per-GPU share of 1024 stripes over
     8 GPUs) and configs[4] (4+2 x 4 KiB x 1 M stripes), encode and decode."""
     from rsamd.device import StripeLayout
