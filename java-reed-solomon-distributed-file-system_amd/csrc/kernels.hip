@@ -559,9 +559,15 @@ hipError_t dispatch_vec(VecArgs a, int nout, Mode mode, hipStream_t s) {
 //   4+2  x 1 MiB + 4 KiB pad   0.62      0.78              0.74
 //   10+4 x 4 MiB + 4 KiB pad   0.75      0.71              0.74
 //
-// The XCD-contiguous remap is the default; rotation wins at 1 MiB shards on
-// 1 MiB-aligned strides and for wide (>= 14-shard) stripes of >= 1 MiB, and
-// loses badly elsewhere (2 MiB, padded strides), so it is used exactly there.  RSAMD_BLOCK_ROT (rotation in chunks, 0 = off)
+// On a physically contiguous pool (rs_dev_alloc; profiles/r1/order_ab/
+// orders_contiguous_pool*.txt, 512k_rotation.txt) the table holds except at
+// 512 KiB, where a quarter-stripe rotation (127 chunks; 3/8 = 191 gives 0.78)
+// reaches 0.809 against 0.791 for the XCD remap (0.787 / 0.785 on hipMalloc).
+//
+// The XCD-contiguous remap is the default; rotation wins at 512 KiB and 1 MiB
+// shards on stripe-aligned strides and for wide (>= 14-shard) stripes of
+// >= 1 MiB, and loses badly elsewhere (2 MiB, padded strides), so it is used
+// exactly there.  RSAMD_BLOCK_ROT (rotation in chunks, 0 = off)
 // and RSAMD_BLOCK_XCD (0 / 1) override the table for A/B runs.  (Remapping
 // within groups of 8 * N blocks instead of the whole launch measured worse.)
 struct BlockOrder {
@@ -576,9 +582,11 @@ BlockOrder block_order(uint32_t chunks, uint32_t total_shards, uint64_t shard_st
         const char *e = std::getenv("RSAMD_BLOCK_XCD");
         return e ? std::atoi(e) : -1;
     }();
-    const bool rotate = (chunks == 1024 && shard_stride % (uint64_t(1) << 20) == 0) ||
+    const bool half = chunks == 512 && shard_stride % (uint64_t(512) << 10) == 0;
+    const bool rotate = (chunks == 1024 && shard_stride % (uint64_t(1) << 20) == 0) || half ||
                         (total_shards >= 14 && chunks >= 1024);
-    const uint32_t rot = env_rot >= 0 ? uint32_t(env_rot) : (rotate ? 3u * chunks / 8u - 1u : 0u);
+    const uint32_t step = half ? chunks / 4u - 1u : 3u * chunks / 8u - 1u;
+    const uint32_t rot = env_rot >= 0 ? uint32_t(env_rot) : (rotate ? step : 0u);
     const bool xcd = env_xcd >= 0 ? env_xcd != 0 : !rotate;
     return BlockOrder{chunks > 1 ? rot % chunks : 0u, xcd ? n_items / 8u : 0u};
 }

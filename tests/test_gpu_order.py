@@ -43,6 +43,7 @@ def _encode_and_check(oracle_lib, k, m, S, B):
 
 @pytest.mark.parametrize("k,m,S,B", [
     (4, 2, 1 << 20, 3),       # 1024 chunks: rotation
+    (4, 2, 512 << 10, 5),     # 512 chunks: quarter-stripe rotation
     (10, 4, 1 << 20, 2),      # wide stripe, 1 MiB: rotation
     (10, 4, 4 << 20, 1),      # wide stripe, 4 MiB: rotation, a single stripe
     (4, 2, 4096, 13),         # XCD remap, 52 blocks: one group of 48 + 4 in place
