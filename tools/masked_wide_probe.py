@@ -1,5 +1,7 @@
+"""Per-stripe-pattern decode (device bitmasks) of 10+4 x 4 MiB x 128 stripes, 4 erasures per stripe
+(random), against the uniform 10+4 decode: fraction of 8 TB/s."""
 import itertools, json, os, sys
-sys.path.insert(0, "/root/repo/java-reed-solomon-distributed-file-system_amd")
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "java-reed-solomon-distributed-file-system_amd"))
 import numpy as np, torch, rsamd
 from rsamd import device as rdev
 from rsamd.device import StripeLayout
