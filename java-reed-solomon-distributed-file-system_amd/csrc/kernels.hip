@@ -620,8 +620,11 @@ hipError_t launch_masked_generic_t(const MaskedArgs &a, hipStream_t s) {
 hipError_t dispatch_masked(const MaskedArgs &a, int ms, hipStream_t s) {
 #define RSAMD_CASE(K, M) \
     if (a.nin == K && ms == M) return launch_masked_t<K, M>(a, s);
+    // Only k = 4 has a compile-time masked kernel: at k = 10 the record-driven
+    // tables spill SGPRs into VGPR lanes (154 VGPRs, 3 waves per SIMD) and the
+    // runtime-k kernel is faster (10+4, 4 erasures per stripe: 0.40 -> 0.63 of
+    // peak; tools/masked_wide_probe.py).
     RSAMD_CASE(4, 1) RSAMD_CASE(4, 2) RSAMD_CASE(4, 3) RSAMD_CASE(4, 4)
-    RSAMD_CASE(10, 1) RSAMD_CASE(10, 2) RSAMD_CASE(10, 3) RSAMD_CASE(10, 4)
 #undef RSAMD_CASE
     switch (ms) {
     case 1: return launch_masked_generic_t<1>(a, s);
