@@ -255,6 +255,11 @@ RS_API int rs_fill_synthetic_dev(uint8_t *dev_base, int data_shards, size_t n_st
  * "measured device copy" the roofline is also quoted against). */
 RS_API int rs_copy_dev(uint8_t *dst, const uint8_t *src, size_t n, void *stream);
 
+/* Process-wide override of the stripe kernels' block order for placement and
+ * order probes: rot = chunk rotation per stripe (0 = none), xcd = 1 for the
+ * XCD-contiguous remap; rot = xcd = -1 restores the measured table. */
+RS_API int rs_debug_block_order(int rot, int xcd);
+
 #ifdef __cplusplus
 }
 #endif

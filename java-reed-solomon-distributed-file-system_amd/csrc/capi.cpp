@@ -876,6 +876,11 @@ int rs_dev_free(void *ptr) {
     return RS_OK;
 }
 
+int rs_debug_block_order(int rot, int xcd) {
+    rsamd::set_debug_block_order(rot, xcd);
+    return RS_OK;
+}
+
 int rs_copy_dev(uint8_t *dst, const uint8_t *src, size_t n, void *stream) {
     if ((!dst || !src) && n) return fail(RS_E_INVALID, "NULL pointer");
     RS_HIP(rsamd::launch_copy(dst, src, n, static_cast<hipStream_t>(stream)));

@@ -27,6 +27,7 @@
 #include "kernels.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <climits>
 #include <cstdlib>
 
@@ -573,6 +574,8 @@ hipError_t dispatch_vec(VecArgs a, int nout, Mode mode, hipStream_t s) {
 struct BlockOrder {
     uint32_t rot, xcd_span;
 };
+std::atomic<int> g_order_rot{-1}, g_order_xcd{-1};  // rs_debug_block_order: -1 = the table
+
 BlockOrder block_order(uint32_t chunks, uint32_t total_shards, uint64_t shard_stride, uint32_t n_items) {
     static const int env_rot = [] {
         const char *e = std::getenv("RSAMD_BLOCK_ROT");
@@ -582,6 +585,11 @@ BlockOrder block_order(uint32_t chunks, uint32_t total_shards, uint64_t shard_st
         const char *e = std::getenv("RSAMD_BLOCK_XCD");
         return e ? std::atoi(e) : -1;
     }();
+    const int dbg_rot = g_order_rot.load(std::memory_order_relaxed), dbg_xcd = g_order_xcd.load(std::memory_order_relaxed);
+    if (dbg_rot >= 0 || dbg_xcd >= 0) {  // rs_debug_block_order (placement probes)
+        const uint32_t r = dbg_rot > 0 ? uint32_t(dbg_rot) % std::max(1u, chunks) : 0u;
+        return BlockOrder{chunks > 1 ? r : 0u, dbg_xcd > 0 ? n_items / 8u : 0u};
+    }
     const bool half = chunks == 512 && shard_stride % (uint64_t(512) << 10) == 0;
     const bool rotate = (chunks == 1024 && shard_stride % (uint64_t(1) << 20) == 0) || half ||
                         (total_shards >= 14 && chunks >= 1024);
@@ -721,6 +729,11 @@ hipError_t launch_gf(const Geometry &g, const DevPlan &p, Mode mode, int *mismat
     const size_t tail = g.len % 16;
     if (tail) return launch_bytes(g, p, g.col0 + size_t(nvec) * 16, tail, mode, mismatch, s);
     return hipSuccess;
+}
+
+void set_debug_block_order(int rot, int xcd) {
+    g_order_rot.store(rot);
+    g_order_xcd.store(xcd);
 }
 
 hipError_t launch_fill_synthetic(uint8_t *base, int k, size_t n_stripes, size_t shard_len, size_t shard_stride,

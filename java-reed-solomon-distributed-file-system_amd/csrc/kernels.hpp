@@ -71,5 +71,8 @@ hipError_t launch_fill_synthetic(uint8_t *base, int k, size_t n_stripes, size_t 
                                  uint64_t stripe0, hipStream_t s);
 
 hipError_t launch_copy(uint8_t *dst, const uint8_t *src, size_t n, hipStream_t s);
+// Overrides the block-order table of the stripe kernels (rot in chunks, xcd 0/1;
+// both -1 = the table).  Placement probes only (rs_debug_block_order).
+void set_debug_block_order(int rot, int xcd);
 
 }  // namespace rsamd

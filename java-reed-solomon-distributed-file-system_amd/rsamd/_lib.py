@@ -60,6 +60,7 @@ SIGNATURES = {
     "rs_copy_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     "rs_dev_alloc": (C.c_int, [C.POINTER(C.c_void_p), C.c_size_t, C.c_int, C.POINTER(C.c_int)]),
     "rs_dev_free": (C.c_int, [C.c_void_p]),
+    "rs_debug_block_order": (C.c_int, [C.c_int, C.c_int]),
 }
 
 _lib = None
