@@ -339,6 +339,13 @@ __global__ void __launch_bounds__(kWave) gf_masked_kernel(MaskedArgs a) {
     const uint32_t *tabs = reinterpret_cast<const uint32_t *>(rec + a.rec_tabs);
     uint8_t *sb = a.base + uint64_t(stripe) * a.stripe_stride + uint64_t(v) * 16;
     RSAMD_CODE_VECTORS(K, MS, tabs, in_idx, out_idx, a.shard_stride)
+    // Pin the accumulators before the stores: their only uses are the
+    // `p < nout` stores, and without this LLVM sinks each output's whole
+    // perm/fold chain into its store block, past every table stage, so all
+    // K*MS*5 table dwords are live at once (10+4: 106 SGPRs, spilled into
+    // VGPR lanes, 154 VGPRs, 0.40 of peak; pinned: 73 VGPRs, no spill).
+#pragma unroll
+    for (int p = 0; p < MS; ++p) asm volatile("" : "+v"(acc[p]));
 #pragma unroll
     for (int p = 0; p < MS; ++p)
         if (p < nout) __builtin_nontemporal_store(acc[p], reinterpret_cast<u32x4 *>(sb + out_off[p]));
@@ -625,14 +632,24 @@ hipError_t launch_masked_generic_t(const MaskedArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// RSAMD_MASKED_WIDE=0 routes k = 10 to the runtime-k masked kernel (A/B runs).
+bool masked_wide_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("RSAMD_MASKED_WIDE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 hipError_t dispatch_masked(const MaskedArgs &a, int ms, hipStream_t s) {
 #define RSAMD_CASE(K, M) \
     if (a.nin == K && ms == M) return launch_masked_t<K, M>(a, s);
-    // Only k = 4 has a compile-time masked kernel: at k = 10 the record-driven
-    // tables spill SGPRs into VGPR lanes (154 VGPRs, 3 waves per SIMD) and the
-    // runtime-k kernel is faster (10+4, 4 erasures per stripe: 0.40 -> 0.63 of
-    // peak; tools/masked_wide_probe.py).
+    // k = 10 (10+4, 4 erasures per stripe, tools/masked_wide_probe.py):
+    // 0.66 of peak, against 0.62 for the runtime-k kernel.
     RSAMD_CASE(4, 1) RSAMD_CASE(4, 2) RSAMD_CASE(4, 3) RSAMD_CASE(4, 4)
+    if (masked_wide_enabled()) {
+        RSAMD_CASE(10, 1) RSAMD_CASE(10, 2) RSAMD_CASE(10, 3) RSAMD_CASE(10, 4)
+    }
 #undef RSAMD_CASE
     switch (ms) {
     case 1: return launch_masked_generic_t<1>(a, s);

@@ -113,8 +113,11 @@ class ReedSolomon:
     def __del__(self):
         h = getattr(self, "_h", None)
         if h:
-            _lib.load().rs_codec_destroy(h)
             self._h = None
+            try:
+                _lib.load().rs_codec_destroy(h)
+            except (TypeError, AttributeError):
+                pass  # interpreter shutdown: module globals already torn down
 
     @property
     def handle(self):
