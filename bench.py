@@ -244,6 +244,23 @@ def other_configs(torch, rsamd, rdev, dev, stream, alloc="hipmalloc"):
         flag = torch.zeros(1, dtype=torch.int32, device=dev)
         rdev.verify(rs, buf.data_ptr(), lay, flag.data_ptr(), stream)
         out[name + "_verified"] = int(flag.item()) == 0
+        # row f3 (isParityCorrect) on the same batch: (k+m)*S*B bytes read
+        t = timed(torch, stream, lambda: rdev.verify(rs, buf.data_ptr(), lay, flag.data_ptr(), stream), 5)
+        out[name + "_verify_hbm_frac"] = round((k + m) * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
+        if name == "cfg3_10p4_4MiB_x128":
+            # row f2 for the wide code: 4 random erasures per stripe, device bitmasks, one launch
+            import numpy as np
+            rng = np.random.default_rng(0)
+            present = np.ones((B, k + m), dtype=bool)
+            for t_ in range(B):
+                present[t_, rng.choice(k + m, 4, replace=False)] = False
+            bits = torch.from_numpy(rdev.presence_bits(present).view(np.int32)).to(dev)
+            alg = (k * B + int((~present).sum())) * S
+            t = timed(torch, stream, lambda: rdev.decode_masked_bits(rs, buf.data_ptr(), bits.data_ptr(), lay, 0,
+                                                                     stream), 5)
+            out[name + "_decode_masked_bits_hbm_frac"] = round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)
+            rdev.verify(rs, buf.data_ptr(), lay, flag.data_ptr(), stream)
+            out[name + "_decode_masked_bits_verified"] = int(flag.item()) == 0
         if name.startswith("cfg4"):
             # row f2: a random presence pattern per stripe (<= 2 erasures), one launch
             import itertools

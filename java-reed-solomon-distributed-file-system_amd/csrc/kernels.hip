@@ -229,6 +229,10 @@ __global__ void __launch_bounds__(kWave) gf_vec_kernel(VecArgs a) {
     if (v >= a.nvec) return;
     uint8_t *sb = a.base + uint64_t(stripe) * a.stripe_stride + uint64_t(v) * 16;
     RSAMD_CODE_VECTORS(K, M, a.tabs, a.in_idx, a.out_idx, a.shard_stride)
+    if (VERIFY) {  // as in gf_masked_kernel: keep the compares' inputs from being sunk
+#pragma unroll
+        for (int p = 0; p < M; ++p) asm volatile("" : "+v"(acc[p]));
+    }
 #pragma unroll
     for (int p = 0; p < M; ++p) emit<VERIFY>(sb + out_off[p], acc[p], a.mismatch);
 }
