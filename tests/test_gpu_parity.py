@@ -140,6 +140,33 @@ def test_decode_generic_17_3(gpu, golden_dir):
         assert np.array_equal(download(dev, B, T, S, stride), shards), miss
 
 
+@pytest.mark.parametrize("name,k,m", [("rs_4_2_s4096_b8.npz", 4, 2), ("rs_10_4_s1024_b4.npz", 10, 4)])
+def test_verify_flags_every_position(gpu, golden_dir, name, k, m):
+    """isParityCorrect (ReedSolomon.java:115-164) on the vector kernels: a single flipped bit in
+    any parity shard, data shard, first/middle/last vector or stripe is caught, and the clean
+    golden batch passes.  Covers every output slot of gf_vec_kernel<K,M,true> (10+4 included,
+    whose accumulators are pinned before the compares)."""
+    torch = _torch()
+    import rsamd
+    from rsamd import device
+    shards, _ = golden(golden_dir, name)
+    B, T, S = shards.shape
+    rs = rsamd.ReedSolomon.create(k, m)
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    st = torch.cuda.current_stream()
+    dev, stride = upload(shards)
+    device.verify(rs, dev.data_ptr(), layout(B, T, S, stride), flag.data_ptr(), st)
+    assert int(flag.item()) == 0
+    for t, shard, col, bit in [(0, k, 0, 0), (B - 1, k + m - 1, S - 1, 7), (B // 2, k + 1, S // 2, 3),
+                               (1, 0, 17, 5), (B - 1, k - 1, S - 16, 1)] + [(2 % B, k + p, 16 * p + 5, p) for p in range(m)]:
+        bad = shards.copy()
+        bad[t, shard, col] ^= 1 << bit
+        dev, stride = upload(bad)
+        flag.zero_()
+        device.verify(rs, dev.data_ptr(), layout(B, T, S, stride), flag.data_ptr(), st)
+        assert int(flag.item()) == 1, (t, shard, col, bit)
+
+
 def test_verify_batch(gpu, golden_dir):
     torch = _torch()
     import rsamd
