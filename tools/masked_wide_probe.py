@@ -27,5 +27,10 @@ def timed(fn, it=5):
 alg = (k * B + int((~present).sum())) * S
 t = timed(lambda: rdev.decode_masked_bits(rs, buf.data_ptr(), bits.data_ptr(), lay, 0, st))
 print(json.dumps({"masked_bits_10_4": round(alg / t / 8e12, 4)}))
+# the uniform pattern {0,1,2,3} through the same masked kernel: separates the
+# per-stripe record chain from the cost of random patterns
+ub = torch.from_numpy(rdev.presence_bits(np.tile(np.arange(14) >= 4, (B, 1))).view(np.int32)).cuda()
+t = timed(lambda: rdev.decode_masked_bits(rs, buf.data_ptr(), ub.data_ptr(), lay, 0, st))
+print(json.dumps({"masked_bits_uniform_pattern_10_4": round(14 * S * B / t / 8e12, 4)}))
 t = timed(lambda: rdev.decode(rs, buf.data_ptr(), [i >= 4 for i in range(14)], lay, st))
 print(json.dumps({"uniform_decode_10_4": round(14 * S * B / t / 8e12, 4)}))
