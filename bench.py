@@ -190,7 +190,12 @@ def alloc_note(contiguous):
 
 def timed(torch, stream, fn, iters):
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    fn()
+    # 3 untimed calls: the first builds any host-side plans, and after that host
+    # work the GPU has idled and its clocks need a few ms of load to come back
+    # (a 10+4 leg timed right after 1 warm-up call read 0.64 instead of 0.72,
+    # profiles/r1/masked/masked_pattern_order.txt)
+    for _ in range(3):
+        fn()
     torch.cuda.synchronize()
     s.record(stream)
     for _ in range(iters):
