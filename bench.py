@@ -190,13 +190,18 @@ def alloc_note(contiguous):
 
 def timed(torch, stream, fn, iters):
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    # 3 untimed calls: the first builds any host-side plans, and after that host
-    # work the GPU has idled and its clocks need a few ms of load to come back
-    # (a 10+4 leg timed right after 1 warm-up call read 0.64 instead of 0.72,
-    # profiles/r1/masked/masked_pattern_order.txt)
-    for _ in range(3):
-        fn()
+    # Untimed calls: the first builds any host-side plans; after that host work
+    # the GPU has idled and needs some tens of ms of load before it runs at its
+    # steady rate (a 10+4 masked leg read 0.64-0.68 of peak over its first ~8
+    # calls, then 0.71-0.75 per call: profiles/r1/masked/masked_per_call.txt).
+    # So warm up for at least 3 calls AND 50 ms.
+    fn()
     torch.cuda.synchronize()
+    t0, n = time.perf_counter(), 0
+    while n < 2 or time.perf_counter() - t0 < 0.05:
+        fn()
+        torch.cuda.synchronize()
+        n += 1
     s.record(stream)
     for _ in range(iters):
         fn()

@@ -30,6 +30,14 @@ for P in [int(x) for x in os.environ.get("PROBE_P", "1,2,4,16,128,1001").split("
     for _ in range(5): fn()
     e.record(st); torch.cuda.synchronize()
     t = s.elapsed_time(e) / 5 * 1e-3
+    if os.environ.get("PROBE_PER_ITER"):  # one event pair per call: is the slow leg slow throughout?
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(11)]
+        ev[0].record(st)
+        for i in range(10):
+            fn(); ev[i + 1].record(st)
+        torch.cuda.synchronize()
+        res[f"P{P}#{len(res)}_per_call"] = [round(14 * S * B / (ev[i].elapsed_time(ev[i + 1]) * 1e-3) / 8e12, 3)
+                                            for i in range(10)]
     rdev.verify(rs, buf.data_ptr(), lay, flag.data_ptr(), st)
     assert int(flag.item()) == 0
     res[f"P{P}#{len(res)}"] = round(14 * S * B / t / 8e12, 4)
