@@ -67,6 +67,24 @@ def main():
         fn = lambda: rdev.decode_masked_bits(rs, buf.data_ptr(), bits.data_ptr(), lay, 0, st)  # noqa: E731
         alg = (4 * int((~present).any(axis=1).sum()) + int((~present).sum())) * S
         kernel = "gf_masked_kernel<4, 2>"
+    elif name == "ver104":
+        k, m, S, B = 10, 4, 4 << 20, 128
+        rs, lay, buf = stripes(k, m, S, B)
+        flag = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+        fn = lambda: rdev.verify(rs, buf.data_ptr(), lay, flag.data_ptr(), st)  # noqa: E731
+        alg = (k + m) * S * B  # read-only
+        kernel = "gf_vec_kernel<10, 4, true>"
+    elif name == "maskbits104":
+        k, m, S, B = 10, 4, 4 << 20, 128
+        rs, lay, buf = stripes(k, m, S, B)
+        rng = np.random.default_rng(0)
+        present = np.ones((B, k + m), dtype=bool)
+        for t in range(B):
+            present[t, rng.choice(k + m, 4, replace=False)] = False
+        bits = torch.from_numpy(rdev.presence_bits(present).view(np.int32)).to("cuda:0")
+        fn = lambda: rdev.decode_masked_bits(rs, buf.data_ptr(), bits.data_ptr(), lay, 0, st)  # noqa: E731
+        alg = (k * B + int((~present).sum())) * S
+        kernel = "gf_masked_kernel<10, 4>"
     elif name in ("fenc", "fdec_05"):
         rs = rsamd.ReedSolomon.create(4, 2)
         n = (4 << 30) // 4000 * 4000
