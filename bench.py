@@ -4,27 +4,40 @@
 Workload (BASELINE.json configs[1]): 4 data + 2 parity shards, 1 MiB per shard,
 4096 stripes per GPU, all resident in HBM ([stripe][shard][1 MiB], 24 GiB per
 GPU) before timing starts.  One step = one rs_encode_batch_dev call over the
-whole batch (one kernel launch).  N GPUs = N independent processes, each
-encoding its own 4096 stripes (stripes are independent: no collective on the
-data path; torch.distributed is used only for the timing barrier and the max
-over ranks).  value = user data protected per second over all GPUs =
-N * k * S * B * steps / t  (GiB/s).
+whole batch (one kernel launch).  N GPUs = N processes, one per GPU, each
+encoding its own 4096 stripes (stripes are independent, ReedSolomon.java:90-104:
+no collective on the data path; torch.distributed only lines the ranks up for
+timing and reduces a few scalars).  value = user data protected per second over
+all GPUs = N * k * S * B * steps / t  (GiB/s), t = the slowest rank's time.
 
-Also reported (rank 0): decode rates for 1 and 2 erasures, the device copy
-kernel rate, the roofline of the encode kernel (HIP events on the launch
-stream), and the CPU baseline -- the oracle's scalar restatement of the
-reference loop (InputOutputByteTableCodingLoop.java:12-44) timed on a bounded
-sample on this host.
+Legs every rank runs at every N (whole-job aggregates, slowest rank's time):
+  * 4+2 decode {0,1} on the same batch (BASELINE configs[2], weak scaling);
+  * BASELINE configs[3] strong-scaled: 10+4 x 4 MiB, 1024 stripes in all, split
+    by stripe index (128 per GPU at N=8), encode and {0,1,2,3} decode;
+  * a sustained >= 5 s back-to-back encode with the GPU clocks sampled;
+  * at N>1: the host-inclusive rate with every rank calling the JNI-facing
+    host API at once.
+At N=1 rank 0 also reports the per-GPU legs (more erasure patterns, verify,
+copy kernel, configs[4], the fused file layout, host-inclusive rates,
+configs[0]) and the CPU baseline -- the oracle's scalar restatement of the
+reference loop (InputOutputByteTableCodingLoop.java:12-44) timed on bounded
+samples on this host, 1 thread and the host's CPU share.
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
-      (N > 1 is launched by torch.distributed.run, one rank per GPU)
+      --gpus N > 1 without WORLD_SIZE in the environment: this process starts
+      torch.distributed.run with N ranks (before anything touches the GPU) and
+      exits with its status; under a launcher WORLD_SIZE must equal N.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -35,9 +48,10 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 SEED = 0x5EED
 METRIC = "RS encode/decode GiB/s device-resident, 4+2×1 MiB stripes, at 1/2/4/8 GPU"
+CFG3_STRIPES = 1024  # BASELINE configs[3]: 10+4 x 4 MiB, 1024 stripes over the GPUs
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -47,16 +61,128 @@ def parse():
     ap.add_argument("--shard-bytes", type=int, default=1 << 20)
     ap.add_argument("--stripes", type=int, default=4096, help="stripes per GPU")
     ap.add_argument("--pad", type=int, default=0, help="bytes of padding between shards (layout A/B only)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
-    ap.add_argument("--no-extras", action="store_true", help="skip decode/copy/host-inclusive/CPU legs")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline sample budget (headline config)")
+    ap.add_argument("--sustained-seconds", type=float, default=5.0, help="back-to-back encode leg length")
+    ap.add_argument("--cfg3-stripes", type=int, default=CFG3_STRIPES,
+                    help="global stripe count of the strong-scaled 10+4 x 4 MiB leg")
+    ap.add_argument("--no-extras", action="store_true", help="headline only")
+    ap.add_argument("--launch-probe", action="store_true",
+                    help="launcher self-test: ranks join the process group on CPU (gloo) and report, no GPU work")
     ap.add_argument("--alloc", choices=["contiguous", "hipmalloc"], default="contiguous",
                     help="HBM for the headline stripe batch: rs_dev_alloc contiguous range (default) or torch/hipMalloc "
                          "(the other configs' pools stay hipMalloc: contiguous measured no better there)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def main():
-    args = parse()
+# ---------------------------------------------------------------------------
+# Rank launcher
+# ---------------------------------------------------------------------------
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_command(n: int, argv, port: int):
+    """torch.distributed.run command that re-runs this script with the same
+    arguments as n ranks on this node (rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(args, argv) -> int:
+    """Start the N ranks as a child launcher and return its exit status.
+    Called before this process touches the GPU (no torch.cuda call here): the
+    ranks are children, never an exec of this process."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(launch_command(args.gpus, argv, free_port()), env=env).returncode
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        return 2
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return launch_ranks(args, argv)
+    if int(env_world or 1) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}: refusing to report a mislabelled line",
+              file=sys.stderr)
+        return 2
+    if args.launch_probe:
+        return launch_probe(args)
+    run(args)
+    return 0
+
+
+def launch_probe(args) -> int:
+    from rsamd import parallel
+    r = parallel.init_from_env(use_gpu=False)
+    total = parallel.sum_over_ranks(r, 1.0)
+    start, count = parallel.stripe_partition(args.cfg3_stripes, r.world, r.rank)
+    covered = parallel.sum_over_ranks(r, float(count))
+    if r.rank == 0:
+        print(json.dumps({"probe": True, "n_gpus": r.world, "ranks_seen": int(total), "backend": r.backend,
+                          "cfg3_stripes_covered": int(covered)}), flush=True)
+    parallel.shutdown(r)
+    return 0
+
+
+# ---------------------------------------------------------------------------
+# Timing helpers
+# ---------------------------------------------------------------------------
+def timed(torch, stream, fn, iters):
+    """Average seconds per call of fn on this GPU alone (HIP events)."""
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # Untimed calls: the first builds any host-side plans; after that host work
+    # the GPU has idled and needs some tens of ms of load before it runs at its
+    # steady rate (a 10+4 masked leg read 0.64-0.68 of peak over its first ~8
+    # calls, then 0.71-0.75 per call: profiles/r1/masked/masked_per_call.txt).
+    # So warm up for at least 3 calls AND 50 ms.
+    fn()
+    torch.cuda.synchronize()
+    t0, n = time.perf_counter(), 0
+    while n < 2 or time.perf_counter() - t0 < 0.05:
+        fn()
+        torch.cuda.synchronize()
+        n += 1
+    s.record(stream)
+    for _ in range(iters):
+        fn()
+    e.record(stream)
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e-3
+
+
+def timed_all_ranks(torch, parallel, r, fn, iters):
+    """Seconds per call with every rank calling fn at once: warm-up as in
+    timed(), then barrier + synchronize on both sides of `iters` calls; the
+    slowest rank's time."""
+    fn()
+    torch.cuda.synchronize()
+    t0, n = time.perf_counter(), 0
+    while n < 2 or time.perf_counter() - t0 < 0.05:
+        fn()
+        torch.cuda.synchronize()
+        n += 1
+    parallel.barrier(r)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    parallel.barrier(r)
+    return parallel.max_over_ranks(r, time.perf_counter() - t0) / iters
+
+
+# ---------------------------------------------------------------------------
+# The run
+# ---------------------------------------------------------------------------
+def run(args):
     import torch
 
     import rsamd
@@ -79,15 +205,12 @@ def main():
     rdev.fill_synthetic(buf.data_ptr(), k, lay, SEED, stripe0=stripe0, stream=stream)
     torch.cuda.synchronize()
 
-    def barrier():
-        parallel.barrier(r)
-
     def step():
         rdev.encode(rs, buf.data_ptr(), lay, stream)
 
     for _ in range(args.warmup):
         step()
-    barrier()
+    parallel.barrier(r)
     # Per-launch HIP events on the launch stream (the kernel's own duration).
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
@@ -95,7 +218,7 @@ def main():
         s.record(stream)
         step()
         e.record(stream)
-    barrier()
+    parallel.barrier(r)
     elapsed = parallel.max_over_ranks(r, time.perf_counter() - t0)
     launch_times = sorted(s.elapsed_time(e) for s, e in evs)
     launch_ms = sum(launch_times) / len(launch_times)
@@ -112,21 +235,27 @@ def main():
     alg_bytes = (k + m) * S * B  # per launch: each data byte read once, each parity byte written once
     achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
 
-    extra = {}
-    cpu = None
-    if rank == 0 and not args.no_extras:
-        extra = device_extras(torch, rs, rdev, buf, lay, stream, k, m, S, B)
+    extra, cpu = {}, None
+    if not args.no_extras:
+        extra.update(decode_all_ranks(torch, parallel, r, rs, rdev, buf, lay, stream, k, m, S, B, args.steps))
+        extra.update(sustained(torch, parallel, r, rs, rdev, buf, lay, stream, k, m, S, B, args.sustained_seconds))
+        if world == 1:
+            extra.update(device_extras(torch, rs, rdev, buf, lay, stream, k, m, S, B))
+        if isinstance(buf, rdev.DeviceBuffer):
+            buf.free()
         del buf
         torch.cuda.empty_cache()
-        if world == 1:  # multi-GPU runs report the scaling line only (the other ranks wait)
+        extra.update(cfg3_strong(torch, rsamd, parallel, r, rdev, dev, stream, args.cfg3_stripes, args.steps))
+        if world == 1:
             extra.update(other_configs(torch, rsamd, rdev, dev, stream))
             extra.update(layout_legs(torch, rsamd, dev, stream))
             cpu = cpu_baseline(k, m, S, args.cpu_seconds)
+            extra["cpu_configs"] = cpu_configs()
             extra.update(host_inclusive(rsamd, k, m))
             extra.update(config0_single_stripe(rsamd, k, m))
-    if world > 1 and not args.no_extras:
-        # every rank at once: the node's aggregate host <-> device rate
-        extra.update(host_inclusive_all_ranks(rsamd, parallel, r, k, m))
+        else:
+            # every rank at once: the node's aggregate host <-> device rate
+            extra.update(host_inclusive_all_ranks(rsamd, parallel, r, k, m))
     traffic = pmc_traffic(k, m, S, B)
 
     if rank == 0:
@@ -188,26 +317,111 @@ def alloc_note(contiguous):
     return "rs_dev_alloc: physically contiguous" if contiguous else "rs_dev_alloc: hipMalloc (no contiguous range)"
 
 
-def timed(torch, stream, fn, iters):
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    # Untimed calls: the first builds any host-side plans; after that host work
-    # the GPU has idled and needs some tens of ms of load before it runs at its
-    # steady rate (a 10+4 masked leg read 0.64-0.68 of peak over its first ~8
-    # calls, then 0.71-0.75 per call: profiles/r1/masked/masked_per_call.txt).
-    # So warm up for at least 3 calls AND 50 ms.
-    fn()
-    torch.cuda.synchronize()
+def decode_all_ranks(torch, parallel, r, rs, rdev, buf, lay, stream, k, m, S, B, iters):
+    """BASELINE configs[2] at N GPUs: every rank decodes erasures {0,1} of its
+    own B stripes at once.  Afterwards shards 0 and 1 are overwritten with
+    other bytes, decoded once more and the batch verified, so a decode that
+    wrote nothing cannot pass."""
+    present = [i not in (0, 1) for i in range(k + m)]
+    t = timed_all_ranks(torch, parallel, r, lambda: rdev.decode(rs, buf.data_ptr(), present, lay, stream), iters)
+    rdev.fill_synthetic(buf.data_ptr(), 2, lay, SEED ^ 0xBAD, 0, stream)  # clobber shards 0 and 1
+    rdev.decode(rs, buf.data_ptr(), present, lay, stream)
+    flag = torch.zeros(1, dtype=torch.int32, device=buf.device)
+    rdev.verify(rs, buf.data_ptr(), lay, flag.data_ptr(), stream)
+    ok = parallel.all_ranks_true(r, int(flag.item()) == 0)
+    return {"decode_0_1_all_ranks_GiBps": round(r.world * k * S * B / t / 2**30, 2),
+            "decode_0_1_all_ranks_hbm_frac_per_gpu": round((k + 2) * S * B / t / 1e9 / HBM_PEAK_GBPS, 4),
+            "decode_0_1_all_ranks_verified": ok}
+
+
+def sustained(torch, parallel, r, rs, rdev, buf, lay, stream, k, m, S, B, seconds):
+    """>= `seconds` of back-to-back headline encodes on every rank (so the
+    rate is seen at thermal steady state, not over an 80 ms burst), with the
+    GPU clocks sampled from sysfs meanwhile."""
+    sampler = ClockSampler()
+    rdev.encode(rs, buf.data_ptr(), lay, stream)
+    parallel.barrier(r)
+    sampler.start()
     t0, n = time.perf_counter(), 0
-    while n < 2 or time.perf_counter() - t0 < 0.05:
-        fn()
+    while True:
+        for _ in range(32):
+            rdev.encode(rs, buf.data_ptr(), lay, stream)
+        n += 32
         torch.cuda.synchronize()
-        n += 1
-    s.record(stream)
-    for _ in range(iters):
-        fn()
-    e.record(stream)
-    torch.cuda.synchronize()
-    return s.elapsed_time(e) / iters * 1e-3
+        if time.perf_counter() - t0 >= seconds:
+            break
+    el = time.perf_counter() - t0
+    clocks = sampler.stop()
+    parallel.barrier(r)
+    el_max = parallel.max_over_ranks(r, el)
+    n_all = parallel.sum_over_ranks(r, float(n))
+    out = {"sustained_seconds": round(el_max, 2), "sustained_launches_all_ranks": int(n_all),
+           "sustained_GiBps": round(k * S * B * n_all / el_max / 2**30, 2),
+           "sustained_hbm_frac": round((k + m) * S * B * n / el / 1e9 / HBM_PEAK_GBPS, 4),
+           "sustained_clocks": clocks}
+    return out
+
+
+class ClockSampler:
+    """Samples busy %, SCLK and MCLK of the GPUs sysfs exposes, every 0.25 s
+    on a thread; stop() reports the busiest card's samples."""
+
+    def __init__(self, period=0.25):
+        import glob
+        self.cards = sorted(d for d in glob.glob("/sys/class/drm/card*/device") if os.path.exists(d + "/pp_dpm_sclk"))
+        self.period, self.samples, self._stop = period, {c: [] for c in self.cards}, threading.Event()
+        self._t = threading.Thread(target=self._loop, daemon=True)
+
+    @staticmethod
+    def _read(path):
+        try:
+            with open(path) as f:
+                return f.read()
+        except OSError:
+            return None
+
+    @staticmethod
+    def _current_mhz(text):
+        for line in (text or "").splitlines():
+            if line.rstrip().endswith("*"):
+                for tok in line.split():
+                    if tok.lower().endswith("mhz"):
+                        try:
+                            return float(tok[:-3])
+                        except ValueError:
+                            return None
+        return None
+
+    def _loop(self):
+        while not self._stop.wait(self.period):
+            for c in self.cards:
+                busy = self._read(c + "/gpu_busy_percent")
+                self.samples[c].append((float(busy) if busy and busy.strip().isdigit() else None,
+                                        self._current_mhz(self._read(c + "/pp_dpm_sclk")),
+                                        self._current_mhz(self._read(c + "/pp_dpm_mclk"))))
+
+    def start(self):
+        self._t.start()
+
+    def stop(self):
+        self._stop.set()
+        self._t.join(timeout=2)
+        if not self.cards:
+            return {"source": "sysfs pp_dpm_sclk", "note": "no card exposes pp_dpm_sclk here"}
+
+        def score(c):
+            return sum(b or 0 for b, _, _ in self.samples[c])
+        c = max(self.cards, key=score)
+        s = self.samples[c]
+
+        def med(vals):
+            vals = sorted(v for v in vals if v is not None)
+            return vals[len(vals) // 2] if vals else None
+        return {"source": "sysfs pp_dpm_sclk / pp_dpm_mclk / gpu_busy_percent", "card": c.split("/")[-2],
+                "samples": len(s), "busy_pct_max": max((b for b, _, _ in s if b is not None), default=None),
+                "busy_pct_median": med(b for b, _, _ in s), "sclk_mhz_median": med(x for _, x, _ in s),
+                "sclk_mhz_min": min((x for _, x, _ in s if x is not None), default=None),
+                "mclk_mhz_median": med(x for _, _, x in s)}
 
 
 def device_extras(torch, rs, rdev, buf, lay, stream, k, m, S, B):
@@ -232,9 +446,53 @@ def device_extras(torch, rs, rdev, buf, lay, stream, k, m, S, B):
     return out
 
 
+def cfg3_strong(torch, rsamd, parallel, r, rdev, dev, stream, total, iters):
+    """BASELINE configs[3]: 10+4 x 4 MiB, `total` stripes split across the
+    ranks by stripe index (strong scaling), encode then a {0,1,2,3} decode,
+    every rank at once.  GiB/s = all data bytes / the slowest rank's time."""
+    from rsamd.device import StripeLayout
+    k, m, S = 10, 4, 4 << 20
+    start, count = parallel.stripe_partition(total, r.world, r.rank)
+    most = parallel.stripe_partition(total, r.world, 0)[1]  # rank 0 holds the largest share
+    rs = rsamd.ReedSolomon.create(k, m)
+    lay = StripeLayout.packed(count, k + m, S)
+    buf = torch.empty(lay.nbytes, dtype=torch.uint8, device=dev)
+    rdev.fill_synthetic(buf.data_ptr(), k, lay, SEED, start, stream)
+    n = max(3, iters // 2)
+    out = {"cfg3_strong_note": f"10+4 x 4 MiB, {total} stripes split over {r.world} GPU(s) "
+                               f"({most} on the busiest), every rank at once"}
+    t = timed_all_ranks(torch, parallel, r, lambda: rdev.encode(rs, buf.data_ptr(), lay, stream), n)
+    out["cfg3_strong_encode_GiBps"] = round(k * S * total / t / 2**30, 2)
+    out["cfg3_strong_encode_hbm_frac_per_gpu"] = round((k + m) * S * most / t / 1e9 / HBM_PEAK_GBPS, 4)
+    miss = (0, 1, 2, 3)
+    present = [i not in miss for i in range(k + m)]
+    t = timed_all_ranks(torch, parallel, r, lambda: rdev.decode(rs, buf.data_ptr(), present, lay, stream), n)
+    out["cfg3_strong_decode_0_1_2_3_GiBps"] = round(k * S * total / t / 2**30, 2)
+    out["cfg3_strong_decode_hbm_frac_per_gpu"] = round((k + len(miss)) * S * most / t / 1e9 / HBM_PEAK_GBPS, 4)
+    buf.view(count, k + m, lay.shard_stride)[:, :len(miss)].fill_(0xA5)  # the decode must rewrite them
+    rdev.decode(rs, buf.data_ptr(), present, lay, stream)
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    rdev.verify(rs, buf.data_ptr(), lay, flag.data_ptr(), stream)
+    out["cfg3_strong_verified"] = parallel.all_ranks_true(r, int(flag.item()) == 0)
+    del buf
+    torch.cuda.empty_cache()
+    return out
+
+
+def clobber(torch, buf, lay, total_shards, present, dev):
+    """Overwrite every absent shard of a (n_stripes, total_shards) presence
+    pattern with 0x5A, so a decode that skips a stripe fails the verify after it."""
+    v = buf.view(lay.n_stripes, lay.stripe_stride)[:, : total_shards * lay.shard_stride]
+    v = v.view(lay.n_stripes, total_shards, lay.shard_stride)
+    mask = torch.from_numpy(~present).to(dev)
+    v[mask] = 0x5A
+
+
 def other_configs(torch, rsamd, rdev, dev, stream, alloc="hipmalloc"):
-    """BASELINE configs[3] (10+4 x 4 MiB; the per-GPU share of 1024 stripes over
-    8 GPUs) and configs[4] (4+2 x 4 KiB x 1 M stripes), encode and decode."""
+    """BASELINE configs[3] per-GPU share at N=8 (10+4 x 4 MiB x 128, packed and
+    4 KiB-padded) and configs[4] (4+2 x 4 KiB x 1 M stripes), encode, decode,
+    verify, and per-stripe erasure patterns (row f2)."""
+    import numpy as np
     from rsamd.device import StripeLayout
     out = {}
     for name, k, m, S, B, miss, pad in [("cfg3_10p4_4MiB_x128", 10, 4, 4 << 20, 128, (0, 1, 2, 3), 0),
@@ -252,6 +510,8 @@ def other_configs(torch, rsamd, rdev, dev, stream, alloc="hipmalloc"):
         out[name + "_decode_" + "_".join(map(str, miss)) + "_GiBps"] = round(k * S * B / t / 2**30, 2)
         out[name + "_decode_hbm_frac"] = round((k + len(miss)) * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
         flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        clobber(torch, buf, lay, k + m, np.tile(np.array(present), (B, 1)), dev)
+        rdev.decode(rs, buf.data_ptr(), present, lay, stream)
         rdev.verify(rs, buf.data_ptr(), lay, flag.data_ptr(), stream)
         out[name + "_verified"] = int(flag.item()) == 0
         # row f3 (isParityCorrect) on the same batch: (k+m)*S*B bytes read
@@ -259,7 +519,6 @@ def other_configs(torch, rsamd, rdev, dev, stream, alloc="hipmalloc"):
         out[name + "_verify_hbm_frac"] = round((k + m) * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
         if name == "cfg3_10p4_4MiB_x128":
             # row f2 for the wide code: 4 random erasures per stripe, device bitmasks, one launch
-            import numpy as np
             rng = np.random.default_rng(0)
             present = np.ones((B, k + m), dtype=bool)
             for t_ in range(B):
@@ -269,12 +528,13 @@ def other_configs(torch, rsamd, rdev, dev, stream, alloc="hipmalloc"):
             t = timed(torch, stream, lambda: rdev.decode_masked_bits(rs, buf.data_ptr(), bits.data_ptr(), lay, 0,
                                                                      stream), 5)
             out[name + "_decode_masked_bits_hbm_frac"] = round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)
+            clobber(torch, buf, lay, k + m, present, dev)
+            rdev.decode_masked_bits(rs, buf.data_ptr(), bits.data_ptr(), lay, 0, stream)
             rdev.verify(rs, buf.data_ptr(), lay, flag.data_ptr(), stream)
             out[name + "_decode_masked_bits_verified"] = int(flag.item()) == 0
         if name.startswith("cfg4"):
             # row f2: a random presence pattern per stripe (<= 2 erasures), one launch
             import itertools
-            import numpy as np
             pats = np.array([[i not in miss for i in range(k + m)] for e in range(3)
                              for miss in itertools.combinations(range(k + m), e)], dtype=bool)
             present = pats[np.random.default_rng(0).integers(0, len(pats), B)]
@@ -285,6 +545,8 @@ def other_configs(torch, rsamd, rdev, dev, stream, alloc="hipmalloc"):
             t = timed(torch, stream, lambda: rdev.decode_masked(rs, buf.data_ptr(), present, lay, stream), 10)
             out[name + "_decode_masked_GiBps"] = round(k * S * B / t / 2**30, 2)
             out[name + "_decode_masked_hbm_frac"] = round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)
+            clobber(torch, buf, lay, k + m, present, dev)
+            rdev.decode_masked(rs, buf.data_ptr(), present, lay, stream)
             rdev.verify(rs, buf.data_ptr(), lay, flag.data_ptr(), stream)
             out[name + "_decode_masked_verified"] = int(flag.item()) == 0
             # the same patterns as device-resident bitmasks (no host work per call)
@@ -293,6 +555,8 @@ def other_configs(torch, rsamd, rdev, dev, stream, alloc="hipmalloc"):
                                                                      stream), 5)
             out[name + "_decode_masked_bits_GiBps"] = round(k * S * B / t / 2**30, 2)
             out[name + "_decode_masked_bits_hbm_frac"] = round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)
+            clobber(torch, buf, lay, k + m, present, dev)
+            rdev.decode_masked_bits(rs, buf.data_ptr(), bits.data_ptr(), lay, 0, stream)
             rdev.verify(rs, buf.data_ptr(), lay, flag.data_ptr(), stream)
             out[name + "_decode_masked_bits_verified"] = int(flag.item()) == 0
         del buf
@@ -329,50 +593,112 @@ def layout_legs(torch, rsamd, dev, stream):
     return out
 
 
-def cpu_baseline(k, m, S, budget_s):
-    """The oracle's scalar InputOutputByteTable loop (the reference's default
-    coding loop, -O2 -fno-tree-vectorize) on host-resident stripes."""
+# ---------------------------------------------------------------------------
+# CPU baseline (the oracle's scalar restatement of the reference loop)
+# ---------------------------------------------------------------------------
+def host_cpu_share():
+    """(threads to use, description): the CPUs this process may run on
+    (sched_getaffinity), capped by a cgroup v2 CPU quota when one is set --
+    the host's CPU share for this job, which on the GPU box is smaller than
+    os.cpu_count()."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, math.floor(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    threads = min(aff, quota) if quota else aff
+    model, sockets = "", set()
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name") and not model:
+                model = line.split(":", 1)[1].strip()
+            if line.startswith("physical id"):
+                sockets.add(line.split(":", 1)[1].strip())
+    except OSError:
+        pass
+    return threads, {"threads": threads, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+                     "os_cpu_count": os.cpu_count(), "sockets": len(sockets) or None, "cpu_model": model}
+
+
+def cpu_rate(codec, k, m, S, present, threads, budget_s, min_stripes):
+    """GiB/s of user data (k*S per stripe) the oracle codes on `threads`
+    pthreads, stripes split across them, over >= budget_s."""
     import numpy as np
     from oracle import c_ref
-    c_ref.build()
-    codec = c_ref.Codec(k, m)
-    n = 8
-    stride = S
-    host = np.zeros(n * (k + m) * stride, dtype=np.uint8)
+    n = max(min_stripes, threads * 2)
+    n = min(n, max(threads, (8 << 30) // ((k + m) * S)))  # <= 8 GiB of host stripes unless a thread has none
+    host = np.zeros(n * (k + m) * S, dtype=np.uint8)
     for t in range(n):
         host[t * (k + m) * S: t * (k + m) * S + k * S] = c_ref.fill_synthetic(k * S, SEED, t)
+    if present is not None:
+        codec.code_stripes(host, n, S, S, (k + m) * S, None, threads)  # parity first, then decode
     done, t0 = 0, time.perf_counter()
     while True:
-        codec.code_stripes(host, n, S, stride, (k + m) * stride, None, 1)
+        codec.code_stripes(host, n, S, S, (k + m) * S, present, threads)
         done += n
         el = time.perf_counter() - t0
         if el >= budget_s:
             break
-    rate = k * S * done / el / 2**30
-    threads = min(16, os.cpu_count() or 1)
-    done_mt, t1 = 0, time.perf_counter()
-    nm = threads * 2
-    host_mt = np.zeros(nm * (k + m) * S, dtype=np.uint8)
-    while time.perf_counter() - t1 < budget_s / 2:
-        codec.code_stripes(host_mt, nm, S, S, (k + m) * S, None, threads)
-        done_mt += nm
-    rate_mt = k * S * done_mt / (time.perf_counter() - t1) / 2**30
-    model = ""
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
+    return k * S * done / el / 2**30, done, el
+
+
+def cpu_baseline(k, m, S, budget_s):
+    """The oracle's scalar InputOutputByteTable loop (the reference's default
+    coding loop, -O2 -fno-tree-vectorize) on host-resident stripes: 1 thread,
+    then the host's CPU share."""
+    from oracle import c_ref
+    c_ref.build()
+    codec = c_ref.Codec(k, m)
+    rate, done, el = cpu_rate(codec, k, m, S, None, 1, budget_s, 8)
+    threads, share = host_cpu_share()
+    rate_mt, done_mt, _ = cpu_rate(codec, k, m, S, None, threads, budget_s / 2, 8)
     return {"value": round(rate, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"{done} stripes of {k}+{m} x {S // 1024} KiB encoded by the scalar restatement of "
                       f"InputOutputByteTableCodingLoop (oracle/rs_oracle.c, -O2 -fno-tree-vectorize), "
                       f"{el:.1f} s, host-resident",
-            "multi_thread": {"value": round(rate_mt, 4), "threads": threads, "stripes": done_mt},
-            "cpu_model": model}
+            "multi_thread": {"value": round(rate_mt, 4), "stripes": done_mt, **share},
+            "cpu_model": share["cpu_model"]}
 
 
+CPU_CONFIGS = [  # name, k, m, S, erasures (None = encode); BASELINE configs[2..4]
+    ("C3_decode_0", 4, 2, 1 << 20, (0,)),
+    ("C3_decode_0_1", 4, 2, 1 << 20, (0, 1)),
+    ("C4_10p4_4MiB_encode", 10, 4, 4 << 20, None),
+    ("C4_10p4_4MiB_decode_0_1_2_3", 10, 4, 4 << 20, (0, 1, 2, 3)),
+    ("C5_4KiB_encode", 4, 2, 4096, None),
+    ("C5_4KiB_decode_0_1", 4, 2, 4096, (0, 1)),
+]
+
+
+def cpu_configs(budget_s=1.0):
+    """The CPU side of BASELINE configs[2..4]: the oracle's decodeMissing /
+    encodeParity restatement (two codeSomeShards passes for a decode, as
+    ReedSolomon.java:175-272) on 1 thread and on the host's CPU share, each a
+    bounded sample of >= budget_s."""
+    from oracle import c_ref
+    threads, _ = host_cpu_share()
+    out = {}
+    for name, k, m, S, miss in CPU_CONFIGS:
+        codec = c_ref.Codec(k, m)
+        present = None if miss is None else [i not in miss for i in range(k + m)]
+        min_stripes = max(1, (32 << 20) // ((k + m) * S))
+        r1, n1, _ = cpu_rate(codec, k, m, S, present, 1, budget_s, min(min_stripes, 64))
+        rn, nn, _ = cpu_rate(codec, k, m, S, present, threads, budget_s, min_stripes)
+        out[name] = {"GiBps_1thr": round(r1, 3), f"GiBps_{threads}thr": round(rn, 3), "stripes_1thr": n1,
+                     "stripes_mt": nn}
+    out["note"] = f"oracle scalar port, host-resident, >= {budget_s} s per sample; GiB/s of k*S user bytes"
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Host-resident legs (PCIe-inclusive; never the bench value)
+# ---------------------------------------------------------------------------
 def host_inclusive(rsamd, k, m):
     """Rates of the JNI-facing host-buffer API: H2D + kernel + D2H on pageable
     buffers, chunked and overlapped on three streams (host.cpp run_chunks)."""
@@ -501,4 +827,4 @@ def pmc_traffic(k, m, S, B):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -40,8 +40,12 @@ def init_from_env(use_gpu: bool = True) -> Rank:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    backend = os.environ.get("RSAMD_DIST_BACKEND", "nccl" if use_gpu else "gloo")
+    backend = os.environ.get("RSAMD_DIST_BACKEND")
     import torch
+    if backend is None:
+        # RCCL needs a device of its own per rank; ranks that share a GPU (more
+        # ranks than devices, e.g. a rehearsal on a one-GPU box) line up over gloo.
+        backend = "nccl" if use_gpu and torch.cuda.device_count() >= world else "gloo"
     if use_gpu:
         torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     if world > 1:

@@ -1,0 +1,60 @@
+"""CPU tests of bench.py's rank launcher (the driver's `bench.py --gpus N`).
+
+`bench.py --gpus N` with no WORLD_SIZE in the environment must start N ranks
+itself (torch.distributed.run as a child process) and relay rank 0's line; under
+a launcher, WORLD_SIZE must equal --gpus or the run refuses to report.  The
+--launch-probe mode makes the ranks join the process group on CPU (gloo) and
+report, so the whole launch path runs here without a GPU.
+"""
+import json
+import os
+import subprocess
+import sys
+
+from conftest import ROOT
+
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT")}
+    env.update(kw)
+    return env
+
+
+def test_launch_command_shape():
+    sys.path.insert(0, ROOT)
+    import bench
+    cmd = bench.launch_command(4, ["--gpus", "4", "--steps", "3"], 12345)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--master-addr=127.0.0.1" in cmd and "--master-port=12345" in cmd
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "3"]
+    assert os.path.samefile(cmd[-5], BENCH)
+
+
+def test_self_launch_two_ranks():
+    """`bench.py --gpus 2` (no launcher) runs 2 ranks that see each other."""
+    p = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--launch-probe", "--cfg3-stripes", "1024"],
+                       env=_env(), capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    got = lines[0]
+    assert got["n_gpus"] == 2 and got["ranks_seen"] == 2 and got["backend"] == "gloo"
+    assert got["cfg3_stripes_covered"] == 1024
+
+
+def test_world_size_mismatch_refused():
+    """Under a launcher that started a different number of ranks, refuse."""
+    p = subprocess.run([sys.executable, BENCH, "--gpus", "8", "--launch-probe"],
+                       env=_env(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"), capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode == 2
+    assert "WORLD_SIZE=1" in p.stderr and not p.stdout.strip()
+
+
+def test_gpus_must_be_positive():
+    p = subprocess.run([sys.executable, BENCH, "--gpus", "0"], env=_env(), capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode == 2

@@ -6,7 +6,9 @@ runs every workload under FETCH_SIZE and WRITE_SIZE and turns the median
 dispatch into HBM bytes per launch (tools/pmc_summary.py).
 
 Workloads (bench.py's configs):
+  enc42      4+2 x 1 MiB x 4096, encode (the headline)  alg (4+2) S B
   dec42_01   4+2 x 1 MiB x 4096, decode {0,1}          alg (4+2) S B
+  enc104p / dec104p   enc104 / dec104 with a 4 KiB pad between shards
   enc104     10+4 x 4 MiB x 128, encode                 alg 14 S B
   dec104     10+4 x 4 MiB x 128, decode {0,1,2,3}       alg 14 S B
   enc42_4k   4+2 x 4 KiB x 1 M, encode                  alg 6 S B
@@ -35,18 +37,20 @@ def main():
     from rsamd.layout import decode_file_dev, encode_file_dev, file_layout
     st = torch.cuda.current_stream()
 
-    def stripes(k, m, S, B):
+    def stripes(k, m, S, B, pad=0):
         rs = rsamd.ReedSolomon.create(k, m)
-        lay = StripeLayout.packed(B, k + m, S)
+        lay = StripeLayout.packed(B, k + m, S, pad=pad)
         buf = torch.empty(lay.nbytes, dtype=torch.uint8, device="cuda:0")
         rdev.fill_synthetic(buf.data_ptr(), k, lay, SEED, 0, st)
         rdev.encode(rs, buf.data_ptr(), lay, st)
         return rs, lay, buf
 
-    if name in ("dec42_01", "dec104", "enc104", "enc42_4k"):
+    if name in ("dec42_01", "dec104", "enc104", "enc42_4k", "enc42", "enc104p", "dec104p"):
         k, m, S, B = {"dec42_01": (4, 2, 1 << 20, 4096), "dec104": (10, 4, 4 << 20, 128),
-                      "enc104": (10, 4, 4 << 20, 128), "enc42_4k": (4, 2, 4096, 1 << 20)}[name]
-        rs, lay, buf = stripes(k, m, S, B)
+                      "enc104": (10, 4, 4 << 20, 128), "enc42_4k": (4, 2, 4096, 1 << 20),
+                      "enc42": (4, 2, 1 << 20, 4096), "enc104p": (10, 4, 4 << 20, 128),
+                      "dec104p": (10, 4, 4 << 20, 128)}[name]
+        rs, lay, buf = stripes(k, m, S, B, 4096 if name.endswith("p") else 0)
         if name.startswith("dec"):
             miss = (0, 1) if k == 4 else (0, 1, 2, 3)
             present = [i not in miss for i in range(k + m)]
