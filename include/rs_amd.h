@@ -260,6 +260,21 @@ RS_API int rs_copy_dev(uint8_t *dst, const uint8_t *src, size_t n, void *stream)
  * XCD-contiguous remap; rot = xcd = -1 restores the measured table. */
 RS_API int rs_debug_block_order(int rot, int xcd);
 
+/* Process-wide switch of the bitsliced XOR-network kernels (run-time compiled
+ * per coefficient matrix) that code launches of at least
+ * RSAMD_XORNET_MIN_BYTES (default 256 MiB) moved: mode -1 = default
+ * (environment RSAMD_XORNET, on unless "0"), 0 = off (table kernels only),
+ * 1 = on, 2 = on for every launch with >= 2 KiB columns (tests).  Returns the
+ * number of XOR-network kernels compiled so far in this process. */
+RS_API int rs_debug_xornet(int mode);
+
+/* The generated HIP source of the XOR-network kernel for rows (nout x nin,
+ * row-major; nout <= 4), coding (verify = 0) or checking.  Writes at most cap
+ * bytes (NUL-terminated when it fits) and returns the full length, or a
+ * negative RS_E_* code; *ops (may be NULL) receives the VALU operation count
+ * per 32 columns.  Host-only: tests emulate the kernel on the CPU with it. */
+RS_API int rs_xornet_source(const uint8_t *rows, int nin, int nout, int verify, char *buf, size_t cap, int *ops);
+
 #ifdef __cplusplus
 }
 #endif

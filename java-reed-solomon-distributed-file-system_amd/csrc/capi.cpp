@@ -27,6 +27,7 @@
 #include "gf256.hpp"
 #include "host.hpp"
 #include "kernels.hpp"
+#include "xornet.hpp"
 #include "layout.hpp"
 
 struct rs_codec {
@@ -879,6 +880,24 @@ int rs_dev_free(void *ptr) {
 int rs_debug_block_order(int rot, int xcd) {
     rsamd::set_debug_block_order(rot, xcd);
     return RS_OK;
+}
+
+int rs_xornet_source(const uint8_t *rows, int nin, int nout, int verify, char *buf, size_t cap, int *ops) {
+    if (!rows || nin < 1 || nout < 1 || nout > rsamd::kMaxOut) return fail(RS_E_INVALID, "bad xornet shape");
+    int n = 0;
+    const std::string src = rsamd::xornet_source(rows, nin, nout, verify != 0, "rsamd_xornet", &n);
+    if (ops) *ops = n;
+    if (buf && cap) {
+        const size_t c = std::min(cap - 1, src.size());
+        std::memcpy(buf, src.data(), c);
+        buf[c] = 0;
+    }
+    return int(src.size());
+}
+
+int rs_debug_xornet(int mode) {
+    if (mode >= -1 && mode <= 2) rsamd::set_debug_xornet_mode(mode);
+    return rsamd::xornet_compiled_count();
 }
 
 int rs_copy_dev(uint8_t *dst, const uint8_t *src, size_t n, void *stream) {

@@ -29,7 +29,16 @@ DevPlan dev_plan_at(const void *base, int nin, int nout) {
 }
 
 Plan::Plan(std::vector<int> in_idx, std::vector<int> out_idx, GfMatrix rows)
-    : in_idx_(std::move(in_idx)), out_idx_(std::move(out_idx)), rows_(std::move(rows)) {}
+    : in_idx_(std::move(in_idx)), out_idx_(std::move(out_idx)), rows_(std::move(rows)) {
+    const int nin = int(in_idx_.size());
+    for (int g = 0; g < groups(); ++g) {
+        const int p0 = g * kMaxOut, nout = std::min<int>(kMaxOut, int(out_idx_.size()) - p0);
+        std::vector<uint8_t> r(size_t(nout) * nin);
+        for (int p = 0; p < nout; ++p)
+            for (int i = 0; i < nin; ++i) r[size_t(p) * nin + i] = rows_.at(p0 + p, i);
+        group_rows_.push_back(std::move(r));
+    }
+}
 
 std::vector<uint8_t> Plan::image(int g) const {
     const int nin = int(in_idx_.size());
@@ -85,6 +94,7 @@ hipError_t Plan::device_plans(std::vector<DevPlan> *out) const {
     for (int g = 0; g < groups(); ++g) {
         const int nout = std::min<int>(kMaxOut, int(out_idx_.size()) - g * kMaxOut);
         out->push_back(dev_plan_at(static_cast<uint8_t *>(it->second) + offs[g], nin, nout));
+        out->back().rows = group_rows_[g].data();
     }
     return hipSuccess;
 }

@@ -42,6 +42,7 @@ public:
 private:
     std::vector<int> in_idx_, out_idx_;
     GfMatrix rows_;
+    std::vector<std::vector<uint8_t>> group_rows_;  // rows of each launch group (DevPlan::rows)
     mutable std::mutex mu_;
     mutable std::map<int, void *> dev_;       // device id -> allocation of all groups
     mutable std::map<int, void *> dev_file_;  // device id -> FileDecodePlan image

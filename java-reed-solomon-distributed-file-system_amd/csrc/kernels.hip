@@ -32,6 +32,7 @@
 #include <cstdlib>
 
 #include "gf_device.hpp"
+#include "xornet.hpp"
 
 namespace rsamd {
 namespace {
@@ -716,9 +717,9 @@ hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t 
 }
 
 namespace {
-}  // namespace
 
-hipError_t launch_gf(const Geometry &g, const DevPlan &p, Mode mode, int *mismatch, hipStream_t s) {
+// The table-lookup (v_perm_b32) kernels: any plan, any geometry.
+hipError_t launch_gf_tables(const Geometry &g, const DevPlan &p, Mode mode, int *mismatch, hipStream_t s) {
     if (g.n_stripes == 0 || g.len == 0 || p.nout == 0) return hipSuccess;
     if (p.nout > kMaxOut || p.nin < 1) return hipErrorInvalidValue;
     uint8_t *base = g.base + g.col0;
@@ -751,6 +752,74 @@ hipError_t launch_gf(const Geometry &g, const DevPlan &p, Mode mode, int *mismat
     if (tail) return launch_bytes(g, p, g.col0 + size_t(nvec) * 16, tail, mode, mismatch, s);
     return hipSuccess;
 }
+
+std::atomic<int> g_xornet_mode{-1};  // rs_debug_xornet
+
+bool xornet_enabled_now() {
+    const int m = g_xornet_mode.load(std::memory_order_relaxed);
+    return m < 0 ? xornet_enabled() : m != 0;
+}
+
+// Launches that move at least this many bytes take the XOR-network kernels
+// (their first use of a matrix compiles it: about 0.5-2 s once per process).
+uint64_t xornet_min_bytes() {
+    static const uint64_t env = [] {
+        const char *e = std::getenv("RSAMD_XORNET_MIN_BYTES");
+        return e ? std::strtoull(e, nullptr, 10) : uint64_t(256) << 20;
+    }();
+    return g_xornet_mode.load(std::memory_order_relaxed) == 2 ? 0 : env;
+}
+
+// The 2 KiB column chunks of g through the matrix's XOR-network kernel.
+// Returns hipErrorNotSupported (nothing launched) when the kernel cannot be
+// had; the caller then codes everything with the table kernels.
+hipError_t launch_gf_xornet(const Geometry &g, const DevPlan &p, Mode mode, int *mismatch, hipStream_t s,
+                            size_t *done_cols) {
+    hipFunction_t fn = nullptr;
+    std::string err;
+    if (xornet_function(p.rows, p.nin, p.nout, mode == Mode::Verify, &fn, &err) != hipSuccess)
+        return hipErrorNotSupported;
+    const size_t chunks = g.len / kXorChunk;
+    const size_t stripes_per_launch = std::max<size_t>(1, kMaxGridBlocks / chunks);
+    for (size_t t0 = 0; t0 < g.n_stripes; t0 += stripes_per_launch) {
+        const size_t nst = std::min(stripes_per_launch, g.n_stripes - t0);
+        const FastDiv d = make_fastdiv(uint32_t(chunks));
+        const uint32_t n_items = uint32_t(nst * chunks);
+        XorNetArgs a{g.base + g.col0 + t0 * g.stripe_stride, p.in_idx, p.out_idx, g.stripe_stride, g.shard_stride,
+                     uint32_t(chunks), n_items, d.m, d.s1, d.s2, n_items / 8u, mismatch};
+        const hipError_t e = launch_xornet(fn, a, s);
+        if (e != hipSuccess) return e;
+    }
+    *done_cols = chunks * kXorChunk;
+    return hipSuccess;
+}
+
+}  // namespace
+
+hipError_t launch_gf(const Geometry &g, const DevPlan &p, Mode mode, int *mismatch, hipStream_t s) {
+    if (g.n_stripes == 0 || g.len == 0 || p.nout == 0) return hipSuccess;
+    const bool aligned = (reinterpret_cast<uintptr_t>(g.base + g.col0) % 16 == 0) && g.shard_stride % 16 == 0 &&
+                         g.stripe_stride % 16 == 0;
+    const uint64_t moved = uint64_t(g.n_stripes) * g.len * uint64_t(p.nin + p.nout);
+    if (p.rows && aligned && g.len >= kXorChunk && g.len / kXorChunk <= UINT32_MAX / 2 &&
+        p.nout <= kMaxOut && xornet_enabled_now() && moved >= xornet_min_bytes()) {
+        size_t done = 0;
+        const hipError_t e = launch_gf_xornet(g, p, mode, mismatch, s, &done);
+        // No kernel for this matrix (compile failure): the table kernels code
+        // it, except under rs_debug_xornet(2), where tests want to know.
+        if (e == hipErrorNotSupported && g_xornet_mode.load(std::memory_order_relaxed) == 2) return hipErrorInvalidImage;
+        if (e != hipErrorNotSupported) {
+            if (e != hipSuccess || done == g.len) return e;
+            Geometry rest = g;  // the last < 2 KiB of columns
+            rest.col0 += done;
+            rest.len -= done;
+            return launch_gf_tables(rest, p, mode, mismatch, s);
+        }
+    }
+    return launch_gf_tables(g, p, mode, mismatch, s);
+}
+
+void set_debug_xornet_mode(int mode) { g_xornet_mode.store(mode); }
 
 void set_debug_block_order(int rot, int xcd) {
     g_order_rot.store(rot);
