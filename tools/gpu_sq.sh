@@ -5,7 +5,7 @@
 # tools/sq_summary.py into gpurun_out/sq_<tag>.json.
 # Usage (via gpurun): bash tools/gpu_sq.sh [tag]
 set -o pipefail
-TAG=${1:-r2}
+TAG=${1:-r2}${RSAMD_XORNET:+_xn$RSAMD_XORNET}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
 mkdir -p "$OUT"
