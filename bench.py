@@ -449,32 +449,34 @@ def device_extras(torch, rs, rdev, buf, lay, stream, k, m, S, B):
 def cfg3_strong(torch, rsamd, parallel, r, rdev, dev, stream, total, iters):
     """BASELINE configs[3]: 10+4 x 4 MiB, `total` stripes split across the
     ranks by stripe index (strong scaling), encode then a {0,1,2,3} decode,
-    every rank at once.  GiB/s = all data bytes / the slowest rank's time."""
+    every rank at once.  GiB/s = all data bytes / the slowest rank's time.
+    The pool is one contiguous range, as the headline's."""
     from rsamd.device import StripeLayout
     k, m, S = 10, 4, 4 << 20
     start, count = parallel.stripe_partition(total, r.world, r.rank)
     most = parallel.stripe_partition(total, r.world, 0)[1]  # rank 0 holds the largest share
     rs = rsamd.ReedSolomon.create(k, m)
     lay = StripeLayout.packed(count, k + m, S)
-    buf = torch.empty(lay.nbytes, dtype=torch.uint8, device=dev)
-    rdev.fill_synthetic(buf.data_ptr(), k, lay, SEED, start, stream)
+    pool = rdev.DeviceBuffer(lay.nbytes, contiguous=True)
+    base = pool.data_ptr()
+    rdev.fill_synthetic(base, k, lay, SEED, start, stream)
     n = max(3, iters // 2)
     out = {"cfg3_strong_note": f"10+4 x 4 MiB, {total} stripes split over {r.world} GPU(s) "
-                               f"({most} on the busiest), every rank at once"}
-    t = timed_all_ranks(torch, parallel, r, lambda: rdev.encode(rs, buf.data_ptr(), lay, stream), n)
+                               f"({most} on the busiest), every rank at once, {alloc_note(pool.contiguous)}"}
+    t = timed_all_ranks(torch, parallel, r, lambda: rdev.encode(rs, base, lay, stream), n)
     out["cfg3_strong_encode_GiBps"] = round(k * S * total / t / 2**30, 2)
     out["cfg3_strong_encode_hbm_frac_per_gpu"] = round((k + m) * S * most / t / 1e9 / HBM_PEAK_GBPS, 4)
     miss = (0, 1, 2, 3)
     present = [i not in miss for i in range(k + m)]
-    t = timed_all_ranks(torch, parallel, r, lambda: rdev.decode(rs, buf.data_ptr(), present, lay, stream), n)
+    t = timed_all_ranks(torch, parallel, r, lambda: rdev.decode(rs, base, present, lay, stream), n)
     out["cfg3_strong_decode_0_1_2_3_GiBps"] = round(k * S * total / t / 2**30, 2)
     out["cfg3_strong_decode_hbm_frac_per_gpu"] = round((k + len(miss)) * S * most / t / 1e9 / HBM_PEAK_GBPS, 4)
-    buf.view(count, k + m, lay.shard_stride)[:, :len(miss)].fill_(0xA5)  # the decode must rewrite them
-    rdev.decode(rs, buf.data_ptr(), present, lay, stream)
+    rdev.fill_synthetic(base, len(miss), lay, SEED ^ 0xBAD, 0, stream)  # the decode must rewrite shards 0-3
+    rdev.decode(rs, base, present, lay, stream)
     flag = torch.zeros(1, dtype=torch.int32, device=dev)
-    rdev.verify(rs, buf.data_ptr(), lay, flag.data_ptr(), stream)
+    rdev.verify(rs, base, lay, flag.data_ptr(), stream)
     out["cfg3_strong_verified"] = parallel.all_ranks_true(r, int(flag.item()) == 0)
-    del buf
+    pool.free()
     torch.cuda.empty_cache()
     return out
 

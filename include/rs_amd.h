@@ -261,11 +261,11 @@ RS_API int rs_copy_dev(uint8_t *dst, const uint8_t *src, size_t n, void *stream)
 RS_API int rs_debug_block_order(int rot, int xcd);
 
 /* Process-wide switch of the bitsliced XOR-network kernels (run-time compiled
- * per coefficient matrix) that code launches of at least
- * RSAMD_XORNET_MIN_BYTES (default 256 MiB) moved: mode -1 = default
- * (environment RSAMD_XORNET, on unless "0"), 0 = off (table kernels only),
- * 1 = on, 2 = on for every launch with >= 2 KiB columns (tests).  Returns the
- * number of XOR-network kernels compiled so far in this process. */
+ * per coefficient matrix) for launches that move at least
+ * RSAMD_XORNET_MIN_BYTES (default 256 MiB): mode -1 = default (environment
+ * RSAMD_XORNET, off unless "1"), 0 = off (table kernels only), 1 = on, 2 = on
+ * for every launch with >= 2 KiB columns (tests).  Returns the number of
+ * XOR-network kernels compiled so far in this process. */
 RS_API int rs_debug_xornet(int mode);
 
 /* The generated HIP source of the XOR-network kernel for rows (nout x nin,

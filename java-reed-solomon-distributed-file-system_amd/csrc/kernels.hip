@@ -603,8 +603,13 @@ BlockOrder block_order(uint32_t chunks, uint32_t total_shards, uint64_t shard_st
         return BlockOrder{chunks > 1 ? r : 0u, dbg_xcd > 0 ? n_items / 8u : 0u};
     }
     const bool half = chunks == 512 && shard_stride % (uint64_t(512) << 10) == 0;
+    // Wide stripes (>= 14 shards of >= 1 MiB): rotation up to 256 stripes per
+    // launch, the XCD remap beyond (10+4 x 4 MiB on contiguous pools: 128 and
+    // 256 stripes 0.72-0.75 rotated vs 0.70-0.71 remapped; 512 a tie at 0.70;
+    // 1024 0.753 remapped vs 0.70 rotated -- profiles/r2/order_pad_*.txt).
+    const uint32_t stripes = n_items / std::max(1u, chunks);
     const bool rotate = (chunks == 1024 && shard_stride % (uint64_t(1) << 20) == 0) || half ||
-                        (total_shards >= 14 && chunks >= 1024);
+                        (total_shards >= 14 && chunks >= 1024 && stripes <= 256);
     const uint32_t step = half ? chunks / 4u - 1u : 3u * chunks / 8u - 1u;
     const uint32_t rot = env_rot >= 0 ? uint32_t(env_rot) : (rotate ? step : 0u);
     const bool xcd = env_xcd >= 0 ? env_xcd != 0 : !rotate;
@@ -770,6 +775,17 @@ uint64_t xornet_min_bytes() {
     return g_xornet_mode.load(std::memory_order_relaxed) == 2 ? 0 : env;
 }
 
+// Block order of the XOR-network kernels: the XCD-contiguous remap unless
+// rs_debug_block_order overrides it (rot in 2 KiB chunks).
+BlockOrder xornet_block_order(uint32_t chunks, uint32_t n_items) {
+    const int dbg_rot = g_order_rot.load(std::memory_order_relaxed), dbg_xcd = g_order_xcd.load(std::memory_order_relaxed);
+    if (dbg_rot >= 0 || dbg_xcd >= 0) {
+        const uint32_t r = dbg_rot > 0 ? uint32_t(dbg_rot) % std::max(1u, chunks) : 0u;
+        return BlockOrder{chunks > 1 ? r : 0u, dbg_xcd > 0 ? n_items / 8u : 0u};
+    }
+    return BlockOrder{0u, n_items / 8u};
+}
+
 // The 2 KiB column chunks of g through the matrix's XOR-network kernel.
 // Returns hipErrorNotSupported (nothing launched) when the kernel cannot be
 // had; the caller then codes everything with the table kernels.
@@ -785,8 +801,9 @@ hipError_t launch_gf_xornet(const Geometry &g, const DevPlan &p, Mode mode, int 
         const size_t nst = std::min(stripes_per_launch, g.n_stripes - t0);
         const FastDiv d = make_fastdiv(uint32_t(chunks));
         const uint32_t n_items = uint32_t(nst * chunks);
+        const BlockOrder o = xornet_block_order(uint32_t(chunks), n_items);
         XorNetArgs a{g.base + g.col0 + t0 * g.stripe_stride, p.in_idx, p.out_idx, g.stripe_stride, g.shard_stride,
-                     uint32_t(chunks), n_items, d.m, d.s1, d.s2, n_items / 8u, mismatch};
+                     uint32_t(chunks), n_items, d.m, d.s1, d.s2, o.xcd_span, o.rot, mismatch};
         const hipError_t e = launch_xornet(fn, a, s);
         if (e != hipSuccess) return e;
     }

@@ -34,7 +34,7 @@ struct XorNetArgs {
     const int *out_idx;
     u64 stripe_stride;
     u64 shard_stride;
-    u32 chunks, n_items, cdiv_m, cdiv_s1, cdiv_s2, xcd_span;
+    u32 chunks, n_items, cdiv_m, cdiv_s1, cdiv_s2, xcd_span, rot;
     int *mismatch;
 };
 static __device__ __forceinline__ u32 x3(u32 a, u32 b, u32 c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
@@ -148,7 +148,12 @@ std::string xornet_source(const uint8_t *rows, int nin, int nout, bool verify, c
     o << "    u32 b = blockIdx.x;\n"
          "    if (a.xcd_span && b < 8u * a.xcd_span) b = (b & 7u) * a.xcd_span + (b >> 3);\n"
          "    const u32 stripe = fdiv(b, a.cdiv_m, a.cdiv_s1, a.cdiv_s2);\n"
-         "    const u32 chunk = b - stripe * a.chunks;\n"
+         "    u32 chunk = b - stripe * a.chunks;\n"
+         "    if (a.rot) {  // stripe * rot < n_items\n"
+         "        const u32 p = stripe * a.rot;\n"
+         "        chunk += p - fdiv(p, a.cdiv_m, a.cdiv_s1, a.cdiv_s2) * a.chunks;\n"
+         "        if (chunk >= a.chunks) chunk -= a.chunks;\n"
+         "    }\n"
          "    unsigned char *sb = a.base + (u64)stripe * a.stripe_stride + (u64)chunk * "
       << kXorChunk << "u + threadIdx.x * 16u;\n";
     for (int p = 0; p < nout; ++p)
@@ -302,7 +307,7 @@ hipError_t launch_xornet(hipFunction_t fn, const XorNetArgs &a, hipStream_t s) {
 bool xornet_enabled() {
     static const bool env_on = [] {
         const char *e = std::getenv("RSAMD_XORNET");
-        return !(e && e[0] == '0');
+        return e && e[0] == '1';
     }();
     return env_on;
 }

@@ -37,6 +37,7 @@ struct XorNetArgs {
     uint32_t n_items;   // blocks in this launch
     uint32_t cdiv_m, cdiv_s1, cdiv_s2;  // division by chunks (multiply-high)
     uint32_t xcd_span;  // XCD-contiguous block remap span (0 = off)
+    uint32_t rot;       // chunk rotation per stripe (0 = off), as the vector kernels' block order
     int *mismatch;      // verify kernels only
 };
 
@@ -57,7 +58,9 @@ hipError_t xornet_function(const uint8_t *rows, int nin, int nout, bool verify, 
 hipError_t launch_xornet(hipFunction_t fn, const XorNetArgs &a, hipStream_t s);
 
 // Whether large launches take these kernels by default: the RSAMD_XORNET
-// environment variable ("0" = off); rs_debug_xornet overrides (kernels.hip).
+// environment variable ("1" = on; off otherwise: measured no faster than the
+// table kernels on MI355X, whose wide-code rate is set by the memory access
+// pattern -- DESIGN.md 3.5); rs_debug_xornet overrides (kernels.hip).
 bool xornet_enabled();
 
 // Number of kernels compiled so far in this process (tests, probes).

@@ -47,7 +47,8 @@ static inline unsigned rs_bitop3(unsigned a, unsigned b, unsigned c, unsigned tt
 
 DRIVER = r"""
 extern "C" void run_all(unsigned char *base, const int *in_idx, const int *out_idx, unsigned long long stripe_stride,
-                        unsigned long long shard_stride, unsigned chunks, unsigned n_stripes, int *mismatch) {
+                        unsigned long long shard_stride, unsigned chunks, unsigned n_stripes, unsigned rot,
+                        int *mismatch) {
     unsigned l = 0;
     while ((1ull << l) < chunks) ++l;
     XorNetArgs a;
@@ -55,7 +56,7 @@ extern "C" void run_all(unsigned char *base, const int *in_idx, const int *out_i
     a.shard_stride = shard_stride; a.chunks = chunks; a.n_items = chunks * n_stripes;
     a.cdiv_m = (unsigned)(((1ull << 32) * ((1ull << l) - chunks)) / chunks + 1);
     a.cdiv_s1 = l < 1 ? l : 1u; a.cdiv_s2 = l > 1 ? l - 1 : 0u;
-    a.xcd_span = a.n_items / 8u; a.mismatch = mismatch;
+    a.xcd_span = a.n_items / 8u; a.rot = rot % chunks; a.mismatch = mismatch;
     for (unsigned b = 0; b < a.n_items; ++b)
         for (unsigned t = 0; t < 64; ++t) {
             blockIdx.x = b; threadIdx.x = t;
@@ -90,20 +91,20 @@ def host_kernel(native, rows, verify):
         subprocess.run([CLANG, "-O1", "-std=c++17", "-shared", "-fPIC", "-w", cpp, "-o", so], check=True)
     lib = C.CDLL(so)
     lib.run_all.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_ulonglong, C.c_ulonglong, C.c_uint, C.c_uint,
-                            C.c_void_p]
+                            C.c_uint, C.c_void_p]
     return lib, ops
 
 
-def run_batch(lib, buf, in_idx, out_idx, stripe_stride, shard_stride, chunks, n_stripes, mismatch=None):
+def run_batch(lib, buf, in_idx, out_idx, stripe_stride, shard_stride, chunks, n_stripes, mismatch=None, rot=0):
     ii = np.ascontiguousarray(in_idx, dtype=np.int32)
     oo = np.ascontiguousarray(out_idx, dtype=np.int32)
     mm = np.zeros(1, dtype=np.int32) if mismatch is None else mismatch
-    lib.run_all(buf.ctypes.data, ii.ctypes.data, oo.ctypes.data, stripe_stride, shard_stride, chunks, n_stripes,
+    lib.run_all(buf.ctypes.data, ii.ctypes.data, oo.ctypes.data, stripe_stride, shard_stride, chunks, n_stripes, rot,
                 mm.ctypes.data)
     return int(mm[0])
 
 
-def check_matrix(native, oracle_lib, rows, seed, S=4096, n_stripes=3, pad=256, verify=True):
+def check_matrix(native, oracle_lib, rows, seed, S=4096, n_stripes=3, pad=256, verify=True, rot=0):
     """Batch of n_stripes stripes [inputs..., outputs...] of S bytes (2 KiB
     chunks), shard stride S + pad: emulated kernel vs the oracle."""
     rows = np.ascontiguousarray(rows, dtype=np.uint8)
@@ -122,7 +123,7 @@ def check_matrix(native, oracle_lib, rows, seed, S=4096, n_stripes=3, pad=256, v
         perm[:, in_idx[i]] = view[:, i]
     view[:] = perm
     lib, ops = host_kernel(native, rows, False)
-    run_batch(lib, buf, in_idx, out_idx, total * stride, stride, S // 2048, n_stripes)
+    run_batch(lib, buf, in_idx, out_idx, total * stride, stride, S // 2048, n_stripes, rot=rot)
     for t in range(n_stripes):
         ins = [np.ascontiguousarray(view[t, in_idx[i], :S]) for i in range(nin)]
         outs = [np.zeros(S, np.uint8) for _ in range(nout)]
@@ -170,6 +171,12 @@ def test_random_matrices(native, oracle_lib, nin, nout, seed):
         rows[0, 1] = 1
         rows[-1, -1] = 255
     check_matrix(native, oracle_lib, rows, seed=seed, n_stripes=2)
+
+
+def test_chunk_rotation_covers_every_chunk(native, oracle_lib):
+    """Block order with a per-stripe chunk rotation (3 chunks, rotation 2)."""
+    G = oracle_lib.build_matrix(4, 6)
+    check_matrix(native, oracle_lib, G[4:], seed=3, S=3 * 2048, n_stripes=4, verify=False, rot=2)
 
 
 def test_zero_row_writes_zeros(native, oracle_lib):
