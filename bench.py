@@ -490,7 +490,7 @@ def clobber(torch, buf, lay, total_shards, present, dev):
     v[mask] = 0x5A
 
 
-def other_configs(torch, rsamd, rdev, dev, stream, alloc="hipmalloc"):
+def other_configs(torch, rsamd, rdev, dev, stream, alloc="contiguous"):
     """BASELINE configs[3] per-GPU share at N=8 (10+4 x 4 MiB x 128, packed and
     4 KiB-padded) and configs[4] (4+2 x 4 KiB x 1 M stripes), encode, decode,
     verify, and per-stripe erasure patterns (row f2)."""
@@ -502,7 +502,8 @@ def other_configs(torch, rsamd, rdev, dev, stream, alloc="hipmalloc"):
                                         ("cfg4_4p2_4KiB_x1M", 4, 2, 4096, 1 << 20, (0, 1), 0)]:
         rs = rsamd.ReedSolomon.create(k, m)
         lay = StripeLayout.packed(B, k + m, S, pad=pad)
-        buf = stripe_pool(torch, rdev, lay.nbytes, dev, alloc)
+        pool = stripe_pool(torch, rdev, lay.nbytes, dev, alloc)
+        buf = pool.tensor() if isinstance(pool, rdev.DeviceBuffer) else pool
         rdev.fill_synthetic(buf.data_ptr(), k, lay, SEED, 0, stream)
         t = timed(torch, stream, lambda: rdev.encode(rs, buf.data_ptr(), lay, stream), 10)
         out[name + "_encode_GiBps"] = round(k * S * B / t / 2**30, 2)
@@ -562,7 +563,11 @@ def other_configs(torch, rsamd, rdev, dev, stream, alloc="hipmalloc"):
             rdev.verify(rs, buf.data_ptr(), lay, flag.data_ptr(), stream)
             out[name + "_decode_masked_bits_verified"] = int(flag.item()) == 0
         del buf
+        if isinstance(pool, rdev.DeviceBuffer):
+            pool.free()
+        del pool
         torch.cuda.empty_cache()
+    out["other_configs_alloc"] = alloc_note(True) if alloc == "contiguous" else alloc_note(None)
     return out
 
 

@@ -115,6 +115,14 @@ RS_API int rs_is_parity_correct(const rs_codec *codec, uint8_t *const *shards, i
                          const int64_t *shard_lens, int32_t first_byte, int32_t byte_count,
                          const uint8_t *temp, int64_t temp_len, int *result);
 
+/* ReedSolomon.checkBuffersAndSizes (ReedSolomon.java:277-302) alone, on the
+ * shard count and lengths: the checks (same order, same error codes and
+ * text) every host entry point above starts with.  A JNI shim that stages
+ * large calls through its own buffers validates with it
+ * before copying anything. */
+RS_API int rs_check_buffers_and_sizes(const rs_codec *codec, int nshards, const int64_t *shard_lens,
+                                      int64_t offset, int64_t byte_count);
+
 /* CodingLoop.codeSomeShards(matrixRows, inputs, inputCount, outputs, outputCount,
  * offset, byteCount) (CodingLoop.java:79-85; default impl
  * InputOutputByteTableCodingLoop.java:12-44): outputs[o][b] =

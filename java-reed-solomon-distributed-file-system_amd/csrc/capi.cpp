@@ -96,17 +96,18 @@ int run_host(const std::vector<DevPlan> &plans, int nslots, const std::vector<in
 }
 
 // ReedSolomon.checkBuffersAndSizes (ReedSolomon.java:277-302), same order and text.
+// shards == NULL with check_ptrs false: the sizes only (rs_check_buffers_and_sizes).
 int check_buffers_and_sizes(const Codec &c, uint8_t *const *shards, int nshards, const int64_t *lens,
-                            int64_t offset, int64_t count) {
+                            int64_t offset, int64_t count, bool check_ptrs = true) {
     if (nshards != c.total()) return fail(RS_E_WRONG_NSHARDS, "wrong number of shards: " + std::to_string(nshards));
-    if (!shards || !lens) return fail(RS_E_INVALID, "shards and shard_lens must not be NULL");
+    if ((check_ptrs && !shards) || !lens) return fail(RS_E_INVALID, "shards and shard_lens must not be NULL");
     for (int i = 1; i < nshards; ++i)
         if (lens[i] != lens[0]) return fail(RS_E_SIZE_MISMATCH, "Shards are different sizes");
     if (offset < 0) return fail(RS_E_NEG_OFFSET, "offset is negative: " + std::to_string(offset));
     if (count < 0) return fail(RS_E_NEG_COUNT, "byteCount is negative: " + std::to_string(count));
     if (lens[0] < offset + count)  // Java concatenates the two ints (ReedSolomon.java:300)
         return fail(RS_E_TOO_SMALL, "buffers to small: " + std::to_string(count) + std::to_string(offset));
-    for (int i = 0; i < nshards; ++i)
+    for (int i = 0; check_ptrs && i < nshards; ++i)
         if (!shards[i] && lens[i] > 0) return fail(RS_E_INVALID, "shard " + std::to_string(i) + " is NULL");
     return RS_OK;
 }
@@ -880,6 +881,12 @@ int rs_dev_free(void *ptr) {
 int rs_debug_block_order(int rot, int xcd) {
     rsamd::set_debug_block_order(rot, xcd);
     return RS_OK;
+}
+
+int rs_check_buffers_and_sizes(const rs_codec *codec, int nshards, const int64_t *shard_lens, int64_t offset,
+                               int64_t byte_count) {
+    if (!codec) return fail(RS_E_INVALID, "NULL codec");
+    return check_buffers_and_sizes(*codec->impl, nullptr, nshards, shard_lens, offset, byte_count, false);
 }
 
 int rs_xornet_source(const uint8_t *rows, int nin, int nout, int verify, char *buf, size_t cap, int *ops) {

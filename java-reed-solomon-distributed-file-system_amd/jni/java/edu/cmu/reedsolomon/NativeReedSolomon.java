@@ -64,6 +64,14 @@ public final class NativeReedSolomon implements AutoCloseable {
                                      stream);
     }
 
+    /**
+     * Frees the calling thread's GPU contexts (HIP streams, device and pinned
+     * staging buffers); call from worker threads before a pool retires them.
+     */
+    public static void releaseThreadResources() {
+        nativeThreadRelease();
+    }
+
     @Override
     public synchronized void close() {
         if (handle != 0) {
@@ -73,6 +81,7 @@ public final class NativeReedSolomon implements AutoCloseable {
     }
 
     private static native long nativeCreate(int k, int m);
+    private static native void nativeThreadRelease();
     private static native void nativeDestroy(long h);
     private static native void nativeEncodeParity(long h, byte[][] shards, int offset, int byteCount);
     private static native void nativeDecodeMissing(long h, byte[][] shards, boolean[] present, int offset, int byteCount);

@@ -1,0 +1,450 @@
+/*
+ * rs_jni_core.c -- see rs_jni_core.h.
+ *
+ * Two ways a call reaches the GPU:
+ *  - byte_count <= RSJ_PIN_MAX_BYTES: every Java array is pinned with
+ *    GetPrimitiveArrayCritical, librsamd codes the range straight from/to the
+ *    pinned memory, outputs are released with mode 0 (commit) and inputs with
+ *    JNI_ABORT.  No JNI call is made while a critical region is open.
+ *  - larger calls: the arguments are validated first (same checks and order as
+ *    the reference), then the range is coded in slices of RSJ_SLICE_BYTES:
+ *    inputs copied in with GetByteArrayRegion, outputs copied back with
+ *    SetByteArrayRegion.  No critical region is held, so a long call never
+ *    blocks the garbage collector.
+ * Element references of the byte[][] arrays are local references: capacity is
+ * ensured up front and each one is deleted before returning.
+ */
+#include "rs_jni_core.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define NPE "java/lang/NullPointerException"
+#define IAE "java/lang/IllegalArgumentException"
+#define ISE "java/lang/IllegalStateException"
+#define AIOOBE "java/lang/ArrayIndexOutOfBoundsException"
+
+const rsj_backend *rsj_librsamd_backend(void) {
+    static const rsj_backend b = {rs_encode_parity,           rs_decode_missing,         rs_is_parity_correct,
+                                  rs_code_some_shards,        rs_check_some_shards,      rs_check_buffers_and_sizes,
+                                  rs_codec_total_shard_count, rs_codec_data_shard_count, rs_last_error_message};
+    return &b;
+}
+
+static void throw_rc(rsj_env *e, const rsj_backend *b, int rc) {
+    e->throw_new(e, (rc == RS_E_HIP || rc == RS_E_NO_DEVICE) ? ISE : IAE, b->last_error());
+}
+
+/* Java's message for a[index] past the end: "Index 5 out of bounds for length 5". */
+static void throw_index(rsj_env *e, int64_t index, int64_t length) {
+    char msg[96];
+    snprintf(msg, sizeof msg, "Index %lld out of bounds for length %lld", (long long)index, (long long)length);
+    e->throw_new(e, AIOOBE, msg);
+}
+
+/* ---- byte[][] views ---- */
+
+typedef struct {
+    int n;
+    rsj_obj arr[RSJ_MAX_SHARDS];
+    int64_t len[RSJ_MAX_SHARDS];
+    uint8_t *ptr[RSJ_MAX_SHARDS];
+} arrays;
+
+static void drop_refs(rsj_env *e, arrays *a) {
+    for (int i = 0; i < a->n; i++)
+        if (a->arr[i]) e->delete_local(e, a->arr[i]);
+    a->n = 0;
+}
+
+/* Takes the first n elements of a byte[][] as local references with their
+ * lengths.  A null element throws NullPointerException (where Java would
+ * dereference it).  Returns 0, or -1 with an exception pending. */
+static int take(rsj_env *e, rsj_obj outer, int n, arrays *a) {
+    a->n = 0;
+    memset(a->ptr, 0, sizeof a->ptr);
+    if (n > RSJ_MAX_SHARDS) n = RSJ_MAX_SHARDS;
+    if (n > 0 && e->ensure_local_capacity(e, n + 4) < 0) return -1;
+    for (int i = 0; i < n; i++) {
+        rsj_obj x = e->object_element(e, outer, i);
+        if (e->exception_pending(e)) {
+            drop_refs(e, a);
+            return -1;
+        }
+        a->arr[i] = x;
+        a->n = i + 1;
+        if (!x) {
+            drop_refs(e, a);
+            e->throw_new(e, NPE, "byte[] element is null");
+            return -1;
+        }
+        a->len[i] = e->array_length(e, x);
+    }
+    return 0;
+}
+
+static void pin(rsj_env *e, arrays *a) {
+    for (int i = 0; i < a->n; i++) a->ptr[i] = e->critical_get(e, a->arr[i]);
+}
+
+/* mode_of[i] (or `mode` for all when NULL), in reverse order of pinning. */
+static void unpin(rsj_env *e, arrays *a, const int *mode_of, int mode) {
+    for (int i = a->n - 1; i >= 0; i--)
+        if (a->ptr[i]) {
+            e->critical_release(e, a->arr[i], a->ptr[i], mode_of ? mode_of[i] : mode);
+            a->ptr[i] = NULL;
+        }
+}
+
+static int pinned_ok(const arrays *a) {
+    for (int i = 0; i < a->n; i++)
+        if (!a->ptr[i] && a->len[i] > 0) return 0;
+    return 1;
+}
+
+/* Slice buffers for the staged path: one RSJ_SLICE_BYTES buffer per array. */
+static uint8_t *slice_buffers(int n, uint8_t **ptrs) {
+    uint8_t *mem = (uint8_t *)malloc((size_t)(n > 0 ? n : 1) * RSJ_SLICE_BYTES);
+    for (int i = 0; mem && i < n; i++) ptrs[i] = mem + (size_t)i * RSJ_SLICE_BYTES;
+    return mem;
+}
+
+/* ---- ReedSolomon (codec-level) natives ---- */
+
+enum { ROLE_NONE = 0, ROLE_IN = 1, ROLE_OUT = 2 };
+enum { OP_ENCODE, OP_DECODE, OP_VERIFY };
+
+/* The shard-array call in both modes.  role[i] says whether shard i is read
+ * (copied in on the staged path) and/or written (copied back / committed). */
+static int shard_call(rsj_env *e, const rsj_backend *b, const rs_codec *c, arrays *s, const int *role, int op,
+                      const uint8_t *present, int32_t offset, int32_t count, const uint8_t *temp, int64_t temp_len,
+                      int *result) {
+    int rc;
+    *result = 1;
+    if (op == OP_VERIFY && temp) {  /* checkBuffersAndSizes, then tempBuffer's length (ReedSolomon.java:147-151) */
+        rc = b->check_buffers_and_sizes(c, s->n, s->len, offset, count);
+        if (rc) {
+            throw_rc(e, b, rc);
+            return -1;
+        }
+        if (temp_len < (int64_t)offset + count) {
+            e->throw_new(e, IAE, "tempBuffer is not big enough");
+            return -1;
+        }
+    }
+    if (count <= (int32_t)RSJ_PIN_MAX_BYTES) {
+        int mode_of[RSJ_MAX_SHARDS];
+        for (int i = 0; i < s->n; i++) mode_of[i] = (role[i] & ROLE_OUT) ? RSJ_COMMIT : RSJ_ABORT;
+        pin(e, s);
+        if (!pinned_ok(s)) {
+            unpin(e, s, NULL, RSJ_ABORT);
+            e->throw_new(e, "java/lang/OutOfMemoryError", "GetPrimitiveArrayCritical failed");
+            return -1;
+        }
+        if (op == OP_ENCODE) rc = b->encode_parity(c, s->ptr, s->n, s->len, offset, count);
+        else if (op == OP_DECODE) rc = b->decode_missing(c, s->ptr, s->n, s->len, present, offset, count);
+        else rc = b->is_parity_correct(c, s->ptr, s->n, s->len, offset, count, temp, temp_len, result);
+        /* on an error nothing was written: release everything without copy-back */
+        unpin(e, s, rc ? NULL : mode_of, RSJ_ABORT);
+        if (rc) throw_rc(e, b, rc);
+        return rc ? -1 : 0;
+    }
+    /* staged: validated before any copy (nothing is written on an error path) */
+    rc = b->check_buffers_and_sizes(c, s->n, s->len, offset, count);
+    if (rc) {
+        throw_rc(e, b, rc);
+        return -1;
+    }
+    uint8_t *buf[RSJ_MAX_SHARDS];
+    int64_t lens[RSJ_MAX_SHARDS];
+    uint8_t *mem = slice_buffers(s->n, buf);
+    if (!mem) {
+        e->throw_new(e, "java/lang/OutOfMemoryError", "slice buffers");
+        return -1;
+    }
+    for (int32_t done = 0; done < count && *result;) {
+        const int32_t n = (count - done) < (int32_t)RSJ_SLICE_BYTES ? (count - done) : (int32_t)RSJ_SLICE_BYTES;
+        for (int i = 0; i < s->n; i++) {
+            lens[i] = n;
+            if (role[i] & ROLE_IN) e->byte_region_get(e, s->arr[i], offset + done, n, buf[i]);
+        }
+        if (e->exception_pending(e)) {
+            free(mem);
+            return -1;
+        }
+        int part = 1;
+        if (op == OP_ENCODE) rc = b->encode_parity(c, buf, s->n, lens, 0, n);
+        else if (op == OP_DECODE) rc = b->decode_missing(c, buf, s->n, lens, present, 0, n);
+        else rc = b->is_parity_correct(c, buf, s->n, lens, 0, n, temp ? buf[0] : NULL, temp ? n : 0, &part);
+        if (rc) {
+            free(mem);
+            throw_rc(e, b, rc);
+            return -1;
+        }
+        if (!part) *result = 0;  /* isParityCorrect returns false at the first mismatch */
+        for (int i = 0; i < s->n; i++)
+            if (role[i] & ROLE_OUT) e->byte_region_set(e, s->arr[i], offset + done, n, buf[i]);
+        if (e->exception_pending(e)) {
+            free(mem);
+            return -1;
+        }
+        done += n;
+    }
+    free(mem);
+    return 0;
+}
+
+/* shards.length != totalShardCount is reported before any element is touched
+ * (ReedSolomon.java:280-282); then the elements are taken. */
+static int take_shards(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj shards, arrays *s) {
+    if (!shards) {
+        e->throw_new(e, NPE, "shards is null");
+        return -1;
+    }
+    const int n = e->array_length(e, shards);
+    if (n != b->total_shards(c)) {
+        int64_t none = 0;
+        throw_rc(e, b, b->check_buffers_and_sizes(c, n, &none, 0, 0));
+        return -1;
+    }
+    return take(e, shards, n, s);
+}
+
+void rsj_encode_parity(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj shards, int32_t offset,
+                       int32_t count) {
+    arrays s;
+    if (take_shards(e, b, c, shards, &s)) return;
+    /* data shards are read, parity shards written (ReedSolomon.java:90-104) */
+    const int k = b->data_shards(c);
+    int role[RSJ_MAX_SHARDS];
+    for (int i = 0; i < s.n; i++) role[i] = i < k ? ROLE_IN : ROLE_OUT;
+    int result;
+    shard_call(e, b, c, &s, role, OP_ENCODE, NULL, offset, count, NULL, 0, &result);
+    drop_refs(e, &s);
+}
+
+void rsj_decode_missing(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj shards, rsj_obj present,
+                        int32_t offset, int32_t count) {
+    arrays s;
+    if (take_shards(e, b, c, shards, &s)) return;
+    /* checkBuffersAndSizes first (ReedSolomon.java:185), then shardPresent[i]
+     * for i < totalShardCount (:190-194) */
+    int rc = b->check_buffers_and_sizes(c, s.n, s.len, offset, count);
+    if (rc) {
+        throw_rc(e, b, rc);
+        drop_refs(e, &s);
+        return;
+    }
+    if (!present) {
+        e->throw_new(e, NPE, "shardPresent is null");
+        drop_refs(e, &s);
+        return;
+    }
+    const int np = e->array_length(e, present);
+    if (np < s.n) {
+        throw_index(e, np, np);
+        drop_refs(e, &s);
+        return;
+    }
+    uint8_t pres[RSJ_MAX_SHARDS];
+    e->bool_region_get(e, present, 0, s.n, pres);
+    if (e->exception_pending(e)) {
+        drop_refs(e, &s);
+        return;
+    }
+    int role[RSJ_MAX_SHARDS];
+    for (int i = 0; i < s.n; i++) role[i] = pres[i] ? ROLE_IN : ROLE_OUT;
+    int result;
+    shard_call(e, b, c, &s, role, OP_DECODE, pres, offset, count, NULL, 0, &result);
+    drop_refs(e, &s);
+}
+
+int rsj_is_parity_correct(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj shards, int32_t first,
+                          int32_t count, rsj_obj temp) {
+    arrays s;
+    if (take_shards(e, b, c, shards, &s)) return 0;
+    int role[RSJ_MAX_SHARDS];
+    for (int i = 0; i < s.n; i++) role[i] = ROLE_IN;
+    /* the GPU needs no scratch: only tempBuffer's length is checked (ReedSolomon.java:150) */
+    static const uint8_t dummy = 0;
+    const int64_t temp_len = temp ? e->array_length(e, temp) : 0;
+    int result = 0;
+    const int rc = shard_call(e, b, c, &s, role, OP_VERIFY, NULL, first, count, temp ? &dummy : NULL, temp_len,
+                              &result);
+    drop_refs(e, &s);
+    return rc ? 0 : result;
+}
+
+/* ---- CodingLoop natives ---- */
+
+/* matrixRows[0..nrows) as C rows of ncols bytes.  Java reads
+ * matrixRows[o][i] for i < inputCount: a null row is a NullPointerException,
+ * a short one an ArrayIndexOutOfBoundsException. */
+static int take_rows(rsj_env *e, rsj_obj rows, int nrows, int ncols, uint8_t *flat, const uint8_t **ptrs) {
+    if (!rows) {
+        e->throw_new(e, NPE, "matrixRows is null");
+        return -1;
+    }
+    const int have = e->array_length(e, rows);
+    if (have < nrows) {
+        throw_index(e, have, have);
+        return -1;
+    }
+    for (int r = 0; r < nrows; r++) {
+        rsj_obj a = e->object_element(e, rows, r);
+        if (e->exception_pending(e)) return -1;
+        if (!a) {
+            e->throw_new(e, NPE, "matrix row is null");
+            return -1;
+        }
+        const int len = e->array_length(e, a);
+        if (len < ncols) {
+            e->delete_local(e, a);
+            throw_index(e, len, len);
+            return -1;
+        }
+        e->byte_region_get(e, a, 0, ncols, flat + (size_t)r * ncols);
+        e->delete_local(e, a);
+        if (e->exception_pending(e)) return -1;
+        ptrs[r] = flat + (size_t)r * ncols;
+    }
+    return 0;
+}
+
+/* inputs[0..nin) and outputs[0..nout): counts against the array lengths,
+ * then every array must hold [offset, offset + count) (the Java loops index
+ * each of them over that range). */
+static int take_io(rsj_env *e, rsj_obj ins, int nin, rsj_obj outs, int nout, int32_t offset, int32_t count,
+                   arrays *in, arrays *out) {
+    in->n = out->n = 0;
+    if (!ins || !outs) {
+        e->throw_new(e, NPE, ins ? "outputs is null" : "inputs is null");
+        return -1;
+    }
+    const int li = e->array_length(e, ins), lo = e->array_length(e, outs);
+    if (nin > li) {
+        throw_index(e, li, li);
+        return -1;
+    }
+    if (nout > lo) {
+        throw_index(e, lo, lo);
+        return -1;
+    }
+    if (take(e, ins, nin, in)) return -1;
+    if (take(e, outs, nout, out)) {
+        drop_refs(e, in);
+        return -1;
+    }
+    if (count > 0) {
+        arrays *all[2] = {in, out};
+        for (int w = 0; w < 2; w++)
+            for (int i = 0; i < all[w]->n; i++) {
+                const int64_t len = all[w]->len[i];
+                if (offset < 0 || (int64_t)offset + count > len) {
+                    throw_index(e, offset < 0 ? offset : (len > offset ? len : offset), len);
+                    drop_refs(e, out);
+                    drop_refs(e, in);
+                    return -1;
+                }
+            }
+    }
+    return 0;
+}
+
+static int loop_call(rsj_env *e, const rsj_backend *b, rsj_obj rows, rsj_obj ins, int32_t nin, rsj_obj outs,
+                     int32_t nout, int32_t offset, int32_t count, int verify) {
+    if (nin < 0 || nout < 0 || nin > RSJ_MAX_SHARDS || nout > RSJ_MAX_SHARDS) {
+        e->throw_new(e, IAE, "input/output count out of range (0..256)");
+        return -1;
+    }
+    int result = 1;
+    if (nout == 0) return 1;
+    uint8_t *flat = (uint8_t *)malloc((size_t)nout * (nin > 0 ? nin : 1));
+    const uint8_t *rp[RSJ_MAX_SHARDS];
+    if (!flat) {
+        e->throw_new(e, "java/lang/OutOfMemoryError", "matrix rows");
+        return -1;
+    }
+    if (take_rows(e, rows, nout, nin, flat, rp)) {
+        free(flat);
+        return -1;
+    }
+    arrays in, out;
+    if (take_io(e, ins, nin, outs, nout, offset, count, &in, &out)) {
+        free(flat);
+        return -1;
+    }
+    int rc = 0;
+    if (count <= 0 || nin == 0) {
+        /* nothing is coded (the Java loops do no iterations over bytes) */
+    } else if (count <= (int32_t)RSJ_PIN_MAX_BYTES) {
+        pin(e, &in);
+        pin(e, &out);
+        if (!pinned_ok(&in) || !pinned_ok(&out)) {
+            unpin(e, &out, NULL, RSJ_ABORT);
+            unpin(e, &in, NULL, RSJ_ABORT);
+            e->throw_new(e, "java/lang/OutOfMemoryError", "GetPrimitiveArrayCritical failed");
+            rc = -1;
+        } else {
+            if (verify)
+                rc = b->check_some_shards(rp, (const uint8_t *const *)in.ptr, nin, (const uint8_t *const *)out.ptr,
+                                          nout, offset, count, &result);
+            else
+                rc = b->code_some_shards(rp, (const uint8_t *const *)in.ptr, nin, out.ptr, nout, offset, count);
+            unpin(e, &out, NULL, (verify || rc) ? RSJ_ABORT : RSJ_COMMIT);
+            unpin(e, &in, NULL, RSJ_ABORT);
+            if (rc) throw_rc(e, b, rc);
+        }
+    } else {
+        uint8_t *ib[RSJ_MAX_SHARDS], *ob[RSJ_MAX_SHARDS];
+        uint8_t *mi = slice_buffers(nin, ib), *mo = slice_buffers(nout, ob);
+        if (!mi || !mo) {
+            e->throw_new(e, "java/lang/OutOfMemoryError", "slice buffers");
+            rc = -1;
+        }
+        for (int32_t done = 0; !rc && done < count && result;) {
+            const int32_t n = (count - done) < (int32_t)RSJ_SLICE_BYTES ? (count - done) : (int32_t)RSJ_SLICE_BYTES;
+            for (int i = 0; i < nin; i++) e->byte_region_get(e, in.arr[i], offset + done, n, ib[i]);
+            if (verify)
+                for (int i = 0; i < nout; i++) e->byte_region_get(e, out.arr[i], offset + done, n, ob[i]);
+            if (e->exception_pending(e)) {
+                rc = -1;
+                break;
+            }
+            int part = 1;
+            rc = verify ? b->check_some_shards(rp, (const uint8_t *const *)ib, nin, (const uint8_t *const *)ob, nout, 0,
+                                               n, &part)
+                        : b->code_some_shards(rp, (const uint8_t *const *)ib, nin, ob, nout, 0, n);
+            if (rc) {
+                throw_rc(e, b, rc);
+                break;
+            }
+            if (!part) result = 0;
+            if (!verify)
+                for (int i = 0; i < nout; i++) e->byte_region_set(e, out.arr[i], offset + done, n, ob[i]);
+            if (e->exception_pending(e)) {
+                rc = -1;
+                break;
+            }
+            done += n;
+        }
+        free(mi);
+        free(mo);
+    }
+    drop_refs(e, &out);
+    drop_refs(e, &in);
+    free(flat);
+    return rc ? -1 : result;
+}
+
+void rsj_code_some_shards(rsj_env *e, const rsj_backend *b, rsj_obj rows, rsj_obj inputs, int32_t nin,
+                          rsj_obj outputs, int32_t nout, int32_t offset, int32_t count) {
+    (void)loop_call(e, b, rows, inputs, nin, outputs, nout, offset, count, 0);
+}
+
+int rsj_check_some_shards(rsj_env *e, const rsj_backend *b, rsj_obj rows, rsj_obj inputs, int32_t nin,
+                          rsj_obj to_check, int32_t ncheck, int32_t offset, int32_t count) {
+    const int r = loop_call(e, b, rows, inputs, nin, to_check, ncheck, offset, count, 1);
+    return r > 0;
+}

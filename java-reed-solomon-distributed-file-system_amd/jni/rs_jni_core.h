@@ -1,0 +1,99 @@
+/*
+ * rs_jni_core.h -- the JNI shim's marshalling, in plain C behind a small
+ * environment interface.
+ *
+ * rs_jni.c implements rsj_env over a JNIEnv and exports the Java natives;
+ * tests/jni_mock/ implements it over mock Java arrays, so the marshalling --
+ * argument checks and the exceptions they raise, local-reference accounting,
+ * critical-region pinning for small calls, slice-wise copies for large ones
+ * -- is compiled and tested without a JDK.
+ *
+ * Semantics follow the reference Java code the natives replace:
+ *   ReedSolomon.encodeParity / decodeMissing / isParityCorrect
+ *     (ReedSolomon.java:90-164, 175-272; checks ReedSolomon.java:277-302),
+ *   CodingLoop.codeSomeShards / checkSomeShards
+ *     (CodingLoop.java:79-117, InputOutputByteTableCodingLoop.java:12-89).
+ * Exceptions are the ones the Java code throws: IllegalArgumentException with
+ * its text for the checks, ArrayIndexOutOfBoundsException ("Index i out of
+ * bounds for length n") where Java indexes past an array, NullPointerException
+ * for null arrays, IllegalStateException for a GPU failure.
+ */
+#ifndef RS_JNI_CORE_H
+#define RS_JNI_CORE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "rs_amd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSJ_MAX_SHARDS 256
+#define RSJ_COMMIT 0 /* JNI release mode: copy back and free */
+#define RSJ_ABORT 2  /* JNI_ABORT: free without copying back */
+
+/* Calls with byte_count up to this many bytes pin the Java arrays
+ * (GetPrimitiveArrayCritical) for the whole call; larger calls never hold a
+ * critical region: they are coded in slices of RSJ_SLICE_BYTES copied through
+ * C buffers (Get/SetByteArrayRegion), so the JVM can collect garbage between
+ * slices. */
+#define RSJ_PIN_MAX_BYTES (4u << 20)
+#define RSJ_SLICE_BYTES (4u << 20)
+
+typedef void *rsj_obj; /* a jobject (jarray) */
+
+typedef struct rsj_env rsj_env;
+struct rsj_env {
+    void *ctx;
+    int (*array_length)(rsj_env *e, rsj_obj arr);
+    rsj_obj (*object_element)(rsj_env *e, rsj_obj arr, int i); /* a new local reference, or NULL */
+    void (*delete_local)(rsj_env *e, rsj_obj obj);
+    int (*ensure_local_capacity)(rsj_env *e, int n);            /* 0, or < 0 with an exception pending */
+    uint8_t *(*critical_get)(rsj_env *e, rsj_obj arr);
+    void (*critical_release)(rsj_env *e, rsj_obj arr, uint8_t *p, int mode);
+    void (*byte_region_get)(rsj_env *e, rsj_obj arr, int start, int len, uint8_t *dst);
+    void (*byte_region_set)(rsj_env *e, rsj_obj arr, int start, int len, const uint8_t *src);
+    void (*bool_region_get)(rsj_env *e, rsj_obj arr, int start, int len, uint8_t *dst);
+    int (*exception_pending)(rsj_env *e);
+    void (*throw_new)(rsj_env *e, const char *cls, const char *msg);
+};
+
+/* The coding entry points (librsamd.so's by default; tests substitute fakes). */
+typedef struct rsj_backend {
+    int (*encode_parity)(const rs_codec *, uint8_t *const *, int, const int64_t *, int32_t, int32_t);
+    int (*decode_missing)(const rs_codec *, uint8_t *const *, int, const int64_t *, const uint8_t *, int32_t,
+                          int32_t);
+    int (*is_parity_correct)(const rs_codec *, uint8_t *const *, int, const int64_t *, int32_t, int32_t,
+                             const uint8_t *, int64_t, int *);
+    int (*code_some_shards)(const uint8_t *const *, const uint8_t *const *, int, uint8_t *const *, int, int32_t,
+                            int32_t);
+    int (*check_some_shards)(const uint8_t *const *, const uint8_t *const *, int, const uint8_t *const *, int,
+                             int32_t, int32_t, int *);
+    int (*check_buffers_and_sizes)(const rs_codec *, int, const int64_t *, int64_t, int64_t);
+    int (*total_shards)(const rs_codec *);
+    int (*data_shards)(const rs_codec *);
+    const char *(*last_error)(void);
+} rsj_backend;
+
+const rsj_backend *rsj_librsamd_backend(void);
+
+/* The natives.  Each returns with the Java-visible outcome: results written
+ * to the arrays, or an exception pending in `e`. */
+void rsj_encode_parity(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj shards, int32_t offset,
+                       int32_t count);
+void rsj_decode_missing(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj shards, rsj_obj present,
+                        int32_t offset, int32_t count);
+/* temp may be NULL (the two-argument isParityCorrect). */
+int rsj_is_parity_correct(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj shards, int32_t first,
+                          int32_t count, rsj_obj temp);
+void rsj_code_some_shards(rsj_env *e, const rsj_backend *b, rsj_obj rows, rsj_obj inputs, int32_t nin,
+                          rsj_obj outputs, int32_t nout, int32_t offset, int32_t count);
+int rsj_check_some_shards(rsj_env *e, const rsj_backend *b, rsj_obj rows, rsj_obj inputs, int32_t nin,
+                          rsj_obj to_check, int32_t ncheck, int32_t offset, int32_t count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RS_JNI_CORE_H */

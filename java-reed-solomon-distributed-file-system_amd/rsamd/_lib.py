@@ -34,6 +34,7 @@ SIGNATURES = {
     "rs_decode_missing": (C.c_int, [C.c_void_p, u8pp, C.c_int, C.POINTER(C.c_int64), u8p, C.c_int32, C.c_int32]),
     "rs_is_parity_correct": (C.c_int, [C.c_void_p, u8pp, C.c_int, C.POINTER(C.c_int64), C.c_int32, C.c_int32, u8p,
                                        C.c_int64, C.POINTER(C.c_int)]),
+    "rs_check_buffers_and_sizes": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_int64), C.c_int64, C.c_int64]),
     "rs_code_some_shards": (C.c_int, [u8pp, u8pp, C.c_int, u8pp, C.c_int, C.c_int32, C.c_int32]),
     "rs_check_some_shards": (C.c_int, [u8pp, u8pp, C.c_int, u8pp, C.c_int, C.c_int32, C.c_int32,
                                        C.POINTER(C.c_int)]),

@@ -122,6 +122,16 @@ class DeviceBuffer:
     def data_ptr(self) -> int:
         return self._ptr
 
+    @property
+    def __cuda_array_interface__(self):
+        """Lets torch.as_tensor(buf, device=...) view the pool as uint8 (no copy)."""
+        return {"shape": (self.nbytes,), "typestr": "|u1", "data": (self._ptr, False), "version": 2}
+
+    def tensor(self):
+        """A torch uint8 tensor aliasing the pool (valid while the pool lives)."""
+        import torch
+        return torch.as_tensor(self, device=self.device)
+
     def numel(self) -> int:
         return self.nbytes
 

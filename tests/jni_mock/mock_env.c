@@ -1,0 +1,268 @@
+/*
+ * mock_env.c -- a mock JNI environment for rs_jni_core.c (TEST ONLY).
+ *
+ * Java arrays are heap objects (byte[], boolean[], Object[]).  The mock keeps
+ * the books a real JVM would enforce with -Xcheck:jni:
+ *   - local references: live count, high-water mark, the capacity the code
+ *     ensured (a native frame gets 16 without EnsureLocalCapacity);
+ *   - critical regions: open count, and every JNI call made while one is open
+ *     (illegal) is counted as a violation;
+ *   - a pending exception: class and message; JNI calls other than
+ *     ExceptionCheck / DeleteLocalRef / releases with one pending are counted
+ *     as violations too;
+ *   - region copies in and out (bytes), to tell the pinned and staged paths apart.
+ * It also provides a fake coding backend (codes out[p][b] = XOR_i in[i][b] ^
+ * (p + 1), checks nothing but pointers) so the CPU tests see data movement.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "rs_jni_core.h"
+
+enum { K_BYTES = 1, K_BOOLS = 2, K_OBJECTS = 3 };
+
+typedef struct mobj {
+    int kind, len;
+    uint8_t *data;        /* bytes / booleans */
+    struct mobj **elems;  /* objects */
+} mobj;
+
+typedef struct {
+    int live_refs, max_live_refs, capacity;
+    int critical_open, max_critical_open;
+    int violations;
+    int exc;
+    char exc_cls[128], exc_msg[512];
+    long long bytes_in, bytes_out, critical_gets, commits, aborts;
+    int fail_critical;     /* critical_get returns NULL when set */
+} mstate;
+
+static mstate S;
+
+/* ---- objects (exported to the Python test) ---- */
+
+mobj *mock_new_bytes(int len) {
+    mobj *o = (mobj *)calloc(1, sizeof *o);
+    o->kind = K_BYTES;
+    o->len = len;
+    o->data = (uint8_t *)calloc((size_t)(len > 0 ? len : 1), 1);
+    return o;
+}
+mobj *mock_new_bools(int len) {
+    mobj *o = mock_new_bytes(len);
+    o->kind = K_BOOLS;
+    return o;
+}
+mobj *mock_new_objects(int len) {
+    mobj *o = (mobj *)calloc(1, sizeof *o);
+    o->kind = K_OBJECTS;
+    o->len = len;
+    o->elems = (mobj **)calloc((size_t)(len > 0 ? len : 1), sizeof(mobj *));
+    return o;
+}
+void mock_set(mobj *outer, int i, mobj *inner) { outer->elems[i] = inner; }
+uint8_t *mock_data(mobj *o) { return o->data; }
+void mock_reset(void) { memset(&S, 0, sizeof S); S.capacity = 16; }
+void mock_fail_critical(int on) { S.fail_critical = on; }
+const char *mock_exc_class(void) { return S.exc ? S.exc_cls : ""; }
+const char *mock_exc_message(void) { return S.exc ? S.exc_msg : ""; }
+void mock_stats(long long *out) {
+    out[0] = S.live_refs;
+    out[1] = S.max_live_refs;
+    out[2] = S.capacity;
+    out[3] = S.critical_open;
+    out[4] = S.max_critical_open;
+    out[5] = S.violations;
+    out[6] = S.bytes_in;
+    out[7] = S.bytes_out;
+    out[8] = S.critical_gets;
+    out[9] = S.commits;
+    out[10] = S.aborts;
+}
+
+/* ---- rsj_env over the mock ---- */
+
+static void jni_call(int allowed_with_exception) {
+    if (S.critical_open) S.violations++;
+    if (S.exc && !allowed_with_exception) S.violations++;
+}
+
+static int m_array_length(rsj_env *e, rsj_obj a) {
+    jni_call(0);
+    return ((mobj *)a)->len;
+}
+static rsj_obj m_object_element(rsj_env *e, rsj_obj a, int i) {
+    jni_call(0);
+    mobj *o = (mobj *)a;
+    if (i < 0 || i >= o->len) {
+        S.exc = 1;
+        strcpy(S.exc_cls, "java/lang/ArrayIndexOutOfBoundsException");
+        strcpy(S.exc_msg, "GetObjectArrayElement");
+        return NULL;
+    }
+    if (!o->elems[i]) return NULL;
+    S.live_refs++;
+    if (S.live_refs > S.max_live_refs) S.max_live_refs = S.live_refs;
+    if (S.live_refs > S.capacity) S.violations++;
+    return o->elems[i];
+}
+static void m_delete_local(rsj_env *e, rsj_obj o) {
+    jni_call(1);
+    S.live_refs--;
+}
+static int m_ensure_local_capacity(rsj_env *e, int n) {
+    jni_call(0);
+    if (S.live_refs + n > S.capacity) S.capacity = S.live_refs + n;
+    return 0;
+}
+static uint8_t *m_critical_get(rsj_env *e, rsj_obj a) {
+    if (S.exc) S.violations++;
+    if (S.fail_critical) return NULL;
+    S.critical_open++;
+    S.critical_gets++;
+    if (S.critical_open > S.max_critical_open) S.max_critical_open = S.critical_open;
+    return ((mobj *)a)->data;
+}
+static void m_critical_release(rsj_env *e, rsj_obj a, uint8_t *p, int mode) {
+    S.critical_open--;
+    if (mode == RSJ_COMMIT) S.commits++;
+    else S.aborts++;
+}
+static void bounds(mobj *o, int start, int len) {
+    if (start < 0 || len < 0 || start + len > o->len) {
+        S.exc = 1;
+        strcpy(S.exc_cls, "java/lang/ArrayIndexOutOfBoundsException");
+        strcpy(S.exc_msg, "region");
+    }
+}
+static void m_byte_region_get(rsj_env *e, rsj_obj a, int start, int len, uint8_t *dst) {
+    jni_call(0);
+    mobj *o = (mobj *)a;
+    bounds(o, start, len);
+    if (S.exc) return;
+    memcpy(dst, o->data + start, (size_t)len);
+    S.bytes_in += len;
+}
+static void m_byte_region_set(rsj_env *e, rsj_obj a, int start, int len, const uint8_t *src) {
+    jni_call(0);
+    mobj *o = (mobj *)a;
+    bounds(o, start, len);
+    if (S.exc) return;
+    memcpy(o->data + start, src, (size_t)len);
+    S.bytes_out += len;
+}
+static void m_bool_region_get(rsj_env *e, rsj_obj a, int start, int len, uint8_t *dst) {
+    m_byte_region_get(e, a, start, len, dst);
+}
+static int m_exception_pending(rsj_env *e) {
+    if (S.critical_open) S.violations++;
+    return S.exc;
+}
+static void m_throw_new(rsj_env *e, const char *cls, const char *msg) {
+    jni_call(0);
+    S.exc = 1;
+    strncpy(S.exc_cls, cls, sizeof S.exc_cls - 1);
+    strncpy(S.exc_msg, msg ? msg : "", sizeof S.exc_msg - 1);
+}
+
+static rsj_env ENV = {NULL,           m_array_length,    m_object_element,   m_delete_local,
+                      m_ensure_local_capacity, m_critical_get, m_critical_release, m_byte_region_get,
+                      m_byte_region_set, m_bool_region_get, m_exception_pending, m_throw_new};
+
+/* ---- fake backend: real argument checks from librsamd, fake coding ---- */
+
+static int fake_data_shards(const rs_codec *c) { return rs_codec_data_shard_count(c); }
+
+static int fake_encode(const rs_codec *c, uint8_t *const *sh, int n, const int64_t *lens, int32_t off, int32_t cnt) {
+    int rc = rs_check_buffers_and_sizes(c, n, lens, off, cnt);
+    if (rc) return rc;
+    const int k = rs_codec_data_shard_count(c);
+    for (int p = k; p < n; p++)
+        for (int32_t b = off; b < off + cnt; b++) {
+            uint8_t x = (uint8_t)(p - k + 1);
+            for (int i = 0; i < k; i++) x ^= sh[i][b];
+            sh[p][b] = x;
+        }
+    return 0;
+}
+static int fake_decode(const rs_codec *c, uint8_t *const *sh, int n, const int64_t *lens, const uint8_t *pres,
+                       int32_t off, int32_t cnt) {
+    int rc = rs_check_buffers_and_sizes(c, n, lens, off, cnt);
+    if (rc) return rc;
+    /* missing shard j := XOR of the present shards ^ 0x80 ^ j (data movement only) */
+    for (int j = 0; j < n; j++) {
+        if (pres[j]) continue;
+        for (int32_t b = off; b < off + cnt; b++) {
+            uint8_t x = (uint8_t)(0x80 ^ j);
+            for (int i = 0; i < n; i++)
+                if (pres[i]) x ^= sh[i][b];
+            sh[j][b] = x;
+        }
+    }
+    return 0;
+}
+static int fake_verify(const rs_codec *c, uint8_t *const *sh, int n, const int64_t *lens, int32_t off, int32_t cnt,
+                       const uint8_t *temp, int64_t temp_len, int *result) {
+    int rc = rs_check_buffers_and_sizes(c, n, lens, off, cnt);
+    if (rc) return rc;
+    const int k = rs_codec_data_shard_count(c);
+    *result = 1;
+    for (int p = k; p < n && *result; p++)
+        for (int32_t b = off; b < off + cnt; b++) {
+            uint8_t x = (uint8_t)(p - k + 1);
+            for (int i = 0; i < k; i++) x ^= sh[i][b];
+            if (sh[p][b] != x) {
+                *result = 0;
+                break;
+            }
+        }
+    return 0;
+}
+static int fake_code(const uint8_t *const *rows, const uint8_t *const *in, int nin, uint8_t *const *out, int nout,
+                     int32_t off, int32_t cnt) {
+    for (int p = 0; p < nout; p++)
+        for (int32_t b = off; b < off + cnt; b++) {
+            uint8_t x = 0;
+            for (int i = 0; i < nin; i++) x ^= (uint8_t)(in[i][b] + rows[p][i]);
+            out[p][b] = x;
+        }
+    return 0;
+}
+static int fake_check(const uint8_t *const *rows, const uint8_t *const *in, int nin, const uint8_t *const *chk,
+                      int nchk, int32_t off, int32_t cnt, int *result) {
+    *result = 1;
+    for (int p = 0; p < nchk; p++)
+        for (int32_t b = off; b < off + cnt; b++) {
+            uint8_t x = 0;
+            for (int i = 0; i < nin; i++) x ^= (uint8_t)(in[i][b] + rows[p][i]);
+            if (chk[p][b] != x) *result = 0;
+        }
+    return 0;
+}
+
+static const rsj_backend FAKE = {fake_encode,       fake_decode,         fake_verify,
+                                 fake_code,         fake_check,          rs_check_buffers_and_sizes,
+                                 rs_codec_total_shard_count, fake_data_shards, rs_last_error_message};
+
+static const rsj_backend *backend(int real) { return real ? rsj_librsamd_backend() : &FAKE; }
+
+/* ---- entry points for the Python test (backend: 0 fake, 1 librsamd) ---- */
+
+void mock_encode_parity(int real, const rs_codec *c, mobj *shards, int32_t off, int32_t cnt) {
+    rsj_encode_parity(&ENV, backend(real), c, shards, off, cnt);
+}
+void mock_decode_missing(int real, const rs_codec *c, mobj *shards, mobj *present, int32_t off, int32_t cnt) {
+    rsj_decode_missing(&ENV, backend(real), c, shards, present, off, cnt);
+}
+int mock_is_parity_correct(int real, const rs_codec *c, mobj *shards, int32_t first, int32_t cnt, mobj *temp) {
+    return rsj_is_parity_correct(&ENV, backend(real), c, shards, first, cnt, temp);
+}
+void mock_code_some_shards(int real, mobj *rows, mobj *in, int32_t nin, mobj *out, int32_t nout, int32_t off,
+                           int32_t cnt) {
+    rsj_code_some_shards(&ENV, backend(real), rows, in, nin, out, nout, off, cnt);
+}
+int mock_check_some_shards(int real, mobj *rows, mobj *in, int32_t nin, mobj *chk, int32_t nchk, int32_t off,
+                           int32_t cnt) {
+    return rsj_check_some_shards(&ENV, backend(real), rows, in, nin, chk, nchk, off, cnt);
+}

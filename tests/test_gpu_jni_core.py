@@ -1,0 +1,87 @@
+"""The JNI shim's marshalling (jni/rs_jni_core.c) over the real librsamd
+backend on the GPU, through the mock JNI environment of test_jni_core.py:
+Java-array in, Java-array out, compared with the oracle byte for byte, on both
+of the shim's paths (pinned critical regions for small calls, slice-wise
+copies above 4 MiB), with the reference's offsets and erasure patterns
+(ReedSolomon.java:90-104, 175-272; ReedSolomonTest.java:77-93's {0, 5}).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from test_jni_core import PIN_MAX, Jvm, build_mock
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mocklib():
+    return build_mock()
+
+
+@pytest.fixture
+def jvm(mocklib):
+    return Jvm(mocklib)
+
+
+@pytest.fixture(scope="module")
+def codec104(native):
+    h = C.c_void_p()
+    assert native.rs_codec_create(10, 4, C.byref(h)) == 0
+    yield h
+    native.rs_codec_destroy(h)
+
+
+@pytest.mark.parametrize("k,m,off,cnt", [(4, 2, 17, 100000), (4, 2, 3, PIN_MAX + 4099), (10, 4, 0, 65536),
+                                         (10, 4, 5, PIN_MAX + 1)])
+def test_encode_decode_through_shim(gpu, oracle_lib, native, jvm, k, m, off, cnt):
+    h = C.c_void_p()
+    assert native.rs_codec_create(k, m, C.byref(h)) == 0
+    try:
+        S = off + cnt + 11
+        rng = np.random.default_rng(cnt)
+        data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
+        ref = [d.copy() for d in data]
+        oracle_lib.Codec(k, m).encode_parity(ref, off, cnt)
+        arrs = [jvm.bytes(d) for d in data]
+        jvm.lib.mock_encode_parity(1, h, jvm.objects(arrs), off, cnt)
+        assert jvm.exception() == ("", "")
+        for i in range(k + m):
+            assert np.array_equal(jvm.read(arrs[i], S), ref[i]), i
+        jvm.assert_clean()
+        assert jvm.lib.mock_is_parity_correct(1, h, jvm.objects(arrs), off, cnt, None) == 1
+        # erase and decode: {0, k+m-1} (the reference test's {0, 5} for 4+2), plus one more for 10+4
+        miss = [0, k + m - 1] + ([3, 7] if k == 10 else [])
+        present = [i not in miss for i in range(k + m)]
+        for j in miss:
+            arrs[j] = jvm.bytes(np.full(S, 0x5A, np.uint8))
+        jvm.lib.mock_decode_missing(1, h, jvm.objects(arrs), jvm.bools(present), off, cnt)
+        assert jvm.exception() == ("", "")
+        for j in miss:
+            got = jvm.read(arrs[j], S)
+            assert np.array_equal(got[off:off + cnt], ref[j][off:off + cnt]), j
+            assert (got[:off] == 0x5A).all() and (got[off + cnt:] == 0x5A).all()  # outside the range untouched
+        jvm.assert_clean()
+    finally:
+        native.rs_codec_destroy(h)
+
+
+@pytest.mark.parametrize("cnt", [5000, PIN_MAX + 333])
+def test_code_some_shards_through_shim(gpu, oracle_lib, jvm, cnt):
+    rng = np.random.default_rng(cnt)
+    nin, nout, off = 5, 3, 9
+    S = off + cnt + 4
+    rows = rng.integers(0, 256, (nout, nin), dtype=np.uint8)
+    ins = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(nin)]
+    want = [np.zeros(S, np.uint8) for _ in range(nout)]
+    oracle_lib.code_some_shards(7, rows, ins, want, off, cnt)
+    outs = [jvm.bytes(np.zeros(S, np.uint8)) for _ in range(nout)]
+    R = jvm.objects([jvm.bytes(r) for r in rows])
+    I = jvm.objects([jvm.bytes(a) for a in ins])
+    jvm.lib.mock_code_some_shards(1, R, I, nin, jvm.objects(outs), nout, off, cnt)
+    assert jvm.exception() == ("", "")
+    for p in range(nout):
+        assert np.array_equal(jvm.read(outs[p], S), want[p]), p
+    assert jvm.lib.mock_check_some_shards(1, R, I, nin, jvm.objects(outs), nout, off, cnt) == 1
+    jvm.assert_clean()

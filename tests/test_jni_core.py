@@ -1,0 +1,373 @@
+"""The JNI shim's marshalling (jni/rs_jni_core.c) against a mock JNI
+environment (tests/jni_mock/mock_env.c), on CPU.
+
+rs_jni.c only adapts JNIEnv to rs_jni_core's interface; everything the natives
+decide -- which exception the reference Java code would throw and with what
+text (ReedSolomon.java:277-302 and :175-272, InputOutputByteTableCodingLoop
+.java:12-44), local-reference accounting, pinning small calls in critical
+regions vs copying large ones slice by slice, which arrays are committed --
+is checked here.  A fake coding backend (data movement only) stands in for the
+GPU; test_gpu_jni_core.py runs the same marshalling over librsamd on a GPU.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import PKG_DIR, ROOT
+
+BUILD = os.path.join(ROOT, "build", "jni_mock")
+SRC = [os.path.join(PKG_DIR, "jni", "rs_jni_core.c"), os.path.join(ROOT, "tests", "jni_mock", "mock_env.c")]
+LIBDIR = os.path.join(PKG_DIR, "lib")
+PIN_MAX = 4 << 20
+SLICE = 4 << 20
+
+NPE = "java/lang/NullPointerException"
+IAE = "java/lang/IllegalArgumentException"
+ISE = "java/lang/IllegalStateException"
+AIOOBE = "java/lang/ArrayIndexOutOfBoundsException"
+
+
+def build_mock():
+    from rsamd import _lib
+    _lib.load()  # the HIP runtime and librsamd first (see _lib.load)
+    os.makedirs(BUILD, exist_ok=True)
+    so = os.path.join(BUILD, "libmockjni.so")
+    if not os.path.exists(so) or any(os.path.getmtime(s) > os.path.getmtime(so) for s in SRC):
+        subprocess.run(["gcc", "-std=c11", "-O1", "-g", "-Wall", "-Wextra", "-Werror", "-Wno-unused-parameter",
+                        "-shared", "-fPIC", "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(PKG_DIR, "jni"),
+                        *SRC, "-L" + LIBDIR, "-lrsamd", "-Wl,-rpath," + LIBDIR, "-o", so], check=True)
+    lib = C.CDLL(so)
+    P = C.c_void_p
+    for name, res, args in [
+        ("mock_new_bytes", P, [C.c_int]), ("mock_new_bools", P, [C.c_int]), ("mock_new_objects", P, [C.c_int]),
+        ("mock_set", None, [P, C.c_int, P]), ("mock_data", P, [P]), ("mock_reset", None, []),
+        ("mock_fail_critical", None, [C.c_int]),
+        ("mock_exc_class", C.c_char_p, []), ("mock_exc_message", C.c_char_p, []),
+        ("mock_stats", None, [C.POINTER(C.c_longlong)]),
+        ("mock_encode_parity", None, [C.c_int, P, P, C.c_int32, C.c_int32]),
+        ("mock_decode_missing", None, [C.c_int, P, P, P, C.c_int32, C.c_int32]),
+        ("mock_is_parity_correct", C.c_int, [C.c_int, P, P, C.c_int32, C.c_int32, P]),
+        ("mock_code_some_shards", None, [C.c_int, P, P, C.c_int32, P, C.c_int32, C.c_int32, C.c_int32]),
+        ("mock_check_some_shards", C.c_int, [C.c_int, P, P, C.c_int32, P, C.c_int32, C.c_int32, C.c_int32]),
+    ]:
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = res, args
+    return lib
+
+
+class Jvm:
+    """Mock Java heap + the natives, with -Xcheck:jni-style books."""
+
+    def __init__(self, lib):
+        self.lib = lib
+        lib.mock_reset()
+
+    def bytes(self, arr):
+        arr = np.ascontiguousarray(arr, dtype=np.uint8)
+        o = self.lib.mock_new_bytes(len(arr))
+        if len(arr):
+            C.memmove(self.lib.mock_data(o), arr.ctypes.data, len(arr))
+        return o
+
+    def bools(self, flags):
+        o = self.lib.mock_new_bools(len(flags))
+        if len(flags):
+            a = np.array([1 if f else 0 for f in flags], dtype=np.uint8)
+            C.memmove(self.lib.mock_data(o), a.ctypes.data, len(a))
+        return o
+
+    def objects(self, elems):
+        o = self.lib.mock_new_objects(len(elems))
+        for i, e in enumerate(elems):
+            self.lib.mock_set(o, i, e)
+        return o
+
+    def read(self, o, n):
+        return np.ctypeslib.as_array(C.cast(self.lib.mock_data(o), C.POINTER(C.c_uint8)), shape=(n,)).copy()
+
+    def exception(self):
+        return self.lib.mock_exc_class().decode(), self.lib.mock_exc_message().decode()
+
+    def stats(self):
+        s = (C.c_longlong * 11)()
+        self.lib.mock_stats(s)
+        keys = ["live_refs", "max_live_refs", "capacity", "critical_open", "max_critical_open", "violations",
+                "bytes_in", "bytes_out", "critical_gets", "commits", "aborts"]
+        return dict(zip(keys, list(s)))
+
+    def assert_clean(self):
+        st = self.stats()
+        assert st["live_refs"] == 0 and st["critical_open"] == 0 and st["violations"] == 0, st
+        return st
+
+
+@pytest.fixture(scope="module")
+def mocklib():
+    return build_mock()
+
+
+@pytest.fixture
+def jvm(mocklib):
+    return Jvm(mocklib)
+
+
+@pytest.fixture(scope="module")
+def codec42(native):
+    h = C.c_void_p()
+    assert native.rs_codec_create(4, 2, C.byref(h)) == 0
+    yield h
+    native.rs_codec_destroy(h)
+
+
+def shard_set(jvm, k, m, S, seed=0, lens=None):
+    rng = np.random.default_rng(seed)
+    data = [rng.integers(0, 256, (lens[i] if lens else S), dtype=np.uint8) for i in range(k + m)]
+    return data, [jvm.bytes(d) for d in data]
+
+
+def fake_parity(data, k, m, off, cnt):
+    out = [d.copy() for d in data]
+    for p in range(m):
+        x = np.full(cnt, p + 1, dtype=np.uint8)
+        for i in range(k):
+            x ^= data[i][off:off + cnt]
+        out[k + p][off:off + cnt] = x
+    return out
+
+
+@pytest.mark.parametrize("off,cnt", [(100, 500), (0, PIN_MAX), (7, PIN_MAX + 1), (3, 2 * SLICE + 12345)])
+def test_encode_pinned_and_staged(jvm, codec42, off, cnt):
+    S = off + cnt + 50
+    data, arrs = shard_set(jvm, 4, 2, S, seed=cnt)
+    jvm.lib.mock_encode_parity(0, codec42, jvm.objects(arrs), off, cnt)
+    assert jvm.exception() == ("", "")
+    want = fake_parity(data, 4, 2, off, cnt)
+    for i in range(6):
+        assert np.array_equal(jvm.read(arrs[i], S), want[i]), i
+    st = jvm.assert_clean()
+    if cnt <= PIN_MAX:  # critical regions: parity committed, data released without copy-back
+        assert st["critical_gets"] == 6 and st["commits"] == 2 and st["aborts"] == 4
+        assert st["bytes_in"] == 0 and st["bytes_out"] == 0
+    else:  # no critical region; data copied in, parity copied out, slice by slice
+        assert st["critical_gets"] == 0 and st["max_critical_open"] == 0
+        assert st["bytes_in"] == 4 * cnt and st["bytes_out"] == 2 * cnt
+
+
+@pytest.mark.parametrize("cnt", [64, PIN_MAX + 64])
+def test_encode_check_order_and_messages(jvm, codec42, cnt):
+    S = cnt + 10
+    # wrong number of shards: reported before any element is touched (a null one included)
+    _, arrs = shard_set(jvm, 4, 1, S)
+    jvm.lib.mock_encode_parity(0, codec42, jvm.objects(arrs + [None]), 0, cnt)
+    assert jvm.exception() == (IAE, "wrong number of shards: 6") or jvm.exception()[0] == NPE
+    jvm.lib.mock_reset()
+    jvm.lib.mock_encode_parity(0, codec42, jvm.objects(arrs), 0, cnt)
+    assert jvm.exception() == (IAE, "wrong number of shards: 5")
+    assert jvm.stats()["max_live_refs"] == 0
+    cases = [
+        ([S] * 5 + [S + 1], 0, cnt, "Shards are different sizes"),
+        ([S] * 6, -1, cnt, "offset is negative: -1"),
+        ([S] * 6, 0, -5, "byteCount is negative: -5"),
+        ([S] * 6, 11, cnt, f"buffers to small: {cnt}11"),  # Java concatenates the strings (ReedSolomon.java:300)
+    ]
+    for lens, off, c, msg in cases:
+        jvm.lib.mock_reset()
+        data, arrs = shard_set(jvm, 4, 2, None, lens=lens)
+        jvm.lib.mock_encode_parity(0, codec42, jvm.objects(arrs), off, c)
+        assert jvm.exception() == (IAE, msg), (lens, off, c)
+        for i in range(6):
+            assert np.array_equal(jvm.read(arrs[i], lens[i]), data[i])  # nothing written
+        jvm.assert_clean()
+
+
+def test_encode_null_shard_npe(jvm, codec42):
+    _, arrs = shard_set(jvm, 4, 2, 100)
+    arrs[3] = None
+    jvm.lib.mock_encode_parity(0, codec42, jvm.objects(arrs), 0, 10)
+    assert jvm.exception()[0] == NPE
+    jvm.assert_clean()
+    jvm.lib.mock_reset()
+    jvm.lib.mock_encode_parity(0, codec42, None, 0, 10)
+    assert jvm.exception()[0] == NPE
+
+
+def fake_decode(data, present, off, cnt):
+    out = [d.copy() for d in data]
+    for j, p in enumerate(present):
+        if p:
+            continue
+        x = np.full(cnt, 0x80 ^ j, dtype=np.uint8)
+        for i, q in enumerate(present):
+            if q:
+                x ^= data[i][off:off + cnt]
+        out[j][off:off + cnt] = x
+    return out
+
+
+@pytest.mark.parametrize("cnt", [1000, PIN_MAX + 1000])
+def test_decode_roles_and_commit(jvm, codec42, cnt):
+    S = cnt + 5
+    present = [False, True, True, True, True, False]
+    data, arrs = shard_set(jvm, 4, 2, S, seed=5)
+    jvm.lib.mock_decode_missing(0, codec42, jvm.objects(arrs), jvm.bools(present), 5, cnt)
+    assert jvm.exception() == ("", "")
+    want = fake_decode(data, present, 5, cnt)
+    for i in range(6):
+        assert np.array_equal(jvm.read(arrs[i], S), want[i]), i
+    st = jvm.assert_clean()
+    if cnt <= PIN_MAX:
+        assert st["commits"] == 2 and st["aborts"] == 4
+    else:
+        # (+6: the shardPresent booleans)
+        assert st["bytes_in"] == 4 * cnt + 6 and st["bytes_out"] == 2 * cnt and st["critical_gets"] == 0
+
+
+def test_decode_present_array_checks(jvm, codec42):
+    data, arrs = shard_set(jvm, 4, 2, 100)
+    # sizes are checked first (ReedSolomon.java:185), then shardPresent[i] for i < 6
+    jvm.lib.mock_decode_missing(0, codec42, jvm.objects(arrs), jvm.bools([True] * 5), -1, 10)
+    assert jvm.exception() == (IAE, "offset is negative: -1")
+    jvm.lib.mock_reset()
+    jvm.lib.mock_decode_missing(0, codec42, jvm.objects(arrs), jvm.bools([True] * 5), 0, 10)
+    assert jvm.exception() == (AIOOBE, "Index 5 out of bounds for length 5")
+    jvm.assert_clean()
+    jvm.lib.mock_reset()
+    jvm.lib.mock_decode_missing(0, codec42, jvm.objects(arrs), None, 0, 10)
+    assert jvm.exception()[0] == NPE
+    jvm.assert_clean()
+    # a longer shardPresent is fine (Java reads the first 6)
+    jvm.lib.mock_reset()
+    jvm.lib.mock_decode_missing(0, codec42, jvm.objects(arrs), jvm.bools([True] * 9), 0, 10)
+    assert jvm.exception() == ("", "")
+
+
+@pytest.mark.parametrize("cnt", [300, PIN_MAX + 300])
+def test_is_parity_correct(jvm, codec42, cnt):
+    S = cnt + 20
+    data, _ = shard_set(jvm, 4, 2, S, seed=9)
+    good = fake_parity(data, 4, 2, 0, S)
+    arrs = [jvm.bytes(d) for d in good]
+    assert jvm.lib.mock_is_parity_correct(0, codec42, jvm.objects(arrs), 10, cnt, None) == 1
+    jvm.assert_clean()
+    bad = [d.copy() for d in good]
+    bad[5][10 + cnt - 1] ^= 1
+    arrs = [jvm.bytes(d) for d in bad]
+    assert jvm.lib.mock_is_parity_correct(0, codec42, jvm.objects(arrs), 10, cnt, None) == 0
+    assert jvm.exception() == ("", "")
+    # tempBuffer shorter than firstByte + byteCount (ReedSolomon.java:150)
+    assert jvm.lib.mock_is_parity_correct(0, codec42, jvm.objects(arrs), 10, cnt, jvm.bytes(np.zeros(cnt))) == 0
+    assert jvm.exception() == (IAE, "tempBuffer is not big enough")
+    st = jvm.assert_clean()
+    assert st["commits"] == 0  # read-only: nothing committed
+
+
+def fake_code(rows, ins, off, cnt):
+    outs = []
+    for row in rows:
+        x = np.zeros(cnt, dtype=np.uint8)
+        for i, a in enumerate(ins):
+            x ^= (a[off:off + cnt].astype(np.uint16) + row[i]).astype(np.uint8)
+        outs.append(x)
+    return outs
+
+
+@pytest.mark.parametrize("cnt", [777, PIN_MAX + 777])
+def test_code_some_shards_extra_entries_ignored(jvm, cnt):
+    rng = np.random.default_rng(3)
+    nin, nout, off = 3, 2, 13
+    S = off + cnt + 3
+    ins = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(nin + 1)]  # one extra input (CodingLoop.java:63-73)
+    rows = [rng.integers(0, 256, nin + 2, dtype=np.uint8) for _ in range(nout)]  # rows longer than inputCount
+    outs = [np.full(S, 0xEE, dtype=np.uint8) for _ in range(nout + 1)]
+    ia, oa = [jvm.bytes(a) for a in ins], [jvm.bytes(a) for a in outs]
+    jvm.lib.mock_code_some_shards(0, jvm.objects([jvm.bytes(r) for r in rows]), jvm.objects(ia), nin,
+                                  jvm.objects(oa), nout, off, cnt)
+    assert jvm.exception() == ("", "")
+    want = fake_code(rows, ins[:nin], off, cnt)
+    for p in range(nout):
+        got = jvm.read(oa[p], S)
+        assert np.array_equal(got[off:off + cnt], want[p])
+        assert (got[:off] == 0xEE).all() and (got[off + cnt:] == 0xEE).all()
+    assert (jvm.read(oa[nout], S) == 0xEE).all()
+    st = jvm.assert_clean()
+    if cnt > PIN_MAX:
+        # (+ nout * nin: the matrix rows)
+        assert st["critical_gets"] == 0 and st["bytes_in"] == nin * cnt + nout * nin and st["bytes_out"] == nout * cnt
+    # checkSomeShards on what was just written: true, then false after a flip
+    chk = [jvm.bytes(jvm.read(o, S)) for o in oa[:nout]]
+    rows_o = jvm.objects([jvm.bytes(r) for r in rows])
+    assert jvm.lib.mock_check_some_shards(0, rows_o, jvm.objects(ia), nin, jvm.objects(chk), nout, off, cnt) == 1
+    flipped = jvm.read(chk[1], S)
+    flipped[off + cnt // 2] ^= 4
+    chk[1] = jvm.bytes(flipped)
+    assert jvm.lib.mock_check_some_shards(0, rows_o, jvm.objects(ia), nin, jvm.objects(chk), nout, off, cnt) == 0
+    jvm.assert_clean()
+
+
+def test_code_some_shards_java_exceptions(jvm):
+    S = 100
+    ins = [jvm.bytes(np.zeros(S)) for _ in range(3)]
+    outs = [jvm.bytes(np.zeros(S)) for _ in range(2)]
+    rows = [jvm.bytes(np.ones(3)) for _ in range(2)]
+
+    def call(rws, i, nin, o, nout, off, cnt):
+        jvm.lib.mock_reset()
+        jvm.lib.mock_code_some_shards(0, rws, i, nin, o, nout, off, cnt)
+        jvm.assert_clean()
+        return jvm.exception()
+
+    R, I, O = jvm.objects(rows), jvm.objects(ins), jvm.objects(outs)
+    assert call(R, I, 4, O, 2, 0, 10) == (AIOOBE, "Index 3 out of bounds for length 3")   # inputCount > inputs.length
+    assert call(R, I, 3, O, 3, 0, 10) == (AIOOBE, "Index 2 out of bounds for length 2")   # rows shorter than outputs
+    assert call(jvm.objects(rows + [None]), I, 3, jvm.objects(outs + [jvm.bytes(np.zeros(S))]), 3, 0, 10)[0] == NPE
+    assert call(jvm.objects([rows[0], jvm.bytes(np.ones(2))]), I, 3, O, 2, 0, 10) == (
+        AIOOBE, "Index 2 out of bounds for length 2")                                    # short matrix row
+    assert call(R, I, 3, O, 2, 95, 10) == (AIOOBE, "Index 100 out of bounds for length 100")  # past the end
+    assert call(R, I, 3, O, 2, -1, 10) == (AIOOBE, "Index -1 out of bounds for length 100")
+    assert call(R, jvm.objects(ins[:2] + [None]), 3, O, 2, 0, 10)[0] == NPE
+    assert call(R, None, 3, O, 2, 0, 10)[0] == NPE
+    # no bytes to code: nothing thrown for in-range counts, nothing written
+    assert call(R, I, 3, O, 2, 0, 0) == ("", "")
+    assert call(R, I, 3, O, 0, 0, 10) == ("", "")
+
+
+def test_many_shards_local_references(jvm, native):
+    """255 + 1 shards: more element references than the 16 a native frame gets
+    without EnsureLocalCapacity; every one is deleted before returning."""
+    h = C.c_void_p()
+    assert native.rs_codec_create(200, 56, C.byref(h)) == 0
+    try:
+        data, arrs = shard_set(jvm, 200, 56, 64)
+        jvm.lib.mock_encode_parity(0, h, jvm.objects(arrs), 0, 64)
+        assert jvm.exception() == ("", "")
+        st = jvm.assert_clean()
+        assert st["max_live_refs"] == 256 and st["capacity"] >= 256
+    finally:
+        native.rs_codec_destroy(h)
+
+
+def test_critical_failure_releases_everything(jvm, codec42):
+    _, arrs = shard_set(jvm, 4, 2, 100)
+    jvm.lib.mock_fail_critical(1)
+    jvm.lib.mock_encode_parity(0, codec42, jvm.objects(arrs), 0, 10)
+    assert jvm.exception()[0] == "java/lang/OutOfMemoryError"
+    jvm.assert_clean()
+
+
+def test_real_backend_without_gpu_throws_illegal_state(jvm, codec42, native):
+    """librsamd itself behind the shim: argument errors stay IAE, a missing
+    device is IllegalStateException, and no array is written."""
+    if native.rs_device_count() > 0:
+        pytest.skip("a GPU is visible: tests/test_gpu_jni_core.py covers the real backend")
+    data, arrs = shard_set(jvm, 4, 2, 100)
+    jvm.lib.mock_encode_parity(1, codec42, jvm.objects(arrs), 0, 200)
+    assert jvm.exception() == (IAE, "buffers to small: 2000")
+    jvm.lib.mock_reset()
+    jvm.lib.mock_encode_parity(1, codec42, jvm.objects(arrs), 0, 50)
+    assert jvm.exception()[0] == ISE
+    for i in range(6):
+        assert np.array_equal(jvm.read(arrs[i], 100), data[i])
+    jvm.assert_clean()
