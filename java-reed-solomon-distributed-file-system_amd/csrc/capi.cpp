@@ -576,7 +576,7 @@ int rs_codec_create(int data_shards, int parity_shards, rs_codec **out) {
 
 void rs_codec_destroy(rs_codec *codec) {
     if (!codec) return;
-    delete codec->impl;  // device plan copies are leaked with the process (no HIP calls at teardown)
+    delete codec->impl;  // frees its device plan copies, except once exit() has begun (codec.cpp free_device)
     delete codec;
 }
 

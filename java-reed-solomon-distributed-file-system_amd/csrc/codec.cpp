@@ -1,11 +1,30 @@
 // codec.cpp -- see codec.hpp.
 #include "codec.hpp"
 
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/rs_amd.h"
 
 namespace rsamd {
+
+namespace {
+std::atomic<bool> g_exiting{false};
+const bool g_exit_hook = [] {
+    std::atexit([] { g_exiting.store(true); });
+    return true;
+}();
+}  // namespace
+
+void free_device(int dev, void *p) {
+    if (!p || g_exiting.load()) return;
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return;
+    if (cur != dev) (void)hipSetDevice(dev);
+    (void)hipFree(p);
+    if (cur != dev) (void)hipSetDevice(cur);
+}
 
 PlanLayout plan_layout(int nin, int nout) {
     PlanLayout l;
@@ -61,6 +80,11 @@ std::vector<uint8_t> Plan::image(int g) const {
         std::memcpy(img.data() + l.out_idx + p * sizeof(int32_t), &v, sizeof v);
     }
     return img;
+}
+
+Plan::~Plan() {
+    for (auto &kv : dev_) free_device(kv.first, kv.second);
+    for (auto &kv : dev_file_) free_device(kv.first, kv.second);
 }
 
 hipError_t Plan::device_plans(std::vector<DevPlan> *out) const {
@@ -154,6 +178,10 @@ Codec::Codec(int k, int m) : k_(k), m_(m), matrix_(build_generator(k, k + m)) {
     encode_.reset(new Plan(in, out, matrix_.select_rows(parity)));  // parityRows, ReedSolomon.java:53-56
 }
 
+Codec::~Codec() {
+    for (auto &kv : patterns_) free_device(kv.first, const_cast<uint8_t *>(kv.second.records));
+}
+
 int Codec::create(int k, int m, Codec **out, std::string *err) {
     if (256 < k + m) {  // ReedSolomon.java:44-46
         *err = "too many shards - max is 256";
@@ -175,7 +203,8 @@ int Codec::decode_plan(const uint8_t *present, std::shared_ptr<const Plan> *out,
         std::lock_guard<std::mutex> lock(mu_);
         auto it = decode_cache_.find(key);
         if (it != decode_cache_.end()) {
-            *out = it->second;
+            lru_.splice(lru_.begin(), lru_, it->second.lru);
+            *out = it->second.plan;
             return RS_OK;
         }
     }
@@ -203,9 +232,22 @@ int Codec::decode_plan(const uint8_t *present, std::shared_ptr<const Plan> *out,
         }
     }
     auto plan = std::make_shared<const Plan>(surv, missing, std::move(rows));
+    std::shared_ptr<const Plan> evicted;  // destroyed (device copy freed) after the lock is released
     std::lock_guard<std::mutex> lock(mu_);
-    auto ins = decode_cache_.emplace(key, plan);
-    *out = ins.first->second;
+    auto it = decode_cache_.find(key);
+    if (it != decode_cache_.end()) {  // another thread built it meanwhile
+        *out = it->second.plan;
+        return RS_OK;
+    }
+    lru_.push_front(key);
+    decode_cache_.emplace(key, CacheEntry{plan, lru_.begin()});
+    if (decode_cache_.size() > kMaxDecodePlans) {
+        auto victim = decode_cache_.find(lru_.back());
+        evicted = std::move(victim->second.plan);
+        decode_cache_.erase(victim);
+        lru_.pop_back();
+    }
+    *out = plan;
     return RS_OK;
 }
 

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <list>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -23,6 +24,9 @@ namespace rsamd {
 class Plan {
 public:
     Plan(std::vector<int> in_idx, std::vector<int> out_idx, GfMatrix rows);
+    ~Plan();  // frees the device copies (hipFree synchronises the device first)
+    Plan(const Plan &) = delete;
+    Plan &operator=(const Plan &) = delete;
     const std::vector<int> &in_idx() const { return in_idx_; }
     const std::vector<int> &out_idx() const { return out_idx_; }
     const GfMatrix &rows() const { return rows_; }
@@ -48,6 +52,10 @@ private:
     mutable std::map<int, void *> dev_file_;  // device id -> FileDecodePlan image
 };
 
+// Device memory freed outside process teardown only: once exit() has begun the
+// HIP runtime may already be gone, and the process releases everything anyway.
+void free_device(int dev, void *p);
+
 // Offsets of one group's image: tabs, then in_idx, then out_idx.
 struct PlanLayout {
     size_t tabs, in_idx, out_idx, bytes;
@@ -71,9 +79,14 @@ struct PatternTables {
 constexpr int kMaxPatternBits = 20;        // k + m for a bitmask table (4 MiB of ids)
 constexpr size_t kMaxPatterns = 1u << 16;  // decodable patterns in one table
 
+// Distinct decode plans a codec keeps (least recently used evicted first):
+// every decodable pattern of a wide code would otherwise stay resident.
+constexpr size_t kMaxDecodePlans = 4096;
+
 class Codec {
 public:
     static int create(int k, int m, Codec **out, std::string *err);
+    ~Codec();  // frees the pattern tables' device memory
 
     int k() const { return k_; }
     int m() const { return m_; }
@@ -104,7 +117,12 @@ private:
     GfMatrix matrix_;
     std::unique_ptr<Plan> encode_;
     mutable std::mutex mu_;
-    mutable std::map<std::vector<uint8_t>, std::shared_ptr<const Plan>> decode_cache_;
+    struct CacheEntry {
+        std::shared_ptr<const Plan> plan;
+        std::list<std::vector<uint8_t>>::iterator lru;
+    };
+    mutable std::map<std::vector<uint8_t>, CacheEntry> decode_cache_;
+    mutable std::list<std::vector<uint8_t>> lru_;  // most recently used first
     mutable std::mutex pat_mu_;
     mutable std::map<int, PatternTables> patterns_;  // device id -> tables (leaked with the process)
     mutable std::vector<int32_t> host_mask_table_;

@@ -11,6 +11,7 @@
 #include <deque>
 #include <map>
 #include <mutex>
+#include <thread>
 
 #include "../../include/rs_amd.h"
 #include "copy_pool.hpp"
@@ -19,8 +20,22 @@ namespace rsamd {
 namespace host {
 
 namespace {
+void release_all(std::map<int, ThreadCtx *> &ctx);
+
+// This thread's contexts (device -> context), released when the thread exits
+// (JVM and gRPC worker pools create and retire threads) or by rs_thread_release.
+// Not for the thread that loaded the library: its thread-locals are destroyed
+// inside exit(), where the HIP runtime may already be shutting down.
+const std::thread::id g_loader_thread = std::this_thread::get_id();
+struct ThreadContexts {
+    std::map<int, ThreadCtx *> m;
+    ~ThreadContexts() {
+        if (std::this_thread::get_id() != g_loader_thread) release_all(m);
+    }
+};
+
 thread_local std::string t_err;
-thread_local std::map<int, ThreadCtx *> t_ctx;  // device -> this thread's context
+thread_local ThreadContexts t_ctx;
 }  // namespace
 
 int fail(int code, const std::string &msg) {
@@ -49,8 +64,8 @@ int need_device() {
 int thread_ctx(ThreadCtx **out) {
     int dev = 0;
     RS_HIP(hipGetDevice(&dev));
-    auto it = t_ctx.find(dev);
-    if (it == t_ctx.end()) {
+    auto it = t_ctx.m.find(dev);
+    if (it == t_ctx.m.end()) {
         auto *c = new ThreadCtx;
         hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
@@ -66,16 +81,18 @@ int thread_ctx(ThreadCtx **out) {
             delete c;
             return hip_fail(e, "thread context");
         }
-        it = t_ctx.emplace(dev, c).first;
+        it = t_ctx.m.emplace(dev, c).first;
     }
     *out = it->second;
     return RS_OK;
 }
 
-void release_thread_contexts() {
+namespace {
+void release_all(std::map<int, ThreadCtx *> &ctx) {
+    if (ctx.empty()) return;  // a thread that never coded makes no HIP call here
     int cur = 0;
     (void)hipGetDevice(&cur);
-    for (auto &kv : t_ctx) {
+    for (auto &kv : ctx) {
         ThreadCtx *c = kv.second;
         (void)hipSetDevice(kv.first);
         if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -102,9 +119,12 @@ void release_thread_contexts() {
         }
         delete c;
     }
-    t_ctx.clear();
+    ctx.clear();
     (void)hipSetDevice(cur);
 }
+}  // namespace
+
+void release_thread_contexts() { release_all(t_ctx.m); }
 
 int grow(uint8_t **buf, size_t *cap, size_t want) {
     if (*cap >= want) return RS_OK;

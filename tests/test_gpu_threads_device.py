@@ -73,3 +73,33 @@ def test_shared_codec_many_streams(gpu, oracle_lib):
     for t in ts:
         t.join()
     assert not errors, errors
+
+
+def test_thread_exit_releases_its_staging(gpu, oracle_lib):
+    """A worker thread's host-API contexts (streams, device staging, pinned
+    mirrors) are freed when the thread exits (JVM / gRPC pools retire
+    threads), not leaked until rs_thread_release."""
+    import torch
+    import rsamd
+    torch.cuda.synchronize()
+    n = 48 << 20
+    rng = np.random.default_rng(1)
+    sh = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(4)] + [np.zeros(n, np.uint8) for _ in range(2)]
+    ref = [a.copy() for a in sh]
+    oracle_lib.Codec(4, 2).encode_parity(ref, 0, n)
+    rs = rsamd.ReedSolomon.create(4, 2)
+    seen = {}
+
+    def work():
+        rs.encodeParity(sh, 0, n)
+        seen["mid"] = torch.cuda.mem_get_info()[0]
+
+    free0 = torch.cuda.mem_get_info()[0]
+    t = threading.Thread(target=work)
+    t.start()
+    t.join()
+    free1 = torch.cuda.mem_get_info()[0]
+    assert all(np.array_equal(a, b) for a, b in zip(sh, ref))
+    held = free0 - seen["mid"]
+    if held > (32 << 20):  # the thread held staging memory while it lived
+        assert free1 - seen["mid"] >= 0.8 * held, (free0, seen["mid"], free1)
