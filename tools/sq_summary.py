@@ -78,6 +78,13 @@ def main():
                     der[k.lower() + "_frac"] = round(c[k] / wc, 4)
             if c.get("SQ_WAVES"):
                 der["wave_cycles_per_wave"] = round(wc / c["SQ_WAVES"], 1)
+        if c.get("TCC_BUSY") and c.get("GRBM_GUI_ACTIVE"):
+            # summed over the TCC channels (16 per XCD, 128 in all) and the 8 XCDs' GUI_ACTIVE
+            cyc = c["GRBM_GUI_ACTIVE"] / 8
+            for k in ("TCC_EA0_RDREQ_DRAM_CREDIT_STALL", "TCC_EA0_WRREQ_DRAM_CREDIT_STALL", "TCC_EA0_WRREQ_STALL",
+                      "TCC_BUSY"):
+                if k in c:
+                    der[k.lower() + "_per_channel_cycle"] = round(c[k] / (128 * cyc), 4)
         if c.get("SQ_BUSY_CYCLES") and c.get("GRBM_GUI_ACTIVE"):
             der["sq_busy_frac"] = round(c["SQ_BUSY_CYCLES"] / c["GRBM_GUI_ACTIVE"], 4)
         r["derived"] = der

@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CHECK(x)                                                                                  \
@@ -101,6 +102,64 @@ __global__ void __launch_bounds__(64) wide_kernel(Geo a) {
     for (int p = 0; p < M; ++p) st(sb + uint64_t(K + p) * a.shard_stride, acc[p]);
 }
 
+// Encode traffic with a choice of cache policy: LP / SP = 1 plain, 0 non-temporal.
+template <int K, int M, int LP, int SP>
+__global__ void __launch_bounds__(64) policy_kernel(Geo a) {
+    uint32_t b = blockIdx.x;
+    if (a.xcd_span && b < 8u * a.xcd_span) b = (b & 7u) * a.xcd_span + (b >> 3);
+    const uint32_t stripe = b / a.chunks;
+    uint32_t chunk = b - stripe * a.chunks;
+    if (a.rot) chunk = (chunk + stripe * a.rot) % a.chunks;
+    uint8_t *sb = a.base + uint64_t(stripe) * a.stripe_stride + uint64_t(chunk) * 1024 + threadIdx.x * 16u;
+    u32x4 x[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const u32x4 *p = reinterpret_cast<const u32x4 *>(sb + uint64_t(i) * a.shard_stride);
+        x[i] = LP ? *p : __builtin_nontemporal_load(p);
+    }
+#pragma unroll
+    for (int p = 0; p < M; ++p) {
+        u32x4 acc = x[0] + u32x4{uint32_t(p), 0, 0, 0};
+#pragma unroll
+        for (int i = 1; i < K; ++i) acc ^= x[i];
+        u32x4 *q = reinterpret_cast<u32x4 *>(sb + uint64_t(K + p) * a.shard_stride);
+        if (SP) *q = acc;
+        else __builtin_nontemporal_store(acc, q);
+    }
+}
+
+// File-encode traffic reference: a wave reads K KiB of the file contiguously
+// (16 B per lane per instruction) and writes K data + M parity KiB, one KiB to
+// each of K+M shards (shard stride S).  file_decode reference (DEC): reads K
+// shards' KiB, writes K KiB of file.
+template <int K, int M, bool DEC>
+__global__ void __launch_bounds__(64) file_ref_kernel(const uint8_t *file, uint8_t *fout, uint8_t *shards,
+                                                      uint64_t S, uint32_t xcd_span, uint32_t n_items) {
+    uint32_t b = blockIdx.x;
+    if (xcd_span && b < 8u * xcd_span) b = (b & 7u) * xcd_span + (b >> 3);
+    const uint64_t col = uint64_t(b) * 1024 + threadIdx.x * 16u;  // column within each shard
+    if (!DEC) {
+        u32x4 x[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) x[i] = ld(file + uint64_t(b) * 1024 * K + uint64_t(i) * 1024 + threadIdx.x * 16u);
+#pragma unroll
+        for (int i = 0; i < K; ++i) st(shards + uint64_t(i) * S + col, x[i]);
+#pragma unroll
+        for (int p = 0; p < M; ++p) {
+            u32x4 acc = x[0] + u32x4{uint32_t(p), 0, 0, 0};
+#pragma unroll
+            for (int i = 1; i < K; ++i) acc ^= x[i];
+            st(shards + uint64_t(K + p) * S + col, acc);
+        }
+    } else {
+        u32x4 x[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) x[i] = ld(shards + uint64_t(i + 1) * S + col);
+#pragma unroll
+        for (int i = 0; i < K; ++i) st(fout + uint64_t(b) * 1024 * K + uint64_t(i) * 1024 + threadIdx.x * 16u, x[i]);
+    }
+}
+
 hipEvent_t e0, e1;
 
 template <class F>
@@ -159,8 +218,68 @@ void sweep(uint8_t *buf, size_t cap, uint32_t *sink, size_t S, size_t B, int rep
     }
 }
 
+template <int K, int M>
+void policies(uint8_t *buf, uint32_t *sink, size_t S, size_t B, int reps) {
+    const size_t stride = S;
+    const uint32_t chunks = uint32_t(S / 1024);
+    static const char *names[] = {"nt load / nt store", "nt load / plain store", "plain load / nt store",
+                                  "plain load / plain store"};
+    for (int order = 0; order < 2; ++order)
+        for (int v = 0; v < 4; ++v) {
+            Geo g{buf, sink, uint64_t((K + M) * stride), uint64_t(stride), chunks, uint32_t(B * chunks), 0, 0};
+            if (order == 0) g.xcd_span = g.n_items / 8u;
+            else g.rot = 3u * chunks / 8u - 1u;
+            const dim3 grid(g.n_items);
+            double ms = 0;
+            if (v == 0) ms = median_ms([&] { hipLaunchKernelGGL((policy_kernel<K, M, 0, 0>), grid, dim3(64), 0, 0, g); }, reps);
+            if (v == 1) ms = median_ms([&] { hipLaunchKernelGGL((policy_kernel<K, M, 0, 1>), grid, dim3(64), 0, 0, g); }, reps);
+            if (v == 2) ms = median_ms([&] { hipLaunchKernelGGL((policy_kernel<K, M, 1, 0>), grid, dim3(64), 0, 0, g); }, reps);
+            if (v == 3) ms = median_ms([&] { hipLaunchKernelGGL((policy_kernel<K, M, 1, 1>), grid, dim3(64), 0, 0, g); }, reps);
+            char name[64], leg[96];
+            std::snprintf(name, sizeof name, "%d+%d %zuKiB x%zu", K, M, S >> 10, B);
+            std::snprintf(leg, sizeof leg, "%s %s", order ? "rot" : "xcd", names[v]);
+            report(name, leg, double(B) * (K + M) * S, ms);
+        }
+}
+
 int main(int argc, char **argv) {
     const int reps = argc > 1 ? std::atoi(argv[1]) : 5;
+    if (argc > 2 && std::string(argv[2]) == "file") {
+        const size_t F = size_t(4) << 30, S = F / 4;  // 4 GiB file, 4+2 shards of 1 GiB
+        uint8_t *file = nullptr, *fout = nullptr, *sh = nullptr;
+        CHECK(hipEventCreate(&e0));
+        CHECK(hipEventCreate(&e1));
+        CHECK(hipMalloc(&file, F));
+        CHECK(hipMalloc(&fout, F));
+        CHECK(hipMalloc(&sh, 6 * S));
+        CHECK(hipMemset(file, 0x11, F));
+        CHECK(hipMemset(sh, 0x22, 6 * S));
+        const uint32_t n = uint32_t(S / 1024);
+        for (int xcd = 0; xcd < 2; ++xcd) {
+            const uint32_t span = xcd ? n / 8 : 0;
+            report("file 4 GiB -> 4+2", xcd ? "encode traffic, xcd" : "encode traffic, plain", double(F) + 6.0 * S,
+                   median_ms([&] { hipLaunchKernelGGL((file_ref_kernel<4, 2, false>), dim3(n), dim3(64), 0, 0, file, fout, sh, S, span, n); }, reps));
+            report("4+2 -> file 4 GiB", xcd ? "decode traffic (4 shards -> file), xcd" : "decode traffic, plain",
+                   double(F) + 4.0 * S,
+                   median_ms([&] { hipLaunchKernelGGL((file_ref_kernel<4, 2, true>), dim3(n), dim3(64), 0, 0, file, fout, sh, S, span, n); }, reps));
+        }
+        return 0;
+    }
+    if (argc > 2 && std::string(argv[2]) == "policy") {
+        const size_t cap = size_t(60) << 30;
+        uint8_t *buf = nullptr;
+        uint32_t *sink = nullptr;
+        CHECK(hipEventCreate(&e0));
+        CHECK(hipEventCreate(&e1));
+        CHECK(hipMalloc(&buf, cap));
+        CHECK(hipMalloc(&sink, 256));
+        CHECK(hipMemset(buf, 0x37, cap));
+        policies<10, 4>(buf, sink, size_t(4) << 20, 128, reps);
+        policies<10, 4>(buf, sink, size_t(4) << 20, 1024, reps);
+        policies<4, 2>(buf, sink, size_t(1) << 20, 4096, reps);
+        CHECK(hipFree(buf));
+        return 0;
+    }
     const size_t cap = size_t(60) << 30;
     uint8_t *buf = nullptr;
     uint32_t *sink = nullptr;
