@@ -160,6 +160,33 @@ __global__ void __launch_bounds__(64) file_ref_kernel(const uint8_t *file, uint8
     }
 }
 
+// Same traffic as the encode, but no wave both reads and writes: even blocks
+// read the K data shards of item b/2, odd blocks write the M parity shards of
+// item b/2 (interleaved in dispatch order).  Tells a per-wave (CU-side)
+// read/write mixing cost from a DRAM-side one.
+template <int K, int M>
+__global__ void __launch_bounds__(64) split_roles_kernel(Geo a) {
+    uint32_t b = blockIdx.x >> 1;
+    if (a.xcd_span && b < 8u * a.xcd_span) b = (b & 7u) * a.xcd_span + (b >> 3);
+    const uint32_t stripe = b / a.chunks;
+    uint32_t chunk = b - stripe * a.chunks;
+    if (a.rot) chunk = (chunk + stripe * a.rot) % a.chunks;
+    uint8_t *sb = a.base + uint64_t(stripe) * a.stripe_stride + uint64_t(chunk) * 1024 + threadIdx.x * 16u;
+    if (blockIdx.x & 1) {
+        const uint32_t t = b * 64u + threadIdx.x;
+#pragma unroll
+        for (int p = 0; p < M; ++p) st(sb + uint64_t(K + p) * a.shard_stride, u32x4{t, t + 1u, t + 2u, uint32_t(p)});
+        return;
+    }
+    u32x4 x[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) x[i] = ld(sb + uint64_t(i) * a.shard_stride);
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) s ^= x[i][0] ^ x[i][1] ^ x[i][2] ^ x[i][3];
+    if (s == 0x9E3779B9u) a.sink[threadIdx.x] = s;
+}
+
 hipEvent_t e0, e1;
 
 template <class F>
@@ -244,6 +271,43 @@ void policies(uint8_t *buf, uint32_t *sink, size_t S, size_t B, int reps) {
 
 int main(int argc, char **argv) {
     const int reps = argc > 1 ? std::atoi(argv[1]) : 5;
+    if (argc > 2 && std::string(argv[2]) == "roles") {
+        const size_t cap = size_t(60) << 30;
+        uint8_t *buf = nullptr;
+        uint32_t *sink = nullptr;
+        CHECK(hipEventCreate(&e0));
+        CHECK(hipEventCreate(&e1));
+        CHECK(hipMalloc(&buf, cap));
+        CHECK(hipMalloc(&sink, 256));
+        CHECK(hipMemset(buf, 0x37, cap));
+        struct Shape { int k, m; size_t S, B; } shapes[] = {{10, 4, size_t(4) << 20, 128}, {4, 2, size_t(1) << 20, 4096}};
+        for (const Shape &sh : shapes) {
+            const uint32_t chunks = uint32_t(sh.S / 1024);
+            for (int order = 0; order < 2; ++order) {
+                Geo g{buf, sink, uint64_t((sh.k + sh.m) * sh.S), uint64_t(sh.S), chunks, uint32_t(sh.B * chunks), 0, 0};
+                if (order == 0) g.xcd_span = g.n_items / 8u;
+                else g.rot = 3u * chunks / 8u - 1u;
+                const double bytes = double(sh.B) * (sh.k + sh.m) * sh.S;
+                char name[64];
+                std::snprintf(name, sizeof name, "%d+%d %zuKiB x%zu", sh.k, sh.m, sh.S >> 10, sh.B);
+                const char *o = order ? "rot" : "xcd";
+                double mixed, split;
+                if (sh.k == 10) {
+                    mixed = median_ms([&] { hipLaunchKernelGGL((wide_kernel<10, 4, 3>), dim3(g.n_items), dim3(64), 0, 0, g); }, reps);
+                    split = median_ms([&] { hipLaunchKernelGGL((split_roles_kernel<10, 4>), dim3(2 * g.n_items), dim3(64), 0, 0, g); }, reps);
+                } else {
+                    mixed = median_ms([&] { hipLaunchKernelGGL((wide_kernel<4, 2, 3>), dim3(g.n_items), dim3(64), 0, 0, g); }, reps);
+                    split = median_ms([&] { hipLaunchKernelGGL((split_roles_kernel<4, 2>), dim3(2 * g.n_items), dim3(64), 0, 0, g); }, reps);
+                }
+                char leg[96];
+                std::snprintf(leg, sizeof leg, "%s read+write in every wave", o);
+                report(name, leg, bytes, mixed);
+                std::snprintf(leg, sizeof leg, "%s reader waves + writer waves", o);
+                report(name, leg, bytes, split);
+            }
+        }
+        return 0;
+    }
     if (argc > 2 && std::string(argv[2]) == "file") {
         const size_t F = size_t(4) << 30, S = F / 4;  // 4 GiB file, 4+2 shards of 1 GiB
         uint8_t *file = nullptr, *fout = nullptr, *sh = nullptr;
