@@ -10,8 +10,8 @@
  *
  * Java side: jni/java/edu/cmu/reedsolomon/{NativeReedSolomon,GpuCodingLoop}.java.
  * This file only adapts JNIEnv to the rsj_env interface of rs_jni_core.h; the
- * marshalling (argument checks, exceptions, local references, pinning of small
- * calls, slice-wise copies of large ones) lives in rs_jni_core.c, which
+ * marshalling (argument checks, exceptions, local references, slice-by-slice
+ * pinning, the copying fallback) lives in rs_jni_core.c, which
  * tests/test_jni_core.py compiles and exercises against mock Java arrays.
  */
 #include <jni.h>
@@ -33,8 +33,11 @@ static rsj_obj j_object_element(rsj_env *e, rsj_obj a, int i) {
 }
 static void j_delete_local(rsj_env *e, rsj_obj o) { (*J(e))->DeleteLocalRef(J(e), (jobject)o); }
 static int j_ensure_local_capacity(rsj_env *e, int n) { return (*J(e))->EnsureLocalCapacity(J(e), n) == 0 ? 0 : -1; }
-static uint8_t *j_critical_get(rsj_env *e, rsj_obj a) {
-    return (uint8_t *)(*J(e))->GetPrimitiveArrayCritical(J(e), (jarray)a, NULL);
+static uint8_t *j_critical_get(rsj_env *e, rsj_obj a, int *is_copy) {
+    jboolean c = JNI_FALSE;
+    uint8_t *p = (uint8_t *)(*J(e))->GetPrimitiveArrayCritical(J(e), (jarray)a, &c);
+    *is_copy = c == JNI_TRUE;
+    return p;
 }
 static void j_critical_release(rsj_env *e, rsj_obj a, uint8_t *p, int mode) {
     (*J(e))->ReleasePrimitiveArrayCritical(J(e), (jarray)a, p, mode);

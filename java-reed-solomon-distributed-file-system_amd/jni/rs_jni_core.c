@@ -1,18 +1,21 @@
 /*
  * rs_jni_core.c -- see rs_jni_core.h.
  *
- * Two ways a call reaches the GPU:
- *  - byte_count <= RSJ_PIN_MAX_BYTES: every Java array is pinned with
- *    GetPrimitiveArrayCritical, librsamd codes the range straight from/to the
- *    pinned memory, outputs are released with mode 0 (commit) and inputs with
- *    JNI_ABORT.  No JNI call is made while a critical region is open.
- *  - larger calls: the arguments are validated first (same checks and order as
- *    the reference), then the range is coded in slices of RSJ_SLICE_BYTES:
- *    inputs copied in with GetByteArrayRegion, outputs copied back with
- *    SetByteArrayRegion.  No critical region is held, so a long call never
- *    blocks the garbage collector.
- * Element references of the byte[][] arrays are local references: capacity is
- * ensured up front and each one is deleted before returning.
+ * How a call reaches the GPU: the range [offset, offset + count) is coded in
+ * slices of RSJ_SLICE_BYTES per shard.  For each slice every Java array is
+ * pinned with GetPrimitiveArrayCritical, librsamd codes the slice straight
+ * from/to the pinned memory (registering it for DMA), and the arrays are
+ * released -- outputs with mode 0 (commit), inputs with JNI_ABORT -- before
+ * the next slice.  So no critical region lasts longer than one slice (a few
+ * ms), the garbage collector can run between slices, and no byte is copied on
+ * the host.  Calls of more than one slice are validated up front (same checks
+ * and order as the reference), so a later slice never fails after an earlier
+ * one was written.  If the JVM answers a critical get with a COPY of the array
+ * (isCopy), pinning per slice would copy whole arrays each time: the call then
+ * copies each slice through C buffers with Get/SetByteArrayRegion instead.
+ * No JNI call is made while a critical region is open.  Element references of
+ * the byte[][] arrays are local references: capacity is ensured up front and
+ * each one is deleted before returning.
  */
 #include "rs_jni_core.h"
 
@@ -84,8 +87,15 @@ static int take(rsj_env *e, rsj_obj outer, int n, arrays *a) {
     return 0;
 }
 
-static void pin(rsj_env *e, arrays *a) {
-    for (int i = 0; i < a->n; i++) a->ptr[i] = e->critical_get(e, a->arr[i]);
+/* Returns whether any array came back as a copy. */
+static int pin(rsj_env *e, arrays *a) {
+    int any_copy = 0;
+    for (int i = 0; i < a->n; i++) {
+        int is_copy = 0;
+        a->ptr[i] = e->critical_get(e, a->arr[i], &is_copy);
+        any_copy |= is_copy;
+    }
+    return any_copy;
 }
 
 /* mode_of[i] (or `mode` for all when NULL), in reverse order of pinning. */
@@ -103,7 +113,7 @@ static int pinned_ok(const arrays *a) {
     return 1;
 }
 
-/* Slice buffers for the staged path: one RSJ_SLICE_BYTES buffer per array. */
+/* Slice buffers for the copying path: one RSJ_SLICE_BYTES buffer per array. */
 static uint8_t *slice_buffers(int n, uint8_t **ptrs) {
     uint8_t *mem = (uint8_t *)malloc((size_t)(n > 0 ? n : 1) * RSJ_SLICE_BYTES);
     for (int i = 0; mem && i < n; i++) ptrs[i] = mem + (size_t)i * RSJ_SLICE_BYTES;
@@ -115,82 +125,89 @@ static uint8_t *slice_buffers(int n, uint8_t **ptrs) {
 enum { ROLE_NONE = 0, ROLE_IN = 1, ROLE_OUT = 2 };
 enum { OP_ENCODE, OP_DECODE, OP_VERIFY };
 
-/* The shard-array call in both modes.  role[i] says whether shard i is read
- * (copied in on the staged path) and/or written (copied back / committed). */
+/* One slice through the backend: arrays at `ptr` with lengths `len`, bytes
+ * [off, off + n) (shard-level calls; the backend re-checks the sizes). */
+static int shard_slice(const rsj_backend *b, const rs_codec *c, int op, uint8_t *const *ptr, int n_arr,
+                       const int64_t *len, const uint8_t *present, int32_t off, int32_t n, const uint8_t *temp,
+                       int64_t temp_len, int *part) {
+    *part = 1;
+    if (op == OP_ENCODE) return b->encode_parity(c, ptr, n_arr, len, off, n);
+    if (op == OP_DECODE) return b->decode_missing(c, ptr, n_arr, len, present, off, n);
+    return b->is_parity_correct(c, ptr, n_arr, len, off, n, temp, temp_len, part);
+}
+
+/* The shard-array call, slice by slice.  role[i] says whether shard i is read
+ * and/or written.  Returns 0 (result in *result) or -1 with an exception pending. */
 static int shard_call(rsj_env *e, const rsj_backend *b, const rs_codec *c, arrays *s, const int *role, int op,
                       const uint8_t *present, int32_t offset, int32_t count, const uint8_t *temp, int64_t temp_len,
                       int *result) {
     int rc;
     *result = 1;
-    if (op == OP_VERIFY && temp) {  /* checkBuffersAndSizes, then tempBuffer's length (ReedSolomon.java:147-151) */
+    const int multi = count > (int32_t)RSJ_SLICE_BYTES;
+    if (multi || (op == OP_VERIFY && temp)) {
         rc = b->check_buffers_and_sizes(c, s->n, s->len, offset, count);
         if (rc) {
             throw_rc(e, b, rc);
             return -1;
         }
-        if (temp_len < (int64_t)offset + count) {
+        if (op == OP_VERIFY && temp && temp_len < (int64_t)offset + count) {  /* ReedSolomon.java:147-151 */
             e->throw_new(e, IAE, "tempBuffer is not big enough");
             return -1;
         }
     }
-    if (count <= (int32_t)RSJ_PIN_MAX_BYTES) {
-        int mode_of[RSJ_MAX_SHARDS];
-        for (int i = 0; i < s->n; i++) mode_of[i] = (role[i] & ROLE_OUT) ? RSJ_COMMIT : RSJ_ABORT;
-        pin(e, s);
-        if (!pinned_ok(s)) {
-            unpin(e, s, NULL, RSJ_ABORT);
-            e->throw_new(e, "java/lang/OutOfMemoryError", "GetPrimitiveArrayCritical failed");
-            return -1;
-        }
-        if (op == OP_ENCODE) rc = b->encode_parity(c, s->ptr, s->n, s->len, offset, count);
-        else if (op == OP_DECODE) rc = b->decode_missing(c, s->ptr, s->n, s->len, present, offset, count);
-        else rc = b->is_parity_correct(c, s->ptr, s->n, s->len, offset, count, temp, temp_len, result);
-        /* on an error nothing was written: release everything without copy-back */
-        unpin(e, s, rc ? NULL : mode_of, RSJ_ABORT);
-        if (rc) throw_rc(e, b, rc);
-        return rc ? -1 : 0;
-    }
-    /* staged: validated before any copy (nothing is written on an error path) */
-    rc = b->check_buffers_and_sizes(c, s->n, s->len, offset, count);
-    if (rc) {
-        throw_rc(e, b, rc);
-        return -1;
-    }
-    uint8_t *buf[RSJ_MAX_SHARDS];
+    int mode_of[RSJ_MAX_SHARDS];
+    for (int i = 0; i < s->n; i++) mode_of[i] = (role[i] & ROLE_OUT) ? RSJ_COMMIT : RSJ_ABORT;
+    uint8_t *mem = NULL, *buf[RSJ_MAX_SHARDS];
     int64_t lens[RSJ_MAX_SHARDS];
-    uint8_t *mem = slice_buffers(s->n, buf);
-    if (!mem) {
-        e->throw_new(e, "java/lang/OutOfMemoryError", "slice buffers");
-        return -1;
-    }
-    for (int32_t done = 0; done < count && *result;) {
-        const int32_t n = (count - done) < (int32_t)RSJ_SLICE_BYTES ? (count - done) : (int32_t)RSJ_SLICE_BYTES;
-        for (int i = 0; i < s->n; i++) {
-            lens[i] = n;
-            if (role[i] & ROLE_IN) e->byte_region_get(e, s->arr[i], offset + done, n, buf[i]);
-        }
-        if (e->exception_pending(e)) {
-            free(mem);
-            return -1;
-        }
+    int32_t done = 0;
+    do {  /* at least once: a zero-byte call still gets the backend's checks */
+        /* a one-slice call hands its count to the backend as is (a negative one is its error to report) */
+        const int32_t left = count - done;
+        const int32_t n = (!multi || left < (int32_t)RSJ_SLICE_BYTES) ? left : (int32_t)RSJ_SLICE_BYTES;
         int part = 1;
-        if (op == OP_ENCODE) rc = b->encode_parity(c, buf, s->n, lens, 0, n);
-        else if (op == OP_DECODE) rc = b->decode_missing(c, buf, s->n, lens, present, 0, n);
-        else rc = b->is_parity_correct(c, buf, s->n, lens, 0, n, temp ? buf[0] : NULL, temp ? n : 0, &part);
+        if (!mem) {
+            const int copied = pin(e, s);
+            if (!pinned_ok(s)) {
+                unpin(e, s, NULL, RSJ_ABORT);
+                e->throw_new(e, "java/lang/OutOfMemoryError", "GetPrimitiveArrayCritical failed");
+                return -1;
+            }
+            if (copied && multi && done == 0) {  /* the JVM copies: slice through C buffers instead */
+                unpin(e, s, NULL, RSJ_ABORT);
+                mem = slice_buffers(s->n, buf);
+                if (!mem) {
+                    e->throw_new(e, "java/lang/OutOfMemoryError", "slice buffers");
+                    return -1;
+                }
+                continue;
+            }
+            rc = shard_slice(b, c, op, s->ptr, s->n, s->len, present, offset + done, n, temp, temp_len, &part);
+            unpin(e, s, rc ? NULL : mode_of, RSJ_ABORT);  /* on an error nothing was written */
+        } else {
+            for (int i = 0; i < s->n; i++) {
+                lens[i] = n;
+                if (role[i] & ROLE_IN) e->byte_region_get(e, s->arr[i], offset + done, n, buf[i]);
+            }
+            if (e->exception_pending(e)) {
+                free(mem);
+                return -1;
+            }
+            rc = shard_slice(b, c, op, buf, s->n, lens, present, 0, n, temp ? buf[0] : NULL, temp ? n : 0, &part);
+            for (int i = 0; !rc && i < s->n; i++)
+                if (role[i] & ROLE_OUT) e->byte_region_set(e, s->arr[i], offset + done, n, buf[i]);
+        }
         if (rc) {
             free(mem);
             throw_rc(e, b, rc);
             return -1;
         }
-        if (!part) *result = 0;  /* isParityCorrect returns false at the first mismatch */
-        for (int i = 0; i < s->n; i++)
-            if (role[i] & ROLE_OUT) e->byte_region_set(e, s->arr[i], offset + done, n, buf[i]);
-        if (e->exception_pending(e)) {
+        if (mem && e->exception_pending(e)) {
             free(mem);
             return -1;
         }
+        if (!part) *result = 0; /* isParityCorrect: false at the first mismatch */
         done += n;
-    }
+    } while (done < count && *result);
     free(mem);
     return 0;
 }
@@ -376,35 +393,37 @@ static int loop_call(rsj_env *e, const rsj_backend *b, rsj_obj rows, rsj_obj ins
         return -1;
     }
     int rc = 0;
-    if (count <= 0 || nin == 0) {
-        /* nothing is coded (the Java loops do no iterations over bytes) */
-    } else if (count <= (int32_t)RSJ_PIN_MAX_BYTES) {
-        pin(e, &in);
-        pin(e, &out);
-        if (!pinned_ok(&in) || !pinned_ok(&out)) {
-            unpin(e, &out, NULL, RSJ_ABORT);
-            unpin(e, &in, NULL, RSJ_ABORT);
-            e->throw_new(e, "java/lang/OutOfMemoryError", "GetPrimitiveArrayCritical failed");
-            rc = -1;
-        } else {
-            if (verify)
-                rc = b->check_some_shards(rp, (const uint8_t *const *)in.ptr, nin, (const uint8_t *const *)out.ptr,
-                                          nout, offset, count, &result);
-            else
-                rc = b->code_some_shards(rp, (const uint8_t *const *)in.ptr, nin, out.ptr, nout, offset, count);
+    /* nothing is coded when count <= 0 or nin == 0 (the Java loops do no byte iterations) */
+    uint8_t *ib[RSJ_MAX_SHARDS], *ob[RSJ_MAX_SHARDS], *mi = NULL, *mo = NULL;
+    for (int32_t done = 0; !rc && nin > 0 && done < count && result;) {
+        const int32_t n = (count - done) < (int32_t)RSJ_SLICE_BYTES ? (count - done) : (int32_t)RSJ_SLICE_BYTES;
+        int part = 1;
+        if (!mi) {
+            const int copied = pin(e, &in) | pin(e, &out);
+            if (!pinned_ok(&in) || !pinned_ok(&out)) {
+                unpin(e, &out, NULL, RSJ_ABORT);
+                unpin(e, &in, NULL, RSJ_ABORT);
+                e->throw_new(e, "java/lang/OutOfMemoryError", "GetPrimitiveArrayCritical failed");
+                rc = -1;
+                break;
+            }
+            if (copied && count > (int32_t)RSJ_SLICE_BYTES && done == 0) {  /* the JVM copies: C buffers */
+                unpin(e, &out, NULL, RSJ_ABORT);
+                unpin(e, &in, NULL, RSJ_ABORT);
+                mi = slice_buffers(nin, ib);
+                mo = slice_buffers(nout, ob);
+                if (!mi || !mo) {
+                    e->throw_new(e, "java/lang/OutOfMemoryError", "slice buffers");
+                    rc = -1;
+                }
+                continue;
+            }
+            rc = verify ? b->check_some_shards(rp, (const uint8_t *const *)in.ptr, nin, (const uint8_t *const *)out.ptr,
+                                               nout, offset + done, n, &part)
+                        : b->code_some_shards(rp, (const uint8_t *const *)in.ptr, nin, out.ptr, nout, offset + done, n);
             unpin(e, &out, NULL, (verify || rc) ? RSJ_ABORT : RSJ_COMMIT);
             unpin(e, &in, NULL, RSJ_ABORT);
-            if (rc) throw_rc(e, b, rc);
-        }
-    } else {
-        uint8_t *ib[RSJ_MAX_SHARDS], *ob[RSJ_MAX_SHARDS];
-        uint8_t *mi = slice_buffers(nin, ib), *mo = slice_buffers(nout, ob);
-        if (!mi || !mo) {
-            e->throw_new(e, "java/lang/OutOfMemoryError", "slice buffers");
-            rc = -1;
-        }
-        for (int32_t done = 0; !rc && done < count && result;) {
-            const int32_t n = (count - done) < (int32_t)RSJ_SLICE_BYTES ? (count - done) : (int32_t)RSJ_SLICE_BYTES;
+        } else {
             for (int i = 0; i < nin; i++) e->byte_region_get(e, in.arr[i], offset + done, n, ib[i]);
             if (verify)
                 for (int i = 0; i < nout; i++) e->byte_region_get(e, out.arr[i], offset + done, n, ob[i]);
@@ -412,26 +431,25 @@ static int loop_call(rsj_env *e, const rsj_backend *b, rsj_obj rows, rsj_obj ins
                 rc = -1;
                 break;
             }
-            int part = 1;
             rc = verify ? b->check_some_shards(rp, (const uint8_t *const *)ib, nin, (const uint8_t *const *)ob, nout, 0,
                                                n, &part)
                         : b->code_some_shards(rp, (const uint8_t *const *)ib, nin, ob, nout, 0, n);
-            if (rc) {
-                throw_rc(e, b, rc);
-                break;
-            }
-            if (!part) result = 0;
-            if (!verify)
+            if (!rc && !verify)
                 for (int i = 0; i < nout; i++) e->byte_region_set(e, out.arr[i], offset + done, n, ob[i]);
-            if (e->exception_pending(e)) {
+            if (!rc && e->exception_pending(e)) {
                 rc = -1;
                 break;
             }
-            done += n;
         }
-        free(mi);
-        free(mo);
+        if (rc) {
+            throw_rc(e, b, rc);
+            break;
+        }
+        if (!part) result = 0;
+        done += n;
     }
+    free(mi);
+    free(mo);
     drop_refs(e, &out);
     drop_refs(e, &in);
     free(flat);

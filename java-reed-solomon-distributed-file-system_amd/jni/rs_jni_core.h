@@ -5,8 +5,8 @@
  * rs_jni.c implements rsj_env over a JNIEnv and exports the Java natives;
  * tests/jni_mock/ implements it over mock Java arrays, so the marshalling --
  * argument checks and the exceptions they raise, local-reference accounting,
- * critical-region pinning for small calls, slice-wise copies for large ones
- * -- is compiled and tested without a JDK.
+ * slice-by-slice critical-region pinning, the copying fallback -- is compiled
+ * and tested without a JDK.
  *
  * Semantics follow the reference Java code the natives replace:
  *   ReedSolomon.encodeParity / decodeMissing / isParityCorrect
@@ -34,13 +34,12 @@ extern "C" {
 #define RSJ_COMMIT 0 /* JNI release mode: copy back and free */
 #define RSJ_ABORT 2  /* JNI_ABORT: free without copying back */
 
-/* Calls with byte_count up to this many bytes pin the Java arrays
- * (GetPrimitiveArrayCritical) for the whole call; larger calls never hold a
- * critical region: they are coded in slices of RSJ_SLICE_BYTES copied through
- * C buffers (Get/SetByteArrayRegion), so the JVM can collect garbage between
- * slices. */
-#define RSJ_PIN_MAX_BYTES (4u << 20)
-#define RSJ_SLICE_BYTES (4u << 20)
+/* Calls are coded in slices of this many bytes per shard, each with the Java
+ * arrays pinned (GetPrimitiveArrayCritical) only for that slice: a critical
+ * region lasts one slice's GPU round trip (4+2: about 3 ms at 32 MiB), and
+ * the GC may run between slices.  When the JVM hands out copies instead of
+ * pinning, the slices are copied through C buffers (Get/SetByteArrayRegion). */
+#define RSJ_SLICE_BYTES (32u << 20)
 
 typedef void *rsj_obj; /* a jobject (jarray) */
 
@@ -51,7 +50,7 @@ struct rsj_env {
     rsj_obj (*object_element)(rsj_env *e, rsj_obj arr, int i); /* a new local reference, or NULL */
     void (*delete_local)(rsj_env *e, rsj_obj obj);
     int (*ensure_local_capacity)(rsj_env *e, int n);            /* 0, or < 0 with an exception pending */
-    uint8_t *(*critical_get)(rsj_env *e, rsj_obj arr);
+    uint8_t *(*critical_get)(rsj_env *e, rsj_obj arr, int *is_copy);
     void (*critical_release)(rsj_env *e, rsj_obj arr, uint8_t *p, int mode);
     void (*byte_region_get)(rsj_env *e, rsj_obj arr, int start, int len, uint8_t *dst);
     void (*byte_region_set)(rsj_env *e, rsj_obj arr, int start, int len, const uint8_t *src);

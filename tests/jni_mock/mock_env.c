@@ -36,6 +36,7 @@ typedef struct {
     char exc_cls[128], exc_msg[512];
     long long bytes_in, bytes_out, critical_gets, commits, aborts;
     int fail_critical;     /* critical_get returns NULL when set */
+    int force_copy;        /* critical_get reports isCopy (the data is still the array's) */
 } mstate;
 
 static mstate S;
@@ -65,6 +66,7 @@ void mock_set(mobj *outer, int i, mobj *inner) { outer->elems[i] = inner; }
 uint8_t *mock_data(mobj *o) { return o->data; }
 void mock_reset(void) { memset(&S, 0, sizeof S); S.capacity = 16; }
 void mock_fail_critical(int on) { S.fail_critical = on; }
+void mock_force_copy(int on) { S.force_copy = on; }
 const char *mock_exc_class(void) { return S.exc ? S.exc_cls : ""; }
 const char *mock_exc_message(void) { return S.exc ? S.exc_msg : ""; }
 void mock_stats(long long *out) {
@@ -116,8 +118,9 @@ static int m_ensure_local_capacity(rsj_env *e, int n) {
     if (S.live_refs + n > S.capacity) S.capacity = S.live_refs + n;
     return 0;
 }
-static uint8_t *m_critical_get(rsj_env *e, rsj_obj a) {
+static uint8_t *m_critical_get(rsj_env *e, rsj_obj a, int *is_copy) {
     if (S.exc) S.violations++;
+    *is_copy = S.force_copy;
     if (S.fail_critical) return NULL;
     S.critical_open++;
     S.critical_gets++;

@@ -10,7 +10,7 @@ import ctypes as C
 import numpy as np
 import pytest
 
-from test_jni_core import PIN_MAX, Jvm, build_mock
+from test_jni_core import SLICE, Jvm, build_mock
 
 pytestmark = pytest.mark.gpu
 
@@ -33,8 +33,8 @@ def codec104(native):
     native.rs_codec_destroy(h)
 
 
-@pytest.mark.parametrize("k,m,off,cnt", [(4, 2, 17, 100000), (4, 2, 3, PIN_MAX + 4099), (10, 4, 0, 65536),
-                                         (10, 4, 5, PIN_MAX + 1)])
+@pytest.mark.parametrize("k,m,off,cnt", [(4, 2, 17, 100000), (4, 2, 3, SLICE + 4099), (10, 4, 0, 65536),
+                                         (10, 4, 5, SLICE + 1)])
 def test_encode_decode_through_shim(gpu, oracle_lib, native, jvm, k, m, off, cnt):
     h = C.c_void_p()
     assert native.rs_codec_create(k, m, C.byref(h)) == 0
@@ -67,7 +67,7 @@ def test_encode_decode_through_shim(gpu, oracle_lib, native, jvm, k, m, off, cnt
         native.rs_codec_destroy(h)
 
 
-@pytest.mark.parametrize("cnt", [5000, PIN_MAX + 333])
+@pytest.mark.parametrize("cnt", [5000, SLICE + 333])
 def test_code_some_shards_through_shim(gpu, oracle_lib, jvm, cnt):
     rng = np.random.default_rng(cnt)
     nin, nout, off = 5, 3, 9

@@ -21,8 +21,7 @@ from conftest import PKG_DIR, ROOT
 BUILD = os.path.join(ROOT, "build", "jni_mock")
 SRC = [os.path.join(PKG_DIR, "jni", "rs_jni_core.c"), os.path.join(ROOT, "tests", "jni_mock", "mock_env.c")]
 LIBDIR = os.path.join(PKG_DIR, "lib")
-PIN_MAX = 4 << 20
-SLICE = 4 << 20
+SLICE = 32 << 20  # RSJ_SLICE_BYTES
 
 NPE = "java/lang/NullPointerException"
 IAE = "java/lang/IllegalArgumentException"
@@ -44,7 +43,7 @@ def build_mock():
     for name, res, args in [
         ("mock_new_bytes", P, [C.c_int]), ("mock_new_bools", P, [C.c_int]), ("mock_new_objects", P, [C.c_int]),
         ("mock_set", None, [P, C.c_int, P]), ("mock_data", P, [P]), ("mock_reset", None, []),
-        ("mock_fail_critical", None, [C.c_int]),
+        ("mock_fail_critical", None, [C.c_int]), ("mock_force_copy", None, [C.c_int]),
         ("mock_exc_class", C.c_char_p, []), ("mock_exc_message", C.c_char_p, []),
         ("mock_stats", None, [C.POINTER(C.c_longlong)]),
         ("mock_encode_parity", None, [C.c_int, P, P, C.c_int32, C.c_int32]),
@@ -138,25 +137,36 @@ def fake_parity(data, k, m, off, cnt):
     return out
 
 
-@pytest.mark.parametrize("off,cnt", [(100, 500), (0, PIN_MAX), (7, PIN_MAX + 1), (3, 2 * SLICE + 12345)])
-def test_encode_pinned_and_staged(jvm, codec42, off, cnt):
+def slices(cnt):
+    return max(1, -(-cnt // SLICE))
+
+
+@pytest.mark.parametrize("off,cnt,copy", [(100, 500, 0), (0, SLICE, 0), (7, SLICE + 1, 0), (3, 2 * SLICE + 12345, 0),
+                                          (7, SLICE + 1, 1), (100, 500, 1)])
+def test_encode_slices(jvm, codec42, off, cnt, copy):
+    """Per-slice pinning: each slice pins all 6 arrays, commits the 2 parity
+    arrays and aborts the 4 data arrays, no byte copied on the host; when the
+    JVM reports copies, a multi-slice call copies slices through C buffers."""
     S = off + cnt + 50
     data, arrs = shard_set(jvm, 4, 2, S, seed=cnt)
+    jvm.lib.mock_force_copy(copy)
     jvm.lib.mock_encode_parity(0, codec42, jvm.objects(arrs), off, cnt)
+    jvm.lib.mock_force_copy(0)
     assert jvm.exception() == ("", "")
     want = fake_parity(data, 4, 2, off, cnt)
     for i in range(6):
         assert np.array_equal(jvm.read(arrs[i], S), want[i]), i
     st = jvm.assert_clean()
-    if cnt <= PIN_MAX:  # critical regions: parity committed, data released without copy-back
-        assert st["critical_gets"] == 6 and st["commits"] == 2 and st["aborts"] == 4
-        assert st["bytes_in"] == 0 and st["bytes_out"] == 0
-    else:  # no critical region; data copied in, parity copied out, slice by slice
-        assert st["critical_gets"] == 0 and st["max_critical_open"] == 0
+    n = slices(cnt)
+    if copy and n > 1:  # one probing pin, then slices copied in and out
+        assert st["critical_gets"] == 6 and st["aborts"] == 6 and st["commits"] == 0
         assert st["bytes_in"] == 4 * cnt and st["bytes_out"] == 2 * cnt
+    else:
+        assert st["critical_gets"] == 6 * n and st["commits"] == 2 * n and st["aborts"] == 4 * n
+        assert st["bytes_in"] == 0 and st["bytes_out"] == 0 and st["max_critical_open"] == 6
 
 
-@pytest.mark.parametrize("cnt", [64, PIN_MAX + 64])
+@pytest.mark.parametrize("cnt", [64, SLICE + 64])
 def test_encode_check_order_and_messages(jvm, codec42, cnt):
     S = cnt + 10
     # wrong number of shards: reported before any element is touched (a null one included)
@@ -207,22 +217,24 @@ def fake_decode(data, present, off, cnt):
     return out
 
 
-@pytest.mark.parametrize("cnt", [1000, PIN_MAX + 1000])
-def test_decode_roles_and_commit(jvm, codec42, cnt):
+@pytest.mark.parametrize("cnt,copy", [(1000, 0), (SLICE + 1000, 0), (SLICE + 1000, 1)])
+def test_decode_roles_and_commit(jvm, codec42, cnt, copy):
     S = cnt + 5
     present = [False, True, True, True, True, False]
     data, arrs = shard_set(jvm, 4, 2, S, seed=5)
+    jvm.lib.mock_force_copy(copy)
     jvm.lib.mock_decode_missing(0, codec42, jvm.objects(arrs), jvm.bools(present), 5, cnt)
+    jvm.lib.mock_force_copy(0)
     assert jvm.exception() == ("", "")
     want = fake_decode(data, present, 5, cnt)
     for i in range(6):
         assert np.array_equal(jvm.read(arrs[i], S), want[i]), i
     st = jvm.assert_clean()
-    if cnt <= PIN_MAX:
-        assert st["commits"] == 2 and st["aborts"] == 4
-    else:
-        # (+6: the shardPresent booleans)
-        assert st["bytes_in"] == 4 * cnt + 6 and st["bytes_out"] == 2 * cnt and st["critical_gets"] == 0
+    n = slices(cnt)
+    if copy:  # (+6: the shardPresent booleans)
+        assert st["bytes_in"] == 4 * cnt + 6 and st["bytes_out"] == 2 * cnt
+    else:  # the missing shards are committed, the survivors released without copy-back
+        assert st["commits"] == 2 * n and st["aborts"] == 4 * n and st["bytes_out"] == 0
 
 
 def test_decode_present_array_checks(jvm, codec42):
@@ -244,7 +256,7 @@ def test_decode_present_array_checks(jvm, codec42):
     assert jvm.exception() == ("", "")
 
 
-@pytest.mark.parametrize("cnt", [300, PIN_MAX + 300])
+@pytest.mark.parametrize("cnt", [300, SLICE + 300])
 def test_is_parity_correct(jvm, codec42, cnt):
     S = cnt + 20
     data, _ = shard_set(jvm, 4, 2, S, seed=9)
@@ -274,8 +286,8 @@ def fake_code(rows, ins, off, cnt):
     return outs
 
 
-@pytest.mark.parametrize("cnt", [777, PIN_MAX + 777])
-def test_code_some_shards_extra_entries_ignored(jvm, cnt):
+@pytest.mark.parametrize("cnt,copy", [(777, 0), (SLICE + 777, 0), (SLICE + 777, 1)])
+def test_code_some_shards_extra_entries_ignored(jvm, cnt, copy):
     rng = np.random.default_rng(3)
     nin, nout, off = 3, 2, 13
     S = off + cnt + 3
@@ -283,8 +295,10 @@ def test_code_some_shards_extra_entries_ignored(jvm, cnt):
     rows = [rng.integers(0, 256, nin + 2, dtype=np.uint8) for _ in range(nout)]  # rows longer than inputCount
     outs = [np.full(S, 0xEE, dtype=np.uint8) for _ in range(nout + 1)]
     ia, oa = [jvm.bytes(a) for a in ins], [jvm.bytes(a) for a in outs]
+    jvm.lib.mock_force_copy(copy)
     jvm.lib.mock_code_some_shards(0, jvm.objects([jvm.bytes(r) for r in rows]), jvm.objects(ia), nin,
                                   jvm.objects(oa), nout, off, cnt)
+    jvm.lib.mock_force_copy(0)
     assert jvm.exception() == ("", "")
     want = fake_code(rows, ins[:nin], off, cnt)
     for p in range(nout):
@@ -293,9 +307,12 @@ def test_code_some_shards_extra_entries_ignored(jvm, cnt):
         assert (got[:off] == 0xEE).all() and (got[off + cnt:] == 0xEE).all()
     assert (jvm.read(oa[nout], S) == 0xEE).all()
     st = jvm.assert_clean()
-    if cnt > PIN_MAX:
-        # (+ nout * nin: the matrix rows)
-        assert st["critical_gets"] == 0 and st["bytes_in"] == nin * cnt + nout * nin and st["bytes_out"] == nout * cnt
+    n = slices(cnt)
+    if copy and n > 1:  # (+ nout * nin: the matrix rows)
+        assert st["bytes_in"] == nin * cnt + nout * nin and st["bytes_out"] == nout * cnt
+    else:
+        assert st["critical_gets"] == (nin + nout) * n and st["commits"] == nout * n
+        assert st["bytes_in"] == nout * nin and st["bytes_out"] == 0
     # checkSomeShards on what was just written: true, then false after a flip
     chk = [jvm.bytes(jvm.read(o, S)) for o in oa[:nout]]
     rows_o = jvm.objects([jvm.bytes(r) for r in rows])
@@ -353,6 +370,7 @@ def test_critical_failure_releases_everything(jvm, codec42):
     _, arrs = shard_set(jvm, 4, 2, 100)
     jvm.lib.mock_fail_critical(1)
     jvm.lib.mock_encode_parity(0, codec42, jvm.objects(arrs), 0, 10)
+    jvm.lib.mock_fail_critical(0)
     assert jvm.exception()[0] == "java/lang/OutOfMemoryError"
     jvm.assert_clean()
 
