@@ -818,7 +818,7 @@ hipError_t launch_gf(const Geometry &g, const DevPlan &p, Mode mode, int *mismat
     const bool aligned = (reinterpret_cast<uintptr_t>(g.base + g.col0) % 16 == 0) && g.shard_stride % 16 == 0 &&
                          g.stripe_stride % 16 == 0;
     const uint64_t moved = uint64_t(g.n_stripes) * g.len * uint64_t(p.nin + p.nout);
-    if (p.rows && aligned && g.len >= kXorChunk && g.len / kXorChunk <= UINT32_MAX / 2 &&
+    if (p.rows && aligned && g.len >= kXorChunk && g.len / kXorChunk <= kMaxGridBlocks &&
         p.nout <= kMaxOut && xornet_enabled_now() && moved >= xornet_min_bytes()) {
         size_t done = 0;
         const hipError_t e = launch_gf_xornet(g, p, mode, mismatch, s, &done);

@@ -249,3 +249,28 @@ def test_kernels_use_no_scratch(native, tmp_path):
     assert len(kernels) > 40
     bad = {k: v for k, v in kernels.items() if any(v.values())}
     assert not bad, bad
+
+
+def test_decode_plan_cache_eviction_keeps_plans_exact(oracle_lib):
+    """More distinct presence patterns than the codec's plan cache holds
+    (kMaxDecodePlans = 4096, least recently used evicted): every fused decode
+    matrix -- fresh, evicted and rebuilt, or a cache hit -- equals the oracle's
+    (ReedSolomon.java:210-271 restated)."""
+    import itertools
+
+    import rsamd
+    k, m = 12, 8
+    rs = rsamd.ReedSolomon.create(k, m)
+    oc = oracle_lib.Codec(k, m)
+    rng = np.random.default_rng(7)
+    pats = []
+    for e in range(1, m + 1):
+        for miss in itertools.islice(itertools.combinations(range(k + m), e), 900):
+            pats.append([i not in miss for i in range(k + m)])
+    assert len(pats) > 4096
+    order = list(range(len(pats))) + list(rng.integers(0, len(pats), 600))  # then revisit evicted ones
+    for idx in order:
+        p = pats[idx]
+        surv, miss, rows = rs.decode_matrix(p)
+        osurv, omiss, orows = oc.decode_rows(p)
+        assert surv == osurv[:k] and miss == omiss and np.array_equal(rows, orows), idx
