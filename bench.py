@@ -21,7 +21,9 @@ At N=1 rank 0 also reports the per-GPU legs (more erasure patterns, verify,
 copy kernel, configs[4], the fused file layout, host-inclusive rates,
 configs[0]) and the CPU baseline -- the oracle's scalar restatement of the
 reference loop (InputOutputByteTableCodingLoop.java:12-44) timed on bounded
-samples on this host, 1 thread and the host's CPU share.
+samples on this host, 1 thread and the host's CPU share.  Before any of that
+(N=1, default config) two rocprofv3 --pmc child runs measure the headline
+kernel's HBM bytes per launch for roofline.traffic (--no-live-pmc skips them).
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       --gpus N > 1 without WORLD_SIZE in the environment: this process starts
@@ -69,8 +71,10 @@ def parse(argv=None):
     ap.add_argument("--launch-probe", action="store_true",
                     help="launcher self-test: ranks join the process group on CPU (gloo) and report, no GPU work")
     ap.add_argument("--alloc", choices=["contiguous", "hipmalloc"], default="contiguous",
-                    help="HBM for the headline stripe batch: rs_dev_alloc contiguous range (default) or torch/hipMalloc "
-                         "(the other configs' pools stay hipMalloc: contiguous measured no better there)")
+                    help="HBM for the headline stripe batch: rs_dev_alloc contiguous range (default) or torch/hipMalloc")
+    ap.add_argument("--no-live-pmc", action="store_true",
+                    help="skip the rocprofv3 --pmc child runs that measure the headline kernel's HBM bytes in this run "
+                         "(roofline.traffic then comes from profiles/pmc_traffic.json)")
     return ap.parse_args(argv)
 
 
@@ -117,7 +121,10 @@ def main(argv=None):
         return 2
     if args.launch_probe:
         return launch_probe(args)
-    run(args)
+    live = None
+    if not (args.no_extras or args.no_live_pmc) and (args.k, args.m, args.shard_bytes, args.stripes) == (4, 2, 1 << 20, 4096):
+        live = live_pmc_traffic()  # before this process touches the GPU: the passes are children
+    run(args, live)
     return 0
 
 
@@ -182,7 +189,7 @@ def timed_all_ranks(torch, parallel, r, fn, iters):
 # ---------------------------------------------------------------------------
 # The run
 # ---------------------------------------------------------------------------
-def run(args):
+def run(args, live_traffic=None):
     import torch
 
     import rsamd
@@ -256,7 +263,9 @@ def run(args):
         else:
             # every rank at once: the node's aggregate host <-> device rate
             extra.update(host_inclusive_all_ranks(rsamd, parallel, r, k, m))
-    traffic = pmc_traffic(k, m, S, B)
+    traffic, traffic_source = pmc_traffic(k, m, S, B), "profiles/pmc_traffic.json (committed rocprofv3 --pmc summary)"
+    if live_traffic and live_traffic.get("hbm_bytes_per_launch"):
+        traffic, traffic_source = live_traffic["hbm_bytes_per_launch"], "rocprofv3 --pmc passes in this run"
 
     if rank == 0:
         line = {
@@ -286,6 +295,8 @@ def run(args):
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_source,
+                "traffic_live": live_traffic,
                 "kernel": f"gf_vec_kernel<{k},{m},false> (rs_encode_batch_dev)",
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_ms": round(launch_ms, 4),
@@ -819,6 +830,68 @@ def host_inclusive_all_ranks(rsamd, parallel, r, k, m, n=64 << 20, reps=4):
                                             f"call, {reps} calls per rank")
     del pin, pageable
     return out
+
+
+def profiled() -> bool:
+    """True when this process already runs under rocprofv3 (its tool library is
+    preloaded): a nested profiler would fight it, so no live passes then."""
+    env = os.environ
+    return any("rocprof" in env.get(v, "") for v in ("LD_PRELOAD", "ROCP_TOOL_LIBRARIES", "HSA_TOOLS_LIB")) or \
+        any(v.startswith("ROCPROF") for v in env)
+
+
+def live_pmc_traffic(seconds=90):
+    """HBM bytes per launch of the headline kernel, measured now: two
+    rocprofv3 --pmc children (FETCH_SIZE, then WRITE_SIZE: they do not fit one
+    gfx950 TCC pass) over tools/pmc_workloads.py enc42, which fills and encodes
+    the headline batch and launches gf_vec_kernel<4,2,false> 3 times.  Bytes =
+    (2 * FETCH_SIZE + WRITE_SIZE) KiB, MI355X_MICROARCH.md's gfx950 wide-read
+    correction (tools/pmc_summary.py does the same for the committed summary).
+    Median over the launches.  Returns None when rocprofv3 is missing, this
+    process is itself profiled, or a pass fails or outlives its limit."""
+    import csv
+    import glob
+    import shutil
+    import statistics
+    import tempfile
+    rocprof = shutil.which("rocprofv3") or ("/opt/rocm/bin/rocprofv3" if os.path.exists("/opt/rocm/bin/rocprofv3")
+                                            else None)
+    if rocprof is None or profiled():
+        return None
+    kernel = "gf_vec_kernel<4, 2, false>"
+    alg = 6 * (1 << 20) * 4096
+    vals = {}
+    t0 = time.perf_counter()
+    env = dict(os.environ, TMPDIR="/tmp")
+    env.pop("RSAMD_XORNET", None)  # the headline's table kernel, not the opt-in XOR network
+    with tempfile.TemporaryDirectory(prefix="rsamd_pmc_", dir="/tmp") as tmp:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, counter)
+            cmd = ["timeout", "-s", "KILL", str(seconds), rocprof, "--pmc", counter, "--output-format", "csv",
+                   "-d", d, "-o", "run", "--", sys.executable, os.path.join(ROOT, "tools", "pmc_workloads.py"),
+                   "enc42"]
+            try:
+                p = subprocess.run(cmd, cwd=tmp, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                   timeout=seconds + 30)
+            except (OSError, subprocess.TimeoutExpired):
+                return None
+            if p.returncode != 0:
+                print(f"bench.py: live {counter} pass failed ({p.returncode}); using the committed summary",
+                      file=sys.stderr)
+                return None
+            got = []
+            for path in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
+                with open(path) as f:
+                    got += [float(row["Counter_Value"]) for row in csv.DictReader(f)
+                            if row.get("Counter_Name") == counter and kernel in row.get("Kernel_Name", "")]
+            if not got:
+                return None
+            vals[counter] = (statistics.median(got), len(got))
+    (f_kib, nf), (w_kib, nw) = vals["FETCH_SIZE"], vals["WRITE_SIZE"]
+    hbm = int(round((2 * f_kib + w_kib) * 1024))
+    return {"kernel": kernel, "launches": [nf, nw], "fetch_kib_raw": f_kib, "write_kib_raw": w_kib,
+            "hbm_bytes_per_launch": hbm, "alg_bytes_per_launch": alg, "ratio": round(hbm / alg, 4),
+            "seconds": round(time.perf_counter() - t0, 1)}
 
 
 def pmc_traffic(k, m, S, B):

@@ -17,6 +17,28 @@ const bool g_exit_hook = [] {
 }();
 }  // namespace
 
+hipError_t upload(int dev, void *dst, const void *src, size_t n) {
+    // One non-blocking stream per device, created on first use and kept for the
+    // process: the copy waits for nothing queued elsewhere (a hipMemcpy on the
+    // null stream would wait for a caller's in-flight work on that stream).
+    static std::mutex mu;
+    static std::map<int, hipStream_t> streams;
+    hipStream_t s = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        auto it = streams.find(dev);
+        if (it == streams.end()) {
+            const hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+            if (e != hipSuccess) return e;
+            it = streams.emplace(dev, s).first;
+        }
+        s = it->second;
+    }
+    hipError_t e = hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    return e;
+}
+
 void free_device(int dev, void *p) {
     if (!p || g_exiting.load()) return;
     int cur = 0;
@@ -106,7 +128,7 @@ hipError_t Plan::device_plans(std::vector<DevPlan> *out) const {
         if (e != hipSuccess) return e;
         for (int g = 0; g < groups(); ++g) {
             const std::vector<uint8_t> img = image(g);
-            e = hipMemcpy(static_cast<uint8_t *>(buf) + offs[g], img.data(), img.size(), hipMemcpyHostToDevice);
+            e = upload(dev, static_cast<uint8_t *>(buf) + offs[g], img.data(), img.size());
             if (e != hipSuccess) {
                 (void)hipFree(buf);
                 return e;
@@ -154,7 +176,7 @@ hipError_t Plan::device_file_plan(int k, FileDecodePlan *out) const {
         void *buf = nullptr;
         e = hipMalloc(&buf, img.size());
         if (e != hipSuccess) return e;
-        e = hipMemcpy(buf, img.data(), img.size(), hipMemcpyHostToDevice);
+        e = upload(dev, buf, img.data(), img.size());
         if (e != hipSuccess) {
             (void)hipFree(buf);
             return e;
@@ -329,7 +351,7 @@ int Codec::pattern_tables(PatternTables *out, std::string *err) const {
         for (size_t q = 0; q < t.npat; ++q) fill_masked_record(*plans[q], g, t.mslots, L, img.data() + (g * t.npat + q) * L.bytes);
     std::memcpy(img.data() + rec_bytes, table.data(), size_t(n) * sizeof(int32_t));
     void *buf = nullptr;
-    if (hipMalloc(&buf, img.size()) != hipSuccess || hipMemcpy(buf, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    if (hipMalloc(&buf, img.size()) != hipSuccess || upload(dev, buf, img.data(), img.size()) != hipSuccess) {
         if (buf) (void)hipFree(buf);
         *err = "pattern table upload failed";
         return RS_E_HIP;

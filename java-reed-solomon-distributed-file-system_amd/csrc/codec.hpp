@@ -33,7 +33,8 @@ public:
     int groups() const { return int((out_idx_.size() + kMaxOut - 1) / kMaxOut); }
 
     // Per-group device plans on the calling thread's current device; uploaded
-    // once per device (blocking hipMemcpy on first use) and then immutable.
+    // once per device on first use (upload(): the host waits for that copy
+    // only) and then immutable.
     hipError_t device_plans(std::vector<DevPlan> *out) const;
 
     // The flat image uploaded for group g (exposed for per-call uploads).
@@ -51,6 +52,10 @@ private:
     mutable std::map<int, void *> dev_;       // device id -> allocation of all groups
     mutable std::map<int, void *> dev_file_;  // device id -> FileDecodePlan image
 };
+
+// Copy host -> device on a private non-blocking stream of device dev and wait
+// for that copy alone (not for work queued on the caller's or the null stream).
+hipError_t upload(int dev, void *dst, const void *src, size_t n);
 
 // Device memory freed outside process teardown only: once exit() has begun the
 // HIP runtime may already be gone, and the process releases everything anyway.
@@ -124,7 +129,7 @@ private:
     mutable std::map<std::vector<uint8_t>, CacheEntry> decode_cache_;
     mutable std::list<std::vector<uint8_t>> lru_;  // most recently used first
     mutable std::mutex pat_mu_;
-    mutable std::map<int, PatternTables> patterns_;  // device id -> tables (leaked with the process)
+    mutable std::map<int, PatternTables> patterns_;  // device id -> tables (freed by ~Codec)
     mutable std::vector<int32_t> host_mask_table_;
     mutable std::string pattern_refusal_;  // set once the code is found too wide for a table
 };

@@ -58,3 +58,39 @@ def test_gpus_must_be_positive():
     p = subprocess.run([sys.executable, BENCH, "--gpus", "0"], env=_env(), capture_output=True, text=True,
                        timeout=120)
     assert p.returncode == 2
+
+
+FAKE_ROCPROF = r'''#!/bin/bash
+# stand-in for rocprofv3 --pmc C --output-format csv -d DIR -o run -- prog...: writes the
+# counter CSV layout rocprofv3 writes, 4 launches of the headline kernel plus the fill kernel
+while [ "$1" != "--" ]; do case "$1" in --pmc) C=$2; shift;; -d) D=$2; shift;; esac; shift; done
+mkdir -p "$D/host/123"
+F="$D/host/123/run_counter_collection.csv"
+echo 'Kernel_Name,Counter_Name,Counter_Value' > "$F"
+echo '"fill_kernel",'$C',999' >> "$F"
+for v in 8388600 8388608 8388610 8388700; do
+  echo '"void gf_vec_kernel<4, 2, false>(GfArgs)",'$C','$v >> "$F"
+done
+'''
+
+
+def test_live_pmc_traffic_parses_and_corrects(tmp_path, monkeypatch):
+    """bench.live_pmc_traffic: two child passes, median over the headline
+    kernel's launches, FETCH_SIZE doubled (gfx950 wide reads), KiB -> bytes;
+    skipped under a profiler."""
+    sys.path.insert(0, ROOT)
+    import bench
+    fake = tmp_path / "rocprofv3"
+    fake.write_text(FAKE_ROCPROF)
+    fake.chmod(0o755)
+    monkeypatch.setenv("PATH", f"{tmp_path}:{os.environ['PATH']}")
+    for v in ("LD_PRELOAD", "ROCP_TOOL_LIBRARIES", "HSA_TOOLS_LIB"):
+        monkeypatch.delenv(v, raising=False)
+    got = bench.live_pmc_traffic(seconds=30)
+    assert got["launches"] == [4, 4]
+    # medians (8388608 + 8388610) / 2 KiB raw for both; reads 16 GiB, FETCH_SIZE shows half, writes 8 GiB
+    assert got["hbm_bytes_per_launch"] == int(round((2 * 8388609 + 8388609) * 1024))
+    assert got["alg_bytes_per_launch"] == 6 * (1 << 20) * 4096
+    assert abs(got["ratio"] - 1.0) < 1e-4
+    monkeypatch.setenv("LD_PRELOAD", "/opt/rocm/lib/librocprofiler-sdk-tool.so")
+    assert bench.live_pmc_traffic(seconds=30) is None

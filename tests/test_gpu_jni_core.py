@@ -1,8 +1,8 @@
 """The JNI shim's marshalling (jni/rs_jni_core.c) over the real librsamd
 backend on the GPU, through the mock JNI environment of test_jni_core.py:
-Java-array in, Java-array out, compared with the oracle byte for byte, on both
-of the shim's paths (pinned critical regions for small calls, slice-wise
-copies above 4 MiB), with the reference's offsets and erasure patterns
+Java-array in, Java-array out, compared with the oracle byte for byte, for
+single-slice calls and for calls pinned slice by slice (more than SLICE bytes
+per shard), with the reference's offsets and erasure patterns
 (ReedSolomon.java:90-104, 175-272; ReedSolomonTest.java:77-93's {0, 5}).
 """
 import ctypes as C
