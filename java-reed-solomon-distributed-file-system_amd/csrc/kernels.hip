@@ -327,8 +327,15 @@ __device__ __forceinline__ void count_undecodable(int32_t *bad, bool col0) {
     if (bad && col0) atomicAdd(bad, 1);
 }
 
+// Register budget for 7 waves per SIMD (72 VGPRs).  At 10+4 the kernel needs
+// 73 and ran at 6 waves, about 1.5 points under an XOR reference of its own
+// access pattern; at 72 it spills 5 dwords per lane (20 B of scratch) and runs
+// at or above that reference, 0.744-0.750 against 0.735-0.745 for the uniform
+// decode on the same pool (tools/masked_ref_probe.py,
+// profiles/r2/masked_ref_r2af.txt).  The same budget on gf_vec_kernel<10,4>
+// (8 waves, 56 B spilled) cost 9 points (masked_ref_r2ae.txt).
 template <int K, int MS>
-__global__ void __launch_bounds__(kWave) gf_masked_kernel(MaskedArgs a) {
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(7, 8))) gf_masked_kernel(MaskedArgs a) {
     uint32_t stripe, chunk;
     block_item(a.chunks, a.cdiv, a.rot, a.xcd_span, stripe, chunk);
     const uint32_t v = chunk * uint32_t(kWave) + threadIdx.x;

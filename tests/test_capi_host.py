@@ -220,7 +220,7 @@ def test_kernels_use_no_scratch(native, tmp_path):
     """Every gfx950 kernel in librsamd.so has a private segment of 0 and no
     VGPR spills: a run-time index into a register array (or a VGPR spill)
     sends vectors through scratch memory and doubles HBM traffic (DESIGN.md
-    3.4).  SGPR spills (the E/M = 3, 4 layout variants) go to VGPR lanes, not
+    3.4) -- with one measured exception below.  SGPR spills (the E/M = 3, 4 layout variants) go to VGPR lanes, not
     memory.  Reads the code object's AMDGPU metadata notes."""
     import shutil
     import subprocess
@@ -247,8 +247,15 @@ def test_kernels_use_no_scratch(native, tmp_path):
             elif name and line.split(":")[0] in (".private_segment_fixed_size", ".vgpr_spill_count"):
                 kernels[name][line.split(":")[0]] = int(line.split(":", 1)[1])
     assert len(kernels) > 40
-    bad = {k: v for k, v in kernels.items() if any(v.values())}
+    # The one deliberate exception: gf_masked_kernel<10,4> is held to 72 VGPRs
+    # (7 waves per SIMD) and spills 5 dwords per lane; measured faster than 73
+    # VGPRs at 6 waves, with the extra bytes staying in L2 (kernels.hip, the
+    # comment on gf_masked_kernel).
+    allowed = {"_ZN5rsamd12_GLOBAL__N_116gf_masked_kernelILi10ELi4EEEvNS0_10MaskedArgsE": 20}
+    bad = {k: v for k, v in kernels.items()
+           if any(v.values()) and v.get(".private_segment_fixed_size", 0) > allowed.get(k, 0)}
     assert not bad, bad
+    assert all(k in kernels for k in allowed)
 
 
 def test_decode_plan_cache_eviction_keeps_plans_exact(oracle_lib):
