@@ -349,7 +349,7 @@ def sustained(torch, parallel, r, rs, rdev, buf, lay, stream, k, m, S, B, second
     """>= `seconds` of back-to-back headline encodes on every rank (so the
     rate is seen at thermal steady state, not over an 80 ms burst), with the
     GPU clocks sampled from sysfs meanwhile."""
-    sampler = ClockSampler()
+    sampler = ClockSampler(pci=pci_address(torch))
     rdev.encode(rs, buf.data_ptr(), lay, stream)
     parallel.barrier(r)
     sampler.start()
@@ -373,13 +373,28 @@ def sustained(torch, parallel, r, rs, rdev, buf, lay, stream, k, m, S, B, second
     return out
 
 
-class ClockSampler:
-    """Samples busy %, SCLK and MCLK of the GPUs sysfs exposes, every 0.25 s
-    on a thread; stop() reports the busiest card's samples."""
+def pci_address(torch):
+    """PCI address prefix ("dddd:bb:dd.") of this rank's GPU, or None."""
+    try:
+        p = torch.cuda.get_device_properties(torch.cuda.current_device())
+        return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}."
+    except (AttributeError, RuntimeError):
+        return None
 
-    def __init__(self, period=0.25):
+
+class ClockSampler:
+    """Samples busy %, SCLK and MCLK every 0.25 s on a thread.  With pci (this
+    rank's GPU, pci_address()) only the DRM card at that PCI address is read
+    -- the node's other GPUs may be busy with other jobs; without it, or when
+    no card matches, stop() reports the busiest card's samples."""
+
+    def __init__(self, period=0.25, pci=None, root="/sys/class/drm"):
         import glob
-        self.cards = sorted(d for d in glob.glob("/sys/class/drm/card*/device") if os.path.exists(d + "/pp_dpm_sclk"))
+        self.cards = sorted(d for d in glob.glob(root + "/card*/device") if os.path.exists(d + "/pp_dpm_sclk"))
+        mine = [d for d in self.cards if pci and os.path.basename(os.path.realpath(d)).startswith(pci)]
+        self.matched = bool(mine)
+        if mine:
+            self.cards = mine[:1]
         self.period, self.samples, self._stop = period, {c: [] for c in self.cards}, threading.Event()
         self._t = threading.Thread(target=self._loop, daemon=True)
 
@@ -429,6 +444,8 @@ class ClockSampler:
             vals = sorted(v for v in vals if v is not None)
             return vals[len(vals) // 2] if vals else None
         return {"source": "sysfs pp_dpm_sclk / pp_dpm_mclk / gpu_busy_percent", "card": c.split("/")[-2],
+                "card_pci": os.path.basename(os.path.realpath(c)),
+                "card_choice": "this GPU's PCI address" if self.matched else "busiest card (no PCI match)",
                 "samples": len(s), "busy_pct_max": max((b for b, _, _ in s if b is not None), default=None),
                 "busy_pct_median": med(b for b, _, _ in s), "sclk_mhz_median": med(x for _, x, _ in s),
                 "sclk_mhz_min": min((x for _, x, _ in s if x is not None), default=None),

@@ -139,21 +139,41 @@ __device__ __forceinline__ void block_item(uint32_t chunks, const FastDiv &cdiv,
 // function behind the kernel's early exits, the same code was scheduled with
 // every table load hoisted: 146 VGPRs and 3 waves per SIMD at 10+4).
 //
-// All K input vectors are loaded up front.  The tables are staged one input
-// at a time: the M*5 dwords of input i+1 are fetched while input i is folded
+// Input vectors: K <= 4 loads all K up front.  Wide codes load AHEAD of them
+// up front and the rest two at a time, as each input pair is folded in and its
+// registers free up.  The tables are staged one input (pair) at a time: the
+// M*5 dwords of the next input are fetched while the current one is folded
 // in, and sched_barrier stops the scheduler from hoisting all K*M*5 of them,
 // which overflows the SGPR file at 10+4 (it spills into VGPR lanes: 3x
 // slower).  For K <= 4 the terms are folded in pairs across inputs
 // (fold_terms: 1.5 v_bitop3_b32 per input and output dword instead of 2); the
-// carried term costs M*4 VGPRs, which at 10+4 would drop the kernel from 7 to
-// 6 waves per SIMD, so wider codes fold each input alone.
-//   in: sb, TABS, IN_IDX, OUT_IDX, SHARD_STRIDE; out: out_off[M], acc[M] (u32x4)
-#define RSAMD_CODE_VECTORS(K, M, TABS, IN_IDX, OUT_IDX, SHARD_STRIDE)                                     \
+// carried term costs M*4 VGPRs, so wider codes fold each input alone.
+//   in: sb, TABS, IN_IDX, OUT_IDX, SHARD_STRIDE, AHEAD; out: out_off[M], acc[M] (u32x4)
+//
+// gf_vec_kernel<10,4> with all 10 loads up front needs 72 VGPRs (7 waves per
+// SIMD); with 5 ahead and a budget of 8 waves it needs 62, unspilled.  On one
+// pool, alternating builds (tools/lib_ab_same.py, profiles/r2/lib_ab_same_r2ak.txt
+// and r2al): 10+4 x 128 encode +0.4-1.0, decode +0.9-1.4, verify +1.2-1.9,
+// x 1024 +0.3 points of peak; 4+2 unchanged (same code).  gf_masked_kernel keeps
+// all loads up front at 7 waves (its comment).  Raising wave priority while
+// loads issue (s_setprio 3) cost 2-9 points; s_sleep before the stores was
+// neutral (lib_ab_same_r2ai.txt).
+#ifndef RSAMD_VEC_WAVES
+#define RSAMD_VEC_WAVES 8  // gf_vec_kernel register budget, waves per SIMD (A/B builds: make KDEFS=...)
+#endif
+#ifndef RSAMD_VEC_AHEAD
+#define RSAMD_VEC_AHEAD 5  // gf_vec_kernel, wide codes: inputs loaded before the first fold
+#endif
+#ifndef RSAMD_MASKED_WAVES
+#define RSAMD_MASKED_WAVES 7  // gf_masked_kernel: see the comment on it
+#endif
+#define RSAMD_CODE_VECTORS(K, M, TABS, IN_IDX, OUT_IDX, SHARD_STRIDE, AHEAD)                              \
     constexpr bool kCarry = (K) <= 4;                                                                     \
     uint64_t out_off[M]; /* read before any store so these stay scalar loads */                          \
     _Pragma("unroll") for (int p = 0; p < (M); ++p) out_off[p] = uint64_t((OUT_IDX)[p]) * (SHARD_STRIDE); \
+    constexpr int kAhead = kCarry ? (K) : ((K) < (AHEAD) ? (K) : (AHEAD));                                \
     u32x4 x[K];                                                                                           \
-    _Pragma("unroll") for (int i = 0; i < (K); ++i) x[i] = load_stream(sb + uint64_t((IN_IDX)[i]) * (SHARD_STRIDE)); \
+    _Pragma("unroll") for (int i = 0; i < kAhead; ++i) x[i] = load_stream(sb + uint64_t((IN_IDX)[i]) * (SHARD_STRIDE)); \
     uint32_t fa[M][4];                                                                                    \
     if (kCarry) {                                                                                         \
         uint32_t Tc[M][5], fc[M][4];                                                                      \
@@ -206,6 +226,10 @@ __device__ __forceinline__ void block_item(uint32_t chunks, const FastDiv &cdiv,
                     }                                                                                     \
                 }                                                                                         \
             }                                                                                             \
+            /* the pair's registers are free: load the inputs kAhead further on */                         \
+            _Pragma("unroll") for (int q = 0; q < 2; ++q)                                                 \
+                if (i + q + kAhead < (K) && q < n2)                                                       \
+                    x[i + q + kAhead] = load_stream(sb + uint64_t((IN_IDX)[i + q + kAhead]) * (SHARD_STRIDE)); \
             __builtin_amdgcn_sched_barrier(0);                                                            \
         }                                                                                                 \
     }                                                                                                     \
@@ -222,14 +246,14 @@ __device__ __forceinline__ void block_item(uint32_t chunks, const FastDiv &cdiv,
 // coefficient tables, so every table load is a scalar load.
 // ---------------------------------------------------------------------------
 template <int K, int M, bool VERIFY>
-__global__ void __launch_bounds__(kWave) gf_vec_kernel(VecArgs a) {
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(RSAMD_VEC_WAVES, 8))) gf_vec_kernel(VecArgs a) {
     if (VERIFY && mismatch_seen(a.mismatch)) return;
     uint32_t stripe, chunk;
     block_item(a.chunks, a.cdiv, a.rot, a.xcd_span, stripe, chunk);
     const uint32_t v = chunk * uint32_t(kWave) + threadIdx.x;
     if (v >= a.nvec) return;
     uint8_t *sb = a.base + uint64_t(stripe) * a.stripe_stride + uint64_t(v) * 16;
-    RSAMD_CODE_VECTORS(K, M, a.tabs, a.in_idx, a.out_idx, a.shard_stride)
+    RSAMD_CODE_VECTORS(K, M, a.tabs, a.in_idx, a.out_idx, a.shard_stride, RSAMD_VEC_AHEAD)
     if (VERIFY) {  // as in gf_masked_kernel: keep the compares' inputs from being sunk
 #pragma unroll
         for (int p = 0; p < M; ++p) asm volatile("" : "+v"(acc[p]));
@@ -335,7 +359,7 @@ __device__ __forceinline__ void count_undecodable(int32_t *bad, bool col0) {
 // profiles/r2/masked_ref_r2af.txt).  The same budget on gf_vec_kernel<10,4>
 // (8 waves, 56 B spilled) cost 9 points (masked_ref_r2ae.txt).
 template <int K, int MS>
-__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(7, 8))) gf_masked_kernel(MaskedArgs a) {
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(RSAMD_MASKED_WAVES, 8))) gf_masked_kernel(MaskedArgs a) {
     uint32_t stripe, chunk;
     block_item(a.chunks, a.cdiv, a.rot, a.xcd_span, stripe, chunk);
     const uint32_t v = chunk * uint32_t(kWave) + threadIdx.x;
@@ -350,7 +374,7 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(7, 8
     const int32_t *out_idx = reinterpret_cast<const int32_t *>(rec + a.rec_out_idx);
     const uint32_t *tabs = reinterpret_cast<const uint32_t *>(rec + a.rec_tabs);
     uint8_t *sb = a.base + uint64_t(stripe) * a.stripe_stride + uint64_t(v) * 16;
-    RSAMD_CODE_VECTORS(K, MS, tabs, in_idx, out_idx, a.shard_stride)
+    RSAMD_CODE_VECTORS(K, MS, tabs, in_idx, out_idx, a.shard_stride, K)
     // Pin the accumulators before the stores: their only uses are the
     // `p < nout` stores, and without this LLVM sinks each output's whole
     // perm/fold chain into its store block, past every table stage, so all

@@ -94,3 +94,31 @@ def test_live_pmc_traffic_parses_and_corrects(tmp_path, monkeypatch):
     assert abs(got["ratio"] - 1.0) < 1e-4
     monkeypatch.setenv("LD_PRELOAD", "/opt/rocm/lib/librocprofiler-sdk-tool.so")
     assert bench.live_pmc_traffic(seconds=30) is None
+
+
+def test_clock_sampler_reads_this_gpus_card(tmp_path):
+    """The sustained leg's clock samples come from the DRM card at this GPU's
+    PCI address, not from the busiest card (a node's other GPUs may run other
+    jobs at 100%)."""
+    sys.path.insert(0, ROOT)
+    import time
+    import bench
+    for card, bdf, busy, sclk in (("card0", "0000:05:00.0", 100, 2400), ("card8", "0000:75:00.0", 40, 2100)):
+        dev = tmp_path / "pci" / bdf
+        dev.mkdir(parents=True)
+        (dev / "gpu_busy_percent").write_text(f"{busy}\n")
+        (dev / "pp_dpm_sclk").write_text(f"0: 500Mhz\n1: {sclk}Mhz *\n")
+        (dev / "pp_dpm_mclk").write_text("0: 900Mhz\n1: 2000Mhz *\n")
+        (tmp_path / card).mkdir()
+        os.symlink(dev, tmp_path / card / "device")
+    s = bench.ClockSampler(period=0.01, pci="0000:75:00.", root=str(tmp_path))
+    s.start()
+    time.sleep(0.1)
+    r = s.stop()
+    assert r["card"] == "card8" and r["card_pci"] == "0000:75:00.0" and r["sclk_mhz_median"] == 2100
+    assert r["card_choice"].startswith("this GPU")
+    s = bench.ClockSampler(period=0.01, pci=None, root=str(tmp_path))
+    s.start()
+    time.sleep(0.1)
+    r = s.stop()
+    assert r["card"] == "card0" and r["card_choice"].startswith("busiest")
