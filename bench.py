@@ -67,6 +67,8 @@ def parse(argv=None):
     ap.add_argument("--sustained-seconds", type=float, default=5.0, help="back-to-back encode leg length")
     ap.add_argument("--cfg3-stripes", type=int, default=CFG3_STRIPES,
                     help="global stripe count of the strong-scaled 10+4 x 4 MiB leg")
+    ap.add_argument("--leg-warm-s", type=float, default=LEG_WARM_S,
+                    help="seconds of back-to-back untimed calls before each extra leg's timed region")
     ap.add_argument("--no-extras", action="store_true", help="headline only")
     ap.add_argument("--launch-probe", action="store_true",
                     help="launcher self-test: ranks join the process group on CPU (gloo) and report, no GPU work")
@@ -109,6 +111,8 @@ def launch_ranks(args, argv) -> int:
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
+    global LEG_WARM_S
+    LEG_WARM_S = args.leg_warm_s
     if args.gpus < 1:
         print("bench.py: --gpus must be >= 1", file=sys.stderr)
         return 2
@@ -144,6 +148,22 @@ def launch_probe(args) -> int:
 # ---------------------------------------------------------------------------
 # Timing helpers
 # ---------------------------------------------------------------------------
+LEG_WARM_S = 0.6  # --leg-warm-s
+
+
+def warm(torch, fn):
+    """Untimed calls before a leg's timed region: at least 3, and back to back
+    (synchronised every 4 calls) for at least LEG_WARM_S seconds."""
+    fn()
+    torch.cuda.synchronize()
+    t0, n = time.perf_counter(), 0
+    while n < 2 or time.perf_counter() - t0 < LEG_WARM_S:
+        for _ in range(4):
+            fn()
+        torch.cuda.synchronize()
+        n += 4
+
+
 def timed(torch, stream, fn, iters):
     """Average seconds per call of fn on this GPU alone (HIP events)."""
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -151,14 +171,11 @@ def timed(torch, stream, fn, iters):
     # the GPU has idled and needs some tens of ms of load before it runs at its
     # steady rate (a 10+4 masked leg read 0.64-0.68 of peak over its first ~8
     # calls, then 0.71-0.75 per call: profiles/r1/masked/masked_per_call.txt).
-    # So warm up for at least 3 calls AND 50 ms.
-    fn()
-    torch.cuda.synchronize()
-    t0, n = time.perf_counter(), 0
-    while n < 2 or time.perf_counter() - t0 < 0.05:
-        fn()
-        torch.cuda.synchronize()
-        n += 1
+    # From idle the memory system itself ramps too: the headline encode reads
+    # 0.76, 0.805, then a steady 0.826-0.829 of peak over its first ~0.5 s of
+    # load at constant clocks (profiles/r2/ab/clock_state_r2aj.txt).  So warm
+    # up for at least 3 calls AND LEG_WARM_S seconds of back-to-back calls.
+    warm(torch, fn)
     s.record(stream)
     for _ in range(iters):
         fn()
@@ -171,13 +188,7 @@ def timed_all_ranks(torch, parallel, r, fn, iters):
     """Seconds per call with every rank calling fn at once: warm-up as in
     timed(), then barrier + synchronize on both sides of `iters` calls; the
     slowest rank's time."""
-    fn()
-    torch.cuda.synchronize()
-    t0, n = time.perf_counter(), 0
-    while n < 2 or time.perf_counter() - t0 < 0.05:
-        fn()
-        torch.cuda.synchronize()
-        n += 1
+    warm(torch, fn)
     parallel.barrier(r)
     t0 = time.perf_counter()
     for _ in range(iters):
