@@ -126,7 +126,11 @@ def main(argv=None):
     if args.launch_probe:
         return launch_probe(args)
     live = None
-    if not (args.no_extras or args.no_live_pmc) and (args.k, args.m, args.shard_bytes, args.stripes) == (4, 2, 1 << 20, 4096):
+    # The live passes profile one process on cuda:0, so they run at N = 1 only:
+    # at N > 1 every rank would start its own pair at once, all on GPU 0 (the
+    # line then cites the committed summary of the same kernel and batch).
+    if (not (args.no_extras or args.no_live_pmc) and args.gpus == 1
+            and (args.k, args.m, args.shard_bytes, args.stripes) == (4, 2, 1 << 20, 4096)):
         live = live_pmc_traffic()  # before this process touches the GPU: the passes are children
     run(args, live)
     return 0

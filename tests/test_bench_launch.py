@@ -122,3 +122,24 @@ def test_clock_sampler_reads_this_gpus_card(tmp_path):
     time.sleep(0.1)
     r = s.stop()
     assert r["card"] == "card0" and r["card_choice"].startswith("busiest")
+
+
+def test_live_pmc_only_at_one_gpu(monkeypatch):
+    """The live PMC passes profile cuda:0 from child processes, so a rank of an
+    N > 1 run (WORLD_SIZE set by the driver's launcher) must not start them --
+    every rank would profile GPU 0 at once.  At N = 1 they run, before run()."""
+    sys.path.insert(0, ROOT)
+    import bench
+    calls = []
+    monkeypatch.setattr(bench, "live_pmc_traffic", lambda: calls.append("pmc") or {"hbm_bytes_per_launch": 1})
+    monkeypatch.setattr(bench, "run", lambda args, live=None: calls.append(("run", args.gpus, live)))
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(v, raising=False)
+    assert bench.main(["--gpus", "1"]) == 0
+    assert calls == ["pmc", ("run", 1, {"hbm_bytes_per_launch": 1})]
+    calls.clear()
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("RANK", "1")
+    monkeypatch.setenv("LOCAL_RANK", "1")
+    assert bench.main(["--gpus", "2"]) == 0
+    assert calls == [("run", 2, None)]
