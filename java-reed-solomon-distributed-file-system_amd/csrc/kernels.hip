@@ -100,13 +100,27 @@ __device__ __forceinline__ u32x4 load_stream(const uint8_t *p) {
     return __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
 }
 
+// Streaming store of one 16-byte vector.  RSAMD_STORE_SC1=1 (A/B builds)
+// adds the sc1 bit to the non-temporal store (global_store_dwordx4 ... sc1 nt).
+// The stores come after every load of the kernel, so the inline asm cannot
+// upset the compiler's vmcnt bookkeeping for a later load.
+#ifndef RSAMD_STORE_SC1
+#define RSAMD_STORE_SC1 0
+#endif
+__device__ __forceinline__ void store_stream(uint8_t *p, const u32x4 &v) {
+    if (RSAMD_STORE_SC1)
+        asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+    else
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
+}
+
 template <bool VERIFY>
 __device__ __forceinline__ void emit(uint8_t *p, const u32x4 &v, int *mismatch) {
     if (VERIFY) {
         const u32x4 have = load_stream(p);
         if (have[0] != v[0] || have[1] != v[1] || have[2] != v[2] || have[3] != v[3]) flag_mismatch(mismatch);
     } else {
-        __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
+        store_stream(p, v);
     }
 }
 
@@ -384,7 +398,7 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(RSAM
     for (int p = 0; p < MS; ++p) asm volatile("" : "+v"(acc[p]));
 #pragma unroll
     for (int p = 0; p < MS; ++p)
-        if (p < nout) __builtin_nontemporal_store(acc[p], reinterpret_cast<u32x4 *>(sb + out_off[p]));
+        if (p < nout) store_stream(sb + out_off[p], acc[p]);
 }
 
 template <int MS>
@@ -431,7 +445,7 @@ __global__ void __launch_bounds__(kWave) gf_masked_generic_kernel(MaskedArgs a) 
     }
 #pragma unroll
     for (int p = 0; p < MS; ++p)
-        if (p < nout) __builtin_nontemporal_store(acc[p], reinterpret_cast<u32x4 *>(sb + out_off[p]));
+        if (p < nout) store_stream(sb + out_off[p], acc[p]);
 }
 
 // Masked byte kernel: any alignment, and the <16-byte tails.
