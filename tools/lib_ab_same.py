@@ -6,13 +6,14 @@ the pool comes from the first one's rs_dev_alloc (contiguous), and the
 builds take turns on it.  Prints one JSON line per repetition with the
 fraction of 8 TB/s per (shape, build).
   python tools/lib_ab_same.py LIB [LIB ...] [--reps N]
-Shapes: 4+2 x 1 MiB x 4096 encode (the headline), 10+4 x 4 MiB x 128 encode
+Shapes: 4+2 x 1 MiB x 4096 encode (the headline) and decode {0}, 10+4 x 4 MiB x 128 encode
 and decode {0,1,2,3} and verify, 10+4 x 4 MiB x 1024 encode."""
 import ctypes as C
 import json
 import sys
 
 SHAPES = [("4p2_1MiB_x4096_enc", 4, 2, 1 << 20, 4096, None),
+          ("4p2_1MiB_x4096_dec0", 4, 2, 1 << 20, 4096, (0,)),
           ("10p4_4MiB_x128_enc", 10, 4, 4 << 20, 128, None),
           ("10p4_4MiB_x128_dec0123", 10, 4, 4 << 20, 128, (0, 1, 2, 3)),
           ("10p4_4MiB_x128_verify", 10, 4, 4 << 20, 128, "verify"),
