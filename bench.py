@@ -63,6 +63,9 @@ def parse(argv=None):
     ap.add_argument("--shard-bytes", type=int, default=1 << 20)
     ap.add_argument("--stripes", type=int, default=4096, help="stripes per GPU")
     ap.add_argument("--pad", type=int, default=0, help="bytes of padding between shards (layout A/B only)")
+    ap.add_argument("--layout", choices=["packed", "granule"], default="packed",
+                    help="HBM layout of the headline batch: packed shards (default) or the granule layout "
+                         "(include/rs_amd.h; the same stripes and bytes, reported in extra.granule_* too)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline sample budget (headline config)")
     ap.add_argument("--sustained-seconds", type=float, default=5.0, help="back-to-back encode leg length")
     ap.add_argument("--cfg3-stripes", type=int, default=CFG3_STRIPES,
@@ -129,7 +132,7 @@ def main(argv=None):
     # The live passes profile one process on cuda:0, so they run at N = 1 only:
     # at N > 1 every rank would start its own pair at once, all on GPU 0 (the
     # line then cites the committed summary of the same kernel and batch).
-    if (not (args.no_extras or args.no_live_pmc) and args.gpus == 1
+    if (not (args.no_extras or args.no_live_pmc) and args.gpus == 1 and args.layout == "packed"
             and (args.k, args.m, args.shard_bytes, args.stripes) == (4, 2, 1 << 20, 4096)):
         live = live_pmc_traffic()  # before this process touches the GPU: the passes are children
     run(args, live)
@@ -221,7 +224,8 @@ def run(args, live_traffic=None):
     stripe0, count = parallel.stripe_partition(B * world, world, rank)
     assert count == B
     rs = rsamd.ReedSolomon.create(k, m)
-    lay = StripeLayout.packed(B, k + m, S, pad=args.pad)
+    lay = (StripeLayout.packed(B, k + m, S, pad=args.pad) if args.layout == "packed"
+           else rdev.GranuleLayout.make(B, k + m, S))
     buf = stripe_pool(torch, rdev, lay.nbytes, dev, args.alloc)
     stream = torch.cuda.current_stream()
     rdev.fill_synthetic(buf.data_ptr(), k, lay, SEED, stripe0=stripe0, stream=stream)
@@ -270,6 +274,7 @@ def run(args, live_traffic=None):
         extra.update(cfg3_strong(torch, rsamd, parallel, r, rdev, dev, stream, args.cfg3_stripes, args.steps))
         if world == 1:
             extra.update(other_configs(torch, rsamd, rdev, dev, stream))
+            extra.update(granule_legs(torch, rsamd, rdev, dev, stream))
             extra.update(layout_legs(torch, rsamd, dev, stream))
             cpu = cpu_baseline(k, m, S, args.cpu_seconds)
             extra["cpu_configs"] = cpu_configs()
@@ -301,6 +306,8 @@ def run(args, live_traffic=None):
                 "k": k, "m": m, "shard_bytes": S, "stripes_per_gpu": B, "global_stripes": B * world,
                 "parallelism": f"stripe-partitioned x{world} (no collective; {r.backend} only for timing)",
                 "hbm_alloc": alloc_note(buf_alloc),
+                "hbm_layout": ("packed shards" if args.layout == "packed"
+                               else f"granule layout, {lay.granule // 1024} KiB granules"),
             },
             "verified": ok,
             "roofline": {
@@ -519,8 +526,58 @@ def cfg3_strong(torch, rsamd, parallel, r, rdev, dev, stream, total, iters):
     flag = torch.zeros(1, dtype=torch.int32, device=dev)
     rdev.verify(rs, base, lay, flag.data_ptr(), stream)
     out["cfg3_strong_verified"] = parallel.all_ranks_true(r, int(flag.item()) == 0)
+    # the same stripes in the granule layout, on the same pool
+    glay = rdev.GranuleLayout.make(count, k + m, S)
+    rdev.fill_synthetic(base, k, glay, SEED, start, stream)
+    tag = f"cfg3_strong_granule{glay.granule // 1024}K"
+    t = timed_all_ranks(torch, parallel, r, lambda: rdev.encode(rs, base, glay, stream), n)
+    out[tag + "_encode_GiBps"] = round(k * S * total / t / 2**30, 2)
+    out[tag + "_encode_hbm_frac_per_gpu"] = round((k + m) * S * most / t / 1e9 / HBM_PEAK_GBPS, 4)
+    t = timed_all_ranks(torch, parallel, r, lambda: rdev.decode(rs, base, present, glay, stream), n)
+    out[tag + "_decode_0_1_2_3_GiBps"] = round(k * S * total / t / 2**30, 2)
+    out[tag + "_decode_hbm_frac_per_gpu"] = round((k + len(miss)) * S * most / t / 1e9 / HBM_PEAK_GBPS, 4)
+    rdev.fill_synthetic(base, len(miss), glay, SEED ^ 0xBAD, 0, stream)
+    rdev.decode(rs, base, present, glay, stream)
+    flag.zero_()
+    rdev.verify(rs, base, glay, flag.data_ptr(), stream)
+    out[tag + "_verified"] = parallel.all_ranks_true(r, int(flag.item()) == 0)
     pool.free()
     torch.cuda.empty_cache()
+    return out
+
+
+def granule_legs(torch, rsamd, rdev, dev, stream):
+    """The same stripes in the granule layout (include/rs_amd.h, DESIGN.md
+    3.6): the headline batch (4+2 x 1 MiB x 4096, 64 KiB granules) and
+    config[3]'s per-GPU share (10+4 x 4 MiB x 128, 32 KiB granules), each on a
+    contiguous pool: encode, decode, verify; then the erased shards are
+    overwritten, decoded and the batch verified."""
+    out = {}
+    for name, k, m, S, B, miss in [("granule_4p2_1MiB_x4096", 4, 2, 1 << 20, 4096, (0, 1)),
+                                   ("granule_10p4_4MiB_x128", 10, 4, 4 << 20, 128, (0, 1, 2, 3))]:
+        rs = rsamd.ReedSolomon.create(k, m)
+        lay = rdev.GranuleLayout.make(B, k + m, S)
+        pool = rdev.DeviceBuffer(lay.nbytes, contiguous=True)
+        base = pool.data_ptr()
+        rdev.fill_synthetic(base, k, lay, SEED, 0, stream)
+        out[name + "_granule_bytes"] = lay.granule
+        t = timed(torch, stream, lambda: rdev.encode(rs, base, lay, stream), 10)
+        out[name + "_encode_GiBps"] = round(k * S * B / t / 2**30, 2)
+        out[name + "_encode_hbm_frac"] = round((k + m) * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
+        present = [i not in miss for i in range(k + m)]
+        t = timed(torch, stream, lambda: rdev.decode(rs, base, present, lay, stream), 10)
+        out[name + "_decode_" + "_".join(map(str, miss)) + "_GiBps"] = round(k * S * B / t / 2**30, 2)
+        out[name + "_decode_hbm_frac"] = round((k + len(miss)) * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
+        flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        t = timed(torch, stream, lambda: rdev.verify(rs, base, lay, flag.data_ptr(), stream), 5)
+        out[name + "_verify_hbm_frac"] = round((k + m) * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
+        rdev.fill_synthetic(base, len(miss), lay, SEED ^ 0xBAD, 0, stream)  # overwrite the erased shards
+        rdev.decode(rs, base, present, lay, stream)
+        flag.zero_()
+        rdev.verify(rs, base, lay, flag.data_ptr(), stream)
+        out[name + "_verified"] = int(flag.item()) == 0
+        pool.free()
+        torch.cuda.empty_cache()
     return out
 
 

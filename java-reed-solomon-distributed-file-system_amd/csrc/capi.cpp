@@ -907,6 +907,36 @@ int rs_debug_xornet(int mode) {
     return rsamd::xornet_compiled_count();
 }
 
+size_t rs_granule_recommended(int total_shards) {
+    if (total_shards < 1) return 0;
+    size_t g = size_t(1) << 20;
+    while (g > 4096 && size_t(total_shards) * g > (size_t(512) << 10)) g >>= 1;
+    return g;
+}
+
+int rs_granule_copy_shard(uint8_t *dev_base, size_t stripe_stride, int total_shards, size_t shard_len,
+                          size_t granule, size_t stripe, int shard, void *buf, int to_granules, void *stream) {
+    if (!dev_base || !buf) return fail(RS_E_INVALID, "NULL pointer");
+    if (total_shards < 1 || shard < 0 || shard >= total_shards)
+        return fail(RS_E_INVALID, "shard " + std::to_string(shard) + " outside [0, " + std::to_string(total_shards) + ")");
+    if (granule == 0 || shard_len % granule != 0)
+        return fail(RS_E_INVALID, "shard_len " + std::to_string(shard_len) + " is not a multiple of the granule " +
+                                      std::to_string(granule));
+    if (stripe_stride < size_t(total_shards) * shard_len)
+        return fail(RS_E_INVALID, "stripe_stride smaller than total_shards * shard_len");
+    if (shard_len == 0) return RS_OK;
+    int rc = need_device();
+    if (rc) return rc;
+    uint8_t *g0 = dev_base + stripe * stripe_stride + size_t(shard) * granule;
+    const size_t pitch = size_t(total_shards) * granule, rows = shard_len / granule;
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    if (to_granules)
+        RS_HIP(hipMemcpy2DAsync(g0, pitch, buf, granule, granule, rows, hipMemcpyDefault, st));
+    else
+        RS_HIP(hipMemcpy2DAsync(buf, granule, g0, pitch, granule, rows, hipMemcpyDefault, st));
+    return RS_OK;
+}
+
 int rs_copy_dev(uint8_t *dst, const uint8_t *src, size_t n, void *stream) {
     if ((!dst || !src) && n) return fail(RS_E_INVALID, "NULL pointer");
     RS_HIP(rsamd::launch_copy(dst, src, n, static_cast<hipStream_t>(stream)));

@@ -38,6 +38,68 @@ class StripeLayout:
         return self.n_stripes * self.stripe_stride
 
 
+def recommended_granule(total_shards: int) -> int:
+    """rs_granule_recommended: the granule measured fastest for stripes of
+    total_shards shards (4+2: 64 KiB, 10+4: 32 KiB)."""
+    return int(_lib.load().rs_granule_recommended(total_shards))
+
+
+@dataclass(frozen=True)
+class GranuleLayout:
+    """The granule layout of a stripe batch in HBM (include/rs_amd.h): the
+    shards of a stripe are cut into `granule`-byte pieces and piece g of every
+    shard is stored together, so byte c of shard s of stripe t lives at
+        t*stripe_stride + (c // granule)*total_shards*granule + s*granule + c % granule
+    with stripe_stride = total_shards*shard_len.  Byte for byte that is the
+    packed batch `view` of n_stripes*shard_len/granule stripes of
+    granule-byte shards, which the batch entry points code unchanged.  It puts
+    a stripe's k+m streams `granule` bytes apart instead of shard_len
+    (DESIGN.md 3.6).  Use make() to validate and pick the granule."""
+
+    n_stripes: int
+    total_shards: int
+    shard_len: int
+    granule: int
+
+    @staticmethod
+    def make(n_stripes: int, total_shards: int, shard_len: int, granule: int = 0) -> "GranuleLayout":
+        g = granule or recommended_granule(total_shards)
+        if g <= 0 or g % 16 or shard_len % g:
+            raise ValueError(f"shard_len {shard_len} must be a multiple of the granule {g} (itself a multiple of 16)")
+        return GranuleLayout(n_stripes, total_shards, shard_len, g)
+
+    @property
+    def subs_per_stripe(self) -> int:
+        return self.shard_len // self.granule
+
+    @property
+    def stripe_stride(self) -> int:
+        return self.total_shards * self.shard_len
+
+    @property
+    def nbytes(self) -> int:
+        return self.n_stripes * self.stripe_stride
+
+    @property
+    def view(self) -> StripeLayout:
+        """The packed batch of granule-byte sub-stripes with the same bytes."""
+        g = self.granule
+        return StripeLayout(self.n_stripes * self.subs_per_stripe, g, g, self.total_shards * g)
+
+
+def _kernel_layout(lay) -> StripeLayout:
+    return lay.view if isinstance(lay, GranuleLayout) else lay
+
+
+def copy_shard(lay: GranuleLayout, dev_base: int, stripe: int, shard: int, buf: int, to_granules: bool,
+               stream=None) -> None:
+    """rs_granule_copy_shard: one shard between a contiguous buffer `buf`
+    (host or device address, shard_len bytes) and the granule batch."""
+    check(_lib.load().rs_granule_copy_shard(C.c_void_p(dev_base), lay.stripe_stride, lay.total_shards,
+                                            lay.shard_len, lay.granule, stripe, shard, C.c_void_p(buf),
+                                            int(bool(to_granules)), C.c_void_p(_stream_handle(stream))))
+
+
 def _stream_handle(stream) -> int:
     if stream is None:
         return 0
@@ -47,11 +109,13 @@ def _stream_handle(stream) -> int:
 
 
 def encode(codec: ReedSolomon, dev_base: int, lay: StripeLayout, stream=None) -> None:
+    lay = _kernel_layout(lay)
     check(_lib.load().rs_encode_batch_dev(codec.handle, C.c_void_p(dev_base), lay.n_stripes, lay.shard_len,
                                           lay.shard_stride, lay.stripe_stride, C.c_void_p(_stream_handle(stream))))
 
 
 def decode(codec: ReedSolomon, dev_base: int, present: Sequence, lay: StripeLayout, stream=None) -> None:
+    lay = _kernel_layout(lay)
     p = _bools(present)
     check(_lib.load().rs_decode_batch_dev(codec.handle, C.c_void_p(dev_base), p.ctypes.data_as(_lib.u8p),
                                           lay.n_stripes, lay.shard_len, lay.shard_stride, lay.stripe_stride,
@@ -60,10 +124,16 @@ def decode(codec: ReedSolomon, dev_base: int, present: Sequence, lay: StripeLayo
 
 def decode_masked(codec: ReedSolomon, dev_base: int, present, lay: StripeLayout, stream=None) -> None:
     """Per-stripe presence patterns: present is (n_stripes, k+m) of bools/0-1
-    (a C-contiguous bool or uint8 array is passed without a copy)."""
+    (a C-contiguous bool or uint8 array is passed without a copy).  For a
+    GranuleLayout each stripe's row is repeated for its sub-stripes."""
     p = present if isinstance(present, np.ndarray) and present.dtype in (np.bool_, np.uint8) else \
         np.asarray(present, dtype=bool)
     p = np.ascontiguousarray(p).view(np.uint8)
+    if isinstance(lay, GranuleLayout):
+        if p.ndim != 2 or p.shape[0] != lay.n_stripes:
+            raise ValueError(f"present must have {lay.n_stripes} rows, got {p.shape}")
+        p = np.repeat(p, lay.subs_per_stripe, axis=0)
+        lay = lay.view
     if p.ndim != 2 or p.shape[0] != lay.n_stripes or p.shape[1] != codec.getTotalShardCount():
         raise ValueError(f"present must be ({lay.n_stripes}, {codec.getTotalShardCount()}), got {p.shape}")
     check(_lib.load().rs_decode_batch_masked_dev(codec.handle, C.c_void_p(dev_base), p.ctypes.data_as(_lib.u8p),
@@ -75,7 +145,11 @@ def decode_masked_bits(codec: ReedSolomon, dev_base: int, dev_bits: int, lay: St
                        stream=None) -> None:
     """Per-stripe presence bitmasks already in device memory: dev_bits points
     at n_stripes uint32 words, bit i = shard i present.  Undecodable stripes
-    are skipped and counted into the device int32 at dev_bad (when given)."""
+    are skipped and counted into the device int32 at dev_bad (when given).
+    For a GranuleLayout dev_bits holds one word per sub-stripe of its view
+    (n_stripes * subs_per_stripe words; an undecodable stripe then counts once
+    per sub-stripe)."""
+    lay = _kernel_layout(lay)
     check(_lib.load().rs_decode_batch_masked_bits_dev(codec.handle, C.c_void_p(dev_base), C.c_void_p(dev_bits),
                                                       lay.n_stripes, lay.shard_len, lay.shard_stride,
                                                       lay.stripe_stride, C.c_void_p(dev_bad or None),
@@ -89,6 +163,7 @@ def presence_bits(present) -> np.ndarray:
 
 
 def verify(codec: ReedSolomon, dev_base: int, lay: StripeLayout, dev_flag: int, stream=None) -> None:
+    lay = _kernel_layout(lay)
     check(_lib.load().rs_verify_batch_dev(codec.handle, C.c_void_p(dev_base), lay.n_stripes, lay.shard_len,
                                           lay.shard_stride, lay.stripe_stride, C.c_void_p(dev_flag),
                                           C.c_void_p(_stream_handle(stream))))
@@ -96,6 +171,11 @@ def verify(codec: ReedSolomon, dev_base: int, lay: StripeLayout, dev_flag: int, 
 
 def fill_synthetic(dev_base: int, data_shards: int, lay: StripeLayout, seed: int, stripe0: int = 0,
                    stream=None) -> None:
+    """Synthetic data shards; for a GranuleLayout the bytes are generated per
+    sub-stripe of its view (stripe0 counts whole stripes)."""
+    if isinstance(lay, GranuleLayout):
+        stripe0 *= lay.subs_per_stripe
+        lay = lay.view
     check(_lib.load().rs_fill_synthetic_dev(C.c_void_p(dev_base), data_shards, lay.n_stripes, lay.shard_len,
                                             lay.shard_stride, lay.stripe_stride, seed, stripe0,
                                             C.c_void_p(_stream_handle(stream))))
@@ -152,7 +232,11 @@ def device_count() -> int:
 
 
 def view_shards(buf: np.ndarray, lay: StripeLayout, total: int) -> np.ndarray:
-    """Host view (n_stripes, total, shard_len) of a host copy of the batch."""
+    """(n_stripes, total, shard_len) shards of a host copy of the batch: a view
+    for a StripeLayout, a gathered copy for a GranuleLayout."""
+    if isinstance(lay, GranuleLayout):
+        v = buf[: lay.nbytes].reshape(lay.n_stripes, lay.subs_per_stripe, total, lay.granule)
+        return np.ascontiguousarray(v.transpose(0, 2, 1, 3)).reshape(lay.n_stripes, total, lay.shard_len)
     v = buf[: lay.nbytes].reshape(lay.n_stripes, lay.stripe_stride)
     v = v[:, : total * lay.shard_stride].reshape(lay.n_stripes, total, lay.shard_stride)
     return v[:, :, : lay.shard_len]

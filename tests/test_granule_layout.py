@@ -1,0 +1,124 @@
+"""CPU tests of the granule layout (include/rs_amd.h).
+
+The layout stores granule g of every shard of a stripe together.  The batch
+entry points code it through its `view`, the packed batch of granule-byte
+sub-stripes with the same bytes.  These tests check, without a GPU:
+  * the view's addresses are exactly the layout's formula;
+  * coding per sub-stripe of the view equals coding the logical stripes (the
+    oracle on both sides; ReedSolomon.java:90-104 codes each byte column
+    independently, so this is exact for encode and decode);
+  * view_shards gathers the logical shards back;
+  * rs_granule_recommended and rs_granule_copy_shard's argument checks.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from oracle import c_ref
+
+
+def _layout(n, total, S, G):
+    from rsamd.device import GranuleLayout
+    return GranuleLayout.make(n, total, S, G)
+
+
+def _to_granules(shards: np.ndarray, G: int) -> np.ndarray:
+    """(n, total, S) logical shards -> flat bytes of the granule layout, by the
+    header's formula: byte c of shard s of stripe t at
+    t*total*S + (c // G)*total*G + s*G + c % G."""
+    n, total, S = shards.shape
+    out = np.zeros(n * total * S, dtype=np.uint8)
+    t, s, c = np.meshgrid(np.arange(n), np.arange(total), np.arange(S), indexing="ij")
+    addr = t * total * S + (c // G) * total * G + s * G + c % G
+    out[addr.reshape(-1)] = shards.reshape(-1)
+    return out
+
+
+def test_recommended_granule():
+    from rsamd.device import recommended_granule
+    assert recommended_granule(6) == 64 << 10      # 4+2
+    assert recommended_granule(14) == 32 << 10     # 10+4
+    assert recommended_granule(20) == 16 << 10     # 17+3
+    assert recommended_granule(3) == 128 << 10
+    assert recommended_granule(1) == 512 << 10
+    assert recommended_granule(256) == 4 << 10     # clamped at 4 KiB
+    assert recommended_granule(0) == 0
+
+
+def test_view_addresses_match_the_formula():
+    from rsamd.device import view_shards
+    rng = np.random.default_rng(3)
+    n, total, S, G = 3, 6, 4096, 1024
+    lay = _layout(n, total, S, G)
+    shards = rng.integers(0, 256, (n, total, S), dtype=np.uint8)
+    flat = _to_granules(shards, G)
+    # the view's sub-stripes: sub-stripe u = t*(S/G) + g holds granule g of every shard of stripe t
+    v = lay.view
+    assert (v.n_stripes, v.shard_len, v.shard_stride, v.stripe_stride) == (n * S // G, G, G, total * G)
+    sub = view_shards(flat, v, total)
+    for t in range(n):
+        for g in range(S // G):
+            np.testing.assert_array_equal(sub[t * (S // G) + g], shards[t, :, g * G:(g + 1) * G])
+    np.testing.assert_array_equal(view_shards(flat, lay, total), shards)
+    assert lay.nbytes == flat.size and lay.stripe_stride == total * S
+
+
+@pytest.mark.parametrize("k,m,S,G", [(4, 2, 8192, 2048), (10, 4, 4096, 1024), (3, 2, 3072, 1024)])
+def test_coding_the_view_equals_coding_the_stripes(k, m, S, G):
+    """Encode and decode per sub-stripe of the view == the oracle on the
+    logical stripes (every byte column is coded on its own)."""
+    from rsamd.device import view_shards
+    rng = np.random.default_rng(k * 100 + m)
+    n, total = 2, k + m
+    lay = _layout(n, total, S, G)
+    codec = c_ref.Codec(k, m)
+    logical = rng.integers(0, 256, (n, total, S), dtype=np.uint8)
+    logical[:, k:, :] = 0
+    want = logical.copy()
+    for t in range(n):
+        sh = [want[t, i] for i in range(total)]
+        codec.encode_parity(sh, 0, S)
+    flat = _to_granules(logical, G)
+    sub = view_shards(flat, lay.view, total).copy()
+    for u in range(sub.shape[0]):
+        sh = [sub[u, i] for i in range(total)]
+        codec.encode_parity(sh, 0, G)
+    got_flat = np.zeros_like(flat)
+    # scatter the coded sub-stripes back through the view's packed addressing
+    got_flat.reshape(sub.shape[0], total, G)[:] = sub
+    np.testing.assert_array_equal(view_shards(got_flat, lay, total), want)
+    # decode: erase data shard 0 and the last parity shard, per sub-stripe
+    present = [i not in (0, total - 1) for i in range(total)]
+    for u in range(sub.shape[0]):
+        sub[u, 0] = 0
+        sub[u, total - 1] = 0
+        sh = [sub[u, i] for i in range(total)]
+        codec.decode_missing(sh, present, 0, G)
+    got_flat.reshape(sub.shape[0], total, G)[:] = sub
+    np.testing.assert_array_equal(view_shards(got_flat, lay, total), want)
+
+
+def test_make_rejects_bad_granules():
+    from rsamd.device import GranuleLayout
+    with pytest.raises(ValueError):
+        GranuleLayout.make(1, 6, 4096, 3000)
+    with pytest.raises(ValueError):
+        GranuleLayout.make(1, 6, 4096, 8)
+    assert GranuleLayout.make(1, 14, 1 << 20).granule == 32 << 10
+
+
+def test_copy_shard_argument_checks(native):
+    """RS_E_INVALID before any HIP call (so these run without a GPU)."""
+    RS_E_INVALID = -10
+    buf = (C.c_uint8 * 64)()
+    base = C.c_void_p(C.addressof(buf))
+    f = native.rs_granule_copy_shard
+    assert f(None, 6 * 4096, 6, 4096, 1024, 0, 0, base, 1, None) == RS_E_INVALID       # NULL base
+    assert f(base, 6 * 4096, 6, 4096, 1024, 0, 0, None, 1, None) == RS_E_INVALID       # NULL buf
+    assert f(base, 6 * 4096, 6, 4096, 1024, 0, 6, base, 1, None) == RS_E_INVALID       # shard out of range
+    assert f(base, 6 * 4096, 6, 4096, 1024, 0, -1, base, 1, None) == RS_E_INVALID
+    assert f(base, 6 * 4096, 6, 4096, 3000, 0, 0, base, 1, None) == RS_E_INVALID       # not a multiple
+    assert b"not a multiple of the granule 3000" in native.rs_last_error_message()
+    assert f(base, 6 * 4096, 6, 4096, 0, 0, 0, base, 1, None) == RS_E_INVALID          # granule 0
+    assert f(base, 6 * 4096 - 1, 6, 4096, 1024, 0, 0, base, 1, None) == RS_E_INVALID   # stride too small
