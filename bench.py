@@ -576,6 +576,26 @@ def granule_legs(torch, rsamd, rdev, dev, stream):
         flag.zero_()
         rdev.verify(rs, base, lay, flag.data_ptr(), stream)
         out[name + "_verified"] = int(flag.item()) == 0
+        if k == 10:
+            # row f2 in the granule layout: 4 random erasures per stripe (the packed leg's
+            # patterns), one bitmask per sub-stripe in HBM, one launch
+            import numpy as np
+            rng = np.random.default_rng(0)
+            pres = np.ones((B, k + m), dtype=bool)
+            for t_ in range(B):
+                pres[t_, rng.choice(k + m, 4, replace=False)] = False
+            bits = torch.from_numpy(np.repeat(rdev.presence_bits(pres), lay.subs_per_stripe).view(np.int32)).to(dev)
+            alg = (k * B + int((~pres).sum())) * S
+            t = timed(torch, stream, lambda: rdev.decode_masked_bits(rs, base, bits.data_ptr(), lay, 0, stream), 5)
+            out[name + "_decode_masked_bits_hbm_frac"] = round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)
+            rdev.fill_synthetic(base, k, lay, SEED, 0, stream)
+            rdev.encode(rs, base, lay, stream)
+            v = pool.tensor().view(B, lay.subs_per_stripe, k + m, lay.granule)
+            v.permute(0, 2, 1, 3)[torch.from_numpy(~pres).to(dev)] = 0x5A  # clobber every absent shard
+            rdev.decode_masked_bits(rs, base, bits.data_ptr(), lay, 0, stream)
+            flag.zero_()
+            rdev.verify(rs, base, lay, flag.data_ptr(), stream)
+            out[name + "_decode_masked_bits_verified"] = int(flag.item()) == 0
         pool.free()
         torch.cuda.empty_cache()
     return out
