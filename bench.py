@@ -548,13 +548,15 @@ def cfg3_strong(torch, rsamd, parallel, r, rdev, dev, stream, total, iters):
 
 def granule_legs(torch, rsamd, rdev, dev, stream):
     """The same stripes in the granule layout (include/rs_amd.h, DESIGN.md
-    3.6): the headline batch (4+2 x 1 MiB x 4096, 64 KiB granules) and
-    config[3]'s per-GPU share (10+4 x 4 MiB x 128, 32 KiB granules), each on a
-    contiguous pool: encode, decode, verify; then the erased shards are
+    3.6): the headline batch (4+2 x 1 MiB x 4096, 64 KiB granules),
+    config[3]'s per-GPU share (10+4 x 4 MiB x 128, 32 KiB granules) and
+    config[4] (4+2 x 4 KiB x 1 M, 16 stripes per 64 KiB granule row), each on
+    a contiguous pool: encode, decode, verify; then the erased shards are
     overwritten, decoded and the batch verified."""
     out = {}
     for name, k, m, S, B, miss in [("granule_4p2_1MiB_x4096", 4, 2, 1 << 20, 4096, (0, 1)),
-                                   ("granule_10p4_4MiB_x128", 10, 4, 4 << 20, 128, (0, 1, 2, 3))]:
+                                   ("granule_10p4_4MiB_x128", 10, 4, 4 << 20, 128, (0, 1, 2, 3)),
+                                   ("granule_4p2_4KiB_x1M", 4, 2, 4096, 1 << 20, (0, 1))]:
         rs = rsamd.ReedSolomon.create(k, m)
         lay = rdev.GranuleLayout.make(B, k + m, S)
         pool = rdev.DeviceBuffer(lay.nbytes, contiguous=True)

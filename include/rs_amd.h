@@ -195,21 +195,25 @@ RS_API int rs_verify_batch_dev(const rs_codec *codec, const uint8_t *dev_base, s
 /* ---------------------------------------------------------------------------
  * Granule layout: an HBM layout for stripe batches (no Java counterpart).
  * Packed, each shard's shard_len bytes are contiguous, so the k+m streams a
- * stripe's coding reads and writes lie shard_len apart (4 MiB for config[3]).
- * In the granule layout a stripe's shards are cut into G-byte granules and
- * granule g of every shard is stored together:
- *     byte c of shard s of stripe t lives at
- *     dev_base + t*stripe_stride + (c / G)*(nshards*G) + s*G + (c % G),
- *     with shard_len % G == 0 and stripe_stride >= nshards*shard_len.
- * With stripe_stride == nshards*shard_len that is, byte for byte, a packed
- * batch of n_stripes*shard_len/G stripes of G-byte shards (shard_stride G,
+ * stripe's coding reads and writes lie shard_len apart (4 MiB for config[3],
+ * 4 KiB for config[4]).  The granule layout lines the batch's byte columns up
+ * -- stripe t's column c is batch column t*shard_len + c -- and stores them in
+ * G-byte granules, granule j of every shard together:
+ *     byte c of shard s of stripe t, with x = t*shard_len + c, lives at
+ *     dev_base + (x / G)*(nshards*G) + s*G + (x % G),
+ * where G divides shard_len (a stripe spans shard_len/G granules) or
+ * shard_len divides G (a granule holds G/shard_len stripes), and G divides
+ * n_stripes*shard_len.  Byte for byte that is a packed batch of
+ * n_stripes*shard_len/G stripes of G-byte shards (shard_stride G,
  * stripe_stride nshards*G).  Coding is per byte column, so every batch entry
  * point above codes a granule batch unchanged through that view: encode,
- * uniform-pattern decode and verify.  (The per-stripe-pattern entry points
- * then take one pattern per G-byte sub-stripe.)  The streams of a stripe now
- * lie G bytes apart, which the HBM serves faster: 10+4 x 4 MiB encode 0.81 of
- * the 8 TB/s peak at G = 32 KiB against 0.70-0.75 packed, 4+2 x 1 MiB 0.84-0.85
- * at G = 64 KiB against 0.83.
+ * uniform-pattern decode and verify.  The per-stripe-pattern entry points
+ * take one pattern per granule row: each stripe's pattern repeated
+ * shard_len/G times when G divides shard_len (stripes sharing a granule row
+ * must share a pattern).  A stripe's streams now lie G bytes apart, which the
+ * HBM serves faster: 10+4 x 4 MiB encode 0.79-0.81 of the 8 TB/s peak at
+ * G = 32 KiB against 0.70-0.75 packed, 4+2 x 1 MiB 0.84-0.85 at G = 64 KiB
+ * against 0.80-0.83.
  * ------------------------------------------------------------------------- */
 
 /* The granule measured fastest for stripes of total_shards shards: the
@@ -217,15 +221,16 @@ RS_API int rs_verify_batch_dev(const rs_codec *codec, const uint8_t *dev_base, s
  * (4+2: 64 KiB, 10+4: 32 KiB).  0 when total_shards < 1. */
 RS_API size_t rs_granule_recommended(int total_shards);
 
-/* Move one shard between a contiguous buffer and a granule batch (one 2-D
- * copy, asynchronous on stream).  to_granules != 0: buf -> shard `shard` of
- * stripe `stripe`; else that shard -> buf.  buf holds shard_len bytes and
- * may be host memory (pinned or pageable) or device memory.  RS_E_INVALID
- * for NULL pointers, granule == 0, shard_len % granule != 0, a shard index
- * outside [0, total_shards) or stripe_stride < total_shards*shard_len. */
-RS_API int rs_granule_copy_shard(uint8_t *dev_base, size_t stripe_stride, int total_shards, size_t shard_len,
-                                 size_t granule, size_t stripe, int shard, void *buf, int to_granules,
-                                 void *stream);
+/* Move one shard between a contiguous buffer and a granule batch
+ * (asynchronous on stream; one 2-D copy of shard_len/G rows when G divides
+ * shard_len, one contiguous run otherwise).  to_granules != 0: buf -> shard
+ * `shard` of stripe `stripe`; else that shard -> buf.  buf holds shard_len
+ * bytes and may be host memory (pinned or pageable) or device memory.
+ * RS_E_INVALID for NULL pointers, shard_len or granule 0, neither of
+ * shard_len and granule dividing the other, or a shard index outside
+ * [0, total_shards). */
+RS_API int rs_granule_copy_shard(uint8_t *dev_base, int total_shards, size_t shard_len, size_t granule,
+                                 size_t stripe, int shard, void *buf, int to_granules, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Client file layout: ReedSolomonEncoder /

@@ -914,26 +914,25 @@ size_t rs_granule_recommended(int total_shards) {
     return g;
 }
 
-int rs_granule_copy_shard(uint8_t *dev_base, size_t stripe_stride, int total_shards, size_t shard_len,
-                          size_t granule, size_t stripe, int shard, void *buf, int to_granules, void *stream) {
+int rs_granule_copy_shard(uint8_t *dev_base, int total_shards, size_t shard_len, size_t granule, size_t stripe,
+                          int shard, void *buf, int to_granules, void *stream) {
     if (!dev_base || !buf) return fail(RS_E_INVALID, "NULL pointer");
     if (total_shards < 1 || shard < 0 || shard >= total_shards)
         return fail(RS_E_INVALID, "shard " + std::to_string(shard) + " outside [0, " + std::to_string(total_shards) + ")");
-    if (granule == 0 || shard_len % granule != 0)
-        return fail(RS_E_INVALID, "shard_len " + std::to_string(shard_len) + " is not a multiple of the granule " +
-                                      std::to_string(granule));
-    if (stripe_stride < size_t(total_shards) * shard_len)
-        return fail(RS_E_INVALID, "stripe_stride smaller than total_shards * shard_len");
-    if (shard_len == 0) return RS_OK;
+    if (granule == 0 || shard_len == 0 || (shard_len % granule != 0 && granule % shard_len != 0))
+        return fail(RS_E_INVALID, "shard_len " + std::to_string(shard_len) + " and the granule " +
+                                      std::to_string(granule) + " must divide one another");
     int rc = need_device();
     if (rc) return rc;
-    uint8_t *g0 = dev_base + stripe * stripe_stride + size_t(shard) * granule;
-    const size_t pitch = size_t(total_shards) * granule, rows = shard_len / granule;
+    // batch column x of the stripe's first byte; granule row x / G, offset x % G
+    const size_t x = stripe * shard_len, pitch = size_t(total_shards) * granule;
+    uint8_t *g0 = dev_base + (x / granule) * pitch + size_t(shard) * granule + x % granule;
+    const size_t width = std::min(shard_len, granule), rows = std::max<size_t>(1, shard_len / granule);
     const hipStream_t st = static_cast<hipStream_t>(stream);
     if (to_granules)
-        RS_HIP(hipMemcpy2DAsync(g0, pitch, buf, granule, granule, rows, hipMemcpyDefault, st));
+        RS_HIP(hipMemcpy2DAsync(g0, pitch, buf, width, width, rows, hipMemcpyDefault, st));
     else
-        RS_HIP(hipMemcpy2DAsync(buf, granule, g0, pitch, granule, rows, hipMemcpyDefault, st));
+        RS_HIP(hipMemcpy2DAsync(buf, width, g0, pitch, width, rows, hipMemcpyDefault, st));
     return RS_OK;
 }
 

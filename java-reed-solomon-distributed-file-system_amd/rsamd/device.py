@@ -47,14 +47,16 @@ def recommended_granule(total_shards: int) -> int:
 @dataclass(frozen=True)
 class GranuleLayout:
     """The granule layout of a stripe batch in HBM (include/rs_amd.h): the
-    shards of a stripe are cut into `granule`-byte pieces and piece g of every
-    shard is stored together, so byte c of shard s of stripe t lives at
-        t*stripe_stride + (c // granule)*total_shards*granule + s*granule + c % granule
-    with stripe_stride = total_shards*shard_len.  Byte for byte that is the
-    packed batch `view` of n_stripes*shard_len/granule stripes of
-    granule-byte shards, which the batch entry points code unchanged.  It puts
-    a stripe's k+m streams `granule` bytes apart instead of shard_len
-    (DESIGN.md 3.6).  Use make() to validate and pick the granule."""
+    batch's byte columns (stripe t's column c is batch column
+    x = t*shard_len + c) are stored in `granule`-byte pieces, piece j of every
+    shard together, so that byte lives at
+        (x // granule)*total_shards*granule + s*granule + x % granule.
+    The granule divides shard_len (a stripe spans several rows) or shard_len
+    divides the granule (a row holds several stripes).  Byte for byte the
+    batch is the packed batch `view` of `rows` stripes of granule-byte shards,
+    which the batch entry points code unchanged.  It puts a stripe's k+m
+    streams `granule` bytes apart instead of shard_len.  Use
+    make() to validate and pick the granule."""
 
     n_stripes: int
     total_shards: int
@@ -64,27 +66,32 @@ class GranuleLayout:
     @staticmethod
     def make(n_stripes: int, total_shards: int, shard_len: int, granule: int = 0) -> "GranuleLayout":
         g = granule or recommended_granule(total_shards)
-        if g <= 0 or g % 16 or shard_len % g:
-            raise ValueError(f"shard_len {shard_len} must be a multiple of the granule {g} (itself a multiple of 16)")
+        if g <= 0 or g % 16 or shard_len <= 0 or (shard_len % g and g % shard_len) or (n_stripes * shard_len) % g:
+            raise ValueError(f"granule {g} (a multiple of 16) and shard_len {shard_len} must divide one another, "
+                             f"and the granule must divide n_stripes * shard_len")
         return GranuleLayout(n_stripes, total_shards, shard_len, g)
 
     @property
+    def rows(self) -> int:
+        """Granule rows of the batch (stripes of the view)."""
+        return self.n_stripes * self.shard_len // self.granule
+
+    @property
     def subs_per_stripe(self) -> int:
+        """Granule rows per stripe (granule <= shard_len)."""
+        if self.shard_len % self.granule:
+            raise ValueError("several stripes share a granule row (shard_len < granule)")
         return self.shard_len // self.granule
 
     @property
-    def stripe_stride(self) -> int:
-        return self.total_shards * self.shard_len
-
-    @property
     def nbytes(self) -> int:
-        return self.n_stripes * self.stripe_stride
+        return self.n_stripes * self.total_shards * self.shard_len
 
     @property
     def view(self) -> StripeLayout:
-        """The packed batch of granule-byte sub-stripes with the same bytes."""
+        """The packed batch of granule-byte stripes with the same bytes."""
         g = self.granule
-        return StripeLayout(self.n_stripes * self.subs_per_stripe, g, g, self.total_shards * g)
+        return StripeLayout(self.rows, g, g, self.total_shards * g)
 
 
 def _kernel_layout(lay) -> StripeLayout:
@@ -95,9 +102,9 @@ def copy_shard(lay: GranuleLayout, dev_base: int, stripe: int, shard: int, buf: 
                stream=None) -> None:
     """rs_granule_copy_shard: one shard between a contiguous buffer `buf`
     (host or device address, shard_len bytes) and the granule batch."""
-    check(_lib.load().rs_granule_copy_shard(C.c_void_p(dev_base), lay.stripe_stride, lay.total_shards,
-                                            lay.shard_len, lay.granule, stripe, shard, C.c_void_p(buf),
-                                            int(bool(to_granules)), C.c_void_p(_stream_handle(stream))))
+    check(_lib.load().rs_granule_copy_shard(C.c_void_p(dev_base), lay.total_shards, lay.shard_len, lay.granule,
+                                            stripe, shard, C.c_void_p(buf), int(bool(to_granules)),
+                                            C.c_void_p(_stream_handle(stream))))
 
 
 def _stream_handle(stream) -> int:
@@ -132,7 +139,14 @@ def decode_masked(codec: ReedSolomon, dev_base: int, present, lay: StripeLayout,
     if isinstance(lay, GranuleLayout):
         if p.ndim != 2 or p.shape[0] != lay.n_stripes:
             raise ValueError(f"present must have {lay.n_stripes} rows, got {p.shape}")
-        p = np.repeat(p, lay.subs_per_stripe, axis=0)
+        if lay.shard_len >= lay.granule:
+            p = np.repeat(p, lay.subs_per_stripe, axis=0)
+        else:  # stripes sharing a granule row must share a pattern
+            per = lay.granule // lay.shard_len
+            g = p.reshape(lay.rows, per, p.shape[1])
+            if not (g == g[:, :1]).all():
+                raise ValueError("stripes that share a granule row need the same presence pattern")
+            p = np.ascontiguousarray(g[:, 0])
         lay = lay.view
     if p.ndim != 2 or p.shape[0] != lay.n_stripes or p.shape[1] != codec.getTotalShardCount():
         raise ValueError(f"present must be ({lay.n_stripes}, {codec.getTotalShardCount()}), got {p.shape}")
@@ -174,7 +188,9 @@ def fill_synthetic(dev_base: int, data_shards: int, lay: StripeLayout, seed: int
     """Synthetic data shards; for a GranuleLayout the bytes are generated per
     sub-stripe of its view (stripe0 counts whole stripes)."""
     if isinstance(lay, GranuleLayout):
-        stripe0 *= lay.subs_per_stripe
+        if (stripe0 * lay.shard_len) % lay.granule:
+            raise ValueError("stripe0 must start a granule row")
+        stripe0 = stripe0 * lay.shard_len // lay.granule
         lay = lay.view
     check(_lib.load().rs_fill_synthetic_dev(C.c_void_p(dev_base), data_shards, lay.n_stripes, lay.shard_len,
                                             lay.shard_stride, lay.stripe_stride, seed, stripe0,
@@ -235,8 +251,12 @@ def view_shards(buf: np.ndarray, lay: StripeLayout, total: int) -> np.ndarray:
     """(n_stripes, total, shard_len) shards of a host copy of the batch: a view
     for a StripeLayout, a gathered copy for a GranuleLayout."""
     if isinstance(lay, GranuleLayout):
-        v = buf[: lay.nbytes].reshape(lay.n_stripes, lay.subs_per_stripe, total, lay.granule)
-        return np.ascontiguousarray(v.transpose(0, 2, 1, 3)).reshape(lay.n_stripes, total, lay.shard_len)
+        S, G = lay.shard_len, lay.granule
+        if S >= G:  # (stripe, row in stripe, shard, G)
+            v = buf[: lay.nbytes].reshape(lay.n_stripes, S // G, total, G).transpose(0, 2, 1, 3)
+        else:       # (row, shard, stripe in row, S)
+            v = buf[: lay.nbytes].reshape(lay.rows, total, G // S, S).transpose(0, 2, 1, 3)
+        return np.ascontiguousarray(v).reshape(lay.n_stripes, total, S)
     v = buf[: lay.nbytes].reshape(lay.n_stripes, lay.stripe_stride)
     v = v[:, : total * lay.shard_stride].reshape(lay.n_stripes, total, lay.shard_stride)
     return v[:, :, : lay.shard_len]

@@ -56,7 +56,8 @@ def _oracle_encode(k, m, shards):
 
 
 @pytest.mark.parametrize("k,m,S,G,n", [(4, 2, 256 << 10, 64 << 10, 6), (10, 4, 128 << 10, 32 << 10, 4),
-                                       (17, 3, 64 << 10, 16 << 10, 3), (4, 2, 48 << 10, 16 << 10, 5)])
+                                       (17, 3, 64 << 10, 16 << 10, 3), (4, 2, 48 << 10, 16 << 10, 5),
+                                       (4, 2, 4 << 10, 64 << 10, 32), (10, 4, 8 << 10, 32 << 10, 8)])
 def test_granule_encode_matches_oracle(gpu, k, m, S, G, n):
     import torch
     import rsamd
@@ -70,13 +71,12 @@ def test_granule_encode_matches_oracle(gpu, k, m, S, G, n):
     device.encode(rs, dev.data_ptr(), lay, torch.cuda.current_stream())
     got = _download(torch, lay, dev, n, k + m)
     np.testing.assert_array_equal(got, _oracle_encode(k, m, shards))
-    # the layout's bytes are the formula's (rs_amd.h): check one sub-stripe directly
+    # the layout's bytes are the formula's (rs_amd.h): the last stripe's last byte column
     flat = dev.cpu().numpy()
-    g = lay.subs_per_stripe - 1
-    t = n - 1
+    t, c = n - 1, S - 1
+    x = t * S + c
     for s in range(k + m):
-        off = t * lay.stripe_stride + g * (k + m) * G + s * G
-        np.testing.assert_array_equal(flat[off:off + G], got[t, s, g * G:(g + 1) * G])
+        assert flat[(x // G) * (k + m) * G + s * G + x % G] == got[t, s, c]
 
 
 @pytest.mark.parametrize("k,m,miss", [(4, 2, (0, 5)), (4, 2, (2, 3)), (10, 4, (0, 1, 2, 3)), (10, 4, (3, 7, 10, 13))])
@@ -123,6 +123,36 @@ def test_granule_per_stripe_patterns(gpu):
     dbits = torch.from_numpy(bits.view(np.int32)).to("cuda:0")
     device.decode_masked_bits(rs, dev.data_ptr(), dbits.data_ptr(), lay, 0, torch.cuda.current_stream())
     np.testing.assert_array_equal(_download(torch, lay, dev, n, k + m), want)
+
+
+def test_granule_small_shards_decode(gpu):
+    """config[4]-style 4 KiB shards, 16 stripes per 64 KiB granule row: {0,1}
+    decode; decode_masked with one pattern per row, and a pattern that
+    differs inside a row is refused."""
+    import torch
+    import rsamd
+    from rsamd import device
+    k, m, S, n = 4, 2, 4 << 10, 64
+    lay = device.GranuleLayout.make(n, k + m, S)
+    assert lay.granule == 64 << 10 and lay.rows == 4
+    want = _oracle_encode(k, m, np.random.default_rng(9).integers(0, 256, (n, k + m, S), dtype=np.uint8))
+    rs = rsamd.ReedSolomon.create(k, m)
+    clobbered = want.copy()
+    clobbered[:, [0, 1], :] = 0x77
+    dev = _upload(torch, lay, clobbered)
+    device.decode(rs, dev.data_ptr(), [False, False, True, True, True, True], lay, torch.cuda.current_stream())
+    np.testing.assert_array_equal(_download(torch, lay, dev, n, k + m), want)
+    present = np.ones((n, k + m), dtype=bool)
+    for row, miss in enumerate([(0,), (2, 5), (), (1, 4)]):
+        present[row * 16:(row + 1) * 16, list(miss)] = False
+    clobbered = want.copy()
+    clobbered[~present] = 0x11
+    dev = _upload(torch, lay, clobbered)
+    device.decode_masked(rs, dev.data_ptr(), present, lay, torch.cuda.current_stream())
+    np.testing.assert_array_equal(_download(torch, lay, dev, n, k + m), want)
+    present[3, 3] = False  # one stripe of row 0 differs from its row
+    with pytest.raises(ValueError):
+        device.decode_masked(rs, dev.data_ptr(), present, lay, torch.cuda.current_stream())
 
 
 def test_granule_verify_flags_one_byte(gpu):

@@ -25,12 +25,13 @@ def _layout(n, total, S, G):
 
 def _to_granules(shards: np.ndarray, G: int) -> np.ndarray:
     """(n, total, S) logical shards -> flat bytes of the granule layout, by the
-    header's formula: byte c of shard s of stripe t at
-    t*total*S + (c // G)*total*G + s*G + c % G."""
+    header's formula: byte c of shard s of stripe t, x = t*S + c, at
+    (x // G)*total*G + s*G + x % G."""
     n, total, S = shards.shape
     out = np.zeros(n * total * S, dtype=np.uint8)
     t, s, c = np.meshgrid(np.arange(n), np.arange(total), np.arange(S), indexing="ij")
-    addr = t * total * S + (c // G) * total * G + s * G + c % G
+    x = t * S + c  # the batch column
+    addr = (x // G) * total * G + s * G + x % G
     out[addr.reshape(-1)] = shards.reshape(-1)
     return out
 
@@ -61,16 +62,36 @@ def test_view_addresses_match_the_formula():
         for g in range(S // G):
             np.testing.assert_array_equal(sub[t * (S // G) + g], shards[t, :, g * G:(g + 1) * G])
     np.testing.assert_array_equal(view_shards(flat, lay, total), shards)
-    assert lay.nbytes == flat.size and lay.stripe_stride == total * S
+    assert lay.nbytes == flat.size
 
 
-@pytest.mark.parametrize("k,m,S,G", [(4, 2, 8192, 2048), (10, 4, 4096, 1024), (3, 2, 3072, 1024)])
+def test_small_shards_share_a_granule_row():
+    """shard_len < granule: a row holds granule/shard_len whole stripes (config[4]'s 4 KiB shards)."""
+    from rsamd.device import view_shards
+    rng = np.random.default_rng(4)
+    n, total, S, G = 8, 6, 1024, 4096
+    lay = _layout(n, total, S, G)
+    shards = rng.integers(0, 256, (n, total, S), dtype=np.uint8)
+    flat = _to_granules(shards, G)
+    v = lay.view
+    assert (v.n_stripes, v.shard_len, v.shard_stride, v.stripe_stride) == (n * S // G, G, G, total * G)
+    sub = view_shards(flat, v, total)
+    for t in range(n):  # stripe t is columns [(t % 4)*S, +S) of row t // 4
+        np.testing.assert_array_equal(sub[t // 4, :, (t % 4) * S:(t % 4 + 1) * S], shards[t])
+    np.testing.assert_array_equal(view_shards(flat, lay, total), shards)
+    with pytest.raises(ValueError):
+        lay.subs_per_stripe
+
+
+@pytest.mark.parametrize("k,m,S,G", [(4, 2, 8192, 2048), (10, 4, 4096, 1024), (3, 2, 3072, 1024),
+                                     (4, 2, 1024, 4096), (10, 4, 512, 2048)])
 def test_coding_the_view_equals_coding_the_stripes(k, m, S, G):
     """Encode and decode per sub-stripe of the view == the oracle on the
     logical stripes (every byte column is coded on its own)."""
     from rsamd.device import view_shards
     rng = np.random.default_rng(k * 100 + m)
-    n, total = 2, k + m
+    total = k + m
+    n = max(2, 2 * G // S)
     lay = _layout(n, total, S, G)
     codec = c_ref.Codec(k, m)
     logical = rng.integers(0, 256, (n, total, S), dtype=np.uint8)
@@ -105,7 +126,10 @@ def test_make_rejects_bad_granules():
         GranuleLayout.make(1, 6, 4096, 3000)
     with pytest.raises(ValueError):
         GranuleLayout.make(1, 6, 4096, 8)
+    with pytest.raises(ValueError):
+        GranuleLayout.make(3, 6, 1024, 4096)  # 3 stripes of 1 KiB do not fill whole 4 KiB rows
     assert GranuleLayout.make(1, 14, 1 << 20).granule == 32 << 10
+    assert GranuleLayout.make(16, 6, 4096).rows == 1  # 16 x 4 KiB stripes in one 64 KiB row
 
 
 def test_copy_shard_argument_checks(native):
@@ -114,11 +138,11 @@ def test_copy_shard_argument_checks(native):
     buf = (C.c_uint8 * 64)()
     base = C.c_void_p(C.addressof(buf))
     f = native.rs_granule_copy_shard
-    assert f(None, 6 * 4096, 6, 4096, 1024, 0, 0, base, 1, None) == RS_E_INVALID       # NULL base
-    assert f(base, 6 * 4096, 6, 4096, 1024, 0, 0, None, 1, None) == RS_E_INVALID       # NULL buf
-    assert f(base, 6 * 4096, 6, 4096, 1024, 0, 6, base, 1, None) == RS_E_INVALID       # shard out of range
-    assert f(base, 6 * 4096, 6, 4096, 1024, 0, -1, base, 1, None) == RS_E_INVALID
-    assert f(base, 6 * 4096, 6, 4096, 3000, 0, 0, base, 1, None) == RS_E_INVALID       # not a multiple
-    assert b"not a multiple of the granule 3000" in native.rs_last_error_message()
-    assert f(base, 6 * 4096, 6, 4096, 0, 0, 0, base, 1, None) == RS_E_INVALID          # granule 0
-    assert f(base, 6 * 4096 - 1, 6, 4096, 1024, 0, 0, base, 1, None) == RS_E_INVALID   # stride too small
+    assert f(None, 6, 4096, 1024, 0, 0, base, 1, None) == RS_E_INVALID       # NULL base
+    assert f(base, 6, 4096, 1024, 0, 0, None, 1, None) == RS_E_INVALID       # NULL buf
+    assert f(base, 6, 4096, 1024, 0, 6, base, 1, None) == RS_E_INVALID       # shard out of range
+    assert f(base, 6, 4096, 1024, 0, -1, base, 1, None) == RS_E_INVALID
+    assert f(base, 6, 4096, 3000, 0, 0, base, 1, None) == RS_E_INVALID       # neither divides the other
+    assert b"must divide one another" in native.rs_last_error_message()
+    assert f(base, 6, 4096, 0, 0, 0, base, 1, None) == RS_E_INVALID          # granule 0
+    assert f(base, 6, 0, 1024, 0, 0, base, 1, None) == RS_E_INVALID          # shard_len 0
