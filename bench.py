@@ -580,27 +580,64 @@ def granule_legs(torch, rsamd, rdev, dev, stream):
         out[name + "_verified"] = int(flag.item()) == 0
         if k == 10:
             # row f2 in the granule layout: 4 random erasures per stripe (the packed leg's
-            # patterns), one bitmask per sub-stripe in HBM, one launch
+            # patterns), one bitmask per stripe in HBM, one launch
             import numpy as np
             rng = np.random.default_rng(0)
             pres = np.ones((B, k + m), dtype=bool)
             for t_ in range(B):
                 pres[t_, rng.choice(k + m, 4, replace=False)] = False
-            bits = torch.from_numpy(np.repeat(rdev.presence_bits(pres), lay.subs_per_stripe).view(np.int32)).to(dev)
+            bits = torch.from_numpy(rdev.presence_bits(pres).view(np.int32)).to(dev)
             alg = (k * B + int((~pres).sum())) * S
             t = timed(torch, stream, lambda: rdev.decode_masked_bits(rs, base, bits.data_ptr(), lay, 0, stream), 5)
             out[name + "_decode_masked_bits_hbm_frac"] = round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)
             rdev.fill_synthetic(base, k, lay, SEED, 0, stream)
             rdev.encode(rs, base, lay, stream)
-            v = pool.tensor().view(B, lay.subs_per_stripe, k + m, lay.granule)
-            v.permute(0, 2, 1, 3)[torch.from_numpy(~pres).to(dev)] = 0x5A  # clobber every absent shard
+            granule_clobber(torch, pool.tensor(), lay, pres, dev)
             rdev.decode_masked_bits(rs, base, bits.data_ptr(), lay, 0, stream)
             flag.zero_()
             rdev.verify(rs, base, lay, flag.data_ptr(), stream)
             out[name + "_decode_masked_bits_verified"] = int(flag.item()) == 0
+        if S < lay.granule:
+            # row f2 for config[4] in the granule layout: the packed leg's random
+            # pattern per stripe (<= 2 erasures), 16 stripes of different patterns
+            # per granule row, as host flags and as device bitmasks
+            import itertools
+            import numpy as np
+            pats = np.array([[i not in mi for i in range(k + m)] for e in range(3)
+                             for mi in itertools.combinations(range(k + m), e)], dtype=bool)
+            pres = pats[np.random.default_rng(0).integers(0, len(pats), B)]
+            alg = (k * int((~pres).any(axis=1).sum()) + int((~pres).sum())) * S
+            t = timed(torch, stream, lambda: rdev.decode_masked(rs, base, pres, lay, stream), 10)
+            out[name + "_decode_masked_GiBps"] = round(k * S * B / t / 2**30, 2)
+            out[name + "_decode_masked_hbm_frac"] = round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)
+            bits = torch.from_numpy(rdev.presence_bits(pres).view(np.int32)).to(dev)
+            t = timed(torch, stream, lambda: rdev.decode_masked_bits(rs, base, bits.data_ptr(), lay, 0, stream), 5)
+            out[name + "_decode_masked_bits_GiBps"] = round(k * S * B / t / 2**30, 2)
+            out[name + "_decode_masked_bits_hbm_frac"] = round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)
+            for tag, call in (("_decode_masked", lambda: rdev.decode_masked(rs, base, pres, lay, stream)),
+                              ("_decode_masked_bits",
+                               lambda: rdev.decode_masked_bits(rs, base, bits.data_ptr(), lay, 0, stream))):
+                rdev.fill_synthetic(base, k, lay, SEED, 0, stream)
+                rdev.encode(rs, base, lay, stream)
+                granule_clobber(torch, pool.tensor(), lay, pres, dev)
+                call()
+                flag.zero_()
+                rdev.verify(rs, base, lay, flag.data_ptr(), stream)
+                out[name + tag + "_verified"] = int(flag.item()) == 0
         pool.free()
         torch.cuda.empty_cache()
     return out
+
+
+def granule_clobber(torch, buf, lay, present, dev):
+    """clobber() for a GranuleLayout batch: 0x5A over every absent shard."""
+    T, G, S = lay.total_shards, lay.granule, lay.shard_len
+    mask = torch.from_numpy(~present).to(dev)
+    if S >= G:  # (stripe, granule row of the stripe, shard, G) -> index by (stripe, shard)
+        buf.view(lay.n_stripes, S // G, T, G).permute(0, 2, 1, 3)[mask] = 0x5A
+    else:  # (granule row, shard, stripe of the row, S) -> index by (row, stripe of the row, shard)
+        per = G // S
+        buf.view(lay.rows, T, per, S).permute(0, 2, 1, 3)[mask.view(lay.rows, per, T)] = 0x5A
 
 
 def clobber(torch, buf, lay, total_shards, present, dev):

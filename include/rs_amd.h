@@ -207,10 +207,9 @@ RS_API int rs_verify_batch_dev(const rs_codec *codec, const uint8_t *dev_base, s
  * n_stripes*shard_len/G stripes of G-byte shards (shard_stride G,
  * stripe_stride nshards*G).  Coding is per byte column, so every batch entry
  * point above codes a granule batch unchanged through that view: encode,
- * uniform-pattern decode and verify.  The per-stripe-pattern entry points
- * take one pattern per granule row: each stripe's pattern repeated
- * shard_len/G times when G divides shard_len (stripes sharing a granule row
- * must share a pattern).  A stripe's streams now lie G bytes apart, which the
+ * uniform-pattern decode and verify.  Per-stripe presence patterns take
+ * the rs_decode_granule_masked*_dev entry points below (one pattern per
+ * stripe, as the packed ones).  A stripe's streams now lie G bytes apart, which the
  * HBM serves faster: 10+4 x 4 MiB encode 0.79-0.81 of the 8 TB/s peak at
  * G = 32 KiB against 0.70-0.75 packed, 4+2 x 1 MiB 0.84-0.85 at G = 64 KiB
  * against 0.80-0.83.
@@ -220,6 +219,25 @@ RS_API int rs_verify_batch_dev(const rs_codec *codec, const uint8_t *dev_base, s
  * largest power of two G in [4 KiB, 1 MiB] with total_shards*G <= 512 KiB
  * (4+2: 64 KiB, 10+4: 32 KiB).  0 when total_shards < 1. */
 RS_API size_t rs_granule_recommended(int total_shards);
+
+/* rs_decode_batch_masked_dev on a granule batch of n_stripes stripes of
+ * shard_len-byte shards (granule G): present holds n_stripes x (k+m) HOST
+ * flags, one pattern per stripe, as there.  Each kernel block looks its
+ * stripe up from its batch column (stripe = column / shard_len), so the
+ * patterns are not repeated per granule row, and stripes sharing a granule
+ * row (shard_len < G) may differ.  Fast vector path when shard_len and G are
+ * multiples of 1 KiB; other shapes run a byte-granular kernel.  RS_E_INVALID
+ * for a G that neither divides nor is divided by shard_len, or that does not
+ * divide n_stripes*shard_len. */
+RS_API int rs_decode_granule_masked_dev(const rs_codec *codec, uint8_t *dev_base, const uint8_t *present,
+                                        size_t n_stripes, size_t shard_len, size_t granule, void *stream);
+
+/* rs_decode_batch_masked_bits_dev on a granule batch: dev_present_bits[t] is
+ * stripe t's presence bitmask (one per stripe, in HBM); dev_bad_count counts
+ * each undecodable stripe once. */
+RS_API int rs_decode_granule_masked_bits_dev(const rs_codec *codec, uint8_t *dev_base,
+                                             const uint32_t *dev_present_bits, size_t n_stripes, size_t shard_len,
+                                             size_t granule, int32_t *dev_bad_count, void *stream);
 
 /* Move one shard between a contiguous buffer and a granule batch
  * (asynchronous on stream; one 2-D copy of shard_len/G rows when G divides

@@ -393,8 +393,8 @@ int upload_slot(ThreadCtx *ctx, MaskedSlot *sl, size_t bytes, hipStream_t stream
 
 // One launch per output group over the pattern tables; plan_ids holds the
 // stripes' presence bitmasks.
-int launch_pattern_groups(const Codec &c, const rsamd::PatternTables &pt, const Geometry &geo, const int32_t *bits,
-                          int32_t *bad, hipStream_t stream) {
+int launch_pattern_groups(const Codec &c, const rsamd::PatternTables &pt, const Geometry &geo, size_t pattern_bytes,
+                          const int32_t *bits, int32_t *bad, hipStream_t stream) {
     for (int g = 0; g < pt.groups; ++g) {
         rsamd::MaskedPlan mp;
         mp.records = pt.records + size_t(g) * pt.npat * pt.rec_stride;
@@ -405,6 +405,7 @@ int launch_pattern_groups(const Codec &c, const rsamd::PatternTables &pt, const 
         mp.mask_table = pt.mask_table;
         mp.mask_bits = c.total();
         mp.bad = g == 0 ? bad : nullptr;
+        mp.pattern_bytes = pattern_bytes;
         RS_HIP(rsamd::launch_gf_masked(geo, mp, stream));
     }
     return RS_OK;
@@ -462,14 +463,13 @@ int presence_bits(const uint8_t *present, size_t n, int T, int k, const int32_t 
     return rc;
 }
 
-int decode_masked_dev(const Codec &c, uint8_t *base, const uint8_t *present, size_t n_stripes, size_t shard_len,
-                      size_t shard_stride, size_t stripe_stride, hipStream_t stream) {
+// n_stripes presence patterns (rows of present) over the stripes of geo:
+// pattern_bytes 0 -> one per stripe of geo; otherwise geo is the packed view of
+// a granule batch and each pattern covers pattern_bytes batch columns
+// (rsamd::MaskedPlan::pattern_bytes).
+int decode_masked_dev(const Codec &c, const uint8_t *present, size_t n_stripes, const Geometry &geo,
+                      size_t pattern_bytes, hipStream_t stream) {
     const int T = c.total(), k = c.k();
-    if (!present) return fail(RS_E_INVALID, "present must not be NULL");
-    if (n_stripes == 0 || shard_len == 0) return RS_OK;
-    if (!base) return fail(RS_E_INVALID, "NULL device base");
-    if (n_stripes > size_t(INT32_MAX)) return fail(RS_E_INVALID, "too many stripes");
-    const Geometry geo{base, n_stripes, 0, shard_len, shard_stride, stripe_stride};
 
     // Codes with a pattern table: upload the stripes' presence bitmasks, the
     // kernels look their records up (no per-call plan building).
@@ -485,7 +485,8 @@ int decode_masked_dev(const Codec &c, uint8_t *base, const uint8_t *present, siz
         if (rc) return fail(rc, rc == RS_E_SINGULAR ? "Matrix is singular" : "Not enough shards present");
         rc = upload_slot(ctx, sl, n_stripes * sizeof(uint32_t), stream);
         if (rc) return rc;
-        rc = launch_pattern_groups(c, pt, geo, reinterpret_cast<const int32_t *>(sl->dev), nullptr, stream);
+        rc = launch_pattern_groups(c, pt, geo, pattern_bytes, reinterpret_cast<const int32_t *>(sl->dev), nullptr,
+                                   stream);
         if (rc) return rc;
         RS_HIP(hipEventRecord(sl->done, stream));
         return RS_OK;
@@ -538,24 +539,35 @@ int decode_masked_dev(const Codec &c, uint8_t *base, const uint8_t *present, siz
         mp.plan_ids = reinterpret_cast<const int32_t *>(sl->dev + ids_off);
         mp.nin = k;
         mp.mslots = ms;
+        mp.pattern_bytes = pattern_bytes;
         RS_HIP(rsamd::launch_gf_masked(geo, mp, stream));
     }
     RS_HIP(hipEventRecord(sl->done, stream));
     return RS_OK;
 }
 
-int decode_masked_bits_dev(const Codec &c, uint8_t *base, const uint32_t *dev_bits, size_t n_stripes,
-                           size_t shard_len, size_t shard_stride, size_t stripe_stride, int32_t *dev_bad,
-                           hipStream_t stream) {
-    if (n_stripes == 0 || shard_len == 0) return RS_OK;
-    if (!base || !dev_bits) return fail(RS_E_INVALID, "NULL device buffer");
-    if (n_stripes > size_t(INT32_MAX)) return fail(RS_E_INVALID, "too many stripes");
+int decode_masked_bits_dev(const Codec &c, const uint32_t *dev_bits, const Geometry &geo, size_t pattern_bytes,
+                           int32_t *dev_bad, hipStream_t stream) {
+    if (!dev_bits) return fail(RS_E_INVALID, "NULL device buffer");
     rsamd::PatternTables pt;
     std::string err;
     int rc = c.pattern_tables(&pt, &err);
     if (rc) return fail(rc, err);
-    const Geometry geo{base, n_stripes, 0, shard_len, shard_stride, stripe_stride};
-    return launch_pattern_groups(c, pt, geo, reinterpret_cast<const int32_t *>(dev_bits), dev_bad, stream);
+    return launch_pattern_groups(c, pt, geo, pattern_bytes, reinterpret_cast<const int32_t *>(dev_bits), dev_bad,
+                                 stream);
+}
+
+// The packed view of a granule batch (rs_amd.h): n_stripes * shard_len / G
+// stripes of G-byte shards.  RS_OK, or RS_E_INVALID for a bad shape.
+int granule_view(int total_shards, uint8_t *base, size_t n_stripes, size_t shard_len, size_t granule, Geometry *geo) {
+    if (granule == 0 || (shard_len % granule != 0 && granule % shard_len != 0))
+        return fail(RS_E_INVALID, "shard_len " + std::to_string(shard_len) + " and the granule " +
+                                      std::to_string(granule) + " must divide one another");
+    if ((n_stripes * shard_len) % granule != 0)
+        return fail(RS_E_INVALID, "the granule " + std::to_string(granule) + " does not divide the batch's " +
+                                      std::to_string(n_stripes * shard_len) + " columns");
+    *geo = Geometry{base, n_stripes * shard_len / granule, 0, granule, granule, size_t(total_shards) * granule};
+    return RS_OK;
 }
 
 const Codec *impl(const rs_codec *c) { return c ? c->impl : nullptr; }
@@ -714,8 +726,26 @@ int rs_decode_batch_masked_dev(const rs_codec *codec, uint8_t *dev_base, const u
                                size_t shard_len, size_t shard_stride, size_t stripe_stride, void *stream) {
     const Codec *c = impl(codec);
     if (!c) return fail(RS_E_INVALID, "codec is NULL");
-    return decode_masked_dev(*c, dev_base, present, n_stripes, shard_len, shard_stride, stripe_stride,
-                             static_cast<hipStream_t>(stream));
+    if (!present) return fail(RS_E_INVALID, "present must not be NULL");
+    if (n_stripes == 0 || shard_len == 0) return RS_OK;
+    if (!dev_base) return fail(RS_E_INVALID, "NULL device base");
+    if (n_stripes > size_t(INT32_MAX)) return fail(RS_E_INVALID, "too many stripes");
+    const Geometry geo{dev_base, n_stripes, 0, shard_len, shard_stride, stripe_stride};
+    return decode_masked_dev(*c, present, n_stripes, geo, 0, static_cast<hipStream_t>(stream));
+}
+
+int rs_decode_granule_masked_dev(const rs_codec *codec, uint8_t *dev_base, const uint8_t *present, size_t n_stripes,
+                                 size_t shard_len, size_t granule, void *stream) {
+    const Codec *c = impl(codec);
+    if (!c) return fail(RS_E_INVALID, "codec is NULL");
+    if (!present) return fail(RS_E_INVALID, "present must not be NULL");
+    if (n_stripes == 0 || shard_len == 0) return RS_OK;
+    if (!dev_base) return fail(RS_E_INVALID, "NULL device base");
+    if (n_stripes > size_t(INT32_MAX)) return fail(RS_E_INVALID, "too many stripes");
+    Geometry geo;
+    int rc = granule_view(c->total(), dev_base, n_stripes, shard_len, granule, &geo);
+    if (rc) return rc;
+    return decode_masked_dev(*c, present, n_stripes, geo, shard_len, static_cast<hipStream_t>(stream));
 }
 
 int rs_decode_batch_masked_bits_dev(const rs_codec *codec, uint8_t *dev_base, const uint32_t *dev_present_bits,
@@ -723,8 +753,26 @@ int rs_decode_batch_masked_bits_dev(const rs_codec *codec, uint8_t *dev_base, co
                                     int32_t *dev_bad_count, void *stream) {
     const Codec *c = impl(codec);
     if (!c) return fail(RS_E_INVALID, "codec is NULL");
-    return decode_masked_bits_dev(*c, dev_base, dev_present_bits, n_stripes, shard_len, shard_stride, stripe_stride,
-                                  dev_bad_count, static_cast<hipStream_t>(stream));
+    if (n_stripes == 0 || shard_len == 0) return RS_OK;
+    if (!dev_base) return fail(RS_E_INVALID, "NULL device buffer");
+    if (n_stripes > size_t(INT32_MAX)) return fail(RS_E_INVALID, "too many stripes");
+    const Geometry geo{dev_base, n_stripes, 0, shard_len, shard_stride, stripe_stride};
+    return decode_masked_bits_dev(*c, dev_present_bits, geo, 0, dev_bad_count, static_cast<hipStream_t>(stream));
+}
+
+int rs_decode_granule_masked_bits_dev(const rs_codec *codec, uint8_t *dev_base, const uint32_t *dev_present_bits,
+                                      size_t n_stripes, size_t shard_len, size_t granule, int32_t *dev_bad_count,
+                                      void *stream) {
+    const Codec *c = impl(codec);
+    if (!c) return fail(RS_E_INVALID, "codec is NULL");
+    if (n_stripes == 0 || shard_len == 0) return RS_OK;
+    if (!dev_base) return fail(RS_E_INVALID, "NULL device buffer");
+    if (n_stripes > size_t(INT32_MAX)) return fail(RS_E_INVALID, "too many stripes");
+    Geometry geo;
+    int rc = granule_view(c->total(), dev_base, n_stripes, shard_len, granule, &geo);
+    if (rc) return rc;
+    return decode_masked_bits_dev(*c, dev_present_bits, geo, shard_len, dev_bad_count,
+                                  static_cast<hipStream_t>(stream));
 }
 
 int rs_verify_batch_dev(const rs_codec *codec, const uint8_t *dev_base, size_t n_stripes, size_t shard_len,

@@ -340,7 +340,29 @@ struct MaskedArgs {
     const int32_t *mask_table;                   // MaskedPlan::mask_table
     int mask_bits;
     int32_t *bad;
+    // Patterns per logical stripe of a granule batch (MaskedPlan::pattern_bytes):
+    // pat_on != 0 -> the block's pattern is plan_ids[(pat_chunk0 + stripe *
+    // chunks + chunk) / pdiv], its 1 KiB column chunk counted along the batch's
+    // byte columns; plan_ids is then not offset per launch.
+    uint32_t pat_on, pat_chunk0;
+    FastDiv pdiv;
+    uint32_t pat_chunks;  // 1 KiB chunks per logical stripe (pdiv's divisor)
 };
+
+// The plan index of the block at (stripe, chunk) and whether it holds the
+// first column of that pattern's stripe (the one that counts an undecodable
+// stripe).  Block-uniform scalar work.
+template <bool PAT>
+__device__ __forceinline__ uint32_t masked_pattern(const MaskedArgs &a, uint32_t stripe, uint32_t chunk, bool &first) {
+    if (!PAT) {
+        first = chunk == 0;
+        return stripe;
+    }
+    const uint32_t x = a.pat_chunk0 + stripe * a.chunks + chunk;
+    const uint32_t t = fast_div(x, a.pdiv);
+    first = x == t * a.pat_chunks;
+    return t;
+}
 
 // Stripe t's record, or nullptr when its presence bitmask is not decodable.
 // No side effects: the caller counts an undecodable stripe (count_undecodable)
@@ -372,15 +394,26 @@ __device__ __forceinline__ void count_undecodable(int32_t *bad, bool col0) {
 // decode on the same pool (tools/masked_ref_probe.py,
 // profiles/r2/masked_ref_r2af.txt).  The same budget on gf_vec_kernel<10,4>
 // (8 waves, 56 B spilled) cost 9 points (masked_ref_r2ae.txt).
-template <int K, int MS>
+template <int K, int MS, bool PAT>
 __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(RSAMD_MASKED_WAVES, 8))) gf_masked_kernel(MaskedArgs a) {
     uint32_t stripe, chunk;
     block_item(a.chunks, a.cdiv, a.rot, a.xcd_span, stripe, chunk);
     const uint32_t v = chunk * uint32_t(kWave) + threadIdx.x;
-    const uint8_t *rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, stripe);
-    if (!rec) {
-        count_undecodable(a.bad, v == 0);
-        return;
+    const uint8_t *rec;
+    if constexpr (PAT) {
+        bool first;
+        const uint32_t pat = masked_pattern<PAT>(a, stripe, chunk, first);
+        rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, pat);
+        if (!rec) {
+            count_undecodable(a.bad, first && threadIdx.x == 0);
+            return;
+        }
+    } else {
+        rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, stripe);
+        if (!rec) {
+            count_undecodable(a.bad, v == 0);
+            return;
+        }
     }
     const int nout = *reinterpret_cast<const int32_t *>(rec);
     if (nout == 0 || v >= a.nvec) return;
@@ -401,15 +434,26 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(RSAM
         if (p < nout) store_stream(sb + out_off[p], acc[p]);
 }
 
-template <int MS>
+template <int MS, bool PAT>
 __global__ void __launch_bounds__(kWave) gf_masked_generic_kernel(MaskedArgs a) {
     uint32_t stripe, chunk;
     block_item(a.chunks, a.cdiv, a.rot, a.xcd_span, stripe, chunk);
     const uint32_t v = chunk * uint32_t(kWave) + threadIdx.x;
-    const uint8_t *rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, stripe);
-    if (!rec) {
-        count_undecodable(a.bad, v == 0);
-        return;
+    const uint8_t *rec;
+    if constexpr (PAT) {
+        bool first;
+        const uint32_t pat = masked_pattern<PAT>(a, stripe, chunk, first);
+        rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, pat);
+        if (!rec) {
+            count_undecodable(a.bad, first && threadIdx.x == 0);
+            return;
+        }
+    } else {
+        rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, stripe);
+        if (!rec) {
+            count_undecodable(a.bad, v == 0);
+            return;
+        }
     }
     const int nout = *reinterpret_cast<const int32_t *>(rec);
     if (nout == 0 || v >= a.nvec) return;
@@ -460,6 +504,7 @@ struct MaskedByteArgs {
     const int32_t *mask_table;
     int mask_bits;
     int32_t *bad;
+    uint64_t pat_bytes, row_bytes;  // MaskedPlan::pattern_bytes (0: per stripe); the view's full shard length
 };
 
 __global__ void __launch_bounds__(kThreads) gf_masked_byte_kernel(MaskedByteArgs a) {
@@ -467,9 +512,16 @@ __global__ void __launch_bounds__(kThreads) gf_masked_byte_kernel(MaskedByteArgs
     for (uint64_t idx = uint64_t(blockIdx.x) * kThreads + threadIdx.x; idx < a.total; idx += step) {
         const uint64_t stripe = idx / a.ncols;
         const uint64_t col = a.col0 + (idx - stripe * a.ncols);
-        const uint8_t *rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, stripe);
+        uint64_t pat = stripe;
+        bool first = col == 0;
+        if (a.pat_bytes) {
+            const uint64_t x = stripe * a.row_bytes + col;
+            pat = x / a.pat_bytes;
+            first = x == pat * a.pat_bytes;
+        }
+        const uint8_t *rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, pat);
         if (!rec) {
-            count_undecodable(a.bad, col == 0);
+            count_undecodable(a.bad, first);
             continue;
         }
         const int nout = *reinterpret_cast<const int32_t *>(rec);
@@ -675,15 +727,30 @@ hipError_t launch_bytes(const Geometry &g, const DevPlan &p, size_t col0, size_t
     return hipGetLastError();
 }
 
+// PAT (a.pat_on) is a template argument, not a uniform branch.  As a branch
+// in one kernel, the pattern divide changed the 10+4 kernel's register
+// allocation (scratch 20 -> 8 B per lane).  On one pool that build ran packed
+// batches at 0.727 against 0.754 and the granule view at 0.796 against 0.752
+// (tools/masked_ab.py, profiles/r2/ab/masked_ab_r2bc.txt).  As a template,
+// PAT = false compiles to the old kernel instruction for instruction and
+// PAT = true (granule batches, the only callers of pattern_bytes) keeps the
+// faster allocation: 0.78-0.79 against 0.75 for the view with repeated
+// patterns on one pool (masked_ab_r2bd.txt).
 template <int K, int MS>
 hipError_t launch_masked_t(const MaskedArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL((gf_masked_kernel<K, MS>), dim3(a.n_items), dim3(kWave), 0, s, a);
+    if (a.pat_on)
+        hipLaunchKernelGGL((gf_masked_kernel<K, MS, true>), dim3(a.n_items), dim3(kWave), 0, s, a);
+    else
+        hipLaunchKernelGGL((gf_masked_kernel<K, MS, false>), dim3(a.n_items), dim3(kWave), 0, s, a);
     return hipGetLastError();
 }
 
 template <int MS>
 hipError_t launch_masked_generic_t(const MaskedArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL((gf_masked_generic_kernel<MS>), dim3(a.n_items), dim3(kWave), 0, s, a);
+    if (a.pat_on)
+        hipLaunchKernelGGL((gf_masked_generic_kernel<MS, true>), dim3(a.n_items), dim3(kWave), 0, s, a);
+    else
+        hipLaunchKernelGGL((gf_masked_generic_kernel<MS, false>), dim3(a.n_items), dim3(kWave), 0, s, a);
     return hipGetLastError();
 }
 
@@ -719,7 +786,7 @@ hipError_t launch_masked_bytes(const Geometry &g, const MaskedPlan &p, const Mas
                                size_t ncols, hipStream_t s) {
     MaskedByteArgs a{g.base, p.records, p.rec_stride, p.plan_ids, g.stripe_stride, g.shard_stride, col0, ncols,
                      uint64_t(g.n_stripes) * ncols, uint32_t(l.in_idx), uint32_t(l.out_idx), uint32_t(l.tabs),
-                     p.nin, p.mslots, p.mask_table, p.mask_bits, p.bad};
+                     p.nin, p.mslots, p.mask_table, p.mask_bits, p.bad, p.pattern_bytes, g.col0 + g.len};
     if (a.total == 0) return hipSuccess;
     const unsigned grid = unsigned(std::min<uint64_t>((a.total + kThreads - 1) / kThreads, 65536));
     hipLaunchKernelGGL(gf_masked_byte_kernel, dim3(grid), dim3(kThreads), 0, s, a);
@@ -744,19 +811,28 @@ hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t 
     uint8_t *base = g.base + g.col0;
     const bool aligned = (reinterpret_cast<uintptr_t>(base) % 16 == 0) && g.shard_stride % 16 == 0 &&
                          g.stripe_stride % 16 == 0;
-    if (!aligned || g.len / 16 > UINT32_MAX - kWave) return launch_masked_bytes(g, p, l, g.col0, g.len, s);
+    // Patterns per logical stripe: the vector kernels need every 1 KiB chunk
+    // inside one pattern (rows of whole 1 KiB chunks, patterns of whole rows
+    // or of whole chunks) and the batch's chunk count in 32 bits.
+    const size_t chunk_bytes = size_t(kWave) * 16;
+    const size_t pb = p.pattern_bytes;
+    const bool pat_vec = pb == 0 || (g.col0 == 0 && g.len % chunk_bytes == 0 && pb % chunk_bytes == 0 &&
+                                     (pb % g.len == 0 || g.len % pb == 0) &&
+                                     g.n_stripes * (g.len / chunk_bytes) <= UINT32_MAX);
+    if (!aligned || !pat_vec || g.len / 16 > UINT32_MAX - kWave) return launch_masked_bytes(g, p, l, g.col0, g.len, s);
     const uint32_t nvec = uint32_t(g.len / 16);
     if (nvec > 0) {
         const uint32_t chunks = (nvec + kWave - 1) / kWave;
+        const uint32_t pat_chunks = pb ? uint32_t(pb / chunk_bytes) : 1u;
         const size_t stripes_per_launch = std::max<size_t>(1, kMaxGridBlocks / chunks);
         for (size_t t0 = 0; t0 < g.n_stripes; t0 += stripes_per_launch) {
             const size_t nst = std::min(stripes_per_launch, g.n_stripes - t0);
             const BlockOrder o = block_order(chunks, uint32_t(g.stripe_stride / std::max<size_t>(1, g.shard_stride)),
                                              g.shard_stride, uint32_t(nst * chunks));
-            MaskedArgs a{base + t0 * g.stripe_stride, p.records, p.rec_stride, p.plan_ids + t0, g.stripe_stride,
-                         g.shard_stride, nvec, chunks, uint32_t(nst * chunks), o.rot, o.xcd_span,
+            MaskedArgs a{base + t0 * g.stripe_stride, p.records, p.rec_stride, p.plan_ids + (pb ? 0 : t0),
+                         g.stripe_stride, g.shard_stride, nvec, chunks, uint32_t(nst * chunks), o.rot, o.xcd_span,
                          make_fastdiv(chunks), uint32_t(l.in_idx), uint32_t(l.out_idx), uint32_t(l.tabs), p.nin, p.mask_table,
-                         p.mask_bits, p.bad};
+                         p.mask_bits, p.bad, pb ? 1u : 0u, uint32_t(t0 * chunks), make_fastdiv(pat_chunks), pat_chunks};
             hipError_t e = dispatch_masked(a, p.mslots, s);
             if (e != hipSuccess) return e;
         }

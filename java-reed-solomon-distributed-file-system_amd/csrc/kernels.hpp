@@ -66,6 +66,11 @@ struct MaskedPlan {
     const int32_t *mask_table = nullptr;
     int mask_bits = 0;
     int32_t *bad = nullptr;
+    // 0: plan_ids[t] is view stripe t's.  Otherwise the Geometry is the packed
+    // view of a granule batch (rs_amd.h) and plan_ids holds one entry per
+    // logical stripe of pattern_bytes columns: view stripe t's column c belongs
+    // to logical stripe (t * (col0 + len) + c) / pattern_bytes.
+    size_t pattern_bytes = 0;
 };
 
 hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t s);

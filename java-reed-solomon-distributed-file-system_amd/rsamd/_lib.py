@@ -46,6 +46,10 @@ SIGNATURES = {
                                              C.c_size_t, C.c_void_p]),
     "rs_decode_batch_masked_bits_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t,
                                                   C.c_size_t, C.c_size_t, C.c_void_p, C.c_void_p]),
+    "rs_decode_granule_masked_dev": (C.c_int, [C.c_void_p, C.c_void_p, u8p, C.c_size_t, C.c_size_t, C.c_size_t,
+                                               C.c_void_p]),
+    "rs_decode_granule_masked_bits_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t,
+                                                    C.c_size_t, C.c_void_p, C.c_void_p]),
     "rs_verify_batch_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t,
                                       C.c_void_p, C.c_void_p]),
     "rs_file_layout": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),

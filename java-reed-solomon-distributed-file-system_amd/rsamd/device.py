@@ -131,43 +131,39 @@ def decode(codec: ReedSolomon, dev_base: int, present: Sequence, lay: StripeLayo
 
 def decode_masked(codec: ReedSolomon, dev_base: int, present, lay: StripeLayout, stream=None) -> None:
     """Per-stripe presence patterns: present is (n_stripes, k+m) of bools/0-1
-    (a C-contiguous bool or uint8 array is passed without a copy).  For a
-    GranuleLayout each stripe's row is repeated for its sub-stripes."""
+    (a C-contiguous bool or uint8 array is passed without a copy).  A
+    GranuleLayout takes one pattern per stripe too
+    (rs_decode_granule_masked_dev: the kernels find a block's stripe from its
+    batch column, so stripes sharing a granule row may differ)."""
     p = present if isinstance(present, np.ndarray) and present.dtype in (np.bool_, np.uint8) else \
         np.asarray(present, dtype=bool)
     p = np.ascontiguousarray(p).view(np.uint8)
-    if isinstance(lay, GranuleLayout):
-        if p.ndim != 2 or p.shape[0] != lay.n_stripes:
-            raise ValueError(f"present must have {lay.n_stripes} rows, got {p.shape}")
-        if lay.shard_len >= lay.granule:
-            p = np.repeat(p, lay.subs_per_stripe, axis=0)
-        else:  # stripes sharing a granule row must share a pattern
-            per = lay.granule // lay.shard_len
-            g = p.reshape(lay.rows, per, p.shape[1])
-            if not (g == g[:, :1]).all():
-                raise ValueError("stripes that share a granule row need the same presence pattern")
-            p = np.ascontiguousarray(g[:, 0])
-        lay = lay.view
     if p.ndim != 2 or p.shape[0] != lay.n_stripes or p.shape[1] != codec.getTotalShardCount():
         raise ValueError(f"present must be ({lay.n_stripes}, {codec.getTotalShardCount()}), got {p.shape}")
-    check(_lib.load().rs_decode_batch_masked_dev(codec.handle, C.c_void_p(dev_base), p.ctypes.data_as(_lib.u8p),
-                                                 lay.n_stripes, lay.shard_len, lay.shard_stride, lay.stripe_stride,
-                                                 C.c_void_p(_stream_handle(stream))))
+    lib, h, st = _lib.load(), C.c_void_p(_stream_handle(stream)), p.ctypes.data_as(_lib.u8p)
+    if isinstance(lay, GranuleLayout):
+        check(lib.rs_decode_granule_masked_dev(codec.handle, C.c_void_p(dev_base), st, lay.n_stripes, lay.shard_len,
+                                               lay.granule, h))
+        return
+    check(lib.rs_decode_batch_masked_dev(codec.handle, C.c_void_p(dev_base), st, lay.n_stripes, lay.shard_len,
+                                         lay.shard_stride, lay.stripe_stride, h))
 
 
 def decode_masked_bits(codec: ReedSolomon, dev_base: int, dev_bits: int, lay: StripeLayout, dev_bad: int = 0,
                        stream=None) -> None:
     """Per-stripe presence bitmasks already in device memory: dev_bits points
-    at n_stripes uint32 words, bit i = shard i present.  Undecodable stripes
-    are skipped and counted into the device int32 at dev_bad (when given).
-    For a GranuleLayout dev_bits holds one word per sub-stripe of its view
-    (n_stripes * subs_per_stripe words; an undecodable stripe then counts once
-    per sub-stripe)."""
-    lay = _kernel_layout(lay)
-    check(_lib.load().rs_decode_batch_masked_bits_dev(codec.handle, C.c_void_p(dev_base), C.c_void_p(dev_bits),
-                                                      lay.n_stripes, lay.shard_len, lay.shard_stride,
-                                                      lay.stripe_stride, C.c_void_p(dev_bad or None),
-                                                      C.c_void_p(_stream_handle(stream))))
+    at n_stripes uint32 words, bit i = shard i present (one word per stripe,
+    for a GranuleLayout too).  Undecodable stripes are skipped and each is
+    counted once into the device int32 at dev_bad (when given)."""
+    lib, h = _lib.load(), C.c_void_p(_stream_handle(stream))
+    if isinstance(lay, GranuleLayout):
+        check(lib.rs_decode_granule_masked_bits_dev(codec.handle, C.c_void_p(dev_base), C.c_void_p(dev_bits),
+                                                    lay.n_stripes, lay.shard_len, lay.granule,
+                                                    C.c_void_p(dev_bad or None), h))
+        return
+    check(lib.rs_decode_batch_masked_bits_dev(codec.handle, C.c_void_p(dev_base), C.c_void_p(dev_bits),
+                                              lay.n_stripes, lay.shard_len, lay.shard_stride, lay.stripe_stride,
+                                              C.c_void_p(dev_bad or None), h))
 
 
 def presence_bits(present) -> np.ndarray:

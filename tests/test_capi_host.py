@@ -250,8 +250,10 @@ def test_kernels_use_no_scratch(native, tmp_path):
     # The one deliberate exception: gf_masked_kernel<10,4> is held to 72 VGPRs
     # (7 waves per SIMD) and spills 5 dwords per lane; measured faster than 73
     # VGPRs at 6 waves, with the extra bytes staying in L2 (kernels.hip, the
-    # comment on gf_masked_kernel).
-    allowed = {"_ZN5rsamd12_GLOBAL__N_116gf_masked_kernelILi10ELi4EEEvNS0_10MaskedArgsE": 20}
+    # comment on gf_masked_kernel).  Its granule-layout build
+    # (PAT = true: the block's stripe from its batch column) spills 2 dwords.
+    allowed = {"_ZN5rsamd12_GLOBAL__N_116gf_masked_kernelILi10ELi4ELb0EEEvNS0_10MaskedArgsE": 20,
+               "_ZN5rsamd12_GLOBAL__N_116gf_masked_kernelILi10ELi4ELb1EEEvNS0_10MaskedArgsE": 8}
     bad = {k: v for k, v in kernels.items()
            if any(v.values()) and v.get(".private_segment_fixed_size", 0) > allowed.get(k, 0)}
     assert not bad, bad

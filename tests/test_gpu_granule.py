@@ -6,8 +6,8 @@ through the C-ABI, against the oracle.  Bit-exact.
     the oracle's encodeParity (ReedSolomon.java:90-104) -- 4+2, 10+4, 17+3;
   * uniform-pattern decode (ReedSolomon.java:175-272): the reference test's
     {0,5} (ReedSolomonTest.java:77-93) and 10+4 {0,1,2,3};
-  * per-stripe patterns (decode_masked, one pattern per stripe repeated over
-    its sub-stripes), and device bitmasks per sub-stripe;
+  * per-stripe patterns (decode_masked, one pattern per stripe; formerly repeated over
+    its sub-stripes), and device bitmasks, one per stripe;
   * verify flags a single flipped byte and passes a clean batch;
   * BASELINE config[3] at full size in the granule layout (10+4 x 4 MiB x 128,
     G = 32 KiB): encode -> verify clean -> erase 4 -> decode -> verify clean,
@@ -99,9 +99,11 @@ def test_granule_uniform_decode(gpu, k, m, miss):
 
 
 def test_granule_per_stripe_patterns(gpu):
-    """decode_masked on a granule batch: every stripe its own erasures (each
-    stripe's pattern repeated over its sub-stripes); then the same patterns
-    as device bitmasks per sub-stripe."""
+    """decode_masked on a granule batch: every stripe its own erasures, one
+    pattern per stripe (rs_decode_granule_masked_dev finds a block's stripe
+    from its batch column); then the same patterns as device bitmasks, one
+    word per stripe, with an undecodable stripe left alone and counted once
+    although it spans 4 granule rows."""
     import torch
     import rsamd
     from rsamd import device
@@ -119,16 +121,57 @@ def test_granule_per_stripe_patterns(gpu):
     device.decode_masked(rs, dev.data_ptr(), present, lay, torch.cuda.current_stream())
     np.testing.assert_array_equal(_download(torch, lay, dev, n, k + m), want)
     dev = _upload(torch, lay, clobbered)
-    bits = np.repeat(device.presence_bits(present), lay.subs_per_stripe)
+    bits = device.presence_bits(present)
+    bits[4] = 0b000111  # 3 of 6 present: undecodable, left as it is
     dbits = torch.from_numpy(bits.view(np.int32)).to("cuda:0")
-    device.decode_masked_bits(rs, dev.data_ptr(), dbits.data_ptr(), lay, 0, torch.cuda.current_stream())
+    bad = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    device.decode_masked_bits(rs, dev.data_ptr(), dbits.data_ptr(), lay, bad.data_ptr(), torch.cuda.current_stream())
+    got = _download(torch, lay, dev, n, k + m)
+    assert int(bad.item()) == 1
+    np.testing.assert_array_equal(got[4], clobbered[4])
+    keep = np.arange(n) != 4
+    np.testing.assert_array_equal(got[keep], want[keep])
+
+
+@pytest.mark.parametrize("S,G", [(4 << 10, 64 << 10), (1 << 10, 8 << 10), (2064, 8256), (4160, 1040)])
+def test_granule_small_shards_patterns_per_stripe(gpu, S, G):
+    """Several stripes per granule row (config[4]'s 4 KiB shards in 64 KiB
+    rows, 16 stripes each), each stripe its OWN pattern -- every 4+2 pattern
+    with at most 2 erasures, cycled; as host flags and as device bitmasks.
+    The 2064/8256 and 4160/1040 shapes (not whole 1 KiB chunks) take the
+    byte-granular kernel."""
+    import itertools
+    import torch
+    import rsamd
+    from rsamd import device
+    k, m = 4, 2
+    n = max(64, 2 * G // S)
+    lay = device.GranuleLayout.make(n, k + m, S, G)
+    pats = [[i not in mi for i in range(k + m)] for e in range(3) for mi in itertools.combinations(range(k + m), e)]
+    present = np.array([pats[(7 * t) % len(pats)] for t in range(n)], dtype=bool)
+    want = _oracle_encode(k, m, np.random.default_rng(9).integers(0, 256, (n, k + m, S), dtype=np.uint8))
+    rs = rsamd.ReedSolomon.create(k, m)
+    clobbered = want.copy()
+    clobbered[~present] = 0x11
+    dev = _upload(torch, lay, clobbered)
+    device.decode_masked(rs, dev.data_ptr(), present, lay, torch.cuda.current_stream())
     np.testing.assert_array_equal(_download(torch, lay, dev, n, k + m), want)
+    dev = _upload(torch, lay, clobbered)
+    bits = device.presence_bits(present)
+    bits[1] = 0b110001  # undecodable: untouched, counted once
+    dbits = torch.from_numpy(bits.view(np.int32)).to("cuda:0")
+    bad = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    device.decode_masked_bits(rs, dev.data_ptr(), dbits.data_ptr(), lay, bad.data_ptr(), torch.cuda.current_stream())
+    got = _download(torch, lay, dev, n, k + m)
+    assert int(bad.item()) == 1
+    np.testing.assert_array_equal(got[1], clobbered[1])
+    keep = np.arange(n) != 1
+    np.testing.assert_array_equal(got[keep], want[keep])
 
 
 def test_granule_small_shards_decode(gpu):
     """config[4]-style 4 KiB shards, 16 stripes per 64 KiB granule row: {0,1}
-    decode; decode_masked with one pattern per row, and a pattern that
-    differs inside a row is refused."""
+    decode with one pattern for the batch."""
     import torch
     import rsamd
     from rsamd import device
@@ -142,17 +185,6 @@ def test_granule_small_shards_decode(gpu):
     dev = _upload(torch, lay, clobbered)
     device.decode(rs, dev.data_ptr(), [False, False, True, True, True, True], lay, torch.cuda.current_stream())
     np.testing.assert_array_equal(_download(torch, lay, dev, n, k + m), want)
-    present = np.ones((n, k + m), dtype=bool)
-    for row, miss in enumerate([(0,), (2, 5), (), (1, 4)]):
-        present[row * 16:(row + 1) * 16, list(miss)] = False
-    clobbered = want.copy()
-    clobbered[~present] = 0x11
-    dev = _upload(torch, lay, clobbered)
-    device.decode_masked(rs, dev.data_ptr(), present, lay, torch.cuda.current_stream())
-    np.testing.assert_array_equal(_download(torch, lay, dev, n, k + m), want)
-    present[3, 3] = False  # one stripe of row 0 differs from its row
-    with pytest.raises(ValueError):
-        device.decode_masked(rs, dev.data_ptr(), present, lay, torch.cuda.current_stream())
 
 
 def test_granule_verify_flags_one_byte(gpu):
