@@ -146,3 +146,28 @@ def test_copy_shard_argument_checks(native):
     assert b"must divide one another" in native.rs_last_error_message()
     assert f(base, 6, 4096, 0, 0, 0, base, 1, None) == RS_E_INVALID          # granule 0
     assert f(base, 6, 0, 1024, 0, 0, base, 1, None) == RS_E_INVALID          # shard_len 0
+
+
+def test_granule_masked_argument_checks(native):
+    """rs_decode_granule_masked[_bits]_dev: shape errors are RS_E_INVALID
+    before any HIP call; an empty batch is RS_OK (runs without a GPU)."""
+    import rsamd
+    RS_E_INVALID = -10
+    rs = rsamd.ReedSolomon.create(4, 2)
+    buf = (C.c_uint8 * 64)()
+    base = C.c_void_p(C.addressof(buf))
+    present = np.ones(6 * 4, dtype=np.uint8)
+    pp = present.ctypes.data_as(C.POINTER(C.c_uint8))
+    f, fb = native.rs_decode_granule_masked_dev, native.rs_decode_granule_masked_bits_dev
+    assert f(rs.handle, base, pp, 4, 4096, 3000, None) == RS_E_INVALID      # neither divides the other
+    assert b"must divide one another" in native.rs_last_error_message()
+    assert f(rs.handle, base, pp, 1, 4096, 8192, None) == RS_E_INVALID      # G does not divide n * S
+    assert b"does not divide" in native.rs_last_error_message()
+    assert f(rs.handle, base, pp, 4, 4096, 0, None) == RS_E_INVALID         # granule 0
+    assert f(rs.handle, base, None, 4, 4096, 1024, None) == RS_E_INVALID    # NULL present
+    assert f(rs.handle, None, pp, 4, 4096, 1024, None) == RS_E_INVALID      # NULL base
+    assert f(None, base, pp, 4, 4096, 1024, None) == RS_E_INVALID           # NULL codec
+    assert f(rs.handle, base, pp, 0, 4096, 1024, None) == 0                 # nothing to do
+    assert fb(rs.handle, base, base, 4, 4096, 3000, None, None) == RS_E_INVALID
+    assert fb(rs.handle, base, None, 4, 4096, 1024, None, None) == RS_E_INVALID
+    assert fb(rs.handle, base, base, 0, 4096, 1024, None, None) == 0
