@@ -275,6 +275,7 @@ def run(args, live_traffic=None):
         if world == 1:
             extra.update(other_configs(torch, rsamd, rdev, dev, stream))
             extra.update(granule_legs(torch, rsamd, rdev, dev, stream))
+            extra.update(chunk_group_legs(torch, rsamd, rdev, dev, stream))
             extra.update(layout_legs(torch, rsamd, dev, stream))
             cpu = cpu_baseline(k, m, S, args.cpu_seconds)
             extra["cpu_configs"] = cpu_configs()
@@ -626,6 +627,60 @@ def granule_legs(torch, rsamd, rdev, dev, stream):
                 out[name + tag + "_verified"] = int(flag.item()) == 0
         pool.free()
         torch.cuda.empty_cache()
+    return out
+
+
+def chunk_group_legs(torch, rsamd, rdev, dev, stream, B=4 << 20):
+    """Row f2 at the DFS's own shard size: the master's recovery decodes one
+    6 x 1000-B chunk group at a time (ChunkserverDiskRecoveryMachine.java:34-48,
+    MasterImpl.java:794-839).  B = 4 M groups of 4+2 x 1000 B packed back to
+    back (stride 1000, 24 GB): the 8-byte-aligned kernels (kernels.hip).
+    Encode and uniform {0,1} decode, then a random pattern per group
+    (<= 2 erasures) as device bitmasks and as host flags; each decode is
+    verified after the absent shards were overwritten."""
+    import itertools
+    import numpy as np
+    from rsamd.device import StripeLayout
+    k, m, S, T = 4, 2, 1000, 6
+    name = "chunk_groups_4p2_1000B_x4M"
+    rs = rsamd.ReedSolomon.create(k, m)
+    lay = StripeLayout(B, S, S, T * S)
+    pool = rdev.DeviceBuffer(lay.nbytes, contiguous=True)
+    buf, base = pool.tensor(), pool.data_ptr()
+    out = {name + "_layout": "packed back to back, shard stride 1000, group stride 6000"}
+    rdev.fill_synthetic(base, k, lay, SEED, 0, stream)
+    t = timed(torch, stream, lambda: rdev.encode(rs, base, lay, stream), 10)
+    out[name + "_encode_GiBps"] = round(k * S * B / t / 2**30, 2)
+    out[name + "_encode_hbm_frac"] = round(T * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
+    present = [False, False, True, True, True, True]
+    t = timed(torch, stream, lambda: rdev.decode(rs, base, present, lay, stream), 10)
+    out[name + "_decode_0_1_hbm_frac"] = round(T * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    clobber(torch, buf, lay, T, np.tile(np.array(present), (B, 1)), dev)
+    rdev.decode(rs, base, present, lay, stream)
+    rdev.verify(rs, base, lay, flag.data_ptr(), stream)
+    out[name + "_decode_verified"] = int(flag.item()) == 0
+    pats = np.array([[i not in mi for i in range(T)] for e in range(3) for mi in itertools.combinations(range(T), e)],
+                    dtype=bool)
+    pres = pats[np.random.default_rng(0).integers(0, len(pats), B)]
+    alg = (k * int((~pres).any(axis=1).sum()) + int((~pres).sum())) * S
+    bits = torch.from_numpy(rdev.presence_bits(pres).view(np.int32)).to(dev)
+    t = timed(torch, stream, lambda: rdev.decode_masked_bits(rs, base, bits.data_ptr(), lay, 0, stream), 10)
+    out[name + "_decode_masked_bits_hbm_frac"] = round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)
+    out[name + "_decode_masked_bits_groups_per_s"] = round(B / t, 0)
+    t = timed(torch, stream, lambda: rdev.decode_masked(rs, base, pres, lay, stream), 10)
+    out[name + "_decode_masked_hbm_frac"] = round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)
+    for tag, call in (("_decode_masked_bits", lambda: rdev.decode_masked_bits(rs, base, bits.data_ptr(), lay, 0,
+                                                                              stream)),
+                      ("_decode_masked", lambda: rdev.decode_masked(rs, base, pres, lay, stream))):
+        clobber(torch, buf, lay, T, pres, dev)
+        call()
+        flag.zero_()
+        rdev.verify(rs, base, lay, flag.data_ptr(), stream)
+        out[name + tag + "_verified"] = int(flag.item()) == 0
+    del buf, bits
+    pool.free()
+    torch.cuda.empty_cache()
     return out
 
 

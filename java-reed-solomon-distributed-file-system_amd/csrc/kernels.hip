@@ -492,6 +492,165 @@ __global__ void __launch_bounds__(kWave) gf_masked_generic_kernel(MaskedArgs a) 
         if (p < nout) store_stream(sb + out_off[p], acc[p]);
 }
 
+// 8-byte-aligned kernels: batches whose base and strides are multiples of 8
+// but not of 16 -- the DFS's 1000-byte chunk groups packed back to back
+// (ChunkserverDiskRecoveryMachine.java:34-48, MasterImpl.java:794-839).  A
+// lane codes one vector of W dwords at byte 16 * v of its stripe's shards:
+// W = 4 (16 B, global_load_dwordx4 on an 8-byte-aligned address) for the
+// shard's whole 16-byte vectors, W = 2 for a last half vector (S % 16 == 8).
+// A 1000-byte shard is 62 + 1 lanes: one wave per stripe.  The other form
+// has every lane code one 8-byte vector (W = 2): 125 lanes per 1000-byte
+// shard, two waves per stripe.  K > 0 issues all K loads before the first
+// fold; K == 0 (runtime k) loads input by input.  a.nvec counts lanes'
+// vectors: whole 16-byte vectors plus the half, or 8-byte vectors.
+//
+// Measured on 4 M chunk groups of 4+2 x 1000 B packed back to back
+// (tools/chunk_group_probe.py, profiles/r2/chunk_groups_r2bi.txt): 16-byte
+// form encode / decode 0.599 / 0.598 of peak, per-group bitmasks 0.556;
+// 8-byte form 0.590 / 0.590 and 0.604; the byte kernel they replace 0.049 and
+// 0.042.  So the uniform kernels take the 16-byte form and the masked kernel
+// the 8-byte one (RSAMD_VEC8_U16 / RSAMD_MASKED8_U16 for A/B builds).
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4a8 __attribute__((ext_vector_type(4), aligned(8)));
+#ifndef RSAMD_VEC8_U16
+#define RSAMD_VEC8_U16 1
+#endif
+#ifndef RSAMD_MASKED8_U16
+#define RSAMD_MASKED8_U16 0
+#endif
+
+template <int W>
+struct Vec8;
+template <>
+struct Vec8<2> {
+    typedef u32x2 T;
+};
+template <>
+struct Vec8<4> {
+    typedef u32x4a8 T;
+};
+
+template <int W>
+__device__ __forceinline__ typename Vec8<W>::T load8(const uint8_t *p) {
+    return __builtin_nontemporal_load(reinterpret_cast<const typename Vec8<W>::T *>(p));
+}
+
+// sb: the lane's vector in shard 0 of its stripe; tabs[nin][MS][5].  With
+// W = 4 and half set, the lane's vector is only its low 8 bytes (a shard's
+// last half vector): it loads and stores 8 bytes and codes zeros above them,
+// so every lane runs the same fold.
+template <int W, int K, int MS, bool VERIFY>
+__device__ __forceinline__ void code8(uint8_t *sb, bool half, const uint32_t *tabs, const int32_t *in_idx,
+                                      const int32_t *out_idx, int nin, int nout, uint64_t shard_stride,
+                                      int *mismatch) {
+    typedef typename Vec8<W>::T V;
+    auto ld = [&](const uint8_t *p) -> V {
+        if (W == 4 && half) {
+            const u32x2 h = load8<2>(p);
+            V x;
+            x[0] = h[0];
+            x[1] = h[1];
+#pragma unroll
+            for (int w = 2; w < W; ++w) x[w] = 0;
+            return x;
+        }
+        return load8<W>(p);
+    };
+    uint64_t out_off[MS];
+#pragma unroll
+    for (int p = 0; p < MS; ++p) out_off[p] = uint64_t(out_idx[p]) * shard_stride;
+    uint32_t acc[MS][W];
+    auto fold = [&](int i, const V &x) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const Sel sl = selectors(x[w]);
+#pragma unroll
+            for (int p = 0; p < MS; ++p) {
+                uint32_t t0, t1, t2;
+                terms(tabs + (i * MS + p) * 5, sl, t0, t1, t2);
+                acc[p][w] = i == 0 ? xor3(t0, t1, t2) : xor3(acc[p][w], t0, t1) ^ t2;
+            }
+        }
+    };
+    if constexpr (K > 0) {
+        V x[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) x[i] = ld(sb + uint64_t(in_idx[i]) * shard_stride);
+#pragma unroll
+        for (int i = 0; i < K; ++i) fold(i, x[i]);
+    } else {
+        for (int i = 0; i < nin; ++i) fold(i, ld(sb + uint64_t(in_idx[i]) * shard_stride));
+    }
+#pragma unroll
+    for (int p = 0; p < MS; ++p) {
+        if (p >= nout) continue;
+        uint8_t *q = sb + out_off[p];
+        if (VERIFY) {
+            const V have = ld(q);
+            bool diff = false;
+#pragma unroll
+            for (int w = 0; w < W; ++w) diff |= have[w] != acc[p][w];
+            if (diff) flag_mismatch(mismatch);
+        } else if (W == 4 && half) {
+            __builtin_nontemporal_store(u32x2{acc[p][0], acc[p][1]}, reinterpret_cast<u32x2 *>(q));
+        } else {
+            V v;
+#pragma unroll
+            for (int w = 0; w < W; ++w) v[w] = acc[p][w];
+            __builtin_nontemporal_store(v, reinterpret_cast<V *>(q));
+        }
+    }
+}
+
+// Lane vector v of a stripe: U16, whole 16-byte vectors below nfull16, then
+// the half vector; otherwise 8-byte vectors throughout.
+template <bool U16, int K, int MS, bool VERIFY>
+__device__ __forceinline__ void code8_lane(uint8_t *stripe_base, uint32_t v, uint32_t nfull16, const uint32_t *tabs,
+                                           const int32_t *in_idx, const int32_t *out_idx, int nin, int nout,
+                                           uint64_t shard_stride, int *mismatch) {
+    uint8_t *sb = stripe_base + uint64_t(v) * (U16 ? 16 : 8);
+    if (U16)
+        code8<4, K, MS, VERIFY>(sb, v >= nfull16, tabs, in_idx, out_idx, nin, nout, shard_stride, mismatch);
+    else
+        code8<2, K, MS, VERIFY>(sb, false, tabs, in_idx, out_idx, nin, nout, shard_stride, mismatch);
+}
+
+template <int K, int MS>
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(8, 8))) gf_masked8_kernel(MaskedArgs a) {
+    uint32_t stripe, chunk;
+    block_item(a.chunks, a.cdiv, a.rot, a.xcd_span, stripe, chunk);
+    const uint32_t v = chunk * uint32_t(kWave) + threadIdx.x;
+    const uint8_t *rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, stripe);
+    if (!rec) {
+        count_undecodable(a.bad, v == 0);
+        return;
+    }
+    const int nout = *reinterpret_cast<const int32_t *>(rec);
+    if (nout == 0 || v >= a.nvec) return;
+    code8_lane<RSAMD_MASKED8_U16, K, MS, false>(a.base + uint64_t(stripe) * a.stripe_stride, v, a.pat_chunk0,
+                             reinterpret_cast<const uint32_t *>(rec + a.rec_tabs),
+                             reinterpret_cast<const int32_t *>(rec + a.rec_in_idx),
+                             reinterpret_cast<const int32_t *>(rec + a.rec_out_idx), a.nin, nout, a.shard_stride,
+                             nullptr);
+}
+
+struct Vec8Args {
+    VecArgs v;
+    uint32_t nfull16;
+};
+
+template <int K, int M, bool VERIFY>
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(7, 8))) gf_vec8_kernel(Vec8Args a8) {
+    const VecArgs &a = a8.v;
+    if (VERIFY && mismatch_seen(a.mismatch)) return;
+    uint32_t stripe, chunk;
+    block_item(a.chunks, a.cdiv, a.rot, a.xcd_span, stripe, chunk);
+    const uint32_t v = chunk * uint32_t(kWave) + threadIdx.x;
+    if (v >= a.nvec) return;
+    code8_lane<RSAMD_VEC8_U16, K, M, VERIFY>(a.base + uint64_t(stripe) * a.stripe_stride, v, a8.nfull16, a.tabs, a.in_idx, a.out_idx,
+                             a.nin, M, a.shard_stride, a.mismatch);
+}
+
 // Masked byte kernel: any alignment, and the <16-byte tails.
 struct MaskedByteArgs {
     uint8_t *base;
@@ -782,6 +941,57 @@ hipError_t dispatch_masked(const MaskedArgs &a, int ms, hipStream_t s) {
     return hipErrorInvalidValue;
 }
 
+template <int K, int MS>
+hipError_t launch_masked8_t(const MaskedArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL((gf_masked8_kernel<K, MS>), dim3(a.n_items), dim3(kWave), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t dispatch_masked8(const MaskedArgs &a, int ms, hipStream_t s) {
+    const bool k4 = a.nin == 4;
+    switch (ms) {
+    case 1: return k4 ? launch_masked8_t<4, 1>(a, s) : launch_masked8_t<0, 1>(a, s);
+    case 2: return k4 ? launch_masked8_t<4, 2>(a, s) : launch_masked8_t<0, 2>(a, s);
+    case 3: return k4 ? launch_masked8_t<4, 3>(a, s) : launch_masked8_t<0, 3>(a, s);
+    case 4: return k4 ? launch_masked8_t<4, 4>(a, s) : launch_masked8_t<0, 4>(a, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+template <int K, int M>
+hipError_t launch_vec8_t(const Vec8Args &a, Mode mode, hipStream_t s) {
+    if (mode == Mode::Verify)
+        hipLaunchKernelGGL((gf_vec8_kernel<K, M, true>), dim3(a.v.n_items), dim3(kWave), 0, s, a);
+    else
+        hipLaunchKernelGGL((gf_vec8_kernel<K, M, false>), dim3(a.v.n_items), dim3(kWave), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t dispatch_vec8(const Vec8Args &a, int nout, Mode mode, hipStream_t s) {
+    const bool k4 = a.v.nin == 4;
+    switch (nout) {
+    case 1: return k4 ? launch_vec8_t<4, 1>(a, mode, s) : launch_vec8_t<0, 1>(a, mode, s);
+    case 2: return k4 ? launch_vec8_t<4, 2>(a, mode, s) : launch_vec8_t<0, 2>(a, mode, s);
+    case 3: return k4 ? launch_vec8_t<4, 3>(a, mode, s) : launch_vec8_t<0, 3>(a, mode, s);
+    case 4: return k4 ? launch_vec8_t<4, 4>(a, mode, s) : launch_vec8_t<0, 4>(a, mode, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+// Lanes per stripe of the 8-byte-aligned kernels and the bytes they cover:
+// whole 16-byte vectors plus a half, or 8-byte vectors.
+struct Lanes8 {
+    uint32_t nvec, nfull16;
+    size_t covered;
+};
+Lanes8 lanes8(size_t len, bool u16) {
+    if (u16) {
+        const size_t full = len / 16, half = (len % 16) >= 8 ? 1 : 0;
+        return Lanes8{uint32_t(full + half), uint32_t(full), full * 16 + half * 8};
+    }
+    return Lanes8{uint32_t(len / 8), 0, len / 8 * 8};
+}
+
 hipError_t launch_masked_bytes(const Geometry &g, const MaskedPlan &p, const MaskedRecordLayout &l, size_t col0,
                                size_t ncols, hipStream_t s) {
     MaskedByteArgs a{g.base, p.records, p.rec_stride, p.plan_ids, g.stripe_stride, g.shard_stride, col0, ncols,
@@ -791,6 +1001,43 @@ hipError_t launch_masked_bytes(const Geometry &g, const MaskedPlan &p, const Mas
     const unsigned grid = unsigned(std::min<uint64_t>((a.total + kThreads - 1) / kThreads, 65536));
     hipLaunchKernelGGL(gf_masked_byte_kernel, dim3(grid), dim3(kThreads), 0, s, a);
     return hipGetLastError();
+}
+
+}  // namespace
+
+namespace {
+
+// RSAMD_MASKED8=0 sends 8-byte-aligned batches to the byte kernel (A/B runs).
+bool masked8_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("RSAMD_MASKED8");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// 8-byte vectors (gf_masked8_kernel), then the < 8-byte tail on the byte kernel.
+hipError_t launch_masked8(const Geometry &g, const MaskedPlan &p, const MaskedRecordLayout &l, hipStream_t s) {
+    uint8_t *base = g.base + g.col0;
+    const Lanes8 n = lanes8(g.len, RSAMD_MASKED8_U16);
+    if (n.nvec > 0) {
+        const uint32_t chunks = (n.nvec + kWave - 1) / kWave;
+        const size_t stripes_per_launch = std::max<size_t>(1, kMaxGridBlocks / chunks);
+        for (size_t t0 = 0; t0 < g.n_stripes; t0 += stripes_per_launch) {
+            const size_t nst = std::min(stripes_per_launch, g.n_stripes - t0);
+            const BlockOrder o = block_order(chunks, uint32_t(g.stripe_stride / std::max<size_t>(1, g.shard_stride)),
+                                             g.shard_stride, uint32_t(nst * chunks));
+            // pat_chunk0 carries nfull16 (the 8-byte kernels take no per-row patterns)
+            MaskedArgs a{base + t0 * g.stripe_stride, p.records, p.rec_stride, p.plan_ids + t0, g.stripe_stride,
+                         g.shard_stride, n.nvec, chunks, uint32_t(nst * chunks), o.rot, o.xcd_span,
+                         make_fastdiv(chunks), uint32_t(l.in_idx), uint32_t(l.out_idx), uint32_t(l.tabs), p.nin,
+                         p.mask_table, p.mask_bits, p.bad, 0u, n.nfull16, make_fastdiv(1), 1u};
+            hipError_t e = dispatch_masked8(a, p.mslots, s);
+            if (e != hipSuccess) return e;
+        }
+    }
+    if (n.covered < g.len) return launch_masked_bytes(g, p, l, g.col0 + n.covered, g.len - n.covered, s);
+    return hipSuccess;
 }
 
 }  // namespace
@@ -819,6 +1066,10 @@ hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t 
     const bool pat_vec = pb == 0 || (g.col0 == 0 && g.len % chunk_bytes == 0 && pb % chunk_bytes == 0 &&
                                      (pb % g.len == 0 || g.len % pb == 0) &&
                                      g.n_stripes * (g.len / chunk_bytes) <= UINT32_MAX);
+    const bool aligned8 = (reinterpret_cast<uintptr_t>(base) % 8 == 0) && g.shard_stride % 8 == 0 &&
+                          g.stripe_stride % 8 == 0;
+    if (!aligned && aligned8 && pb == 0 && g.len / 8 <= UINT32_MAX - kWave && masked8_enabled())
+        return launch_masked8(g, p, l, s);
     if (!aligned || !pat_vec || g.len / 16 > UINT32_MAX - kWave) return launch_masked_bytes(g, p, l, g.col0, g.len, s);
     const uint32_t nvec = uint32_t(g.len / 16);
     if (nvec > 0) {
@@ -845,12 +1096,19 @@ hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t 
 namespace {
 
 // The table-lookup (v_perm_b32) kernels: any plan, any geometry.
+hipError_t launch_vec8(const Geometry &g, const DevPlan &p, Mode mode, int *mismatch, hipStream_t s);
+
 hipError_t launch_gf_tables(const Geometry &g, const DevPlan &p, Mode mode, int *mismatch, hipStream_t s) {
     if (g.n_stripes == 0 || g.len == 0 || p.nout == 0) return hipSuccess;
     if (p.nout > kMaxOut || p.nin < 1) return hipErrorInvalidValue;
     uint8_t *base = g.base + g.col0;
     const bool aligned = (reinterpret_cast<uintptr_t>(base) % 16 == 0) && g.shard_stride % 16 == 0 &&
                          g.stripe_stride % 16 == 0;
+    const bool aligned8 = (reinterpret_cast<uintptr_t>(base) % 8 == 0) && g.shard_stride % 8 == 0 &&
+                          g.stripe_stride % 8 == 0;
+    if (!aligned && aligned8 && uint64_t(g.n_stripes) * g.len > kSmallBytes && g.len / 8 <= UINT32_MAX - kWave &&
+        masked8_enabled())
+        return launch_vec8(g, p, mode, mismatch, s);
     if (!aligned || g.len / 16 > UINT32_MAX - kWave) return launch_bytes(g, p, g.col0, g.len, mode, mismatch, s);
     // A few KiB of ragged columns: one byte-kernel launch instead of a vector
     // launch plus a tail launch (small host calls are launch-latency bound).
@@ -876,6 +1134,29 @@ hipError_t launch_gf_tables(const Geometry &g, const DevPlan &p, Mode mode, int 
     }
     const size_t tail = g.len % 16;
     if (tail) return launch_bytes(g, p, g.col0 + size_t(nvec) * 16, tail, mode, mismatch, s);
+    return hipSuccess;
+}
+
+// 8-byte vectors (gf_vec8_kernel), then the < 8-byte tail on the byte kernel.
+hipError_t launch_vec8(const Geometry &g, const DevPlan &p, Mode mode, int *mismatch, hipStream_t s) {
+    uint8_t *base = g.base + g.col0;
+    const Lanes8 n = lanes8(g.len, RSAMD_VEC8_U16);
+    if (n.nvec > 0) {
+        const uint32_t chunks = (n.nvec + kWave - 1) / kWave;
+        const size_t stripes_per_launch = std::max<size_t>(1, kMaxGridBlocks / chunks);
+        for (size_t t0 = 0; t0 < g.n_stripes; t0 += stripes_per_launch) {
+            const size_t nst = std::min(stripes_per_launch, g.n_stripes - t0);
+            const BlockOrder o = block_order(chunks, uint32_t(g.stripe_stride / std::max<size_t>(1, g.shard_stride)),
+                                             g.shard_stride, uint32_t(nst * chunks));
+            Vec8Args a{{base + t0 * g.stripe_stride, p.tabs, p.in_idx, p.out_idx, g.stripe_stride, g.shard_stride,
+                        n.nvec, chunks, uint32_t(nst * chunks), o.rot, o.xcd_span, make_fastdiv(chunks), p.nin,
+                        mismatch},
+                       n.nfull16};
+            hipError_t e = dispatch_vec8(a, p.nout, mode, s);
+            if (e != hipSuccess) return e;
+        }
+    }
+    if (n.covered < g.len) return launch_bytes(g, p, g.col0 + n.covered, g.len - n.covered, mode, mismatch, s);
     return hipSuccess;
 }
 

@@ -1,0 +1,77 @@
+"""GPU parity of the 8-byte-vector kernels (gf_vec8_kernel, gf_masked8_kernel):
+stripe batches whose base and strides are multiples of 8 but not of 16, the
+DFS's 1000-byte chunk groups packed back to back (ChunkserverDiskRecoveryMachine
+.java:34-48; the 6 x 1000-B groups of MasterImpl.java:794-839).  Encode
+(ReedSolomon.java:90-104), uniform decode (ReedSolomon.java:175-272, the
+reference test's {0,5}: ReedSolomonTest.java:77-93) and verify
+(ReedSolomon.java:115-164) through the C-ABI, bit-exact against the oracle.
+Shapes: 1000/1000 (125 vectors, two vectors per lane leave 3 lanes idle),
+1004/1016 (a 4-byte tail on the byte kernel), 10+4 and 3+3 (the runtime-k
+build), and 8-aligned stripe strides with 16-aligned shard strides."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _encoded(oracle_lib, k, m, S, B, seed):
+    rng = np.random.default_rng(seed)
+    batch = np.zeros((B, k + m, S), np.uint8)
+    batch[:, :k] = rng.integers(0, 256, (B, k, S), dtype=np.uint8)
+    c = oracle_lib.Codec(k, m)
+    for t in range(B):
+        c.encode_parity([batch[t, i] for i in range(k + m)], 0, S)
+    return batch
+
+
+def _to_dev(torch, batch, shard_stride, stripe_stride):
+    B, T, S = batch.shape
+    host = np.zeros(B * stripe_stride, np.uint8)
+    v = np.lib.stride_tricks.as_strided(host, (B, T, S), (stripe_stride, shard_stride, 1))
+    v[...] = batch
+    return torch.from_numpy(host).to("cuda:0")
+
+
+def _from_dev(dev, B, T, S, shard_stride, stripe_stride):
+    host = dev.cpu().numpy()
+    return np.lib.stride_tricks.as_strided(host, (B, T, S), (stripe_stride, shard_stride, 1)).copy()
+
+
+@pytest.mark.parametrize("k,m,S,shard_stride,stripe_pad", [(4, 2, 1000, 1000, 0), (4, 2, 1004, 1016, 0),
+                                                           (10, 4, 1000, 1000, 0), (3, 3, 2040, 2040, 0),
+                                                           (4, 2, 4096, 4096, 8), (4, 2, 1000, 1000, 8)])
+def test_vec8_encode_decode_verify(gpu, oracle_lib, k, m, S, shard_stride, stripe_pad):
+    import torch
+    import rsamd
+    from rsamd import device
+    from rsamd.device import StripeLayout
+    T, B = k + m, 700
+    stripe_stride = T * shard_stride + stripe_pad
+    want = _encoded(oracle_lib, k, m, S, B, S + k)
+    lay = StripeLayout(B, S, shard_stride, stripe_stride)
+    rs = rsamd.ReedSolomon.create(k, m)
+    st = torch.cuda.current_stream()
+    # encode over garbage parity
+    clob = want.copy()
+    clob[:, k:] = 0xA5
+    dev = _to_dev(torch, clob, shard_stride, stripe_stride)
+    device.encode(rs, dev.data_ptr(), lay, st)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_from_dev(dev, B, T, S, shard_stride, stripe_stride), want)
+    # verify: clean, then one flipped byte in the last stripe's last parity byte
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    device.verify(rs, dev.data_ptr(), lay, flag.data_ptr(), st)
+    assert int(flag.item()) == 0
+    bad = want.copy()
+    bad[-1, -1, -1] ^= 1
+    dev_bad = _to_dev(torch, bad, shard_stride, stripe_stride)
+    device.verify(rs, dev_bad.data_ptr(), lay, flag.data_ptr(), st)
+    assert int(flag.item()) == 1
+    # uniform decode of {0, T-1} (4+2: the reference test's {0,5}) and of {1}
+    for miss in [(0, T - 1), (1,)]:
+        clob = want.copy()
+        clob[:, list(miss)] = 0x3C
+        dev = _to_dev(torch, clob, shard_stride, stripe_stride)
+        device.decode(rs, dev.data_ptr(), [i not in miss for i in range(T)], lay, st)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(_from_dev(dev, B, T, S, shard_stride, stripe_stride), want)

@@ -75,6 +75,30 @@ def test_masked_10_4_and_generic_17_3(gpu, golden_dir):
     assert np.array_equal(_run_masked(rsamd.ReedSolomon.create(17, 3), g, pats), g)
 
 
+@pytest.mark.parametrize("k,m", [(10, 4), (3, 3), (6, 3)])
+def test_masked8_runtime_k_chunk_groups(gpu, oracle_lib, k, m):
+    """The 8-byte kernel's runtime-k build (k != 4) on 1000-byte shards packed
+    back to back: random patterns of up to m erasures, host flags and device
+    bitmasks, against the oracle."""
+    import rsamd
+    from rsamd.device import presence_bits
+    S, B, T = 1000, 300, k + m
+    rng = np.random.default_rng(k * 31 + m)
+    batch = np.zeros((B, T, S), np.uint8)
+    batch[:, :k] = rng.integers(0, 256, (B, k, S), dtype=np.uint8)
+    c = oracle_lib.Codec(k, m)
+    for t in range(B):
+        c.encode_parity([batch[t, i] for i in range(T)], 0, S)
+    pats = []
+    for t in range(B):
+        miss = rng.choice(T, int(rng.integers(0, m + 1)), replace=False)
+        pats.append([i not in miss for i in range(T)])
+    rs = rsamd.ReedSolomon.create(k, m)
+    assert np.array_equal(_run_masked(rs, batch, pats, S), batch)
+    out, bad, _ = _run_bits(rs, batch, presence_bits(pats), S)
+    assert bad == 0 and np.array_equal(out, batch)
+
+
 def test_masked_more_than_four_outputs(gpu, oracle_lib):
     """m = 6: patterns with 5-6 erasures need two output groups."""
     import rsamd
@@ -90,10 +114,12 @@ def test_masked_more_than_four_outputs(gpu, oracle_lib):
     assert np.array_equal(_run_masked(rsamd.ReedSolomon.create(k, m), batch, pats), batch)
 
 
-@pytest.mark.parametrize("S,stride", [(1000, 1000), (1000, 1008), (4096, 4099)])
+@pytest.mark.parametrize("S,stride", [(1000, 1000), (1000, 1008), (4096, 4099), (1004, 1016), (1000, 1024)])
 def test_masked_chunk_groups_like_the_master(gpu, oracle_lib, S, stride):
-    """The DFS recovers 6 x 1000-byte chunk groups (S % 16 != 0: tail kernel);
-    odd strides take the byte kernel."""
+    """The DFS recovers 6 x 1000-byte chunk groups: packed back to back
+    (stride 1000) they take the 8-byte kernel (gf_masked8_kernel, 125 vectors
+    per shard); stride 1008 the 16-byte kernel plus an 8-byte tail; 1004/1016
+    the 8-byte kernel plus a 4-byte tail; odd strides the byte kernel."""
     import rsamd
     rng = np.random.default_rng(S + stride)
     B = 500
@@ -185,7 +211,7 @@ def _run_bits(rs, batch, words, stride=None):
     return dev.cpu().numpy().reshape(B, T, stride)[:, :, :S], int(bad.item()), host[:, :, :S]
 
 
-@pytest.mark.parametrize("S,stride", [(4096, 4096), (1000, 1008), (999, 1001)])
+@pytest.mark.parametrize("S,stride", [(4096, 4096), (1000, 1008), (999, 1001), (1000, 1000), (1004, 1016)])
 def test_bits_every_bitmask_4_2(gpu, oracle_lib, S, stride):
     """All 64 bitmasks of 4+2 plus out-of-range words: decodable stripes are
     rebuilt bit-exact, the rest are left untouched and counted."""
