@@ -631,10 +631,17 @@ def granule_legs(torch, rsamd, rdev, dev, stream):
 
 
 def chunk_group_legs(torch, rsamd, rdev, dev, stream, B=4 << 20):
+    out = chunk_group_leg(torch, rsamd, rdev, dev, stream, B, 1000)
+    out.update(chunk_group_leg(torch, rsamd, rdev, dev, stream, B, 1024))
+    return out
+
+
+def chunk_group_leg(torch, rsamd, rdev, dev, stream, B, stride):
     """Row f2 at the DFS's own shard size: the master's recovery decodes one
     6 x 1000-B chunk group at a time (ChunkserverDiskRecoveryMachine.java:34-48,
     MasterImpl.java:794-839).  B = 4 M groups of 4+2 x 1000 B packed back to
-    back (stride 1000, 24 GB): the 8-byte-aligned kernels (kernels.hip).
+    back (stride 1000, 24 GB: the 8-byte-aligned kernels, kernels.hip) or
+    with each shard padded to 1 KiB (stride 1024).
     Encode and uniform {0,1} decode, then a random pattern per group
     (<= 2 erasures) as device bitmasks and as host flags; each decode is
     verified after the absent shards were overwritten."""
@@ -642,12 +649,12 @@ def chunk_group_legs(torch, rsamd, rdev, dev, stream, B=4 << 20):
     import numpy as np
     from rsamd.device import StripeLayout
     k, m, S, T = 4, 2, 1000, 6
-    name = "chunk_groups_4p2_1000B_x4M"
+    name = "chunk_groups_4p2_1000B_x4M" + ("" if stride == S else f"_stride{stride}")
     rs = rsamd.ReedSolomon.create(k, m)
-    lay = StripeLayout(B, S, S, T * S)
+    lay = StripeLayout(B, S, stride, T * stride)
     pool = rdev.DeviceBuffer(lay.nbytes, contiguous=True)
     buf, base = pool.tensor(), pool.data_ptr()
-    out = {name + "_layout": "packed back to back, shard stride 1000, group stride 6000"}
+    out = {name + "_layout": f"shard stride {stride}, group stride {T * stride}"}
     rdev.fill_synthetic(base, k, lay, SEED, 0, stream)
     t = timed(torch, stream, lambda: rdev.encode(rs, base, lay, stream), 10)
     out[name + "_encode_GiBps"] = round(k * S * B / t / 2**30, 2)

@@ -505,15 +505,19 @@ __global__ void __launch_bounds__(kWave) gf_masked_generic_kernel(MaskedArgs a) 
 // vectors: whole 16-byte vectors plus the half, or 8-byte vectors.
 //
 // Measured on 4 M chunk groups of 4+2 x 1000 B packed back to back
-// (tools/chunk_group_probe.py, profiles/r2/chunk_groups_r2bi.txt): 16-byte
-// form encode / decode 0.599 / 0.598 of peak, per-group bitmasks 0.556;
-// 8-byte form 0.590 / 0.590 and 0.604; the byte kernel they replace 0.049 and
-// 0.042.  So the uniform kernels take the 16-byte form and the masked kernel
-// the 8-byte one (RSAMD_VEC8_U16 / RSAMD_MASKED8_U16 for A/B builds).
+// (tools/chunk_group_probe.py; profiles/r2/chunk_groups_r2bi.txt, cg_ab_r2bk.txt):
+// 8-byte form encode / decode 0.590 / 0.590 of peak, per-group bitmasks
+// 0.604-0.605; 16-byte form 0.51-0.60 / 0.50-0.60 and 0.556 (it needs 65
+// VGPRs: capped at 8 waves it spills, at 7 it ran 0.513); the byte kernel
+// they replace 0.049 and 0.042.  An XOR reference of the same access pattern
+// reads 0.486 (8-byte) and 0.420 (16-byte) and its write-only half 0.325
+// (tools/group_mem.hip, profiles/r2/group_mem_r2bk.txt): the 1000-byte write
+// runs set the rate.  Both families take the 8-byte form
+// (RSAMD_VEC8_U16 / RSAMD_MASKED8_U16 = 1 for A/B builds).
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4a8 __attribute__((ext_vector_type(4), aligned(8)));
 #ifndef RSAMD_VEC8_U16
-#define RSAMD_VEC8_U16 1
+#define RSAMD_VEC8_U16 0
 #endif
 #ifndef RSAMD_MASKED8_U16
 #define RSAMD_MASKED8_U16 0
@@ -640,7 +644,7 @@ struct Vec8Args {
 };
 
 template <int K, int M, bool VERIFY>
-__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(7, 8))) gf_vec8_kernel(Vec8Args a8) {
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(8, 8))) gf_vec8_kernel(Vec8Args a8) {
     const VecArgs &a = a8.v;
     if (VERIFY && mismatch_seen(a.mismatch)) return;
     uint32_t stripe, chunk;
@@ -1007,6 +1011,13 @@ hipError_t launch_masked_bytes(const Geometry &g, const MaskedPlan &p, const Mas
 
 namespace {
 
+// Shards of a few KiB whose length leaves an 8-byte remainder after the
+// 16-byte vectors (S = 1000 at stride 1008 or 1024) take the 8-byte kernels
+// even when 16-byte aligned: one launch instead of the 16-byte kernel plus a
+// byte-kernel tail launch, 0.59 of peak against 0.54 at stride 1008
+// (profiles/r2/chunk_groups_r2bl.txt).
+bool small_with_tail8(size_t len) { return len % 16 == 8 && len < 16384; }
+
 // RSAMD_MASKED8=0 sends 8-byte-aligned batches to the byte kernel (A/B runs).
 bool masked8_enabled() {
     static const bool on = [] {
@@ -1068,7 +1079,8 @@ hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t 
                                      g.n_stripes * (g.len / chunk_bytes) <= UINT32_MAX);
     const bool aligned8 = (reinterpret_cast<uintptr_t>(base) % 8 == 0) && g.shard_stride % 8 == 0 &&
                           g.stripe_stride % 8 == 0;
-    if (!aligned && aligned8 && pb == 0 && g.len / 8 <= UINT32_MAX - kWave && masked8_enabled())
+    if (aligned8 && pb == 0 && (!aligned || small_with_tail8(g.len)) && g.len / 8 <= UINT32_MAX - kWave &&
+        masked8_enabled())
         return launch_masked8(g, p, l, s);
     if (!aligned || !pat_vec || g.len / 16 > UINT32_MAX - kWave) return launch_masked_bytes(g, p, l, g.col0, g.len, s);
     const uint32_t nvec = uint32_t(g.len / 16);
@@ -1106,8 +1118,8 @@ hipError_t launch_gf_tables(const Geometry &g, const DevPlan &p, Mode mode, int 
                          g.stripe_stride % 16 == 0;
     const bool aligned8 = (reinterpret_cast<uintptr_t>(base) % 8 == 0) && g.shard_stride % 8 == 0 &&
                           g.stripe_stride % 8 == 0;
-    if (!aligned && aligned8 && uint64_t(g.n_stripes) * g.len > kSmallBytes && g.len / 8 <= UINT32_MAX - kWave &&
-        masked8_enabled())
+    if (aligned8 && (!aligned || small_with_tail8(g.len)) && uint64_t(g.n_stripes) * g.len > kSmallBytes &&
+        g.len / 8 <= UINT32_MAX - kWave && masked8_enabled())
         return launch_vec8(g, p, mode, mismatch, s);
     if (!aligned || g.len / 16 > UINT32_MAX - kWave) return launch_bytes(g, p, g.col0, g.len, mode, mismatch, s);
     // A few KiB of ragged columns: one byte-kernel launch instead of a vector

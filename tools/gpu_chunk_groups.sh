@@ -8,7 +8,7 @@ set -o pipefail
 TAG=${1:?tag}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python3 -u -m pytest tests/test_gpu_recovery.py tests/test_gpu_chunk_groups.py tests/test_gpu_parity.py \
+timeout -k 10 400 python3 -u -m pytest tests \
     -x -q -m gpu --timeout 120 --timeout-method thread \
     > gpurun_out/pytest_recovery_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_recovery_$TAG.log; exit 1; }
 tail -1 gpurun_out/pytest_recovery_$TAG.log
