@@ -63,9 +63,10 @@ def parse(argv=None):
     ap.add_argument("--shard-bytes", type=int, default=1 << 20)
     ap.add_argument("--stripes", type=int, default=4096, help="stripes per GPU")
     ap.add_argument("--pad", type=int, default=0, help="bytes of padding between shards (layout A/B only)")
-    ap.add_argument("--layout", choices=["packed", "granule"], default="packed",
-                    help="HBM layout of the headline batch: packed shards (default) or the granule layout "
-                         "(include/rs_amd.h; the same stripes and bytes, reported in extra.granule_* too)")
+    ap.add_argument("--layout", choices=["packed", "granule"], default="granule",
+                    help="HBM layout of the headline batch: the granule layout (default; include/rs_amd.h, "
+                         "64 KiB granules: the same stripes and bytes, placement-robust, DESIGN.md 3.6) or "
+                         "packed shards (also timed in extra.packed_4p2_1MiB_x4096_*)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline sample budget (headline config)")
     ap.add_argument("--sustained-seconds", type=float, default=5.0, help="back-to-back encode leg length")
     ap.add_argument("--cfg3-stripes", type=int, default=CFG3_STRIPES,
@@ -132,9 +133,10 @@ def main(argv=None):
     # The live passes profile one process on cuda:0, so they run at N = 1 only:
     # at N > 1 every rank would start its own pair at once, all on GPU 0 (the
     # line then cites the committed summary of the same kernel and batch).
-    if (not (args.no_extras or args.no_live_pmc) and args.gpus == 1 and args.layout == "packed"
+    if (not (args.no_extras or args.no_live_pmc) and args.gpus == 1 and args.pad == 0
             and (args.k, args.m, args.shard_bytes, args.stripes) == (4, 2, 1 << 20, 4096)):
-        live = live_pmc_traffic()  # before this process touches the GPU: the passes are children
+        # before this process touches the GPU: the passes are children
+        live = live_pmc_traffic("enc42" if args.layout == "packed" else "enc42g")
     run(args, live)
     return 0
 
@@ -274,7 +276,7 @@ def run(args, live_traffic=None):
         extra.update(cfg3_strong(torch, rsamd, parallel, r, rdev, dev, stream, args.cfg3_stripes, args.steps))
         if world == 1:
             extra.update(other_configs(torch, rsamd, rdev, dev, stream))
-            extra.update(granule_legs(torch, rsamd, rdev, dev, stream))
+            extra.update(granule_legs(torch, rsamd, rdev, dev, stream, headline_layout=args.layout))
             extra.update(chunk_group_legs(torch, rsamd, rdev, dev, stream))
             extra.update(layout_legs(torch, rsamd, dev, stream))
             cpu = cpu_baseline(k, m, S, args.cpu_seconds)
@@ -284,7 +286,8 @@ def run(args, live_traffic=None):
         else:
             # every rank at once: the node's aggregate host <-> device rate
             extra.update(host_inclusive_all_ranks(rsamd, parallel, r, k, m))
-    traffic, traffic_source = pmc_traffic(k, m, S, B), "profiles/pmc_traffic.json (committed rocprofv3 --pmc summary)"
+    traffic = pmc_traffic(k, m, S, B, 0 if args.layout == "packed" else lay.granule)
+    traffic_source = "profiles/pmc_traffic.json (committed rocprofv3 --pmc summary)"
     if live_traffic and live_traffic.get("hbm_bytes_per_launch"):
         traffic, traffic_source = live_traffic["hbm_bytes_per_launch"], "rocprofv3 --pmc passes in this run"
 
@@ -547,17 +550,19 @@ def cfg3_strong(torch, rsamd, parallel, r, rdev, dev, stream, total, iters):
     return out
 
 
-def granule_legs(torch, rsamd, rdev, dev, stream):
+def granule_legs(torch, rsamd, rdev, dev, stream, headline_layout="granule"):
     """The same stripes in the granule layout (include/rs_amd.h, DESIGN.md
     3.6): the headline batch (4+2 x 1 MiB x 4096, 64 KiB granules),
     config[3]'s per-GPU share (10+4 x 4 MiB x 128, 32 KiB granules) and
     config[4] (4+2 x 4 KiB x 1 M, 16 stripes per 64 KiB granule row), each on
     a contiguous pool: encode, decode, verify; then the erased shards are
     overwritten, decoded and the batch verified."""
-    out = {}
+    out = packed_headline_leg(torch, rsamd, rdev, dev, stream) if headline_layout == "granule" else {}
     for name, k, m, S, B, miss in [("granule_4p2_1MiB_x4096", 4, 2, 1 << 20, 4096, (0, 1)),
                                    ("granule_10p4_4MiB_x128", 10, 4, 4 << 20, 128, (0, 1, 2, 3)),
                                    ("granule_4p2_4KiB_x1M", 4, 2, 4096, 1 << 20, (0, 1))]:
+        if name == "granule_4p2_1MiB_x4096" and headline_layout == "granule":
+            continue  # the headline itself
         rs = rsamd.ReedSolomon.create(k, m)
         lay = rdev.GranuleLayout.make(B, k + m, S)
         pool = rdev.DeviceBuffer(lay.nbytes, contiguous=True)
@@ -627,6 +632,39 @@ def granule_legs(torch, rsamd, rdev, dev, stream):
                 out[name + tag + "_verified"] = int(flag.item()) == 0
         pool.free()
         torch.cuda.empty_cache()
+    return out
+
+
+def packed_headline_leg(torch, rsamd, rdev, dev, stream):
+    """The headline's stripes (4+2 x 1 MiB x 4096) in the packed layout
+    (shard s of stripe t at t*6 MiB + s MiB, the shards as contiguous byte
+    ranges), on a contiguous pool: encode, decode {0,1} and verify, then
+    shards 0-1 overwritten, decoded and verified."""
+    from rsamd.device import StripeLayout
+    k, m, S, B = 4, 2, 1 << 20, 4096
+    name = "packed_4p2_1MiB_x4096"
+    rs = rsamd.ReedSolomon.create(k, m)
+    lay = StripeLayout.packed(B, k + m, S)
+    pool = rdev.DeviceBuffer(lay.nbytes, contiguous=True)
+    base = pool.data_ptr()
+    rdev.fill_synthetic(base, k, lay, SEED, 0, stream)
+    out = {name + "_alloc": alloc_note(pool.contiguous)}
+    t = timed(torch, stream, lambda: rdev.encode(rs, base, lay, stream), 20)
+    out[name + "_encode_GiBps"] = round(k * S * B / t / 2**30, 2)
+    out[name + "_encode_hbm_frac"] = round((k + m) * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
+    present = [False, False, True, True, True, True]
+    t = timed(torch, stream, lambda: rdev.decode(rs, base, present, lay, stream), 10)
+    out[name + "_decode_0_1_hbm_frac"] = round((k + 2) * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    t = timed(torch, stream, lambda: rdev.verify(rs, base, lay, flag.data_ptr(), stream), 5)
+    out[name + "_verify_hbm_frac"] = round((k + m) * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
+    rdev.fill_synthetic(base, 2, lay, SEED ^ 0xBAD, 0, stream)  # overwrite shards 0 and 1
+    rdev.decode(rs, base, present, lay, stream)
+    flag.zero_()
+    rdev.verify(rs, base, lay, flag.data_ptr(), stream)
+    out[name + "_verified"] = int(flag.item()) == 0
+    pool.free()
+    torch.cuda.empty_cache()
     return out
 
 
@@ -1059,11 +1097,12 @@ def profiled() -> bool:
         any(v.startswith("ROCPROF") for v in env)
 
 
-def live_pmc_traffic(seconds=90):
+def live_pmc_traffic(workload="enc42g", seconds=90):
     """HBM bytes per launch of the headline kernel, measured now: two
     rocprofv3 --pmc children (FETCH_SIZE, then WRITE_SIZE: they do not fit one
-    gfx950 TCC pass) over tools/pmc_workloads.py enc42, which fills and encodes
-    the headline batch and launches gf_vec_kernel<4,2,false> 3 times.  Bytes =
+    gfx950 TCC pass) over tools/pmc_workloads.py `workload` (enc42g: the
+    granule layout, enc42: packed), which fills and encodes the headline
+    batch and launches gf_vec_kernel<4,2,false> 3 times.  Bytes =
     (2 * FETCH_SIZE + WRITE_SIZE) KiB, MI355X_MICROARCH.md's gfx950 wide-read
     correction (tools/pmc_summary.py does the same for the committed summary).
     Median over the launches.  Returns None when rocprofv3 is missing, this
@@ -1088,7 +1127,7 @@ def live_pmc_traffic(seconds=90):
             d = os.path.join(tmp, counter)
             cmd = ["timeout", "-s", "KILL", str(seconds), rocprof, "--pmc", counter, "--output-format", "csv",
                    "-d", d, "-o", "run", "--", sys.executable, os.path.join(ROOT, "tools", "pmc_workloads.py"),
-                   "enc42"]
+                   workload]
             try:
                 p = subprocess.run(cmd, cwd=tmp, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                                    timeout=seconds + 30)
@@ -1113,13 +1152,13 @@ def live_pmc_traffic(seconds=90):
             "seconds": round(time.perf_counter() - t0, 1)}
 
 
-def pmc_traffic(k, m, S, B):
+def pmc_traffic(k, m, S, B, granule=0):
     """HBM bytes per launch from the committed rocprofv3 PMC summary for this
-    exact workload (profiles/pmc_traffic.json), or None."""
+    exact workload and layout (profiles/pmc_traffic.json), or None."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(p))
-        key = f"encode_{k}_{m}_{S}_{B}"
+        key = f"encode_{k}_{m}_{S}_{B}" + (f"_granule{granule}" if granule else "")
         return d[key]["hbm_bytes_per_launch"] if key in d else None
     except (OSError, ValueError, KeyError):
         return None

@@ -131,12 +131,15 @@ def test_live_pmc_only_at_one_gpu(monkeypatch):
     sys.path.insert(0, ROOT)
     import bench
     calls = []
-    monkeypatch.setattr(bench, "live_pmc_traffic", lambda: calls.append("pmc") or {"hbm_bytes_per_launch": 1})
+    monkeypatch.setattr(bench, "live_pmc_traffic", lambda w: calls.append(("pmc", w)) or {"hbm_bytes_per_launch": 1})
     monkeypatch.setattr(bench, "run", lambda args, live=None: calls.append(("run", args.gpus, live)))
     for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         monkeypatch.delenv(v, raising=False)
-    assert bench.main(["--gpus", "1"]) == 0
-    assert calls == ["pmc", ("run", 1, {"hbm_bytes_per_launch": 1})]
+    assert bench.main(["--gpus", "1"]) == 0  # the headline's default layout: granule
+    assert calls == [("pmc", "enc42g"), ("run", 1, {"hbm_bytes_per_launch": 1})]
+    calls.clear()
+    assert bench.main(["--gpus", "1", "--layout", "packed"]) == 0
+    assert calls == [("pmc", "enc42"), ("run", 1, {"hbm_bytes_per_launch": 1})]
     calls.clear()
     monkeypatch.setenv("WORLD_SIZE", "2")
     monkeypatch.setenv("RANK", "1")

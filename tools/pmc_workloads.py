@@ -6,7 +6,8 @@ runs every workload under FETCH_SIZE and WRITE_SIZE and turns the median
 dispatch into HBM bytes per launch (tools/pmc_summary.py).
 
 Workloads (bench.py's configs):
-  enc42      4+2 x 1 MiB x 4096, encode (the headline)  alg (4+2) S B
+  enc42g     4+2 x 1 MiB x 4096, encode, granule layout (the headline)  alg (4+2) S B
+  enc42      the same, packed shards
   dec42_01   4+2 x 1 MiB x 4096, decode {0,1}          alg (4+2) S B
   enc104p / dec104p   enc104 / dec104 with a 4 KiB pad between shards
   enc104     10+4 x 4 MiB x 128, encode                 alg 14 S B
@@ -45,7 +46,16 @@ def main():
         rdev.encode(rs, buf.data_ptr(), lay, st)
         return rs, lay, buf
 
-    if name in ("dec42_01", "dec104", "enc104", "enc42_4k", "enc42", "enc104p", "dec104p"):
+    if name == "enc42g":
+        k, m, S, B = 4, 2, 1 << 20, 4096
+        rs = rsamd.ReedSolomon.create(k, m)
+        lay = rdev.GranuleLayout.make(B, k + m, S)
+        buf = torch.empty(lay.nbytes, dtype=torch.uint8, device="cuda:0")
+        rdev.fill_synthetic(buf.data_ptr(), k, lay, SEED, 0, st)
+        fn = lambda: rdev.encode(rs, buf.data_ptr(), lay, st)  # noqa: E731
+        alg = (k + m) * S * B
+        kernel = f"gf_vec_kernel<{k}, {m}, false>"
+    elif name in ("dec42_01", "dec104", "enc104", "enc42_4k", "enc42", "enc104p", "dec104p"):
         k, m, S, B = {"dec42_01": (4, 2, 1 << 20, 4096), "dec104": (10, 4, 4 << 20, 128),
                       "enc104": (10, 4, 4 << 20, 128), "enc42_4k": (4, 2, 4096, 1 << 20),
                       "enc42": (4, 2, 1 << 20, 4096), "enc104p": (10, 4, 4 << 20, 128),
