@@ -10,8 +10,8 @@ mkdir -p gpurun_out
 OUT=gpurun_out/placement_layouts_$TAG.txt
 : > "$OUT"
 for i in $(seq 1 "$REPS"); do
-  for layout in packed granule; do
-    for alloc in contiguous hipmalloc; do
+  for layout in ${LAYOUTS:-packed granule}; do
+    for alloc in ${ALLOCS:-contiguous hipmalloc}; do
       echo "== rep $i layout $layout alloc $alloc $(date +%T)"
       timeout -k 10 120 python3 bench.py --no-extras --no-live-pmc --steps 20 --warmup 3 --layout $layout --alloc $alloc \
           > /tmp/pl.json 2> /tmp/pl.err || { tail -20 /tmp/pl.err; exit 1; }
