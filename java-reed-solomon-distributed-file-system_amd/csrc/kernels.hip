@@ -873,15 +873,14 @@ BlockOrder block_order(uint32_t chunks, uint32_t total_shards, uint64_t shard_st
                         (total_shards >= 14 && chunks >= 1024 && stripes <= 256);
     const uint32_t step = half ? chunks / 4u - 1u : 3u * chunks / 8u - 1u;
     const uint32_t rot = env_rot >= 0 ? uint32_t(env_rot) : (rotate ? step : 0u);
-    // The 4+2 granule view (64 KiB granules: 64 chunks of a 64 KiB shard
-    // stride): plain order for plans with >= 2 outputs.  On one pool, two
-    // rounds (tools/granule_decode_probe.py, profiles/r2/granule_decode_r2bq.txt):
-    // encode 0.851-0.852 plain against 0.846-0.847 remapped, decode {0,1} and
-    // {2,3} 0.851-0.852 against 0.845-0.846; one-output decodes lose in plain
-    // order ({0}: 0.783-0.798 against 0.809), so they keep the remap, and so
-    // does verify (not measured in plain order).
-    const bool granule42 = total_shards <= 6 && chunks == 64 && shard_stride == (uint64_t(64) << 10) && nout >= 2;
-    const bool xcd = env_xcd >= 0 ? env_xcd != 0 : (!rotate && !granule42);
+    // The 4+2 granule view (64 KiB granules) keeps the XCD remap.  Plain order
+    // read +0.5 points for two-output plans on one box (encode 0.850-0.851 vs
+    // 0.845-0.847 in fresh processes, profiles/r2/order_ab_headline_r2bs.txt)
+    // but -0.3 on another (0.842 vs 0.845 on one pool, granule_decode_r2bu.txt)
+    // with one 0.841 run among four (placement_layouts_r2br.txt); the remap read
+    // 0.8444-0.8467 on every box and process.  nout is kept for such rules.
+    (void)nout;
+    const bool xcd = env_xcd >= 0 ? env_xcd != 0 : !rotate;
     return BlockOrder{chunks > 1 ? rot % chunks : 0u, xcd ? n_items / 8u : 0u};
 }
 

@@ -5,7 +5,9 @@ granules G = 16 KiB .. 256 KiB, timed for encode and decodes {0}, {5}, {0,5},
 {0,1}, {2,3}, with the block-order table and with plain / XCD-contiguous order
 (rs_debug_block_order).  Legs alternated, each warmed up 0.6 s.  Fractions
 of 8 TB/s of the algorithmic bytes ((k + outputs) * S * B).
-Usage: python tools/granule_decode_probe.py [ROUNDS]"""
+Usage: python tools/granule_decode_probe.py [ROUNDS] [GRANULES_KIB] [ORDERS]
+  GRANULES_KIB: comma list (default 16,32,64,128,256)
+  ORDERS: name:rot:xcd;... (default table:-1:-1;plain:0:0;xcd:0:1)"""
 import json
 import os
 import sys
@@ -34,6 +36,9 @@ def timed(torch, st, fn, iters=8, warm_s=0.6):
 
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    granules = [int(x) << 10 for x in (sys.argv[2] if len(sys.argv) > 2 else "16,32,64,128,256").split(",")]
+    spec = sys.argv[3] if len(sys.argv) > 3 else "table:-1:-1;plain:0:0;xcd:0:1"
+    orders = [(n, int(r), int(x)) for n, r, x in (o.split(":") for o in spec.split(";"))]
     import torch
     import rsamd
     from rsamd import _lib
@@ -45,9 +50,8 @@ def main():
     base = pool.data_ptr()
     lib = _lib.load()
     legs = [("enc", None), ("dec0", (0,)), ("dec5", (5,)), ("dec05", (0, 5)), ("dec01", (0, 1)), ("dec23", (2, 3))]
-    orders = [("table", -1, -1), ("plain", 0, 0), ("xcd", 0, 1)]
     for r in range(rounds):
-        for G in (16 << 10, 32 << 10, 64 << 10, 128 << 10, 256 << 10):
+        for G in granules:
             lay = rdev.GranuleLayout.make(B, k + m, S, G)
             rdev.fill_synthetic(base, k, lay, 0x5EED, 0, st)
             rdev.encode(rs, base, lay, st)
