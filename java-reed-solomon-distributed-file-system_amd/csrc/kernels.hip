@@ -494,15 +494,14 @@ __global__ void __launch_bounds__(kWave) gf_masked_generic_kernel(MaskedArgs a) 
 
 // 8-byte-aligned kernels: batches whose base and strides are multiples of 8
 // but not of 16 -- the DFS's 1000-byte chunk groups packed back to back
-// (ChunkserverDiskRecoveryMachine.java:34-48, MasterImpl.java:794-839).  A
-// lane codes one vector of W dwords at byte 16 * v of its stripe's shards:
-// W = 4 (16 B, global_load_dwordx4 on an 8-byte-aligned address) for the
-// shard's whole 16-byte vectors, W = 2 for a last half vector (S % 16 == 8).
-// A 1000-byte shard is 62 + 1 lanes: one wave per stripe.  The other form
-// has every lane code one 8-byte vector (W = 2): 125 lanes per 1000-byte
-// shard, two waves per stripe.  K > 0 issues all K loads before the first
-// fold; K == 0 (runtime k) loads input by input.  a.nvec counts lanes'
-// vectors: whole 16-byte vectors plus the half, or 8-byte vectors.
+// (ChunkserverDiskRecoveryMachine.java:34-48, MasterImpl.java:794-839), and
+// shards below 16 KiB whose length leaves an 8-byte tail (small_with_tail8).
+// The built form: every lane codes one 8-byte vector (W = 2), 125 lanes per
+// 1000-byte shard, two waves per stripe.  The A/B form (U16): a lane codes a
+// 16-byte vector at an 8-byte-aligned address (W = 4, global_load_dwordx4)
+// and the shard's last half vector takes W = 2: 62 + 1 lanes, one wave per
+// stripe.  K > 0 issues all K loads before the first fold; K == 0 (runtime
+// k) loads input by input.  a.nvec counts lanes' vectors.
 //
 // Measured on 4 M chunk groups of 4+2 x 1000 B packed back to back
 // (tools/chunk_group_probe.py; profiles/r2/chunk_groups_r2bi.txt, cg_ab_r2bk.txt):
@@ -512,7 +511,8 @@ __global__ void __launch_bounds__(kWave) gf_masked_generic_kernel(MaskedArgs a) 
 // they replace 0.049 and 0.042.  An XOR reference of the same access pattern
 // reads 0.486 (8-byte) and 0.420 (16-byte) and its write-only half 0.325
 // (tools/group_mem.hip, profiles/r2/group_mem_r2bk.txt): the 1000-byte write
-// runs set the rate.  Both families take the 8-byte form
+// runs set the rate.  With 1 KiB slots (stride 1024) the same kernels run
+// 0.71-0.73 (chunk_groups_r2bm.txt).  Both families take the 8-byte form
 // (RSAMD_VEC8_U16 / RSAMD_MASKED8_U16 = 1 for A/B builds).
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4a8 __attribute__((ext_vector_type(4), aligned(8)));
