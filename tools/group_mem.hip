@@ -11,6 +11,8 @@
 //   sep8   read 4000 B per group from this pool, write 2000 B per group to a
 //          second pool (the same bytes, reads and writes in different pages)
 //   copy   a 16-byte copy of 16 GB into a second pool (the streaming ceiling)
+//   x8 at strides 1024 / 1008, and xal: stride 1000 with the parity region
+//          written as aligned 16-byte stores (is the partial-line write the cost?)
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/group_mem.hip -o tools/bin/group_mem
 #include <hip/hip_runtime.h>
 
@@ -63,6 +65,37 @@ __global__ void __launch_bounds__(64) x8_kernel(uint8_t *base, uint8_t *out, uin
     uint8_t *o = OP == 3 ? out + uint64_t(group) * 2 * S + v * 8 : g + 4 * S;
     st<u32x2>(o, acc);
     st<u32x2>(o + S, acc ^ u32x2{1, 1});
+}
+
+// x8 at any shard stride SS (group stride 6 * SS), in place.
+template <uint64_t SS>
+__global__ void __launch_bounds__(64) x8s_kernel(uint8_t *base) {
+    const uint32_t group = blockIdx.x >> 1, v = (blockIdx.x & 1) * 64 + threadIdx.x;
+    if (v >= S / 8) return;
+    uint8_t *g = base + uint64_t(group) * 6 * SS + v * 8;
+    u32x2 x[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = ld<u32x2>(g + i * SS);
+    const u32x2 acc = x[0] ^ x[1] ^ x[2] ^ x[3];
+    st<u32x2>(g + 4 * SS, acc);
+    st<u32x2>(g + 5 * SS, acc ^ u32x2{1, 1});
+}
+
+// Stride 1000, reads as x8, but the 2000-byte parity region of a group (16-byte
+// aligned at both ends) written as aligned 16-byte stores: wave w of the group
+// stores region bytes [1024 w, 1024 w + 1024) clipped to 2000.
+__global__ void __launch_bounds__(64) xal_kernel(uint8_t *base) {
+    const uint32_t group = blockIdx.x >> 1, w = blockIdx.x & 1, v = w * 64 + threadIdx.x;
+    uint8_t *g = base + uint64_t(group) * G;
+    u32x2 acc{0, 0};
+    if (v < S / 8) {
+        u32x2 x[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[i] = ld<u32x2>(g + v * 8 + i * S);
+        acc = x[0] ^ x[1] ^ x[2] ^ x[3];
+    }
+    const uint32_t off = w * 1024 + threadIdx.x * 16;
+    if (off < 2 * S) st<u32x4>(g + 4 * S + off, u32x4{acc[0], acc[1], acc[0] ^ 1u, acc[1] ^ 1u});
 }
 
 __global__ void __launch_bounds__(64) x16_kernel(uint8_t *base) {
@@ -119,7 +152,7 @@ static void report(const char *leg, double bytes, double ms) {
 int main(int argc, char **argv) {
     const int reps = argc > 1 ? std::atoi(argv[1]) : 10;
     const uint32_t B = 4u << 20;
-    const size_t pool = size_t(B) * G, out_bytes = size_t(B) * 2 * S;
+    const size_t pool = size_t(B) * 6 * 1024, out_bytes = size_t(B) * 2 * S;  // room for 1 KiB slots
     uint8_t *base = nullptr, *out = nullptr;
     uint32_t *sink = nullptr;
     CHECK(hipEventCreate(&e0));
@@ -141,6 +174,12 @@ int main(int argc, char **argv) {
                median_ms([&] { hipLaunchKernelGGL(x8_kernel<2>, dim3(2 * B), dim3(64), 0, 0, base, out, sink); }, reps));
         report("sep8 read 4 here -> write 2 to a second pool", all,
                median_ms([&] { hipLaunchKernelGGL(x8_kernel<3>, dim3(2 * B), dim3(64), 0, 0, base, out, sink); }, reps));
+        report("x8 stride 1024 (1 KiB slots) in place", all,
+               median_ms([&] { hipLaunchKernelGGL(x8s_kernel<1024>, dim3(2 * B), dim3(64), 0, 0, base); }, reps));
+        report("x8 stride 1008 in place", all,
+               median_ms([&] { hipLaunchKernelGGL(x8s_kernel<1008>, dim3(2 * B), dim3(64), 0, 0, base); }, reps));
+        report("xal stride 1000, parity region as aligned 16-byte stores", all,
+               median_ms([&] { hipLaunchKernelGGL(xal_kernel, dim3(2 * B), dim3(64), 0, 0, base); }, reps));
         const size_t n = size_t(16) << 30;
         report("copy 16 GB -> second pool", 2.0 * n,
                median_ms([&] { hipLaunchKernelGGL(copy_kernel, dim3(uint32_t(n / 1024)), dim3(64), 0, 0, base, out); }, reps));
