@@ -639,7 +639,8 @@ def packed_headline_leg(torch, rsamd, rdev, dev, stream):
     """The headline's stripes (4+2 x 1 MiB x 4096) in the packed layout
     (shard s of stripe t at t*6 MiB + s MiB, the shards as contiguous byte
     ranges), on a contiguous pool: encode, decode {0,1} and verify, then
-    shards 0-1 overwritten, decoded and verified."""
+    shards 0-1 overwritten, decoded and verified.  Then the headline's
+    granule layout on plain hipMalloc memory: encode and verify."""
     from rsamd.device import StripeLayout
     k, m, S, B = 4, 2, 1 << 20, 4096
     name = "packed_4p2_1MiB_x4096"
@@ -664,6 +665,20 @@ def packed_headline_leg(torch, rsamd, rdev, dev, stream):
     rdev.verify(rs, base, lay, flag.data_ptr(), stream)
     out[name + "_verified"] = int(flag.item()) == 0
     pool.free()
+    torch.cuda.empty_cache()
+    # The headline's own layout on plain hipMalloc memory (a torch tensor), for
+    # callers without rs_dev_alloc's contiguous pools.
+    glay = rdev.GranuleLayout.make(B, k + m, S)
+    buf = torch.empty(glay.nbytes, dtype=torch.uint8, device=dev)
+    rdev.fill_synthetic(buf.data_ptr(), k, glay, SEED, 0, stream)
+    t = timed(torch, stream, lambda: rdev.encode(rs, buf.data_ptr(), glay, stream), 20)
+    gname = "granule_4p2_1MiB_x4096_hipmalloc"
+    out[gname + "_encode_GiBps"] = round(k * S * B / t / 2**30, 2)
+    out[gname + "_encode_hbm_frac"] = round((k + m) * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
+    flag.zero_()
+    rdev.verify(rs, buf.data_ptr(), glay, flag.data_ptr(), stream)
+    out[gname + "_verified"] = int(flag.item()) == 0
+    del buf
     torch.cuda.empty_cache()
     return out
 

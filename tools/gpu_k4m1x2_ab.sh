@@ -1,4 +1,6 @@
 #!/bin/bash
+# (gf_vec_k4m1x2_kernel and RSAMD_K4M1X2 were removed after this A/B, run r2bx: the
+# two-chunk kernel lost; this script records how profiles/r2/ab/k4m1x2_ab_r2bx.txt was measured.)
 # A/B of the two-chunk-per-wave kernel for one-output 4-input plans
 # (gf_vec_k4m1x2_kernel; RSAMD_K4M1X2=0 keeps gf_vec_kernel<4,1>): GPU tests,
 # then tools/granule_decode_probe.py (granule view, G = 64 KiB) and
