@@ -98,6 +98,39 @@ __global__ void __launch_bounds__(64) xal_kernel(uint8_t *base) {
     if (off < 2 * S) st<u32x4>(g + 4 * S + off, u32x4{acc[0], acc[1], acc[0] ^ 1u, acc[1] ^ 1u});
 }
 
+// Stride 1000, x8's loads and per-shard spans, but each output shard's bytes
+// stored as 16-byte-aligned pairs of lanes' 8-byte vectors (the lane whose
+// address is 16-aligned takes its neighbour's half by ds_bpermute; edge lanes
+// store 8 bytes): does the store granularity alone matter?
+__global__ void __launch_bounds__(64) xpair_kernel(uint8_t *base) {
+    const uint32_t group = blockIdx.x >> 1, v = (blockIdx.x & 1) * 64 + threadIdx.x;
+    const bool act = v < S / 8;
+    uint8_t *g = base + uint64_t(group) * G + uint64_t(v) * 8;
+    u32x2 acc{0, 0};
+    if (act) {
+        u32x2 x[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[i] = ld<u32x2>(g + i * S);
+        acc = x[0] ^ x[1] ^ x[2] ^ x[3];
+    }
+    const int nb = (threadIdx.x + 1) & 63;
+    const bool nb_act = threadIdx.x < 63 && v + 1 < S / 8;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const u32x2 mine = acc ^ u32x2{uint32_t(p), uint32_t(p)};
+        const u32x2 next{uint32_t(__builtin_amdgcn_ds_bpermute(nb << 2, int(mine[0]))),
+                         uint32_t(__builtin_amdgcn_ds_bpermute(nb << 2, int(mine[1])))};
+        if (!act) continue;
+        uint8_t *q = g + (4 + p) * S;
+        const bool lead = (reinterpret_cast<uintptr_t>(q) & 15) == 0;
+        const bool prev_leads = !lead && threadIdx.x > 0;  // the lane before stored this half
+        if (lead && nb_act)
+            st<u32x4>(q, u32x4{mine[0], mine[1], next[0], next[1]});
+        else if (!prev_leads)
+            st<u32x2>(q, mine);
+    }
+}
+
 __global__ void __launch_bounds__(64) x16_kernel(uint8_t *base) {
     const uint32_t group = blockIdx.x, v = threadIdx.x;
     if (v > S / 16) return;
@@ -178,6 +211,8 @@ int main(int argc, char **argv) {
                median_ms([&] { hipLaunchKernelGGL(x8s_kernel<1024>, dim3(2 * B), dim3(64), 0, 0, base); }, reps));
         report("x8 stride 1008 in place", all,
                median_ms([&] { hipLaunchKernelGGL(x8s_kernel<1008>, dim3(2 * B), dim3(64), 0, 0, base); }, reps));
+        report("xpair stride 1000, 8-byte loads, per-shard 16-byte-aligned paired stores", all,
+               median_ms([&] { hipLaunchKernelGGL(xpair_kernel, dim3(2 * B), dim3(64), 0, 0, base); }, reps));
         report("xal stride 1000, parity region as aligned 16-byte stores", all,
                median_ms([&] { hipLaunchKernelGGL(xal_kernel, dim3(2 * B), dim3(64), 0, 0, base); }, reps));
         const size_t n = size_t(16) << 30;
