@@ -245,3 +245,27 @@ def test_granule_config3_full_size_round_trip(gpu):
     torch.cuda.synchronize()
     assert torch.equal(pool.tensor(), snap)
     pool.free()
+
+
+def test_granule_per_stripe_patterns_wide_code(gpu):
+    """k+m = 21 > 20: no pattern table, so rs_decode_granule_masked_dev builds
+    per-call records for the distinct patterns; up to 9 erasures per stripe
+    take three output groups.  Each stripe spans 2 granule rows; against the
+    oracle's encodeParity."""
+    import torch
+    import rsamd
+    from rsamd import device
+    k, m, S, n = 12, 9, 32 << 10, 6
+    lay = device.GranuleLayout.make(n, k + m, S)
+    assert lay.granule == 16 << 10
+    rng = np.random.default_rng(21)
+    want = _oracle_encode(k, m, rng.integers(0, 256, (n, k + m, S), dtype=np.uint8))
+    present = np.ones((n, k + m), dtype=bool)
+    for t, e in enumerate([9, 0, 1, 5, 9, 3]):
+        present[t, rng.choice(k + m, e, replace=False)] = False
+    clobbered = want.copy()
+    clobbered[~present] = 0x6B
+    rs = rsamd.ReedSolomon.create(k, m)
+    dev = _upload(torch, lay, clobbered)
+    device.decode_masked(rs, dev.data_ptr(), present, lay, torch.cuda.current_stream())
+    np.testing.assert_array_equal(_download(torch, lay, dev, n, k + m), want)
