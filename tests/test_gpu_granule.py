@@ -269,3 +269,7 @@ def test_granule_per_stripe_patterns_wide_code(gpu):
     dev = _upload(torch, lay, clobbered)
     device.decode_masked(rs, dev.data_ptr(), present, lay, torch.cuda.current_stream())
     np.testing.assert_array_equal(_download(torch, lay, dev, n, k + m), want)
+    # device bitmasks need the pattern table (k+m <= 20): refused before any launch
+    bits = torch.zeros(n, dtype=torch.int32, device="cuda:0")
+    with pytest.raises(rsamd.IllegalArgumentException):
+        device.decode_masked_bits(rs, dev.data_ptr(), bits.data_ptr(), lay)
