@@ -143,7 +143,9 @@ RS_API int rs_check_some_shards(const uint8_t *const *matrix_rows, const uint8_t
  * it is what a stripe-batching caller uses).  Layout: shard s of stripe t
  * starts at dev_base + t*stripe_stride + s*shard_stride; shard_len bytes are
  * coded per shard.  Fast path when dev_base, both strides are multiples of 16
- * (any shard_len); otherwise a byte-granular kernel is used.
+ * (any shard_len); when they are multiples of 8 (the DFS's 1000-byte chunk
+ * groups packed back to back), 8-byte-vector kernels; otherwise a
+ * byte-granular kernel is used.
  * ------------------------------------------------------------------------- */
 
 /* Encode parity for n_stripes stripes. */
