@@ -14,6 +14,8 @@ Workloads (bench.py's configs):
   dec104     10+4 x 4 MiB x 128, decode {0,1,2,3}       alg 14 S B
   enc42_4k   4+2 x 4 KiB x 1 M, encode                  alg 6 S B
   maskbits   4+2 x 4 KiB x 1 M, per-stripe bitmasks      alg (4 * stripes with a loss + erased shards) S
+  gmaskbits  the same in the granule layout (64 KiB rows of 16 stripes)
+  cgmaskbits / cgmaskbits1k   4+2 x 1000 B x 4 M chunk groups, stride 1000 / 1024, bitmasks
   fenc       4 GiB file -> 4+2 shards (fused)            alg file + 6 S
   fdec_05    4+2 shards {0,5} -> 4 GiB file (tiled)      alg 4 S + file
 """
@@ -81,6 +83,37 @@ def main():
         fn = lambda: rdev.decode_masked_bits(rs, buf.data_ptr(), bits.data_ptr(), lay, 0, st)  # noqa: E731
         alg = (4 * int((~present).any(axis=1).sum()) + int((~present).sum())) * S
         kernel = "gf_masked_kernel<4, 2>"
+    elif name == "gmaskbits":
+        # config[4] in the granule layout, a random pattern per stripe (<= 2 erasures)
+        k, m, S, B = 4, 2, 4096, 1 << 20
+        rs = rsamd.ReedSolomon.create(k, m)
+        lay = rdev.GranuleLayout.make(B, k + m, S)
+        buf = torch.empty(lay.nbytes, dtype=torch.uint8, device="cuda:0")
+        rdev.fill_synthetic(buf.data_ptr(), k, lay, SEED, 0, st)
+        rdev.encode(rs, buf.data_ptr(), lay, st)
+        pats = np.array([[i not in miss for i in range(6)] for e in range(3)
+                         for miss in itertools.combinations(range(6), e)], dtype=bool)
+        present = pats[np.random.default_rng(0).integers(0, len(pats), B)]
+        bits = torch.from_numpy(rdev.presence_bits(present).view(np.int32)).to("cuda:0")
+        fn = lambda: rdev.decode_masked_bits(rs, buf.data_ptr(), bits.data_ptr(), lay, 0, st)  # noqa: E731
+        alg = (4 * int((~present).any(axis=1).sum()) + int((~present).sum())) * S
+        kernel = "gf_masked_kernel<4, 2, true>"
+    elif name in ("cgmaskbits", "cgmaskbits1k"):
+        # the master's chunk groups: 4+2 x 1000 B x 4 M, stride 1000 (8-byte kernel) or 1024
+        k, m, S, B = 4, 2, 1000, 4 << 20
+        stride = 1000 if name == "cgmaskbits" else 1024
+        rs = rsamd.ReedSolomon.create(k, m)
+        lay = StripeLayout(B, S, stride, 6 * stride)
+        buf = torch.empty(lay.nbytes, dtype=torch.uint8, device="cuda:0")
+        rdev.fill_synthetic(buf.data_ptr(), k, lay, SEED, 0, st)
+        rdev.encode(rs, buf.data_ptr(), lay, st)
+        pats = np.array([[i not in miss for i in range(6)] for e in range(3)
+                         for miss in itertools.combinations(range(6), e)], dtype=bool)
+        present = pats[np.random.default_rng(0).integers(0, len(pats), B)]
+        bits = torch.from_numpy(rdev.presence_bits(present).view(np.int32)).to("cuda:0")
+        fn = lambda: rdev.decode_masked_bits(rs, buf.data_ptr(), bits.data_ptr(), lay, 0, st)  # noqa: E731
+        alg = (4 * int((~present).any(axis=1).sum()) + int((~present).sum())) * S
+        kernel = "gf_masked8_kernel<4, 2>"
     elif name == "ver104":
         k, m, S, B = 10, 4, 4 << 20, 128
         rs, lay, buf = stripes(k, m, S, B)
