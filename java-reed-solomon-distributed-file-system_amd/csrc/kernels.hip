@@ -512,7 +512,9 @@ __global__ void __launch_bounds__(kWave) gf_masked_generic_kernel(MaskedArgs a) 
 // reads 0.486 (8-byte) and 0.420 (16-byte) and its write-only half 0.325
 // (tools/group_mem.hip, profiles/r2/group_mem_r2bk.txt): the 1000-byte write
 // runs set the rate.  With 1 KiB slots (stride 1024) the same kernels run
-// 0.71-0.73 (chunk_groups_r2bm.txt).  Both families take the 8-byte form
+// 0.71-0.73 (chunk_groups_r2bm.txt).  Plain (temporal) stores, which could let
+// L2 merge the halves of a line two waves write, cost 10-14 points at either
+// stride (profiles/r2/ab/cg_st8_r2cb.txt).  Both families take the 8-byte form
 // (RSAMD_VEC8_U16 / RSAMD_MASKED8_U16 = 1 for A/B builds).
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4a8 __attribute__((ext_vector_type(4), aligned(8)));
