@@ -137,8 +137,7 @@ def main(argv=None):
             and (args.k, args.m, args.shard_bytes, args.stripes) == (4, 2, 1 << 20, 4096)):
         # before this process touches the GPU: the passes are children
         live = live_pmc_traffic("enc42" if args.layout == "packed" else "enc42g")
-    run(args, live)
-    return 0
+    return run(args, live)
 
 
 def launch_probe(args) -> int:
@@ -147,9 +146,12 @@ def launch_probe(args) -> int:
     total = parallel.sum_over_ranks(r, 1.0)
     start, count = parallel.stripe_partition(args.cfg3_stripes, r.world, r.rank)
     covered = parallel.sum_over_ranks(r, float(count))
+    # the headline's per-rank record exchange (device identities), here with
+    # host identities since the probe touches no GPU
+    recs = parallel.gather_objects(r, {"rank": r.rank, "pid": os.getpid(), "stripe0": start, "stripes": count})
     if r.rank == 0:
         print(json.dumps({"probe": True, "n_gpus": r.world, "ranks_seen": int(total), "backend": r.backend,
-                          "cfg3_stripes_covered": int(covered)}), flush=True)
+                          "cfg3_stripes_covered": int(covered), "records": recs}), flush=True)
     parallel.shutdown(r)
     return 0
 
@@ -247,23 +249,45 @@ def run(args, live_traffic=None):
         step()
         e.record(stream)
     parallel.barrier(r)
-    elapsed = parallel.max_over_ranks(r, time.perf_counter() - t0)
+    local_elapsed = time.perf_counter() - t0
+    elapsed = parallel.max_over_ranks(r, local_elapsed)
     launch_times = sorted(s.elapsed_time(e) for s, e in evs)
     launch_ms = sum(launch_times) / len(launch_times)
     median_ms = launch_times[len(launch_times) // 2]
 
-    # Verify the timed result before reporting (a wrong fast kernel is not done).
+    # Verify the timed result before reporting (a wrong fast kernel is not done):
+    # the GPU's own parity check over every stripe, and sampled stripes
+    # gathered to the host and compared with the oracle (the checker only).
     flag = torch.zeros(1, dtype=torch.int32, device=dev)
     rdev.verify(rs, buf.data_ptr(), lay, flag.data_ptr(), stream)
     ok = parallel.all_ranks_true(r, int(flag.item()) == 0)
+    oracle_check = check_vs_oracle(torch, rdev, buf, lay, k, m, S, B, stripe0, stream)
+    oracle_ok = parallel.all_ranks_true(r, oracle_check["ok"])
+
+    # Which GPU each rank ran on, and its own launch times: the line must show
+    # that N GPUs did the work (distinct devices), not N ranks on one.
+    me = dict(parallel.device_identity(torch), rank=rank, avg_launch_ms=round(launch_ms, 4),
+              median_launch_ms=round(median_ms, 4), stripe0=stripe0, stripes=count,
+              timed_region_s=round(local_elapsed, 4))
+    ranks = parallel.gather_objects(r, me)
+    distinct = parallel.distinct_devices(ranks)
+    refusal = device_refusal(r.backend, world, ranks)
+    if refusal:
+        if rank == 0:
+            print(f"bench.py: {refusal}: refusing to report", file=sys.stderr, flush=True)
+        parallel.shutdown(r)
+        return 3
+    slow_ms = max(d["avg_launch_ms"] for d in ranks)
+    fast_ms = min(d["avg_launch_ms"] for d in ranks)
 
     buf_alloc = buf.contiguous if isinstance(buf, rdev.DeviceBuffer) else None
     user_bytes = k * S * B  # per GPU per step
     value = world * user_bytes * args.steps / elapsed / 2**30
     alg_bytes = (k + m) * S * B  # per launch: each data byte read once, each parity byte written once
-    achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
+    # Per-GPU roofline of the slowest rank's kernel (at N = 1: this GPU's).
+    achieved = alg_bytes / (slow_ms * 1e-3) / 1e9
 
-    extra, cpu = {}, None
+    extra, cpu, link = {}, None, None
     if not args.no_extras:
         extra.update(decode_all_ranks(torch, parallel, r, rs, rdev, buf, lay, stream, k, m, S, B, args.steps))
         extra.update(sustained(torch, parallel, r, rs, rdev, buf, lay, stream, k, m, S, B, args.sustained_seconds))
@@ -281,11 +305,19 @@ def run(args, live_traffic=None):
             extra.update(layout_legs(torch, rsamd, dev, stream))
             cpu = cpu_baseline(k, m, S, args.cpu_seconds)
             extra["cpu_configs"] = cpu_configs()
-            extra.update(host_inclusive(rsamd, k, m))
+            link = host_link(torch)
+            extra.update(host_inclusive(rsamd, k, m, link))
             extra.update(config0_single_stripe(rsamd, k, m))
         else:
             # every rank at once: the node's aggregate host <-> device rate
-            extra.update(host_inclusive_all_ranks(rsamd, parallel, r, k, m))
+            link = host_link(torch)
+            extra.update(host_inclusive_all_ranks(rsamd, parallel, r, k, m, link))
+            # The CPU baseline at N > 1: rank 0 alone, after every GPU leg,
+            # 1 thread (the reference's single-threaded client loop).
+            parallel.barrier(r)
+            if rank == 0:
+                cpu = cpu_baseline(k, m, S, args.cpu_seconds, multi=False)
+            parallel.barrier(r, sync_gpu=False)
     traffic = pmc_traffic(k, m, S, B, 0 if args.layout == "packed" else lay.granule)
     traffic_source = "profiles/pmc_traffic.json (committed rocprofv3 --pmc summary)"
     if live_traffic and live_traffic.get("hbm_bytes_per_launch"):
@@ -314,6 +346,14 @@ def run(args, live_traffic=None):
                                else f"granule layout, {lay.granule // 1024} KiB granules"),
             },
             "verified": ok,
+            "verified_vs_oracle": oracle_ok,
+            "oracle_check": oracle_check["note"],
+            "devices": ranks,
+            "distinct_gpus": distinct,
+            "backend": r.backend,
+            "rank_avg_launch_ms_min": fast_ms,
+            "rank_avg_launch_ms_max": slow_ms,
+            "host_link": link,
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
@@ -325,6 +365,12 @@ def run(args, live_traffic=None):
                 "traffic_live": live_traffic,
                 "kernel": f"gf_vec_kernel<{k},{m},false> (rs_encode_batch_dev)",
                 "alg_bytes_per_launch": alg_bytes,
+                "achieved_basis": ("the slowest rank's mean HIP-event launch time; per GPU" if world > 1
+                                   else "mean HIP-event launch time"),
+                "frac_per_gpu_min": round(alg_bytes / (slow_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                "frac_per_gpu_max": round(alg_bytes / (fast_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                "aggregate_achieved": round(world * alg_bytes / (slow_ms * 1e-3) / 1e9, 1),
+                "aggregate_peak": world * HBM_PEAK_GBPS,
                 "avg_launch_ms": round(launch_ms, 4),
                 "median_launch_ms": round(median_ms, 4),  # SURVEY 8(d) asks for the median too
                 # also as a fraction of the measured device copy kernel
@@ -336,6 +382,52 @@ def run(args, live_traffic=None):
         }
         print(json.dumps(line), flush=True)
     parallel.shutdown(r)
+    return 0
+
+
+def device_refusal(backend, world, ranks):
+    """Why a line of `world` ranks with these device identities must not be
+    reported, or None.  Under RCCL ("nccl") every rank owns a GPU, so N ranks
+    must sit on N distinct GPUs; gloo is how ranks share one GPU on purpose
+    (rehearsals) and the line then says distinct_gpus < n_gpus."""
+    from rsamd import parallel
+    if len(ranks) != world:
+        return f"{len(ranks)} device records for {world} ranks"
+    distinct = parallel.distinct_devices(ranks)
+    if backend == "nccl" and distinct != world:
+        return f"{world} nccl ranks ran on {distinct} distinct GPU(s) ({[d.get('pci') for d in ranks]})"
+    return None
+
+
+def check_vs_oracle(torch, rdev, buf, lay, k, m, S, B, stripe0, stream):
+    """The timed batch against the oracle: stripes {0, 1, B/2, B-1} of this
+    rank are gathered to the host (rs_granule_copy_shard for the granule
+    layout, a slice copy for packed shards) and compared, data and parity
+    bytes, with the oracle's restatement of encodeParity
+    (ReedSolomon.java:90-104) on the same synthetic bytes.  The oracle is the
+    checker here: nothing it computes feeds the timed path."""
+    import numpy as np
+    from oracle import c_ref
+    c_ref.build()
+    oc = c_ref.Codec(k, m)
+    picks = sorted({0, min(1, B - 1), B // 2, B - 1})
+    ok = True
+    for t in picks:
+        got = [np.empty(S, np.uint8) for _ in range(k + m)]
+        for s_ in range(k + m):
+            if isinstance(lay, rdev.GranuleLayout):
+                rdev.copy_shard(lay, buf.data_ptr(), t, s_, got[s_].ctypes.data, False, stream)
+            else:
+                tv = buf.tensor() if isinstance(buf, rdev.DeviceBuffer) else buf
+                off = t * lay.stripe_stride + s_ * lay.shard_stride
+                got[s_][:] = tv[off: off + S].cpu().numpy()
+        torch.cuda.synchronize()
+        data = c_ref.fill_synthetic(k * S, SEED, stripe0 + t)
+        ref = [data[i * S:(i + 1) * S].copy() for i in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
+        oc.encode_parity(ref, 0, S)
+        ok = ok and all(np.array_equal(a, b) for a, b in zip(got, ref))
+    return {"ok": bool(ok), "note": f"stripes {picks} of each rank's batch, all {k + m} shards gathered from HBM "
+                                    f"after the timed region, equal to oracle/rs_oracle.c encodeParity: {bool(ok)}"}
 
 
 def stripe_pool(torch, rdev, nbytes, dev, mode):
@@ -929,15 +1021,21 @@ def cpu_rate(codec, k, m, S, present, threads, budget_s, min_stripes):
     return k * S * done / el / 2**30, done, el
 
 
-def cpu_baseline(k, m, S, budget_s):
+def cpu_baseline(k, m, S, budget_s, multi=True):
     """The oracle's scalar InputOutputByteTable loop (the reference's default
     coding loop, -O2 -fno-tree-vectorize) on host-resident stripes: 1 thread,
-    then the host's CPU share."""
+    then (multi) the host's CPU share."""
     from oracle import c_ref
     c_ref.build()
     codec = c_ref.Codec(k, m)
     rate, done, el = cpu_rate(codec, k, m, S, None, 1, budget_s, 8)
     threads, share = host_cpu_share()
+    if not multi:
+        return {"value": round(rate, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+                "sample": f"{done} stripes of {k}+{m} x {S // 1024} KiB encoded by the scalar restatement of "
+                          f"InputOutputByteTableCodingLoop (oracle/rs_oracle.c, -O2 -fno-tree-vectorize), "
+                          f"{el:.1f} s, host-resident, rank 0 after every GPU leg",
+                "cpu_model": share["cpu_model"]}
     rate_mt, done_mt, _ = cpu_rate(codec, k, m, S, None, threads, budget_s / 2, 8)
     # The same at os.cpu_count() threads (the plan's `nproc`, BASELINE.md 2):
     # on the GPU box they time-share the job's CPU quota, so this is a check
@@ -989,9 +1087,59 @@ def cpu_configs(budget_s=1.0):
 # ---------------------------------------------------------------------------
 # Host-resident legs (PCIe-inclusive; never the bench value)
 # ---------------------------------------------------------------------------
-def host_inclusive(rsamd, k, m):
+def host_link(torch, n=64 << 20, reps=8):
+    """The host <-> device link measured in this run: pinned n-byte copies
+    H2D alone, D2H alone, and both at once on two streams (SDMA), GB/s.
+    The host-inclusive legs are quoted against the bound these give."""
+    a = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    b = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    d1 = torch.empty(n, dtype=torch.uint8, device="cuda")
+    d2 = torch.empty(n, dtype=torch.uint8, device="cuda")
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def rate(fn):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps
+
+    def h2d():
+        with torch.cuda.stream(s1):
+            d1.copy_(a, non_blocking=True)
+
+    def d2h():
+        with torch.cuda.stream(s2):
+            b.copy_(d2, non_blocking=True)
+
+    def both():
+        h2d()
+        d2h()
+
+    th, td, tb = rate(h2d), rate(d2h), rate(both)
+    del a, b, d1, d2
+    return {"h2d_GBps": round(n / th / 1e9, 2), "d2h_GBps": round(n / td / 1e9, 2),
+            "both_GBps": round(2 * n / tb / 1e9, 2),
+            "note": f"pinned {n >> 20} MiB copies, {reps} reps each, torch copy_ on dedicated streams (SDMA)"}
+
+
+def link_bound_GiBps(link, up, down):
+    """User GiB/s the measured link allows for a call that moves `up` bytes
+    H2D and `down` bytes D2H per user byte: the slowest of the two directions
+    alone and both together."""
+    if not link:
+        return None
+    t = max(up / (link["h2d_GBps"] * 1e9), down / (link["d2h_GBps"] * 1e9) if down else 0.0,
+            (up + down) / (link["both_GBps"] * 1e9))
+    return round(1 / t / 2**30, 2)
+
+
+def host_inclusive(rsamd, k, m, link=None):
     """Rates of the JNI-facing host-buffer API: H2D + kernel + D2H on pageable
-    buffers, chunked and overlapped on three streams (host.cpp run_chunks)."""
+    buffers, chunked and overlapped on three streams (host.cpp run_chunks),
+    each next to the bound of the link measured in this run (host_link)."""
     import numpy as np
     from rsamd.layout import file_encode_into, file_layout
     n = 64 << 20
@@ -1030,6 +1178,19 @@ def host_inclusive(rsamd, k, m):
     del pin
     out["host_inclusive_note"] = (f"{k}+{m}, {n >> 20} MiB host shards per call, pageable unless 'pinned' "
                                   f"(file legs: a {len(data) >> 20} MiB file); PCIe-bound, never the bench value")
+    # Each leg against the link bound of its traffic (bytes up / down per user byte):
+    # encode k up, m down per k user bytes; decode {0,1} k up, 2 down; file encode
+    # 1 up, (k+m)/k down; file decode {0,k+m-1} 1 up (the k survivors), 1 + 1/k down
+    # (the file and the rebuilt data shard).
+    legs = {"host_inclusive_encode_GiBps": (1.0, m / k), "host_inclusive_pinned_encode_GiBps": (1.0, m / k),
+            "host_inclusive_decode_0_1_GiBps": (1.0, 2 / k), "host_inclusive_pinned_decode_0_1_GiBps": (1.0, 2 / k),
+            "host_inclusive_file_encode_GiBps": (1.0, (k + m) / k),
+            "host_inclusive_file_decode_0_%d_GiBps" % (k + m - 1): (1.0, 1.0 + 1.0 / k)}
+    for key, (up, down) in legs.items():
+        bound = link_bound_GiBps(link, up, down)
+        if bound and key in out:
+            out[key.replace("_GiBps", "_link_bound_GiBps")] = bound
+            out[key.replace("_GiBps", "_frac_of_link_bound")] = round(out[key] / bound, 4)
     return out
 
 
@@ -1076,7 +1237,7 @@ def config0_single_stripe(rsamd, k, m, S=64 << 10, reps=200):
     return out
 
 
-def host_inclusive_all_ranks(rsamd, parallel, r, k, m, n=64 << 20, reps=4):
+def host_inclusive_all_ranks(rsamd, parallel, r, k, m, link=None, n=64 << 20, reps=4):
     """SURVEY 8(d) host-inclusive rate at N GPUs: every rank calls the
     JNI-facing encodeParity on its own host shards at the same time (pinned,
     then pageable), bracketed by barriers; aggregate user bytes over the
@@ -1100,6 +1261,11 @@ def host_inclusive_all_ranks(rsamd, parallel, r, k, m, n=64 << 20, reps=4):
         out[f"host_inclusive_{name}_encode_all_ranks_GiBps"] = round(r.world * reps * k * n / el / 2**30, 2)
     out["host_inclusive_all_ranks_note"] = (f"{r.world} ranks at once, {k}+{m} x {n >> 20} MiB host shards per "
                                             f"call, {reps} calls per rank")
+    bound = link_bound_GiBps(link, 1.0, m / k)  # rank 0's own link, measured alone
+    if bound:
+        out["host_inclusive_rank0_link_bound_GiBps"] = bound
+        out["host_inclusive_pinned_encode_all_ranks_frac_of_N_links"] = round(
+            out["host_inclusive_pinned_encode_all_ranks_GiBps"] / (r.world * bound), 4)
     del pin, pageable
     return out
 
@@ -1136,7 +1302,6 @@ def live_pmc_traffic(workload="enc42g", seconds=90):
     vals = {}
     t0 = time.perf_counter()
     env = dict(os.environ, TMPDIR="/tmp")
-    env.pop("RSAMD_XORNET", None)  # the headline's table kernel, not the opt-in XOR network
     with tempfile.TemporaryDirectory(prefix="rsamd_pmc_", dir="/tmp") as tmp:
         for counter in ("FETCH_SIZE", "WRITE_SIZE"):
             d = os.path.join(tmp, counter)

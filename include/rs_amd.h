@@ -241,16 +241,16 @@ RS_API int rs_decode_granule_masked_bits_dev(const rs_codec *codec, uint8_t *dev
                                              const uint32_t *dev_present_bits, size_t n_stripes, size_t shard_len,
                                              size_t granule, int32_t *dev_bad_count, void *stream);
 
-/* Move one shard between a contiguous buffer and a granule batch
- * (asynchronous on stream; one 2-D copy of shard_len/G rows when G divides
- * shard_len, one contiguous run otherwise).  to_granules != 0: buf -> shard
- * `shard` of stripe `stripe`; else that shard -> buf.  buf holds shard_len
- * bytes and may be host memory (pinned or pageable) or device memory.
- * RS_E_INVALID for NULL pointers, shard_len or granule 0, neither of
- * shard_len and granule dividing the other, or a shard index outside
- * [0, total_shards). */
-RS_API int rs_granule_copy_shard(uint8_t *dev_base, int total_shards, size_t shard_len, size_t granule,
-                                 size_t stripe, int shard, void *buf, int to_granules, void *stream);
+/* Move one shard between a contiguous buffer and a granule batch of
+ * n_stripes stripes (asynchronous on stream; one 2-D copy of shard_len/G rows
+ * when G divides shard_len, one contiguous run otherwise).  to_granules != 0:
+ * buf -> shard `shard` of stripe `stripe`; else that shard -> buf.  buf holds
+ * shard_len bytes and may be host memory (pinned or pageable) or device
+ * memory.  RS_E_INVALID (nothing copied) for NULL pointers, a stripe outside
+ * [0, n_stripes), shard_len or granule 0, neither of shard_len and granule
+ * dividing the other, or a shard index outside [0, total_shards). */
+RS_API int rs_granule_copy_shard(uint8_t *dev_base, int total_shards, size_t n_stripes, size_t shard_len,
+                                 size_t granule, size_t stripe, int shard, void *buf, int to_granules, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Client file layout: ReedSolomonEncoder /
@@ -322,26 +322,6 @@ RS_API int rs_fill_synthetic_dev(uint8_t *dev_base, int data_shards, size_t n_st
 /* dst := src, n bytes, with the same 16-byte streaming kernel style (the
  * "measured device copy" the roofline is also quoted against). */
 RS_API int rs_copy_dev(uint8_t *dst, const uint8_t *src, size_t n, void *stream);
-
-/* Process-wide override of the stripe kernels' block order for placement and
- * order probes: rot = chunk rotation per stripe (0 = none), xcd = 1 for the
- * XCD-contiguous remap; rot = xcd = -1 restores the measured table. */
-RS_API int rs_debug_block_order(int rot, int xcd);
-
-/* Process-wide switch of the bitsliced XOR-network kernels (run-time compiled
- * per coefficient matrix) for launches that move at least
- * RSAMD_XORNET_MIN_BYTES (default 256 MiB): mode -1 = default (environment
- * RSAMD_XORNET, off unless "1"), 0 = off (table kernels only), 1 = on, 2 = on
- * for every launch with >= 2 KiB columns (tests).  Returns the number of
- * XOR-network kernels compiled so far in this process. */
-RS_API int rs_debug_xornet(int mode);
-
-/* The generated HIP source of the XOR-network kernel for rows (nout x nin,
- * row-major; nout <= 4), coding (verify = 0) or checking.  Writes at most cap
- * bytes (NUL-terminated when it fits) and returns the full length, or a
- * negative RS_E_* code; *ops (may be NULL) receives the VALU operation count
- * per 32 columns.  Host-only: tests emulate the kernel on the CPU with it. */
-RS_API int rs_xornet_source(const uint8_t *rows, int nin, int nout, int verify, char *buf, size_t cap, int *ops);
 
 #ifdef __cplusplus
 }

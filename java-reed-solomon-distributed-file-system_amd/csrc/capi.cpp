@@ -27,7 +27,6 @@
 #include "gf256.hpp"
 #include "host.hpp"
 #include "kernels.hpp"
-#include "xornet.hpp"
 #include "layout.hpp"
 
 struct rs_codec {
@@ -926,33 +925,10 @@ int rs_dev_free(void *ptr) {
     return RS_OK;
 }
 
-int rs_debug_block_order(int rot, int xcd) {
-    rsamd::set_debug_block_order(rot, xcd);
-    return RS_OK;
-}
-
 int rs_check_buffers_and_sizes(const rs_codec *codec, int nshards, const int64_t *shard_lens, int64_t offset,
                                int64_t byte_count) {
     if (!codec) return fail(RS_E_INVALID, "NULL codec");
     return check_buffers_and_sizes(*codec->impl, nullptr, nshards, shard_lens, offset, byte_count, false);
-}
-
-int rs_xornet_source(const uint8_t *rows, int nin, int nout, int verify, char *buf, size_t cap, int *ops) {
-    if (!rows || nin < 1 || nout < 1 || nout > rsamd::kMaxOut) return fail(RS_E_INVALID, "bad xornet shape");
-    int n = 0;
-    const std::string src = rsamd::xornet_source(rows, nin, nout, verify != 0, "rsamd_xornet", &n);
-    if (ops) *ops = n;
-    if (buf && cap) {
-        const size_t c = std::min(cap - 1, src.size());
-        std::memcpy(buf, src.data(), c);
-        buf[c] = 0;
-    }
-    return int(src.size());
-}
-
-int rs_debug_xornet(int mode) {
-    if (mode >= -1 && mode <= 2) rsamd::set_debug_xornet_mode(mode);
-    return rsamd::xornet_compiled_count();
 }
 
 size_t rs_granule_recommended(int total_shards) {
@@ -962,9 +938,11 @@ size_t rs_granule_recommended(int total_shards) {
     return g;
 }
 
-int rs_granule_copy_shard(uint8_t *dev_base, int total_shards, size_t shard_len, size_t granule, size_t stripe,
-                          int shard, void *buf, int to_granules, void *stream) {
+int rs_granule_copy_shard(uint8_t *dev_base, int total_shards, size_t n_stripes, size_t shard_len, size_t granule,
+                          size_t stripe, int shard, void *buf, int to_granules, void *stream) {
     if (!dev_base || !buf) return fail(RS_E_INVALID, "NULL pointer");
+    if (stripe >= n_stripes)
+        return fail(RS_E_INVALID, "stripe " + std::to_string(stripe) + " outside [0, " + std::to_string(n_stripes) + ")");
     if (total_shards < 1 || shard < 0 || shard >= total_shards)
         return fail(RS_E_INVALID, "shard " + std::to_string(shard) + " outside [0, " + std::to_string(total_shards) + ")");
     if (granule == 0 || shard_len == 0 || (shard_len % granule != 0 && granule % shard_len != 0))

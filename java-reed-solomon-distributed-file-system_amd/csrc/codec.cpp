@@ -17,6 +17,8 @@ const bool g_exit_hook = [] {
 }();
 }  // namespace
 
+bool process_exiting() { return g_exiting.load(); }
+
 hipError_t upload(int dev, void *dst, const void *src, size_t n) {
     // One non-blocking stream per device, created on first use and kept for the
     // process: the copy waits for nothing queued elsewhere (a hipMemcpy on the
@@ -48,6 +50,38 @@ void free_device(int dev, void *p) {
     if (cur != dev) (void)hipSetDevice(cur);
 }
 
+namespace {
+// Device copies of evicted decode plans wait here and are freed in batches:
+// hipFree synchronises the whole device, so freeing each one as the LRU
+// evicts it would stall the thread building a new plan on every stream's
+// in-flight work, once per eviction.  A kernel still using an evicted plan is
+// covered the same way (hipFree waits for it).
+constexpr size_t kDeferredFreeBatch = 64;
+std::mutex g_grave_mu;
+std::vector<std::pair<int, void *>> g_grave;
+}  // namespace
+
+void free_device_deferred(int dev, void *p) {
+    if (!p || g_exiting.load()) return;
+    std::vector<std::pair<int, void *>> batch;
+    {
+        std::lock_guard<std::mutex> lock(g_grave_mu);
+        g_grave.emplace_back(dev, p);
+        if (g_grave.size() < kDeferredFreeBatch) return;
+        batch.swap(g_grave);
+    }
+    for (auto &kv : batch) free_device(kv.first, kv.second);
+}
+
+void flush_deferred_frees() {
+    std::vector<std::pair<int, void *>> batch;
+    {
+        std::lock_guard<std::mutex> lock(g_grave_mu);
+        batch.swap(g_grave);
+    }
+    for (auto &kv : batch) free_device(kv.first, kv.second);
+}
+
 PlanLayout plan_layout(int nin, int nout) {
     PlanLayout l;
     l.tabs = 0;
@@ -70,16 +104,7 @@ DevPlan dev_plan_at(const void *base, int nin, int nout) {
 }
 
 Plan::Plan(std::vector<int> in_idx, std::vector<int> out_idx, GfMatrix rows)
-    : in_idx_(std::move(in_idx)), out_idx_(std::move(out_idx)), rows_(std::move(rows)) {
-    const int nin = int(in_idx_.size());
-    for (int g = 0; g < groups(); ++g) {
-        const int p0 = g * kMaxOut, nout = std::min<int>(kMaxOut, int(out_idx_.size()) - p0);
-        std::vector<uint8_t> r(size_t(nout) * nin);
-        for (int p = 0; p < nout; ++p)
-            for (int i = 0; i < nin; ++i) r[size_t(p) * nin + i] = rows_.at(p0 + p, i);
-        group_rows_.push_back(std::move(r));
-    }
-}
+    : in_idx_(std::move(in_idx)), out_idx_(std::move(out_idx)), rows_(std::move(rows)) {}
 
 std::vector<uint8_t> Plan::image(int g) const {
     const int nin = int(in_idx_.size());
@@ -105,8 +130,8 @@ std::vector<uint8_t> Plan::image(int g) const {
 }
 
 Plan::~Plan() {
-    for (auto &kv : dev_) free_device(kv.first, kv.second);
-    for (auto &kv : dev_file_) free_device(kv.first, kv.second);
+    for (auto &kv : dev_) free_device_deferred(kv.first, kv.second);
+    for (auto &kv : dev_file_) free_device_deferred(kv.first, kv.second);
 }
 
 hipError_t Plan::device_plans(std::vector<DevPlan> *out) const {
@@ -140,7 +165,6 @@ hipError_t Plan::device_plans(std::vector<DevPlan> *out) const {
     for (int g = 0; g < groups(); ++g) {
         const int nout = std::min<int>(kMaxOut, int(out_idx_.size()) - g * kMaxOut);
         out->push_back(dev_plan_at(static_cast<uint8_t *>(it->second) + offs[g], nin, nout));
-        out->back().rows = group_rows_[g].data();
     }
     return hipSuccess;
 }
@@ -202,6 +226,9 @@ Codec::Codec(int k, int m) : k_(k), m_(m), matrix_(build_generator(k, k + m)) {
 
 Codec::~Codec() {
     for (auto &kv : patterns_) free_device(kv.first, const_cast<uint8_t *>(kv.second.records));
+    decode_cache_.clear();  // the plans' device copies join the deferred list ...
+    encode_.reset();
+    flush_deferred_frees();  // ... and go now, with every other pending one
 }
 
 int Codec::create(int k, int m, Codec **out, std::string *err) {
@@ -230,10 +257,33 @@ int Codec::decode_plan(const uint8_t *present, std::shared_ptr<const Plan> *out,
             return RS_OK;
         }
     }
+    std::shared_ptr<const Plan> plan;
+    const int rc = make_decode_plan(present, data_only, &plan);
+    if (rc) return rc;
+    std::shared_ptr<const Plan> evicted;  // destroyed after the lock is released
+    std::lock_guard<std::mutex> lock(mu_);
+    auto it = decode_cache_.find(key);
+    if (it != decode_cache_.end()) {  // another thread built it meanwhile
+        *out = it->second.plan;
+        return RS_OK;
+    }
+    lru_.push_front(key);
+    decode_cache_.emplace(key, CacheEntry{plan, lru_.begin()});
+    if (decode_cache_.size() > kMaxDecodePlans) {
+        auto victim = decode_cache_.find(lru_.back());
+        evicted = std::move(victim->second.plan);
+        decode_cache_.erase(victim);
+        lru_.pop_back();
+    }
+    *out = plan;
+    return RS_OK;
+}
+
+int Codec::make_decode_plan(const uint8_t *present, bool data_only, std::shared_ptr<const Plan> *out) const {
     std::vector<int> surv, missing;
     for (int i = 0; i < total(); ++i) {
-        if (key[i] && int(surv.size()) < k_) surv.push_back(i);
-        if (!key[i] && (!data_only || i < k_)) missing.push_back(i);
+        if (present[i] && int(surv.size()) < k_) surv.push_back(i);
+        if (!present[i] && (!data_only || i < k_)) missing.push_back(i);
     }
     if (int(surv.size()) < k_) return RS_E_NOT_ENOUGH;
     GfMatrix dinv;
@@ -253,23 +303,7 @@ int Codec::decode_plan(const uint8_t *present, std::shared_ptr<const Plan> *out,
             for (int c = 0; c < k_; ++c) rows.at(int(r), c) = fused.at(0, c);
         }
     }
-    auto plan = std::make_shared<const Plan>(surv, missing, std::move(rows));
-    std::shared_ptr<const Plan> evicted;  // destroyed (device copy freed) after the lock is released
-    std::lock_guard<std::mutex> lock(mu_);
-    auto it = decode_cache_.find(key);
-    if (it != decode_cache_.end()) {  // another thread built it meanwhile
-        *out = it->second.plan;
-        return RS_OK;
-    }
-    lru_.push_front(key);
-    decode_cache_.emplace(key, CacheEntry{plan, lru_.begin()});
-    if (decode_cache_.size() > kMaxDecodePlans) {
-        auto victim = decode_cache_.find(lru_.back());
-        evicted = std::move(victim->second.plan);
-        decode_cache_.erase(victim);
-        lru_.pop_back();
-    }
-    *out = plan;
+    *out = std::make_shared<const Plan>(surv, missing, std::move(rows));
     return RS_OK;
 }
 
@@ -329,7 +363,9 @@ int Codec::pattern_tables(PatternTables *out, std::string *err) const {
         if (__builtin_popcount(bits) < k_) continue;
         for (int i = 0; i < T; ++i) present[i] = (bits >> i) & 1;
         std::shared_ptr<const Plan> p;
-        const int rc = decode_plan(present.data(), &p);
+        // Host-side plans only (the records are filled from them): built
+        // outside the LRU, so 2^(k+m) patterns do not flush its hot plans.
+        const int rc = make_decode_plan(present.data(), false, &p);
         if (rc == RS_E_SINGULAR) continue;  // stays -1: such stripes are skipped and counted
         if (rc) {
             *err = "decode plan";

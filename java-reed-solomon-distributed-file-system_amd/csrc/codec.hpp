@@ -47,7 +47,6 @@ public:
 private:
     std::vector<int> in_idx_, out_idx_;
     GfMatrix rows_;
-    std::vector<std::vector<uint8_t>> group_rows_;  // rows of each launch group (DevPlan::rows)
     mutable std::mutex mu_;
     mutable std::map<int, void *> dev_;       // device id -> allocation of all groups
     mutable std::map<int, void *> dev_file_;  // device id -> FileDecodePlan image
@@ -60,6 +59,11 @@ hipError_t upload(int dev, void *dst, const void *src, size_t n);
 // Device memory freed outside process teardown only: once exit() has begun the
 // HIP runtime may already be gone, and the process releases everything anyway.
 void free_device(int dev, void *p);
+// True once exit() has begun (an atexit hook): device frees are skipped then.
+bool process_exiting();
+// Frees p later, in a batch with other deferred frees (codec.cpp).
+void free_device_deferred(int dev, void *p);
+void flush_deferred_frees();
 
 // Offsets of one group's image: tabs, then in_idx, then out_idx.
 struct PlanLayout {
@@ -108,6 +112,8 @@ public:
     // decode-to-file path needs no parity).  Returns 0, RS_E_NOT_ENOUGH or
     // RS_E_SINGULAR.
     int decode_plan(const uint8_t *present, std::shared_ptr<const Plan> *out, bool data_only = false) const;
+    // The same plan built fresh, outside the cache.
+    int make_decode_plan(const uint8_t *present, bool data_only, std::shared_ptr<const Plan> *out) const;
 
     // The pattern tables on the calling thread's current device, built on
     // first use (every bitmask with >= k present bits gets decode_plan's

@@ -14,7 +14,12 @@
 #include <thread>
 
 #include "../../include/rs_amd.h"
+#include "codec.hpp"
 #include "copy_pool.hpp"
+#include "tuning.hpp"
+
+#include <sys/syscall.h>
+#include <unistd.h>
 
 namespace rsamd {
 namespace host {
@@ -24,13 +29,15 @@ void release_all(std::map<int, ThreadCtx *> &ctx);
 
 // This thread's contexts (device -> context), released when the thread exits
 // (JVM and gRPC worker pools create and retire threads) or by rs_thread_release.
-// Not for the thread that loaded the library: its thread-locals are destroyed
-// inside exit(), where the HIP runtime may already be shutting down.
-const std::thread::id g_loader_thread = std::this_thread::get_id();
+// Not for the process's main thread: its thread-locals are destroyed inside
+// exit() (glibc runs them before the atexit handlers), where the HIP runtime
+// may already be shutting down.  Whichever thread loaded the library (a JVM
+// loads it from a worker) is released like any other.
+bool on_main_thread() { return pid_t(syscall(SYS_gettid)) == getpid(); }
 struct ThreadContexts {
     std::map<int, ThreadCtx *> m;
     ~ThreadContexts() {
-        if (std::this_thread::get_id() != g_loader_thread) release_all(m);
+        if (!on_main_thread() && !process_exiting()) release_all(m);
     }
 };
 
@@ -171,7 +178,7 @@ constexpr size_t kZeroCopyBytes = size_t(64) << 20; // single-chunk calls up to 
 // slots per buffer.
 size_t chunks_per_call() {
     static const size_t v = [] {
-        const char *e = std::getenv("RSAMD_CHUNKS");
+        const char *e = tuning_env("RSAMD_CHUNKS");
         const long n = e ? std::atol(e) : 0;
         return n > 0 ? size_t(n) : size_t(8);
     }();
@@ -241,7 +248,7 @@ void release_locked(HostRegistry &reg, std::vector<uintptr_t> &held) {
 
 bool HostRegistration::lock(const std::vector<std::pair<const uint8_t *, size_t>> &ranges) {
     static const bool enabled = [] {
-        const char *e = std::getenv("RSAMD_HOST_REGISTER");
+        const char *e = tuning_env("RSAMD_HOST_REGISTER");
         return !(e && e[0] == '0');
     }();
     if (!enabled) return false;
@@ -331,7 +338,7 @@ namespace {
 // limit of the staging buffer (0 disables).
 size_t zero_copy_limit() {
     static const size_t v = [] {
-        const char *e = std::getenv("RSAMD_ZC_BYTES");
+        const char *e = tuning_env("RSAMD_ZC_BYTES");
         return e ? size_t(std::strtoull(e, nullptr, 10)) : kZeroCopyBytes;
     }();
     return v;
@@ -378,7 +385,7 @@ int run_zero_copy(ThreadCtx *ctx, size_t buf_bytes, const ChunkIo &io, const Chu
 // puts them back on the kernel stream.
 hipStream_t upload_stream(const ThreadCtx *ctx) {
     static const bool two = [] {
-        const char *e = std::getenv("RSAMD_PIPE_STREAMS");
+        const char *e = tuning_env("RSAMD_PIPE_STREAMS");
         return e && std::atoi(e) == 2;
     }();
     return two ? ctx->stream : ctx->stream3;

@@ -32,7 +32,7 @@
 #include <cstdlib>
 
 #include "gf_device.hpp"
-#include "xornet.hpp"
+#include "tuning.hpp"
 
 namespace rsamd {
 namespace {
@@ -178,6 +178,9 @@ __device__ __forceinline__ void block_item(uint32_t chunks, const FastDiv &cdiv,
 #ifndef RSAMD_VEC_AHEAD
 #define RSAMD_VEC_AHEAD 5  // gf_vec_kernel, wide codes: inputs loaded before the first fold
 #endif
+// The pair loop loads input i+q+AHEAD after folding the pair at i; with
+// AHEAD < 2 input i+1 would be read before it is loaded.
+static_assert(RSAMD_VEC_AHEAD >= 2, "RSAMD_VEC_AHEAD must be >= 2");
 #ifndef RSAMD_MASKED_WAVES
 #define RSAMD_MASKED_WAVES 7  // gf_masked_kernel: see the comment on it
 #endif
@@ -842,29 +845,23 @@ hipError_t dispatch_vec(VecArgs a, int nout, Mode mode, hipStream_t s) {
 // The XCD-contiguous remap is the default; rotation wins at 512 KiB and 1 MiB
 // shards on stripe-aligned strides and for wide (>= 14-shard) stripes of
 // >= 1 MiB, and loses badly elsewhere (2 MiB, padded strides), so it is used
-// exactly there.  RSAMD_BLOCK_ROT (rotation in chunks, 0 = off)
-// and RSAMD_BLOCK_XCD (0 / 1) override the table for A/B runs.  (Remapping
+// exactly there.  In a TUNING=1 build (tuning.hpp) RSAMD_BLOCK_ROT (rotation
+// in chunks, 0 = off) and RSAMD_BLOCK_XCD (0 / 1) override the table for A/B runs.  (Remapping
 // within groups of 8 * N blocks instead of the whole launch measured worse.)
 struct BlockOrder {
     uint32_t rot, xcd_span;
 };
-std::atomic<int> g_order_rot{-1}, g_order_xcd{-1};  // rs_debug_block_order: -1 = the table
 
 BlockOrder block_order(uint32_t chunks, uint32_t total_shards, uint64_t shard_stride, uint32_t n_items,
                        int nout = 0) {
     static const int env_rot = [] {
-        const char *e = std::getenv("RSAMD_BLOCK_ROT");
+        const char *e = tuning_env("RSAMD_BLOCK_ROT");
         return e ? std::atoi(e) : -1;
     }();
     static const int env_xcd = [] {
-        const char *e = std::getenv("RSAMD_BLOCK_XCD");
+        const char *e = tuning_env("RSAMD_BLOCK_XCD");
         return e ? std::atoi(e) : -1;
     }();
-    const int dbg_rot = g_order_rot.load(std::memory_order_relaxed), dbg_xcd = g_order_xcd.load(std::memory_order_relaxed);
-    if (dbg_rot >= 0 || dbg_xcd >= 0) {  // rs_debug_block_order (placement probes)
-        const uint32_t r = dbg_rot > 0 ? uint32_t(dbg_rot) % std::max(1u, chunks) : 0u;
-        return BlockOrder{chunks > 1 ? r : 0u, dbg_xcd > 0 ? n_items / 8u : 0u};
-    }
     const bool half = chunks == 512 && shard_stride % (uint64_t(512) << 10) == 0;
     // Wide stripes (>= 14 shards of >= 1 MiB): rotation up to 256 stripes per
     // launch, the XCD remap beyond (10+4 x 4 MiB on contiguous pools: 128 and
@@ -930,7 +927,7 @@ hipError_t launch_masked_generic_t(const MaskedArgs &a, hipStream_t s) {
 // RSAMD_MASKED_WIDE=0 routes k = 10 to the runtime-k masked kernel (A/B runs).
 bool masked_wide_enabled() {
     static const bool on = [] {
-        const char *e = std::getenv("RSAMD_MASKED_WIDE");
+        const char *e = tuning_env("RSAMD_MASKED_WIDE");
         return !(e && e[0] == '0');
     }();
     return on;
@@ -1031,7 +1028,7 @@ bool small_with_tail8(size_t len) { return len % 16 == 8 && len < 16384; }
 // RSAMD_MASKED8=0 sends 8-byte-aligned batches to the byte kernel (A/B runs).
 bool masked8_enabled() {
     static const bool on = [] {
-        const char *e = std::getenv("RSAMD_MASKED8");
+        const char *e = tuning_env("RSAMD_MASKED8");
         return !(e && e[0] == '0');
     }();
     return on;
@@ -1182,89 +1179,10 @@ hipError_t launch_vec8(const Geometry &g, const DevPlan &p, Mode mode, int *mism
     return hipSuccess;
 }
 
-std::atomic<int> g_xornet_mode{-1};  // rs_debug_xornet
-
-bool xornet_enabled_now() {
-    const int m = g_xornet_mode.load(std::memory_order_relaxed);
-    return m < 0 ? xornet_enabled() : m != 0;
-}
-
-// Launches that move at least this many bytes take the XOR-network kernels
-// (their first use of a matrix compiles it: about 0.5-2 s once per process).
-uint64_t xornet_min_bytes() {
-    static const uint64_t env = [] {
-        const char *e = std::getenv("RSAMD_XORNET_MIN_BYTES");
-        return e ? std::strtoull(e, nullptr, 10) : uint64_t(256) << 20;
-    }();
-    return g_xornet_mode.load(std::memory_order_relaxed) == 2 ? 0 : env;
-}
-
-// Block order of the XOR-network kernels: the XCD-contiguous remap unless
-// rs_debug_block_order overrides it (rot in 2 KiB chunks).
-BlockOrder xornet_block_order(uint32_t chunks, uint32_t n_items) {
-    const int dbg_rot = g_order_rot.load(std::memory_order_relaxed), dbg_xcd = g_order_xcd.load(std::memory_order_relaxed);
-    if (dbg_rot >= 0 || dbg_xcd >= 0) {
-        const uint32_t r = dbg_rot > 0 ? uint32_t(dbg_rot) % std::max(1u, chunks) : 0u;
-        return BlockOrder{chunks > 1 ? r : 0u, dbg_xcd > 0 ? n_items / 8u : 0u};
-    }
-    return BlockOrder{0u, n_items / 8u};
-}
-
-// The 2 KiB column chunks of g through the matrix's XOR-network kernel.
-// Returns hipErrorNotSupported (nothing launched) when the kernel cannot be
-// had; the caller then codes everything with the table kernels.
-hipError_t launch_gf_xornet(const Geometry &g, const DevPlan &p, Mode mode, int *mismatch, hipStream_t s,
-                            size_t *done_cols) {
-    hipFunction_t fn = nullptr;
-    std::string err;
-    if (xornet_function(p.rows, p.nin, p.nout, mode == Mode::Verify, &fn, &err) != hipSuccess)
-        return hipErrorNotSupported;
-    const size_t chunks = g.len / kXorChunk;
-    const size_t stripes_per_launch = std::max<size_t>(1, kMaxGridBlocks / chunks);
-    for (size_t t0 = 0; t0 < g.n_stripes; t0 += stripes_per_launch) {
-        const size_t nst = std::min(stripes_per_launch, g.n_stripes - t0);
-        const FastDiv d = make_fastdiv(uint32_t(chunks));
-        const uint32_t n_items = uint32_t(nst * chunks);
-        const BlockOrder o = xornet_block_order(uint32_t(chunks), n_items);
-        XorNetArgs a{g.base + g.col0 + t0 * g.stripe_stride, p.in_idx, p.out_idx, g.stripe_stride, g.shard_stride,
-                     uint32_t(chunks), n_items, d.m, d.s1, d.s2, o.xcd_span, o.rot, mismatch};
-        const hipError_t e = launch_xornet(fn, a, s);
-        if (e != hipSuccess) return e;
-    }
-    *done_cols = chunks * kXorChunk;
-    return hipSuccess;
-}
-
 }  // namespace
 
 hipError_t launch_gf(const Geometry &g, const DevPlan &p, Mode mode, int *mismatch, hipStream_t s) {
-    if (g.n_stripes == 0 || g.len == 0 || p.nout == 0) return hipSuccess;
-    const bool aligned = (reinterpret_cast<uintptr_t>(g.base + g.col0) % 16 == 0) && g.shard_stride % 16 == 0 &&
-                         g.stripe_stride % 16 == 0;
-    const uint64_t moved = uint64_t(g.n_stripes) * g.len * uint64_t(p.nin + p.nout);
-    if (p.rows && aligned && g.len >= kXorChunk && g.len / kXorChunk <= kMaxGridBlocks &&
-        p.nout <= kMaxOut && xornet_enabled_now() && moved >= xornet_min_bytes()) {
-        size_t done = 0;
-        const hipError_t e = launch_gf_xornet(g, p, mode, mismatch, s, &done);
-        // No kernel for this matrix (compile failure): the table kernels code
-        // it, except under rs_debug_xornet(2), where tests want to know.
-        if (e == hipErrorNotSupported && g_xornet_mode.load(std::memory_order_relaxed) == 2) return hipErrorInvalidImage;
-        if (e != hipErrorNotSupported) {
-            if (e != hipSuccess || done == g.len) return e;
-            Geometry rest = g;  // the last < 2 KiB of columns
-            rest.col0 += done;
-            rest.len -= done;
-            return launch_gf_tables(rest, p, mode, mismatch, s);
-        }
-    }
     return launch_gf_tables(g, p, mode, mismatch, s);
-}
-
-void set_debug_xornet_mode(int mode) { g_xornet_mode.store(mode); }
-
-void set_debug_block_order(int rot, int xcd) {
-    g_order_rot.store(rot);
-    g_order_xcd.store(xcd);
 }
 
 hipError_t launch_fill_synthetic(uint8_t *base, int k, size_t n_stripes, size_t shard_len, size_t shard_stride,

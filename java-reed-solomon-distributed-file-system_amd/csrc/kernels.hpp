@@ -21,10 +21,6 @@ struct DevPlan {
     const int32_t *in_idx = nullptr;
     const int32_t *out_idx = nullptr;
     int nin = 0, nout = 0;
-    // The coefficient rows in HOST memory (nout x nin, row-major; owned by the
-    // Plan) for the run-time compiled XOR-network kernels (xornet.hpp); null
-    // for per-call plans, which always take the table kernels.
-    const uint8_t *rows = nullptr;
 };
 
 // Stripe-batched layout: shard s of stripe t at base + t*stripe_stride + s*shard_stride,
@@ -80,10 +76,5 @@ hipError_t launch_fill_synthetic(uint8_t *base, int k, size_t n_stripes, size_t 
                                  uint64_t stripe0, hipStream_t s);
 
 hipError_t launch_copy(uint8_t *dst, const uint8_t *src, size_t n, hipStream_t s);
-// Overrides the block-order table of the stripe kernels (rot in chunks, xcd 0/1;
-// both -1 = the table).  Placement probes only (rs_debug_block_order).
-void set_debug_block_order(int rot, int xcd);
-// rs_debug_xornet: -1 default, 0 off, 1 on, 2 on at any size.
-void set_debug_xornet_mode(int mode);
 
 }  // namespace rsamd

@@ -24,6 +24,7 @@
 #include <cstdlib>
 
 #include "gf_device.hpp"
+#include "tuning.hpp"
 
 namespace rsamd {
 namespace {
@@ -575,7 +576,7 @@ __global__ void __launch_bounds__(kThreads) split_merge_kernel(CopyArgs a) {
 
 int file_io_mode() {
     static const int v = [] {
-        const char *e = std::getenv("RSAMD_LAYOUT_IO");
+        const char *e = tuning_env("RSAMD_LAYOUT_IO");
         return e ? std::atoi(e) : int(IO_PLAIN8);
     }();
     return v;
@@ -585,7 +586,7 @@ int file_io_mode() {
 // remap off for A/B runs).
 uint32_t file_xcd_span(uint64_t n_blocks) {
     static const bool on = [] {
-        const char *e = std::getenv("RSAMD_FILE_XCD");
+        const char *e = tuning_env("RSAMD_FILE_XCD");
         return !(e && e[0] == '0');
     }();
     return on ? uint32_t(n_blocks / 8u) : 0u;
@@ -649,7 +650,7 @@ struct DecTile {
 
 DecTile dec_tile() {
     static const DecTile v = [] {
-        const char *e = std::getenv("RSAMD_DEC_TILE");  // "threads,slots" (A/B)
+        const char *e = tuning_env("RSAMD_DEC_TILE");  // "threads,slots" (A/B)
         DecTile d{kDecTileThreads, kDecTileSlots};
         if (e) {
             int t = 0, sl = 0;
@@ -705,7 +706,7 @@ hipError_t launch_file_encode_fused(const FileGeom &g, const DevPlan *parity0, h
     // tiled one measured 0.67-0.78 of peak against 0.72-0.78 across boxes
     // (profiles/r1/file_decode_ab/).
     // RSAMD_FILE_ENCODE=1 selects it (A/B).
-    const char *mode = std::getenv("RSAMD_FILE_ENCODE");
+    const char *mode = tuning_env("RSAMD_FILE_ENCODE");
     uint32_t R = tile_rows(g);
     if (R && (g.S / g.block + R - 1) / R * uint64_t(kTileThreads) > UINT32_MAX) R = 0;  // grid > 2^32 work-items
     if (R && aligned(g.file, 16) && mode && mode[0] == '1') {
@@ -740,7 +741,7 @@ hipError_t launch_file_decode_fused(const FileGeom &g, const FileDecodePlan &p, 
     if (g.S == 0 || g.file_len == 0) return hipSuccess;
     uint32_t R = tile_rows(g, dec_tile().threads, dec_tile().slots);
     if (R && (g.S / g.block + R - 1) / R * uint64_t(dec_tile().threads) > UINT32_MAX) R = 0;  // grid > 2^32 work-items
-    const char *mode = std::getenv("RSAMD_FILE_DECODE");
+    const char *mode = tuning_env("RSAMD_FILE_DECODE");
     if (R && !(mode && mode[0] == '0')) {  // RSAMD_FILE_DECODE=0 selects the untiled kernel (A/B only)
         TileArgs a{g.file_out, g.file_len, g.shards, g.shard_stride, g.S / g.block, uint32_t(g.block), R,
                    uint32_t((uint64_t(1) << 32) / g.block + 1), uint32_t((uint64_t(1) << 32) / (uint64_t(g.k) * g.block) + 1),

@@ -64,13 +64,10 @@ SIGNATURES = {
                                         C.c_uint64, C.c_uint64, C.c_void_p]),
     "rs_copy_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     "rs_granule_recommended": (C.c_size_t, [C.c_int]),
-    "rs_granule_copy_shard": (C.c_int, [C.c_void_p, C.c_int, C.c_size_t, C.c_size_t, C.c_size_t, C.c_int,
-                                        C.c_void_p, C.c_int, C.c_void_p]),
+    "rs_granule_copy_shard": (C.c_int, [C.c_void_p, C.c_int, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t,
+                                        C.c_int, C.c_void_p, C.c_int, C.c_void_p]),
     "rs_dev_alloc": (C.c_int, [C.POINTER(C.c_void_p), C.c_size_t, C.c_int, C.POINTER(C.c_int)]),
     "rs_dev_free": (C.c_int, [C.c_void_p]),
-    "rs_debug_block_order": (C.c_int, [C.c_int, C.c_int]),
-    "rs_debug_xornet": (C.c_int, [C.c_int]),
-    "rs_xornet_source": (C.c_int, [u8p, C.c_int, C.c_int, C.c_int, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]),
 }
 
 _lib = None

@@ -101,9 +101,15 @@ def _kernel_layout(lay) -> StripeLayout:
 def copy_shard(lay: GranuleLayout, dev_base: int, stripe: int, shard: int, buf: int, to_granules: bool,
                stream=None) -> None:
     """rs_granule_copy_shard: one shard between a contiguous buffer `buf`
-    (host or device address, shard_len bytes) and the granule batch."""
-    check(_lib.load().rs_granule_copy_shard(C.c_void_p(dev_base), lay.total_shards, lay.shard_len, lay.granule,
-                                            stripe, shard, C.c_void_p(buf), int(bool(to_granules)),
+    (host or device address, shard_len bytes) and the granule batch.
+    ValueError for a stripe or shard outside the batch (the library checks
+    them too, with RS_E_INVALID)."""
+    if not 0 <= stripe < lay.n_stripes:
+        raise ValueError(f"stripe {stripe} outside [0, {lay.n_stripes})")
+    if not 0 <= shard < lay.total_shards:
+        raise ValueError(f"shard {shard} outside [0, {lay.total_shards})")
+    check(_lib.load().rs_granule_copy_shard(C.c_void_p(dev_base), lay.total_shards, lay.n_stripes, lay.shard_len,
+                                            lay.granule, stripe, shard, C.c_void_p(buf), int(bool(to_granules)),
                                             C.c_void_p(_stream_handle(stream))))
 
 

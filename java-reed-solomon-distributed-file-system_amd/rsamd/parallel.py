@@ -3,8 +3,10 @@
 Stripes are independent: GPU g owns a contiguous range
 of stripe indices and codes it with no data-path collective.  torch.distributed
 is used only to line ranks up for timing and to reduce a few scalars (elapsed
-time, verification flags).  The backend is RCCL ("nccl") on GPU nodes; set
-RSAMD_DIST_BACKEND=gloo to run several ranks on one GPU or on CPU.
+time, verification flags, device identities).  The backend is RCCL ("nccl")
+when every rank of this node has a GPU of its own (LOCAL_WORLD_SIZE <= visible
+devices, so a multi-node job keeps RCCL); gloo when ranks share a GPU or run on
+CPU.  RSAMD_DIST_BACKEND=gloo|nccl overrides the choice.
 """
 from __future__ import annotations
 
@@ -44,8 +46,10 @@ def init_from_env(use_gpu: bool = True) -> Rank:
     import torch
     if backend is None:
         # RCCL needs a device of its own per rank; ranks that share a GPU (more
-        # ranks than devices, e.g. a rehearsal on a one-GPU box) line up over gloo.
-        backend = "nccl" if use_gpu and torch.cuda.device_count() >= world else "gloo"
+        # ranks on this node than devices, e.g. a rehearsal on a one-GPU box)
+        # line up over gloo.  Per node: LOCAL_WORLD_SIZE, not WORLD_SIZE.
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+        backend = "nccl" if use_gpu and torch.cuda.device_count() >= local_world else "gloo"
     if use_gpu:
         torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     if world > 1:
@@ -95,3 +99,36 @@ def shutdown(r: Rank) -> None:
         import torch.distributed as dist
         if dist.is_initialized():
             dist.destroy_process_group()
+
+
+def gather_objects(r: Rank, obj) -> list:
+    """obj from every rank, in rank order (a one-element list at world 1)."""
+    if not r.distributed:
+        return [obj]
+    import torch.distributed as dist
+    out = [None] * r.world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def device_identity(torch) -> dict:
+    """This rank's GPU: torch index, PCI address (domain:bus:device) and UUID
+    as the runtime reports them (None where the runtime has no field)."""
+    idx = torch.cuda.current_device()
+    p = torch.cuda.get_device_properties(idx)
+    pci = None
+    if all(hasattr(p, a) for a in ("pci_domain_id", "pci_bus_id", "pci_device_id")):
+        pci = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+    uuid = getattr(p, "uuid", None)
+    return {"index": idx, "pci": pci, "uuid": str(uuid) if uuid is not None else None, "name": p.name,
+            "visible_devices": os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES")
+            or os.environ.get("CUDA_VISIBLE_DEVICES")}
+
+
+def distinct_devices(identities) -> int:
+    """Distinct physical GPUs among rank identities (by PCI address, else
+    UUID, else torch index)."""
+    keys = set()
+    for d in identities:
+        keys.add(d.get("pci") or d.get("uuid") or f"index{d.get('index')}")
+    return len(keys)

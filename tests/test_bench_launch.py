@@ -43,6 +43,9 @@ def test_self_launch_two_ranks():
     got = lines[0]
     assert got["n_gpus"] == 2 and got["ranks_seen"] == 2 and got["backend"] == "gloo"
     assert got["cfg3_stripes_covered"] == 1024
+    recs = got["records"]  # gathered in rank order, one per process
+    assert [d["rank"] for d in recs] == [0, 1] and len({d["pid"] for d in recs}) == 2
+    assert [(d["stripe0"], d["stripes"]) for d in recs] == [(0, 512), (512, 512)]
 
 
 def test_world_size_mismatch_refused():
@@ -132,7 +135,7 @@ def test_live_pmc_only_at_one_gpu(monkeypatch):
     import bench
     calls = []
     monkeypatch.setattr(bench, "live_pmc_traffic", lambda w: calls.append(("pmc", w)) or {"hbm_bytes_per_launch": 1})
-    monkeypatch.setattr(bench, "run", lambda args, live=None: calls.append(("run", args.gpus, live)))
+    monkeypatch.setattr(bench, "run", lambda args, live=None: calls.append(("run", args.gpus, live)) or 0)
     for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         monkeypatch.delenv(v, raising=False)
     assert bench.main(["--gpus", "1"]) == 0  # the headline's default layout: granule
@@ -146,3 +149,31 @@ def test_live_pmc_only_at_one_gpu(monkeypatch):
     monkeypatch.setenv("LOCAL_RANK", "1")
     assert bench.main(["--gpus", "2"]) == 0
     assert calls == [("run", 2, None)]
+
+
+def test_device_refusal_under_nccl():
+    """N nccl ranks must sit on N distinct GPUs; gloo rehearsals may share one."""
+    sys.path.insert(0, ROOT)
+    import bench
+    a = {"index": 0, "pci": "0000:05:00", "uuid": "u0"}
+    b = {"index": 1, "pci": "0000:15:00", "uuid": "u1"}
+    same = dict(a, index=1)
+    assert bench.device_refusal("nccl", 2, [a, b]) is None
+    msg = bench.device_refusal("nccl", 2, [a, same])
+    assert msg and "1 distinct GPU" in msg
+    assert bench.device_refusal("gloo", 2, [a, same]) is None
+    assert bench.device_refusal("nccl", 2, [a]) is not None  # a missing record
+    # no PCI address: the UUID tells the devices apart
+    assert bench.device_refusal("nccl", 2, [dict(a, pci=None), dict(b, pci=None)]) is None
+
+
+def test_link_bound():
+    """link_bound_GiBps: the slowest of H2D, D2H and both directions at once."""
+    sys.path.insert(0, ROOT)
+    import bench
+    link = {"h2d_GBps": 50.0, "d2h_GBps": 50.0, "both_GBps": 90.0}
+    # 4+2 encode: 1 byte up, 0.5 down per user byte -> H2D-bound, 50 GB/s of user data
+    assert abs(bench.link_bound_GiBps(link, 1.0, 0.5) - 50e9 / 2**30) < 0.01
+    # 1 up, 1 down: both directions together bind (90 GB/s over 2 bytes)
+    assert abs(bench.link_bound_GiBps(link, 1.0, 1.0) - 45e9 / 2**30) < 0.01
+    assert bench.link_bound_GiBps(None, 1.0, 0.5) is None

@@ -247,6 +247,53 @@ def test_granule_config3_full_size_round_trip(gpu):
     pool.free()
 
 
+def test_granule_headline_full_size_round_trip(gpu):
+    """The bench headline's own batch at full size: 4+2 x 1 MiB x 4096
+    stripes in the granule layout, G = 64 KiB, on a contiguous pool
+    (BASELINE configs[1]).  Encode, verify clean, stripes {0, 1, 2048, 4095}
+    gathered and compared with the oracle (data from the synthetic fill,
+    parity from encodeParity, ReedSolomon.java:90-104); then shards 0 and 5 of
+    EVERY stripe overwritten -- the erasure pattern of ReedSolomonTest.java:77-93
+    -- decoded, and the whole 24 GiB batch compared byte for byte with the
+    encoded one."""
+    import torch
+    import rsamd
+    from rsamd import device
+    k, m, S, n = 4, 2, 1 << 20, 4096
+    lay = device.GranuleLayout.make(n, k + m, S)
+    assert lay.granule == 64 << 10
+    pool = device.DeviceBuffer(lay.nbytes, contiguous=True)
+    st = torch.cuda.current_stream()
+    base = pool.data_ptr()
+    device.fill_synthetic(base, k, lay, 0x5EED, 0, st)
+    rs = rsamd.ReedSolomon.create(k, m)
+    device.encode(rs, base, lay, st)
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    device.verify(rs, base, lay, flag.data_ptr(), st)
+    assert int(flag.item()) == 0
+    oc = c_ref.Codec(k, m)
+    for t in (0, 1, n // 2, n - 1):
+        got = np.zeros((k + m, S), dtype=np.uint8)
+        for s in range(k + m):
+            device.copy_shard(lay, base, t, s, got[s].ctypes.data, False, st)
+        torch.cuda.synchronize()
+        data = c_ref.fill_synthetic(k * S, 0x5EED, t)
+        want = np.zeros_like(got)
+        want[:k] = data.reshape(k, S)
+        oc.encode_parity([want[i] for i in range(k + m)], 0, S)
+        np.testing.assert_array_equal(got, want)
+    snap = pool.tensor().clone()
+    rows = pool.tensor().view(lay.rows, k + m, lay.granule)
+    rows[:, 0] = 0x5A  # shard 0 (DataDiskOne) of every stripe
+    rows[:, 5] = 0xA5  # shard 5 (ParityDiskTwo)
+    device.decode(rs, base, [False, True, True, True, True, False], lay, st)
+    torch.cuda.synchronize()
+    assert torch.equal(pool.tensor(), snap)
+    del snap, rows
+    pool.free()
+    torch.cuda.empty_cache()
+
+
 def test_granule_per_stripe_patterns_wide_code(gpu):
     """k+m = 21 > 20: no pattern table, so rs_decode_granule_masked_dev builds
     per-call records for the distinct patterns; up to 9 erasures per stripe

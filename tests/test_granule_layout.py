@@ -138,14 +138,28 @@ def test_copy_shard_argument_checks(native):
     buf = (C.c_uint8 * 64)()
     base = C.c_void_p(C.addressof(buf))
     f = native.rs_granule_copy_shard
-    assert f(None, 6, 4096, 1024, 0, 0, base, 1, None) == RS_E_INVALID       # NULL base
-    assert f(base, 6, 4096, 1024, 0, 0, None, 1, None) == RS_E_INVALID       # NULL buf
-    assert f(base, 6, 4096, 1024, 0, 6, base, 1, None) == RS_E_INVALID       # shard out of range
-    assert f(base, 6, 4096, 1024, 0, -1, base, 1, None) == RS_E_INVALID
-    assert f(base, 6, 4096, 3000, 0, 0, base, 1, None) == RS_E_INVALID       # neither divides the other
+    assert f(None, 6, 4, 4096, 1024, 0, 0, base, 1, None) == RS_E_INVALID       # NULL base
+    assert f(base, 6, 4, 4096, 1024, 0, 0, None, 1, None) == RS_E_INVALID       # NULL buf
+    assert f(base, 6, 4, 4096, 1024, 0, 6, base, 1, None) == RS_E_INVALID       # shard out of range
+    assert f(base, 6, 4, 4096, 1024, 0, -1, base, 1, None) == RS_E_INVALID
+    assert f(base, 6, 4, 4096, 1024, 4, 0, base, 1, None) == RS_E_INVALID       # stripe out of range
+    assert b"stripe 4 outside [0, 4)" in native.rs_last_error_message()
+    assert f(base, 6, 0, 4096, 1024, 0, 0, base, 0, None) == RS_E_INVALID       # empty batch
+    assert f(base, 6, 4, 4096, 3000, 0, 0, base, 1, None) == RS_E_INVALID       # neither divides the other
     assert b"must divide one another" in native.rs_last_error_message()
-    assert f(base, 6, 4096, 0, 0, 0, base, 1, None) == RS_E_INVALID          # granule 0
-    assert f(base, 6, 0, 1024, 0, 0, base, 1, None) == RS_E_INVALID          # shard_len 0
+    assert f(base, 6, 4, 4096, 0, 0, 0, base, 1, None) == RS_E_INVALID          # granule 0
+    assert f(base, 6, 4, 0, 1024, 0, 0, base, 1, None) == RS_E_INVALID          # shard_len 0
+
+
+def test_copy_shard_python_checks():
+    """device.copy_shard refuses a stripe or shard outside the batch before
+    calling the library (no GPU needed)."""
+    from rsamd import device
+    from rsamd.device import GranuleLayout
+    lay = GranuleLayout.make(4, 6, 4096, 1024)
+    for stripe, shard in ((4, 0), (-1, 0), (0, 6), (0, -1)):
+        with pytest.raises(ValueError):
+            device.copy_shard(lay, 1 << 20, stripe, shard, 1 << 21, True)
 
 
 def test_granule_masked_argument_checks(native):

@@ -151,8 +151,6 @@ def main():
             alg, kernel = 4 * S + n, "file_decode_tiled_kernel<4, 1"
     else:
         raise SystemExit(f"unknown workload {name}")
-    if kernel.startswith("gf_vec_kernel") and os.environ.get("RSAMD_XORNET") == "1":
-        kernel = "rsamd_xornet"  # large launches take the run-time compiled XOR-network kernel (xornet.cpp)
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
