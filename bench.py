@@ -422,8 +422,9 @@ def check_vs_oracle(torch, rdev, buf, lay, k, m, S, B, stripe0, stream):
                 off = t * lay.stripe_stride + s_ * lay.shard_stride
                 got[s_][:] = tv[off: off + S].cpu().numpy()
         torch.cuda.synchronize()
-        data = c_ref.fill_synthetic(k * S, SEED, stripe0 + t)
-        ref = [data[i * S:(i + 1) * S].copy() for i in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
+        data = c_ref.synthetic_shards(k, S, SEED, stripe0 + t,
+                                      lay.granule if isinstance(lay, rdev.GranuleLayout) else 0)
+        ref = [data[i].copy() for i in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
         oc.encode_parity(ref, 0, S)
         ok = ok and all(np.array_equal(a, b) for a, b in zip(got, ref))
     return {"ok": bool(ok), "note": f"stripes {picks} of each rank's batch, all {k + m} shards gathered from HBM "

@@ -209,3 +209,22 @@ def fill_synthetic(n_bytes: int, seed: int, stripe: int, start_byte: int = 0) ->
     out = np.zeros(n_bytes, dtype=np.uint8)
     lib().orc_fill_synthetic(ptr(out), n_bytes, seed, stripe, start_byte)
     return out
+
+
+def synthetic_shards(k: int, S: int, seed: int, stripe: int, granule: int = 0) -> np.ndarray:
+    """The k data shards (k x S) that rs_fill_synthetic_dev writes for global
+    stripe `stripe`: packed batches generate k*S bytes per stripe; a granule
+    batch (rsamd.device.fill_synthetic on a GranuleLayout) generates k*G bytes
+    per granule row of its view, row r = (stripe*S + c) // G for column c."""
+    if not granule:
+        return fill_synthetic(k * S, seed, stripe).reshape(k, S)
+    out = np.empty((k, S), dtype=np.uint8)
+    c = 0
+    while c < S:
+        x = stripe * S + c
+        r, o = divmod(x, granule)
+        n = min(granule - o, S - c)
+        row = fill_synthetic(k * granule, seed, r).reshape(k, granule)
+        out[:, c:c + n] = row[:, o:o + n]
+        c += n
+    return out

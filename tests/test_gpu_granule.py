@@ -277,9 +277,8 @@ def test_granule_headline_full_size_round_trip(gpu):
         for s in range(k + m):
             device.copy_shard(lay, base, t, s, got[s].ctypes.data, False, st)
         torch.cuda.synchronize()
-        data = c_ref.fill_synthetic(k * S, 0x5EED, t)
         want = np.zeros_like(got)
-        want[:k] = data.reshape(k, S)
+        want[:k] = c_ref.synthetic_shards(k, S, 0x5EED, t, lay.granule)
         oc.encode_parity([want[i] for i in range(k + m)], 0, S)
         np.testing.assert_array_equal(got, want)
     snap = pool.tensor().clone()

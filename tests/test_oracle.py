@@ -193,3 +193,19 @@ def test_error_contract(oracle_lib):
         c.decode_missing(sh, [True, True, True, False, False, False], 0, 10)
     with pytest.raises(ValueError, match="^too many shards - max is 256$"):
         oracle_lib.Codec(200, 57)
+
+
+def test_synthetic_shards_granule_rows(oracle_lib):
+    """synthetic_shards: a granule batch's stripe is assembled from the k*G
+    fills of its view's rows (rows of several stripes, or stripes of several rows)."""
+    k, S, G = 4, 4096, 1024
+    for t in (0, 3):
+        got = oracle_lib.synthetic_shards(k, S, 7, t, G)
+        for j in range(S // G):
+            row = oracle_lib.fill_synthetic(k * G, 7, t * (S // G) + j).reshape(k, G)
+            np.testing.assert_array_equal(got[:, j * G:(j + 1) * G], row)
+    S, G = 1024, 4096  # 4 stripes per row
+    got = oracle_lib.synthetic_shards(k, S, 7, 6, G)
+    row = oracle_lib.fill_synthetic(k * G, 7, 1).reshape(k, G)
+    np.testing.assert_array_equal(got, row[:, 2048:3072])
+    np.testing.assert_array_equal(oracle_lib.synthetic_shards(k, S, 7, 6), oracle_lib.fill_synthetic(k * S, 7, 6).reshape(k, S))
