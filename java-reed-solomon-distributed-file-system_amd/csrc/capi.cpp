@@ -695,7 +695,7 @@ int rs_encode_batch_dev(const rs_codec *codec, uint8_t *dev_base, size_t n_strip
     if (!c || (!dev_base && n_stripes && shard_len)) return fail(RS_E_INVALID, "NULL codec or device base");
     std::vector<DevPlan> plans;
     RS_HIP(c->encode_plan().device_plans(&plans));
-    Geometry g{dev_base, n_stripes, 0, shard_len, shard_stride, stripe_stride};
+    Geometry g{dev_base, n_stripes, 0, shard_len, shard_stride, stripe_stride, c->total()};
     for (const DevPlan &p : plans)
         RS_HIP(rsamd::launch_gf(g, p, Mode::Code, nullptr, static_cast<hipStream_t>(stream)));
     return RS_OK;
@@ -715,7 +715,7 @@ int rs_decode_batch_dev(const rs_codec *codec, uint8_t *dev_base, const uint8_t 
     if (rc) return fail(rc, rc == RS_E_SINGULAR ? "Matrix is singular" : "Not enough shards present");
     std::vector<DevPlan> plans;
     RS_HIP(plan->device_plans(&plans));
-    Geometry g{dev_base, n_stripes, 0, shard_len, shard_stride, stripe_stride};
+    Geometry g{dev_base, n_stripes, 0, shard_len, shard_stride, stripe_stride, c->total()};
     for (const DevPlan &p : plans)
         RS_HIP(rsamd::launch_gf(g, p, Mode::Code, nullptr, static_cast<hipStream_t>(stream)));
     return RS_OK;

@@ -660,6 +660,105 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(8, 8
                              a.nin, M, a.shard_stride, a.mismatch);
 }
 
+// ---------------------------------------------------------------------------
+// Line-owner kernel for chunk groups packed back to back: the master's
+// 6 x 1000-byte groups (ChunkserverDiskRecoveryMachine.java:34-48,
+// MasterImpl.java:794-839) at shard stride 1000, group stride 6000.  There
+// a group's written region -- its output shards, consecutive, e.g. parity
+// 4-5 -- starts and ends inside 128-byte lines, and the 8-byte kernels above
+// write it as 1000-byte runs split over two waves: lines written piecewise by
+// two waves, and a partially written line at each end of the region.  HBM
+// serves partial lines with read-modify-writes (PMC: 1.055x the algorithmic
+// bytes, 0.59 of peak against 0.72 for the same groups in 1 KiB slots).
+//
+// Here ONE wave owns every 128-byte line the region touches.  Phase 1: each
+// lane codes 8-byte columns of all M outputs and parks them in LDS in the
+// region's byte order.  The bytes of the region's first and last line that
+// lie outside it belong to input shards of this group or of its neighbour
+// (never to an output shard of this launch: outputs are one run per group and
+// the runs are >= 256 bytes apart), so the wave loads them too.  Phase 2: the
+// wave stores whole lines from LDS as aligned 16-byte non-temporal stores --
+// the foreign bytes written back with the values just read -- so HBM never
+// sees a partial line.  Lines that reach outside the batch are left partial.
+// ---------------------------------------------------------------------------
+struct GroupArgs {
+    uint8_t *base;            // stripe 0 of this launch
+    const uint32_t *tabs;     // tabs[nin][M][5]
+    const int32_t *in_idx;
+    uint64_t stripe_stride;
+    uint8_t *lo, *hi;         // the batch's bytes: [lo, hi)
+    uint32_t len;             // shard length = shard stride (multiple of 8, >= 128)
+    uint32_t out_first;       // first output shard; outputs are out_first .. out_first + M - 1
+    uint32_t n_items;         // stripes in this launch
+    uint32_t xcd_span;        // block order: XCD-contiguous remap span (0 = off)
+};
+
+typedef uint32_t u32x2a __attribute__((ext_vector_type(2)));
+
+template <int K, int M>
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(8, 8))) gf_group8_kernel(GroupArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint32_t t = blockIdx.x;
+    if (a.xcd_span && t < 8u * a.xcd_span) t = (t & 7u) * a.xcd_span + (t >> 3);
+    const uint32_t lane = threadIdx.x;
+    uint8_t *sb = a.base + uint64_t(t) * a.stripe_stride;
+    uint8_t *r0 = sb + uint64_t(a.out_first) * a.len;
+    uint8_t *r1 = r0 + uint64_t(M) * a.len;
+    uint8_t *l0 = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(r0) & ~uintptr_t(127));
+    uint8_t *l1 = reinterpret_cast<uint8_t *>((reinterpret_cast<uintptr_t>(r1) + 127) & ~uintptr_t(127));
+    uint8_t *w0 = l0 >= a.lo ? l0 : r0;  // the span this wave stores
+    uint8_t *w1 = l1 <= a.hi ? l1 : r1;
+    const uint32_t head = uint32_t(r0 - l0);
+    const uint32_t nw = a.len / 8;
+    // Phase 1: code 8-byte columns, park them in LDS at their region offsets.
+    for (uint32_t v = lane; v < nw; v += kWave) {
+        u32x2a x[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+            x[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x2a *>(sb + uint64_t(a.in_idx[i]) * a.len + 8u * v));
+        uint32_t acc[M][2];
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                const Sel sl = selectors(x[i][w]);
+#pragma unroll
+                for (int p = 0; p < M; ++p) {
+                    uint32_t t0, t1, t2;
+                    terms(a.tabs + (i * M + p) * 5, sl, t0, t1, t2);
+                    acc[p][w] = i == 0 ? xor3(t0, t1, t2) : xor3(acc[p][w], t0, t1) ^ t2;
+                }
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < M; ++p)
+            *reinterpret_cast<u32x2a *>(lds + head + p * a.len + 8u * v) = u32x2a{acc[p][0], acc[p][1]};
+    }
+    // The foreign bytes of the first and last line (inside the batch only).
+    if (lane < 16) {
+        uint8_t *q = l0 + 8u * lane;
+        if (q >= w0 && q < r0) *reinterpret_cast<u32x2a *>(lds + (q - l0)) = *reinterpret_cast<const u32x2a *>(q);
+    } else if (lane < 32) {
+        uint8_t *q = r1 + 8u * (lane - 16);
+        if (q < w1) *reinterpret_cast<u32x2a *>(lds + (q - l0)) = *reinterpret_cast<const u32x2a *>(q);
+    }
+    __syncthreads();
+    // Phase 2: the owned lines, as aligned 16-byte stores (8-byte halves where
+    // the span starts or ends mid-vector).
+    uint8_t *x0 = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(w0) & ~uintptr_t(15));
+    for (uint8_t *q = x0 + 16u * lane; q < w1; q += 16u * kWave) {
+        const u32x4 v = *reinterpret_cast<const u32x4 *>(lds + (q - l0));
+        const bool lo_in = q >= w0 && q + 8 <= w1, hi_in = q + 8 >= w0 && q + 16 <= w1;
+        if (lo_in && hi_in) {
+            __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(q));
+        } else if (lo_in) {
+            __builtin_nontemporal_store(u32x2a{v[0], v[1]}, reinterpret_cast<u32x2a *>(q));
+        } else if (hi_in) {
+            __builtin_nontemporal_store(u32x2a{v[2], v[3]}, reinterpret_cast<u32x2a *>(q + 8));
+        }
+    }
+}
+
 // Masked byte kernel: any alignment, and the <16-byte tails.
 struct MaskedByteArgs {
     uint8_t *base;
@@ -989,6 +1088,55 @@ hipError_t dispatch_vec8(const Vec8Args &a, int nout, Mode mode, hipStream_t s) 
     return hipErrorInvalidValue;
 }
 
+template <int K, int M>
+hipError_t launch_group8_t(const GroupArgs &a, size_t lds, hipStream_t s) {
+    hipLaunchKernelGGL((gf_group8_kernel<K, M>), dim3(a.n_items), dim3(kWave), lds, s, a);
+    return hipGetLastError();
+}
+
+// RSAMD_GROUP8=0 (TUNING builds) keeps such batches on the 8-byte kernels (A/B runs).
+bool group8_enabled() {
+    static const bool on = [] {
+        const char *e = tuning_env("RSAMD_GROUP8");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// The line-owner kernel takes an encode or uniform decode whose outputs are
+// one run of consecutive shards, on stripes of back-to-back shards (shard
+// stride = shard length, stripe stride = total shards x that) of 8-byte
+// multiples >= 128 bytes, with >= 256 bytes of non-output shards between runs
+// and a region small enough for LDS.
+constexpr size_t kGroupLdsMax = 16384;
+bool group8_applies(const Geometry &g, const DevPlan &p, Mode mode) {
+    const uintptr_t b = reinterpret_cast<uintptr_t>(g.base);
+    return mode == Mode::Code && p.out_first >= 0 && p.nin == 4 && p.nout >= 1 && p.nout <= 4 && g.total > 0 &&
+           g.col0 == 0 && g.len == g.shard_stride && g.len % 8 == 0 && g.len >= 128 && b % 8 == 0 &&
+           g.stripe_stride == size_t(g.total) * g.len && p.out_first + p.nout <= g.total &&
+           size_t(g.total - p.nout) * g.len >= 256 && size_t(p.nout) * g.len + 256 <= kGroupLdsMax &&
+           g.len / 8 <= UINT32_MAX && group8_enabled();
+}
+
+hipError_t launch_group8(const Geometry &g, const DevPlan &p, hipStream_t s) {
+    const size_t lds = (size_t(p.nout) * g.len + 256 + 15) / 16 * 16;
+    uint8_t *lo = g.base, *hi = g.base + g.n_stripes * g.stripe_stride;
+    for (size_t t0 = 0; t0 < g.n_stripes; t0 += kMaxGridBlocks) {
+        const size_t nst = std::min<size_t>(kMaxGridBlocks, g.n_stripes - t0);
+        GroupArgs a{g.base + t0 * g.stripe_stride, p.tabs, p.in_idx, g.stripe_stride, lo, hi, uint32_t(g.len),
+                    uint32_t(p.out_first), uint32_t(nst), uint32_t(nst / 8)};
+        hipError_t e = hipErrorInvalidValue;
+        switch (p.nout) {
+        case 1: e = launch_group8_t<4, 1>(a, lds, s); break;
+        case 2: e = launch_group8_t<4, 2>(a, lds, s); break;
+        case 3: e = launch_group8_t<4, 3>(a, lds, s); break;
+        case 4: e = launch_group8_t<4, 4>(a, lds, s); break;
+        }
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 // Lanes per stripe of the 8-byte-aligned kernels and the bytes they cover:
 // whole 16-byte vectors plus a half, or 8-byte vectors.
 struct Lanes8 {
@@ -1125,6 +1273,8 @@ hipError_t launch_gf_tables(const Geometry &g, const DevPlan &p, Mode mode, int 
                          g.stripe_stride % 16 == 0;
     const bool aligned8 = (reinterpret_cast<uintptr_t>(base) % 8 == 0) && g.shard_stride % 8 == 0 &&
                           g.stripe_stride % 8 == 0;
+    if (aligned8 && !aligned && uint64_t(g.n_stripes) * g.len > kSmallBytes && group8_applies(g, p, mode))
+        return launch_group8(g, p, s);
     if (aligned8 && (!aligned || small_with_tail8(g.len)) && uint64_t(g.n_stripes) * g.len > kSmallBytes &&
         g.len / 8 <= UINT32_MAX - kWave && masked8_enabled())
         return launch_vec8(g, p, mode, mismatch, s);

@@ -21,6 +21,10 @@ struct DevPlan {
     const int32_t *in_idx = nullptr;
     const int32_t *out_idx = nullptr;
     int nin = 0, nout = 0;
+    // out_idx[0] when the outputs are consecutive shards in ascending order
+    // (encode: k..k+m-1; decode {0,1}: 0, 1), else -1.  Host-side; selects the
+    // line-owner kernel for back-to-back chunk groups (kernels.hip).
+    int out_first = -1;
 };
 
 // Stripe-batched layout: shard s of stripe t at base + t*stripe_stride + s*shard_stride,
@@ -32,6 +36,7 @@ struct Geometry {
     size_t len = 0;
     size_t shard_stride = 0;
     size_t stripe_stride = 0;
+    int total = 0;  // shards per stripe (k + m) when the caller knows it, else 0
 };
 
 enum class Mode { Code, Verify };

@@ -75,3 +75,40 @@ def test_vec8_encode_decode_verify(gpu, oracle_lib, k, m, S, shard_stride, strip
         device.decode(rs, dev.data_ptr(), [i not in miss for i in range(T)], lay, st)
         torch.cuda.synchronize()
         np.testing.assert_array_equal(_from_dev(dev, B, T, S, shard_stride, stripe_stride), want)
+
+
+@pytest.mark.parametrize("offset", [136, 64])
+def test_line_owner_kernel_edges(gpu, oracle_lib, offset):
+    """The line-owner kernel (gf_group8_kernel: 4+2 x 1000-B groups packed
+    back to back, outputs one run of consecutive shards) writes whole 128-byte
+    lines, rewriting the input bytes that share a line with an output with
+    their own values -- but never a byte outside the batch.  The batch sits
+    inside a guarded buffer (base 8- but not 16-aligned, or 64-aligned); every
+    run of consecutive shards is erased and rebuilt (encode: 4-5; decodes:
+    {0}, {0,1}, {1,2,3}, {2,3}, {5}) and every other byte, guards included,
+    must be unchanged."""
+    import torch
+    import rsamd
+    from rsamd import device
+    from rsamd.device import StripeLayout
+    k, m, S, B = 4, 2, 1000, 701
+    T = k + m
+    want = _encoded(oracle_lib, k, m, S, B, 11)
+    guard = 512
+    host = np.full(guard + offset + B * T * S + guard, 0x77, np.uint8)
+    host[guard + offset: guard + offset + B * T * S] = want.reshape(-1)
+    lay = StripeLayout(B, S, S, T * S)
+    rs = rsamd.ReedSolomon.create(k, m)
+    st = torch.cuda.current_stream()
+    for miss in [(4, 5), (0,), (0, 1), (1, 2, 3), (2, 3), (5,)]:
+        clob = host.copy()
+        v = clob[guard + offset: guard + offset + B * T * S].reshape(B, T, S)
+        v[:, list(miss)] = 0x3C
+        dev = torch.from_numpy(clob).to("cuda:0")
+        base = dev.data_ptr() + guard + offset
+        if miss == (4, 5):
+            device.encode(rs, base, lay, st)
+        else:
+            device.decode(rs, base, [i not in miss for i in range(T)], lay, st)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(dev.cpu().numpy(), host, err_msg=f"erased {miss}")
