@@ -85,7 +85,7 @@ def test_line_owner_kernel_edges(gpu, oracle_lib, offset):
     their own values -- but never a byte outside the batch.  The batch sits
     inside a guarded buffer (base 8- but not 16-aligned, or 64-aligned); every
     run of consecutive shards is erased and rebuilt (encode: 4-5; decodes:
-    {0}, {0,1}, {1,2,3}, {2,3}, {5}) and every other byte, guards included,
+    {0}, {0,1}, {1,2}, {2,3}, {3,4}, {5}) and every other byte, guards included,
     must be unchanged."""
     import torch
     import rsamd
@@ -100,7 +100,7 @@ def test_line_owner_kernel_edges(gpu, oracle_lib, offset):
     lay = StripeLayout(B, S, S, T * S)
     rs = rsamd.ReedSolomon.create(k, m)
     st = torch.cuda.current_stream()
-    for miss in [(4, 5), (0,), (0, 1), (1, 2, 3), (2, 3), (5,)]:
+    for miss in [(4, 5), (0,), (0, 1), (1, 2), (2, 3), (3, 4), (5,)]:
         clob = host.copy()
         v = clob[guard + offset: guard + offset + B * T * S].reshape(B, T, S)
         v[:, list(miss)] = 0x3C
