@@ -690,71 +690,112 @@ struct GroupArgs {
     uint32_t len;             // shard length = shard stride (multiple of 8, >= 128)
     uint32_t out_first;       // first output shard; outputs are out_first .. out_first + M - 1
     uint32_t n_items;         // stripes in this launch
+    uint32_t n_blocks;        // blocks in this launch (RSAMD_GROUP_PER_WAVE stripes each)
     uint32_t xcd_span;        // block order: XCD-contiguous remap span (0 = off)
 };
 
 typedef uint32_t u32x2a __attribute__((ext_vector_type(2)));
 
+// A/B knobs of the line-owner kernel (make KDEFS=...): groups per wave,
+// whether the foreign bytes of the end lines are written back (0: those lines
+// stay partial), and non-temporal (1) or plain (0) stores.
+#ifndef RSAMD_GROUP_PER_WAVE
+#define RSAMD_GROUP_PER_WAVE 1
+#endif
+#ifndef RSAMD_GROUP_REWRITE
+#define RSAMD_GROUP_REWRITE 1
+#endif
+#ifndef RSAMD_GROUP_NT
+#define RSAMD_GROUP_NT 1
+#endif
+
+template <typename V>
+__device__ __forceinline__ void group_store(uint8_t *q, const V &v) {
+    if (RSAMD_GROUP_NT)
+        __builtin_nontemporal_store(v, reinterpret_cast<V *>(q));
+    else
+        *reinterpret_cast<V *>(q) = v;
+}
+
 template <int K, int M>
 __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(8, 8))) gf_group8_kernel(GroupArgs a) {
+    constexpr int G = RSAMD_GROUP_PER_WAVE;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    uint32_t t = blockIdx.x;
-    if (a.xcd_span && t < 8u * a.xcd_span) t = (t & 7u) * a.xcd_span + (t >> 3);
+    uint32_t b = blockIdx.x;
+    if (a.xcd_span && b < 8u * a.xcd_span) b = (b & 7u) * a.xcd_span + (b >> 3);
     const uint32_t lane = threadIdx.x;
-    uint8_t *sb = a.base + uint64_t(t) * a.stripe_stride;
-    uint8_t *r0 = sb + uint64_t(a.out_first) * a.len;
-    uint8_t *r1 = r0 + uint64_t(M) * a.len;
-    uint8_t *l0 = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(r0) & ~uintptr_t(127));
-    uint8_t *l1 = reinterpret_cast<uint8_t *>((reinterpret_cast<uintptr_t>(r1) + 127) & ~uintptr_t(127));
-    uint8_t *w0 = l0 >= a.lo ? l0 : r0;  // the span this wave stores
-    uint8_t *w1 = l1 <= a.hi ? l1 : r1;
-    const uint32_t head = uint32_t(r0 - l0);
     const uint32_t nw = a.len / 8;
+    const uint32_t slot = (uint32_t(M) * a.len + 256u + 15u) & ~15u;  // LDS bytes per group
     // Phase 1: code 8-byte columns, park them in LDS at their region offsets.
-    for (uint32_t v = lane; v < nw; v += kWave) {
-        u32x2a x[K];
 #pragma unroll
-        for (int i = 0; i < K; ++i)
-            x[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x2a *>(sb + uint64_t(a.in_idx[i]) * a.len + 8u * v));
-        uint32_t acc[M][2];
+    for (int g = 0; g < G; ++g) {
+        const uint32_t t = b * G + g;
+        if (t >= a.n_items) break;
+        uint8_t *sb = a.base + uint64_t(t) * a.stripe_stride;
+        uint8_t *r0 = sb + uint64_t(a.out_first) * a.len;
+        uint8_t *l0 = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(r0) & ~uintptr_t(127));
+        uint8_t *ls = lds + g * slot + (r0 - l0);
+        for (uint32_t v = lane; v < nw; v += kWave) {
+            u32x2a x[K];
 #pragma unroll
-        for (int w = 0; w < 2; ++w) {
+            for (int i = 0; i < K; ++i)
+                x[i] = __builtin_nontemporal_load(
+                    reinterpret_cast<const u32x2a *>(sb + uint64_t(a.in_idx[i]) * a.len + 8u * v));
+            uint32_t acc[M][2];
 #pragma unroll
-            for (int i = 0; i < K; ++i) {
-                const Sel sl = selectors(x[i][w]);
+            for (int w = 0; w < 2; ++w) {
 #pragma unroll
-                for (int p = 0; p < M; ++p) {
-                    uint32_t t0, t1, t2;
-                    terms(a.tabs + (i * M + p) * 5, sl, t0, t1, t2);
-                    acc[p][w] = i == 0 ? xor3(t0, t1, t2) : xor3(acc[p][w], t0, t1) ^ t2;
+                for (int i = 0; i < K; ++i) {
+                    const Sel sl = selectors(x[i][w]);
+#pragma unroll
+                    for (int p = 0; p < M; ++p) {
+                        uint32_t t0, t1, t2;
+                        terms(a.tabs + (i * M + p) * 5, sl, t0, t1, t2);
+                        acc[p][w] = i == 0 ? xor3(t0, t1, t2) : xor3(acc[p][w], t0, t1) ^ t2;
+                    }
                 }
             }
-        }
 #pragma unroll
-        for (int p = 0; p < M; ++p)
-            *reinterpret_cast<u32x2a *>(lds + head + p * a.len + 8u * v) = u32x2a{acc[p][0], acc[p][1]};
+            for (int p = 0; p < M; ++p)
+                *reinterpret_cast<u32x2a *>(ls + p * a.len + 8u * v) = u32x2a{acc[p][0], acc[p][1]};
+        }
     }
-    // The foreign bytes of the first and last line (inside the batch only).
-    if (lane < 16) {
-        uint8_t *q = l0 + 8u * lane;
-        if (q >= w0 && q < r0) *reinterpret_cast<u32x2a *>(lds + (q - l0)) = *reinterpret_cast<const u32x2a *>(q);
-    } else if (lane < 32) {
-        uint8_t *q = r1 + 8u * (lane - 16);
-        if (q < w1) *reinterpret_cast<u32x2a *>(lds + (q - l0)) = *reinterpret_cast<const u32x2a *>(q);
+    // The foreign bytes of each group's first and last line (inside the batch only).
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const uint32_t t = b * G + g;
+        if (!RSAMD_GROUP_REWRITE || t >= a.n_items) break;
+        uint8_t *r0 = a.base + uint64_t(t) * a.stripe_stride + uint64_t(a.out_first) * a.len;
+        uint8_t *r1 = r0 + uint64_t(M) * a.len;
+        uint8_t *l0 = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(r0) & ~uintptr_t(127));
+        uint8_t *l1 = reinterpret_cast<uint8_t *>((reinterpret_cast<uintptr_t>(r1) + 127) & ~uintptr_t(127));
+        uint8_t *q = lane < 16 ? l0 + 8u * lane : r1 + 8u * (lane - 16);
+        const bool in = lane < 16 ? (l0 >= a.lo && q < r0) : (lane < 32 && l1 <= a.hi && q < l1);
+        if (in) *reinterpret_cast<u32x2a *>(lds + g * slot + (q - l0)) = *reinterpret_cast<const u32x2a *>(q);
     }
     __syncthreads();
     // Phase 2: the owned lines, as aligned 16-byte stores (8-byte halves where
     // the span starts or ends mid-vector).
-    uint8_t *x0 = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(w0) & ~uintptr_t(15));
-    for (uint8_t *q = x0 + 16u * lane; q < w1; q += 16u * kWave) {
-        const u32x4 v = *reinterpret_cast<const u32x4 *>(lds + (q - l0));
-        const bool lo_in = q >= w0 && q + 8 <= w1, hi_in = q + 8 >= w0 && q + 16 <= w1;
-        if (lo_in && hi_in) {
-            __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(q));
-        } else if (lo_in) {
-            __builtin_nontemporal_store(u32x2a{v[0], v[1]}, reinterpret_cast<u32x2a *>(q));
-        } else if (hi_in) {
-            __builtin_nontemporal_store(u32x2a{v[2], v[3]}, reinterpret_cast<u32x2a *>(q + 8));
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const uint32_t t = b * G + g;
+        if (t >= a.n_items) break;
+        uint8_t *r0 = a.base + uint64_t(t) * a.stripe_stride + uint64_t(a.out_first) * a.len;
+        uint8_t *r1 = r0 + uint64_t(M) * a.len;
+        uint8_t *l0 = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(r0) & ~uintptr_t(127));
+        uint8_t *l1 = reinterpret_cast<uint8_t *>((reinterpret_cast<uintptr_t>(r1) + 127) & ~uintptr_t(127));
+        uint8_t *w0 = RSAMD_GROUP_REWRITE && l0 >= a.lo ? l0 : r0;  // the span this wave stores
+        uint8_t *w1 = RSAMD_GROUP_REWRITE && l1 <= a.hi ? l1 : r1;
+        uint8_t *x0 = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(w0) & ~uintptr_t(15));
+        for (uint8_t *q = x0 + 16u * lane; q < w1; q += 16u * kWave) {
+            const u32x4 v = *reinterpret_cast<const u32x4 *>(lds + g * slot + (q - l0));
+            const bool lo_in = q >= w0 && q + 8 <= w1, hi_in = q + 8 >= w0 && q + 16 <= w1;
+            if (lo_in && hi_in)
+                group_store(q, v);
+            else if (lo_in)
+                group_store(q, u32x2a{v[0], v[1]});
+            else if (hi_in)
+                group_store(q + 8, u32x2a{v[2], v[3]});
         }
     }
 }
@@ -1090,7 +1131,7 @@ hipError_t dispatch_vec8(const Vec8Args &a, int nout, Mode mode, hipStream_t s) 
 
 template <int K, int M>
 hipError_t launch_group8_t(const GroupArgs &a, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((gf_group8_kernel<K, M>), dim3(a.n_items), dim3(kWave), lds, s, a);
+    hipLaunchKernelGGL((gf_group8_kernel<K, M>), dim3(a.n_blocks), dim3(kWave), lds, s, a);
     return hipGetLastError();
 }
 
@@ -1114,17 +1155,19 @@ bool group8_applies(const Geometry &g, const DevPlan &p, Mode mode) {
     return mode == Mode::Code && p.out_first >= 0 && p.nin == 4 && p.nout >= 1 && p.nout <= 4 && g.total > 0 &&
            g.col0 == 0 && g.len == g.shard_stride && g.len % 8 == 0 && g.len >= 128 && b % 8 == 0 &&
            g.stripe_stride == size_t(g.total) * g.len && p.out_first + p.nout <= g.total &&
-           size_t(g.total - p.nout) * g.len >= 256 && size_t(p.nout) * g.len + 256 <= kGroupLdsMax &&
+           size_t(g.total - p.nout) * g.len >= 256 && RSAMD_GROUP_PER_WAVE * (size_t(p.nout) * g.len + 256) <= kGroupLdsMax &&
            g.len / 8 <= UINT32_MAX && group8_enabled();
 }
 
 hipError_t launch_group8(const Geometry &g, const DevPlan &p, hipStream_t s) {
-    const size_t lds = (size_t(p.nout) * g.len + 256 + 15) / 16 * 16;
+    constexpr size_t G = RSAMD_GROUP_PER_WAVE;
+    const size_t lds = G * ((size_t(p.nout) * g.len + 256 + 15) / 16 * 16);
     uint8_t *lo = g.base, *hi = g.base + g.n_stripes * g.stripe_stride;
-    for (size_t t0 = 0; t0 < g.n_stripes; t0 += kMaxGridBlocks) {
-        const size_t nst = std::min<size_t>(kMaxGridBlocks, g.n_stripes - t0);
+    for (size_t t0 = 0; t0 < g.n_stripes; t0 += kMaxGridBlocks * G) {
+        const size_t nst = std::min<size_t>(kMaxGridBlocks * G, g.n_stripes - t0);
+        const size_t blocks = (nst + G - 1) / G;
         GroupArgs a{g.base + t0 * g.stripe_stride, p.tabs, p.in_idx, g.stripe_stride, lo, hi, uint32_t(g.len),
-                    uint32_t(p.out_first), uint32_t(nst), uint32_t(nst / 8)};
+                    uint32_t(p.out_first), uint32_t(nst), uint32_t(blocks), uint32_t(blocks / 8)};
         hipError_t e = hipErrorInvalidValue;
         switch (p.nout) {
         case 1: e = launch_group8_t<4, 1>(a, lds, s); break;

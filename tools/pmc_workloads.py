@@ -16,6 +16,7 @@ Workloads (bench.py's configs):
   maskbits   4+2 x 4 KiB x 1 M, per-stripe bitmasks      alg (4 * stripes with a loss + erased shards) S
   gmaskbits  the same in the granule layout (64 KiB rows of 16 stripes)
   cgmaskbits / cgmaskbits1k   4+2 x 1000 B x 4 M chunk groups, stride 1000 / 1024, bitmasks
+  cgenc / cgdec01             the same groups at stride 1000: encode / uniform {0,1} decode (line-owner kernel)
   fenc       4 GiB file -> 4+2 shards (fused)            alg file + 6 S
   fdec_05    4+2 shards {0,5} -> 4 GiB file (tiled)      alg 4 S + file
 """
@@ -114,6 +115,21 @@ def main():
         fn = lambda: rdev.decode_masked_bits(rs, buf.data_ptr(), bits.data_ptr(), lay, 0, st)  # noqa: E731
         alg = (4 * int((~present).any(axis=1).sum()) + int((~present).sum())) * S
         kernel = "gf_masked8_kernel<4, 2>"
+    elif name in ("cgenc", "cgdec01"):
+        # the master's chunk groups packed back to back (stride 1000): the
+        # line-owner kernel, encode or the uniform {0,1} decode
+        k, m, S, B = 4, 2, 1000, 4 << 20
+        rs = rsamd.ReedSolomon.create(k, m)
+        lay = StripeLayout(B, S, S, 6 * S)
+        buf = torch.empty(lay.nbytes, dtype=torch.uint8, device="cuda:0")
+        rdev.fill_synthetic(buf.data_ptr(), k, lay, SEED, 0, st)
+        rdev.encode(rs, buf.data_ptr(), lay, st)
+        if name == "cgenc":
+            fn = lambda: rdev.encode(rs, buf.data_ptr(), lay, st)  # noqa: E731
+        else:
+            fn = lambda: rdev.decode(rs, buf.data_ptr(), [False, False, True, True, True, True], lay, st)  # noqa: E731
+        alg = 6 * S * B
+        kernel = "gf_group8_kernel<4, 2>"
     elif name == "ver104":
         k, m, S, B = 10, 4, 4 << 20, 128
         rs, lay, buf = stripes(k, m, S, B)
