@@ -708,6 +708,10 @@ typedef uint32_t u32x2a __attribute__((ext_vector_type(2)));
 #ifndef RSAMD_GROUP_NT
 #define RSAMD_GROUP_NT 1
 #endif
+#ifndef RSAMD_GROUP_ALIGNED_READ
+#define RSAMD_GROUP_ALIGNED_READ 0  // 1: inputs read as whole lines (aligned 16-byte loads) into LDS first
+#endif
+static_assert(!RSAMD_GROUP_ALIGNED_READ || RSAMD_GROUP_PER_WAVE == 1, "aligned reads: one group per wave");
 
 template <typename V>
 __device__ __forceinline__ void group_store(uint8_t *q, const V &v) {
@@ -735,12 +739,52 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(8, 8
         uint8_t *r0 = sb + uint64_t(a.out_first) * a.len;
         uint8_t *l0 = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(r0) & ~uintptr_t(127));
         uint8_t *ls = lds + g * slot + (r0 - l0);
+#if RSAMD_GROUP_ALIGNED_READ
+        // Each input shard's lines as aligned 16-byte loads (whole 128-byte
+        // lines, no split requests), parked in LDS behind the output slot.
+        const uint32_t islot = (a.len + 256u + 15u) & ~15u;
+        uint8_t *in_lds = lds + slot;
+        uint32_t in_off[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            const uint8_t *si = sb + uint64_t(a.in_idx[i]) * a.len;
+            in_off[i] = uint32_t(reinterpret_cast<uintptr_t>(si) & 127u);
+        }
+        const uint32_t span_max = (a.len + 127u + 127u) & ~127u;
+        for (uint32_t q0 = 0; q0 < span_max; q0 += 2u * 16u * kWave) {
+            u32x4 r[K][2];
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                const uint8_t *ai = sb + uint64_t(a.in_idx[i]) * a.len - in_off[i];
+                const uint32_t span = (in_off[i] + a.len + 127u) & ~127u;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t q = q0 + uint32_t(h) * 16u * kWave + 16u * lane;
+                    if (q < span) r[i][h] = load_stream(ai + q);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                const uint32_t span = (in_off[i] + a.len + 127u) & ~127u;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t q = q0 + uint32_t(h) * 16u * kWave + 16u * lane;
+                    if (q < span) *reinterpret_cast<u32x4 *>(in_lds + i * islot + q) = r[i][h];
+                }
+            }
+        }
+        __syncthreads();
+#endif
         for (uint32_t v = lane; v < nw; v += kWave) {
             u32x2a x[K];
 #pragma unroll
             for (int i = 0; i < K; ++i)
+#if RSAMD_GROUP_ALIGNED_READ
+                x[i] = *reinterpret_cast<const u32x2a *>(in_lds + i * islot + in_off[i] + 8u * v);
+#else
                 x[i] = __builtin_nontemporal_load(
                     reinterpret_cast<const u32x2a *>(sb + uint64_t(a.in_idx[i]) * a.len + 8u * v));
+#endif
             uint32_t acc[M][2];
 #pragma unroll
             for (int w = 0; w < 2; ++w) {
@@ -1155,13 +1199,15 @@ bool group8_applies(const Geometry &g, const DevPlan &p, Mode mode) {
     return mode == Mode::Code && p.out_first >= 0 && p.nin == 4 && p.nout >= 1 && p.nout <= 4 && g.total > 0 &&
            g.col0 == 0 && g.len == g.shard_stride && g.len % 8 == 0 && g.len >= 128 && b % 8 == 0 &&
            g.stripe_stride == size_t(g.total) * g.len && p.out_first + p.nout <= g.total &&
-           size_t(g.total - p.nout) * g.len >= 256 && RSAMD_GROUP_PER_WAVE * (size_t(p.nout) * g.len + 256) <= kGroupLdsMax &&
+           size_t(g.total - p.nout) * g.len >= 256 && RSAMD_GROUP_PER_WAVE * (size_t(p.nout) * g.len + 256) +
+               (RSAMD_GROUP_ALIGNED_READ ? size_t(p.nin) * (g.len + 256) : 0) <= 2 * kGroupLdsMax &&
            g.len / 8 <= UINT32_MAX && group8_enabled();
 }
 
 hipError_t launch_group8(const Geometry &g, const DevPlan &p, hipStream_t s) {
     constexpr size_t G = RSAMD_GROUP_PER_WAVE;
-    const size_t lds = G * ((size_t(p.nout) * g.len + 256 + 15) / 16 * 16);
+    const size_t lds = G * ((size_t(p.nout) * g.len + 256 + 15) / 16 * 16) +
+                       (RSAMD_GROUP_ALIGNED_READ ? size_t(p.nin) * ((g.len + 256 + 15) / 16 * 16) : 0);
     uint8_t *lo = g.base, *hi = g.base + g.n_stripes * g.stripe_stride;
     for (size_t t0 = 0; t0 < g.n_stripes; t0 += kMaxGridBlocks * G) {
         const size_t nst = std::min<size_t>(kMaxGridBlocks * G, g.n_stripes - t0);

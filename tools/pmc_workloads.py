@@ -35,6 +35,9 @@ def main():
     name = sys.argv[1]
     import numpy as np
     import torch
+    if len(sys.argv) > 2:  # a variant librsamd.so (A/B builds)
+        from rsamd import _lib
+        _lib.LIB_PATH = os.path.abspath(sys.argv[2])
     import rsamd
     from rsamd import device as rdev
     from rsamd.device import StripeLayout
