@@ -740,37 +740,53 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(8, 8
         uint8_t *l0 = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(r0) & ~uintptr_t(127));
         uint8_t *ls = lds + g * slot + (r0 - l0);
 #if RSAMD_GROUP_ALIGNED_READ
-        // Each input shard's lines as aligned 16-byte loads (whole 128-byte
-        // lines, no split requests), parked in LDS behind the output slot.
-        const uint32_t islot = (a.len + 256u + 15u) & ~15u;
+        // The input shards' lines as aligned 16-byte loads (whole 128-byte
+        // lines: no request splits a line), into LDS behind the output slot.
+        // Consecutive input shards form one run whose lines are loaded once
+        // (the line two shards share is not fetched twice); the LDS input
+        // area mirrors each run's line span, runs back to back.
         uint8_t *in_lds = lds + slot;
-        uint32_t in_off[K];
+        const uint8_t *run_a[K];
+        uint32_t run_base[K], in_lds_off[K];
+        int nr = 0;
+        uint32_t cum = 0;
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             const uint8_t *si = sb + uint64_t(a.in_idx[i]) * a.len;
-            in_off[i] = uint32_t(reinterpret_cast<uintptr_t>(si) & 127u);
+            if (i == 0 || a.in_idx[i] != a.in_idx[i - 1] + 1) {  // a new run starts at input i
+                if (nr > 0) {
+                    const uint8_t *prev_end = sb + uint64_t(a.in_idx[i - 1] + 1) * a.len;
+                    cum += uint32_t(((reinterpret_cast<uintptr_t>(prev_end) + 127) & ~uintptr_t(127)) -
+                                    reinterpret_cast<uintptr_t>(run_a[nr - 1]));
+                }
+                run_a[nr] = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(si) & ~uintptr_t(127));
+                run_base[nr] = cum;
+                ++nr;
+            }
+            in_lds_off[i] = run_base[nr - 1] + uint32_t(si - run_a[nr - 1]);
         }
-        const uint32_t span_max = (a.len + 127u + 127u) & ~127u;
-        for (uint32_t q0 = 0; q0 < span_max; q0 += 2u * 16u * kWave) {
-            u32x4 r[K][2];
+        {
+            const uint8_t *last_end = sb + uint64_t(a.in_idx[K - 1] + 1) * a.len;
+            cum += uint32_t(((reinterpret_cast<uintptr_t>(last_end) + 127) & ~uintptr_t(127)) -
+                            reinterpret_cast<uintptr_t>(run_a[nr - 1]));
+        }
+        for (uint32_t q0 = 0; q0 < cum; q0 += 4u * 16u * kWave) {
+            u32x4 r[4];
 #pragma unroll
-            for (int i = 0; i < K; ++i) {
-                const uint8_t *ai = sb + uint64_t(a.in_idx[i]) * a.len - in_off[i];
-                const uint32_t span = (in_off[i] + a.len + 127u) & ~127u;
+            for (int h = 0; h < 4; ++h) {
+                const uint32_t q = q0 + uint32_t(h) * 16u * kWave + 16u * lane;
+                if (q < cum) {
+                    int rr = 0;
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const uint32_t q = q0 + uint32_t(h) * 16u * kWave + 16u * lane;
-                    if (q < span) r[i][h] = load_stream(ai + q);
+                    for (int j = 1; j < K; ++j)
+                        if (j < nr && q >= run_base[j]) rr = j;
+                    r[h] = load_stream(run_a[rr] + (q - run_base[rr]));
                 }
             }
 #pragma unroll
-            for (int i = 0; i < K; ++i) {
-                const uint32_t span = (in_off[i] + a.len + 127u) & ~127u;
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const uint32_t q = q0 + uint32_t(h) * 16u * kWave + 16u * lane;
-                    if (q < span) *reinterpret_cast<u32x4 *>(in_lds + i * islot + q) = r[i][h];
-                }
+            for (int h = 0; h < 4; ++h) {
+                const uint32_t q = q0 + uint32_t(h) * 16u * kWave + 16u * lane;
+                if (q < cum) *reinterpret_cast<u32x4 *>(in_lds + q) = r[h];
             }
         }
         __syncthreads();
@@ -780,7 +796,7 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(8, 8
 #pragma unroll
             for (int i = 0; i < K; ++i)
 #if RSAMD_GROUP_ALIGNED_READ
-                x[i] = *reinterpret_cast<const u32x2a *>(in_lds + i * islot + in_off[i] + 8u * v);
+                x[i] = *reinterpret_cast<const u32x2a *>(in_lds + in_lds_off[i] + 8u * v);
 #else
                 x[i] = __builtin_nontemporal_load(
                     reinterpret_cast<const u32x2a *>(sb + uint64_t(a.in_idx[i]) * a.len + 8u * v));
@@ -1206,8 +1222,10 @@ bool group8_applies(const Geometry &g, const DevPlan &p, Mode mode) {
 
 hipError_t launch_group8(const Geometry &g, const DevPlan &p, hipStream_t s) {
     constexpr size_t G = RSAMD_GROUP_PER_WAVE;
+    // input area (aligned reads): each run of consecutive input shards spans
+    // at most its bytes + 254 rounded to lines; nin runs at worst
     const size_t lds = G * ((size_t(p.nout) * g.len + 256 + 15) / 16 * 16) +
-                       (RSAMD_GROUP_ALIGNED_READ ? size_t(p.nin) * ((g.len + 256 + 15) / 16 * 16) : 0);
+                       (RSAMD_GROUP_ALIGNED_READ ? size_t(p.nin) * (g.len + 256) : 0);
     uint8_t *lo = g.base, *hi = g.base + g.n_stripes * g.stripe_stride;
     for (size_t t0 = 0; t0 < g.n_stripes; t0 += kMaxGridBlocks * G) {
         const size_t nst = std::min<size_t>(kMaxGridBlocks * G, g.n_stripes - t0);

@@ -19,6 +19,12 @@ for p in (ROOT, PKG_DIR):
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
+# A/B runs of the GPU tests against a variant build (make OUT=... KDEFS=...):
+# RSAMD_TEST_LIB names the librsamd.so to load instead of the in-tree one.
+if os.environ.get("RSAMD_TEST_LIB"):
+    from rsamd import _lib as _rs_lib
+    _rs_lib.LIB_PATH = os.path.abspath(os.environ["RSAMD_TEST_LIB"])
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: requires an MI355X GPU and the HIP extension")
