@@ -729,7 +729,7 @@ int rs_decode_batch_masked_dev(const rs_codec *codec, uint8_t *dev_base, const u
     if (n_stripes == 0 || shard_len == 0) return RS_OK;
     if (!dev_base) return fail(RS_E_INVALID, "NULL device base");
     if (n_stripes > size_t(INT32_MAX)) return fail(RS_E_INVALID, "too many stripes");
-    const Geometry geo{dev_base, n_stripes, 0, shard_len, shard_stride, stripe_stride};
+    const Geometry geo{dev_base, n_stripes, 0, shard_len, shard_stride, stripe_stride, c->total()};
     return decode_masked_dev(*c, present, n_stripes, geo, 0, static_cast<hipStream_t>(stream));
 }
 
@@ -755,7 +755,7 @@ int rs_decode_batch_masked_bits_dev(const rs_codec *codec, uint8_t *dev_base, co
     if (n_stripes == 0 || shard_len == 0) return RS_OK;
     if (!dev_base) return fail(RS_E_INVALID, "NULL device buffer");
     if (n_stripes > size_t(INT32_MAX)) return fail(RS_E_INVALID, "too many stripes");
-    const Geometry geo{dev_base, n_stripes, 0, shard_len, shard_stride, stripe_stride};
+    const Geometry geo{dev_base, n_stripes, 0, shard_len, shard_stride, stripe_stride, c->total()};
     return decode_masked_bits_dev(*c, dev_present_bits, geo, 0, dev_bad_count, static_cast<hipStream_t>(stream));
 }
 

@@ -664,198 +664,253 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(8, 8
 // Line-owner kernel for chunk groups packed back to back: the master's
 // 6 x 1000-byte groups (ChunkserverDiskRecoveryMachine.java:34-48,
 // MasterImpl.java:794-839) at shard stride 1000, group stride 6000.  There
-// a group's written region -- its output shards, consecutive, e.g. parity
-// 4-5 -- starts and ends inside 128-byte lines, and the 8-byte kernels above
-// write it as 1000-byte runs split over two waves: lines written piecewise by
-// two waves, and a partially written line at each end of the region.  HBM
-// serves partial lines with read-modify-writes (PMC: 1.055x the algorithmic
-// bytes, 0.59 of peak against 0.72 for the same groups in 1 KiB slots).
+// every shard starts and ends inside a 128-byte line.  The 8-byte kernels
+// above read and write it as 1000-byte runs of 8-byte lanes split over two
+// waves: lines written piecewise by two waves, a partially written line at
+// each end of an output shard, and reads that split lines into separate
+// requests.  HBM serves partial lines with read-modify-writes; the 8-byte
+// kernels ran at 0.59 of peak against 0.72 for the same groups in 1 KiB slots.
 //
-// Here ONE wave owns every 128-byte line the region touches.  Phase 1: each
-// lane codes 8-byte columns of all M outputs and parks them in LDS in the
-// region's byte order.  The bytes of the region's first and last line that
-// lie outside it belong to input shards of this group or of its neighbour
-// (never to an output shard of this launch: outputs are one run per group and
-// the runs are >= 256 bytes apart), so the wave loads them too.  Phase 2: the
-// wave stores whole lines from LDS as aligned 16-byte non-temporal stores --
-// the foreign bytes written back with the values just read -- so HBM never
-// sees a partial line.  Lines that reach outside the batch are left partial.
+// Here ONE wave owns a group, and every line it touches it touches whole:
+//  * phase 0: each input shard's lines (the shard's bytes rounded out to
+//    128-byte lines) as aligned 16-byte loads into LDS;
+//  * phase 1: each lane codes 8-byte columns of every output from LDS and
+//    parks them in LDS in memory order, one slot per run of consecutive
+//    output shards;
+//  * phase 2: each run is stored as whole aligned lines (16-byte non-temporal
+//    stores).  The bytes of a run's first and last line that lie outside it
+//    belong to the neighbouring shard; when nobody writes that shard in this
+//    launch (a shard of this group that is not an output -- runs are maximal
+//    -- or a neighbouring group's shard that group does not rebuild), the wave
+//    loads those bytes and writes them back unchanged, so HBM sees no partial
+//    line.  Otherwise (or at the batch's ends) the line stays partial.
+// Shards of >= 256 bytes keep two runs of one group on different lines.
+// Measured on 4 M groups (profiles/r3/): encode 0.738 of peak against 0.590
+// for the 8-byte kernel, with PMC traffic 1.07x the algorithmic bytes (the
+// rounding to lines).  Variants measured and dropped (A/B builds): 8-byte
+// lane loads straight from HBM 0.645, no write-back of the foreign bytes
+// 0.578, plain stores 0.58, two groups per wave 0.62, loading a line shared by
+// two input shards once 0.60 (its loads took two round trips).
 // ---------------------------------------------------------------------------
 struct GroupArgs {
     uint8_t *base;            // stripe 0 of this launch
-    const uint32_t *tabs;     // tabs[nin][M][5]
-    const int32_t *in_idx;
-    uint64_t stripe_stride;
+    uint64_t stripe_stride;   // = total * len
     uint8_t *lo, *hi;         // the batch's bytes: [lo, hi)
-    uint32_t len;             // shard length = shard stride (multiple of 8, >= 128)
-    uint32_t out_first;       // first output shard; outputs are out_first .. out_first + M - 1
-    uint32_t n_items;         // stripes in this launch
-    uint32_t n_blocks;        // blocks in this launch (RSAMD_GROUP_PER_WAVE stripes each)
+    uint32_t len;             // shard length = shard stride (multiple of 8, >= 256)
+    uint32_t total;           // shards per stripe
+    uint32_t n_items;         // stripes in this launch (one wave each)
     uint32_t xcd_span;        // block order: XCD-contiguous remap span (0 = off)
+    // one plan for every stripe (MASKED = false)
+    const uint32_t *tabs;     // tabs[nin][MS][5]
+    const int32_t *in_idx;
+    const int32_t *out_idx;   // ascending
+    // a record per stripe (MASKED = true), as MaskedArgs
+    const uint8_t *records;
+    uint64_t rec_stride;
+    const int32_t *plan_ids;  // offset to this launch's stripe 0
+    const int32_t *mask_table;
+    int mask_bits;
+    int32_t *bad;
+    uint32_t rec_in_idx, rec_out_idx, rec_tabs;
+    uint32_t has_prev;        // stripe 0 of this launch has a predecessor in the batch
+    uint32_t has_next_last;   // the launch's last stripe has a successor in the batch
 };
 
 typedef uint32_t u32x2a __attribute__((ext_vector_type(2)));
 
-// A/B knobs of the line-owner kernel (make KDEFS=...): groups per wave,
-// whether the foreign bytes of the end lines are written back (0: those lines
-// stay partial), and non-temporal (1) or plain (0) stores.
-#ifndef RSAMD_GROUP_PER_WAVE
-#define RSAMD_GROUP_PER_WAVE 1
-#endif
-#ifndef RSAMD_GROUP_REWRITE
-#define RSAMD_GROUP_REWRITE 1
-#endif
-#ifndef RSAMD_GROUP_NT
-#define RSAMD_GROUP_NT 1
-#endif
-#ifndef RSAMD_GROUP_ALIGNED_READ
-#define RSAMD_GROUP_ALIGNED_READ 0  // 1: inputs read as whole lines (aligned 16-byte loads) into LDS first
-#endif
-static_assert(!RSAMD_GROUP_ALIGNED_READ || RSAMD_GROUP_PER_WAVE == 1, "aligned reads: one group per wave");
-
-template <typename V>
-__device__ __forceinline__ void group_store(uint8_t *q, const V &v) {
-    if (RSAMD_GROUP_NT)
-        __builtin_nontemporal_store(v, reinterpret_cast<V *>(q));
-    else
-        *reinterpret_cast<V *>(q) = v;
+// Might stripe u of this launch (u may be -1 or n_items) rebuild shard s?
+// Uniform plans: s is an output.  Per-stripe bitmasks: u is decodable and
+// lacks s (conservative when a code needs several launches: a shard another
+// launch rebuilds is treated as written).  Per-call records: s is an output
+// of u's record.
+template <int MS, bool MASKED>
+__device__ __forceinline__ bool group_writes(const GroupArgs &a, int64_t u, int s) {
+    if (MASKED && a.mask_table) {
+        const uint32_t bits = uint32_t(a.plan_ids[u]);
+        return !(bits >> a.mask_bits) && a.mask_table[bits] >= 0 && !((bits >> s) & 1u);
+    }
+    const int32_t *out = a.out_idx;
+    int nout = MS;
+    if (MASKED) {
+        const int32_t id = a.plan_ids[u];
+        if (id < 0) return false;
+        const uint8_t *rec = a.records + uint64_t(id) * a.rec_stride;
+        nout = *reinterpret_cast<const int32_t *>(rec);
+        out = reinterpret_cast<const int32_t *>(rec + a.rec_out_idx);
+    }
+    bool w = false;
+#pragma unroll
+    for (int p = 0; p < MS; ++p) w |= p < nout && out[p] == s;
+    return w;
 }
 
-template <int K, int M>
-__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(8, 8))) gf_group8_kernel(GroupArgs a) {
-    constexpr int G = RSAMD_GROUP_PER_WAVE;
+// LDS bounds occupancy here (4+2 x 1000 B: 7.6 KiB per wave, 21 waves per
+// CU), so the register budget is 5 waves per SIMD (<= 96 VGPRs, no spills).
+template <int K, int MS, bool MASKED>
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5, 8))) gf_group8_kernel(GroupArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    uint32_t b = blockIdx.x;
-    if (a.xcd_span && b < 8u * a.xcd_span) b = (b & 7u) * a.xcd_span + (b >> 3);
+    uint32_t t = blockIdx.x;
+    if (a.xcd_span && t < 8u * a.xcd_span) t = (t & 7u) * a.xcd_span + (t >> 3);
     const uint32_t lane = threadIdx.x;
-    const uint32_t nw = a.len / 8;
-    const uint32_t slot = (uint32_t(M) * a.len + 256u + 15u) & ~15u;  // LDS bytes per group
-    // Phase 1: code 8-byte columns, park them in LDS at their region offsets.
+    const uint32_t len = a.len;
+    const uint32_t *tabs;
+    const int32_t *in_idx, *out_idx;
+    int nout;
+    if (MASKED) {
+        // The record id first, the pointer after the check: a pointer that may
+        // be null is a generic one, which may alias the LDS stores below, and
+        // the record's tables would then be read with per-lane vector loads.
+        int32_t id = a.plan_ids[t];
+        if (a.mask_table) {
+            const uint32_t bits = uint32_t(id);
+            id = (bits >> a.mask_bits) ? -1 : a.mask_table[bits];
+        }
+        if (id < 0) {
+            count_undecodable(a.bad, lane == 0);
+            return;
+        }
+        const uint8_t *rec = a.records + uint64_t(id) * a.rec_stride;
+        nout = *reinterpret_cast<const int32_t *>(rec);
+        in_idx = reinterpret_cast<const int32_t *>(rec + a.rec_in_idx);
+        out_idx = reinterpret_cast<const int32_t *>(rec + a.rec_out_idx);
+        tabs = reinterpret_cast<const uint32_t *>(rec + a.rec_tabs);
+    } else {
+        nout = MS;
+        in_idx = a.in_idx;
+        out_idx = a.out_idx;
+        tabs = a.tabs;
+    }
+    if (nout == 0) return;
+    uint8_t *sb = a.base + uint64_t(t) * a.stripe_stride;
+
+    // Runs of consecutive output shards and their LDS slots (memory order).
+    // Every array is indexed by the unrolled p only (a runtime index would
+    // put it in scratch): run_start[p] marks the first output of a run,
+    // run_lds[p] its slot, run_last[p] the last shard of p's run.
+    bool run_start[MS];
+    uint32_t out_lds[MS], run_lds[MS];
+    int run_last[MS];
+    uint32_t cum = 0, cur_lds = 0;
+    int cur_p0 = 0;
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-        const uint32_t t = b * G + g;
-        if (t >= a.n_items) break;
-        uint8_t *sb = a.base + uint64_t(t) * a.stripe_stride;
-        uint8_t *r0 = sb + uint64_t(a.out_first) * a.len;
-        uint8_t *l0 = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(r0) & ~uintptr_t(127));
-        uint8_t *ls = lds + g * slot + (r0 - l0);
-#if RSAMD_GROUP_ALIGNED_READ
-        // The input shards' lines as aligned 16-byte loads (whole 128-byte
-        // lines: no request splits a line), into LDS behind the output slot.
-        // Consecutive input shards form one run whose lines are loaded once
-        // (the line two shards share is not fetched twice); the LDS input
-        // area mirrors each run's line span, runs back to back.
-        uint8_t *in_lds = lds + slot;
-        const uint8_t *run_a[K];
-        uint32_t run_base[K], in_lds_off[K];
-        int nr = 0;
-        uint32_t cum = 0;
+    for (int p = 0; p < MS; ++p) {
+        run_start[p] = p < nout && (p == 0 || out_idx[p] != out_idx[p - 1] + 1);
+        if (run_start[p] && p > 0) {
+            cum += (uint32_t(p - cur_p0) * len + 256u + 15u) & ~15u;
+            cur_p0 = p;
+        }
+        cur_lds = cum;
+        run_lds[p] = cur_lds;
+        const uint8_t *r0 = sb + uint64_t(out_idx[cur_p0]) * len;
+        out_lds[p] = cur_lds + uint32_t(reinterpret_cast<uintptr_t>(r0) & 127u) + uint32_t(p - cur_p0) * len;
+    }
+    cum += (uint32_t(nout - cur_p0) * len + 256u + 15u) & ~15u;
+    {
+        int last = 0;
+#pragma unroll
+        for (int p = MS - 1; p >= 0; --p) {
+            if (p < nout && (p == nout - 1 || (p + 1 < MS && run_start[p + 1]))) last = out_idx[p];
+            run_last[p] = last;
+        }
+    }
+    // Input area behind the output slots: each input shard rounded out to lines.
+    const uint32_t islot = (len + 256u + 15u) & ~15u;
+    uint8_t *in_lds = lds + cum;
+
+    // Phase 0: the input shards' whole lines, all loads issued before the LDS writes.
+    uint32_t in_off[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        in_off[i] = uint32_t(reinterpret_cast<uintptr_t>(sb + uint64_t(in_idx[i]) * len) & 127u);
+    const uint32_t span_max = (len + 127u + 127u) & ~127u;
+    for (uint32_t q0 = 0; q0 < span_max; q0 += 2u * 16u * kWave) {
+        u32x4 r[K][2];
 #pragma unroll
         for (int i = 0; i < K; ++i) {
-            const uint8_t *si = sb + uint64_t(a.in_idx[i]) * a.len;
-            if (i == 0 || a.in_idx[i] != a.in_idx[i - 1] + 1) {  // a new run starts at input i
-                if (nr > 0) {
-                    const uint8_t *prev_end = sb + uint64_t(a.in_idx[i - 1] + 1) * a.len;
-                    cum += uint32_t(((reinterpret_cast<uintptr_t>(prev_end) + 127) & ~uintptr_t(127)) -
-                                    reinterpret_cast<uintptr_t>(run_a[nr - 1]));
-                }
-                run_a[nr] = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(si) & ~uintptr_t(127));
-                run_base[nr] = cum;
-                ++nr;
-            }
-            in_lds_off[i] = run_base[nr - 1] + uint32_t(si - run_a[nr - 1]);
-        }
-        {
-            const uint8_t *last_end = sb + uint64_t(a.in_idx[K - 1] + 1) * a.len;
-            cum += uint32_t(((reinterpret_cast<uintptr_t>(last_end) + 127) & ~uintptr_t(127)) -
-                            reinterpret_cast<uintptr_t>(run_a[nr - 1]));
-        }
-        for (uint32_t q0 = 0; q0 < cum; q0 += 4u * 16u * kWave) {
-            u32x4 r[4];
+            const uint8_t *ai = sb + uint64_t(in_idx[i]) * len - in_off[i];
+            const uint32_t span = (in_off[i] + len + 127u) & ~127u;
 #pragma unroll
-            for (int h = 0; h < 4; ++h) {
+            for (int h = 0; h < 2; ++h) {
                 const uint32_t q = q0 + uint32_t(h) * 16u * kWave + 16u * lane;
-                if (q < cum) {
-                    int rr = 0;
-#pragma unroll
-                    for (int j = 1; j < K; ++j)
-                        if (j < nr && q >= run_base[j]) rr = j;
-                    r[h] = load_stream(run_a[rr] + (q - run_base[rr]));
-                }
+                if (q < span) r[i][h] = load_stream(ai + q);
             }
+        }
 #pragma unroll
-            for (int h = 0; h < 4; ++h) {
+        for (int i = 0; i < K; ++i) {
+            const uint32_t span = (in_off[i] + len + 127u) & ~127u;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
                 const uint32_t q = q0 + uint32_t(h) * 16u * kWave + 16u * lane;
-                if (q < cum) *reinterpret_cast<u32x4 *>(in_lds + q) = r[h];
+                if (q < span) *reinterpret_cast<u32x4 *>(in_lds + i * islot + q) = r[i][h];
             }
         }
-        __syncthreads();
-#endif
-        for (uint32_t v = lane; v < nw; v += kWave) {
-            u32x2a x[K];
-#pragma unroll
-            for (int i = 0; i < K; ++i)
-#if RSAMD_GROUP_ALIGNED_READ
-                x[i] = *reinterpret_cast<const u32x2a *>(in_lds + in_lds_off[i] + 8u * v);
-#else
-                x[i] = __builtin_nontemporal_load(
-                    reinterpret_cast<const u32x2a *>(sb + uint64_t(a.in_idx[i]) * a.len + 8u * v));
-#endif
-            uint32_t acc[M][2];
-#pragma unroll
-            for (int w = 0; w < 2; ++w) {
-#pragma unroll
-                for (int i = 0; i < K; ++i) {
-                    const Sel sl = selectors(x[i][w]);
-#pragma unroll
-                    for (int p = 0; p < M; ++p) {
-                        uint32_t t0, t1, t2;
-                        terms(a.tabs + (i * M + p) * 5, sl, t0, t1, t2);
-                        acc[p][w] = i == 0 ? xor3(t0, t1, t2) : xor3(acc[p][w], t0, t1) ^ t2;
-                    }
-                }
-            }
-#pragma unroll
-            for (int p = 0; p < M; ++p)
-                *reinterpret_cast<u32x2a *>(ls + p * a.len + 8u * v) = u32x2a{acc[p][0], acc[p][1]};
-        }
-    }
-    // The foreign bytes of each group's first and last line (inside the batch only).
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        const uint32_t t = b * G + g;
-        if (!RSAMD_GROUP_REWRITE || t >= a.n_items) break;
-        uint8_t *r0 = a.base + uint64_t(t) * a.stripe_stride + uint64_t(a.out_first) * a.len;
-        uint8_t *r1 = r0 + uint64_t(M) * a.len;
-        uint8_t *l0 = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(r0) & ~uintptr_t(127));
-        uint8_t *l1 = reinterpret_cast<uint8_t *>((reinterpret_cast<uintptr_t>(r1) + 127) & ~uintptr_t(127));
-        uint8_t *q = lane < 16 ? l0 + 8u * lane : r1 + 8u * (lane - 16);
-        const bool in = lane < 16 ? (l0 >= a.lo && q < r0) : (lane < 32 && l1 <= a.hi && q < l1);
-        if (in) *reinterpret_cast<u32x2a *>(lds + g * slot + (q - l0)) = *reinterpret_cast<const u32x2a *>(q);
     }
     __syncthreads();
-    // Phase 2: the owned lines, as aligned 16-byte stores (8-byte halves where
-    // the span starts or ends mid-vector).
+
+    // Phase 1: 8-byte columns of every output, from LDS into the run slots.
+    const uint32_t nw = len / 8;
+    for (uint32_t v = lane; v < nw; v += kWave) {
+        u32x2a x[K];
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-        const uint32_t t = b * G + g;
-        if (t >= a.n_items) break;
-        uint8_t *r0 = a.base + uint64_t(t) * a.stripe_stride + uint64_t(a.out_first) * a.len;
-        uint8_t *r1 = r0 + uint64_t(M) * a.len;
-        uint8_t *l0 = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(r0) & ~uintptr_t(127));
-        uint8_t *l1 = reinterpret_cast<uint8_t *>((reinterpret_cast<uintptr_t>(r1) + 127) & ~uintptr_t(127));
-        uint8_t *w0 = RSAMD_GROUP_REWRITE && l0 >= a.lo ? l0 : r0;  // the span this wave stores
-        uint8_t *w1 = RSAMD_GROUP_REWRITE && l1 <= a.hi ? l1 : r1;
-        uint8_t *x0 = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(w0) & ~uintptr_t(15));
+        for (int i = 0; i < K; ++i) x[i] = *reinterpret_cast<const u32x2a *>(in_lds + i * islot + in_off[i] + 8u * v);
+        uint32_t acc[MS][2];
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                const Sel sl = selectors(x[i][w]);
+#pragma unroll
+                for (int p = 0; p < MS; ++p) {
+                    uint32_t t0, t1, t2;
+                    terms(tabs + (i * MS + p) * 5, sl, t0, t1, t2);
+                    acc[p][w] = i == 0 ? xor3(t0, t1, t2) : xor3(acc[p][w], t0, t1) ^ t2;
+                }
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < MS; ++p)
+            if (p < nout) *reinterpret_cast<u32x2a *>(lds + out_lds[p] + 8u * v) = u32x2a{acc[p][0], acc[p][1]};
+    }
+    // Neighbours: is the shard next to this stripe's first / last shard rebuilt?
+    // (Asked after the input loads are in flight: a dependent chain of scalar loads.)
+    const bool has_prev = t > 0 || a.has_prev, has_next = t + 1 < a.n_items || a.has_next_last;
+    const bool prev_busy = !has_prev || group_writes<MS, MASKED>(a, int64_t(t) - 1, int(a.total) - 1);
+    const bool next_busy = !has_next || group_writes<MS, MASKED>(a, int64_t(t) + 1, 0);
+    // The foreign bytes of each run's first and last line, where nobody writes them.
+#pragma unroll
+    for (int r = 0; r < MS; ++r) {
+        if (!run_start[r]) continue;
+        const int s0 = out_idx[r], s1 = run_last[r];
+        uint8_t *r0 = sb + uint64_t(s0) * len, *r1 = sb + uint64_t(s1 + 1) * len;
+        uint8_t *l0 = r0 - (reinterpret_cast<uintptr_t>(r0) & 127u);  // pointer arithmetic keeps the
+        uint8_t *l1 = r1 + ((128u - (reinterpret_cast<uintptr_t>(r1) & 127u)) & 127u);  // global address space
+        const bool head = s0 > 0 || !prev_busy, tail = s1 + 1 < int(a.total) || !next_busy;
+        uint8_t *q = lane < 16 ? l0 + 8u * lane : r1 + 8u * (lane - 16);
+        const bool in = lane < 16 ? (head && q < r0) : (lane < 32 && tail && q < l1);
+        if (in) *reinterpret_cast<u32x2a *>(lds + run_lds[r] + (q - l0)) = *reinterpret_cast<const u32x2a *>(q);
+    }
+    __syncthreads();
+    // Phase 2: each run's lines, as aligned 16-byte stores (8-byte halves where
+    // a partial line starts or ends mid-vector).
+#pragma unroll
+    for (int r = 0; r < MS; ++r) {
+        if (!run_start[r]) continue;
+        const int s0 = out_idx[r], s1 = run_last[r];
+        uint8_t *r0 = sb + uint64_t(s0) * len, *r1 = sb + uint64_t(s1 + 1) * len;
+        uint8_t *l0 = r0 - (reinterpret_cast<uintptr_t>(r0) & 127u);  // pointer arithmetic keeps the
+        uint8_t *l1 = r1 + ((128u - (reinterpret_cast<uintptr_t>(r1) & 127u)) & 127u);  // global address space
+        const bool head = s0 > 0 || !prev_busy, tail = s1 + 1 < int(a.total) || !next_busy;
+        uint8_t *w0 = head ? l0 : r0, *w1 = tail ? l1 : r1;
+        uint8_t *x0 = w0 - (reinterpret_cast<uintptr_t>(w0) & 15u);
         for (uint8_t *q = x0 + 16u * lane; q < w1; q += 16u * kWave) {
-            const u32x4 v = *reinterpret_cast<const u32x4 *>(lds + g * slot + (q - l0));
+            const u32x4 v = *reinterpret_cast<const u32x4 *>(lds + run_lds[r] + (q - l0));
             const bool lo_in = q >= w0 && q + 8 <= w1, hi_in = q + 8 >= w0 && q + 16 <= w1;
             if (lo_in && hi_in)
-                group_store(q, v);
+                __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(q));
             else if (lo_in)
-                group_store(q, u32x2a{v[0], v[1]});
+                __builtin_nontemporal_store(u32x2a{v[0], v[1]}, reinterpret_cast<u32x2a *>(q));
             else if (hi_in)
-                group_store(q + 8, u32x2a{v[2], v[3]});
+                __builtin_nontemporal_store(u32x2a{v[2], v[3]}, reinterpret_cast<u32x2a *>(q + 8));
         }
     }
 }
@@ -1189,9 +1244,9 @@ hipError_t dispatch_vec8(const Vec8Args &a, int nout, Mode mode, hipStream_t s) 
     return hipErrorInvalidValue;
 }
 
-template <int K, int M>
+template <int K, int MS, bool MASKED>
 hipError_t launch_group8_t(const GroupArgs &a, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((gf_group8_kernel<K, M>), dim3(a.n_blocks), dim3(kWave), lds, s, a);
+    hipLaunchKernelGGL((gf_group8_kernel<K, MS, MASKED>), dim3(a.n_items), dim3(kWave), lds, s, a);
     return hipGetLastError();
 }
 
@@ -1204,40 +1259,47 @@ bool group8_enabled() {
     return on;
 }
 
-// The line-owner kernel takes an encode or uniform decode whose outputs are
-// one run of consecutive shards, on stripes of back-to-back shards (shard
-// stride = shard length, stripe stride = total shards x that) of 8-byte
-// multiples >= 128 bytes, with >= 256 bytes of non-output shards between runs
-// and a region small enough for LDS.
-constexpr size_t kGroupLdsMax = 16384;
-bool group8_applies(const Geometry &g, const DevPlan &p, Mode mode) {
-    const uintptr_t b = reinterpret_cast<uintptr_t>(g.base);
-    return mode == Mode::Code && p.out_first >= 0 && p.nin == 4 && p.nout >= 1 && p.nout <= 4 && g.total > 0 &&
-           g.col0 == 0 && g.len == g.shard_stride && g.len % 8 == 0 && g.len >= 128 && b % 8 == 0 &&
-           g.stripe_stride == size_t(g.total) * g.len && p.out_first + p.nout <= g.total &&
-           size_t(g.total - p.nout) * g.len >= 256 && RSAMD_GROUP_PER_WAVE * (size_t(p.nout) * g.len + 256) +
-               (RSAMD_GROUP_ALIGNED_READ ? size_t(p.nin) * (g.len + 256) : 0) <= 2 * kGroupLdsMax &&
-           g.len / 8 <= UINT32_MAX && group8_enabled();
+// LDS of one wave: MS output slots (a run each, at worst) and nin input slots.
+size_t group8_lds(size_t len, int nin, int ms) {
+    return size_t(ms) * ((len + 256 + 15) / 16 * 16) + size_t(nin) * ((len + 256 + 15) / 16 * 16);
 }
 
-hipError_t launch_group8(const Geometry &g, const DevPlan &p, hipStream_t s) {
-    constexpr size_t G = RSAMD_GROUP_PER_WAVE;
-    // input area (aligned reads): each run of consecutive input shards spans
-    // at most its bytes + 254 rounded to lines; nin runs at worst
-    const size_t lds = G * ((size_t(p.nout) * g.len + 256 + 15) / 16 * 16) +
-                       (RSAMD_GROUP_ALIGNED_READ ? size_t(p.nin) * (g.len + 256) : 0);
-    uint8_t *lo = g.base, *hi = g.base + g.n_stripes * g.stripe_stride;
-    for (size_t t0 = 0; t0 < g.n_stripes; t0 += kMaxGridBlocks * G) {
-        const size_t nst = std::min<size_t>(kMaxGridBlocks * G, g.n_stripes - t0);
-        const size_t blocks = (nst + G - 1) / G;
-        GroupArgs a{g.base + t0 * g.stripe_stride, p.tabs, p.in_idx, g.stripe_stride, lo, hi, uint32_t(g.len),
-                    uint32_t(p.out_first), uint32_t(nst), uint32_t(blocks), uint32_t(blocks / 8)};
+// The line-owner kernel takes k = 4 codes on stripes of back-to-back shards
+// (shard stride = shard length, stripe stride = total shards x that) of
+// 8-byte multiples >= 256 bytes, 8-byte but not 16-byte aligned (aligned
+// batches keep the 16-byte kernels), small enough for LDS.
+constexpr size_t kGroupLdsMax = 32768;
+bool group8_geometry(const Geometry &g, int nin, int ms) {
+    const uintptr_t b = reinterpret_cast<uintptr_t>(g.base);
+    return nin == 4 && ms >= 1 && ms <= kMaxOut && g.total > 0 && g.col0 == 0 && g.len == g.shard_stride &&
+           g.len % 8 == 0 && g.len >= 256 && g.len <= UINT32_MAX && b % 8 == 0 &&
+           g.stripe_stride == size_t(g.total) * g.len && group8_lds(g.len, nin, ms) <= kGroupLdsMax &&
+           group8_enabled();
+}
+
+template <bool MASKED>
+hipError_t launch_group8(const Geometry &g, GroupArgs a, int ms, hipStream_t s) {
+    const size_t lds = group8_lds(g.len, 4, ms);
+    a.stripe_stride = g.stripe_stride;
+    a.lo = g.base;
+    a.hi = g.base + g.n_stripes * g.stripe_stride;
+    a.len = uint32_t(g.len);
+    a.total = uint32_t(g.total);
+    const int32_t *ids0 = a.plan_ids;
+    for (size_t t0 = 0; t0 < g.n_stripes; t0 += kMaxGridBlocks) {
+        const size_t nst = std::min<size_t>(kMaxGridBlocks, g.n_stripes - t0);
+        a.base = g.base + t0 * g.stripe_stride;
+        a.n_items = uint32_t(nst);
+        a.xcd_span = uint32_t(nst / 8);
+        a.plan_ids = ids0 ? ids0 + t0 : nullptr;
+        a.has_prev = t0 > 0;
+        a.has_next_last = t0 + nst < g.n_stripes;
         hipError_t e = hipErrorInvalidValue;
-        switch (p.nout) {
-        case 1: e = launch_group8_t<4, 1>(a, lds, s); break;
-        case 2: e = launch_group8_t<4, 2>(a, lds, s); break;
-        case 3: e = launch_group8_t<4, 3>(a, lds, s); break;
-        case 4: e = launch_group8_t<4, 4>(a, lds, s); break;
+        switch (ms) {
+        case 1: e = launch_group8_t<4, 1, MASKED>(a, lds, s); break;
+        case 2: e = launch_group8_t<4, 2, MASKED>(a, lds, s); break;
+        case 3: e = launch_group8_t<4, 3, MASKED>(a, lds, s); break;
+        case 4: e = launch_group8_t<4, 4, MASKED>(a, lds, s); break;
         }
         if (e != hipSuccess) return e;
     }
@@ -1341,6 +1403,19 @@ hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t 
                                      g.n_stripes * (g.len / chunk_bytes) <= UINT32_MAX);
     const bool aligned8 = (reinterpret_cast<uintptr_t>(base) % 8 == 0) && g.shard_stride % 8 == 0 &&
                           g.stripe_stride % 8 == 0;
+    if (aligned8 && !aligned && pb == 0 && group8_geometry(g, p.nin, p.mslots)) {
+        GroupArgs a{};
+        a.records = p.records;
+        a.rec_stride = p.rec_stride;
+        a.plan_ids = p.plan_ids;
+        a.mask_table = p.mask_table;
+        a.mask_bits = p.mask_bits;
+        a.bad = p.bad;
+        a.rec_in_idx = uint32_t(l.in_idx);
+        a.rec_out_idx = uint32_t(l.out_idx);
+        a.rec_tabs = uint32_t(l.tabs);
+        return launch_group8<true>(g, a, p.mslots, s);
+    }
     if (aligned8 && pb == 0 && (!aligned || small_with_tail8(g.len)) && g.len / 8 <= UINT32_MAX - kWave &&
         masked8_enabled())
         return launch_masked8(g, p, l, s);
@@ -1380,8 +1455,14 @@ hipError_t launch_gf_tables(const Geometry &g, const DevPlan &p, Mode mode, int 
                          g.stripe_stride % 16 == 0;
     const bool aligned8 = (reinterpret_cast<uintptr_t>(base) % 8 == 0) && g.shard_stride % 8 == 0 &&
                           g.stripe_stride % 8 == 0;
-    if (aligned8 && !aligned && uint64_t(g.n_stripes) * g.len > kSmallBytes && group8_applies(g, p, mode))
-        return launch_group8(g, p, s);
+    if (aligned8 && !aligned && mode == Mode::Code && uint64_t(g.n_stripes) * g.len > kSmallBytes &&
+        group8_geometry(g, p.nin, p.nout)) {
+        GroupArgs a{};
+        a.tabs = p.tabs;
+        a.in_idx = p.in_idx;
+        a.out_idx = p.out_idx;
+        return launch_group8<false>(g, a, p.nout, s);
+    }
     if (aligned8 && (!aligned || small_with_tail8(g.len)) && uint64_t(g.n_stripes) * g.len > kSmallBytes &&
         g.len / 8 <= UINT32_MAX - kWave && masked8_enabled())
         return launch_vec8(g, p, mode, mismatch, s);
