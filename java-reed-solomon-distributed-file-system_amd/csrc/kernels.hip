@@ -744,44 +744,138 @@ __device__ __forceinline__ bool group_writes(const GroupArgs &a, int64_t u, int 
     return w;
 }
 
-// LDS bounds occupancy here (4+2 x 1000 B: 7.6 KiB per wave, 21 waves per
-// CU), so the register budget is 5 waves per SIMD (<= 96 VGPRs, no spills).
+// One wave per stripe; shards of 256 .. kGroupMaxLen bytes, so one pass of
+// 2 x 1 KiB loads per input covers a shard's lines and a lane codes at most
+// kGroupIters 8-byte columns.  The LDS area first holds the input lines, then
+// (after every lane has its columns in registers) the output runs: 5 KiB per
+// wave at 4+2 x 1000 B, 32 waves per CU.  Three or four outputs hold up to
+// 32 accumulator registers per lane: a budget of 5 waves per SIMD, unspilled.
+constexpr uint32_t kGroupMaxLen = 1792;
+constexpr int kGroupIters = 4;
+
 template <int K, int MS, bool MASKED>
-__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5, 8))) gf_group8_kernel(GroupArgs a) {
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MS >= 3 ? 5 : 8, 8))) gf_group8_kernel(GroupArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint32_t t = blockIdx.x;
     if (a.xcd_span && t < 8u * a.xcd_span) t = (t & 7u) * a.xcd_span + (t >> 3);
     const uint32_t lane = threadIdx.x;
     const uint32_t len = a.len;
-    const uint32_t *tabs;
-    const int32_t *in_idx, *out_idx;
-    int nout;
-    if (MASKED) {
-        // The record id first, the pointer after the check: a pointer that may
-        // be null is a generic one, which may alias the LDS stores below, and
-        // the record's tables would then be read with per-lane vector loads.
-        int32_t id = a.plan_ids[t];
-        if (a.mask_table) {
-            const uint32_t bits = uint32_t(id);
-            id = (bits >> a.mask_bits) ? -1 : a.mask_table[bits];
+    uint8_t *sb = a.base + uint64_t(t) * a.stripe_stride;
+
+    // The input shards: the first K present ones (ReedSolomon.java:210-223),
+    // straight from the stripe's bitmask when there is one -- so the input
+    // loads go out before the record lookup's chain of scalar loads returns.
+    int sidx[K];
+    uint32_t bits = 0;
+    int32_t id = 0;
+    if (!MASKED) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) sidx[i] = a.in_idx[i];
+    } else if (a.mask_table) {
+        bits = uint32_t(a.plan_ids[t]);
+        const uint32_t full = (1u << a.mask_bits) - 1u;
+        if ((bits >> a.mask_bits) || __builtin_popcount(bits) < K) {
+            count_undecodable(a.bad, lane == 0);
+            return;
         }
+        if (bits == full) return;  // nothing missing
+        uint32_t rest = bits;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            sidx[i] = __builtin_ctz(rest);
+            rest &= rest - 1u;
+        }
+    } else {
+        id = a.plan_ids[t];
         if (id < 0) {
             count_undecodable(a.bad, lane == 0);
             return;
         }
+        const int32_t *ri = reinterpret_cast<const int32_t *>(a.records + uint64_t(id) * a.rec_stride + a.rec_in_idx);
+#pragma unroll
+        for (int i = 0; i < K; ++i) sidx[i] = ri[i];
+    }
+
+    // Phase 0: each input shard's whole lines, 16-byte aligned loads, one pass.
+    const uint32_t islot = (len + 256u + 15u) & ~15u;
+    uint32_t in_off[K];
+    u32x4 r[K][2];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const uint8_t *si = sb + uint64_t(sidx[i]) * len;
+        in_off[i] = uint32_t(reinterpret_cast<uintptr_t>(si) & 127u);
+        const uint8_t *ai = si - in_off[i];
+        const uint32_t span = (in_off[i] + len + 127u) & ~127u;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t q = uint32_t(h) * 16u * kWave + 16u * lane;
+            if (q < span) r[i][h] = load_stream(ai + q);
+        }
+    }
+
+    // The coding plan (MASKED: the stripe's record, found while the loads fly).
+    // The record pointer is formed after the id check: a pointer that may be
+    // null is a generic one, which may alias LDS, and the tables would then be
+    // read with per-lane vector loads.
+    const uint32_t *tabs;
+    const int32_t *out_idx;
+    int nout;
+    if (MASKED) {
+        if (a.mask_table) {
+            id = a.mask_table[bits];
+            if (id < 0) {  // a singular survivor matrix
+                count_undecodable(a.bad, lane == 0);
+                return;
+            }
+        }
         const uint8_t *rec = a.records + uint64_t(id) * a.rec_stride;
         nout = *reinterpret_cast<const int32_t *>(rec);
-        in_idx = reinterpret_cast<const int32_t *>(rec + a.rec_in_idx);
         out_idx = reinterpret_cast<const int32_t *>(rec + a.rec_out_idx);
         tabs = reinterpret_cast<const uint32_t *>(rec + a.rec_tabs);
+        if (nout == 0) return;
     } else {
         nout = MS;
-        in_idx = a.in_idx;
         out_idx = a.out_idx;
         tabs = a.tabs;
     }
-    if (nout == 0) return;
-    uint8_t *sb = a.base + uint64_t(t) * a.stripe_stride;
+
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const uint32_t span = (in_off[i] + len + 127u) & ~127u;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t q = uint32_t(h) * 16u * kWave + 16u * lane;
+            if (q < span) *reinterpret_cast<u32x4 *>(lds + i * islot + q) = r[i][h];
+        }
+    }
+    __syncthreads();
+
+    // Phase 1: 8-byte columns of every output, from LDS into registers.
+    const uint32_t nw = len / 8;
+    uint32_t acc[kGroupIters][MS][2];
+#pragma unroll
+    for (int it = 0; it < kGroupIters; ++it) {
+        const uint32_t v = uint32_t(it) * kWave + lane;
+        if (v < nw) {
+            u32x2a x[K];
+#pragma unroll
+            for (int i = 0; i < K; ++i) x[i] = *reinterpret_cast<const u32x2a *>(lds + i * islot + in_off[i] + 8u * v);
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    const Sel sl = selectors(x[i][w]);
+#pragma unroll
+                    for (int p = 0; p < MS; ++p) {
+                        uint32_t t0, t1, t2;
+                        terms(tabs + (i * MS + p) * 5, sl, t0, t1, t2);
+                        acc[it][p][w] = i == 0 ? xor3(t0, t1, t2) : xor3(acc[it][p][w], t0, t1) ^ t2;
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();  // every lane is done with the input lines: LDS now takes the outputs
 
     // Runs of consecutive output shards and their LDS slots (memory order).
     // Every array is indexed by the unrolled p only (a runtime index would
@@ -790,22 +884,20 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5, 8
     bool run_start[MS];
     uint32_t out_lds[MS], run_lds[MS];
     int run_last[MS];
-    uint32_t cum = 0, cur_lds = 0;
-    int cur_p0 = 0;
-#pragma unroll
-    for (int p = 0; p < MS; ++p) {
-        run_start[p] = p < nout && (p == 0 || out_idx[p] != out_idx[p - 1] + 1);
-        if (run_start[p] && p > 0) {
-            cum += (uint32_t(p - cur_p0) * len + 256u + 15u) & ~15u;
-            cur_p0 = p;
-        }
-        cur_lds = cum;
-        run_lds[p] = cur_lds;
-        const uint8_t *r0 = sb + uint64_t(out_idx[cur_p0]) * len;
-        out_lds[p] = cur_lds + uint32_t(reinterpret_cast<uintptr_t>(r0) & 127u) + uint32_t(p - cur_p0) * len;
-    }
-    cum += (uint32_t(nout - cur_p0) * len + 256u + 15u) & ~15u;
     {
+        uint32_t cum = 0;
+        int cur_p0 = 0;
+#pragma unroll
+        for (int p = 0; p < MS; ++p) {
+            run_start[p] = p < nout && (p == 0 || out_idx[p] != out_idx[p - 1] + 1);
+            if (run_start[p] && p > 0) {
+                cum += (uint32_t(p - cur_p0) * len + 256u + 15u) & ~15u;
+                cur_p0 = p;
+            }
+            run_lds[p] = cum;
+            const uint8_t *r0 = sb + uint64_t(out_idx[cur_p0]) * len;
+            out_lds[p] = cum + uint32_t(reinterpret_cast<uintptr_t>(r0) & 127u) + uint32_t(p - cur_p0) * len;
+        }
         int last = 0;
 #pragma unroll
         for (int p = MS - 1; p >= 0; --p) {
@@ -813,97 +905,48 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5, 8
             run_last[p] = last;
         }
     }
-    // Input area behind the output slots: each input shard rounded out to lines.
-    const uint32_t islot = (len + 256u + 15u) & ~15u;
-    uint8_t *in_lds = lds + cum;
-
-    // Phase 0: the input shards' whole lines, all loads issued before the LDS writes.
-    uint32_t in_off[K];
 #pragma unroll
-    for (int i = 0; i < K; ++i)
-        in_off[i] = uint32_t(reinterpret_cast<uintptr_t>(sb + uint64_t(in_idx[i]) * len) & 127u);
-    const uint32_t span_max = (len + 127u + 127u) & ~127u;
-    for (uint32_t q0 = 0; q0 < span_max; q0 += 2u * 16u * kWave) {
-        u32x4 r[K][2];
+    for (int it = 0; it < kGroupIters; ++it) {
+        const uint32_t v = uint32_t(it) * kWave + lane;
+        if (v < nw) {
 #pragma unroll
-        for (int i = 0; i < K; ++i) {
-            const uint8_t *ai = sb + uint64_t(in_idx[i]) * len - in_off[i];
-            const uint32_t span = (in_off[i] + len + 127u) & ~127u;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const uint32_t q = q0 + uint32_t(h) * 16u * kWave + 16u * lane;
-                if (q < span) r[i][h] = load_stream(ai + q);
-            }
+            for (int p = 0; p < MS; ++p)
+                if (p < nout)
+                    *reinterpret_cast<u32x2a *>(lds + out_lds[p] + 8u * v) = u32x2a{acc[it][p][0], acc[it][p][1]};
         }
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            const uint32_t span = (in_off[i] + len + 127u) & ~127u;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const uint32_t q = q0 + uint32_t(h) * 16u * kWave + 16u * lane;
-                if (q < span) *reinterpret_cast<u32x4 *>(in_lds + i * islot + q) = r[i][h];
-            }
-        }
-    }
-    __syncthreads();
-
-    // Phase 1: 8-byte columns of every output, from LDS into the run slots.
-    const uint32_t nw = len / 8;
-    for (uint32_t v = lane; v < nw; v += kWave) {
-        u32x2a x[K];
-#pragma unroll
-        for (int i = 0; i < K; ++i) x[i] = *reinterpret_cast<const u32x2a *>(in_lds + i * islot + in_off[i] + 8u * v);
-        uint32_t acc[MS][2];
-#pragma unroll
-        for (int w = 0; w < 2; ++w) {
-#pragma unroll
-            for (int i = 0; i < K; ++i) {
-                const Sel sl = selectors(x[i][w]);
-#pragma unroll
-                for (int p = 0; p < MS; ++p) {
-                    uint32_t t0, t1, t2;
-                    terms(tabs + (i * MS + p) * 5, sl, t0, t1, t2);
-                    acc[p][w] = i == 0 ? xor3(t0, t1, t2) : xor3(acc[p][w], t0, t1) ^ t2;
-                }
-            }
-        }
-#pragma unroll
-        for (int p = 0; p < MS; ++p)
-            if (p < nout) *reinterpret_cast<u32x2a *>(lds + out_lds[p] + 8u * v) = u32x2a{acc[p][0], acc[p][1]};
     }
     // Neighbours: is the shard next to this stripe's first / last shard rebuilt?
-    // (Asked after the input loads are in flight: a dependent chain of scalar loads.)
     const bool has_prev = t > 0 || a.has_prev, has_next = t + 1 < a.n_items || a.has_next_last;
     const bool prev_busy = !has_prev || group_writes<MS, MASKED>(a, int64_t(t) - 1, int(a.total) - 1);
     const bool next_busy = !has_next || group_writes<MS, MASKED>(a, int64_t(t) + 1, 0);
     // The foreign bytes of each run's first and last line, where nobody writes them.
 #pragma unroll
-    for (int r = 0; r < MS; ++r) {
-        if (!run_start[r]) continue;
-        const int s0 = out_idx[r], s1 = run_last[r];
+    for (int p = 0; p < MS; ++p) {
+        if (!run_start[p]) continue;
+        const int s0 = out_idx[p], s1 = run_last[p];
         uint8_t *r0 = sb + uint64_t(s0) * len, *r1 = sb + uint64_t(s1 + 1) * len;
         uint8_t *l0 = r0 - (reinterpret_cast<uintptr_t>(r0) & 127u);  // pointer arithmetic keeps the
         uint8_t *l1 = r1 + ((128u - (reinterpret_cast<uintptr_t>(r1) & 127u)) & 127u);  // global address space
         const bool head = s0 > 0 || !prev_busy, tail = s1 + 1 < int(a.total) || !next_busy;
         uint8_t *q = lane < 16 ? l0 + 8u * lane : r1 + 8u * (lane - 16);
         const bool in = lane < 16 ? (head && q < r0) : (lane < 32 && tail && q < l1);
-        if (in) *reinterpret_cast<u32x2a *>(lds + run_lds[r] + (q - l0)) = *reinterpret_cast<const u32x2a *>(q);
+        if (in) *reinterpret_cast<u32x2a *>(lds + run_lds[p] + (q - l0)) = *reinterpret_cast<const u32x2a *>(q);
     }
     __syncthreads();
     // Phase 2: each run's lines, as aligned 16-byte stores (8-byte halves where
     // a partial line starts or ends mid-vector).
 #pragma unroll
-    for (int r = 0; r < MS; ++r) {
-        if (!run_start[r]) continue;
-        const int s0 = out_idx[r], s1 = run_last[r];
+    for (int p = 0; p < MS; ++p) {
+        if (!run_start[p]) continue;
+        const int s0 = out_idx[p], s1 = run_last[p];
         uint8_t *r0 = sb + uint64_t(s0) * len, *r1 = sb + uint64_t(s1 + 1) * len;
-        uint8_t *l0 = r0 - (reinterpret_cast<uintptr_t>(r0) & 127u);  // pointer arithmetic keeps the
-        uint8_t *l1 = r1 + ((128u - (reinterpret_cast<uintptr_t>(r1) & 127u)) & 127u);  // global address space
+        uint8_t *l0 = r0 - (reinterpret_cast<uintptr_t>(r0) & 127u);
+        uint8_t *l1 = r1 + ((128u - (reinterpret_cast<uintptr_t>(r1) & 127u)) & 127u);
         const bool head = s0 > 0 || !prev_busy, tail = s1 + 1 < int(a.total) || !next_busy;
         uint8_t *w0 = head ? l0 : r0, *w1 = tail ? l1 : r1;
         uint8_t *x0 = w0 - (reinterpret_cast<uintptr_t>(w0) & 15u);
         for (uint8_t *q = x0 + 16u * lane; q < w1; q += 16u * kWave) {
-            const u32x4 v = *reinterpret_cast<const u32x4 *>(lds + run_lds[r] + (q - l0));
+            const u32x4 v = *reinterpret_cast<const u32x4 *>(lds + run_lds[p] + (q - l0));
             const bool lo_in = q >= w0 && q + 8 <= w1, hi_in = q + 8 >= w0 && q + 16 <= w1;
             if (lo_in && hi_in)
                 __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(q));
@@ -1259,9 +1302,11 @@ bool group8_enabled() {
     return on;
 }
 
-// LDS of one wave: MS output slots (a run each, at worst) and nin input slots.
+// LDS of one wave: the nin input slots, reused for the output runs (at worst
+// one run per output, each rounded out to lines).
 size_t group8_lds(size_t len, int nin, int ms) {
-    return size_t(ms) * ((len + 256 + 15) / 16 * 16) + size_t(nin) * ((len + 256 + 15) / 16 * 16);
+    const size_t slot = (len + 256 + 15) / 16 * 16;
+    return std::max(size_t(nin), size_t(ms)) * slot;
 }
 
 // The line-owner kernel takes k = 4 codes on stripes of back-to-back shards
@@ -1272,7 +1317,7 @@ constexpr size_t kGroupLdsMax = 32768;
 bool group8_geometry(const Geometry &g, int nin, int ms) {
     const uintptr_t b = reinterpret_cast<uintptr_t>(g.base);
     return nin == 4 && ms >= 1 && ms <= kMaxOut && g.total > 0 && g.col0 == 0 && g.len == g.shard_stride &&
-           g.len % 8 == 0 && g.len >= 256 && g.len <= UINT32_MAX && b % 8 == 0 &&
+           g.len % 8 == 0 && g.len >= 256 && g.len <= kGroupMaxLen && b % 8 == 0 &&
            g.stripe_stride == size_t(g.total) * g.len && group8_lds(g.len, nin, ms) <= kGroupLdsMax &&
            group8_enabled();
 }

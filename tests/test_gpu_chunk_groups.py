@@ -112,3 +112,58 @@ def test_line_owner_kernel_edges(gpu, oracle_lib, offset):
             device.decode(rs, base, [i not in miss for i in range(T)], lay, st)
         torch.cuda.synchronize()
         np.testing.assert_array_equal(dev.cpu().numpy(), host, err_msg=f"erased {miss}")
+
+
+@pytest.mark.parametrize("offset", [136, 64])
+def test_line_owner_kernel_per_group_patterns(gpu, oracle_lib, offset):
+    """The line-owner kernel with a presence pattern per group (the master's
+    recovery, MasterImpl.java:794-839): random patterns of <= 2 erasures, plus
+    undecodable and complete groups, and runs that meet across a group
+    boundary ({5} in one group, {0} in the next).  A group rewrites a
+    neighbour's bytes only where that neighbour rebuilds nothing there; every
+    byte outside the rebuilt shards, guards included, must be unchanged."""
+    import itertools
+    import torch
+    import rsamd
+    from rsamd import device
+    from rsamd.device import StripeLayout
+    k, m, S, B = 4, 2, 1000, 603
+    T = k + m
+    want = _encoded(oracle_lib, k, m, S, B, 13)
+    guard = 512
+    host = np.full(guard + offset + B * T * S + guard, 0x77, np.uint8)
+    host[guard + offset: guard + offset + B * T * S] = want.reshape(-1)
+    allp = [[i not in mi for i in range(T)] for e in range(3) for mi in itertools.combinations(range(T), e)]
+    rng = np.random.default_rng(offset)
+    pres = np.array([allp[i] for i in rng.integers(0, len(allp), B)], dtype=bool)
+    pres[0] = [False] + [True] * (T - 1)            # the batch's first byte is rebuilt
+    pres[-1] = [True] * (T - 1) + [False]           # ... and its last
+    pres[10] = [True] * (T - 1) + [False]           # {5} next to {0}: both groups write one line
+    pres[11] = [False] + [True] * (T - 1)
+    pres[20] = [False, False, False, True, True, True]  # undecodable: untouched, counted
+    words = pres.astype(np.uint32) @ (1 << np.arange(T, dtype=np.uint32))
+    clob = host.copy()
+    v = clob[guard + offset: guard + offset + B * T * S].reshape(B, T, S)
+    v[~pres] = 0x3C
+    expect = host.copy()
+    expect[guard + offset: guard + offset + B * T * S].reshape(B, T, S)[20] = v[20]
+    dev = torch.from_numpy(clob).to("cuda:0")
+    base = dev.data_ptr() + guard + offset
+    bits = torch.from_numpy(words.view(np.int32)).to("cuda:0")
+    bad = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    rs = rsamd.ReedSolomon.create(k, m)
+    device.decode_masked_bits(rs, base, bits.data_ptr(), StripeLayout(B, S, S, T * S), bad.data_ptr(),
+                              torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert int(bad.item()) == 1
+    np.testing.assert_array_equal(dev.cpu().numpy(), expect)
+    # the same patterns as host flags (rs_decode_batch_masked_dev), stripe 20 made decodable
+    pres[20] = True
+    pres[20, [0, 1]] = False
+    v[20] = want[20]
+    v[20, [0, 1]] = 0x3C
+    dev = torch.from_numpy(clob).to("cuda:0")
+    device.decode_masked(rs, dev.data_ptr() + guard + offset, pres, StripeLayout(B, S, S, T * S),
+                         torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(dev.cpu().numpy(), host)
