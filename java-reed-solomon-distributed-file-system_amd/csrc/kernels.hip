@@ -1304,9 +1304,12 @@ bool group8_enabled() {
 
 // LDS of one wave: the nin input slots, reused for the output runs (at worst
 // one run per output, each rounded out to lines).
+#ifndef RSAMD_GROUP_LDS_PAD
+#define RSAMD_GROUP_LDS_PAD 0  // extra LDS bytes per wave: an occupancy cap for A/B builds
+#endif
 size_t group8_lds(size_t len, int nin, int ms) {
     const size_t slot = (len + 256 + 15) / 16 * 16;
-    return std::max(size_t(nin), size_t(ms)) * slot;
+    return std::max(size_t(nin), size_t(ms)) * slot + RSAMD_GROUP_LDS_PAD;
 }
 
 // The line-owner kernel takes k = 4 codes on stripes of back-to-back shards
