@@ -718,17 +718,11 @@ struct GroupArgs {
 
 typedef uint32_t u32x2a __attribute__((ext_vector_type(2)));
 
-// Might stripe u of this launch (u may be -1 or n_items) rebuild shard s?
-// Uniform plans: s is an output.  Per-stripe bitmasks: u is decodable and
-// lacks s (conservative when a code needs several launches: a shard another
-// launch rebuilds is treated as written).  Per-call records: s is an output
-// of u's record.
+// Does stripe u of this launch (u may be -1 or n_items) rebuild shard s?
+// Uniform plans: s is an output.  Per-call records: s is an output of u's
+// record.  (Per-stripe bitmasks are read in the kernel.)
 template <int MS, bool MASKED>
 __device__ __forceinline__ bool group_writes(const GroupArgs &a, int64_t u, int s) {
-    if (MASKED && a.mask_table) {
-        const uint32_t bits = uint32_t(a.plan_ids[u]);
-        return !(bits >> a.mask_bits) && a.mask_table[bits] >= 0 && !((bits >> s) & 1u);
-    }
     const int32_t *out = a.out_idx;
     int nout = MS;
     if (MASKED) {
@@ -766,13 +760,17 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MS >
     // straight from the stripe's bitmask when there is one -- so the input
     // loads go out before the record lookup's chain of scalar loads returns.
     int sidx[K];
-    uint32_t bits = 0;
+    uint32_t bits = 0, bits_prev = 0, bits_next = 0;
     int32_t id = 0;
+    const bool has_prev = t > 0 || a.has_prev, has_next = t + 1 < a.n_items || a.has_next_last;
     if (!MASKED) {
 #pragma unroll
         for (int i = 0; i < K; ++i) sidx[i] = a.in_idx[i];
     } else if (a.mask_table) {
         bits = uint32_t(a.plan_ids[t]);
+        // the neighbours' bitmasks now, in the same scalar round trip
+        bits_prev = has_prev ? uint32_t(a.plan_ids[int64_t(t) - 1]) : 0u;
+        bits_next = has_next ? uint32_t(a.plan_ids[t + 1]) : 0u;
         const uint32_t full = (1u << a.mask_bits) - 1u;
         if ((bits >> a.mask_bits) || __builtin_popcount(bits) < K) {
             count_undecodable(a.bad, lane == 0);
@@ -915,10 +913,18 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MS >
                     *reinterpret_cast<u32x2a *>(lds + out_lds[p] + 8u * v) = u32x2a{acc[it][p][0], acc[it][p][1]};
         }
     }
-    // Neighbours: is the shard next to this stripe's first / last shard rebuilt?
-    const bool has_prev = t > 0 || a.has_prev, has_next = t + 1 < a.n_items || a.has_next_last;
-    const bool prev_busy = !has_prev || group_writes<MS, MASKED>(a, int64_t(t) - 1, int(a.total) - 1);
-    const bool next_busy = !has_next || group_writes<MS, MASKED>(a, int64_t(t) + 1, 0);
+    // Neighbours: might the shard next to this stripe's first / last shard be
+    // rebuilt?  With bitmasks: whenever it is absent (an undecodable
+    // neighbour leaves it alone, but treating it as written only costs a
+    // partial line).
+    bool prev_busy, next_busy;
+    if (MASKED && a.mask_table) {
+        prev_busy = !has_prev || (bits_prev >> a.mask_bits) || !((bits_prev >> (a.total - 1)) & 1u);
+        next_busy = !has_next || (bits_next >> a.mask_bits) || !(bits_next & 1u);
+    } else {
+        prev_busy = !has_prev || group_writes<MS, MASKED>(a, int64_t(t) - 1, int(a.total) - 1);
+        next_busy = !has_next || group_writes<MS, MASKED>(a, int64_t(t) + 1, 0);
+    }
     // The foreign bytes of each run's first and last line, where nobody writes them.
 #pragma unroll
     for (int p = 0; p < MS; ++p) {
@@ -1304,12 +1310,24 @@ bool group8_enabled() {
 
 // LDS of one wave: the nin input slots, reused for the output runs (at worst
 // one run per output, each rounded out to lines).
+// The LDS a launch asks per wave also caps the waves per CU, and the two
+// forms want different caps (4 M groups of 4+2 x 1000 B, extra LDS per wave
+// on top of the 5 KiB the inputs need; profiles/r3/cg_pad_r3k.txt):
+//   extra LDS                     0      1 KiB   2.5 KiB   5 KiB
+//   waves per CU                 32       26       21       16
+//   encode / decode {0,1}       0.708    0.726    0.730    0.692
+//   per-group bitmasks          0.667    0.635    0.585    0.503
+// One plan for every group: all its waves stream, and fewer of them in flight
+// keep DRAM pages open longer; per-group records: each wave first waits for a
+// chain of dependent scalar loads, and more waves hide it.  So a uniform plan
+// asks for (nin + ms) slots (21 waves per CU), per-group records for the
+// max(nin, ms) slots they use (32).
 #ifndef RSAMD_GROUP_LDS_PAD
-#define RSAMD_GROUP_LDS_PAD 0  // extra LDS bytes per wave: an occupancy cap for A/B builds
+#define RSAMD_GROUP_LDS_PAD 0  // extra LDS bytes per wave (A/B builds)
 #endif
-size_t group8_lds(size_t len, int nin, int ms) {
+size_t group8_lds(size_t len, int nin, int ms, bool masked) {
     const size_t slot = (len + 256 + 15) / 16 * 16;
-    return std::max(size_t(nin), size_t(ms)) * slot + RSAMD_GROUP_LDS_PAD;
+    return (masked ? std::max(size_t(nin), size_t(ms)) : size_t(nin + ms)) * slot + RSAMD_GROUP_LDS_PAD;
 }
 
 // The line-owner kernel takes k = 4 codes on stripes of back-to-back shards
@@ -1321,13 +1339,13 @@ bool group8_geometry(const Geometry &g, int nin, int ms) {
     const uintptr_t b = reinterpret_cast<uintptr_t>(g.base);
     return nin == 4 && ms >= 1 && ms <= kMaxOut && g.total > 0 && g.col0 == 0 && g.len == g.shard_stride &&
            g.len % 8 == 0 && g.len >= 256 && g.len <= kGroupMaxLen && b % 8 == 0 &&
-           g.stripe_stride == size_t(g.total) * g.len && group8_lds(g.len, nin, ms) <= kGroupLdsMax &&
+           g.stripe_stride == size_t(g.total) * g.len && group8_lds(g.len, nin, ms, false) <= kGroupLdsMax &&
            group8_enabled();
 }
 
 template <bool MASKED>
 hipError_t launch_group8(const Geometry &g, GroupArgs a, int ms, hipStream_t s) {
-    const size_t lds = group8_lds(g.len, 4, ms);
+    const size_t lds = group8_lds(g.len, 4, ms, MASKED);
     a.stripe_stride = g.stripe_stride;
     a.lo = g.base;
     a.hi = g.base + g.n_stripes * g.stripe_stride;
