@@ -1090,50 +1090,53 @@ def cpu_configs(budget_s=1.0):
 # ---------------------------------------------------------------------------
 def host_link(torch, n=64 << 20, reps=8):
     """The host <-> device link measured in this run: pinned n-byte copies
-    H2D alone, D2H alone, and both at once on two streams (SDMA), GB/s.
-    The host-inclusive legs are quoted against the bound these give."""
+    H2D alone, D2H alone, and both at once on two streams (each direction
+    timed by events on its own stream), GB/s.  The host-inclusive legs are
+    quoted against the bound these give (link_bound_GiBps)."""
     a = torch.empty(n, dtype=torch.uint8, pin_memory=True)
     b = torch.empty(n, dtype=torch.uint8, pin_memory=True)
     d1 = torch.empty(n, dtype=torch.uint8, device="cuda")
     d2 = torch.empty(n, dtype=torch.uint8, device="cuda")
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
 
-    def rate(fn):
-        fn()
+    def run(up, down):
+        ev = {}
+        for name, on, st, fn in (("h2d", up, s1, lambda: d1.copy_(a, non_blocking=True)),
+                                 ("d2h", down, s2, lambda: b.copy_(d2, non_blocking=True))):
+            if not on:
+                continue
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(st):
+                e0.record(st)
+                for _ in range(reps):
+                    fn()
+                e1.record(st)
+            ev[name] = (e0, e1)
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            fn()
-        torch.cuda.synchronize()
-        return (time.perf_counter() - t0) / reps
+        return {k: n * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9 for k, (e0, e1) in ev.items()}
 
-    def h2d():
-        with torch.cuda.stream(s1):
-            d1.copy_(a, non_blocking=True)
-
-    def d2h():
-        with torch.cuda.stream(s2):
-            b.copy_(d2, non_blocking=True)
-
-    def both():
-        h2d()
-        d2h()
-
-    th, td, tb = rate(h2d), rate(d2h), rate(both)
+    run(True, True)  # warm-up
+    h2d, d2h, both = run(True, False)["h2d"], run(False, True)["d2h"], run(True, True)
     del a, b, d1, d2
-    return {"h2d_GBps": round(n / th / 1e9, 2), "d2h_GBps": round(n / td / 1e9, 2),
-            "both_GBps": round(2 * n / tb / 1e9, 2),
-            "note": f"pinned {n >> 20} MiB copies, {reps} reps each, torch copy_ on dedicated streams (SDMA)"}
+    return {"h2d_GBps": round(h2d, 2), "d2h_GBps": round(d2h, 2),
+            "both_h2d_GBps": round(both["h2d"], 2), "both_d2h_GBps": round(both["d2h"], 2),
+            "both_GBps": round(both["h2d"] + both["d2h"], 2),
+            "note": f"pinned {n >> 20} MiB copies, {reps} per direction, torch copy_ on dedicated streams, "
+                    f"each direction timed by HIP events on its own stream, alone and with the other running"}
 
 
 def link_bound_GiBps(link, up, down):
     """User GiB/s the measured link allows for a call that moves `up` bytes
-    H2D and `down` bytes D2H per user byte: the slowest of the two directions
-    alone and both together."""
+    H2D and `down` bytes D2H per user byte, with both directions overlapped
+    as far as the data allows: while both run, each moves at its rate with
+    the other running (both_*); the remainder of the larger direction at its
+    rate alone."""
     if not link:
         return None
-    t = max(up / (link["h2d_GBps"] * 1e9), down / (link["d2h_GBps"] * 1e9) if down else 0.0,
-            (up + down) / (link["both_GBps"] * 1e9))
+    h, d = link["h2d_GBps"] * 1e9, link["d2h_GBps"] * 1e9
+    hb, db = link.get("both_h2d_GBps", h / 1e9) * 1e9, link.get("both_d2h_GBps", d / 1e9) * 1e9
+    tc = min(up / hb, down / db) if down else 0.0  # both directions busy
+    t = tc + (up - hb * tc) / h + ((down - db * tc) / d if down else 0.0)
     return round(1 / t / 2**30, 2)
 
 

@@ -168,12 +168,15 @@ def test_device_refusal_under_nccl():
 
 
 def test_link_bound():
-    """link_bound_GiBps: the slowest of H2D, D2H and both directions at once."""
+    """link_bound_GiBps: both directions overlapped while both have bytes to
+    move (at their rates with the other running), then the rest alone."""
     sys.path.insert(0, ROOT)
     import bench
-    link = {"h2d_GBps": 50.0, "d2h_GBps": 50.0, "both_GBps": 90.0}
-    # 4+2 encode: 1 byte up, 0.5 down per user byte -> H2D-bound, 50 GB/s of user data
-    assert abs(bench.link_bound_GiBps(link, 1.0, 0.5) - 50e9 / 2**30) < 0.01
-    # 1 up, 1 down: both directions together bind (90 GB/s over 2 bytes)
-    assert abs(bench.link_bound_GiBps(link, 1.0, 1.0) - 45e9 / 2**30) < 0.01
+    link = {"h2d_GBps": 50.0, "d2h_GBps": 50.0, "both_h2d_GBps": 40.0, "both_d2h_GBps": 40.0}
+    # 1 byte up, 0.5 down per user byte: 12.5 ps both (0.5 up, 0.5 down), then 0.5 up alone in 10 ps
+    assert abs(bench.link_bound_GiBps(link, 1.0, 0.5) - 1 / 22.5e-12 / 2**30) < 0.01
+    # only uploads: the H2D rate alone
+    assert abs(bench.link_bound_GiBps(link, 1.0, 0.0) - 50e9 / 2**30) < 0.01
+    # 1 up, 1 down: all of it at the both-ways rates
+    assert abs(bench.link_bound_GiBps(link, 1.0, 1.0) - 40e9 / 2**30) < 0.01
     assert bench.link_bound_GiBps(None, 1.0, 0.5) is None

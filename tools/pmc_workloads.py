@@ -117,7 +117,7 @@ def main():
         bits = torch.from_numpy(rdev.presence_bits(present).view(np.int32)).to("cuda:0")
         fn = lambda: rdev.decode_masked_bits(rs, buf.data_ptr(), bits.data_ptr(), lay, 0, st)  # noqa: E731
         alg = (4 * int((~present).any(axis=1).sum()) + int((~present).sum())) * S
-        kernel = "gf_masked8_kernel<4, 2>"
+        kernel = "gf_group8_kernel<4, 2, true>" if stride == 1000 else "gf_masked8_kernel<4, 2>"
     elif name in ("cgenc", "cgdec01"):
         # the master's chunk groups packed back to back (stride 1000): the
         # line-owner kernel, encode or the uniform {0,1} decode
@@ -132,7 +132,7 @@ def main():
         else:
             fn = lambda: rdev.decode(rs, buf.data_ptr(), [False, False, True, True, True, True], lay, st)  # noqa: E731
         alg = 6 * S * B
-        kernel = "gf_group8_kernel<4, 2>"
+        kernel = "gf_group8_kernel<4, 2, false>"
     elif name == "ver104":
         k, m, S, B = 10, 4, 4 << 20, 128
         rs, lay, buf = stripes(k, m, S, B)
