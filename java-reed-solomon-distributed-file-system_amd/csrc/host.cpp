@@ -68,15 +68,41 @@ int need_device() {
     return RS_OK;
 }
 
+// The pipeline's three streams (kernels, D2H, H2D) must not share a hardware
+// queue: HIP maps streams onto a few hardware queues (GPU_MAX_HW_QUEUES, 4),
+// and two streams on one queue run in order -- a D2H copy (a blit kernel)
+// queued behind an H2D copy's wait serialises the two directions.  Which
+// queue a stream gets depends on the streams the process made before it:
+// the same 4+2 x 64 MiB pinned encode ran at 34 GiB/s or 44 GiB/s depending
+// only on how many torch streams existed first (tools/host_queues.py,
+// profiles/r3/host_queues_r3n.txt).  Streams of different priorities come
+// from different queue pools, so H2D takes the highest priority, D2H the
+// lowest and the kernels the default.
+#ifndef RSAMD_PIPE_PRIO
+#define RSAMD_PIPE_PRIO 1
+#endif
+hipError_t create_pipeline_streams(ThreadCtx *c) {
+    int least = 0, greatest = 0;
+    if (!RSAMD_PIPE_PRIO || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess || least == greatest) {
+        (void)hipGetLastError();
+        hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking);
+        return e;
+    }
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, least);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, greatest);
+    return e;
+}
+
 int thread_ctx(ThreadCtx **out) {
     int dev = 0;
     RS_HIP(hipGetDevice(&dev));
     auto it = t_ctx.m.find(dev);
     if (it == t_ctx.m.end()) {
         auto *c = new ThreadCtx;
-        hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking);
+        hipError_t e = create_pipeline_streams(c);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ready, hipEventDisableTiming);
         for (int b = 0; b < kStageBufs && e == hipSuccess; ++b) {
             e = hipEventCreateWithFlags(&c->coded[b], hipEventDisableTiming);

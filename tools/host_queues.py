@@ -4,7 +4,7 @@ created before it?  (HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues
 round robin; if the pipeline's H2D and D2H streams land on one queue, their
 copies serialize.)  Creates N torch streams (each used once), then times
 encodeParity on pinned 4+2 x 64 MiB host shards.
-  python tools/host_queues.py N"""
+  python tools/host_queues.py N [LIB]"""
 import json
 import os
 import sys
@@ -19,6 +19,9 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 def main():
     n_extra = int(sys.argv[1]) if len(sys.argv) > 1 else 0
     import torch
+    if len(sys.argv) > 2:  # a variant librsamd.so
+        from rsamd import _lib
+        _lib.LIB_PATH = os.path.abspath(sys.argv[2])
     import rsamd
     streams = [torch.cuda.Stream() for _ in range(n_extra)]
     x = torch.zeros(1024, device="cuda")
@@ -38,7 +41,7 @@ def main():
         t0 = time.perf_counter()
         rs.encodeParity(pin, 0, n)
         ts.append(time.perf_counter() - t0)
-    print(json.dumps({"extra_streams": n_extra, "GiBps": [round(k * n / t / 2**30, 2) for t in ts]}), flush=True)
+    print(json.dumps({"extra_streams": n_extra, "lib": sys.argv[2] if len(sys.argv) > 2 else "in-tree", "GiBps": [round(k * n / t / 2**30, 2) for t in ts]}), flush=True)
 
 
 if __name__ == "__main__":
