@@ -78,12 +78,22 @@ int need_device() {
 // profiles/r3/host_queues_r3n.txt).  Streams of different priorities come
 // from different queue pools, so H2D takes the highest priority, D2H the
 // lowest and the kernels the default.
-#ifndef RSAMD_PIPE_PRIO
-#define RSAMD_PIPE_PRIO 1
+#ifndef RSAMD_PIPE_MODE
+#define RSAMD_PIPE_MODE 1  // A/B: 0 plain streams, 1 priorities, 2 CU-masked streams, 3 D2H on the kernel stream
 #endif
 hipError_t create_pipeline_streams(ThreadCtx *c) {
     int least = 0, greatest = 0;
-    if (!RSAMD_PIPE_PRIO || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess || least == greatest) {
+    if (RSAMD_PIPE_MODE == 2) {
+        int dev = 0, ncu = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        std::vector<uint32_t> mask(size_t(ncu + 31) / 32, 0xFFFFFFFFu);
+        if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&c->stream, uint32_t(mask.size()), mask.data());
+        if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&c->stream2, uint32_t(mask.size()), mask.data());
+        if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&c->stream3, uint32_t(mask.size()), mask.data());
+        return e;
+    }
+    if (RSAMD_PIPE_MODE != 1 || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess || least == greatest) {
         (void)hipGetLastError();
         hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
@@ -428,7 +438,7 @@ int run_chunks_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinn
         rc = grow_pinned(&ctx->mirror, &ctx->mirror_cap, buf_bytes * size_t(nbuf));
         if (rc) return rc;
     }
-    hipStream_t up_s = upload_stream(ctx), in_s = ctx->stream, out_s = ctx->stream2;
+    hipStream_t up_s = upload_stream(ctx), in_s = ctx->stream, out_s = RSAMD_PIPE_MODE == 3 ? ctx->stream : ctx->stream2;
     rsamd::CopyPool &pool = rsamd::CopyPool::get();
     // Staged outputs are drained nbuf - 1 chunks behind (their D2H is long
     // done by then), in the same pool batch as the next chunk's inputs.  A
