@@ -68,18 +68,23 @@ int need_device() {
     return RS_OK;
 }
 
-// The pipeline's three streams (kernels, D2H, H2D) must not share a hardware
-// queue: HIP maps streams onto a few hardware queues (GPU_MAX_HW_QUEUES, 4),
-// and two streams on one queue run in order -- a D2H copy (a blit kernel)
-// queued behind an H2D copy's wait serialises the two directions.  Which
-// queue a stream gets depends on the streams the process made before it:
-// the same 4+2 x 64 MiB pinned encode ran at 34 GiB/s or 44 GiB/s depending
-// only on how many torch streams existed first (tools/host_queues.py,
-// profiles/r3/host_queues_r3n.txt).  Streams of different priorities come
-// from different queue pools, so H2D takes the highest priority, D2H the
-// lowest and the kernels the default.
+// Streams and hardware queues.  HIP maps streams onto a few hardware queues
+// (GPU_MAX_HW_QUEUES, 4); two streams on one queue run in order.  With H2D
+// copies, kernels and D2H copies on three streams, which queue each got
+// depended on the streams the process had made before: the same 4+2 x 64 MiB
+// pinned encode ran at 34 or 44 GiB/s depending only on how many torch
+// streams existed first (tools/host_queues.py, profiles/r3/host_queues_*.txt),
+// because a D2H copy (a blit kernel) queued behind an H2D copy's wait
+// serialises the two directions.  Measured over 0-5 prior streams:
+//   three plain streams                34.3, then 44.0-44.7
+//   D2H / H2D at low / high priority   44.4, 44.4, 44.4, 43.0, 40.6, 42.4
+//   three CU-masked streams            43.2-44.4
+//   D2H on the kernel stream           44.1-45.0   <- used
+// The D2H of chunk j now runs before chunk j+1's kernel on one stream, which
+// costs nothing (that kernel waits for its own, longer upload anyway), and
+// only two streams must differ: uploads (stream3) and the rest (stream).
 #ifndef RSAMD_PIPE_MODE
-#define RSAMD_PIPE_MODE 1  // A/B: 0 plain streams, 1 priorities, 2 CU-masked streams, 3 D2H on the kernel stream
+#define RSAMD_PIPE_MODE 3  // A/B: 0 plain streams, 1 priorities, 2 CU-masked streams, 3 D2H on the kernel stream
 #endif
 hipError_t create_pipeline_streams(ThreadCtx *c) {
     int least = 0, greatest = 0;
@@ -191,11 +196,12 @@ int grow_pinned(uint8_t **buf, size_t *cap, size_t want) {
 
 // ---------------------------------------------------------------------------
 // Host-buffer pipeline.  A call is cut into chunks staged through kStageBufs
-// device buffers.  `stream3` carries every H2D copy, `stream` every kernel and
-// `stream2` every D2H copy, each in chunk order, so chunk j's D2H runs beside
-// chunk j+1's H2D; events hand each buffer from its upload to its kernels, to
-// its D2H and back to the H2D that reuses it.  (Two streams that each ran
-// H2D -> kernel -> D2H fell into lockstep and never overlapped the directions.)
+// device buffers.  `stream3` carries every H2D copy and `stream` every kernel
+// and D2H copy, each in chunk order, so chunk j's D2H runs beside chunk j+1's
+// H2D; events hand each buffer from its upload to its kernels and back (after
+// its D2H) to the H2D that reuses it.  (Two streams that each ran H2D ->
+// kernel -> D2H fell into lockstep and never overlapped the directions; why
+// the D2H copies share the kernels' stream: create_pipeline_streams.)
 //
 // The link is full duplex only for async copies from page-locked memory
 // (57 GB/s one way, 97 GB/s both ways; pageable copies share one staged path
