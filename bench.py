@@ -1152,8 +1152,12 @@ def host_inclusive(rsamd, k, m, link=None):
     rs = rsamd.ReedSolomon.create(k, m)
     out = {}
 
-    def rate(fn, user_bytes, reps=3):
-        fn()
+    def rate(fn, user_bytes, reps=5):
+        # 3 untimed calls: the first allocates the staging buffers, and the
+        # second of a fresh process still runs at a third of the rate (14.6 ms
+        # against 5.6 ms for a 4+2 x 64 MiB encode, tools/host_trace.py)
+        for _ in range(3):
+            fn()
         t0 = time.perf_counter()
         for _ in range(reps):
             fn()
@@ -1256,7 +1260,8 @@ def host_inclusive_all_ranks(rsamd, parallel, r, k, m, link=None, n=64 << 20, re
     pageable = [a.copy() for a in pin]
     out = {}
     for name, sh in (("pinned", pin), ("pageable", pageable)):
-        rs.encodeParity(sh, 0, n)  # warm-up (staging buffers, pinned mirrors)
+        for _ in range(3):  # warm-up (staging buffers, pinned mirrors; a fresh process's second call is slow)
+            rs.encodeParity(sh, 0, n)
         parallel.barrier(r)
         t0 = time.perf_counter()
         for _ in range(reps):
