@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--lib", default=None)
     ap.add_argument("--granule", type=int, default=64)
+    ap.add_argument("--row-pad", type=int, default=0, help="KiB between granule rows (the packed view's stripe stride grows)")
     a = ap.parse_args()
     import torch
     if a.lib:
@@ -46,13 +47,16 @@ def main():
     k, m, S, B = 4, 2, 1 << 20, 4096
     rs = rsamd.ReedSolomon.create(k, m)
     lay = rdev.GranuleLayout.make(B, k + m, S, a.granule << 10)
+    if a.row_pad:
+        G = a.granule << 10
+        lay = rdev.StripeLayout(lay.rows, G, G, (k + m) * G + (a.row_pad << 10))
     pool = rdev.DeviceBuffer(lay.nbytes, contiguous=True)
     base, st = pool.data_ptr(), torch.cuda.current_stream()
     rdev.fill_synthetic(base, k, lay, 0x5EED, 0, st)
     rdev.encode(rs, base, lay, st)
     legs = [("enc", None), ("dec0", (0,)), ("dec5", (5,)), ("dec05", (0, 5)), ("dec01", (0, 1))]
     for r in range(a.rounds):
-        out = {"round": r, "lib": a.lib or "in-tree", "G_KiB": a.granule}
+        out = {"round": r, "lib": a.lib or "in-tree", "G_KiB": a.granule, "row_pad_KiB": a.row_pad}
         for name, miss in legs:
             if miss is None:
                 t = timed(torch, st, lambda: rdev.encode(rs, base, lay, st))
