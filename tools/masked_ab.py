@@ -61,7 +61,7 @@ def main():
         del args[i:i + 2]
     import torch
     libs = [bind(p) for p in args]
-    names = [p.split("/")[-1].replace(".so", "") for p in args]
+    names = [f"{i}:" + "/".join(p.split("/")[-2:]).replace(".so", "") for i, p in enumerate(args)]
     st = torch.cuda.current_stream()
     sp = C.c_void_p(st.cuda_stream)
     for name, k, m, S, B, G, kind in SHAPES:
