@@ -191,9 +191,6 @@ static_assert(RSAMD_VEC_AHEAD >= 2, "RSAMD_VEC_AHEAD must be >= 2");
 #ifndef RSAMD_MASKED_WAVES
 #define RSAMD_MASKED_WAVES 7  // gf_masked_kernel: see the comment on it
 #endif
-#ifndef RSAMD_MASKED_EARLY
-#define RSAMD_MASKED_EARLY 0  // gf_masked_kernel: survivors from the bitmask, loads before the record (A/B)
-#endif
 #define RSAMD_CODE_VECTORS(K, M, TABS, IN_IDX, OUT_IDX, SHARD_STRIDE, AHEAD)                              \
     constexpr bool kCarry = (K) <= 4;                                                                     \
     uint64_t out_off[M]; /* read before any store so these stay scalar loads */                          \
@@ -416,41 +413,6 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(RSAM
     bool first = v == 0;
     uint32_t pat = stripe;
     if constexpr (PAT) pat = masked_pattern<PAT>(a, stripe, chunk, first);
-#if RSAMD_MASKED_EARLY
-    if (K <= 4 && a.mask_table) {  // (wide codes: the extra registers spill)
-        // The survivors straight from the bitmask (the first K present
-        // shards, ReedSolomon.java:210-223), so the input loads go out before
-        // the record lookup's chain of scalar loads returns.  A singular
-        // survivor matrix (id < 0) codes record 0 and stores nothing.
-        const uint32_t bits = uint32_t(a.plan_ids[pat]);
-        if ((bits >> a.mask_bits) || __builtin_popcount(bits) < K) {
-            count_undecodable(a.bad, first && (PAT ? threadIdx.x == 0 : true));
-            return;
-        }
-        if (bits == (1u << a.mask_bits) - 1u || v >= a.nvec) return;
-        int32_t sidx[K];
-        uint32_t rest = bits;
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            sidx[i] = __builtin_ctz(rest);
-            rest &= rest - 1u;
-        }
-        const int32_t id = a.mask_table[bits];
-        const uint8_t *rec = a.records + uint64_t(id < 0 ? 0 : id) * a.rec_stride;
-        const int nout = id < 0 ? 0 : *reinterpret_cast<const int32_t *>(rec);
-        const int32_t *out_idx = reinterpret_cast<const int32_t *>(rec + a.rec_out_idx);
-        const uint32_t *tabs = reinterpret_cast<const uint32_t *>(rec + a.rec_tabs);
-        uint8_t *sb = a.base + uint64_t(stripe) * a.stripe_stride + uint64_t(v) * 16;
-        RSAMD_CODE_VECTORS(K, MS, tabs, sidx, out_idx, a.shard_stride, K)
-#pragma unroll
-        for (int p = 0; p < MS; ++p) asm volatile("" : "+v"(acc[p]));
-        if (id < 0) count_undecodable(a.bad, first && (PAT ? threadIdx.x == 0 : true));
-#pragma unroll
-        for (int p = 0; p < MS; ++p)
-            if (p < nout) store_stream(sb + out_off[p], acc[p]);
-        return;
-    }
-#endif
     const uint8_t *rec = masked_record(a.records, a.rec_stride, a.plan_ids, a.mask_table, a.mask_bits, pat);
     if (!rec) {
         count_undecodable(a.bad, first && (PAT ? threadIdx.x == 0 : true));
