@@ -1187,12 +1187,12 @@ def host_inclusive(rsamd, k, m, link=None):
                                   f"(file legs: a {len(data) >> 20} MiB file); PCIe-bound, never the bench value")
     # Each leg against the link bound of its traffic (bytes up / down per user byte):
     # encode k up, m down per k user bytes; decode {0,1} k up, 2 down; file encode
-    # 1 up, (k+m)/k down; file decode {0,k+m-1} 1 up (the k survivors), 1 + 1/k down
-    # (the file and the rebuilt data shard).
+    # 1 up, (k+m)/k down; file decode {0,k+m-1} 1 up (the k survivors), 1 + 2/k down
+    # (the file, and both absent shards rebuilt in place as decodeMissing does).
     legs = {"host_inclusive_encode_GiBps": (1.0, m / k), "host_inclusive_pinned_encode_GiBps": (1.0, m / k),
             "host_inclusive_decode_0_1_GiBps": (1.0, 2 / k), "host_inclusive_pinned_decode_0_1_GiBps": (1.0, 2 / k),
             "host_inclusive_file_encode_GiBps": (1.0, (k + m) / k),
-            "host_inclusive_file_decode_0_%d_GiBps" % (k + m - 1): (1.0, 1.0 + 1.0 / k)}
+            "host_inclusive_file_decode_0_%d_GiBps" % (k + m - 1): (1.0, 1.0 + 2.0 / k)}
     for key, (up, down) in legs.items():
         bound = link_bound_GiBps(link, up, down)
         if bound and key in out:
