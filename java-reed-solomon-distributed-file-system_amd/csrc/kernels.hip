@@ -141,13 +141,26 @@ __device__ __forceinline__ void emit(uint8_t *p, const u32x4 &v, int *mismatch) 
 #ifndef RSAMD_VEC_WPB
 #define RSAMD_VEC_WPB 1
 #endif
+#ifndef RSAMD_ROW_PAIR
+#define RSAMD_ROW_PAIR 0
+#endif
 __device__ __forceinline__ void block_item(uint32_t chunks, const FastDiv &cdiv, uint32_t rot, uint32_t xcd_span,
                                            uint32_t &stripe, uint32_t &chunk, uint32_t wpb = 1) {
     uint32_t b = blockIdx.x;
     if (xcd_span && b < 8u * xcd_span) b = (b & 7u) * xcd_span + (b >> 3);
     if (wpb > 1) b = b * wpb + threadIdx.x / kWave;
+#if RSAMD_ROW_PAIR
+    // A/B: stripes in pairs, the pair's chunks interleaved (stripe 2p chunk c,
+    // stripe 2p+1 chunk c, stripe 2p chunk c+1, ...); batches of an even stripe count.
+    {
+        const uint32_t pc = 2u * chunks, pair = b / pc, w = b - pair * pc;
+        stripe = 2u * pair + (w & 1u);
+        chunk = w >> 1;
+    }
+#else
     stripe = fast_div(b, cdiv);
     chunk = b - stripe * chunks;
+#endif
     if (rot) {  // stripe * rot < n_items: fits 32 bits
         const uint32_t p = stripe * rot;
         chunk += p - fast_div(p, cdiv) * chunks;
