@@ -135,32 +135,12 @@ __device__ __forceinline__ void emit(uint8_t *p, const u32x4 &v, int *mismatch) 
 //    contiguous range per XCD instead of every 8th chunk.
 // Both are bijections on [0, n_items); blocks past 8 * xcd_span keep the
 // identity map.
-// RSAMD_VEC_WPB (A/B builds): waves per workgroup of gf_vec_kernel; the
-// waves of workgroup B take items B*WPB .. B*WPB+WPB-1 (the remap works on
-// workgroups, so they stay on one XCD).
-#ifndef RSAMD_VEC_WPB
-#define RSAMD_VEC_WPB 1
-#endif
-#ifndef RSAMD_ROW_PAIR
-#define RSAMD_ROW_PAIR 0
-#endif
 __device__ __forceinline__ void block_item(uint32_t chunks, const FastDiv &cdiv, uint32_t rot, uint32_t xcd_span,
-                                           uint32_t &stripe, uint32_t &chunk, uint32_t wpb = 1) {
+                                           uint32_t &stripe, uint32_t &chunk) {
     uint32_t b = blockIdx.x;
     if (xcd_span && b < 8u * xcd_span) b = (b & 7u) * xcd_span + (b >> 3);
-    if (wpb > 1) b = b * wpb + threadIdx.x / kWave;
-#if RSAMD_ROW_PAIR
-    // A/B: stripes in pairs, the pair's chunks interleaved (stripe 2p chunk c,
-    // stripe 2p+1 chunk c, stripe 2p chunk c+1, ...); batches of an even stripe count.
-    {
-        const uint32_t pc = 2u * chunks, pair = b / pc, w = b - pair * pc;
-        stripe = 2u * pair + (w & 1u);
-        chunk = w >> 1;
-    }
-#else
     stripe = fast_div(b, cdiv);
     chunk = b - stripe * chunks;
-#endif
     if (rot) {  // stripe * rot < n_items: fits 32 bits
         const uint32_t p = stripe * rot;
         chunk += p - fast_div(p, cdiv) * chunks;
@@ -283,12 +263,11 @@ static_assert(RSAMD_VEC_AHEAD >= 2, "RSAMD_VEC_AHEAD must be >= 2");
 // coefficient tables, so every table load is a scalar load.
 // ---------------------------------------------------------------------------
 template <int K, int M, bool VERIFY>
-__global__ void __launch_bounds__(kWave * RSAMD_VEC_WPB) __attribute__((amdgpu_waves_per_eu(RSAMD_VEC_WAVES, 8))) gf_vec_kernel(VecArgs a) {
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(RSAMD_VEC_WAVES, 8))) gf_vec_kernel(VecArgs a) {
     if (VERIFY && mismatch_seen(a.mismatch)) return;
     uint32_t stripe, chunk;
-    block_item(a.chunks, a.cdiv, a.rot, a.xcd_span, stripe, chunk, RSAMD_VEC_WPB);
-    if (RSAMD_VEC_WPB > 1 && stripe * a.chunks + chunk >= a.n_items) return;
-    const uint32_t v = chunk * uint32_t(kWave) + threadIdx.x % kWave;
+    block_item(a.chunks, a.cdiv, a.rot, a.xcd_span, stripe, chunk);
+    const uint32_t v = chunk * uint32_t(kWave) + threadIdx.x;
     if (v >= a.nvec) return;
     uint8_t *sb = a.base + uint64_t(stripe) * a.stripe_stride + uint64_t(v) * 16;
     RSAMD_CODE_VECTORS(K, M, a.tabs, a.in_idx, a.out_idx, a.shard_stride, RSAMD_VEC_AHEAD)
@@ -1102,13 +1081,10 @@ __global__ void copy_tail_kernel(uint8_t *dst, const uint8_t *src, uint64_t n) {
 // ---------------------------------------------------------------------------
 template <int K, int M>
 hipError_t launch_vec_t(VecArgs a, Mode mode, hipStream_t s) {
-    constexpr uint32_t W = RSAMD_VEC_WPB;
-    const uint32_t blocks = (a.n_items + W - 1) / W;
-    if (W > 1) a.xcd_span = a.xcd_span ? blocks / 8u : 0u;  // remap workgroups
     if (mode == Mode::Verify)
-        hipLaunchKernelGGL((gf_vec_kernel<K, M, true>), dim3(blocks), dim3(kWave * W), 0, s, a);
+        hipLaunchKernelGGL((gf_vec_kernel<K, M, true>), dim3(a.n_items), dim3(kWave), 0, s, a);
     else
-        hipLaunchKernelGGL((gf_vec_kernel<K, M, false>), dim3(blocks), dim3(kWave * W), 0, s, a);
+        hipLaunchKernelGGL((gf_vec_kernel<K, M, false>), dim3(a.n_items), dim3(kWave), 0, s, a);
     return hipGetLastError();
 }
 
