@@ -710,32 +710,12 @@ struct GroupArgs {
 
 typedef uint32_t u32x2a __attribute__((ext_vector_type(2)));
 
-// Does stripe u of this launch (u may be -1 or n_items) rebuild shard s?
-// Uniform plans: s is an output.  Per-call records: s is an output of u's
-// record.  (Per-stripe bitmasks are read in the kernel.)
-template <int MS, bool MASKED>
-__device__ __forceinline__ bool group_writes(const GroupArgs &a, int64_t u, int s) {
-    const int32_t *out = a.out_idx;
-    int nout = MS;
-    if (MASKED) {
-        const int32_t id = a.plan_ids[u];
-        if (id < 0) return false;
-        const uint8_t *rec = a.records + uint64_t(id) * a.rec_stride;
-        nout = *reinterpret_cast<const int32_t *>(rec);
-        out = reinterpret_cast<const int32_t *>(rec + a.rec_out_idx);
-    }
-    bool w = false;
-#pragma unroll
-    for (int p = 0; p < MS; ++p) w |= p < nout && out[p] == s;
-    return w;
-}
-
 // One wave per stripe; shards of 256 .. kGroupMaxLen bytes, so one pass of
 // 2 x 1 KiB loads per input covers a shard's lines and a lane codes at most
 // kGroupIters 8-byte columns.  The LDS area first holds the input lines, then
 // (after every lane has its columns in registers) the output runs: 5 KiB per
-// wave at 4+2 x 1000 B, 32 waves per CU.  Three or four outputs hold up to
-// 32 accumulator registers per lane: a budget of 5 waves per SIMD, unspilled.
+// wave at 4+2 x 1000 B.  Three or four outputs hold up to 32 accumulator
+// registers per lane: a budget of 5 waves per SIMD, unspilled.
 constexpr uint32_t kGroupMaxLen = 1792;
 constexpr int kGroupIters = 4;
 
@@ -746,47 +726,98 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MS >
     if (a.xcd_span && t < 8u * a.xcd_span) t = (t & 7u) * a.xcd_span + (t >> 3);
     const uint32_t lane = threadIdx.x;
     const uint32_t len = a.len;
+    const int T = int(a.total);
     uint8_t *sb = a.base + uint64_t(t) * a.stripe_stride;
-
-    // The input shards: the first K present ones (ReedSolomon.java:210-223),
-    // straight from the stripe's bitmask when there is one -- so the input
-    // loads go out before the record lookup's chain of scalar loads returns.
-    int sidx[K];
-    uint32_t bits = 0, bits_prev = 0, bits_next = 0;
-    int32_t id = 0;
     const bool has_prev = t > 0 || a.has_prev, has_next = t + 1 < a.n_items || a.has_next_last;
-    if (!MASKED) {
-#pragma unroll
-        for (int i = 0; i < K; ++i) sidx[i] = a.in_idx[i];
-    } else if (a.mask_table) {
+
+    // Inputs, outputs and the neighbours' claims on this stripe's edge shards,
+    // all known before any load: the first K present shards are the survivors
+    // (ReedSolomon.java:210-223) and every absent shard is an output, in
+    // ascending order -- read off the stripe's bitmask (MASKED) or the plan.
+    int sidx[K], oidx[MS];
+    int nout;
+    const uint32_t *tabs;
+    bool prev_busy, next_busy;  // the previous stripe rebuilds its last shard / the next its first
+    uint32_t bits = 0;
+    if (MASKED) {
         bits = uint32_t(a.plan_ids[t]);
-        // the neighbours' bitmasks now, in the same scalar round trip
-        bits_prev = has_prev ? uint32_t(a.plan_ids[int64_t(t) - 1]) : 0u;
-        bits_next = has_next ? uint32_t(a.plan_ids[t + 1]) : 0u;
+        const uint32_t bp = has_prev ? uint32_t(a.plan_ids[int64_t(t) - 1]) : 0u;
+        const uint32_t bn = has_next ? uint32_t(a.plan_ids[t + 1]) : 0u;
         const uint32_t full = (1u << a.mask_bits) - 1u;
         if ((bits >> a.mask_bits) || __builtin_popcount(bits) < K) {
             count_undecodable(a.bad, lane == 0);
             return;
         }
         if (bits == full) return;  // nothing missing
-        uint32_t rest = bits;
+        uint32_t rest = bits, miss = ~bits & full;
+        nout = __builtin_popcount(miss);
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             sidx[i] = __builtin_ctz(rest);
             rest &= rest - 1u;
         }
-    } else {
-        id = a.plan_ids[t];
-        if (id < 0) {
+#pragma unroll
+        for (int p = 0; p < MS; ++p) {
+            oidx[p] = miss ? __builtin_ctz(miss) : T;
+            miss &= miss - 1u;
+        }
+        // conservative: an absent shard of an undecodable neighbour counts as rebuilt
+        prev_busy = !has_prev || (bp >> a.mask_bits) || !((bp >> (T - 1)) & 1u);
+        next_busy = !has_next || (bn >> a.mask_bits) || !(bn & 1u);
+        // The record's tables.  Its id is read before any vector load (there
+        // it stays a scalar load; behind the input loads the compiler read it
+        // per lane, and the tables with it).  The pointer is formed after the
+        // id check: a pointer that may be null is a generic one, which may
+        // alias LDS, and the tables would then be read with per-lane loads.
+        const int32_t id = a.mask_table[bits];
+        if (id < 0) {  // a singular survivor matrix
             count_undecodable(a.bad, lane == 0);
             return;
         }
-        const int32_t *ri = reinterpret_cast<const int32_t *>(a.records + uint64_t(id) * a.rec_stride + a.rec_in_idx);
+        tabs = reinterpret_cast<const uint32_t *>(a.records + uint64_t(id) * a.rec_stride + a.rec_tabs);
+    } else {
+        nout = MS;
+        tabs = a.tabs;
 #pragma unroll
-        for (int i = 0; i < K; ++i) sidx[i] = ri[i];
+        for (int i = 0; i < K; ++i) sidx[i] = a.in_idx[i];
+#pragma unroll
+        for (int p = 0; p < MS; ++p) oidx[p] = a.out_idx[p];
+        prev_busy = !has_prev || oidx[MS - 1] == T - 1;
+        next_busy = !has_next || oidx[0] == 0;
     }
 
-    // Phase 0: each input shard's whole lines, 16-byte aligned loads, one pass.
+    // Runs of consecutive output shards and their LDS slots (memory order).
+    // Every array is indexed by the unrolled p only (a runtime index would
+    // put it in scratch): run_start[p] marks the first output of a run,
+    // run_lds[p] its slot, run_last[p] the last shard of p's run.
+    bool run_start[MS];
+    uint32_t out_lds[MS], run_lds[MS];
+    int run_last[MS];
+    {
+        uint32_t cum = 0;
+        int cur_p0 = 0;
+#pragma unroll
+        for (int p = 0; p < MS; ++p) {
+            run_start[p] = p < nout && (p == 0 || oidx[p] != oidx[p - 1] + 1);
+            if (run_start[p] && p > 0) {
+                cum += (uint32_t(p - cur_p0) * len + 256u + 15u) & ~15u;
+                cur_p0 = p;
+            }
+            run_lds[p] = cum;
+            const uint8_t *r0 = sb + uint64_t(oidx[cur_p0]) * len;
+            out_lds[p] = cum + uint32_t(reinterpret_cast<uintptr_t>(r0) & 127u) + uint32_t(p - cur_p0) * len;
+        }
+        int last = 0;
+#pragma unroll
+        for (int p = MS - 1; p >= 0; --p) {
+            if (p < nout && (p == nout - 1 || (p + 1 < MS && run_start[p + 1]))) last = oidx[p];
+            run_last[p] = last;
+        }
+    }
+
+    // Phase 0: each input shard's whole lines (16-byte aligned loads, one
+    // pass), and the foreign bytes of each run's first and last line where
+    // nobody writes them -- all loads issued together.
     const uint32_t islot = (len + 256u + 15u) & ~15u;
     uint32_t in_off[K];
     u32x4 r[K][2];
@@ -802,31 +833,23 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MS >
             if (q < span) r[i][h] = load_stream(ai + q);
         }
     }
-
-    // The coding plan (MASKED: the stripe's record, found while the loads fly).
-    // The record pointer is formed after the id check: a pointer that may be
-    // null is a generic one, which may alias LDS, and the tables would then be
-    // read with per-lane vector loads.
-    const uint32_t *tabs;
-    const int32_t *out_idx;
-    int nout;
-    if (MASKED) {
-        if (a.mask_table) {
-            id = a.mask_table[bits];
-            if (id < 0) {  // a singular survivor matrix
-                count_undecodable(a.bad, lane == 0);
-                return;
-            }
-        }
-        const uint8_t *rec = a.records + uint64_t(id) * a.rec_stride;
-        nout = *reinterpret_cast<const int32_t *>(rec);
-        out_idx = reinterpret_cast<const int32_t *>(rec + a.rec_out_idx);
-        tabs = reinterpret_cast<const uint32_t *>(rec + a.rec_tabs);
-        if (nout == 0) return;
-    } else {
-        nout = MS;
-        out_idx = a.out_idx;
-        tabs = a.tabs;
+    bool head[MS], tail[MS], fin[MS];
+    uint32_t foff[MS];
+    u32x2a fv[MS];
+#pragma unroll
+    for (int p = 0; p < MS; ++p) {
+        fin[p] = false;
+        if (!run_start[p]) continue;
+        const int s0 = oidx[p], s1 = run_last[p];
+        uint8_t *r0 = sb + uint64_t(s0) * len, *r1 = sb + uint64_t(s1 + 1) * len;
+        uint8_t *l0 = r0 - (reinterpret_cast<uintptr_t>(r0) & 127u);  // pointer arithmetic keeps the
+        uint8_t *l1 = r1 + ((128u - (reinterpret_cast<uintptr_t>(r1) & 127u)) & 127u);  // global address space
+        head[p] = s0 > 0 || !prev_busy;
+        tail[p] = s1 + 1 < T || !next_busy;
+        uint8_t *q = lane < 16 ? l0 + 8u * lane : r1 + 8u * (lane - 16);
+        fin[p] = lane < 16 ? (head[p] && q < r0) : (lane < 32 && tail[p] && q < l1);
+        foff[p] = run_lds[p] + uint32_t(q - l0);
+        if (fin[p]) fv[p] = *reinterpret_cast<const u32x2a *>(q);
     }
 
 #pragma unroll
@@ -840,7 +863,12 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MS >
     }
     __syncthreads();
 
-    // Phase 1: 8-byte columns of every output, from LDS into registers.
+    // Phase 1: 8-byte columns of every output, from LDS into registers.  The
+    // tables are read through the constant address space: they are not
+    // written while the kernel runs, and a load behind a barrier from a
+    // global pointer cannot be proven unclobbered (it would be read per lane).
+    const __attribute__((address_space(4))) uint32_t *ctabs =
+        (const __attribute__((address_space(4))) uint32_t *)(tabs);
     const uint32_t nw = len / 8;
     uint32_t acc[kGroupIters][MS][2];
 #pragma unroll
@@ -857,8 +885,10 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MS >
                     const Sel sl = selectors(x[i][w]);
 #pragma unroll
                     for (int p = 0; p < MS; ++p) {
-                        uint32_t t0, t1, t2;
-                        terms(tabs + (i * MS + p) * 5, sl, t0, t1, t2);
+                        uint32_t t0, t1, t2, tp[5];
+#pragma unroll
+                        for (int j = 0; j < 5; ++j) tp[j] = ctabs[(i * MS + p) * 5 + j];
+                        terms(tp, sl, t0, t1, t2);
                         acc[it][p][w] = i == 0 ? xor3(t0, t1, t2) : xor3(acc[it][p][w], t0, t1) ^ t2;
                     }
                 }
@@ -867,34 +897,6 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MS >
     }
     __syncthreads();  // every lane is done with the input lines: LDS now takes the outputs
 
-    // Runs of consecutive output shards and their LDS slots (memory order).
-    // Every array is indexed by the unrolled p only (a runtime index would
-    // put it in scratch): run_start[p] marks the first output of a run,
-    // run_lds[p] its slot, run_last[p] the last shard of p's run.
-    bool run_start[MS];
-    uint32_t out_lds[MS], run_lds[MS];
-    int run_last[MS];
-    {
-        uint32_t cum = 0;
-        int cur_p0 = 0;
-#pragma unroll
-        for (int p = 0; p < MS; ++p) {
-            run_start[p] = p < nout && (p == 0 || out_idx[p] != out_idx[p - 1] + 1);
-            if (run_start[p] && p > 0) {
-                cum += (uint32_t(p - cur_p0) * len + 256u + 15u) & ~15u;
-                cur_p0 = p;
-            }
-            run_lds[p] = cum;
-            const uint8_t *r0 = sb + uint64_t(out_idx[cur_p0]) * len;
-            out_lds[p] = cum + uint32_t(reinterpret_cast<uintptr_t>(r0) & 127u) + uint32_t(p - cur_p0) * len;
-        }
-        int last = 0;
-#pragma unroll
-        for (int p = MS - 1; p >= 0; --p) {
-            if (p < nout && (p == nout - 1 || (p + 1 < MS && run_start[p + 1]))) last = out_idx[p];
-            run_last[p] = last;
-        }
-    }
 #pragma unroll
     for (int it = 0; it < kGroupIters; ++it) {
         const uint32_t v = uint32_t(it) * kWave + lane;
@@ -905,43 +907,20 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MS >
                     *reinterpret_cast<u32x2a *>(lds + out_lds[p] + 8u * v) = u32x2a{acc[it][p][0], acc[it][p][1]};
         }
     }
-    // Neighbours: might the shard next to this stripe's first / last shard be
-    // rebuilt?  With bitmasks: whenever it is absent (an undecodable
-    // neighbour leaves it alone, but treating it as written only costs a
-    // partial line).
-    bool prev_busy, next_busy;
-    if (MASKED && a.mask_table) {
-        prev_busy = !has_prev || (bits_prev >> a.mask_bits) || !((bits_prev >> (a.total - 1)) & 1u);
-        next_busy = !has_next || (bits_next >> a.mask_bits) || !(bits_next & 1u);
-    } else {
-        prev_busy = !has_prev || group_writes<MS, MASKED>(a, int64_t(t) - 1, int(a.total) - 1);
-        next_busy = !has_next || group_writes<MS, MASKED>(a, int64_t(t) + 1, 0);
-    }
-    // The foreign bytes of each run's first and last line, where nobody writes them.
 #pragma unroll
-    for (int p = 0; p < MS; ++p) {
-        if (!run_start[p]) continue;
-        const int s0 = out_idx[p], s1 = run_last[p];
-        uint8_t *r0 = sb + uint64_t(s0) * len, *r1 = sb + uint64_t(s1 + 1) * len;
-        uint8_t *l0 = r0 - (reinterpret_cast<uintptr_t>(r0) & 127u);  // pointer arithmetic keeps the
-        uint8_t *l1 = r1 + ((128u - (reinterpret_cast<uintptr_t>(r1) & 127u)) & 127u);  // global address space
-        const bool head = s0 > 0 || !prev_busy, tail = s1 + 1 < int(a.total) || !next_busy;
-        uint8_t *q = lane < 16 ? l0 + 8u * lane : r1 + 8u * (lane - 16);
-        const bool in = lane < 16 ? (head && q < r0) : (lane < 32 && tail && q < l1);
-        if (in) *reinterpret_cast<u32x2a *>(lds + run_lds[p] + (q - l0)) = *reinterpret_cast<const u32x2a *>(q);
-    }
+    for (int p = 0; p < MS; ++p)
+        if (fin[p]) *reinterpret_cast<u32x2a *>(lds + foff[p]) = fv[p];
     __syncthreads();
     // Phase 2: each run's lines, as aligned 16-byte stores (8-byte halves where
     // a partial line starts or ends mid-vector).
 #pragma unroll
     for (int p = 0; p < MS; ++p) {
         if (!run_start[p]) continue;
-        const int s0 = out_idx[p], s1 = run_last[p];
+        const int s0 = oidx[p], s1 = run_last[p];
         uint8_t *r0 = sb + uint64_t(s0) * len, *r1 = sb + uint64_t(s1 + 1) * len;
         uint8_t *l0 = r0 - (reinterpret_cast<uintptr_t>(r0) & 127u);
         uint8_t *l1 = r1 + ((128u - (reinterpret_cast<uintptr_t>(r1) & 127u)) & 127u);
-        const bool head = s0 > 0 || !prev_busy, tail = s1 + 1 < int(a.total) || !next_busy;
-        uint8_t *w0 = head ? l0 : r0, *w1 = tail ? l1 : r1;
+        uint8_t *w0 = head[p] ? l0 : r0, *w1 = tail[p] ? l1 : r1;
         uint8_t *x0 = w0 - (reinterpret_cast<uintptr_t>(w0) & 15u);
         for (uint8_t *q = x0 + 16u * lane; q < w1; q += 16u * kWave) {
             const u32x4 v = *reinterpret_cast<const u32x4 *>(lds + run_lds[p] + (q - l0));
@@ -1461,7 +1440,10 @@ hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t 
                                      g.n_stripes * (g.len / chunk_bytes) <= UINT32_MAX);
     const bool aligned8 = (reinterpret_cast<uintptr_t>(base) % 8 == 0) && g.shard_stride % 8 == 0 &&
                           g.stripe_stride % 8 == 0;
-    if (aligned8 && !aligned && pb == 0 && group8_geometry(g, p.nin, p.mslots)) {
+    // (the line-owner kernel reads a stripe's outputs off its bitmask: a
+    // pattern table, and every pattern's absent shards in one launch group)
+    if (aligned8 && !aligned && pb == 0 && p.mask_table && g.total > 0 && p.mslots >= g.total - p.nin &&
+        group8_geometry(g, p.nin, p.mslots)) {
         GroupArgs a{};
         a.records = p.records;
         a.rec_stride = p.rec_stride;
