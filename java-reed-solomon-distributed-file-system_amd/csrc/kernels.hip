@@ -1296,9 +1296,13 @@ bool group8_enabled() {
 #ifndef RSAMD_GROUP_LDS_PAD
 #define RSAMD_GROUP_LDS_PAD 0  // extra LDS bytes per wave (A/B builds)
 #endif
+#ifndef RSAMD_GROUP_LDS_MODE
+#define RSAMD_GROUP_LDS_MODE 0  // A/B: 0 per form (below), 1 both at max(nin, ms) slots, 2 both at nin + ms
+#endif
 size_t group8_lds(size_t len, int nin, int ms, bool masked) {
     const size_t slot = (len + 256 + 15) / 16 * 16;
-    return (masked ? std::max(size_t(nin), size_t(ms)) : size_t(nin + ms)) * slot + RSAMD_GROUP_LDS_PAD;
+    const bool wide = RSAMD_GROUP_LDS_MODE == 2 || (RSAMD_GROUP_LDS_MODE == 0 && !masked);
+    return (wide ? size_t(nin + ms) : std::max(size_t(nin), size_t(ms))) * slot + RSAMD_GROUP_LDS_PAD;
 }
 
 // The line-owner kernel takes k = 4 codes on stripes of back-to-back shards
