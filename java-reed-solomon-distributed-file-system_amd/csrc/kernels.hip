@@ -666,23 +666,25 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(8, 8
 // Here ONE wave owns a group, and every line it touches it touches whole:
 //  * phase 0: each input shard's lines (the shard's bytes rounded out to
 //    128-byte lines) as aligned 16-byte loads into LDS;
-//  * phase 1: each lane codes 8-byte columns of every output from LDS and
-//    parks them in LDS in memory order, one slot per run of consecutive
-//    output shards;
+//  * phase 1: each lane codes 8-byte columns of every output from LDS into
+//    registers, then (the input lines no longer needed) parks them in LDS in
+//    memory order, one slot per run of consecutive output shards;
 //  * phase 2: each run is stored as whole aligned lines (16-byte non-temporal
 //    stores).  The bytes of a run's first and last line that lie outside it
 //    belong to the neighbouring shard; when nobody writes that shard in this
 //    launch (a shard of this group that is not an output -- runs are maximal
 //    -- or a neighbouring group's shard that group does not rebuild), the wave
-//    loads those bytes and writes them back unchanged, so HBM sees no partial
-//    line.  Otherwise (or at the batch's ends) the line stays partial.
+//    loads those bytes (with the input loads) and writes them back unchanged,
+//    so HBM sees no partial line.  Otherwise (or at the batch's ends) the line
+//    stays partial.
 // Shards of >= 256 bytes keep two runs of one group on different lines.
-// Measured on 4 M groups (profiles/r3/): encode 0.738 of peak against 0.590
-// for the 8-byte kernel, with PMC traffic 1.07x the algorithmic bytes (the
-// rounding to lines).  Variants measured and dropped (A/B builds): 8-byte
-// lane loads straight from HBM 0.645, no write-back of the foreign bytes
-// 0.578, plain stores 0.58, two groups per wave 0.62, loading a line shared by
-// two input shards once 0.60 (its loads took two round trips).
+// Measured on 4 M groups (profiles/r3/): encode and decode
+// {0,1} 0.745 of peak against 0.590 for the 8-byte kernels, per-group
+// bitmasks 0.69 against 0.605, PMC traffic 1.07x / 1.12x the algorithmic
+// bytes (the rounding to lines).  Variants measured and dropped (A/B builds):
+// 8-byte lane loads straight from HBM 0.645, no write-back of the foreign
+// bytes 0.578, plain stores 0.58, two groups per wave 0.62, loading a line
+// shared by two input shards once 0.60 (its loads took two round trips).
 // ---------------------------------------------------------------------------
 struct GroupArgs {
     uint8_t *base;            // stripe 0 of this launch
