@@ -85,8 +85,9 @@ def test_line_owner_kernel_edges(gpu, oracle_lib, offset):
     their own values -- but never a byte outside the batch.  The batch sits
     inside a guarded buffer (base 8- but not 16-aligned, or 64-aligned); every
     run of consecutive shards is erased and rebuilt (encode: 4-5; decodes:
-    {0}, {0,1}, {1,2}, {2,3}, {3,4}, {5}) and every other byte, guards included,
-    must be unchanged."""
+    {0}, {0,1}, {1,2}, {2,3}, {3,4}, {5}, and {0,5}, where every group boundary
+    line is rebuilt by both groups and the earlier one writes it whole) and
+    every other byte, guards included, must be unchanged."""
     import torch
     import rsamd
     from rsamd import device
@@ -100,7 +101,7 @@ def test_line_owner_kernel_edges(gpu, oracle_lib, offset):
     lay = StripeLayout(B, S, S, T * S)
     rs = rsamd.ReedSolomon.create(k, m)
     st = torch.cuda.current_stream()
-    for miss in [(4, 5), (0,), (0, 1), (1, 2), (2, 3), (3, 4), (5,)]:
+    for miss in [(4, 5), (0,), (0, 1), (1, 2), (2, 3), (3, 4), (5,), (0, 5)]:
         clob = host.copy()
         v = clob[guard + offset: guard + offset + B * T * S].reshape(B, T, S)
         v[:, list(miss)] = 0x3C
@@ -140,13 +141,21 @@ def test_line_owner_kernel_per_group_patterns(gpu, oracle_lib, offset):
     pres[-1] = [True] * (T - 1) + [False]           # ... and its last
     pres[10] = [True] * (T - 1) + [False]           # {5} next to {0}: both groups write one line
     pres[11] = [False] + [True] * (T - 1)
+    pres[30:40] = [False] + [True] * (T - 2) + [False]  # a run of {0,5} groups
+    pres[50] = [False] + [True] * (T - 2) + [False]     # {0,5} between an undecodable group ...
+    pres[51] = [False, False, False, True, True, True]
+    pres[49] = [True] * (T - 1) + [False]               # ... and a {5}
+    pres[60] = [True] * (T - 2) + [False, False]        # {4,5} before a singular-free {0,1}
+    pres[61] = [False, False] + [True] * (T - 2)
     pres[20] = [False, False, False, True, True, True]  # undecodable: untouched, counted
+    n_bad = 2
     words = pres.astype(np.uint32) @ (1 << np.arange(T, dtype=np.uint32))
     clob = host.copy()
     v = clob[guard + offset: guard + offset + B * T * S].reshape(B, T, S)
     v[~pres] = 0x3C
     expect = host.copy()
     expect[guard + offset: guard + offset + B * T * S].reshape(B, T, S)[20] = v[20]
+    expect[guard + offset: guard + offset + B * T * S].reshape(B, T, S)[51] = v[51]
     dev = torch.from_numpy(clob).to("cuda:0")
     base = dev.data_ptr() + guard + offset
     bits = torch.from_numpy(words.view(np.int32)).to("cuda:0")
@@ -155,13 +164,14 @@ def test_line_owner_kernel_per_group_patterns(gpu, oracle_lib, offset):
     device.decode_masked_bits(rs, base, bits.data_ptr(), StripeLayout(B, S, S, T * S), bad.data_ptr(),
                               torch.cuda.current_stream())
     torch.cuda.synchronize()
-    assert int(bad.item()) == 1
+    assert int(bad.item()) == n_bad
     np.testing.assert_array_equal(dev.cpu().numpy(), expect)
-    # the same patterns as host flags (rs_decode_batch_masked_dev), stripe 20 made decodable
-    pres[20] = True
-    pres[20, [0, 1]] = False
-    v[20] = want[20]
-    v[20, [0, 1]] = 0x3C
+    # the same patterns as host flags (rs_decode_batch_masked_dev), stripes 20 and 51 made decodable
+    for t in (20, 51):
+        pres[t] = True
+        pres[t, [0, 1]] = False
+        v[t] = want[t]
+        v[t, [0, 1]] = 0x3C
     dev = torch.from_numpy(clob).to("cuda:0")
     device.decode_masked(rs, dev.data_ptr() + guard + offset, pres, StripeLayout(B, S, S, T * S),
                          torch.cuda.current_stream())

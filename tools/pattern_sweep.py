@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Every erasure pattern of 4+2 as a uniform decode over a granule batch, and
-the random per-stripe mix as one bitmask launch.
+the random per-stripe mix as one bitmask launch (--config chunk/chunk1024: the
+master's packed 6 x 1000-B chunk groups instead).
 
 For each of the 21 non-empty patterns (6 single, 15 double erasures) the whole
 batch is decoded with that pattern (rs_decode_batch_dev on the granule view)
@@ -41,24 +42,33 @@ def timed(torch, st, fn, iters=10, warm_s=0.3):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="cfg4", choices=["headline", "cfg4"])
+    ap.add_argument("--config", default="cfg4", choices=["headline", "cfg4", "chunk", "chunk1024"])
     ap.add_argument("--shift", type=int, default=0, help="KiB added to the batch's base address")
     ap.add_argument("--no-mix", action="store_true")
+    ap.add_argument("--lib", default=None, help="a variant librsamd.so (A/B runs)")
     a = ap.parse_args()
     import numpy as np
     import torch
+    if a.lib:
+        from rsamd import _lib
+        _lib.LIB_PATH = os.path.abspath(a.lib)
     import rsamd
     from rsamd import device as rdev
     k, m = 4, 2
-    S, B = (1 << 20, 4096) if a.config == "headline" else (4096, 1 << 20)
     rs = rsamd.ReedSolomon.create(k, m)
-    lay = rdev.GranuleLayout.make(B, k + m, S)
+    if a.config.startswith("chunk"):  # the master's chunk groups, packed (bench.py chunk_group_leg)
+        S, B = 1000, 4 << 20
+        stride = 1024 if a.config == "chunk1024" else 1000
+        lay = rdev.StripeLayout(B, S, stride, (k + m) * stride)
+    else:
+        S, B = (1 << 20, 4096) if a.config == "headline" else (4096, 1 << 20)
+        lay = rdev.GranuleLayout.make(B, k + m, S)
     pool = rdev.DeviceBuffer(lay.nbytes + (a.shift << 10), contiguous=True)
     base, st = pool.data_ptr() + (a.shift << 10), torch.cuda.current_stream()
     rdev.fill_synthetic(base, k, lay, 0x5EED, 0, st)
     rdev.encode(rs, base, lay, st)
     t_enc = timed(torch, st, lambda: rdev.encode(rs, base, lay, st))
-    print(json.dumps({"config": a.config, "S": S, "B": B, "granule": lay.granule, "shift_KiB": a.shift,
+    print(json.dumps({"config": a.config, "S": S, "B": B, "granule": getattr(lay, "granule", 0), "shift_KiB": a.shift, "lib": a.lib or "in-tree",
                       "encode": round((k + m) * S * B / t_enc / 8e12, 4)}), flush=True)
     t_pat = {}
     for e in (1, 2):

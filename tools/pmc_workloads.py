@@ -17,6 +17,7 @@ Workloads (bench.py's configs):
   gmaskbits  the same in the granule layout (64 KiB rows of 16 stripes)
   cgmaskbits / cgmaskbits1k   4+2 x 1000 B x 4 M chunk groups, stride 1000 / 1024, bitmasks
   cgenc / cgdec01             the same groups at stride 1000: encode / uniform {0,1} decode (line-owner kernel)
+  cgdec05 / cgdec15           ... uniform {0,5} / {1,5} decodes
   fenc       4 GiB file -> 4+2 shards (fused)            alg file + 6 S
   fdec_05    4+2 shards {0,5} -> 4 GiB file (tiled)      alg 4 S + file
 """
@@ -118,7 +119,7 @@ def main():
         fn = lambda: rdev.decode_masked_bits(rs, buf.data_ptr(), bits.data_ptr(), lay, 0, st)  # noqa: E731
         alg = (4 * int((~present).any(axis=1).sum()) + int((~present).sum())) * S
         kernel = "gf_group8_kernel<4, 2, true>" if stride == 1000 else "gf_masked8_kernel<4, 2>"
-    elif name in ("cgenc", "cgdec01"):
+    elif name in ("cgenc", "cgdec01", "cgdec05", "cgdec15"):
         # the master's chunk groups packed back to back (stride 1000): the
         # line-owner kernel, encode or the uniform {0,1} decode
         k, m, S, B = 4, 2, 1000, 4 << 20
@@ -130,7 +131,9 @@ def main():
         if name == "cgenc":
             fn = lambda: rdev.encode(rs, buf.data_ptr(), lay, st)  # noqa: E731
         else:
-            fn = lambda: rdev.decode(rs, buf.data_ptr(), [False, False, True, True, True, True], lay, st)  # noqa: E731
+            miss = {"cgdec01": (0, 1), "cgdec05": (0, 5), "cgdec15": (1, 5)}[name]
+            pres = [i not in miss for i in range(6)]
+            fn = lambda: rdev.decode(rs, buf.data_ptr(), pres, lay, st)  # noqa: E731
         alg = 6 * S * B
         kernel = "gf_group8_kernel<4, 2, false>"
     elif name == "ver104":
