@@ -1151,10 +1151,12 @@ def host_inclusive(rsamd, k, m, link=None):
     rs = rsamd.ReedSolomon.create(k, m)
     out = {}
 
-    def rate(fn, user_bytes, reps=5):
+    def rate(fn, user_bytes, reps=12):
         # 3 untimed calls: the first allocates the staging buffers, and the
         # second of a fresh process still runs at a third of the rate (14.6 ms
-        # against 5.6 ms for a 4+2 x 64 MiB encode, tools/host_trace.py)
+        # against 5.6 ms for a 4+2 x 64 MiB encode, tools/host_trace.py).
+        # 12 timed calls: a single slow call moved a 5-call mean by 5%
+        # (profiles/r3/host_calls_r3zf.txt: pageable calls 5.56-5.65 ms)
         for _ in range(3):
             fn()
         t0 = time.perf_counter()
