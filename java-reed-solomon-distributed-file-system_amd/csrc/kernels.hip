@@ -181,6 +181,17 @@ __device__ __forceinline__ void block_item(uint32_t chunks, const FastDiv &cdiv,
 // The pair loop loads input i+q+AHEAD after folding the pair at i; with
 // AHEAD < 2 input i+1 would be read before it is loaded.
 static_assert(RSAMD_VEC_AHEAD >= 2, "RSAMD_VEC_AHEAD must be >= 2");
+// Per output count (A/B builds, profiles/r3/ahead_ab_r3zh.txt, 10+4 x 4 MiB x 128, one
+// pool): one output (a single lost shard) reads 0.749 in the granule view at 5 ahead,
+// 0.740-0.742 at 2 or 4, 0.73 with all 10 up front; two outputs with all 10 up front
+// gain 0.8 points in the granule view and lose 0.8 packed.  Both stay at 5.
+#ifndef RSAMD_VEC_AHEAD_M1
+#define RSAMD_VEC_AHEAD_M1 RSAMD_VEC_AHEAD  // ... for one output (A/B)
+#endif
+#ifndef RSAMD_VEC_AHEAD_M2
+#define RSAMD_VEC_AHEAD_M2 RSAMD_VEC_AHEAD  // ... for two outputs (A/B; >= K: all up front)
+#endif
+static_assert(RSAMD_VEC_AHEAD_M1 >= 2 && RSAMD_VEC_AHEAD_M2 >= 2, "lookahead must be >= 2");
 #ifndef RSAMD_MASKED_WAVES
 #define RSAMD_MASKED_WAVES 7  // gf_masked_kernel: see the comment on it
 #endif
@@ -270,7 +281,8 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(RSAM
     const uint32_t v = chunk * uint32_t(kWave) + threadIdx.x;
     if (v >= a.nvec) return;
     uint8_t *sb = a.base + uint64_t(stripe) * a.stripe_stride + uint64_t(v) * 16;
-    RSAMD_CODE_VECTORS(K, M, a.tabs, a.in_idx, a.out_idx, a.shard_stride, RSAMD_VEC_AHEAD)
+    RSAMD_CODE_VECTORS(K, M, a.tabs, a.in_idx, a.out_idx, a.shard_stride,
+                       M == 1 ? RSAMD_VEC_AHEAD_M1 : M == 2 ? RSAMD_VEC_AHEAD_M2 : RSAMD_VEC_AHEAD)
     if (VERIFY) {  // as in gf_masked_kernel: keep the compares' inputs from being sunk
 #pragma unroll
         for (int p = 0; p < M; ++p) asm volatile("" : "+v"(acc[p]));

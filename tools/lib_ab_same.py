@@ -5,9 +5,11 @@ every build: each library is loaded with its own handle (ctypes, RTLD_LOCAL),
 the pool comes from the first one's rs_dev_alloc (contiguous), and the
 builds take turns on it.  Prints one JSON line per repetition with the
 fraction of 8 TB/s per (shape, build).
-  python tools/lib_ab_same.py LIB [LIB ...] [--reps N]
+  python tools/lib_ab_same.py LIB [LIB ...] [--reps N] [--set single]
 Shapes: 4+2 x 1 MiB x 4096 encode (the headline) and decode {0}, 10+4 x 4 MiB x 128 encode
-and decode {0,1,2,3} and verify, 10+4 x 4 MiB x 1024 encode."""
+and decode {0,1,2,3} and verify, 10+4 x 4 MiB x 1024 encode.  --set single: decodes
+of one and two shards, packed and in the granule layout's view (4+2: 64 KiB
+granules, 10+4: 32 KiB), with the encodes for reference."""
 import ctypes as C
 import json
 import sys
@@ -18,6 +20,15 @@ SHAPES = [("4p2_1MiB_x4096_enc", 4, 2, 1 << 20, 4096, None),
           ("10p4_4MiB_x128_dec0123", 10, 4, 4 << 20, 128, (0, 1, 2, 3)),
           ("10p4_4MiB_x128_verify", 10, 4, 4 << 20, 128, "verify"),
           ("10p4_4MiB_x1024_enc", 10, 4, 4 << 20, 1024, None)]
+# (name, k, m, S, B, miss, granule)
+SINGLE = [("4p2g_enc", 4, 2, 1 << 20, 4096, None, 64 << 10),
+          ("4p2g_dec0", 4, 2, 1 << 20, 4096, (0,), 64 << 10),
+          ("10p4g_enc", 10, 4, 4 << 20, 128, None, 32 << 10),
+          ("10p4g_dec0", 10, 4, 4 << 20, 128, (0,), 32 << 10),
+          ("10p4g_dec01", 10, 4, 4 << 20, 128, (0, 1), 32 << 10),
+          ("10p4g_dec012", 10, 4, 4 << 20, 128, (0, 1, 2), 32 << 10),
+          ("10p4_dec0", 10, 4, 4 << 20, 128, (0,), 0),
+          ("10p4_dec01", 10, 4, 4 << 20, 128, (0, 1), 0)]
 
 
 def bind(path):
@@ -41,11 +52,19 @@ def main():
         i = args.index("--reps")
         reps = int(args[i + 1])
         del args[i:i + 2]
+    shapes = [sh + (0,) for sh in SHAPES]
+    if "--set" in args:
+        i = args.index("--set")
+        if args[i + 1] == "single":
+            shapes = SINGLE
+        del args[i:i + 2]
     import torch
     libs = [bind(p) for p in args]
     st = torch.cuda.current_stream()
     sp = C.c_void_p(st.cuda_stream)
-    for name, k, m, S, B, miss in SHAPES:
+    for name, k, m, S, B, miss, G in shapes:
+        if G:  # the granule layout through its packed view: B*S/G stripes of G-byte shards
+            S, B = G, B * S // G
         stride = S
         nbytes = B * (k + m) * stride
         pool, got = C.c_void_p(), C.c_int(0)
