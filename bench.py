@@ -579,6 +579,7 @@ def device_extras(torch, rs, rdev, buf, lay, stream, k, m, S, B):
         key = "decode_" + "_".join(map(str, miss))
         out[key + "_GiBps"] = round(k * S * B / t / 2**30, 2)
         out[key + "_hbm_frac"] = round((k + e) * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
+    out.update(decode_patterns(torch, rs, rdev, buf.data_ptr(), lay, stream, k, m, S, B)[0])
     # row f3: isParityCorrect over the batch (reads k+m shards, writes nothing)
     flag = torch.zeros(1, dtype=torch.int32, device=buf.device)
     t = timed(torch, stream, lambda: rdev.verify(rs, buf.data_ptr(), lay, flag.data_ptr(), stream), 5)
@@ -590,6 +591,34 @@ def device_extras(torch, rs, rdev, buf, lay, stream, k, m, S, B):
     out["copy_kernel_GBps"] = round(2 * n / t / 1e9, 1)
     out["copy_kernel_hbm_frac"] = round(2 * n / t / 1e9 / HBM_PEAK_GBPS, 4)
     return out
+
+
+def decode_patterns(torch, rs, rdev, base, lay, stream, k, m, S, B, prefix="decode_patterns"):
+    """Every erasure pattern of 1..m shards decoded uniformly over the batch
+    (after one warm-up, back to back: 2 untimed and 5 timed calls each),
+    fractions of 8 TB/s of (k + e) * S * B.  On the granule layout the
+    patterns whose rebuilt shards fill whole 128 KiB-aligned blocks run with
+    the encode and the rest 4-5 points lower."""
+    import itertools
+    pats = [mi for e in range(1, m + 1) for mi in itertools.combinations(range(k + m), e)]
+    warm(torch, lambda: rdev.decode(rs, base, [i not in pats[0] for i in range(k + m)], lay, stream))
+    fr, secs = {}, {}
+    for mi in pats:
+        present = [i not in mi for i in range(k + m)]
+        for _ in range(2):
+            rdev.decode(rs, base, present, lay, stream)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record(stream)
+        for _ in range(5):
+            rdev.decode(rs, base, present, lay, stream)
+        e.record(stream)
+        torch.cuda.synchronize()
+        t = s.elapsed_time(e) / 5 * 1e-3
+        secs[mi] = t
+        fr["_".join(map(str, mi))] = round((k + len(mi)) * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
+    v = list(fr.values())
+    return {prefix + "_hbm_frac": fr, prefix + "_min": min(v), prefix + "_max": max(v),
+            prefix + "_mean": round(sum(v) / len(v), 4)}, secs
 
 
 def cfg3_strong(torch, rsamd, parallel, r, rdev, dev, stream, total, iters):
@@ -712,6 +741,16 @@ def granule_legs(torch, rsamd, rdev, dev, stream, headline_layout="granule"):
             t = timed(torch, stream, lambda: rdev.decode_masked_bits(rs, base, bits.data_ptr(), lay, 0, stream), 5)
             out[name + "_decode_masked_bits_GiBps"] = round(k * S * B / t / 2**30, 2)
             out[name + "_decode_masked_bits_hbm_frac"] = round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)
+            # the same stripes at their patterns' uniform rates: the time the mix
+            # would take if each stripe ran as fast as a batch of its own pattern
+            pat_out, secs = decode_patterns(torch, rs, rdev, base, lay, stream, k, m, S, B,
+                                            prefix=name + "_decode_patterns")
+            out.update(pat_out)
+            counts = np.bincount(rdev.presence_bits(pres), minlength=1 << (k + m))
+            pred = sum(int(c) * secs[tuple(i for i in range(k + m) if not (w >> i) & 1)] / B
+                       for w, c in enumerate(counts) if c and w != (1 << (k + m)) - 1)
+            out[name + "_decode_masked_bits_uniform_prediction_hbm_frac"] = round(alg / pred / 1e9 / HBM_PEAK_GBPS, 4)
+            out[name + "_decode_masked_bits_time_over_prediction"] = round(t / pred, 4)
             for tag, call in (("_decode_masked", lambda: rdev.decode_masked(rs, base, pres, lay, stream)),
                               ("_decode_masked_bits",
                                lambda: rdev.decode_masked_bits(rs, base, bits.data_ptr(), lay, 0, stream))):
