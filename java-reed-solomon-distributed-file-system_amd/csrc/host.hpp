@@ -43,7 +43,10 @@ struct MaskedSlot {
     hipEvent_t uploaded = nullptr;
 };
 
-constexpr int kStageBufs = 3;  // staging buffers of the host-buffer pipeline
+#ifndef RSAMD_STAGE_BUFS
+#define RSAMD_STAGE_BUFS 3  // A/B builds: make KDEFS=-DRSAMD_STAGE_BUFS=n
+#endif
+constexpr int kStageBufs = RSAMD_STAGE_BUFS;  // staging buffers of the host-buffer pipeline
 
 struct ThreadCtx {
     hipStream_t stream = nullptr;   // host pipeline: kernels, in chunk order
