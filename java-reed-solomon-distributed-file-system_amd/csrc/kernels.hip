@@ -731,6 +731,9 @@ typedef uint32_t u32x2a __attribute__((ext_vector_type(2)));
 // wave at 4+2 x 1000 B.  Three or four outputs hold up to 32 accumulator
 // registers per lane: a budget of 5 waves per SIMD, unspilled.
 constexpr uint32_t kGroupMaxLen = 1792;
+#ifndef RSAMD_GROUP_FOREIGN_LDS
+#define RSAMD_GROUP_FOREIGN_LDS 1  // foreign bytes of a survivor's line from LDS: 0 never, 1 per-group records, 2 always
+#endif
 constexpr int kGroupIters = 4;
 
 template <int K, int MS, bool MASKED>
@@ -847,12 +850,12 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MS >
             if (q < span) r[i][h] = load_stream(ai + q);
         }
     }
-    bool head[MS], tail[MS], fin[MS];
-    uint32_t foff[MS];
+    bool head[MS], tail[MS], fin[MS], fin_lds[MS];
+    uint32_t foff[MS], fsrc[MS];
     u32x2a fv[MS];
 #pragma unroll
     for (int p = 0; p < MS; ++p) {
-        fin[p] = false;
+        fin[p] = fin_lds[p] = false;
         if (!run_start[p]) continue;
         const int s0 = oidx[p], s1 = run_last[p];
         uint8_t *r0 = sb + uint64_t(s0) * len, *r1 = sb + uint64_t(s1 + 1) * len;
@@ -863,7 +866,19 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MS >
         uint8_t *q = lane < 16 ? l0 + 8u * lane : r1 + 8u * (lane - 16);
         fin[p] = lane < 16 ? (head[p] && q < r0) : (lane < 32 && tail[p] && q < l1);
         foff[p] = run_lds[p] + uint32_t(q - l0);
-        if (fin[p]) fv[p] = *reinterpret_cast<const u32x2a *>(q);
+        // A neighbour shard of this stripe that is a survivor has the line in
+        // LDS after phase 0: read the bytes there instead of loading the line
+        // again.  Per-group records only (A/B in RSAMD_GROUP_FOREIGN_LDS).
+        if (RSAMD_GROUP_FOREIGN_LDS == 2 || (RSAMD_GROUP_FOREIGN_LDS == 1 && MASKED)) {
+            const int nb = lane < 16 ? s0 - 1 : s1 + 1;
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                if (sidx[i] == nb) {
+                    fin_lds[p] = fin[p];
+                    fsrc[p] = uint32_t(i) * islot + uint32_t(q - (sb + uint64_t(sidx[i]) * len)) + in_off[i];
+                }
+        }
+        if (fin[p] && !fin_lds[p]) fv[p] = *reinterpret_cast<const u32x2a *>(q);
     }
 
 #pragma unroll
@@ -876,6 +891,9 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MS >
         }
     }
     __syncthreads();
+#pragma unroll
+    for (int p = 0; p < MS; ++p)
+        if (fin_lds[p]) fv[p] = *reinterpret_cast<const u32x2a *>(lds + fsrc[p]);
 
     // Phase 1: 8-byte columns of every output, from LDS into registers.  The
     // tables are read through the constant address space: they are not
