@@ -692,7 +692,7 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(8, 8
 // Shards of >= 256 bytes keep two runs of one group on different lines.
 // Measured on 4 M groups (profiles/r3/): encode and decode
 // {0,1} 0.745 of peak against 0.590 for the 8-byte kernels, per-group
-// bitmasks 0.69 against 0.605, PMC traffic 1.07x / 1.12x the algorithmic
+// bitmasks 0.70 against 0.605, PMC traffic 1.05x / 1.08x the algorithmic
 // bytes (the rounding to lines).  Variants measured and dropped (A/B builds):
 // 8-byte lane loads straight from HBM 0.645, no write-back of the foreign
 // bytes 0.578, plain stores 0.58, two groups per wave 0.62, loading a line
