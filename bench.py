@@ -1135,9 +1135,10 @@ def host_link(torch, n=64 << 20, reps=8):
     b = torch.empty(n, dtype=torch.uint8, pin_memory=True)
     d1 = torch.empty(n, dtype=torch.uint8, device="cuda")
     d2 = torch.empty(n, dtype=torch.uint8, device="cuda")
-    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
 
     def run(up, down):
+        s1, s2 = streams
         ev = {}
         for name, on, st, fn in (("h2d", up, s1, lambda: d1.copy_(a, non_blocking=True)),
                                  ("d2h", down, s2, lambda: b.copy_(d2, non_blocking=True))):
@@ -1153,14 +1154,29 @@ def host_link(torch, n=64 << 20, reps=8):
         torch.cuda.synchronize()
         return {k: n * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9 for k, (e0, e1) in ev.items()}
 
-    run(True, True)  # warm-up
-    h2d, d2h, both = run(True, False)["h2d"], run(False, True)["d2h"], run(True, True)
+    # Warm-up: a fresh process's first ~2 s of two-way copies run the D2H side
+    # at 28-33 GB/s instead of 48 (profiles/r3/link_probe_r3zq.txt).
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 2.5:
+        run(True, True)
+    h2d, d2h = run(True, False)["h2d"], run(False, True)["d2h"]
+    # Both at once: the best of 3 stream pairs.  Streams map onto the
+    # process's few hardware queues by creation order, and a pair that lands
+    # on one queue serialises the directions (D2H read 28 GB/s instead of 48
+    # in one run, bench_r3zp.json): that is the pair, not the link.
+    both = None
+    for _ in range(3):
+        streams[:] = [torch.cuda.Stream(), torch.cuda.Stream()]
+        got = run(True, True)
+        if both is None or got["h2d"] + got["d2h"] > both["h2d"] + both["d2h"]:
+            both = got
     del a, b, d1, d2
     return {"h2d_GBps": round(h2d, 2), "d2h_GBps": round(d2h, 2),
             "both_h2d_GBps": round(both["h2d"], 2), "both_d2h_GBps": round(both["d2h"], 2),
             "both_GBps": round(both["h2d"] + both["d2h"], 2),
             "note": f"pinned {n >> 20} MiB copies, {reps} per direction, torch copy_ on dedicated streams, "
-                    f"each direction timed by HIP events on its own stream, alone and with the other running"}
+                    f"each direction timed by HIP events on its own stream, alone and with the other running "
+                    f"(best of 3 stream pairs)"}
 
 
 def link_bound_GiBps(link, up, down):
