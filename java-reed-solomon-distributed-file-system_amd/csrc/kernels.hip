@@ -1090,21 +1090,66 @@ __global__ void copy_tail_kernel(uint8_t *dst, const uint8_t *src, uint64_t n) {
 // ---------------------------------------------------------------------------
 // Host-side dispatch.
 // ---------------------------------------------------------------------------
+#ifndef RSAMD_VEC_LDS_PAD
+#define RSAMD_VEC_LDS_PAD -1  // A/B: dynamic LDS bytes per wave of gf_vec_kernel (-1: the table below)
+#endif
+// Occupancy cap of the vector kernels.  A one-wave workgroup that asks for
+// `pad` bytes of (unused) dynamic LDS leaves 160 KiB / pad waves per CU, and
+// fewer waves in flight stream HBM better: at the VGPR limit (32 waves per
+// CU) the 4+2 encode reads 0.836 of peak, at 12 waves 0.860.  Measured per
+// shape on one pool, pads alternated (tools/occ_sweep.py,
+// profiles/r3/occ_sweep_r3zs.txt; fractions of 8 TB/s, pad in bytes):
+//   shape                        0      10240  11520  12544  13568  14848  16384  20480
+//   4+2 granule encode         0.836  0.847  0.852  0.861  0.860  0.855  0.828  0.777
+//   4+2 granule decode {0}     0.796  0.797  0.813  0.837  0.837  0.830  0.803  0.754
+//   4+2 granule decode {0,5}   0.800  0.813  0.814  0.820  0.822  0.819  0.804  0.762
+//   4+2 granule verify         0.887  0.933  0.950  0.897  0.844  0.788  0.731  0.669
+//   4+2 packed encode          0.801  0.828  0.852  0.860  0.857  0.844  0.811  0.762
+//   4+2 x 4 KiB packed encode  0.760  0.791  0.795  0.807  0.813  0.814  0.801  0.759
+//   10+4 granule encode        0.801  0.814  0.812  0.803  0.792  0.778  0.758  0.733
+//   10+4 granule decode {0,1}  0.795  0.794  0.793  0.798  0.818  0.843  0.845  0.821
+//   10+4 granule decode {0}    0.747  0.765  0.773  0.780  0.784  0.789  0.796  0.802
+//   10+4 granule verify        0.827  0.807  0.800  0.768  0.753  0.729  0.684  0.632
+//   10+4 packed encode         0.737  0.758  0.761  0.764  0.765  0.754  0.744  0.713
+// The table below takes each column's best per (k, outputs, verify).
+size_t vec_lds_pad(int k, int m, bool verify) {
+    if (const char *e = tuning_env("RSAMD_VEC_LDS_PAD")) return size_t(std::atol(e));  // per launch: sweeps
+    if (RSAMD_VEC_LDS_PAD >= 0) return size_t(RSAMD_VEC_LDS_PAD);
+    if (k == 4) return verify ? 11520 : 13568;
+    if (k == 10) {
+        if (verify) return 0;
+        return m >= 4 ? 10240 : m == 3 ? 13568 : m == 2 ? 16384 : 20480;
+    }
+    return 0;
+}
+
+// The same cap for the per-stripe-pattern kernels (gf_masked_kernel), granule
+// batches with a random pattern per stripe (tools/occ_sweep2.py --family
+// masked, profiles/r3/occ_sweep2_r3zt.txt): config[4] 0.797 uncapped, 0.824
+// at 12544 B; 4+2 x 1 MiB 0.80 -> 0.829 at 12544; 10+4 x 4 MiB with 4 erasures
+// 0.76-0.79 -> 0.80-0.806 at 10240.  (The copy kernel, two streams per wave,
+// is best uncapped: 0.851, and 0.78 at 10240.)
+size_t masked_lds_pad(int k, int ms) {
+    (void)ms;
+    return tuning_size("RSAMD_MASKED_LDS_PAD", k == 4 ? 12544 : k == 10 ? 10240 : 0);
+}
+
 template <int K, int M>
 hipError_t launch_vec_t(VecArgs a, Mode mode, hipStream_t s) {
+    const size_t lds = vec_lds_pad(K, M, mode == Mode::Verify);
     if (mode == Mode::Verify)
-        hipLaunchKernelGGL((gf_vec_kernel<K, M, true>), dim3(a.n_items), dim3(kWave), 0, s, a);
+        hipLaunchKernelGGL((gf_vec_kernel<K, M, true>), dim3(a.n_items), dim3(kWave), lds, s, a);
     else
-        hipLaunchKernelGGL((gf_vec_kernel<K, M, false>), dim3(a.n_items), dim3(kWave), 0, s, a);
+        hipLaunchKernelGGL((gf_vec_kernel<K, M, false>), dim3(a.n_items), dim3(kWave), lds, s, a);
     return hipGetLastError();
 }
 
 template <int M>
 hipError_t launch_vec_generic_t(VecArgs a, Mode mode, hipStream_t s) {
     if (mode == Mode::Verify)
-        hipLaunchKernelGGL((gf_vec_generic_kernel<M, true>), dim3(a.n_items), dim3(kWave), 0, s, a);
+        hipLaunchKernelGGL((gf_vec_generic_kernel<M, true>), dim3(a.n_items), dim3(kWave), vec_lds_pad(0, M, true), s, a);
     else
-        hipLaunchKernelGGL((gf_vec_generic_kernel<M, false>), dim3(a.n_items), dim3(kWave), 0, s, a);
+        hipLaunchKernelGGL((gf_vec_generic_kernel<M, false>), dim3(a.n_items), dim3(kWave), vec_lds_pad(0, M, false), s, a);
     return hipGetLastError();
 }
 
@@ -1216,18 +1261,18 @@ hipError_t launch_bytes(const Geometry &g, const DevPlan &p, size_t col0, size_t
 template <int K, int MS>
 hipError_t launch_masked_t(const MaskedArgs &a, hipStream_t s) {
     if (a.pat_on)
-        hipLaunchKernelGGL((gf_masked_kernel<K, MS, true>), dim3(a.n_items), dim3(kWave), 0, s, a);
+        hipLaunchKernelGGL((gf_masked_kernel<K, MS, true>), dim3(a.n_items), dim3(kWave), masked_lds_pad(K, MS), s, a);
     else
-        hipLaunchKernelGGL((gf_masked_kernel<K, MS, false>), dim3(a.n_items), dim3(kWave), 0, s, a);
+        hipLaunchKernelGGL((gf_masked_kernel<K, MS, false>), dim3(a.n_items), dim3(kWave), masked_lds_pad(K, MS), s, a);
     return hipGetLastError();
 }
 
 template <int MS>
 hipError_t launch_masked_generic_t(const MaskedArgs &a, hipStream_t s) {
     if (a.pat_on)
-        hipLaunchKernelGGL((gf_masked_generic_kernel<MS, true>), dim3(a.n_items), dim3(kWave), 0, s, a);
+        hipLaunchKernelGGL((gf_masked_generic_kernel<MS, true>), dim3(a.n_items), dim3(kWave), masked_lds_pad(0, MS), s, a);
     else
-        hipLaunchKernelGGL((gf_masked_generic_kernel<MS, false>), dim3(a.n_items), dim3(kWave), 0, s, a);
+        hipLaunchKernelGGL((gf_masked_generic_kernel<MS, false>), dim3(a.n_items), dim3(kWave), masked_lds_pad(0, MS), s, a);
     return hipGetLastError();
 }
 
@@ -1620,7 +1665,8 @@ hipError_t launch_copy(uint8_t *dst, const uint8_t *src, size_t n, hipStream_t s
         const uint64_t nvec = n / 16;
         for (uint64_t v0 = 0; v0 < nvec;) {  // one-shot grids of at most kMaxGridBlocks blocks
             const uint64_t nv = std::min<uint64_t>(nvec - v0, uint64_t(kMaxGridBlocks) * kWave);
-            hipLaunchKernelGGL(copy_kernel, dim3(unsigned((nv + kWave - 1) / kWave)), dim3(kWave), 0, s,
+            hipLaunchKernelGGL(copy_kernel, dim3(unsigned((nv + kWave - 1) / kWave)), dim3(kWave),
+                               tuning_size("RSAMD_COPY_LDS_PAD", 0), s,
                                dst + v0 * 16, src + v0 * 16, nv);
             v0 += nv;
         }

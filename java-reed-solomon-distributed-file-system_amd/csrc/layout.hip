@@ -592,13 +592,20 @@ uint32_t file_xcd_span(uint64_t n_blocks) {
     return on ? uint32_t(n_blocks / 8u) : 0u;
 }
 
+// Occupancy cap of the untiled file kernels (one-wave workgroups): dynamic
+// LDS bytes per wave, 160 KiB / pad waves per CU (as kernels.hip vec_lds_pad).
+// The 4 GiB file encode reads 0.775 uncapped and 0.79 at 10240-11520 B
+// (tools/occ_sweep2.py --family file, profiles/r3/occ_sweep2_r3zt.txt); the
+// tiled decode is best as it is (extra LDS per workgroup: +0 .. -3.5 points).
+size_t file_lds_pad(bool encode) { return tuning_size("RSAMD_FILE_LDS_PAD", encode ? 11520 : 0); }
+
 template <int K, int M>
 hipError_t launch_enc_t(const FileArgs &a, hipStream_t s) {
     const dim3 grid((a.nvec + kWave - 1) / kWave);
     switch (file_io_mode()) {
-    case IO_NT8: hipLaunchKernelGGL((file_encode_kernel<K, M, IO_NT8>), grid, dim3(kWave), 0, s, a); break;
-    case IO_PLAIN8: hipLaunchKernelGGL((file_encode_kernel<K, M, IO_PLAIN8>), grid, dim3(kWave), 0, s, a); break;
-    default: hipLaunchKernelGGL((file_encode_kernel<K, M, IO_PAIR16>), grid, dim3(kWave), 0, s, a); break;
+    case IO_NT8: hipLaunchKernelGGL((file_encode_kernel<K, M, IO_NT8>), grid, dim3(kWave), file_lds_pad(true), s, a); break;
+    case IO_PLAIN8: hipLaunchKernelGGL((file_encode_kernel<K, M, IO_PLAIN8>), grid, dim3(kWave), file_lds_pad(true), s, a); break;
+    default: hipLaunchKernelGGL((file_encode_kernel<K, M, IO_PAIR16>), grid, dim3(kWave), file_lds_pad(true), s, a); break;
     }
     return hipGetLastError();
 }
@@ -607,9 +614,9 @@ template <int K, int E>
 hipError_t launch_dec_t(const FileArgs &a, hipStream_t s) {
     const dim3 grid((a.nvec + kWave - 1) / kWave);
     switch (file_io_mode()) {
-    case IO_NT8: hipLaunchKernelGGL((file_decode_kernel<K, E, IO_NT8>), grid, dim3(kWave), 0, s, a); break;
-    case IO_PLAIN8: hipLaunchKernelGGL((file_decode_kernel<K, E, IO_PLAIN8>), grid, dim3(kWave), 0, s, a); break;
-    default: hipLaunchKernelGGL((file_decode_kernel<K, E, IO_PAIR16>), grid, dim3(kWave), 0, s, a); break;
+    case IO_NT8: hipLaunchKernelGGL((file_decode_kernel<K, E, IO_NT8>), grid, dim3(kWave), file_lds_pad(false), s, a); break;
+    case IO_PLAIN8: hipLaunchKernelGGL((file_decode_kernel<K, E, IO_PLAIN8>), grid, dim3(kWave), file_lds_pad(false), s, a); break;
+    default: hipLaunchKernelGGL((file_decode_kernel<K, E, IO_PAIR16>), grid, dim3(kWave), file_lds_pad(false), s, a); break;
     }
     return hipGetLastError();
 }
@@ -664,7 +671,7 @@ DecTile dec_tile() {
 
 template <int K, int E>
 hipError_t launch_tiled_t(const TileArgs &a, uint64_t tiles, hipStream_t s) {
-    const size_t lds = size_t(K) * a.rows * a.block;
+    const size_t lds = size_t(K) * a.rows * a.block + tuning_size("RSAMD_FILE_TILE_LDS_PAD", 0);
     const DecTile d = dec_tile();
     const dim3 grid{unsigned(tiles)}, blk{unsigned(d.threads)};
 #define RSAMD_DEC_TILE(T, SL)                                                                   \

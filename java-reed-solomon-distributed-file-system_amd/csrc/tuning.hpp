@@ -8,6 +8,7 @@
 // is how the A/B scripts under tools/ compare choices on one box.
 #pragma once
 
+#include <cstddef>
 #include <cstdlib>
 
 #ifndef RSAMD_TUNING_ENV
@@ -24,6 +25,13 @@ inline const char *tuning_env(const char *name) {
     (void)name;
     return nullptr;
 #endif
+}
+
+// A size knob: the variable's value in a TUNING=1 build (read at each call,
+// so a sweep can change it between launches), else `dflt`.
+inline size_t tuning_size(const char *name, size_t dflt) {
+    const char *e = tuning_env(name);
+    return e ? size_t(std::strtoull(e, nullptr, 10)) : dflt;
 }
 
 }  // namespace rsamd

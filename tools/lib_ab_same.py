@@ -29,6 +29,18 @@ SINGLE = [("4p2g_enc", 4, 2, 1 << 20, 4096, None, 64 << 10),
           ("10p4g_dec012", 10, 4, 4 << 20, 128, (0, 1, 2), 32 << 10),
           ("10p4_dec0", 10, 4, 4 << 20, 128, (0,), 0),
           ("10p4_dec01", 10, 4, 4 << 20, 128, (0, 1), 0)]
+# --set occ: the shapes of an occupancy sweep (granule and packed, encode and decodes)
+OCC = [("4p2g_enc", 4, 2, 1 << 20, 4096, None, 64 << 10),
+       ("4p2g_dec0", 4, 2, 1 << 20, 4096, (0,), 64 << 10),
+       ("4p2g_dec01", 4, 2, 1 << 20, 4096, (0, 1), 64 << 10),
+       ("4p2g_dec05", 4, 2, 1 << 20, 4096, (0, 5), 64 << 10),
+       ("4p2_enc", 4, 2, 1 << 20, 4096, None, 0),
+       ("4p2g4k_enc", 4, 2, 4096, 1 << 20, None, 64 << 10),
+       ("10p4g_enc", 10, 4, 4 << 20, 128, None, 32 << 10),
+       ("10p4g_dec0123", 10, 4, 4 << 20, 128, (0, 1, 2, 3), 32 << 10),
+       ("10p4g_dec0", 10, 4, 4 << 20, 128, (0,), 32 << 10),
+       ("10p4_enc", 10, 4, 4 << 20, 128, None, 0),
+       ("10p4_dec0123", 10, 4, 4 << 20, 128, (0, 1, 2, 3), 0)]
 
 
 def bind(path):
@@ -57,6 +69,8 @@ def main():
         i = args.index("--set")
         if args[i + 1] == "single":
             shapes = SINGLE
+        elif args[i + 1] == "occ":
+            shapes = OCC
         del args[i:i + 2]
     import torch
     libs = [bind(p) for p in args]
