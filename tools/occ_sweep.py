@@ -33,7 +33,16 @@ SHAPES = [("4p2g_enc", 4, 2, 1 << 20, 4096, None, 64 << 10),
           ("10p4g_verify", 10, 4, 4 << 20, 128, "verify", 32 << 10),
           ("10p4_enc", 10, 4, 4 << 20, 128, None, 0),
           ("10p4_dec0123", 10, 4, 4 << 20, 128, (0, 1, 2, 3), 0),
-          ("10p4x1024_enc", 10, 4, 4 << 20, 1024, None, 0)]
+          ("10p4x1024_enc", 10, 4, 4 << 20, 1024, None, 0),
+          # other granules, for the layout x occupancy cross-check
+          ("4p2g32_enc", 4, 2, 1 << 20, 4096, None, 32 << 10),
+          ("4p2g128_enc", 4, 2, 1 << 20, 4096, None, 128 << 10),
+          ("4p2g32_dec0", 4, 2, 1 << 20, 4096, (0,), 32 << 10),
+          ("4p2g128_dec0", 4, 2, 1 << 20, 4096, (0,), 128 << 10),
+          ("4p2g128_dec05", 4, 2, 1 << 20, 4096, (0, 5), 128 << 10),
+          ("10p4g16_enc", 10, 4, 4 << 20, 128, None, 16 << 10),
+          ("10p4g64_enc", 10, 4, 4 << 20, 128, None, 64 << 10),
+          ("10p4g64_dec0123", 10, 4, 4 << 20, 128, (0, 1, 2, 3), 64 << 10)]
 
 
 def main():

@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--shift", type=int, default=0, help="KiB added to the batch's base address")
     ap.add_argument("--no-mix", action="store_true")
     ap.add_argument("--lib", default=None, help="a variant librsamd.so (A/B runs)")
+    ap.add_argument("--granule", type=int, default=0, help="granule KiB (default: rs_granule_recommended)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -62,7 +63,7 @@ def main():
         lay = rdev.StripeLayout(B, S, stride, (k + m) * stride)
     else:
         S, B = (1 << 20, 4096) if a.config == "headline" else (4096, 1 << 20)
-        lay = rdev.GranuleLayout.make(B, k + m, S)
+        lay = rdev.GranuleLayout.make(B, k + m, S, a.granule << 10)
     pool = rdev.DeviceBuffer(lay.nbytes + (a.shift << 10), contiguous=True)
     base, st = pool.data_ptr() + (a.shift << 10), torch.cuda.current_stream()
     rdev.fill_synthetic(base, k, lay, 0x5EED, 0, st)
