@@ -1206,14 +1206,10 @@ struct BlockOrder {
 
 BlockOrder block_order(uint32_t chunks, uint32_t total_shards, uint64_t shard_stride, uint32_t n_items,
                        int nout = 0) {
-    static const int env_rot = [] {
-        const char *e = tuning_env("RSAMD_BLOCK_ROT");
-        return e ? std::atoi(e) : -1;
-    }();
-    static const int env_xcd = [] {
-        const char *e = tuning_env("RSAMD_BLOCK_XCD");
-        return e ? std::atoi(e) : -1;
-    }();
+    // read at every launch (TUNING builds only): sweeps change them between legs
+    const char *er = tuning_env("RSAMD_BLOCK_ROT"), *ex = tuning_env("RSAMD_BLOCK_XCD");
+    const int env_rot = er ? std::atoi(er) : -1;
+    const int env_xcd = ex ? std::atoi(ex) : -1;
     const bool half = chunks == 512 && shard_stride % (uint64_t(512) << 10) == 0;
     // Wide stripes (>= 14 shards of >= 1 MiB): rotation up to 256 stripes per
     // launch, the XCD remap beyond (10+4 x 4 MiB on contiguous pools: 128 and

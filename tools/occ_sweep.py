@@ -6,7 +6,8 @@ one-wave workgroup: 160 KiB / pad waves per CU).  Pads alternate within a
 repetition, so placement and clock drift are common to all of them.
 Prints one JSON line per (shape, repetition): fraction of 8 TB/s per pad.
   python tools/occ_sweep.py [--lib build/ab/tuning/librsamd.so] [--reps N]
-                            [--pads 0,10240,...] [--shapes name,...] [--env VAR]"""
+                            [--pads 0,10240,...] [--shapes name,...] [--env VAR]
+                            [--cross RSAMD_BLOCK_XCD=0,1 ...]"""
 import argparse
 import json
 import os
@@ -52,7 +53,15 @@ def main():
     ap.add_argument("--pads", default="0,10240,11520,12544,13568,14848,16384,20480,27136")
     ap.add_argument("--shapes", default="")
     ap.add_argument("--env", default="RSAMD_VEC_LDS_PAD")
+    ap.add_argument("--cross", action="append", default=[],
+                    help="VAR=v1,v2,...: an outer knob; 'unset' leaves VAR unset (repeatable: all combinations)")
     a = ap.parse_args()
+    import itertools
+    cross = []
+    for c in a.cross:
+        var, _, vals = c.partition("=")
+        cross.append([(var, v) for v in vals.split(",")])
+    combos = list(itertools.product(*cross)) if cross else [()]
     import ctypes as C
     import torch
     from lib_ab_same import bind
@@ -89,7 +98,12 @@ def main():
                 assert lib.rs_encode_batch_dev(h, pool, B, S, stride, stride * (k + m), sp) == 0
         for rep in range(a.reps):
             out = {"shape": name, "rep": rep}
-            for pad in pads:
+            for combo, pad in itertools.product(combos, pads):
+                for var, v in combo:
+                    if v == "unset":
+                        os.environ.pop(var, None)
+                    else:
+                        os.environ[var] = v
                 os.environ[a.env] = str(pad)
                 for _ in range(6):
                     call()
@@ -100,9 +114,12 @@ def main():
                     call()
                 e1.record(st)
                 torch.cuda.synchronize()
-                out[str(pad)] = round(alg / (e0.elapsed_time(e1) / 10 * 1e-3) / 8e12, 4)
+                key = "/".join([f"{var}={v}" for var, v in combo] + [str(pad)])
+                out[key] = round(alg / (e0.elapsed_time(e1) / 10 * 1e-3) / 8e12, 4)
             print(json.dumps(out), flush=True)
         os.environ.pop(a.env, None)
+        for c in cross:
+            os.environ.pop(c[0][0], None)
         torch.cuda.synchronize()
         assert int(flag.item()) == 0, name
         lib.rs_dev_free(pool)
