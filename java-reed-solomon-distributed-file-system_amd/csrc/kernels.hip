@@ -1204,8 +1204,16 @@ struct BlockOrder {
     uint32_t rot, xcd_span;
 };
 
+// With an occupancy cap (vec_lds_pad / masked_lds_pad > 0: `capped`) plain
+// order wins everywhere it was measured (tools/occ_sweep.py --cross,
+// profiles/r3/occ_order_r3zy.txt; tools/pattern_sweep.py,
+// profiles/r3/order_caps_r3zz.txt): 4+2 granule encode 0.874 against 0.863
+// with the XCD remap, every 4+2 decode pattern 0.851-0.878 against
+// 0.817-0.861, per-stripe patterns 0.848-0.861 against 0.824-0.833; 4+2 packed
+// 0.869 against 0.863 rotated; 10+4 granule 0.810 against 0.808 and packed
+// x 128 0.774 against 0.770.  The table above stays for uncapped launches.
 BlockOrder block_order(uint32_t chunks, uint32_t total_shards, uint64_t shard_stride, uint32_t n_items,
-                       int nout = 0) {
+                       int nout = 0, bool capped = false) {
     // read at every launch (TUNING builds only): sweeps change them between legs
     const char *er = tuning_env("RSAMD_BLOCK_ROT"), *ex = tuning_env("RSAMD_BLOCK_XCD");
     const int env_rot = er ? std::atoi(er) : -1;
@@ -1228,6 +1236,10 @@ BlockOrder block_order(uint32_t chunks, uint32_t total_shards, uint64_t shard_st
     // 0.8444-0.8467 on every box and process.  nout is kept for such rules.
     (void)nout;
     const bool xcd = env_xcd >= 0 ? env_xcd != 0 : !rotate;
+    // (Not for packed wide stripes beyond 256: 10+4 x 4 MiB x 1024 keeps the
+    // XCD remap, 0.775 against 0.762 plain.)
+    const bool wide_many = total_shards >= 14 && chunks >= 1024 && stripes > 256;
+    if (capped && !wide_many && env_rot < 0 && env_xcd < 0) return BlockOrder{0u, 0u};
     return BlockOrder{chunks > 1 ? rot % chunks : 0u, xcd ? n_items / 8u : 0u};
 }
 
@@ -1545,7 +1557,8 @@ hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t 
         for (size_t t0 = 0; t0 < g.n_stripes; t0 += stripes_per_launch) {
             const size_t nst = std::min(stripes_per_launch, g.n_stripes - t0);
             const BlockOrder o = block_order(chunks, uint32_t(g.stripe_stride / std::max<size_t>(1, g.shard_stride)),
-                                             g.shard_stride, uint32_t(nst * chunks));
+                                             g.shard_stride, uint32_t(nst * chunks), 0,
+                                             masked_lds_pad(p.nin, p.mslots) > 0);
             MaskedArgs a{base + t0 * g.stripe_stride, p.records, p.rec_stride, p.plan_ids + (pb ? 0 : t0),
                          g.stripe_stride, g.shard_stride, nvec, chunks, uint32_t(nst * chunks), o.rot, o.xcd_span,
                          make_fastdiv(chunks), uint32_t(l.in_idx), uint32_t(l.out_idx), uint32_t(l.tabs), p.nin, p.mask_table,
@@ -1598,7 +1611,8 @@ hipError_t launch_gf_tables(const Geometry &g, const DevPlan &p, Mode mode, int 
         for (size_t t0 = 0; t0 < g.n_stripes; t0 += stripes_per_launch) {
             const size_t nst = std::min(stripes_per_launch, g.n_stripes - t0);
             const BlockOrder o = block_order(chunks, uint32_t(g.stripe_stride / std::max<size_t>(1, g.shard_stride)),
-                                             g.shard_stride, uint32_t(nst * chunks), mode == Mode::Code ? p.nout : 0);
+                                             g.shard_stride, uint32_t(nst * chunks), mode == Mode::Code ? p.nout : 0,
+                                             vec_lds_pad(p.nin, p.nout, mode == Mode::Verify) > 0);
             VecArgs a{base + t0 * g.stripe_stride, p.tabs, p.in_idx, p.out_idx, g.stripe_stride, g.shard_stride,
                       nvec, chunks, uint32_t(nst * chunks), o.rot, o.xcd_span, make_fastdiv(chunks), p.nin,
                       mismatch};
