@@ -1416,7 +1416,8 @@ hipError_t launch_group8(const Geometry &g, GroupArgs a, int ms, hipStream_t s) 
         const size_t nst = std::min<size_t>(kMaxGridBlocks, g.n_stripes - t0);
         a.base = g.base + t0 * g.stripe_stride;
         a.n_items = uint32_t(nst);
-        a.xcd_span = uint32_t(nst / 8);
+        const char *gx = tuning_env("RSAMD_GROUP_XCD");  // A/B (TUNING builds): 0 = plain order
+        a.xcd_span = gx && gx[0] == '0' ? 0u : uint32_t(nst / 8);
         a.plan_ids = ids0 ? ids0 + t0 : nullptr;
         a.has_prev = t0 > 0;
         a.has_next_last = t0 + nst < g.n_stripes;

@@ -585,10 +585,8 @@ int file_io_mode() {
 // XCD span for a file-kernel grid of n blocks (RSAMD_FILE_XCD=0 turns the
 // remap off for A/B runs).
 uint32_t file_xcd_span(uint64_t n_blocks) {
-    static const bool on = [] {
-        const char *e = tuning_env("RSAMD_FILE_XCD");
-        return !(e && e[0] == '0');
-    }();
+    const char *e = tuning_env("RSAMD_FILE_XCD");  // per launch (TUNING builds): sweeps
+    const bool on = !(e && e[0] == '0');
     return on ? uint32_t(n_blocks / 8u) : 0u;
 }
 

@@ -8,6 +8,9 @@ process changes it between legs (pads alternate within a repetition).
   --family file: the fused file kernels (RSAMD_FILE_LDS_PAD for the untiled
       encode, RSAMD_FILE_TILE_LDS_PAD extra bytes per tiled-decode workgroup)
   --family copy: the copy kernel (RSAMD_COPY_LDS_PAD), 2 x 8 GiB
+  --family group: the master's chunk groups, XCD remap (1) or plain order (0)
+      of the line-owner kernel (RSAMD_GROUP_XCD); the file family also
+      sweeps RSAMD_FILE_XCD
 Prints one JSON line per (leg, repetition): fraction of 8 TB/s per pad.
   python tools/occ_sweep2.py --family masked|file|copy [--pads ...] [--reps N]"""
 import argparse
@@ -42,7 +45,7 @@ def sweep(torch, st, name, env, pads, fn, alg, reps):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--family", required=True, choices=["masked", "file", "copy"])
+    ap.add_argument("--family", required=True, choices=["masked", "file", "copy", "group"])
     ap.add_argument("--lib", default=os.path.join(ROOT, "build/ab/tuning/librsamd.so"))
     ap.add_argument("--pads", default="0,10240,11520,12544,13568,14848,16384,20480")
     ap.add_argument("--reps", type=int, default=2)
@@ -102,8 +105,34 @@ def main():
         sweep(torch, st, "file_decode_0_5_4GiB_tiled", "RSAMD_FILE_TILE_LDS_PAD", tile_pads,
               lambda: decode_file_dev(rs, sh.data_ptr(), S, stride, present, g.data_ptr(), n, stream=st),
               4 * S + n, a.reps)
+        sweep(torch, st, "file_encode_4GiB_order", "RSAMD_FILE_XCD", [1, 0],
+              lambda: encode_file_dev(rs, f.data_ptr(), n, sh.data_ptr(), stride, stream=st), n + 6 * S, a.reps)
+        sweep(torch, st, "file_decode_0_5_4GiB_order", "RSAMD_FILE_XCD", [1, 0],
+              lambda: decode_file_dev(rs, sh.data_ptr(), S, stride, present, g.data_ptr(), n, stream=st),
+              4 * S + n, a.reps)
         torch.cuda.synchronize()
         assert torch.equal(f, g)
+    elif a.family == "group":
+        # the master's chunk groups (line-owner kernel): the knob is RSAMD_GROUP_XCD (0 plain, 1 remap)
+        from rsamd.device import StripeLayout
+        k, m, S, B = 4, 2, 1000, 4 << 20
+        rs = rsamd.ReedSolomon.create(k, m)
+        lay = StripeLayout(B, S, S, 6 * S)
+        buf = torch.empty(lay.nbytes, dtype=torch.uint8, device="cuda:0")
+        rdev.fill_synthetic(buf.data_ptr(), k, lay, 0x5EED, 0, st)
+        rdev.encode(rs, buf.data_ptr(), lay, st)
+        sweep(torch, st, "cg_encode", "RSAMD_GROUP_XCD", [1, 0], lambda: rdev.encode(rs, buf.data_ptr(), lay, st),
+              6 * S * B, a.reps)
+        pres01 = [False, False, True, True, True, True]
+        sweep(torch, st, "cg_decode01", "RSAMD_GROUP_XCD", [1, 0],
+              lambda: rdev.decode(rs, buf.data_ptr(), pres01, lay, st), 6 * S * B, a.reps)
+        pats = np.array([[i not in mi for i in range(6)] for e in range(3)
+                         for mi in itertools.combinations(range(6), e)], dtype=bool)
+        pres = pats[np.random.default_rng(0).integers(0, len(pats), B)]
+        alg = (k * int((~pres).any(axis=1).sum()) + int((~pres).sum())) * S
+        bits = torch.from_numpy(rdev.presence_bits(pres).view(np.int32)).to("cuda:0")
+        sweep(torch, st, "cg_masked_bits", "RSAMD_GROUP_XCD", [1, 0],
+              lambda: rdev.decode_masked_bits(rs, buf.data_ptr(), bits.data_ptr(), lay, 0, st), alg, a.reps)
     else:
         n = 8 << 30
         buf = torch.empty(2 * n, dtype=torch.uint8, device="cuda:0")
