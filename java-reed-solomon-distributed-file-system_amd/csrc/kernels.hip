@@ -1115,11 +1115,14 @@ __global__ void copy_tail_kernel(uint8_t *dst, const uint8_t *src, uint64_t n) {
 //   10+4 granule decode {0}    0.747  0.765  0.773  0.780  0.784  0.789  0.796  0.802
 //   10+4 granule verify        0.827  0.807  0.800  0.768  0.753  0.729  0.684  0.632
 //   10+4 packed encode         0.737  0.758  0.761  0.764  0.765  0.754  0.744  0.713
-// The table below takes each column's best per (k, outputs, verify).
+// The table below takes each column's best per (k, outputs, verify), checked
+// again in plain block order (block_order: capped launches), which moved the
+// 4+2 decodes' best to 12544 ({0} 0.877 against 0.872 at 13568, encode a tie;
+// profiles/r3/occ_plain_r3zz3.txt, occ_plain2_r3zz4.txt).
 size_t vec_lds_pad(int k, int m, bool verify) {
     if (const char *e = tuning_env("RSAMD_VEC_LDS_PAD")) return size_t(std::atol(e));  // per launch: sweeps
     if (RSAMD_VEC_LDS_PAD >= 0) return size_t(RSAMD_VEC_LDS_PAD);
-    if (k == 4) return verify ? 11520 : 13568;
+    if (k == 4) return verify ? 11520 : 12544;
     if (k == 10) {
         if (verify) return 0;
         return m >= 4 ? 10240 : m == 3 ? 13568 : m == 2 ? 16384 : 20480;
