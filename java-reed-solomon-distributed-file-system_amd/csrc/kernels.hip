@@ -1321,7 +1321,8 @@ hipError_t dispatch_masked(const MaskedArgs &a, int ms, hipStream_t s) {
 
 template <int K, int MS>
 hipError_t launch_masked8_t(const MaskedArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL((gf_masked8_kernel<K, MS>), dim3(a.n_items), dim3(kWave), 0, s, a);
+    hipLaunchKernelGGL((gf_masked8_kernel<K, MS>), dim3(a.n_items), dim3(kWave), tuning_size("RSAMD_MASKED8_LDS_PAD", 0),
+                       s, a);
     return hipGetLastError();
 }
 
@@ -1339,9 +1340,11 @@ hipError_t dispatch_masked8(const MaskedArgs &a, int ms, hipStream_t s) {
 template <int K, int M>
 hipError_t launch_vec8_t(const Vec8Args &a, Mode mode, hipStream_t s) {
     if (mode == Mode::Verify)
-        hipLaunchKernelGGL((gf_vec8_kernel<K, M, true>), dim3(a.v.n_items), dim3(kWave), 0, s, a);
+        hipLaunchKernelGGL((gf_vec8_kernel<K, M, true>), dim3(a.v.n_items), dim3(kWave), tuning_size("RSAMD_VEC8_LDS_PAD", 0),
+                           s, a);
     else
-        hipLaunchKernelGGL((gf_vec8_kernel<K, M, false>), dim3(a.v.n_items), dim3(kWave), 0, s, a);
+        hipLaunchKernelGGL((gf_vec8_kernel<K, M, false>), dim3(a.v.n_items), dim3(kWave), tuning_size("RSAMD_VEC8_LDS_PAD", 0),
+                           s, a);
     return hipGetLastError();
 }
 

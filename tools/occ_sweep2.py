@@ -45,7 +45,7 @@ def sweep(torch, st, name, env, pads, fn, alg, reps):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--family", required=True, choices=["masked", "file", "copy", "group"])
+    ap.add_argument("--family", required=True, choices=["masked", "file", "copy", "group", "slots"])
     ap.add_argument("--lib", default=os.path.join(ROOT, "build/ab/tuning/librsamd.so"))
     ap.add_argument("--pads", default="0,10240,11520,12544,13568,14848,16384,20480")
     ap.add_argument("--reps", type=int, default=2)
@@ -112,6 +112,25 @@ def main():
               4 * S + n, a.reps)
         torch.cuda.synchronize()
         assert torch.equal(f, g)
+    elif a.family == "slots":
+        # the master's chunk groups in 1 KiB slots (shard stride 1024, 1000-B shards: the
+        # 8-byte kernels gf_vec8_kernel / gf_masked8_kernel)
+        from rsamd.device import StripeLayout
+        k, m, S, B = 4, 2, 1000, 4 << 20
+        rs = rsamd.ReedSolomon.create(k, m)
+        lay = StripeLayout(B, S, 1024, 6 * 1024)
+        buf = torch.empty(lay.nbytes, dtype=torch.uint8, device="cuda:0")
+        rdev.fill_synthetic(buf.data_ptr(), k, lay, 0x5EED, 0, st)
+        rdev.encode(rs, buf.data_ptr(), lay, st)
+        sweep(torch, st, "slots_encode", "RSAMD_VEC8_LDS_PAD", pads, lambda: rdev.encode(rs, buf.data_ptr(), lay, st),
+              6 * S * B, a.reps)
+        pats = np.array([[i not in mi for i in range(6)] for e in range(3)
+                         for mi in itertools.combinations(range(6), e)], dtype=bool)
+        pres = pats[np.random.default_rng(0).integers(0, len(pats), B)]
+        alg = (k * int((~pres).any(axis=1).sum()) + int((~pres).sum())) * S
+        bits = torch.from_numpy(rdev.presence_bits(pres).view(np.int32)).to("cuda:0")
+        sweep(torch, st, "slots_masked_bits", "RSAMD_MASKED8_LDS_PAD", pads,
+              lambda: rdev.decode_masked_bits(rs, buf.data_ptr(), bits.data_ptr(), lay, 0, st), alg, a.reps)
     elif a.family == "group":
         # the master's chunk groups (line-owner kernel): the knob is RSAMD_GROUP_XCD (0 plain, 1 remap)
         from rsamd.device import StripeLayout
