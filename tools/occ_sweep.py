@@ -30,6 +30,7 @@ SHAPES = [("4p2g_enc", 4, 2, 1 << 20, 4096, None, 64 << 10),
           ("10p4g_enc", 10, 4, 4 << 20, 128, None, 32 << 10),
           ("10p4g_dec0123", 10, 4, 4 << 20, 128, (0, 1, 2, 3), 32 << 10),
           ("10p4g_dec01", 10, 4, 4 << 20, 128, (0, 1), 32 << 10),
+          ("10p4g_dec012", 10, 4, 4 << 20, 128, (0, 1, 2), 32 << 10),
           ("10p4g_dec0", 10, 4, 4 << 20, 128, (0,), 32 << 10),
           ("10p4g_verify", 10, 4, 4 << 20, 128, "verify", 32 << 10),
           ("10p4_enc", 10, 4, 4 << 20, 128, None, 0),
