@@ -689,7 +689,7 @@ hipError_t launch_tiled_t(const TileArgs &a, uint64_t tiles, hipStream_t s) {
 
 template <int K, int M>
 hipError_t launch_enc_tiled_t(const EncTileArgs &a, uint64_t tiles, hipStream_t s) {
-    const size_t lds = size_t(K) * a.rows * a.block;
+    const size_t lds = size_t(K) * a.rows * a.block + tuning_size("RSAMD_FILE_TILE_LDS_PAD", 0);
     hipLaunchKernelGGL((file_encode_tiled_kernel<K, M>), dim3(unsigned(tiles)), dim3(kTileThreads), lds, s, a);
     return hipGetLastError();
 }

@@ -110,6 +110,11 @@ def main():
         sweep(torch, st, "file_decode_0_5_4GiB_order", "RSAMD_FILE_XCD", [1, 0],
               lambda: decode_file_dev(rs, sh.data_ptr(), S, stride, present, g.data_ptr(), n, stream=st),
               4 * S + n, a.reps)
+        # the tiled encode (RSAMD_FILE_ENCODE=1) at extra LDS per workgroup, against the default
+        os.environ["RSAMD_FILE_ENCODE"] = "1"
+        sweep(torch, st, "file_encode_4GiB_tiled", "RSAMD_FILE_TILE_LDS_PAD", tile_pads,
+              lambda: encode_file_dev(rs, f.data_ptr(), n, sh.data_ptr(), stride, stream=st), n + 6 * S, a.reps)
+        os.environ.pop("RSAMD_FILE_ENCODE")
         torch.cuda.synchronize()
         assert torch.equal(f, g)
     elif a.family == "slots":
