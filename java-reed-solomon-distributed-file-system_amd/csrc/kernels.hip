@@ -1397,7 +1397,8 @@ bool group8_enabled() {
 size_t group8_lds(size_t len, int nin, int ms, bool masked) {
     const size_t slot = (len + 256 + 15) / 16 * 16;
     const bool wide = RSAMD_GROUP_LDS_MODE == 2 || (RSAMD_GROUP_LDS_MODE == 0 && !masked);
-    return (wide ? size_t(nin + ms) : std::max(size_t(nin), size_t(ms))) * slot + RSAMD_GROUP_LDS_PAD;
+    return (wide ? size_t(nin + ms) : std::max(size_t(nin), size_t(ms))) * slot +
+           tuning_size("RSAMD_GROUP_LDS_PAD_ENV", RSAMD_GROUP_LDS_PAD);  // per launch in TUNING builds
 }
 
 // The line-owner kernel takes k = 4 codes on stripes of back-to-back shards

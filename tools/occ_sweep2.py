@@ -147,6 +147,11 @@ def main():
         rdev.encode(rs, buf.data_ptr(), lay, st)
         sweep(torch, st, "cg_encode", "RSAMD_GROUP_XCD", [1, 0], lambda: rdev.encode(rs, buf.data_ptr(), lay, st),
               6 * S * B, a.reps)
+        for xcd in ("1", "0"):  # extra LDS per wave (fewer waves per CU) in either order
+            os.environ["RSAMD_GROUP_XCD"] = xcd
+            sweep(torch, st, f"cg_encode_xcd{xcd}", "RSAMD_GROUP_LDS_PAD_ENV", [0, 1280, 2560, 5120, 8192],
+                  lambda: rdev.encode(rs, buf.data_ptr(), lay, st), 6 * S * B, a.reps)
+        os.environ.pop("RSAMD_GROUP_XCD")
         pres01 = [False, False, True, True, True, True]
         sweep(torch, st, "cg_decode01", "RSAMD_GROUP_XCD", [1, 0],
               lambda: rdev.decode(rs, buf.data_ptr(), pres01, lay, st), 6 * S * B, a.reps)
@@ -157,6 +162,11 @@ def main():
         bits = torch.from_numpy(rdev.presence_bits(pres).view(np.int32)).to("cuda:0")
         sweep(torch, st, "cg_masked_bits", "RSAMD_GROUP_XCD", [1, 0],
               lambda: rdev.decode_masked_bits(rs, buf.data_ptr(), bits.data_ptr(), lay, 0, st), alg, a.reps)
+        for xcd in ("1", "0"):
+            os.environ["RSAMD_GROUP_XCD"] = xcd
+            sweep(torch, st, f"cg_masked_bits_xcd{xcd}", "RSAMD_GROUP_LDS_PAD_ENV", [0, 1280, 2560, 5120, 8192],
+                  lambda: rdev.decode_masked_bits(rs, buf.data_ptr(), bits.data_ptr(), lay, 0, st), alg, a.reps)
+        os.environ.pop("RSAMD_GROUP_XCD")
     else:
         n = 8 << 30
         buf = torch.empty(2 * n, dtype=torch.uint8, device="cuda:0")
