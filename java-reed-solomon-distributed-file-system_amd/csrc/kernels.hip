@@ -100,7 +100,14 @@ struct ByteArgs {
     int *mismatch;
 };
 
+#ifndef RSAMD_LOAD_NT
+#define RSAMD_LOAD_NT 1  // A/B builds: 0 = plain loads
+#endif
+#ifndef RSAMD_STORE_NT
+#define RSAMD_STORE_NT 1  // A/B builds: 0 = plain stores
+#endif
 __device__ __forceinline__ u32x4 load_stream(const uint8_t *p) {
+    if (!RSAMD_LOAD_NT) return *reinterpret_cast<const u32x4 *>(p);
     return __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
 }
 
@@ -114,6 +121,8 @@ __device__ __forceinline__ u32x4 load_stream(const uint8_t *p) {
 __device__ __forceinline__ void store_stream(uint8_t *p, const u32x4 &v) {
     if (RSAMD_STORE_SC1)
         asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+    else if (!RSAMD_STORE_NT)
+        *reinterpret_cast<u32x4 *>(p) = v;
     else
         __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
 }
