@@ -36,6 +36,13 @@ SHAPES = [("4p2g_enc", 4, 2, 1 << 20, 4096, None, 64 << 10),
           ("10p4_enc", 10, 4, 4 << 20, 128, None, 0),
           ("10p4_dec0123", 10, 4, 4 << 20, 128, (0, 1, 2, 3), 0),
           ("10p4x1024_enc", 10, 4, 4 << 20, 1024, None, 0),
+          # other codes (runtime-k kernel), granule layout at rs_granule_recommended
+          ("17p3g_enc", 17, 3, 1 << 20, 512, None, 16 << 10),
+          ("17p3g_dec012", 17, 3, 1 << 20, 512, (0, 1, 2), 16 << 10),
+          ("8p4g_enc", 8, 4, 1 << 20, 1024, None, 32 << 10),
+          ("8p4g_dec0", 8, 4, 1 << 20, 1024, (0,), 32 << 10),
+          ("6p3g_enc", 6, 3, 1 << 20, 2048, None, 32 << 10),
+          ("6p3g_dec01", 6, 3, 1 << 20, 2048, (0, 1), 32 << 10),
           # other granules, for the layout x occupancy cross-check
           ("4p2g32_enc", 4, 2, 1 << 20, 4096, None, 32 << 10),
           ("4p2g128_enc", 4, 2, 1 << 20, 4096, None, 128 << 10),
