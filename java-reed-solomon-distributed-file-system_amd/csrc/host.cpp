@@ -329,7 +329,7 @@ bool HostRegistration::lock(const std::vector<std::pair<const uint8_t *, size_t>
             }
         }
         if ((next != reg.regs.end() && next->first < pe) ||
-            hipHostRegister(reinterpret_cast<void *>(ps), pe - ps, hipHostRegisterDefault) != hipSuccess) {
+            hipHostRegister(reinterpret_cast<void *>(ps), pe - ps, hipHostRegisterMapped) != hipSuccess) {
             (void)hipGetLastError();
             release_locked(reg, held_);
             return false;

@@ -1101,6 +1101,118 @@ __global__ void copy_tail_kernel(uint8_t *dst, const uint8_t *src, uint64_t n) {
 }
 
 // ---------------------------------------------------------------------------
+// Direct kernel: shards in page-locked HOST memory, coded in place over the
+// link (the host-buffer entry points, capi.cpp run_direct).  Every input
+// vector is loaded across PCIe and every output vector stored back across it,
+// so the link carries H2D and D2H at once with no copy engine, no staging
+// buffer and no per-chunk hand-off.  tools/zc_probe.hip, profiles/r3/
+// zc_probe_r3s2b.txt: 4 host loads -> 2 host stores per column run at 50.3-50.6
+// GiB/s of data shards, 0.96 of the link bound, where the chunked DMA
+// pipeline reaches 0.86.  The link, not the GF arithmetic, is the bound, so
+// the kernel keeps a plain shape: a grid-stride loop over W-byte vectors
+// (W = 16, or 8 when the shards' addresses agree only modulo 8), one input
+// at a time, the pointers as wave-uniform kernel arguments.  Bytes before the
+// first aligned vector (head) and after the last (tail) go one per thread.
+// ---------------------------------------------------------------------------
+struct DirectArgs {
+    const uint8_t *in[kMaxDirectIn];
+    uint8_t *out[kMaxOut];
+    const uint32_t *tabs;  // [nin][M][5]
+    uint64_t head;         // bytes before the first W-aligned vector
+    uint64_t nvec;         // W-byte vectors after the head
+    uint64_t n;            // bytes per shard
+    int nin;
+    int *mismatch;
+};
+
+template <int W>
+struct DirectVec;
+template <>
+struct DirectVec<16> {
+    typedef u32x4 T;
+    static constexpr int kDwords = 4;
+};
+template <>
+struct DirectVec<8> {
+    typedef uint32_t T __attribute__((ext_vector_type(2)));
+    static constexpr int kDwords = 2;
+};
+
+template <int W, int M, bool VERIFY>
+__global__ void __launch_bounds__(kThreads) gf_direct_kernel(DirectArgs a) {
+    typedef typename DirectVec<W>::T V;
+    constexpr int D = DirectVec<W>::kDwords;
+    const uint64_t step = uint64_t(gridDim.x) * kThreads;
+    for (uint64_t v = uint64_t(blockIdx.x) * kThreads + threadIdx.x; v < a.nvec; v += step) {
+        if (VERIFY && mismatch_seen(a.mismatch)) return;
+        const uint64_t off = a.head + v * W;
+        uint32_t acc[M][D];
+#pragma unroll
+        for (int p = 0; p < M; ++p)
+#pragma unroll
+            for (int w = 0; w < D; ++w) acc[p][w] = 0;
+        for (int i = 0; i < a.nin; ++i) {
+            const V x = __builtin_nontemporal_load(reinterpret_cast<const V *>(a.in[i] + off));
+            uint32_t T[M][5];
+#pragma unroll
+            for (int p = 0; p < M; ++p)
+#pragma unroll
+                for (int j = 0; j < 5; ++j) T[p][j] = a.tabs[(i * M + p) * 5 + j];
+#pragma unroll
+            for (int w = 0; w < D; ++w) {
+                const Sel s = selectors(x[w]);
+#pragma unroll
+                for (int p = 0; p < M; ++p) {
+                    uint32_t t0, t1, t2;
+                    terms(T[p], s, t0, t1, t2);
+                    acc[p][w] = xor3(acc[p][w], t0, t1) ^ t2;
+                }
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < M; ++p) {
+            V y;
+#pragma unroll
+            for (int w = 0; w < D; ++w) y[w] = acc[p][w];
+            V *dst = reinterpret_cast<V *>(a.out[p] + off);
+            if (VERIFY) {
+                const V have = __builtin_nontemporal_load(dst);
+                bool same = true;
+#pragma unroll
+                for (int w = 0; w < D; ++w) same = same && have[w] == y[w];
+                if (!same) flag_mismatch(a.mismatch);
+            } else {
+                __builtin_nontemporal_store(y, dst);
+            }
+        }
+    }
+    // head and tail bytes (fewer than 2 W): the first threads of block 0
+    const uint64_t tail0 = a.head + a.nvec * W;
+    const uint64_t nbytes = a.head + (a.n - tail0);
+    if (blockIdx.x == 0 && threadIdx.x < nbytes) {
+        const uint64_t b = threadIdx.x < a.head ? threadIdx.x : tail0 + (threadIdx.x - a.head);
+        uint32_t acc[M] = {};
+        for (int i = 0; i < a.nin; ++i) {
+            const Sel s = selectors(a.in[i][b]);
+#pragma unroll
+            for (int p = 0; p < M; ++p) {
+                uint32_t t0, t1, t2;
+                terms(a.tabs + (i * M + p) * 5, s, t0, t1, t2);
+                acc[p] = xor3(acc[p], t0, t1) ^ t2;
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < M; ++p) {
+            if (VERIFY) {
+                if (a.out[p][b] != uint8_t(acc[p])) flag_mismatch(a.mismatch);
+            } else {
+                a.out[p][b] = uint8_t(acc[p]);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Host-side dispatch.
 // ---------------------------------------------------------------------------
 #ifndef RSAMD_VEC_LDS_PAD
@@ -1673,6 +1785,61 @@ hipError_t launch_vec8(const Geometry &g, const DevPlan &p, Mode mode, int *mism
 
 hipError_t launch_gf(const Geometry &g, const DevPlan &p, Mode mode, int *mismatch, hipStream_t s) {
     return launch_gf_tables(g, p, mode, mismatch, s);
+}
+
+namespace {
+template <int W, int M>
+void launch_direct_t(const DirectArgs &a, unsigned grid, Mode mode, hipStream_t s) {
+    if (mode == Mode::Verify)
+        hipLaunchKernelGGL((gf_direct_kernel<W, M, true>), dim3(grid), dim3(kThreads), 0, s, a);
+    else
+        hipLaunchKernelGGL((gf_direct_kernel<W, M, false>), dim3(grid), dim3(kThreads), 0, s, a);
+}
+template <int W>
+hipError_t dispatch_direct(const DirectArgs &a, int nout, unsigned grid, Mode mode, hipStream_t s) {
+    switch (nout) {
+    case 1: launch_direct_t<W, 1>(a, grid, mode, s); break;
+    case 2: launch_direct_t<W, 2>(a, grid, mode, s); break;
+    case 3: launch_direct_t<W, 3>(a, grid, mode, s); break;
+    case 4: launch_direct_t<W, 4>(a, grid, mode, s); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+}  // namespace
+
+// Blocks of the direct kernel: 512 x 256 threads keep ~2 MiB of loads in
+// flight, far more than the link's bandwidth-delay product; the probe read
+// the same rate from 256 to 4096 blocks (zc_probe_r3s2b.txt).
+constexpr unsigned kDirectBlocks = 512;
+
+hipError_t launch_gf_direct(const DirectPlan &p, size_t n, Mode mode, int *mismatch, hipStream_t s) {
+    if (p.nin < 1 || p.nin > kMaxDirectIn || p.nout < 1 || p.nout > kMaxOut) return hipErrorInvalidValue;
+    if (n == 0) return hipSuccess;
+    // The widest vector every shard's address agrees on (same residue).
+    int W = 16;
+    for (int wide : {16, 8}) {
+        W = wide;
+        const uintptr_t r = reinterpret_cast<uintptr_t>(p.in[0]) % wide;
+        bool same = true;
+        for (int i = 0; i < p.nin; ++i) same = same && reinterpret_cast<uintptr_t>(p.in[i]) % wide == r;
+        for (int q = 0; q < p.nout; ++q) same = same && reinterpret_cast<uintptr_t>(p.out[q]) % wide == r;
+        if (same) break;
+        W = 0;
+    }
+    if (W == 0) return hipErrorInvalidValue;  // the caller keeps the staged pipeline
+    DirectArgs a{};
+    for (int i = 0; i < p.nin; ++i) a.in[i] = p.in[i];
+    for (int q = 0; q < p.nout; ++q) a.out[q] = p.out[q];
+    a.tabs = p.tabs;
+    a.head = std::min<uint64_t>(n, (W - reinterpret_cast<uintptr_t>(p.in[0]) % W) % W);
+    a.nvec = (n - a.head) / W;
+    a.n = n;
+    a.nin = p.nin;
+    a.mismatch = mismatch;
+    const uint64_t blocks = tuning_size("RSAMD_DIRECT_BLOCKS", kDirectBlocks);  // per call in TUNING builds
+    const unsigned grid = unsigned(std::max<uint64_t>(1, std::min<uint64_t>(blocks, (a.nvec + kThreads - 1) / kThreads)));
+    return W == 16 ? dispatch_direct<16>(a, p.nout, grid, mode, s) : dispatch_direct<8>(a, p.nout, grid, mode, s);
 }
 
 hipError_t launch_fill_synthetic(uint8_t *base, int k, size_t n_stripes, size_t shard_len, size_t shard_stride,

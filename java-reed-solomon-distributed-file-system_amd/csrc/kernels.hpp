@@ -76,6 +76,20 @@ struct MaskedPlan {
 
 hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t s);
 
+// Shards in page-locked host memory, coded in place across the link by one
+// kernel (host-buffer calls, capi.cpp run_direct).  in / out are the device
+// addresses of each shard's first byte (hipHostGetDevicePointer); tabs are a
+// DevPlan's.  hipErrorInvalidValue when the plan is too wide or the shards'
+// addresses do not share an 8-byte residue (the caller then stages).
+constexpr int kMaxDirectIn = 32;
+struct DirectPlan {
+    const uint8_t *in[kMaxDirectIn] = {};
+    uint8_t *out[kMaxOut] = {};
+    const uint32_t *tabs = nullptr;
+    int nin = 0, nout = 0;
+};
+hipError_t launch_gf_direct(const DirectPlan &p, size_t n, Mode mode, int *mismatch, hipStream_t s);
+
 hipError_t launch_fill_synthetic(uint8_t *base, int k, size_t n_stripes, size_t shard_len,
                                  size_t shard_stride, size_t stripe_stride, uint64_t seed,
                                  uint64_t stripe0, hipStream_t s);
