@@ -58,6 +58,16 @@ bool direct_enabled() {
     return on;
 }
 
+// Device address of page-locked host memory (nullptr if it has none).
+uint8_t *host_dev_addr(const void *p) {
+    void *d = nullptr;
+    if (hipHostGetDevicePointer(&d, const_cast<void *>(p), 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return static_cast<uint8_t *>(d);
+}
+
 int run_direct(ThreadCtx *ctx, const std::vector<DevPlan> &plans, const std::vector<int> &in_slots,
                const std::vector<int> &out_slots, uint8_t *const *host, size_t offset, size_t count, Mode mode,
                bool *taken) {
@@ -65,13 +75,9 @@ int run_direct(ThreadCtx *ctx, const std::vector<DevPlan> &plans, const std::vec
     if (!direct_enabled() || plans.empty()) return RS_OK;
     std::vector<rsamd::DirectPlan> dp(plans.size());
     auto dev_addr = [&](int slot, uint8_t **out) {
-        void *d = nullptr;
-        if (hipHostGetDevicePointer(&d, host[slot], 0) != hipSuccess || !d) {
-            (void)hipGetLastError();
-            return false;
-        }
-        *out = static_cast<uint8_t *>(d) + offset;
-        return true;
+        uint8_t *d = host_dev_addr(host[slot]);
+        *out = d ? d + offset : nullptr;
+        return d != nullptr;
     };
     for (size_t g = 0; g < plans.size(); ++g) {
         const DevPlan &p = plans[g];
@@ -372,6 +378,72 @@ FileChunks file_chunks(int k, int total, size_t S, size_t block, bool pinned) {
     return f;
 }
 
+// Direct path of the host file calls (layout.hpp FileDirect): page-locked file
+// and shards coded in place across the link by one kernel, as run_direct does
+// for shards.  *taken = false, nothing enqueued, when the code or a pointer
+// does not fit the direct kernels (more than kMaxOut outputs, k above
+// kMaxDirectIn, no device address, not 8-byte aligned): the call is staged.
+int file_encode_direct(const Codec &c, const uint8_t *file, size_t file_len, size_t blk, uint8_t *const *shards,
+                       size_t S, ThreadCtx *ctx, bool *taken) {
+    *taken = false;
+    if (!direct_enabled() || c.m() > rsamd::kMaxOut || c.k() > rsamd::kMaxDirectIn) return RS_OK;
+    rsamd::FileDirect d;
+    d.k = c.k();
+    d.nout = c.m();
+    d.block = blk;
+    d.units = S / 8;
+    d.file_len = file_len;
+    d.file = host_dev_addr(file);
+    if (!d.file) return RS_OK;
+    for (int i = 0; i < c.total(); ++i)
+        if (!(d.out[i] = host_dev_addr(shards[i]))) return RS_OK;
+    if (c.m() > 0) {
+        std::vector<DevPlan> plans;
+        RS_HIP(c.encode_plan().device_plans(&plans));
+        d.tabs = plans[0].tabs;
+    }
+    if (!rsamd::file_direct_ok(d, true)) return RS_OK;
+    RS_HIP(rsamd::launch_file_encode_direct(d, ctx->stream));
+    *taken = true;
+    RS_HIP(hipStreamSynchronize(ctx->stream));
+    return RS_OK;
+}
+
+int file_decode_direct(const Codec &c, uint8_t *const *shards, const uint8_t *present, const std::vector<int> &surv,
+                       const std::vector<int> &missing, size_t blk, uint8_t *file_out, size_t file_size,
+                       size_t cols, ThreadCtx *ctx, bool *taken) {
+    *taken = false;
+    if (!direct_enabled() || missing.size() > size_t(rsamd::kMaxOut) || c.k() > rsamd::kMaxDirectIn) return RS_OK;
+    rsamd::FileDirect d;
+    d.k = c.k();
+    d.nout = int(missing.size());
+    d.block = blk;
+    d.units = cols / 8;
+    d.file_len = file_size;
+    std::shared_ptr<const Plan> plan;
+    std::vector<DevPlan> plans;
+    if (!missing.empty()) {  // survivors = the first k present, outputs = every absent shard
+        int rc = c.decode_plan(present, &plan);
+        if (rc) return fail(rc, rc == RS_E_SINGULAR ? "Matrix is singular" : "Not enough shards present");
+        RS_HIP(plan->device_plans(&plans));
+        d.tabs = plans[0].tabs;
+    }
+    for (int i = 0; i < d.k; ++i) {
+        d.in_shard[i] = surv[i];
+        if (!(d.in[i] = host_dev_addr(shards[surv[i]]))) return RS_OK;
+    }
+    for (int q = 0; q < d.nout; ++q) {
+        d.out_shard[q] = missing[q];
+        if (!(d.out[q] = host_dev_addr(shards[missing[q]]))) return RS_OK;
+    }
+    if (file_size && !(d.file_out = host_dev_addr(file_out))) return RS_OK;
+    if (!rsamd::file_direct_ok(d, false)) return RS_OK;
+    RS_HIP(rsamd::launch_file_decode_direct(d, ctx->stream));
+    *taken = true;
+    RS_HIP(hipStreamSynchronize(ctx->stream));
+    return RS_OK;
+}
+
 // rs_file_decode when byteCntInShard is the whole shard: one pass per chunk
 // -- upload the first k present shards, rebuild every absent shard and merge
 // the data shards into the file chunk on the GPU, download the rebuilt shards
@@ -418,6 +490,12 @@ int file_decode_chunked(const Codec &c, uint8_t *const *shards, const int64_t *l
     }
     // Nothing to rebuild: only the rows holding file bytes are needed.
     const size_t rows_needed = missing.empty() ? std::min(f.rows, (size_t(file_size) + kb - 1) / kb) : f.rows;
+    if (pinned) {  // direct path: the survivors, rebuilt shards and file coded in place
+        bool taken = false;
+        rc = file_decode_direct(c, shards, present, surv, missing, blk, file_out, size_t(file_size),
+                                rows_needed * blk, ctx, &taken);
+        if (rc || taken) return rc;
+    }
     auto flen_of = [&](size_t r0, size_t rc_rows) {
         const size_t fo = r0 * kb;
         return size_t(file_size) > fo ? std::min(rc_rows * kb, size_t(file_size) - fo) : size_t(0);
@@ -917,6 +995,11 @@ int rs_file_encode(const rs_codec *codec, const uint8_t *file, int64_t file_len,
         for (int i = 0; i < nshards; ++i) ranges.push_back({shards_out[i], size_t(S)});
         ranges.push_back({file, size_t(file_len)});
         pinned = reg.lock(ranges);
+    }
+    if (pinned) {
+        bool taken = false;
+        rc = file_encode_direct(*c, file, size_t(file_len), blk, shards_out, size_t(S), ctx, &taken);
+        if (rc || taken) return rc;
     }
     const FileChunks f = file_chunks(c->k(), c->total(), size_t(S), blk, pinned);
     auto flen_of = [&](size_t r0, size_t rc_rows) {  // every row holds file bytes

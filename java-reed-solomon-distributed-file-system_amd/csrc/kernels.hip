@@ -1186,11 +1186,11 @@ __global__ void __launch_bounds__(kThreads) gf_direct_kernel(DirectArgs a) {
             }
         }
     }
-    // head and tail bytes (fewer than 2 W): the first threads of block 0
+    // head bytes (< 4 KiB) and tail bytes (< W): block 0, one byte per thread
     const uint64_t tail0 = a.head + a.nvec * W;
     const uint64_t nbytes = a.head + (a.n - tail0);
-    if (blockIdx.x == 0 && threadIdx.x < nbytes) {
-        const uint64_t b = threadIdx.x < a.head ? threadIdx.x : tail0 + (threadIdx.x - a.head);
+    for (uint64_t t = threadIdx.x; blockIdx.x == 0 && t < nbytes; t += kThreads) {
+        const uint64_t b = t < a.head ? t : tail0 + (t - a.head);
         uint32_t acc[M] = {};
         for (int i = 0; i < a.nin; ++i) {
             const Sel s = selectors(a.in[i][b]);
@@ -1808,10 +1808,13 @@ hipError_t dispatch_direct(const DirectArgs &a, int nout, unsigned grid, Mode mo
 }
 }  // namespace
 
-// Blocks of the direct kernel: 512 x 256 threads keep ~2 MiB of loads in
-// flight, far more than the link's bandwidth-delay product; the probe read
-// the same rate from 256 to 4096 blocks (zc_probe_r3s2b.txt).
-constexpr unsigned kDirectBlocks = 512;
+// Blocks of the direct kernel: 256 x 256 threads keep ~1 MiB of loads in
+// flight, far more than the link's bandwidth-delay product.  4+2 x 64 MiB
+// encode, GiB/s (tools/direct_probe.py, profiles/r3/direct_probe_r3s2f.txt):
+//   blocks           64     128    256    512    1024
+//   pinned          50.6   51.8   51.7   50.5   44.2
+//   anonymous mmap  47.3   51.6   52.4   51.1   47.5
+constexpr unsigned kDirectBlocks = 256;
 
 hipError_t launch_gf_direct(const DirectPlan &p, size_t n, Mode mode, int *mismatch, hipStream_t s) {
     if (p.nin < 1 || p.nin > kMaxDirectIn || p.nout < 1 || p.nout > kMaxOut) return hipErrorInvalidValue;
@@ -1832,7 +1835,24 @@ hipError_t launch_gf_direct(const DirectPlan &p, size_t n, Mode mode, int *misma
     for (int i = 0; i < p.nin; ++i) a.in[i] = p.in[i];
     for (int q = 0; q < p.nout; ++q) a.out[q] = p.out[q];
     a.tabs = p.tabs;
-    a.head = std::min<uint64_t>(n, (W - reinterpret_cast<uintptr_t>(p.in[0]) % W) % W);
+    // The vectors start at the widest power-of-two boundary (up to a 4 KiB
+    // page) on which every shard agrees, so a wave's 1 KiB is whole 128-byte
+    // lines of one page: numpy arrays (malloc'd 16 bytes past a page start)
+    // read 48.5 GiB/s with 16-byte alignment and 52.4 with page alignment, as
+    // fast as pinned buffers (tools/direct_probe.py, profiles/r3/
+    // direct_probe_r3s2f.txt and r3s2g.txt).
+    uintptr_t align = W;
+    for (uintptr_t A = 4096; A > uintptr_t(W); A >>= 1) {
+        const uintptr_t r = reinterpret_cast<uintptr_t>(p.in[0]) % A;
+        bool same = true;
+        for (int i = 0; i < p.nin; ++i) same = same && reinterpret_cast<uintptr_t>(p.in[i]) % A == r;
+        for (int q = 0; q < p.nout; ++q) same = same && reinterpret_cast<uintptr_t>(p.out[q]) % A == r;
+        if (same) {
+            align = A;
+            break;
+        }
+    }
+    a.head = std::min<uint64_t>(n, (align - reinterpret_cast<uintptr_t>(p.in[0]) % align) % align);
     a.nvec = (n - a.head) / W;
     a.n = n;
     a.nin = p.nin;

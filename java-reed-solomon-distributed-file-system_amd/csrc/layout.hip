@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
+#include <vector>
 
 #include "gf_device.hpp"
 #include "tuning.hpp"
@@ -773,6 +774,175 @@ hipError_t launch_file_decode_fused(const FileGeom &g, const FileDecodePlan &p, 
     case 4: return launch_dec_t<4, 4>(a, s);
     }
     return hipErrorInvalidValue;
+}
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Direct file kernels: the host file API (rs_file_encode / rs_file_decode,
+// capi.cpp) on page-locked caller buffers, coded in place across the link
+// like kernels.hip gf_direct_kernel -- no staging buffers, no copy engine, H2D
+// and D2H at once.  One thread codes one 8-byte column unit of every shard
+// (block % 8 == 0, so a unit never crosses a block and its bytes of data shard
+// i are one 8-byte run of the file); runtime k, the output count a template
+// argument, so nothing is indexed dynamically in registers:
+//   encode: for each data shard i, load its file run (zero past file_len:
+//     the pad, ReedSolomonEncoder.java:76-85), store it to shard i and fold
+//     it into the M parity units, then store those.
+//   decode: for each survivor (the plan's first k present shards), load its
+//     unit, fold it into the E rebuilt units and, if it is a data shard, store
+//     it to its file run (trimmed at file_size); then store the rebuilt units
+//     to their shards (decodeMissing fills them in, ReedSolomonDecoder.java:36)
+//     and the rebuilt data units to the file.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t load_run8(const uint8_t *p, uint64_t f, uint64_t len) {
+    if (f + 8 <= len) return __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(p + f));
+    uint64_t v = 0;
+    for (uint64_t b = f; b < len && b < f + 8; ++b) v |= uint64_t(p[b]) << (8 * (b - f));
+    return v;
+}
+
+__device__ __forceinline__ void store_run8(uint8_t *p, uint64_t f, uint64_t len, uint64_t v) {
+    if (f + 8 <= len) {
+        __builtin_nontemporal_store(v, reinterpret_cast<uint64_t *>(p + f));
+        return;
+    }
+    for (uint64_t b = f; b < len && b < f + 8; ++b) p[b] = uint8_t(v >> (8 * (b - f)));
+}
+
+__device__ __forceinline__ void fold_unit(const uint32_t *t, uint64_t x, uint32_t &lo, uint32_t &hi) {
+    uint32_t a, b, c;
+    terms(t, selectors(uint32_t(x)), a, b, c);
+    lo = xor3(lo, a, b) ^ c;
+    terms(t, selectors(uint32_t(x >> 32)), a, b, c);
+    hi = xor3(hi, a, b) ^ c;
+}
+
+// Unit u codes shard column rot + 8u (mod cols): the shards' runs of a wave
+// then start on the widest power-of-two boundary (up to a page) their
+// addresses share, so a wave writes whole 128-byte lines (malloc'd arrays sit
+// 16 bytes past a page start; see kernels.hip launch_gf_direct).
+__device__ __forceinline__ uint64_t rotated_column(uint64_t u, const FileDirect &a) {
+    const uint64_t c = u * 8 + a.rot;
+    return c >= a.units * 8 ? c - a.units * 8 : c;
+}
+
+template <int M>
+__global__ void __launch_bounds__(kThreads) file_direct_encode_kernel(FileDirect a) {
+    const uint64_t step = uint64_t(gridDim.x) * kThreads;
+    for (uint64_t u = uint64_t(blockIdx.x) * kThreads + threadIdx.x; u < a.units; u += step) {
+        const uint64_t c = rotated_column(u, a), r = c / a.block, w = c - r * a.block;
+        uint32_t lo[M > 0 ? M : 1] = {}, hi[M > 0 ? M : 1] = {};
+        for (int i = 0; i < a.k; ++i) {
+            const uint64_t x = load_run8(a.file, (r * uint64_t(a.k) + uint64_t(i)) * a.block + w, a.file_len);
+            __builtin_nontemporal_store(x, reinterpret_cast<uint64_t *>(a.out[i] + c));
+#pragma unroll
+            for (int p = 0; p < M; ++p) fold_unit(a.tabs + (i * M + p) * 5, x, lo[p], hi[p]);
+        }
+#pragma unroll
+        for (int p = 0; p < M; ++p)
+            __builtin_nontemporal_store(uint64_t(lo[p]) | (uint64_t(hi[p]) << 32),
+                                        reinterpret_cast<uint64_t *>(a.out[a.k + p] + c));
+    }
+}
+
+template <int E>
+__global__ void __launch_bounds__(kThreads) file_direct_decode_kernel(FileDirect a) {
+    const uint64_t step = uint64_t(gridDim.x) * kThreads;
+    for (uint64_t u = uint64_t(blockIdx.x) * kThreads + threadIdx.x; u < a.units; u += step) {
+        const uint64_t c = rotated_column(u, a), r = c / a.block, w = c - r * a.block;
+        const uint64_t row0 = r * uint64_t(a.k) * a.block + w;
+        uint32_t lo[E > 0 ? E : 1] = {}, hi[E > 0 ? E : 1] = {};
+        for (int i = 0; i < a.k; ++i) {
+            const uint64_t x = __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(a.in[i] + c));
+#pragma unroll
+            for (int p = 0; p < E; ++p) fold_unit(a.tabs + (i * E + p) * 5, x, lo[p], hi[p]);
+            const int d = a.in_shard[i];
+            if (d < a.k) store_run8(a.file_out, row0 + uint64_t(d) * a.block, a.file_len, x);
+        }
+#pragma unroll
+        for (int p = 0; p < E; ++p) {
+            const uint64_t y = uint64_t(lo[p]) | (uint64_t(hi[p]) << 32);
+            __builtin_nontemporal_store(y, reinterpret_cast<uint64_t *>(a.out[p] + c));
+            const int d = a.out_shard[p];
+            if (d < a.k) store_run8(a.file_out, row0 + uint64_t(d) * a.block, a.file_len, y);
+        }
+    }
+}
+
+// 128 x 256 threads.  256 MiB file, 4+2, GiB/s (tools/direct_file_probe.py,
+// profiles/r3/direct_file_r3s2j.txt; link bound 32.1):
+//   blocks                     128    256    512
+//   encode numpy / pinned     30.0   29.4   28.8  /  30.1   29.7   29.6
+//   decode {0,5}              29.2   29.0   29.1  /  29.2   29.1   29.2
+// Before the column rotation, numpy arrays read 27.2 / 27.6 (r3s2i).
+constexpr unsigned kFileDirectBlocks = 128;
+
+unsigned file_direct_grid(uint64_t units) {
+    const uint64_t blocks = tuning_size("RSAMD_DIRECT_BLOCKS", kFileDirectBlocks);
+    return unsigned(std::max<uint64_t>(1, std::min<uint64_t>(blocks, (units + kThreads - 1) / kThreads)));
+}
+
+}  // namespace
+
+bool file_direct_ok(const FileDirect &d, bool encode) {
+    const int nptr = encode ? d.k + d.nout : d.nout;
+    bool ok = d.k >= 1 && d.k <= kMaxDirectIn && d.nout >= 0 && d.nout <= kMaxOut && d.block >= 8 &&
+              d.block % 8 == 0 && d.units * 8 % d.block == 0 && aligned(encode ? d.file : d.file_out, 8);
+    for (int i = 0; ok && !encode && i < d.k; ++i) ok = aligned(d.in[i], 8);
+    for (int i = 0; ok && i < nptr; ++i) ok = aligned(d.out[i], 8);
+    return ok;
+}
+
+// The rotation of rotated_column: bytes from the first shard's address to the
+// widest power-of-two boundary (<= 4 KiB) every shard address agrees on.
+static uint64_t file_direct_rot(const FileDirect &d, bool encode) {
+    std::vector<const void *> ptrs;
+    if (encode) {
+        for (int i = 0; i < d.k + d.nout; ++i) ptrs.push_back(d.out[i]);
+    } else {
+        for (int i = 0; i < d.k; ++i) ptrs.push_back(d.in[i]);
+        for (int i = 0; i < d.nout; ++i) ptrs.push_back(d.out[i]);
+    }
+    for (uintptr_t A = 4096; A > 8; A >>= 1) {
+        const uintptr_t r = reinterpret_cast<uintptr_t>(ptrs[0]) % A;
+        bool same = true;
+        for (const void *p : ptrs) same = same && reinterpret_cast<uintptr_t>(p) % A == r;
+        if (same) return ((A - r) % A) % (d.units * 8);
+    }
+    return 0;
+}
+
+hipError_t launch_file_encode_direct(const FileDirect &d0, hipStream_t s) {
+    if (!file_direct_ok(d0, true)) return hipErrorInvalidValue;
+    if (d0.units == 0) return hipSuccess;
+    FileDirect d = d0;
+    d.rot = file_direct_rot(d, true);
+    const dim3 grid(file_direct_grid(d.units));
+    switch (d.nout) {
+    case 0: hipLaunchKernelGGL((file_direct_encode_kernel<0>), grid, dim3(kThreads), 0, s, d); break;
+    case 1: hipLaunchKernelGGL((file_direct_encode_kernel<1>), grid, dim3(kThreads), 0, s, d); break;
+    case 2: hipLaunchKernelGGL((file_direct_encode_kernel<2>), grid, dim3(kThreads), 0, s, d); break;
+    case 3: hipLaunchKernelGGL((file_direct_encode_kernel<3>), grid, dim3(kThreads), 0, s, d); break;
+    default: hipLaunchKernelGGL((file_direct_encode_kernel<4>), grid, dim3(kThreads), 0, s, d); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_file_decode_direct(const FileDirect &d0, hipStream_t s) {
+    if (!file_direct_ok(d0, false)) return hipErrorInvalidValue;
+    if (d0.units == 0) return hipSuccess;
+    FileDirect d = d0;
+    d.rot = file_direct_rot(d, false);
+    const dim3 grid(file_direct_grid(d.units));
+    switch (d.nout) {
+    case 0: hipLaunchKernelGGL((file_direct_decode_kernel<0>), grid, dim3(kThreads), 0, s, d); break;
+    case 1: hipLaunchKernelGGL((file_direct_decode_kernel<1>), grid, dim3(kThreads), 0, s, d); break;
+    case 2: hipLaunchKernelGGL((file_direct_decode_kernel<2>), grid, dim3(kThreads), 0, s, d); break;
+    case 3: hipLaunchKernelGGL((file_direct_decode_kernel<3>), grid, dim3(kThreads), 0, s, d); break;
+    default: hipLaunchKernelGGL((file_direct_decode_kernel<4>), grid, dim3(kThreads), 0, s, d); break;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_split(const FileGeom &g, hipStream_t s) { return launch_split_merge(g, true, s); }

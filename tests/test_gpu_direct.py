@@ -25,21 +25,24 @@ def _shards(big, starts, n):
     return [big[s:s + n] for s in starts]
 
 
-@pytest.mark.parametrize("gap,offset", [
-    (0, 0),     # one residue modulo 16: 16-byte vectors, no head
-    (0, 9),     # same residue 9: 16-byte vectors after a 7-byte head
-    (8, 0),     # residues 0 / 8 alternate: 8-byte vectors
-    (8, 5),     # 8-byte vectors after a 3-byte head
-    (3, 0),     # no common residue modulo 8: the staged pipeline
+@pytest.mark.parametrize("page,gap,offset", [
+    (16, 0, 0),       # one residue modulo 16: 16-byte vectors, no head
+    (16, 0, 9),       # same residue 9: 16-byte vectors after a 7-byte head
+    (16, 8, 0),       # residues 0 / 8 alternate: 8-byte vectors
+    (16, 8, 5),       # 8-byte vectors after a 3-byte head
+    (16, 3, 0),       # no common residue modulo 8: the staged pipeline
+    (4096, 0, 16),    # one residue modulo 4 KiB (malloc'd arrays): a 4080-byte head to the page
+    (4096, 0, 4095),  # a 1-byte head
 ])
-def test_direct_encode_verify_decode(gpu, oracle_lib, gap, offset):
+def test_direct_encode_verify_decode(gpu, oracle_lib, page, gap, offset):
     import rsamd
     rs = rsamd.ReedSolomon.create(4, 2)
     n = N + offset + 32
-    slot = (n + 15) // 16 * 16 + gap
-    big = _pinned_block(6 * slot + 64)
+    slot = (n + page - 1) // page * page + gap
+    big = _pinned_block(6 * slot + 4096 + 64)
+    big = big[(-big.ctypes.data) % 4096:]  # page-aligned start
     sh = _shards(big, [i * slot for i in range(6)], n)
-    rng = np.random.default_rng(100 + gap * 10 + offset)
+    rng = np.random.default_rng(100 + gap * 10 + offset + page)
     for a in sh:
         a[:] = rng.integers(0, 256, n, dtype=np.uint8)
     count = N
@@ -139,3 +142,45 @@ def test_direct_threads(gpu, oracle_lib):
     for t in ts:
         t.join()
     assert not errors, errors
+
+
+# ---------------------------------------------------------------------------
+# The host file API's direct path (capi.cpp file_encode_direct /
+# file_decode_direct, layout.hip file_direct_*_kernel): ReedSolomonEncoder's
+# pad + split + encode and ReedSolomonDecoder's decode + merge + trim
+# (ReedSolomonEncoder.java:56-85, ReedSolomonDecoder.java:36,62-103) on
+# page-locked (or per-call locked) file and shard buffers.
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("k,m,n,file_off,pinned,misses", [
+    (4, 2, 20_000_003, 0, True, [(), (0, 5), (1, 4), (2,), (4, 5)]),   # ragged file end (pad inside a unit)
+    (4, 2, 16_000_000, 8, True, [(0, 1), (3,)]),                     # whole rows; 8-byte-aligned file start
+    (4, 2, 9_999_999, 3, True, [(0, 5)]),                            # file start not 8-aligned: staged
+    (10, 4, 30_000_001, 0, False, [(0, 3, 7, 12), (13,)]),           # pageable, locked per call
+    (3, 5, 7_000_011, 0, True, [(0, 1, 2, 3, 4)]),                   # 5 parity shards (> 4 outputs): staged encode
+])
+def test_direct_file_paths(gpu, oracle_lib, k, m, n, file_off, pinned, misses):
+    import rsamd
+    from rsamd.layout import file_decode_into, file_encode_into, file_layout
+    rs = rsamd.ReedSolomon.create(k, m)
+    oc = oracle_lib.Codec(k, m)
+    rng = np.random.default_rng(n)
+    alloc = _pinned_block if pinned else (lambda nb: np.empty(nb, np.uint8))
+    fbuf = alloc(n + 64)
+    fbuf = fbuf[(-fbuf.ctypes.data) % 64 + file_off:][:n]
+    fbuf[:] = rng.integers(0, 256, n, dtype=np.uint8)
+    _, S = file_layout(rs, n)
+    sh = [alloc(S) for _ in range(k + m)]
+    for a in sh:
+        a[:] = 0xEE  # every byte must be written
+    file_encode_into(rs, fbuf, sh)
+    ref = oc.file_encode(fbuf.tobytes())
+    assert np.array_equal(np.stack(sh), ref)
+    for miss in misses:
+        for j in miss:
+            sh[j][:] = 0
+        out = alloc(n + 64)[8:8 + n]
+        out[:] = 0x33
+        file_decode_into(rs, sh, [i not in miss for i in range(k + m)], S, out)
+        assert np.array_equal(out, fbuf), miss
+        assert np.array_equal(np.stack(sh), ref), miss  # absent shards rebuilt in place

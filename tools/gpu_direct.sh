@@ -1,0 +1,8 @@
+# Direct host path: its GPU tests, then the memory-backing x block-count probe.
+set -o pipefail
+tag=${1:-direct}
+mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_direct.py tests/test_gpu_host_register.py -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_direct_$tag.log 2>&1 || { tail -30 gpurun_out/pytest_direct_$tag.log; exit 1; }
+tail -1 gpurun_out/pytest_direct_$tag.log
+timeout -k 10 300 python3 tools/direct_probe.py --lib build/ab/tuning/librsamd.so --blocks ${2:-128,256,512} > gpurun_out/direct_probe_$tag.txt 2>&1 || { tail gpurun_out/direct_probe_$tag.txt; exit 1; }
+grep "^{" gpurun_out/direct_probe_$tag.txt
