@@ -68,6 +68,15 @@ uint8_t *host_dev_addr(const void *p) {
     return static_cast<uint8_t *>(d);
 }
 
+// Bytes per shard from which a pageable call is page-locked for the call and
+// coded by the direct kernel instead of being copied through the zero-copy
+// staging buffer (TUNING builds: RSAMD_DIRECT_MIN, read per call).  4+2
+// encodeParity per call, pageable / pinned, staged -> direct
+// (tools/direct_small_probe.py, profiles/r3/direct_small_r3s2k.txt):
+//   4 KiB 26.6 -> 31.5 / 26.3 -> 29.7 us;  64 KiB 39.8 -> 38.3 / 38.8 -> 31.8 us;
+//   256 KiB 93.5 -> 54.7 / 96.3 -> 50.5;  1 MiB 291 -> 122;  4 MiB 696 -> 371 us.
+size_t direct_min_bytes() { return rsamd::tuning_size("RSAMD_DIRECT_MIN", size_t(64) << 10); }
+
 int run_direct(ThreadCtx *ctx, const std::vector<DevPlan> &plans, const std::vector<int> &in_slots,
                const std::vector<int> &out_slots, uint8_t *const *host, size_t offset, size_t count, Mode mode,
                bool *taken) {
@@ -127,11 +136,13 @@ int run_host(const std::vector<DevPlan> &plans, int nslots, const std::vector<in
     ThreadCtx *ctx = nullptr;
     int rc = thread_ctx(&ctx);
     if (rc) return rc;
-    // Calls of <= 1 MiB per shard are one chunk either way (zero-copy path):
-    // skip the per-buffer pointer queries.
-    bool pinned = count > (size_t(1) << 20) && all_pinned(host, nslots);
+    // Small calls stay on the zero-copy staging path (direct_min_bytes): skip the
+    // per-buffer pointer queries.  Larger pageable calls lock the caller's
+    // ranges for the call and take the direct path (or the pipeline).
+    const size_t dmin = direct_min_bytes();
+    bool pinned = count >= std::min(dmin, size_t(1) << 20) && all_pinned(host, nslots);
     HostRegistration reg;
-    if (!pinned && count > chunk_bytes(count, nslots, false)) {  // pipelined: lock the caller's ranges
+    if (!pinned && (count > chunk_bytes(count, nslots, false) || count >= dmin)) {
         std::vector<std::pair<const uint8_t *, size_t>> ranges;
         for (int sl : in_slots) ranges.push_back({host[sl] + offset, count});
         if (mode == Mode::Code)
@@ -476,7 +487,7 @@ int file_decode_chunked(const Codec &c, uint8_t *const *shards, const int64_t *l
     bufs.push_back(file_out);
     bool pinned = all_pinned(bufs.data(), int(bufs.size()));
     HostRegistration reg;
-    if (!pinned && file_chunks(k, T, size_t(S), blk, false).n > 1) {
+    if (!pinned && (file_chunks(k, T, size_t(S), blk, false).n > 1 || size_t(S) >= direct_min_bytes())) {
         std::vector<std::pair<const uint8_t *, size_t>> ranges;
         for (int i = 0; i < T; ++i) ranges.push_back({shards[i], size_t(S)});
         ranges.push_back({file_out, size_t(file_size)});
@@ -990,7 +1001,7 @@ int rs_file_encode(const rs_codec *codec, const uint8_t *file, int64_t file_len,
     bufs.push_back(file);
     bool pinned = all_pinned(bufs.data(), int(bufs.size()));
     HostRegistration reg;
-    if (!pinned && file_chunks(c->k(), c->total(), size_t(S), blk, false).n > 1) {
+    if (!pinned && (file_chunks(c->k(), c->total(), size_t(S), blk, false).n > 1 || size_t(S) >= direct_min_bytes())) {
         std::vector<std::pair<const uint8_t *, size_t>> ranges;
         for (int i = 0; i < nshards; ++i) ranges.push_back({shards_out[i], size_t(S)});
         ranges.push_back({file, size_t(file_len)});

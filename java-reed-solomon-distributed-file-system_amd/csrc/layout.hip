@@ -846,27 +846,37 @@ __global__ void __launch_bounds__(kThreads) file_direct_encode_kernel(FileDirect
     }
 }
 
+// One 8-byte unit of the decode: column c (w = c % block) of block row r.
+template <int E>
+__device__ __forceinline__ void decode_unit(const FileDirect &a, uint64_t c, uint64_t r, uint64_t w) {
+    const uint64_t row0 = r * uint64_t(a.k) * a.block + w;
+    uint32_t lo[E > 0 ? E : 1] = {}, hi[E > 0 ? E : 1] = {};
+    for (int i = 0; i < a.k; ++i) {
+        const uint64_t x = __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(a.in[i] + c));
+#pragma unroll
+        for (int p = 0; p < E; ++p) fold_unit(a.tabs + (i * E + p) * 5, x, lo[p], hi[p]);
+        const int d = a.in_shard[i];
+        if (d < a.k) store_run8(a.file_out, row0 + uint64_t(d) * a.block, a.file_len, x);
+    }
+#pragma unroll
+    for (int p = 0; p < E; ++p) {
+        const uint64_t y = uint64_t(lo[p]) | (uint64_t(hi[p]) << 32);
+        __builtin_nontemporal_store(y, reinterpret_cast<uint64_t *>(a.out[p] + c));
+        const int d = a.out_shard[p];
+        if (d < a.k) store_run8(a.file_out, row0 + uint64_t(d) * a.block, a.file_len, y);
+    }
+}
+
+// Units in rotated column order, as the encode.  One wave per block row (so
+// that a wave writes the row's k * block contiguous file bytes instead of k
+// runs of 512 bytes that start anywhere in a line) read 27.6-27.8 GiB/s
+// against 29.2-29.3 (direct_file_r3s2m.txt) and was dropped.
 template <int E>
 __global__ void __launch_bounds__(kThreads) file_direct_decode_kernel(FileDirect a) {
     const uint64_t step = uint64_t(gridDim.x) * kThreads;
     for (uint64_t u = uint64_t(blockIdx.x) * kThreads + threadIdx.x; u < a.units; u += step) {
-        const uint64_t c = rotated_column(u, a), r = c / a.block, w = c - r * a.block;
-        const uint64_t row0 = r * uint64_t(a.k) * a.block + w;
-        uint32_t lo[E > 0 ? E : 1] = {}, hi[E > 0 ? E : 1] = {};
-        for (int i = 0; i < a.k; ++i) {
-            const uint64_t x = __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(a.in[i] + c));
-#pragma unroll
-            for (int p = 0; p < E; ++p) fold_unit(a.tabs + (i * E + p) * 5, x, lo[p], hi[p]);
-            const int d = a.in_shard[i];
-            if (d < a.k) store_run8(a.file_out, row0 + uint64_t(d) * a.block, a.file_len, x);
-        }
-#pragma unroll
-        for (int p = 0; p < E; ++p) {
-            const uint64_t y = uint64_t(lo[p]) | (uint64_t(hi[p]) << 32);
-            __builtin_nontemporal_store(y, reinterpret_cast<uint64_t *>(a.out[p] + c));
-            const int d = a.out_shard[p];
-            if (d < a.k) store_run8(a.file_out, row0 + uint64_t(d) * a.block, a.file_len, y);
-        }
+        const uint64_t c = rotated_column(u, a), r = c / a.block;
+        decode_unit<E>(a, c, r, c - r * a.block);
     }
 }
 

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--lib", default=None)
     ap.add_argument("--calls", type=int, default=5)
     ap.add_argument("--blocks", default="256")
+    ap.add_argument("--rows", default="1", help="RSAMD_FILE_DEC_ROWS values (a dropped decode mapping A/B; ignored by current builds)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -41,8 +42,10 @@ def main():
         f[:] = src
         kinds[name] = (f, [alloc(S) for _ in range(k + m)], alloc(n))
     present = [False] + [True] * (k + m - 2) + [False]
-    for blocks in [int(b) for b in a.blocks.split(",")]:
+    import itertools
+    for blocks, rows in itertools.product([int(b) for b in a.blocks.split(",")], a.rows.split(",")):
         os.environ["RSAMD_DIRECT_BLOCKS"] = str(blocks)
+        os.environ["RSAMD_FILE_DEC_ROWS"] = rows
         for name, (f, sh, out) in kinds.items():
             for leg in ("encode", "decode_0_5"):
                 def call():
@@ -58,7 +61,7 @@ def main():
                     ts.append((time.perf_counter() - t0) * 1e3)
                 ts.sort()
                 ok = bool(np.array_equal(out, f)) if leg != "encode" else True
-                print(json.dumps({"blocks": blocks, "mem": name, "leg": leg, "median_ms": round(ts[len(ts) // 2], 3),
+                print(json.dumps({"blocks": blocks, "rows": rows, "mem": name, "leg": leg, "median_ms": round(ts[len(ts) // 2], 3),
                                   "GiBps": round(n / (ts[len(ts) // 2] * 1e-3) / 2**30, 2), "file_ok": ok}), flush=True)
 
 
