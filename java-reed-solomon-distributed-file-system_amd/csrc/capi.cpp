@@ -83,10 +83,11 @@ int run_direct(ThreadCtx *ctx, const std::vector<DevPlan> &plans, const std::vec
     *taken = false;
     if (!direct_enabled() || plans.empty()) return RS_OK;
     std::vector<rsamd::DirectPlan> dp(plans.size());
+    // The range's own first byte: a call locked for its range only has no
+    // device mapping before host[slot] + offset.
     auto dev_addr = [&](int slot, uint8_t **out) {
-        uint8_t *d = host_dev_addr(host[slot]);
-        *out = d ? d + offset : nullptr;
-        return d != nullptr;
+        *out = host_dev_addr(host[slot] + offset);
+        return *out != nullptr;
     };
     for (size_t g = 0; g < plans.size(); ++g) {
         const DevPlan &p = plans[g];

@@ -85,6 +85,24 @@ def test_direct_pageable_registered(gpu, oracle_lib):
     assert rs.isParityCorrect(sh, 0, n)
 
 
+def test_direct_pageable_offset_range(gpu, oracle_lib):
+    """A pageable call on a range far into its arrays: only the range's pages
+    are locked, so the kernel's addresses come from the range's first byte."""
+    import rsamd
+    rs = rsamd.ReedSolomon.create(4, 2)
+    n, off, cnt = 12 << 20, (3 << 20) + 5, (4 << 20) + 3
+    rng = np.random.default_rng(17)
+    sh = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(6)]
+    ref = [a.copy() for a in sh]
+    oracle_lib.Codec(4, 2).encode_parity(ref, off, cnt)
+    rs.encodeParity(sh, off, cnt)
+    assert all(np.array_equal(a, b) for a, b in zip(sh, ref))  # outside the range untouched
+    assert rs.isParityCorrect(sh, off, cnt)
+    sh[2][off:off + cnt] = 0
+    rs.decodeMissing(sh, [True, True, False, True, True, True], off, cnt)
+    assert all(np.array_equal(a, b) for a, b in zip(sh, ref))
+
+
 @pytest.mark.parametrize("nin,nout", [(7, 9), (32, 2), (33, 1)])
 def test_direct_code_some_shards(gpu, oracle_lib, nin, nout):
     """CodingLoop.codeSomeShards / checkSomeShards on pinned buffers: more
