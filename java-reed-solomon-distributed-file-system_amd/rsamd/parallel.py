@@ -10,7 +10,9 @@ CPU.  RSAMD_DIST_BACKEND=gloo|nccl overrides the choice.
 """
 from __future__ import annotations
 
+import contextlib
 import os
+import sys
 from dataclasses import dataclass
 
 
@@ -58,8 +60,27 @@ def init_from_env(use_gpu: bool = True) -> Rank:
             kw = {}
             if backend == "nccl":
                 kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
-            dist.init_process_group(backend, **kw)
+            # gloo prints "Rank r is connected to ..." on stdout while it
+            # connects; the bench's stdout must carry its JSON line only.
+            with _stdout_to_stderr():
+                dist.init_process_group(backend, **kw)
+                dist.barrier()
     return Rank(rank, world, local, backend)
+
+
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """File descriptor 1 points at stderr inside the block (native code
+    writing to stdout included)."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 def _reduce(r: Rank, value: float, op: str, dtype=None) -> float:

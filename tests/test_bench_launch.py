@@ -38,6 +38,9 @@ def test_self_launch_two_ranks():
     p = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--launch-probe", "--cfg3-stripes", "1024"],
                        env=_env(), capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-3000:]
+    # stdout is the one JSON line and nothing else (gloo's connect messages
+    # are kept on stderr: parallel.init_from_env)
+    assert len(p.stdout.strip().splitlines()) == 1, p.stdout
     lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout  # rank 0 only
     got = lines[0]
