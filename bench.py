@@ -33,6 +33,7 @@ Run:  python bench.py [--gpus N --steps K --warmup W]
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import math
 import os
@@ -305,13 +306,15 @@ def run(args, live_traffic=None):
             extra.update(layout_legs(torch, rsamd, dev, stream))
             cpu = cpu_baseline(k, m, S, args.cpu_seconds)
             extra["cpu_configs"] = cpu_configs()
-            link = host_link(torch)
-            extra.update(host_inclusive(rsamd, k, m, link))
-            extra.update(config0_single_stripe(rsamd, k, m))
+            with gpu_numa_bound(torch, parallel, extra):
+                link = host_link(torch)
+                extra.update(host_inclusive(rsamd, k, m, link))
+                extra.update(config0_single_stripe(rsamd, k, m))
         else:
             # every rank at once: the node's aggregate host <-> device rate
-            link = host_link(torch)
-            extra.update(host_inclusive_all_ranks(rsamd, parallel, r, k, m, link))
+            with gpu_numa_bound(torch, parallel, extra):
+                link = host_link(torch)
+                extra.update(host_inclusive_all_ranks(rsamd, parallel, r, k, m, link))
             # The CPU baseline at N > 1: rank 0 alone, after every GPU leg,
             # 1 thread (the reference's single-threaded client loop).
             parallel.barrier(r)
@@ -1126,6 +1129,30 @@ def cpu_configs(budget_s=1.0):
 # ---------------------------------------------------------------------------
 # Host-resident legs (PCIe-inclusive; never the bench value)
 # ---------------------------------------------------------------------------
+@contextlib.contextmanager
+def gpu_numa_bound(torch, parallel, extra):
+    """The host legs run on the CPUs of this GPU's NUMA node, as a deployment
+    places one client process per GPU: the legs' host arrays are allocated
+    inside, so first touch puts them on that node.  Unbound, the pageable
+    direct-path legs read 49.8-52.6 GiB/s by where the scheduler put the
+    process; bound 51.5-52.7 (tools/numa_probe.py, profiles/r3/numa_r3s2n.txt).
+    The affinity is restored afterwards (the CPU baseline runs unbound)."""
+    ident = parallel.device_identity(torch)
+    node, cpus = parallel.gpu_numa_cpus(ident.get("pci"))
+    saved = os.sched_getaffinity(0)
+    bound = bool(cpus)
+    if bound:
+        os.sched_setaffinity(0, cpus)
+    extra["host_legs_numa"] = {"gpu_numa_node": node, "bound_cpus": len(cpus) if bound else 0,
+                               "note": "host legs bound to the GPU's NUMA node" if bound
+                               else "GPU NUMA node unknown: host legs unbound"}
+    try:
+        yield
+    finally:
+        if bound:
+            os.sched_setaffinity(0, saved)
+
+
 def host_link(torch, n=64 << 20, reps=8):
     """The host <-> device link measured in this run: pinned n-byte copies
     H2D alone, D2H alone, and both at once on two streams (each direction

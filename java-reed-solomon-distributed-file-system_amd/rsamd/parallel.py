@@ -153,3 +153,37 @@ def distinct_devices(identities) -> int:
     for d in identities:
         keys.add(d.get("pci") or d.get("uuid") or f"index{d.get('index')}")
     return len(keys)
+
+
+def _cpulist(text: str) -> set:
+    """CPU ids of a sysfs cpulist ("0-3,8,10-11")."""
+    out = set()
+    for part in text.strip().split(","):
+        if part:
+            a, _, b = part.partition("-")
+            out.update(range(int(a), int(b or a) + 1))
+    return out
+
+
+def gpu_numa_cpus(pci, sysfs="/sys"):
+    """(NUMA node of the GPU at PCI address `pci` (domain:bus:device), the
+    CPUs of that node this process may run on) from sysfs, or (None, set())
+    when either is unknown.  A host process that feeds one GPU from its own
+    memory runs best there: first touch then places its buffers on the node
+    of the GPU's PCIe root (numa_r3s2n.txt)."""
+    if not pci:
+        return None, set()
+    node = None
+    for fn in range(8):
+        path = os.path.join(sysfs, "bus/pci/devices", f"{pci}.{fn}", "numa_node")
+        if os.path.exists(path):
+            with open(path) as f:
+                node = int(f.read())
+            break
+    if node is None or node < 0:
+        return None, set()
+    path = os.path.join(sysfs, "devices/system/node", f"node{node}", "cpulist")
+    if not os.path.exists(path):
+        return node, set()
+    with open(path) as f:
+        return node, _cpulist(f.read()) & os.sched_getaffinity(0)
