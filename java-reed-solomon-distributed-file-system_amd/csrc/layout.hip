@@ -880,6 +880,72 @@ __global__ void __launch_bounds__(kThreads) file_direct_decode_kernel(FileDirect
     }
 }
 
+// Tiled form: a workgroup owns R whole block rows at a time.  Phase 1 codes
+// the tile's units and parks every data unit (survivor or rebuilt) at its
+// place in an LDS copy of the tile's file bytes, and the rebuilt units in LDS
+// copies of their shard runs; phase 2 writes each as ONE contiguous run of
+// 16-byte stores (8-byte at an 8-byte-aligned start), so every line but the
+// two at a run's ends is written whole, where the untiled form writes k runs
+// of 512 bytes per wave that start anywhere in a line.  LDS: (k + E) * R *
+// block bytes, R = the rows that fit kDecTileLds.  256 MiB file, {0,5}: 30.0 /
+// 30.1 GiB/s (numpy / pinned) against 29.2 / 29.1 untiled, 0.94 of the link
+// bound (tools/direct_file_probe.py --rows 0,1, profiles/r3/direct_file_r3s2p.txt).
+constexpr size_t kDecTileLds = 65536;
+
+__device__ __forceinline__ void lds_run_out(uint8_t *dst, const uint8_t *lds, uint64_t n) {
+    // dst and lds are 8-byte aligned; 16-byte vectors when both are 16-byte aligned.
+    uint64_t b = 0;
+    const bool v16 = reinterpret_cast<uintptr_t>(dst) % 16 == 0 && reinterpret_cast<uintptr_t>(lds) % 16 == 0;
+    if (v16) {
+        for (b = uint64_t(threadIdx.x) * 16; b + 16 <= n; b += uint64_t(kThreads) * 16)
+            __builtin_nontemporal_store(*reinterpret_cast<const u32x4 *>(lds + b), reinterpret_cast<u32x4 *>(dst + b));
+        b = n / 16 * 16;
+    }
+    for (uint64_t q = b + uint64_t(threadIdx.x) * 8; q + 8 <= n; q += uint64_t(kThreads) * 8)
+        __builtin_nontemporal_store(*reinterpret_cast<const uint64_t *>(lds + q), reinterpret_cast<uint64_t *>(dst + q));
+    for (uint64_t q = n / 8 * 8 + threadIdx.x; q < n; q += kThreads) dst[q] = lds[q];
+}
+
+template <int E>
+__global__ void __launch_bounds__(kThreads) file_direct_decode_tiled_kernel(FileDirect a, uint32_t R) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    const uint64_t blk = a.block, k = uint64_t(a.k);
+    const uint64_t rows = a.units * 8 / blk, tiles = (rows + R - 1) / R;
+    const uint64_t fstride = uint64_t(R) * k * blk;  // LDS bytes of the file tile
+    for (uint64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+        const uint64_t r0 = t * R, nrows = rows - r0 < R ? rows - r0 : R;
+        const uint64_t c0 = r0 * blk, ncols = nrows * blk, f0 = r0 * k * blk;
+        for (uint64_t cc = uint64_t(threadIdx.x) * 8; cc < ncols; cc += uint64_t(kThreads) * 8) {
+            const uint64_t rr = cc / blk, w = cc - rr * blk, frow = rr * k * blk + w;
+            uint32_t lo[E > 0 ? E : 1] = {}, hi[E > 0 ? E : 1] = {};
+            for (int i = 0; i < a.k; ++i) {
+                const uint64_t x = __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(a.in[i] + c0 + cc));
+#pragma unroll
+                for (int p = 0; p < E; ++p) fold_unit(a.tabs + (i * E + p) * 5, x, lo[p], hi[p]);
+                const int d = a.in_shard[i];
+                if (d < a.k) *reinterpret_cast<uint64_t *>(lds + frow + uint64_t(d) * blk) = x;
+            }
+#pragma unroll
+            for (int p = 0; p < E; ++p) {
+                const uint64_t y = uint64_t(lo[p]) | (uint64_t(hi[p]) << 32);
+                *reinterpret_cast<uint64_t *>(lds + fstride + uint64_t(p) * R * blk + cc) = y;
+                const int d = a.out_shard[p];
+                if (d < a.k) *reinterpret_cast<uint64_t *>(lds + frow + uint64_t(d) * blk) = y;
+            }
+        }
+        __syncthreads();
+        if (f0 < a.file_len) lds_run_out(a.file_out + f0, lds, a.file_len - f0 < nrows * k * blk ? a.file_len - f0 : nrows * k * blk);
+#pragma unroll
+        for (int p = 0; p < E; ++p) lds_run_out(a.out[p] + c0, lds + fstride + uint64_t(p) * R * blk, ncols);
+        __syncthreads();
+    }
+}
+
+uint32_t dec_tile_rows(const FileDirect &d) {
+    const uint64_t per_row = uint64_t(d.k + d.nout) * d.block;
+    return uint32_t(std::min<uint64_t>(tuning_size("RSAMD_DEC_TILE_LDS", kDecTileLds) / per_row, d.units * 8 / d.block));
+}
+
 // 128 x 256 threads.  256 MiB file, 4+2, GiB/s (tools/direct_file_probe.py,
 // profiles/r3/direct_file_r3s2j.txt; link bound 32.1):
 //   blocks                     128    256    512
@@ -945,6 +1011,18 @@ hipError_t launch_file_decode_direct(const FileDirect &d0, hipStream_t s) {
     FileDirect d = d0;
     d.rot = file_direct_rot(d, false);
     const dim3 grid(file_direct_grid(d.units));
+    const uint32_t R = dec_tile_rows(d);
+    if (R >= 1 && tuning_size("RSAMD_DEC_TILED", 1)) {
+        const size_t lds = size_t(d.k + d.nout) * R * d.block;
+        switch (d.nout) {
+        case 0: hipLaunchKernelGGL((file_direct_decode_tiled_kernel<0>), grid, dim3(kThreads), lds, s, d, R); break;
+        case 1: hipLaunchKernelGGL((file_direct_decode_tiled_kernel<1>), grid, dim3(kThreads), lds, s, d, R); break;
+        case 2: hipLaunchKernelGGL((file_direct_decode_tiled_kernel<2>), grid, dim3(kThreads), lds, s, d, R); break;
+        case 3: hipLaunchKernelGGL((file_direct_decode_tiled_kernel<3>), grid, dim3(kThreads), lds, s, d, R); break;
+        default: hipLaunchKernelGGL((file_direct_decode_tiled_kernel<4>), grid, dim3(kThreads), lds, s, d, R); break;
+        }
+        return hipGetLastError();
+    }
     switch (d.nout) {
     case 0: hipLaunchKernelGGL((file_direct_decode_kernel<0>), grid, dim3(kThreads), 0, s, d); break;
     case 1: hipLaunchKernelGGL((file_direct_decode_kernel<1>), grid, dim3(kThreads), 0, s, d); break;

@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--lib", default=None)
     ap.add_argument("--calls", type=int, default=5)
     ap.add_argument("--blocks", default="256")
-    ap.add_argument("--rows", default="1", help="RSAMD_FILE_DEC_ROWS values (a dropped decode mapping A/B; ignored by current builds)")
+    ap.add_argument("--rows", default="1", help="RSAMD_DEC_TILED values (direct file decode: 1 LDS-tiled, 0 untiled)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -45,7 +45,7 @@ def main():
     import itertools
     for blocks, rows in itertools.product([int(b) for b in a.blocks.split(",")], a.rows.split(",")):
         os.environ["RSAMD_DIRECT_BLOCKS"] = str(blocks)
-        os.environ["RSAMD_FILE_DEC_ROWS"] = rows
+        os.environ["RSAMD_DEC_TILED"] = rows
         for name, (f, sh, out) in kinds.items():
             for leg in ("encode", "decode_0_5"):
                 def call():
