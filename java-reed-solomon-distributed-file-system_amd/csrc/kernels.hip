@@ -305,9 +305,15 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(RSAM
 }
 
 // ---------------------------------------------------------------------------
-// Vector kernel, runtime input count (any k), M outputs; the next input's
-// vector is prefetched while the current one is folded in.
+// Vector kernel, runtime input count (any k), M outputs.  Inputs go in groups
+// of RSAMD_GEN_GROUP, software-pipelined: group g+1's loads are issued before
+// group g is folded in, so a wave keeps up to 2 * RSAMD_GEN_GROUP input
+// vectors in flight (the compiled shapes load theirs up front or 5 ahead).
+// Every group condition is wave-uniform.
 // ---------------------------------------------------------------------------
+#ifndef RSAMD_GEN_GROUP
+#define RSAMD_GEN_GROUP 4  // A/B builds: 1 = one input ahead (the round-2 form)
+#endif
 template <int M, bool VERIFY>
 __global__ void __launch_bounds__(kWave) gf_vec_generic_kernel(VecArgs a) {
     if (VERIFY && mismatch_seen(a.mismatch)) return;
@@ -316,31 +322,45 @@ __global__ void __launch_bounds__(kWave) gf_vec_generic_kernel(VecArgs a) {
     const uint32_t v = chunk * uint32_t(kWave) + threadIdx.x;
     if (v >= a.nvec) return;
     uint8_t *sb = a.base + uint64_t(stripe) * a.stripe_stride + uint64_t(v) * 16;
+    constexpr int G = RSAMD_GEN_GROUP;
+    const int nin = a.nin;
     uint64_t out_off[M];
 #pragma unroll
     for (int p = 0; p < M; ++p) out_off[p] = uint64_t(a.out_idx[p]) * a.shard_stride;
     u32x4 acc[M];
 #pragma unroll
     for (int p = 0; p < M; ++p) acc[p] = u32x4{0, 0, 0, 0};
-    u32x4 next = load_stream(sb + uint64_t(a.in_idx[0]) * a.shard_stride);
-    for (int i = 0; i < a.nin; ++i) {
-        const u32x4 x = next;
-        if (i + 1 < a.nin) next = load_stream(sb + uint64_t(a.in_idx[i + 1]) * a.shard_stride);
-        uint32_t T[M][5];
+    u32x4 cur[G];
 #pragma unroll
-        for (int p = 0; p < M; ++p)
+    for (int q = 0; q < G; ++q)
+        if (q < nin) cur[q] = load_stream(sb + uint64_t(a.in_idx[q]) * a.shard_stride);
+    for (int i0 = 0; i0 < nin; i0 += G) {
+        u32x4 nxt[G];
 #pragma unroll
-            for (int j = 0; j < 5; ++j) T[p][j] = a.tabs[(i * M + p) * 5 + j];
+        for (int q = 0; q < G; ++q)
+            if (i0 + G + q < nin) nxt[q] = load_stream(sb + uint64_t(a.in_idx[i0 + G + q]) * a.shard_stride);
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const Sel s = selectors(x[w]);
+        for (int q = 0; q < G; ++q) {
+            if (i0 + q >= nin) break;
+            uint32_t T[M][5];
 #pragma unroll
-            for (int p = 0; p < M; ++p) {
-                uint32_t t0, t1, t2;
-                terms(T[p], s, t0, t1, t2);
-                acc[p][w] = xor3(acc[p][w], t0, t1) ^ t2;
+            for (int p = 0; p < M; ++p)
+#pragma unroll
+                for (int j = 0; j < 5; ++j) T[p][j] = a.tabs[((i0 + q) * M + p) * 5 + j];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const Sel s = selectors(cur[q][w]);
+#pragma unroll
+                for (int p = 0; p < M; ++p) {
+                    uint32_t t0, t1, t2;
+                    terms(T[p], s, t0, t1, t2);
+                    acc[p][w] = xor3(acc[p][w], t0, t1) ^ t2;
+                }
             }
         }
+#pragma unroll
+        for (int q = 0; q < G; ++q)
+            if (i0 + G + q < nin) cur[q] = nxt[q];
     }
 #pragma unroll
     for (int p = 0; p < M; ++p) emit<VERIFY>(sb + out_off[p], acc[p], a.mismatch);
@@ -1248,7 +1268,15 @@ size_t vec_lds_pad(int k, int m, bool verify) {
         if (verify) return 0;
         return m >= 4 ? 10240 : m == 3 ? 13568 : m == 2 ? 16384 : 20480;
     }
-    return 0;
+    // The runtime-k kernel (every other k; called with k = 0), since it loads
+    // its inputs in pipelined groups of 4.  Granule batches, one pool per
+    // shape, builds alternated (tools/gpu_gen.sh, profiles/r3/gen_r3s2q.txt),
+    // best group-of-1 build (the round-2 kernel, uncapped) -> groups of 4 here:
+    // 17+3 encode 0.742 -> 0.759, {0,1,2} 0.742 -> 0.762; 8+4 encode 0.797 ->
+    // 0.805; 8+4 decode {0} 0.69 -> 0.772 (at 12544); 6+3 encode 0.811 -> 0.84,
+    // {0,1} 0.80 -> 0.852.  Verify stays uncapped (as 10+4 verify).
+    if (verify) return 0;
+    return m == 1 ? 12544 : 10240;
 }
 
 // The same cap for the per-stripe-pattern kernels (gf_masked_kernel), granule
@@ -1282,7 +1310,8 @@ hipError_t launch_vec_generic_t(VecArgs a, Mode mode, hipStream_t s) {
 }
 
 // Compile-time shapes for the BASELINE geometries (4+2 and 10+4 with any
-// erasure count); every other shape runs the runtime-k kernel.
+// erasure count); every other shape runs the runtime-k kernel, capped and in
+// plain order like them (block_order: capped).
 hipError_t dispatch_vec(VecArgs a, int nout, Mode mode, hipStream_t s) {
 #define RSAMD_CASE(K, M) \
     if (a.nin == K && nout == M) return launch_vec_t<K, M>(a, mode, s);
