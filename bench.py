@@ -1153,22 +1153,49 @@ def gpu_numa_bound(torch, parallel, extra):
             os.sched_setaffinity(0, saved)
 
 
+def _host_dev_ptr(ptr):
+    """Device address of page-locked host memory (hipHostGetDevicePointer)."""
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so")
+    d = C.c_void_p()
+    if hip.hipHostGetDevicePointer(C.byref(d), C.c_void_p(ptr), C.c_uint(0)) != 0 or not d.value:
+        return None
+    return d.value
+
+
 def host_link(torch, n=64 << 20, reps=8):
     """The host <-> device link measured in this run: pinned n-byte copies
     H2D alone, D2H alone, and both at once on two streams (each direction
-    timed by events on its own stream), GB/s.  The host-inclusive legs are
-    quoted against the bound these give (link_bound_GiBps)."""
+    timed by events on its own stream), GB/s -- by the copy engines (torch
+    copy_), and by a copy kernel loading or storing the pinned buffer through
+    its device mapping (rs_copy_dev), the way the direct host path moves its
+    bytes.  The host-inclusive legs are quoted against the larger of the two
+    bounds these give (link_bound_GiBps)."""
+    from rsamd import device as rdev
     a = torch.empty(n, dtype=torch.uint8, pin_memory=True)
     b = torch.empty(n, dtype=torch.uint8, pin_memory=True)
     d1 = torch.empty(n, dtype=torch.uint8, device="cuda")
     d2 = torch.empty(n, dtype=torch.uint8, device="cuda")
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    pa, pb = _host_dev_ptr(a.data_ptr()), _host_dev_ptr(b.data_ptr())
+    kernel_mode = [False]
+
+    def up_fn():
+        if kernel_mode[0]:
+            rdev.copy(d1.data_ptr(), pa, n, torch.cuda.current_stream())
+        else:
+            d1.copy_(a, non_blocking=True)
+
+    def down_fn():
+        if kernel_mode[0]:
+            rdev.copy(pb, d2.data_ptr(), n, torch.cuda.current_stream())
+        else:
+            b.copy_(d2, non_blocking=True)
 
     def run(up, down):
         s1, s2 = streams
         ev = {}
-        for name, on, st, fn in (("h2d", up, s1, lambda: d1.copy_(a, non_blocking=True)),
-                                 ("d2h", down, s2, lambda: b.copy_(d2, non_blocking=True))):
+        for name, on, st, fn in (("h2d", up, s1, up_fn), ("d2h", down, s2, down_fn)):
             if not on:
                 continue
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -1197,13 +1224,22 @@ def host_link(torch, n=64 << 20, reps=8):
         got = run(True, True)
         if both is None or got["h2d"] + got["d2h"] > both["h2d"] + both["d2h"]:
             both = got
+    out = {"h2d_GBps": round(h2d, 2), "d2h_GBps": round(d2h, 2),
+           "both_h2d_GBps": round(both["h2d"], 2), "both_d2h_GBps": round(both["d2h"], 2),
+           "both_GBps": round(both["h2d"] + both["d2h"], 2),
+           "note": f"pinned {n >> 20} MiB copies, {reps} per direction, torch copy_ on dedicated streams, "
+                   f"each direction timed by HIP events on its own stream, alone and with the other running "
+                   f"(best of 3 stream pairs); kernel_*: the same by a copy kernel through the buffers' "
+                   f"device mapping"}
+    if pa and pb:
+        kernel_mode[0] = True
+        run(True, True)
+        kh, kd = run(True, False)["h2d"], run(False, True)["d2h"]
+        kb = run(True, True)
+        out["kernel"] = {"h2d_GBps": round(kh, 2), "d2h_GBps": round(kd, 2), "both_h2d_GBps": round(kb["h2d"], 2),
+                         "both_d2h_GBps": round(kb["d2h"], 2), "both_GBps": round(kb["h2d"] + kb["d2h"], 2)}
     del a, b, d1, d2
-    return {"h2d_GBps": round(h2d, 2), "d2h_GBps": round(d2h, 2),
-            "both_h2d_GBps": round(both["h2d"], 2), "both_d2h_GBps": round(both["d2h"], 2),
-            "both_GBps": round(both["h2d"] + both["d2h"], 2),
-            "note": f"pinned {n >> 20} MiB copies, {reps} per direction, torch copy_ on dedicated streams, "
-                    f"each direction timed by HIP events on its own stream, alone and with the other running "
-                    f"(best of 3 stream pairs)"}
+    return out
 
 
 def link_bound_GiBps(link, up, down):
@@ -1211,9 +1247,13 @@ def link_bound_GiBps(link, up, down):
     H2D and `down` bytes D2H per user byte, with both directions overlapped
     as far as the data allows: while both run, each moves at its rate with
     the other running (both_*); the remainder of the larger direction at its
-    rate alone."""
+    rate alone.  With a kernel-driven measurement in `link` as well, the
+    larger of the two bounds."""
     if not link:
         return None
+    if link.get("kernel"):
+        return max(link_bound_GiBps({k: v for k, v in link.items() if k != "kernel"}, up, down),
+                   link_bound_GiBps(link["kernel"], up, down))
     h, d = link["h2d_GBps"] * 1e9, link["d2h_GBps"] * 1e9
     hb, db = link.get("both_h2d_GBps", h / 1e9) * 1e9, link.get("both_d2h_GBps", d / 1e9) * 1e9
     tc = min(up / hb, down / db) if down else 0.0  # both directions busy

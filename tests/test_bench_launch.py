@@ -183,3 +183,9 @@ def test_link_bound():
     # 1 up, 1 down: all of it at the both-ways rates
     assert abs(bench.link_bound_GiBps(link, 1.0, 1.0) - 40e9 / 2**30) < 0.01
     assert bench.link_bound_GiBps(None, 1.0, 0.5) is None
+    # a kernel-driven measurement too: the larger of the two bounds
+    link2 = dict(link, kernel={"h2d_GBps": 60.0, "d2h_GBps": 45.0, "both_h2d_GBps": 44.0, "both_d2h_GBps": 44.0})
+    assert abs(bench.link_bound_GiBps(link2, 1.0, 0.0) - 60e9 / 2**30) < 0.01
+    assert abs(bench.link_bound_GiBps(link2, 1.0, 1.0) - 44e9 / 2**30) < 0.01
+    link3 = dict(link, kernel={"h2d_GBps": 30.0, "d2h_GBps": 30.0, "both_h2d_GBps": 20.0, "both_d2h_GBps": 20.0})
+    assert bench.link_bound_GiBps(link3, 1.0, 0.5) == bench.link_bound_GiBps(link, 1.0, 0.5)
