@@ -234,7 +234,15 @@ size_t chunk_bytes(size_t total, int nslots, bool pinned) {
     return std::min(kChunk, c);
 }
 
-// True when every non-null pointer is page-locked host memory known to HIP.
+namespace {
+bool registry_holds(const void *p);  // below: locked for a call by HostRegistration
+}
+
+// True when every non-null pointer is page-locked host memory known to HIP
+// and stays so for the call: memory that HostRegistration locked for another
+// thread's call reads as pinned too, but is unlocked when that call ends, so
+// it counts as pageable here (the caller then locks it and shares that
+// registration by reference count).
 bool all_pinned(const uint8_t *const *ptrs, int n) {
     for (int i = 0; i < n; ++i) {
         if (!ptrs[i]) continue;
@@ -243,7 +251,7 @@ bool all_pinned(const uint8_t *const *ptrs, int n) {
             (void)hipGetLastError();  // pageable memory: clear the sticky error
             return false;
         }
-        if (attr.type != hipMemoryTypeHost) return false;
+        if (attr.type != hipMemoryTypeHost || registry_holds(ptrs[i])) return false;
     }
     return true;
 }
@@ -272,6 +280,16 @@ struct HostRegistry {
 HostRegistry &host_registry() {
     static HostRegistry *r = new HostRegistry;  // never destroyed: no HIP calls at exit
     return *r;
+}
+
+bool registry_holds(const void *p) {
+    HostRegistry &reg = host_registry();
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> guard(reg.mu);
+    auto next = reg.regs.upper_bound(a);
+    if (next == reg.regs.begin()) return false;
+    const auto prev = std::prev(next);
+    return a >= prev->first && a < prev->second.first;
 }
 
 // Drops this call's references; the last one unregisters.  Caller holds reg.mu.

@@ -73,3 +73,37 @@ def test_same_array_twice_as_input(gpu, oracle_lib):
     oracle_lib.code_some_shards(7, rows, [a, b, a], ref, 0, N)
     rsamd.codeSomeShards(rows, [a, b, a], 3, out, 1, 0, N)
     assert np.array_equal(out[0], ref[0])
+
+
+def test_threads_check_the_same_shards(gpu, oracle_lib):
+    """Several threads run isParityCorrect on the SAME pageable shards (every
+    slot an input).  Memory another thread's call has locked reads as pinned;
+    each call must still take its own reference on the registration (host.cpp
+    all_pinned / registry_holds), or the first call to finish would unlock the
+    pages under the others' kernels.  Then decodes of the same shards into
+    per-thread copies of the absent ones."""
+    import rsamd
+    rs = rsamd.ReedSolomon.create(4, 2)
+    rng = np.random.default_rng(33)
+    sh = [rng.integers(0, 256, N, dtype=np.uint8) for _ in range(4)] + [np.zeros(N, np.uint8) for _ in range(2)]
+    oracle_lib.Codec(4, 2).encode_parity(sh, 0, N)
+    errors = []
+
+    def work(seed):
+        try:
+            for _ in range(4):
+                assert rs.isParityCorrect(sh, 0, N)
+                mine = list(sh)
+                mine[seed % 4] = np.zeros(N, np.uint8)
+                present = [i != seed % 4 for i in range(6)]
+                rs.decodeMissing(mine, present, 0, N)
+                assert np.array_equal(mine[seed % 4], sh[seed % 4])
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    ts = [threading.Thread(target=work, args=(s,)) for s in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
