@@ -507,25 +507,40 @@ __global__ void __launch_bounds__(kWave) gf_masked_generic_kernel(MaskedArgs a) 
     u32x4 acc[MS];
 #pragma unroll
     for (int p = 0; p < MS; ++p) acc[p] = u32x4{0, 0, 0, 0};
-    u32x4 next = load_stream(sb + uint64_t(in_idx[0]) * a.shard_stride);
-    for (int i = 0; i < a.nin; ++i) {
-        const u32x4 x = next;
-        if (i + 1 < a.nin) next = load_stream(sb + uint64_t(in_idx[i + 1]) * a.shard_stride);
-        uint32_t T[MS][5];
+    // inputs in pipelined groups, as gf_vec_generic_kernel
+    constexpr int G = RSAMD_GEN_GROUP;
+    const int nin = a.nin;
+    u32x4 cur[G];
 #pragma unroll
-        for (int p = 0; p < MS; ++p)
+    for (int q = 0; q < G; ++q)
+        if (q < nin) cur[q] = load_stream(sb + uint64_t(in_idx[q]) * a.shard_stride);
+    for (int i0 = 0; i0 < nin; i0 += G) {
+        u32x4 nxt[G];
 #pragma unroll
-            for (int j = 0; j < 5; ++j) T[p][j] = tabs[(i * MS + p) * 5 + j];
+        for (int q = 0; q < G; ++q)
+            if (i0 + G + q < nin) nxt[q] = load_stream(sb + uint64_t(in_idx[i0 + G + q]) * a.shard_stride);
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const Sel s = selectors(x[w]);
+        for (int q = 0; q < G; ++q) {
+            if (i0 + q >= nin) break;
+            uint32_t T[MS][5];
 #pragma unroll
-            for (int p = 0; p < MS; ++p) {
-                uint32_t t0, t1, t2;
-                terms(T[p], s, t0, t1, t2);
-                acc[p][w] = xor3(acc[p][w], t0, t1) ^ t2;
+            for (int p = 0; p < MS; ++p)
+#pragma unroll
+                for (int j = 0; j < 5; ++j) T[p][j] = tabs[((i0 + q) * MS + p) * 5 + j];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const Sel s = selectors(cur[q][w]);
+#pragma unroll
+                for (int p = 0; p < MS; ++p) {
+                    uint32_t t0, t1, t2;
+                    terms(T[p], s, t0, t1, t2);
+                    acc[p][w] = xor3(acc[p][w], t0, t1) ^ t2;
+                }
             }
         }
+#pragma unroll
+        for (int q = 0; q < G; ++q)
+            if (i0 + G + q < nin) cur[q] = nxt[q];
     }
 #pragma unroll
     for (int p = 0; p < MS; ++p)
@@ -1285,9 +1300,14 @@ size_t vec_lds_pad(int k, int m, bool verify) {
 // at 12544 B; 4+2 x 1 MiB 0.80 -> 0.829 at 12544; 10+4 x 4 MiB with 4 erasures
 // 0.76-0.79 -> 0.80-0.806 at 10240.  (The copy kernel, two streams per wave,
 // is best uncapped: 0.851, and 0.78 at 10240.)
+// The runtime-k masked kernel (other k, called with k = 0 or the code's k)
+// takes 10240 since it loads in pipelined groups (tools/occ_sweep2.py --family
+// masked, profiles/r3/masked_gen_r3s2t.txt; granule batches, random erasures
+// per stripe, one-input-ahead build uncapped -> groups of 4 at 10240): 6+3
+// 0.77-0.78 -> 0.833, 8+4 0.72 -> 0.72-0.725, 17+3 0.71-0.75 -> 0.73.
 size_t masked_lds_pad(int k, int ms) {
     (void)ms;
-    return tuning_size("RSAMD_MASKED_LDS_PAD", k == 4 ? 12544 : k == 10 ? 10240 : 0);
+    return tuning_size("RSAMD_MASKED_LDS_PAD", k == 4 ? 12544 : 10240);
 }
 
 template <int K, int M>

@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--lib", default=os.path.join(ROOT, "build/ab/tuning/librsamd.so"))
     ap.add_argument("--pads", default="0,10240,11520,12544,13568,14848,16384,20480")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--shapes", default="", help="masked family: comma-separated shape names")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -59,9 +60,17 @@ def main():
     pads = [int(x) for x in a.pads.split(",")]
     st = torch.cuda.current_stream()
     if a.family == "masked":
-        for name, k, m, S, B, nerase in [("cfg4_granule_random", 4, 2, 4096, 1 << 20, None),
-                                         ("10p4_granule_4random", 10, 4, 4 << 20, 128, 4),
-                                         ("4p2_1MiB_granule_random", 4, 2, 1 << 20, 4096, None)]:
+        shapes = [("cfg4_granule_random", 4, 2, 4096, 1 << 20, None),
+                  ("10p4_granule_4random", 10, 4, 4 << 20, 128, 4),
+                  ("4p2_1MiB_granule_random", 4, 2, 1 << 20, 4096, None),
+                  # other codes (the runtime-k masked kernel)
+                  ("6p3_granule_3random", 6, 3, 1 << 20, 2048, 3),
+                  ("8p4_granule_2random", 8, 4, 1 << 20, 1024, 2),
+                  ("17p3_granule_3random", 17, 3, 1 << 20, 512, 3)]
+        want = set(a.shapes.split(",")) if a.shapes else None
+        for name, k, m, S, B, nerase in shapes:
+            if want and name not in want:
+                continue
             T = k + m
             rs = rsamd.ReedSolomon.create(k, m)
             lay = rdev.GranuleLayout.make(B, T, S)
