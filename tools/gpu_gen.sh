@@ -1,5 +1,6 @@
 # Runtime-k kernel: input group size (RSAMD_GEN_GROUP builds) x occupancy
 # cap on the codes outside the compiled shapes; builds alternated.
+# Builds (in csrc/): for G in 1 2 4 8: make TUNING=1 OUT=../../build/ab/gen$G OBJ=../../build/ab/gen$G/obj KDEFS=-DRSAMD_GEN_GROUP=$G
 set -o pipefail
 tag=${1:-gen}
 mkdir -p gpurun_out

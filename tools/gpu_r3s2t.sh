@@ -1,6 +1,8 @@
 # Runtime-k masked kernel (per-stripe patterns, other codes): group size
 # (gen1 = one input ahead, tuning = groups of 4) x occupancy cap, builds
 # alternated; then the GPU tests that use it.
+# Builds (in csrc/): make TUNING=1 OUT=../../build/ab/tuning OBJ=../../build/ab/tuning/obj, and the same
+# with OUT/OBJ under build/ab/gen1 and KDEFS=-DRSAMD_GEN_GROUP=1.
 set -o pipefail
 tag=${1:-r3s2t}
 mkdir -p gpurun_out
