@@ -1283,6 +1283,11 @@ size_t vec_lds_pad(int k, int m, bool verify) {
         if (verify) return 0;
         return m >= 4 ? 10240 : m == 3 ? 13568 : m == 2 ? 16384 : 20480;
     }
+    // 17+m (the upstream library's benchmark code, compiled like 10+m): 17+3
+    // granule encode / decode {0,1,2} 0.777 / 0.770 at 16384 B against the
+    // runtime-k kernel's 0.760-0.766 / 0.748-0.765 at its best cap (tools/gpu_k17.sh,
+    // profiles/r3/k17_r3s2v.txt, k17_r3s2w.txt).
+    if (k == 17) return verify ? 0 : 16384;
     // The runtime-k kernel (every other k; called with k = 0), since it loads
     // its inputs in pipelined groups of 4.  Granule batches, one pool per
     // shape, builds alternated (tools/gpu_gen.sh, profiles/r3/gen_r3s2q.txt),
@@ -1330,13 +1335,14 @@ hipError_t launch_vec_generic_t(VecArgs a, Mode mode, hipStream_t s) {
 }
 
 // Compile-time shapes for the BASELINE geometries (4+2 and 10+4 with any
-// erasure count); every other shape runs the runtime-k kernel, capped and in
-// plain order like them (block_order: capped).
+// erasure count) and 17+m (up to 3 outputs); every other shape runs the
+// runtime-k kernel, capped and in plain order like them (block_order: capped).
 hipError_t dispatch_vec(VecArgs a, int nout, Mode mode, hipStream_t s) {
 #define RSAMD_CASE(K, M) \
     if (a.nin == K && nout == M) return launch_vec_t<K, M>(a, mode, s);
     RSAMD_CASE(4, 1) RSAMD_CASE(4, 2) RSAMD_CASE(4, 3) RSAMD_CASE(4, 4)
     RSAMD_CASE(10, 1) RSAMD_CASE(10, 2) RSAMD_CASE(10, 3) RSAMD_CASE(10, 4)
+    RSAMD_CASE(17, 1) RSAMD_CASE(17, 2) RSAMD_CASE(17, 3)
 #undef RSAMD_CASE
     switch (nout) {
     case 1: return launch_vec_generic_t<1>(a, mode, s);
