@@ -1288,6 +1288,12 @@ size_t vec_lds_pad(int k, int m, bool verify) {
     // runtime-k kernel's 0.760-0.766 / 0.748-0.765 at its best cap (tools/gpu_k17.sh,
     // profiles/r3/k17_r3s2v.txt, k17_r3s2w.txt).
     if (k == 17) return verify ? 0 : 16384;
+    // 6+m and 8+m, compiled since the end of round 3 (tools/gpu_k68.sh,
+    // profiles/r3/k68_r3s2w2.txt; runtime-k kernel at its best cap -> compiled):
+    // 8+4 encode 0.805 -> 0.827 (10240 B), decode {0} 0.758 -> 0.777 (16384);
+    // 6+3 encode 0.834 -> 0.855, decode {0,1} 0.848 -> 0.869 (14848).
+    if (k == 8) return verify ? 0 : m == 1 ? 16384 : m == 2 ? 12544 : 10240;
+    if (k == 6) return verify ? 0 : m == 1 ? 16384 : 14848;
     // The runtime-k kernel (every other k; called with k = 0), since it loads
     // its inputs in pipelined groups of 4.  Granule batches, one pool per
     // shape, builds alternated (tools/gpu_gen.sh, profiles/r3/gen_r3s2q.txt),
@@ -1335,14 +1341,17 @@ hipError_t launch_vec_generic_t(VecArgs a, Mode mode, hipStream_t s) {
 }
 
 // Compile-time shapes for the BASELINE geometries (4+2 and 10+4 with any
-// erasure count) and 17+m (up to 3 outputs); every other shape runs the
-// runtime-k kernel, capped and in plain order like them (block_order: capped).
+// erasure count), and for 6+m, 8+m and 17+m (the common wider codes and the
+// upstream library's benchmark code); every other shape runs the runtime-k
+// kernel, capped and in plain order like them (block_order: capped).
 hipError_t dispatch_vec(VecArgs a, int nout, Mode mode, hipStream_t s) {
 #define RSAMD_CASE(K, M) \
     if (a.nin == K && nout == M) return launch_vec_t<K, M>(a, mode, s);
     RSAMD_CASE(4, 1) RSAMD_CASE(4, 2) RSAMD_CASE(4, 3) RSAMD_CASE(4, 4)
     RSAMD_CASE(10, 1) RSAMD_CASE(10, 2) RSAMD_CASE(10, 3) RSAMD_CASE(10, 4)
     RSAMD_CASE(17, 1) RSAMD_CASE(17, 2) RSAMD_CASE(17, 3)
+    RSAMD_CASE(6, 1) RSAMD_CASE(6, 2) RSAMD_CASE(6, 3)
+    RSAMD_CASE(8, 1) RSAMD_CASE(8, 2) RSAMD_CASE(8, 3) RSAMD_CASE(8, 4)
 #undef RSAMD_CASE
     switch (nout) {
     case 1: return launch_vec_generic_t<1>(a, mode, s);

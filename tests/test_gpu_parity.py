@@ -485,3 +485,66 @@ def test_extreme_shard_counts(gpu, oracle_lib, k, m):
     device.decode_masked(rs, dev.data_ptr(), pats, lay)
     torch.cuda.synchronize()
     assert np.array_equal(dev.cpu().numpy().reshape(2, T, -1)[:, :, :S], host[:, :, :S])
+
+
+@pytest.mark.parametrize("k,m", [(6, 3), (8, 4), (17, 3)])
+def test_compiled_wide_shapes(gpu, oracle_lib, k, m):
+    """The compiled 6+m, 8+m and 17+m kernels (kernels.hip dispatch_vec), packed
+    and granule batches: encode against the oracle, then every erasure count
+    up to m (1 .. m outputs) decoded and compared, and verify clean."""
+    torch = _torch()
+    import rsamd
+    from rsamd import device
+    from rsamd.device import StripeLayout
+    rs = rsamd.ReedSolomon.create(k, m)
+    S, B = 64 << 10, 6
+    for lay in (StripeLayout.packed(B, k + m, S), device.GranuleLayout.make(B, k + m, S, 16 << 10)):
+        buf = torch.zeros(lay.nbytes, dtype=torch.uint8, device="cuda:0")
+        st = torch.cuda.current_stream()
+        rng = np.random.default_rng(k * 10 + m)
+        data = rng.integers(0, 256, (B, k, S), dtype=np.uint8)
+        for t in range(B):
+            for i in range(k):
+                if isinstance(lay, StripeLayout):
+                    off = t * lay.stripe_stride + i * lay.shard_stride
+                    buf[off:off + S] = torch.from_numpy(data[t, i]).to("cuda:0")
+                else:
+                    device.copy_shard(lay, buf.data_ptr(), t, i, data[t, i].ctypes.data, True, st)
+        torch.cuda.synchronize()
+        device.encode(rs, buf.data_ptr(), lay, st)
+
+        def shard(t, i):
+            if isinstance(lay, StripeLayout):
+                off = t * lay.stripe_stride + i * lay.shard_stride
+                return buf[off:off + S].cpu().numpy()
+            out = np.zeros(S, np.uint8)
+            device.copy_shard(lay, buf.data_ptr(), t, i, out.ctypes.data, False, st)
+            torch.cuda.synchronize()
+            return out
+
+        oc = oracle_lib.Codec(k, m)
+        full = []
+        for t in range(B):
+            ref = [data[t, i].copy() for i in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
+            oc.encode_parity(ref, 0, S)
+            full.append(ref)
+            for p in range(m):
+                assert np.array_equal(shard(t, k + p), ref[k + p]), (t, p)
+        for e in range(1, m + 1):
+            miss = sorted(rng.choice(k + m, e, replace=False).tolist())
+            zero = np.zeros(S, np.uint8)
+            for t in range(B):
+                for j in miss:
+                    if isinstance(lay, StripeLayout):
+                        off = t * lay.stripe_stride + j * lay.shard_stride
+                        buf[off:off + S] = 0
+                    else:
+                        device.copy_shard(lay, buf.data_ptr(), t, j, zero.ctypes.data, True, st)
+            torch.cuda.synchronize()
+            device.decode(rs, buf.data_ptr(), [i not in miss for i in range(k + m)], lay, st)
+            for t in range(B):
+                for j in miss:
+                    assert np.array_equal(shard(t, j), full[t][j]), (e, miss, t, j)
+        flag = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+        device.verify(rs, buf.data_ptr(), lay, flag.data_ptr(), st)
+        assert int(flag.item()) == 0
