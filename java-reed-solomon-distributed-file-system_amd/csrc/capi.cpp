@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/rs_amd.h"
+#include "bounds.hpp"
 #include "codec.hpp"
 #include "copy_pool.hpp"
 #include "gf256.hpp"
@@ -42,6 +43,16 @@ using rsamd::Geometry;
 using rsamd::Mode;
 using rsamd::Plan;
 using namespace rsamd::host;
+namespace bounds = rsamd::bounds;
+
+// Bounds-checking build (bounds.hpp): the bytes a stripe batch's arguments
+// describe -- stripe t's shard s at base + t * stripe_stride + s * shard_stride,
+// len bytes each.  A no-op in the product build.
+void allow_batch(const uint8_t *base, size_t n_stripes, size_t len, size_t shard_stride, size_t stripe_stride,
+                 int total) {
+    if (!base || n_stripes == 0 || len == 0 || total < 1) return;
+    bounds::allow(base, (n_stripes - 1) * stripe_stride + size_t(total - 1) * shard_stride + len);
+}
 
 // Direct path: the caller's page-locked shards coded in place across the link,
 // one launch_gf_direct per launch group on the context's stream (kernels.hip
@@ -113,6 +124,10 @@ int run_direct(ThreadCtx *ctx, const std::vector<DevPlan> &plans, const std::vec
             if (reinterpret_cast<uintptr_t>(d.in[i]) % 8 != r8) return RS_OK;
         for (int q = 0; q < d.nout; ++q)
             if (reinterpret_cast<uintptr_t>(d.out[q]) % 8 != r8) return RS_OK;
+    }
+    for (const rsamd::DirectPlan &d : dp) {
+        for (int i = 0; i < d.nin; ++i) bounds::allow(d.in[i], count);
+        for (int q = 0; q < d.nout; ++q) bounds::allow(d.out[q], count);
     }
     for (size_t g = 0; g < dp.size(); ++g) {
         const hipError_t e = rsamd::launch_gf_direct(dp[g], count, mode, ctx->flag, ctx->stream);
@@ -302,6 +317,8 @@ int file_encode_dev(const Codec &c, const uint8_t *file, size_t file_len, size_t
     g.S = size_t(S);
     g.shards = shards;
     g.shard_stride = stride;
+    bounds::allow(file, file_len);
+    allow_batch(shards, 1, size_t(S), stride, 0, c.total());
     std::vector<DevPlan> plans;
     RS_HIP(c.encode_plan().device_plans(&plans));
     Geometry sg{shards, 1, 0, size_t(S), stride, stride * size_t(c.total())};
@@ -336,6 +353,8 @@ int file_decode_dev(const Codec &c, uint8_t *shards, size_t S, size_t stride, co
     g.S = S;
     g.shards = shards;
     g.shard_stride = stride;
+    bounds::allow(file_out, file_size);
+    allow_batch(shards, 1, S, stride, 0, c.total());
     std::shared_ptr<const Plan> plan;
     int n_missing_data = 0;
     for (int i = 0; i < c.k(); ++i) n_missing_data += present[i] ? 0 : 1;
@@ -415,6 +434,8 @@ int file_encode_direct(const Codec &c, const uint8_t *file, size_t file_len, siz
         d.tabs = plans[0].tabs;
     }
     if (!rsamd::file_direct_ok(d, true)) return RS_OK;
+    bounds::allow(d.file, file_len);
+    for (int i = 0; i < c.total(); ++i) bounds::allow(d.out[i], S);
     RS_HIP(rsamd::launch_file_encode_direct(d, ctx->stream));
     *taken = true;
     RS_HIP(hipStreamSynchronize(ctx->stream));
@@ -450,6 +471,9 @@ int file_decode_direct(const Codec &c, uint8_t *const *shards, const uint8_t *pr
     }
     if (file_size && !(d.file_out = host_dev_addr(file_out))) return RS_OK;
     if (!rsamd::file_direct_ok(d, false)) return RS_OK;
+    bounds::allow(d.file_out, file_size);
+    for (int i = 0; i < d.k; ++i) bounds::allow(d.in[i], cols);
+    for (int q = 0; q < d.nout; ++q) bounds::allow(d.out[q], cols);
     RS_HIP(rsamd::launch_file_decode_direct(d, ctx->stream));
     *taken = true;
     RS_HIP(hipStreamSynchronize(ctx->stream));
@@ -801,6 +825,7 @@ int rs_device_count(void) {
 
 int rs_encode_parity(const rs_codec *codec, uint8_t *const *shards, int nshards, const int64_t *shard_lens,
                      int32_t offset, int32_t byte_count) {
+    bounds::Scope bs;
     const Codec *c = impl(codec);
     if (!c) return fail(RS_E_INVALID, "codec is NULL");
     int rc = check_buffers_and_sizes(*c, shards, nshards, shard_lens, offset, byte_count);
@@ -812,6 +837,7 @@ int rs_encode_parity(const rs_codec *codec, uint8_t *const *shards, int nshards,
 
 int rs_decode_missing(const rs_codec *codec, uint8_t *const *shards, int nshards, const int64_t *shard_lens,
                       const uint8_t *present, int32_t offset, int32_t byte_count) {
+    bounds::Scope bs;
     const Codec *c = impl(codec);
     if (!c) return fail(RS_E_INVALID, "codec is NULL");
     int rc = check_buffers_and_sizes(*c, shards, nshards, shard_lens, offset, byte_count);
@@ -832,6 +858,7 @@ int rs_decode_missing(const rs_codec *codec, uint8_t *const *shards, int nshards
 int rs_is_parity_correct(const rs_codec *codec, uint8_t *const *shards, int nshards, const int64_t *shard_lens,
                          int32_t first_byte, int32_t byte_count, const uint8_t *temp, int64_t temp_len,
                          int *result) {
+    bounds::Scope bs;
     const Codec *c = impl(codec);
     if (!c || !result) return fail(RS_E_INVALID, "codec and result must not be NULL");
     int rc = check_buffers_and_sizes(*c, shards, nshards, shard_lens, first_byte, byte_count);
@@ -848,6 +875,7 @@ int rs_is_parity_correct(const rs_codec *codec, uint8_t *const *shards, int nsha
 
 int rs_code_some_shards(const uint8_t *const *matrix_rows, const uint8_t *const *inputs, int input_count,
                         uint8_t *const *outputs, int output_count, int32_t offset, int32_t byte_count) {
+    bounds::Scope bs;
     return code_rows(matrix_rows, inputs, input_count, outputs, output_count, offset, byte_count, Mode::Code,
                      nullptr);
 }
@@ -856,6 +884,7 @@ int rs_check_some_shards(const uint8_t *const *matrix_rows, const uint8_t *const
                          const uint8_t *const *to_check, int check_count, int32_t offset, int32_t byte_count,
                          int *result) {
     if (!result) return fail(RS_E_INVALID, "result must not be NULL");
+    bounds::Scope bs;
     return code_rows(matrix_rows, inputs, input_count, const_cast<uint8_t *const *>(to_check), check_count, offset,
                      byte_count, Mode::Verify, result);
 }
@@ -864,6 +893,8 @@ int rs_encode_batch_dev(const rs_codec *codec, uint8_t *dev_base, size_t n_strip
                         size_t shard_stride, size_t stripe_stride, void *stream) {
     const Codec *c = impl(codec);
     if (!c || (!dev_base && n_stripes && shard_len)) return fail(RS_E_INVALID, "NULL codec or device base");
+    bounds::Scope bs(stream);
+    allow_batch(dev_base, n_stripes, shard_len, shard_stride, stripe_stride, c->total());
     std::vector<DevPlan> plans;
     RS_HIP(c->encode_plan().device_plans(&plans));
     Geometry g{dev_base, n_stripes, 0, shard_len, shard_stride, stripe_stride, c->total()};
@@ -884,6 +915,8 @@ int rs_decode_batch_dev(const rs_codec *codec, uint8_t *dev_base, const uint8_t 
     std::shared_ptr<const Plan> plan;
     int rc = c->decode_plan(present, &plan);
     if (rc) return fail(rc, rc == RS_E_SINGULAR ? "Matrix is singular" : "Not enough shards present");
+    bounds::Scope bs(stream);
+    allow_batch(dev_base, n_stripes, shard_len, shard_stride, stripe_stride, c->total());
     std::vector<DevPlan> plans;
     RS_HIP(plan->device_plans(&plans));
     Geometry g{dev_base, n_stripes, 0, shard_len, shard_stride, stripe_stride, c->total()};
@@ -901,6 +934,8 @@ int rs_decode_batch_masked_dev(const rs_codec *codec, uint8_t *dev_base, const u
     if (!dev_base) return fail(RS_E_INVALID, "NULL device base");
     if (n_stripes > size_t(INT32_MAX)) return fail(RS_E_INVALID, "too many stripes");
     const Geometry geo{dev_base, n_stripes, 0, shard_len, shard_stride, stripe_stride, c->total()};
+    bounds::Scope bs(stream);
+    allow_batch(dev_base, n_stripes, shard_len, shard_stride, stripe_stride, c->total());
     return decode_masked_dev(*c, present, n_stripes, geo, 0, static_cast<hipStream_t>(stream));
 }
 
@@ -915,6 +950,8 @@ int rs_decode_granule_masked_dev(const rs_codec *codec, uint8_t *dev_base, const
     Geometry geo;
     int rc = granule_view(c->total(), dev_base, n_stripes, shard_len, granule, &geo);
     if (rc) return rc;
+    bounds::Scope bs(stream);
+    bounds::allow(dev_base, n_stripes * shard_len * size_t(c->total()));
     return decode_masked_dev(*c, present, n_stripes, geo, shard_len, static_cast<hipStream_t>(stream));
 }
 
@@ -927,6 +964,10 @@ int rs_decode_batch_masked_bits_dev(const rs_codec *codec, uint8_t *dev_base, co
     if (!dev_base) return fail(RS_E_INVALID, "NULL device buffer");
     if (n_stripes > size_t(INT32_MAX)) return fail(RS_E_INVALID, "too many stripes");
     const Geometry geo{dev_base, n_stripes, 0, shard_len, shard_stride, stripe_stride, c->total()};
+    bounds::Scope bs(stream);
+    allow_batch(dev_base, n_stripes, shard_len, shard_stride, stripe_stride, c->total());
+    bounds::allow(dev_present_bits, n_stripes * sizeof(uint32_t));
+    bounds::allow(dev_bad_count, sizeof(int32_t));
     return decode_masked_bits_dev(*c, dev_present_bits, geo, 0, dev_bad_count, static_cast<hipStream_t>(stream));
 }
 
@@ -941,6 +982,10 @@ int rs_decode_granule_masked_bits_dev(const rs_codec *codec, uint8_t *dev_base, 
     Geometry geo;
     int rc = granule_view(c->total(), dev_base, n_stripes, shard_len, granule, &geo);
     if (rc) return rc;
+    bounds::Scope bs(stream);
+    bounds::allow(dev_base, n_stripes * shard_len * size_t(c->total()));
+    bounds::allow(dev_present_bits, n_stripes * sizeof(uint32_t));
+    bounds::allow(dev_bad_count, sizeof(int32_t));
     return decode_masked_bits_dev(*c, dev_present_bits, geo, shard_len, dev_bad_count,
                                   static_cast<hipStream_t>(stream));
 }
@@ -950,6 +995,9 @@ int rs_verify_batch_dev(const rs_codec *codec, const uint8_t *dev_base, size_t n
     const Codec *c = impl(codec);
     if (!c || !dev_mismatch || (!dev_base && n_stripes && shard_len))
         return fail(RS_E_INVALID, "NULL codec, device base or mismatch flag");
+    bounds::Scope bs(stream);
+    allow_batch(dev_base, n_stripes, shard_len, shard_stride, stripe_stride, c->total());
+    bounds::allow(dev_mismatch, sizeof(int));
     std::vector<DevPlan> plans;
     RS_HIP(c->verify_plan().device_plans(&plans));
     Geometry g{const_cast<uint8_t *>(dev_base), n_stripes, 0, shard_len, shard_stride, stripe_stride};
@@ -968,6 +1016,7 @@ int rs_file_encode_dev(const rs_codec *codec, const uint8_t *dev_file, size_t fi
                        uint8_t *dev_shards, size_t shard_stride, void *stream) {
     const Codec *c = impl(codec);
     if (!c) return fail(RS_E_INVALID, "codec is NULL");
+    bounds::Scope bs(stream);
     return file_encode_dev(*c, dev_file, file_len, block, dev_shards, shard_stride, static_cast<hipStream_t>(stream));
 }
 
@@ -976,12 +1025,14 @@ int rs_file_decode_dev(const rs_codec *codec, uint8_t *dev_shards, size_t shard_
                        int write_missing, void *stream) {
     const Codec *c = impl(codec);
     if (!c) return fail(RS_E_INVALID, "codec is NULL");
+    bounds::Scope bs(stream);
     return file_decode_dev(*c, dev_shards, shard_len, shard_stride, present, block, dev_file_out, file_size,
                            write_missing != 0, static_cast<hipStream_t>(stream));
 }
 
 int rs_file_encode(const rs_codec *codec, const uint8_t *file, int64_t file_len, int32_t block,
                    uint8_t *const *shards_out, int nshards, const int64_t *shard_lens) {
+    bounds::Scope bs;
     const Codec *c = impl(codec);
     if (!c) return fail(RS_E_INVALID, "codec is NULL");
     int64_t padded = 0, S = 0;
@@ -1033,6 +1084,7 @@ int rs_file_encode(const rs_codec *codec, const uint8_t *file, int64_t file_len,
 int rs_file_decode(const rs_codec *codec, uint8_t *const *shards, int nshards, const int64_t *shard_lens,
                    const uint8_t *present, int32_t byte_cnt_in_shard, int32_t block, uint8_t *file_out,
                    int64_t file_size) {
+    bounds::Scope bs;
     const Codec *c = impl(codec);
     if (!c) return fail(RS_E_INVALID, "codec is NULL");
     if (nshards == c->total() && shards && shard_lens && present && byte_cnt_in_shard == shard_lens[0] &&
@@ -1072,6 +1124,8 @@ int rs_fill_synthetic_dev(uint8_t *dev_base, int data_shards, size_t n_stripes, 
                           size_t stripe_stride, uint64_t seed, uint64_t stripe0, void *stream) {
     if (!dev_base || data_shards < 1) return fail(RS_E_INVALID, "NULL device base or data_shards < 1");
     if (shard_len % 8) return fail(RS_E_INVALID, "shard_len must be a multiple of 8");
+    bounds::Scope bs(stream);
+    allow_batch(dev_base, n_stripes, shard_len, shard_stride, stripe_stride, data_shards);
     RS_HIP(rsamd::launch_fill_synthetic(dev_base, data_shards, n_stripes, shard_len, shard_stride, stripe_stride,
                                         seed, stripe0, static_cast<hipStream_t>(stream)));
     return RS_OK;
@@ -1140,8 +1194,27 @@ int rs_granule_copy_shard(uint8_t *dev_base, int total_shards, size_t n_stripes,
 
 int rs_copy_dev(uint8_t *dst, const uint8_t *src, size_t n, void *stream) {
     if ((!dst || !src) && n) return fail(RS_E_INVALID, "NULL pointer");
+    bounds::Scope bs(stream);
+    bounds::allow(dst, n);
+    bounds::allow(src, n);
     RS_HIP(rsamd::launch_copy(dst, src, n, static_cast<hipStream_t>(stream)));
     return RS_OK;
 }
 
 }  // extern "C"
+
+#if RSAMD_BOUNDS
+// Bounds-checking build only (bounds.hpp): the accesses outside every declared
+// range since the last call -- count, the first one's address, bytes and site
+// (translation unit * 100000 + line; 1 = kernels.hip, 2 = layout.hip).
+extern "C" RS_API int rs_bounds_report(unsigned long long *count, unsigned long long *addr, unsigned long long *len,
+                                unsigned *where) {
+    rsamd::BoundsReport r;
+    rsamd::bounds::report(&r);
+    if (count) *count = r.count;
+    if (addr) *addr = r.addr;
+    if (len) *len = r.len;
+    if (where) *where = r.where;
+    return RS_OK;
+}
+#endif

@@ -6,6 +6,7 @@
 #include <cstring>
 
 #include "../../include/rs_amd.h"
+#include "bounds.hpp"
 
 namespace rsamd {
 
@@ -161,6 +162,7 @@ hipError_t Plan::device_plans(std::vector<DevPlan> *out) const {
         }
         it = dev_.emplace(dev, buf).first;
     }
+    bounds::allow(it->second, total ? total : 256);
     out->clear();
     for (int g = 0; g < groups(); ++g) {
         const int nout = std::min<int>(kMaxOut, int(out_idx_.size()) - g * kMaxOut);
@@ -211,6 +213,7 @@ hipError_t Plan::device_file_plan(int k, FileDecodePlan *out) const {
         it = dev_file_.emplace(dev, buf).first;
     }
     const uint8_t *b = static_cast<const uint8_t *>(it->second);
+    bounds::allow(b, tabs_bytes + 2 * size_t(k) * sizeof(int32_t));
     out->tabs = reinterpret_cast<const uint32_t *>(b);
     out->in_idx = reinterpret_cast<const int32_t *>(b + tabs_bytes);
     out->dsrc = reinterpret_cast<const int32_t *>(b + tabs_bytes + size_t(k) * sizeof(int32_t));
@@ -341,6 +344,7 @@ int Codec::pattern_tables(PatternTables *out, std::string *err) const {
     auto it = patterns_.find(dev);
     if (it != patterns_.end()) {
         *out = it->second;
+        bounds::allow(out->records, out->bytes);
         return RS_OK;
     }
     const int T = total();
@@ -399,6 +403,8 @@ int Codec::pattern_tables(PatternTables *out, std::string *err) const {
     t.host_mask_table = host_mask_table_.data();
     t.records = static_cast<const uint8_t *>(buf);
     t.mask_table = reinterpret_cast<const int32_t *>(static_cast<const uint8_t *>(buf) + rec_bytes);
+    t.bytes = img.size();
+    bounds::allow(t.records, t.bytes);
     patterns_.emplace(dev, t);
     *out = t;
     return RS_OK;

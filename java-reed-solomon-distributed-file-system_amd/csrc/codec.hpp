@@ -84,6 +84,7 @@ struct PatternTables {
     const int32_t *mask_table = nullptr;       // [2^total]: pattern id, or -1 (not decodable)
     const int32_t *host_mask_table = nullptr;  // the same ids in host memory
     int groups = 0, mslots = 0;
+    size_t bytes = 0;  // the device allocation: records, then mask_table
 };
 constexpr int kMaxPatternBits = 20;        // k + m for a bitmask table (4 MiB of ids)
 constexpr size_t kMaxPatterns = 1u << 16;  // decodable patterns in one table

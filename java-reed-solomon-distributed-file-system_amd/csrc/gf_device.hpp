@@ -6,6 +6,8 @@
 
 #include <cstdint>
 
+#include "bounds.hpp"
+
 namespace rsamd {
 namespace dev {
 
@@ -66,7 +68,7 @@ __device__ __forceinline__ uint32_t dot_dword(const uint32_t (&T)[N][5], const S
 }
 
 __device__ __forceinline__ void flag_mismatch(int *mismatch) {
-    __hip_atomic_fetch_or(mismatch, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_or(RSAMD_G(mismatch, 4), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Early-exit hint for verify launches: a plain load, possibly stale (a block
@@ -74,7 +76,7 @@ __device__ __forceinline__ void flag_mismatch(int *mismatch) {
 // the compiler models an atomic load as a possible clobber of every later
 // load, which turns the scalar table loads into per-lane vector loads
 // (252 VGPRs and 2 waves per SIMD for the 10+4 verify kernel).
-__device__ __forceinline__ bool mismatch_seen(const int *mismatch) { return *mismatch != 0; }
+__device__ __forceinline__ bool mismatch_seen(const int *mismatch) { return *RSAMD_G(mismatch, 4) != 0; }
 
 }  // namespace dev
 }  // namespace rsamd

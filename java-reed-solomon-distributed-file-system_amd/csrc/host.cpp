@@ -14,6 +14,7 @@
 #include <thread>
 
 #include "../../include/rs_amd.h"
+#include "bounds.hpp"
 #include "codec.hpp"
 #include "copy_pool.hpp"
 #include "tuning.hpp"
@@ -132,6 +133,7 @@ int thread_ctx(ThreadCtx **out) {
         it = t_ctx.m.emplace(dev, c).first;
     }
     *out = it->second;
+    bounds::allow(it->second->flag, 256);
     return RS_OK;
 }
 
@@ -175,12 +177,16 @@ void release_all(std::map<int, ThreadCtx *> &ctx) {
 void release_thread_contexts() { release_all(t_ctx.m); }
 
 int grow(uint8_t **buf, size_t *cap, size_t want) {
-    if (*cap >= want) return RS_OK;
+    if (*cap >= want) {
+        bounds::allow(*buf, *cap);
+        return RS_OK;
+    }
     if (*buf) RS_HIP(hipFree(*buf));
     *buf = nullptr;
     *cap = 0;
     RS_HIP(hipMalloc(reinterpret_cast<void **>(buf), want));
     *cap = want;
+    bounds::allow(*buf, *cap);
     return RS_OK;
 }
 
@@ -414,6 +420,7 @@ int run_zero_copy(ThreadCtx *ctx, size_t buf_bytes, const ChunkIo &io, const Chu
         ctx->zc_cap = buf_bytes;
         RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->zc_dev), ctx->zc, 0));
     }
+    bounds::allow(ctx->zc_dev, ctx->zc_cap);
     std::vector<Xfer> in, out;
     io(0, &in, &out);
     // Host copies on the calling thread; the copy pool only above 2 MiB (its
@@ -525,4 +532,114 @@ int run_chunks_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinn
 }  // namespace
 
 }  // namespace host
+
+#if RSAMD_BOUNDS
+// ---------------------------------------------------------------------------
+// The bounds-checking build's host half (bounds.hpp): one process-wide table,
+// set by the outermost Scope of a call and widened by allow(), uploaded to
+// both translation units' device copies.
+// ---------------------------------------------------------------------------
+namespace bounds {
+namespace {
+std::recursive_mutex g_mu;
+thread_local int t_depth = 0;
+thread_local bool t_passive = false;  // inside a stream capture: no checking
+BoundsTable g_table;
+BoundsReport g_seen;  // accumulated over calls until rs_bounds_report
+
+void put(const BoundsTable &t) {
+    (void)bounds_put_kernels(t);
+    (void)bounds_put_layout(t);
+}
+
+void take() {
+    for (auto fn : {bounds_take_kernels, bounds_take_layout}) {
+        BoundsReport r;
+        if (fn(&r) != hipSuccess || r.count == 0) continue;
+        if (g_seen.count == 0) {
+            g_seen.addr = r.addr;
+            g_seen.len = r.len;
+            g_seen.where = r.where;
+        }
+        g_seen.count += r.count;
+    }
+}
+}  // namespace
+
+Scope::Scope(const void *stream) {
+    g_mu.lock();
+    if (t_depth++ > 0) return;
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    t_passive = stream && hipStreamIsCapturing(static_cast<hipStream_t>(const_cast<void *>(stream)), &st) == hipSuccess &&
+                st != hipStreamCaptureStatusNone;
+    if (t_passive) return;
+    (void)hipDeviceSynchronize();
+    g_table = BoundsTable{};
+    g_table.n = 0;
+    put(g_table);
+}
+
+Scope::~Scope() {
+    if (--t_depth == 0 && !t_passive) {
+        (void)hipDeviceSynchronize();
+        take();
+        g_table = BoundsTable{};  // outside a call: everything allowed
+        put(g_table);
+    }
+    g_mu.unlock();
+}
+
+// A host-side finding (a declared range not inside a live allocation).
+void note(uint64_t addr, uint64_t len, unsigned where) {
+    if (g_seen.count++ == 0) {
+        g_seen.addr = addr;
+        g_seen.len = len;
+        g_seen.where = where;
+    }
+}
+
+void allow(const void *p, size_t n, bool check_alloc) {
+    if (!p || n == 0) return;
+    std::lock_guard<std::recursive_mutex> lock(g_mu);
+    if (t_depth == 0 || t_passive) return;
+    if (check_alloc) {
+        hipPointerAttribute_t attr;
+        if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+            (void)hipGetLastError();
+            note(reinterpret_cast<uint64_t>(p), n, 900001);  // not in any live allocation
+        } else if (attr.type == hipMemoryTypeDevice) {
+            hipDeviceptr_t base = nullptr;
+            size_t size = 0;
+            if (hipMemGetAddressRange(&base, &size, const_cast<void *>(p)) != hipSuccess) {
+                (void)hipGetLastError();
+                note(reinterpret_cast<uint64_t>(p), n, 900002);
+            } else if (static_cast<const uint8_t *>(p) + n > static_cast<const uint8_t *>(base) + size) {
+                note(reinterpret_cast<uint64_t>(p), n, 900003);  // runs past its allocation:
+                n = size_t(static_cast<const uint8_t *>(base) + size - static_cast<const uint8_t *>(p));  // kernels get the part inside
+            }
+        }
+    }
+    if (g_table.n == kBoundsAll) return;
+    if (g_table.n == kBoundsMax) {  // table full: stop checking for the rest of the call
+        g_table.n = kBoundsAll;
+        put(g_table);
+        return;
+    }
+    const uint64_t lo = reinterpret_cast<uint64_t>(p);
+    for (uint32_t i = 0; i < g_table.n; ++i)
+        if (g_table.lo[i] == lo && g_table.hi[i] == lo + n) return;
+    g_table.lo[g_table.n] = lo;
+    g_table.hi[g_table.n] = lo + n;
+    ++g_table.n;
+    put(g_table);  // widens the table: kernels already running see a superset
+}
+
+void report(BoundsReport *out) {
+    std::lock_guard<std::recursive_mutex> lock(g_mu);
+    *out = g_seen;
+    g_seen = BoundsReport{};
+}
+}  // namespace bounds
+#endif
+
 }  // namespace rsamd

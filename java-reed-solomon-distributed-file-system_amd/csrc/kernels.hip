@@ -28,6 +28,9 @@
 //    touches, so a CU holds 11-16 of these waves instead of 32 (vec_lds_pad,
 //    masked_lds_pad), and capped launches run in plain block order
 //    (block_order): 4+2 encode 0.836 -> 0.874 of HBM peak.
+//  * Every global access goes through RSAMD_G (bounds.hpp): the identity in
+//    the product, a range check in the bounds-checking build.
+#define RSAMD_TU_ID 1
 #include "kernels.hpp"
 
 #include <algorithm>
@@ -106,7 +109,8 @@ struct ByteArgs {
 #ifndef RSAMD_STORE_NT
 #define RSAMD_STORE_NT 1  // A/B builds: 0 = plain stores
 #endif
-__device__ __forceinline__ u32x4 load_stream(const uint8_t *p) {
+__device__ __forceinline__ u32x4 load_stream(const uint8_t *p, uint32_t line = __builtin_LINE()) {
+    p = RSAMD_GL(p, 16, line);
     if (!RSAMD_LOAD_NT) return *reinterpret_cast<const u32x4 *>(p);
     return __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
 }
@@ -118,7 +122,8 @@ __device__ __forceinline__ u32x4 load_stream(const uint8_t *p) {
 #ifndef RSAMD_STORE_SC1
 #define RSAMD_STORE_SC1 0
 #endif
-__device__ __forceinline__ void store_stream(uint8_t *p, const u32x4 &v) {
+__device__ __forceinline__ void store_stream(uint8_t *p, const u32x4 &v, uint32_t line = __builtin_LINE()) {
+    p = RSAMD_GL(p, 16, line);
     if (RSAMD_STORE_SC1)
         asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
     else if (!RSAMD_STORE_NT)
@@ -128,12 +133,12 @@ __device__ __forceinline__ void store_stream(uint8_t *p, const u32x4 &v) {
 }
 
 template <bool VERIFY>
-__device__ __forceinline__ void emit(uint8_t *p, const u32x4 &v, int *mismatch) {
+__device__ __forceinline__ void emit(uint8_t *p, const u32x4 &v, int *mismatch, uint32_t line = __builtin_LINE()) {
     if (VERIFY) {
-        const u32x4 have = load_stream(p);
+        const u32x4 have = load_stream(p, line);
         if (have[0] != v[0] || have[1] != v[1] || have[2] != v[2] || have[3] != v[3]) flag_mismatch(mismatch);
     } else {
-        store_stream(p, v);
+        store_stream(p, v, line);
     }
 }
 
@@ -294,7 +299,9 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(RSAM
     const uint32_t v = chunk * uint32_t(kWave) + threadIdx.x;
     if (v >= a.nvec) return;
     uint8_t *sb = a.base + uint64_t(stripe) * a.stripe_stride + uint64_t(v) * 16;
-    RSAMD_CODE_VECTORS(K, M, a.tabs, a.in_idx, a.out_idx, a.shard_stride,
+    const uint32_t *tabs = RSAMD_G(a.tabs, K * M * 20);
+    const int32_t *in_idx = RSAMD_G(a.in_idx, K * 4), *out_idx = RSAMD_G(a.out_idx, M * 4);
+    RSAMD_CODE_VECTORS(K, M, tabs, in_idx, out_idx, a.shard_stride,
                        M == 1 ? RSAMD_VEC_AHEAD_M1 : M == 2 ? RSAMD_VEC_AHEAD_M2 : RSAMD_VEC_AHEAD)
     if (VERIFY) {  // as in gf_masked_kernel: keep the compares' inputs from being sunk
 #pragma unroll
@@ -324,21 +331,23 @@ __global__ void __launch_bounds__(kWave) gf_vec_generic_kernel(VecArgs a) {
     uint8_t *sb = a.base + uint64_t(stripe) * a.stripe_stride + uint64_t(v) * 16;
     constexpr int G = RSAMD_GEN_GROUP;
     const int nin = a.nin;
+    const uint32_t *tabs = RSAMD_G(a.tabs, nin * M * 20);
+    const int32_t *in_idx = RSAMD_G(a.in_idx, nin * 4), *out_idx = RSAMD_G(a.out_idx, M * 4);
     uint64_t out_off[M];
 #pragma unroll
-    for (int p = 0; p < M; ++p) out_off[p] = uint64_t(a.out_idx[p]) * a.shard_stride;
+    for (int p = 0; p < M; ++p) out_off[p] = uint64_t(out_idx[p]) * a.shard_stride;
     u32x4 acc[M];
 #pragma unroll
     for (int p = 0; p < M; ++p) acc[p] = u32x4{0, 0, 0, 0};
     u32x4 cur[G];
 #pragma unroll
     for (int q = 0; q < G; ++q)
-        if (q < nin) cur[q] = load_stream(sb + uint64_t(a.in_idx[q]) * a.shard_stride);
+        if (q < nin) cur[q] = load_stream(sb + uint64_t(in_idx[q]) * a.shard_stride);
     for (int i0 = 0; i0 < nin; i0 += G) {
         u32x4 nxt[G];
 #pragma unroll
         for (int q = 0; q < G; ++q)
-            if (i0 + G + q < nin) nxt[q] = load_stream(sb + uint64_t(a.in_idx[i0 + G + q]) * a.shard_stride);
+            if (i0 + G + q < nin) nxt[q] = load_stream(sb + uint64_t(in_idx[i0 + G + q]) * a.shard_stride);
 #pragma unroll
         for (int q = 0; q < G; ++q) {
             if (i0 + q >= nin) break;
@@ -346,7 +355,7 @@ __global__ void __launch_bounds__(kWave) gf_vec_generic_kernel(VecArgs a) {
 #pragma unroll
             for (int p = 0; p < M; ++p)
 #pragma unroll
-                for (int j = 0; j < 5; ++j) T[p][j] = a.tabs[((i0 + q) * M + p) * 5 + j];
+                for (int j = 0; j < 5; ++j) T[p][j] = tabs[((i0 + q) * M + p) * 5 + j];
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
                 const Sel s = selectors(cur[q][w]);
@@ -421,18 +430,18 @@ __device__ __forceinline__ uint32_t masked_pattern(const MaskedArgs &a, uint32_t
 __device__ __forceinline__ const uint8_t *masked_record(const uint8_t *records, uint64_t rec_stride,
                                                         const int32_t *plan_ids, const int32_t *mask_table,
                                                         int mask_bits, uint64_t t) {
-    int32_t id = plan_ids[t];
+    int32_t id = *RSAMD_G(plan_ids + t, 4);
     if (mask_table) {
         const uint32_t bits = uint32_t(id);
-        id = (bits >> mask_bits) ? -1 : mask_table[bits];
+        id = (bits >> mask_bits) ? -1 : *RSAMD_G(mask_table + bits, 4);
         if (id < 0) return nullptr;
     }
-    return records + uint64_t(id) * rec_stride;
+    return RSAMD_G(records + uint64_t(id) * rec_stride, rec_stride);
 }
 
 // One count per undecodable stripe: by the thread that owns its column 0.
 __device__ __forceinline__ void count_undecodable(int32_t *bad, bool col0) {
-    if (bad && col0) atomicAdd(bad, 1);
+    if (bad && col0) atomicAdd(RSAMD_G(bad, 4), 1);
 }
 
 // Register budget for 7 waves per SIMD (72 VGPRs).  At 10+4 the kernel needs
@@ -592,8 +601,8 @@ struct Vec8<4> {
 };
 
 template <int W>
-__device__ __forceinline__ typename Vec8<W>::T load8(const uint8_t *p) {
-    return __builtin_nontemporal_load(reinterpret_cast<const typename Vec8<W>::T *>(p));
+__device__ __forceinline__ typename Vec8<W>::T load8(const uint8_t *p, uint32_t line = __builtin_LINE()) {
+    return __builtin_nontemporal_load(reinterpret_cast<const typename Vec8<W>::T *>(RSAMD_GL(p, W * 4, line)));
 }
 
 // sb: the lane's vector in shard 0 of its stripe; tabs[nin][MS][5].  With
@@ -653,12 +662,12 @@ __device__ __forceinline__ void code8(uint8_t *sb, bool half, const uint32_t *ta
             for (int w = 0; w < W; ++w) diff |= have[w] != acc[p][w];
             if (diff) flag_mismatch(mismatch);
         } else if (W == 4 && half) {
-            __builtin_nontemporal_store(u32x2{acc[p][0], acc[p][1]}, reinterpret_cast<u32x2 *>(q));
+            __builtin_nontemporal_store(u32x2{acc[p][0], acc[p][1]}, reinterpret_cast<u32x2 *>(RSAMD_G(q, 8)));
         } else {
             V v;
 #pragma unroll
             for (int w = 0; w < W; ++w) v[w] = acc[p][w];
-            __builtin_nontemporal_store(v, reinterpret_cast<V *>(q));
+            __builtin_nontemporal_store(v, reinterpret_cast<V *>(RSAMD_G(q, W * 4)));
         }
     }
 }
@@ -708,8 +717,9 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(8, 8
     block_item(a.chunks, a.cdiv, a.rot, a.xcd_span, stripe, chunk);
     const uint32_t v = chunk * uint32_t(kWave) + threadIdx.x;
     if (v >= a.nvec) return;
-    code8_lane<RSAMD_VEC8_U16, K, M, VERIFY>(a.base + uint64_t(stripe) * a.stripe_stride, v, a8.nfull16, a.tabs, a.in_idx, a.out_idx,
-                             a.nin, M, a.shard_stride, a.mismatch);
+    code8_lane<RSAMD_VEC8_U16, K, M, VERIFY>(a.base + uint64_t(stripe) * a.stripe_stride, v, a8.nfull16,
+                                             RSAMD_G(a.tabs, a.nin * M * 20), RSAMD_G(a.in_idx, a.nin * 4),
+                                             RSAMD_G(a.out_idx, M * 4), a.nin, M, a.shard_stride, a.mismatch);
 }
 
 // ---------------------------------------------------------------------------
@@ -805,9 +815,9 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MS >
     bool prev_busy, next_busy;  // the previous stripe rebuilds its last shard / the next its first
     uint32_t bits = 0;
     if (MASKED) {
-        bits = uint32_t(a.plan_ids[t]);
-        const uint32_t bp = has_prev ? uint32_t(a.plan_ids[int64_t(t) - 1]) : 0u;
-        const uint32_t bn = has_next ? uint32_t(a.plan_ids[t + 1]) : 0u;
+        bits = uint32_t(*RSAMD_G(a.plan_ids + t, 4));
+        const uint32_t bp = has_prev ? uint32_t(*RSAMD_G(a.plan_ids + (int64_t(t) - 1), 4)) : 0u;
+        const uint32_t bn = has_next ? uint32_t(*RSAMD_G(a.plan_ids + (t + 1), 4)) : 0u;
         const uint32_t full = (1u << a.mask_bits) - 1u;
         if ((bits >> a.mask_bits) || __builtin_popcount(bits) < K) {
             count_undecodable(a.bad, lane == 0);
@@ -834,19 +844,19 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MS >
         // per lane, and the tables with it).  The pointer is formed after the
         // id check: a pointer that may be null is a generic one, which may
         // alias LDS, and the tables would then be read with per-lane loads.
-        const int32_t id = a.mask_table[bits];
+        const int32_t id = *RSAMD_G(a.mask_table + bits, 4);
         if (id < 0) {  // a singular survivor matrix
             count_undecodable(a.bad, lane == 0);
             return;
         }
-        tabs = reinterpret_cast<const uint32_t *>(a.records + uint64_t(id) * a.rec_stride + a.rec_tabs);
+        tabs = reinterpret_cast<const uint32_t *>(RSAMD_G(a.records + uint64_t(id) * a.rec_stride + a.rec_tabs, K * MS * 20));
     } else {
         nout = MS;
-        tabs = a.tabs;
+        tabs = RSAMD_G(a.tabs, K * MS * 20);
 #pragma unroll
-        for (int i = 0; i < K; ++i) sidx[i] = a.in_idx[i];
+        for (int i = 0; i < K; ++i) sidx[i] = *RSAMD_G(a.in_idx + i, 4);
 #pragma unroll
-        for (int p = 0; p < MS; ++p) oidx[p] = a.out_idx[p];
+        for (int p = 0; p < MS; ++p) oidx[p] = *RSAMD_G(a.out_idx + p, 4);
         prev_busy = !has_prev || oidx[MS - 1] == T - 1;
         next_busy = !has_next || oidx[0] == 0;
     }
@@ -926,7 +936,7 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MS >
                     fsrc[p] = uint32_t(i) * islot + uint32_t(q - (sb + uint64_t(sidx[i]) * len)) + in_off[i];
                 }
         }
-        if (fin[p] && !fin_lds[p]) fv[p] = *reinterpret_cast<const u32x2a *>(q);
+        if (fin[p] && !fin_lds[p]) fv[p] = *reinterpret_cast<const u32x2a *>(RSAMD_G(q, 8));
     }
 
 #pragma unroll
@@ -1006,11 +1016,11 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MS >
             const u32x4 v = *reinterpret_cast<const u32x4 *>(lds + run_lds[p] + (q - l0));
             const bool lo_in = q >= w0 && q + 8 <= w1, hi_in = q + 8 >= w0 && q + 16 <= w1;
             if (lo_in && hi_in)
-                __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(q));
+                __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(RSAMD_G(q, 16)));
             else if (lo_in)
-                __builtin_nontemporal_store(u32x2a{v[0], v[1]}, reinterpret_cast<u32x2a *>(q));
+                __builtin_nontemporal_store(u32x2a{v[0], v[1]}, reinterpret_cast<u32x2a *>(RSAMD_G(q, 8)));
             else if (hi_in)
-                __builtin_nontemporal_store(u32x2a{v[2], v[3]}, reinterpret_cast<u32x2a *>(q + 8));
+                __builtin_nontemporal_store(u32x2a{v[2], v[3]}, reinterpret_cast<u32x2a *>(RSAMD_G(q + 8, 8)));
         }
     }
 }
@@ -1055,14 +1065,14 @@ __global__ void __launch_bounds__(kThreads) gf_masked_byte_kernel(MaskedByteArgs
         uint8_t *sb = a.base + stripe * a.stripe_stride + col;
         uint32_t acc[kMaxOut] = {0, 0, 0, 0};
         for (int i = 0; i < a.nin; ++i) {
-            const Sel s = selectors(sb[uint64_t(in_idx[i]) * a.shard_stride]);
+            const Sel s = selectors(*RSAMD_G(sb + uint64_t(in_idx[i]) * a.shard_stride, 1));
             for (int p = 0; p < nout; ++p) {
                 uint32_t t0, t1, t2;
                 terms(tabs + (i * a.mslots + p) * 5, s, t0, t1, t2);
                 acc[p] = xor3(acc[p], t0, t1) ^ t2;
             }
         }
-        for (int p = 0; p < nout; ++p) sb[uint64_t(out_idx[p]) * a.shard_stride] = uint8_t(acc[p]);
+        for (int p = 0; p < nout; ++p) *RSAMD_G(sb + uint64_t(out_idx[p]) * a.shard_stride, 1) = uint8_t(acc[p]);
     }
 }
 
@@ -1078,17 +1088,19 @@ __global__ void __launch_bounds__(kThreads) gf_byte_kernel(ByteArgs a) {
         const uint64_t stripe = idx / a.ncols;
         const uint64_t col = a.col0 + (idx - stripe * a.ncols);
         uint8_t *sb = a.base + stripe * a.stripe_stride + col;
+        const uint32_t *tabs = RSAMD_G(a.tabs, a.nin * a.nout * 20);
+        const int32_t *in_idx = RSAMD_G(a.in_idx, a.nin * 4), *out_idx = RSAMD_G(a.out_idx, a.nout * 4);
         uint32_t acc[kMaxOut] = {0, 0, 0, 0};
         for (int i = 0; i < a.nin; ++i) {
-            const Sel s = selectors(sb[uint64_t(a.in_idx[i]) * a.shard_stride]);
+            const Sel s = selectors(*RSAMD_G(sb + uint64_t(in_idx[i]) * a.shard_stride, 1));
             for (int p = 0; p < a.nout; ++p) {
                 uint32_t t0, t1, t2;
-                terms(a.tabs + (i * a.nout + p) * 5, s, t0, t1, t2);
+                terms(tabs + (i * a.nout + p) * 5, s, t0, t1, t2);
                 acc[p] = xor3(acc[p], t0, t1) ^ t2;
             }
         }
         for (int p = 0; p < a.nout; ++p) {
-            uint8_t *dst = sb + uint64_t(a.out_idx[p]) * a.shard_stride;
+            uint8_t *dst = RSAMD_G(sb + uint64_t(out_idx[p]) * a.shard_stride, 1);
             if (VERIFY) {
                 if (*dst != uint8_t(acc[p])) flag_mismatch(a.mismatch);
             } else {
@@ -1118,7 +1130,7 @@ __global__ void __launch_bounds__(kThreads)
         const uint64_t w = idx - t * words_per_stripe;
         const uint64_t shard = w / words_per_shard;
         const uint64_t col = (w - shard * words_per_shard) * 8;
-        *reinterpret_cast<uint64_t *>(base + t * stripe_stride + shard * shard_stride + col) =
+        *reinterpret_cast<uint64_t *>(RSAMD_G(base + t * stripe_stride + shard * shard_stride + col, 8)) =
             splitmix64_at(seed ^ (stripe0 + t), w + 1);
     }
 }
@@ -1127,12 +1139,12 @@ __global__ void __launch_bounds__(kThreads)
 // vector per lane, non-temporal both ways, one-shot grid.
 __global__ void __launch_bounds__(kWave) copy_kernel(uint8_t *dst, const uint8_t *src, uint64_t nvec) {
     const uint64_t i = uint64_t(blockIdx.x) * kWave + threadIdx.x;
-    if (i < nvec) __builtin_nontemporal_store(load_stream(src + i * 16), reinterpret_cast<u32x4 *>(dst + i * 16));
+    if (i < nvec) __builtin_nontemporal_store(load_stream(src + i * 16), reinterpret_cast<u32x4 *>(RSAMD_G(dst + i * 16, 16)));
 }
 
 __global__ void copy_tail_kernel(uint8_t *dst, const uint8_t *src, uint64_t n) {
     const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i < n) dst[i] = src[i];
+    if (i < n) *RSAMD_G(dst + i, 1) = *RSAMD_G(src + i, 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -1187,12 +1199,12 @@ __global__ void __launch_bounds__(kThreads) gf_direct_kernel(DirectArgs a) {
 #pragma unroll
             for (int w = 0; w < D; ++w) acc[p][w] = 0;
         for (int i = 0; i < a.nin; ++i) {
-            const V x = __builtin_nontemporal_load(reinterpret_cast<const V *>(a.in[i] + off));
+            const V x = __builtin_nontemporal_load(reinterpret_cast<const V *>(RSAMD_G(a.in[i] + off, W)));
             uint32_t T[M][5];
 #pragma unroll
             for (int p = 0; p < M; ++p)
 #pragma unroll
-                for (int j = 0; j < 5; ++j) T[p][j] = a.tabs[(i * M + p) * 5 + j];
+                for (int j = 0; j < 5; ++j) T[p][j] = *RSAMD_G(a.tabs + ((i * M + p) * 5 + j), 4);
 #pragma unroll
             for (int w = 0; w < D; ++w) {
                 const Sel s = selectors(x[w]);
@@ -1209,7 +1221,7 @@ __global__ void __launch_bounds__(kThreads) gf_direct_kernel(DirectArgs a) {
             V y;
 #pragma unroll
             for (int w = 0; w < D; ++w) y[w] = acc[p][w];
-            V *dst = reinterpret_cast<V *>(a.out[p] + off);
+            V *dst = reinterpret_cast<V *>(RSAMD_G(a.out[p] + off, W));
             if (VERIFY) {
                 const V have = __builtin_nontemporal_load(dst);
                 bool same = true;
@@ -1228,20 +1240,20 @@ __global__ void __launch_bounds__(kThreads) gf_direct_kernel(DirectArgs a) {
         const uint64_t b = t < a.head ? t : tail0 + (t - a.head);
         uint32_t acc[M] = {};
         for (int i = 0; i < a.nin; ++i) {
-            const Sel s = selectors(a.in[i][b]);
+            const Sel s = selectors(*RSAMD_G(a.in[i] + b, 1));
 #pragma unroll
             for (int p = 0; p < M; ++p) {
                 uint32_t t0, t1, t2;
-                terms(a.tabs + (i * M + p) * 5, s, t0, t1, t2);
+                terms(RSAMD_G(a.tabs + (i * M + p) * 5, 20), s, t0, t1, t2);
                 acc[p] = xor3(acc[p], t0, t1) ^ t2;
             }
         }
 #pragma unroll
         for (int p = 0; p < M; ++p) {
             if (VERIFY) {
-                if (a.out[p][b] != uint8_t(acc[p])) flag_mismatch(a.mismatch);
+                if (*RSAMD_G(a.out[p] + b, 1) != uint8_t(acc[p])) flag_mismatch(a.mismatch);
             } else {
-                a.out[p][b] = uint8_t(acc[p]);
+                *RSAMD_G(a.out[p] + b, 1) = uint8_t(acc[p]);
             }
         }
     }
@@ -1605,6 +1617,13 @@ hipError_t launch_group8(const Geometry &g, GroupArgs a, int ms, hipStream_t s) 
     a.stripe_stride = g.stripe_stride;
     a.lo = g.base;
     a.hi = g.base + g.n_stripes * g.stripe_stride;
+    // Phase 0 reads whole 128-byte lines, so the batch's first and last line
+    // may be read past its ends (never written there: a foreign byte is
+    // written back only inside the batch).  A line never crosses a page.
+    const uintptr_t line_lo = reinterpret_cast<uintptr_t>(a.lo) & ~uintptr_t(127);
+    bounds::allow(a.lo, size_t(a.hi - a.lo));
+    bounds::allow(reinterpret_cast<const void *>(line_lo),
+                  ((reinterpret_cast<uintptr_t>(a.hi) + 127) & ~uintptr_t(127)) - line_lo, false);
     a.len = uint32_t(g.len);
     a.total = uint32_t(g.total);
     const int32_t *ids0 = a.plan_ids;
@@ -1963,3 +1982,5 @@ hipError_t launch_copy(uint8_t *dst, const uint8_t *src, size_t n, hipStream_t s
 }
 
 }  // namespace rsamd
+
+RSAMD_BOUNDS_TU(kernels)

@@ -16,7 +16,9 @@
 // block % 8 == 0 (the DFS uses 1000), so every 8-byte half of a lane's 16-byte
 // column vector maps to one contiguous 8-byte run of the file.  Any other
 // block size, alignment or k uses the generic split / merge kernels plus the
-// stripe kernels of kernels.hip.
+// stripe kernels of kernels.hip.  Global accesses go through RSAMD_G
+// (bounds.hpp: the identity in the product build).
+#define RSAMD_TU_ID 2
 #include "layout.hpp"
 
 #include <algorithm>
@@ -63,26 +65,26 @@ enum FileIo { IO_NT8 = 0, IO_PLAIN8 = 1, IO_PAIR16 = 2 };
 
 // File byte runs of 8: [f, f+8) clipped to len, zero beyond (the padding).
 template <int IO>
-__device__ __forceinline__ u32x2 load8(const uint8_t *file, uint64_t len, uint64_t f) {
+__device__ __forceinline__ u32x2 load8(const uint8_t *file, uint64_t len, uint64_t f, uint32_t line = __builtin_LINE()) {
     if (f + 8 <= len)
-        return IO == IO_NT8 ? __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(file + f))
-                            : *reinterpret_cast<const u32x2 *>(file + f);
+        return IO == IO_NT8 ? __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(RSAMD_GL(file + f, 8, line)))
+                            : *reinterpret_cast<const u32x2 *>(RSAMD_GL(file + f, 8, line));
     uint64_t v = 0;
-    for (uint64_t b = f; b < len && b < f + 8; ++b) v |= uint64_t(file[b]) << (8 * (b - f));
+    for (uint64_t b = f; b < len && b < f + 8; ++b) v |= uint64_t(*RSAMD_GL(file + b, 1, line)) << (8 * (b - f));
     return u32x2{uint32_t(v), uint32_t(v >> 32)};
 }
 
 template <int IO>
-__device__ __forceinline__ void store8(uint8_t *file, uint64_t len, uint64_t f, u32x2 v) {
+__device__ __forceinline__ void store8(uint8_t *file, uint64_t len, uint64_t f, u32x2 v, uint32_t line = __builtin_LINE()) {
     if (f + 8 <= len) {
         if (IO == IO_NT8)
-            __builtin_nontemporal_store(v, reinterpret_cast<u32x2 *>(file + f));
+            __builtin_nontemporal_store(v, reinterpret_cast<u32x2 *>(RSAMD_GL(file + f, 8, line)));
         else
-            *reinterpret_cast<u32x2 *>(file + f) = v;
+            *reinterpret_cast<u32x2 *>(RSAMD_GL(file + f, 8, line)) = v;
         return;
     }
     const uint64_t x = uint64_t(v[0]) | uint64_t(v[1]) << 32;
-    for (uint64_t b = f; b < len && b < f + 8; ++b) file[b] = uint8_t(x >> (8 * (b - f)));
+    for (uint64_t b = f; b < len && b < f + 8; ++b) *RSAMD_GL(file + b, 1, line) = uint8_t(x >> (8 * (b - f)));
 }
 
 // 16 file bytes [f, f+16) when both halves are contiguous (same block row),
@@ -91,11 +93,11 @@ struct alignas(8) u32x4_a8 {
     uint32_t v[4];
 };
 __device__ __forceinline__ u32x4 load16_a8(const uint8_t *p) {
-    const u32x4_a8 t = *reinterpret_cast<const u32x4_a8 *>(p);
+    const u32x4_a8 t = *reinterpret_cast<const u32x4_a8 *>(RSAMD_G(p, 16));
     return u32x4{t.v[0], t.v[1], t.v[2], t.v[3]};
 }
 __device__ __forceinline__ void store16_a8(uint8_t *p, const u32x4 &v) {
-    *reinterpret_cast<u32x4_a8 *>(p) = u32x4_a8{{v[0], v[1], v[2], v[3]}};
+    *reinterpret_cast<u32x4_a8 *>(RSAMD_G(p, 16)) = u32x4_a8{{v[0], v[1], v[2], v[3]}};
 }
 
 // Row r and in-row offset w of shard column cc = c0 + d, given the
@@ -142,7 +144,7 @@ __global__ void __launch_bounds__(kWave) file_encode_kernel(FileArgs a) {
 #pragma unroll
         for (int i = 0; i < K; ++i)
 #pragma unroll
-            for (int j = 0; j < 5; ++j) T[p][i][j] = a.tabs[(i * M + p) * 5 + j];
+            for (int j = 0; j < 5; ++j) T[p][i][j] = *RSAMD_G(a.tabs + ((i * M + p) * 5 + j), 4);
     u32x4 x[K];
     const bool pair = IO == IO_PAIR16 && hi && rr[0] == rr[1];
 #pragma unroll
@@ -161,9 +163,9 @@ __global__ void __launch_bounds__(kWave) file_encode_kernel(FileArgs a) {
     for (int i = 0; i < K; ++i) {
         uint8_t *dst = col + uint64_t(i) * a.shard_stride;
         if (hi)
-            __builtin_nontemporal_store(x[i], reinterpret_cast<u32x4 *>(dst));
+            __builtin_nontemporal_store(x[i], reinterpret_cast<u32x4 *>(RSAMD_G(dst, 16)));
         else
-            __builtin_nontemporal_store(u32x2{x[i][0], x[i][1]}, reinterpret_cast<u32x2 *>(dst));
+            __builtin_nontemporal_store(u32x2{x[i][0], x[i][1]}, reinterpret_cast<u32x2 *>(RSAMD_G(dst, 8)));
     }
     if (M == 0) return;
     u32x4 acc[M > 0 ? M : 1];
@@ -179,9 +181,9 @@ __global__ void __launch_bounds__(kWave) file_encode_kernel(FileArgs a) {
     for (int p = 0; p < M; ++p) {
         uint8_t *dst = col + uint64_t(K + p) * a.shard_stride;
         if (hi)
-            __builtin_nontemporal_store(acc[p], reinterpret_cast<u32x4 *>(dst));
+            __builtin_nontemporal_store(acc[p], reinterpret_cast<u32x4 *>(RSAMD_G(dst, 16)));
         else
-            __builtin_nontemporal_store(u32x2{acc[p][0], acc[p][1]}, reinterpret_cast<u32x2 *>(dst));
+            __builtin_nontemporal_store(u32x2{acc[p][0], acc[p][1]}, reinterpret_cast<u32x2 *>(RSAMD_G(dst, 8)));
     }
 }
 
@@ -208,18 +210,18 @@ __global__ void __launch_bounds__(kWave) file_decode_kernel(FileArgs a) {
     const uint32_t w0 = uint32_t(c0 - r0 * a.block);
     int dsrc[K];
 #pragma unroll
-    for (int i = 0; i < K; ++i) dsrc[i] = a.dsrc[i];
+    for (int i = 0; i < K; ++i) dsrc[i] = *RSAMD_G(a.dsrc + i, 4);
     if (v >= a.nvec) return;
     const uint64_t c = uint64_t(v) * 16;
     const bool hi = c + 16 <= a.S;
     u32x4 x[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        const uint8_t *src = a.shards + uint64_t(a.in_idx[j]) * a.shard_stride + c;
+        const uint8_t *src = a.shards + uint64_t(*RSAMD_G(a.in_idx + j, 4)) * a.shard_stride + c;
         if (hi) {
-            x[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src));
+            x[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(RSAMD_G(src, 16)));
         } else {
-            const u32x2 h = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(src));
+            const u32x2 h = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(RSAMD_G(src, 8)));
             x[j] = u32x4{h[0], h[1], 0, 0};
         }
     }
@@ -236,7 +238,7 @@ __global__ void __launch_bounds__(kWave) file_decode_kernel(FileArgs a) {
 #pragma unroll
                 for (int j = 0; j < K; ++j)
 #pragma unroll
-                    for (int q = 0; q < 5; ++q) T[j][q] = a.tabs[(j * E + e) * 5 + q];
+                    for (int q = 0; q < 5; ++q) T[j][q] = *RSAMD_G(a.tabs + ((j * E + e) * 5 + q), 4);
                 y[e][w] = dot_dword<K>(T, s);
             }
         }
@@ -307,9 +309,9 @@ __device__ __forceinline__ void tile_load(u32x4 (&x)[K], const uint8_t *shards, 
     for (int j = 0; j < K; ++j) {
         const uint8_t *src = shards + in_off[j] + c;
         if (c + 16 <= span) {
-            x[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src));
+            x[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(RSAMD_G(src, 16)));
         } else if (c < span) {
-            const u32x2 h = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(src));
+            const u32x2 h = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(RSAMD_G(src, 8)));
             x[j] = u32x4{h[0], h[1], 0, 0};
         }
     }
@@ -357,17 +359,17 @@ __global__ void __launch_bounds__(THREADS) file_decode_tiled_kernel(TileArgs a) 
     const uint64_t col0 = r0 * a.block;
     int dsrc[K];
 #pragma unroll
-    for (int i = 0; i < K; ++i) dsrc[i] = a.dsrc[i];
+    for (int i = 0; i < K; ++i) dsrc[i] = *RSAMD_G(a.dsrc + i, 4);
     uint32_t T[E > 0 ? E : 1][K][5];
 #pragma unroll
     for (int e = 0; e < E; ++e)
 #pragma unroll
         for (int j = 0; j < K; ++j)
 #pragma unroll
-            for (int q = 0; q < 5; ++q) T[e][j][q] = a.tabs[(j * E + e) * 5 + q];
+            for (int q = 0; q < 5; ++q) T[e][j][q] = *RSAMD_G(a.tabs + ((j * E + e) * 5 + q), 4);
     uint64_t in_off[K];
 #pragma unroll
-    for (int j = 0; j < K; ++j) in_off[j] = uint64_t(a.in_idx[j]) * a.shard_stride + col0;
+    for (int j = 0; j < K; ++j) in_off[j] = uint64_t(*RSAMD_G(a.in_idx + j, 4)) * a.shard_stride + col0;
 
     // Phase 1: survivors -> data vectors -> LDS.  span % 8 == 0 (block % 8 == 0)
     // and span <= 2 * 256 * 16: both slots' loads are issued before any
@@ -401,10 +403,10 @@ __global__ void __launch_bounds__(THREADS) file_decode_tiled_kernel(TileArgs a) 
         }
         const u32x4 v{half[0][0], half[0][1], half[1][0], half[1][1]};
         if (f + 16 <= a.file_size) {
-            __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(a.file_out + f));
+            __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(RSAMD_G(a.file_out + f, 16)));
         } else {
             for (uint32_t b = 0; b < 16 && f + b < a.file_size; ++b)
-                a.file_out[f + b] = uint8_t(v[b / 4] >> (8 * (b % 4)));
+                *RSAMD_G(a.file_out + (f + b), 1) = uint8_t(v[b / 4] >> (8 * (b % 4)));
         }
     }
 }
@@ -451,7 +453,7 @@ __global__ void __launch_bounds__(kTileThreads) file_encode_tiled_kernel(EncTile
 #pragma unroll
         for (int i = 0; i < K; ++i)
 #pragma unroll
-            for (int j = 0; j < 5; ++j) T[p][i][j] = a.tabs[(i * M + p) * 5 + j];
+            for (int j = 0; j < 5; ++j) T[p][i][j] = *RSAMD_G(a.tabs + ((i * M + p) * 5 + j), 4);
 
     // Phase 1: run <= kTileSlots * 256 * 16 * K bytes, so 2K loads per thread.
     constexpr int NL = kTileSlots * K;
@@ -463,10 +465,10 @@ __global__ void __launch_bounds__(kTileThreads) file_encode_tiled_kernel(EncTile
         v[u] = u32x4{0, 0, 0, 0};
         if (t < run) {
             if (f + 16 <= a.file_len) {
-                v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(a.file + f));
+                v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(RSAMD_G(a.file + f, 16)));
             } else if (f < a.file_len) {
                 uint32_t w[4] = {0, 0, 0, 0};
-                for (uint64_t b = f; b < a.file_len; ++b) w[(b - f) / 4] |= uint32_t(a.file[b]) << (8 * ((b - f) % 4));
+                for (uint64_t b = f; b < a.file_len; ++b) w[(b - f) / 4] |= uint32_t(*RSAMD_G(a.file + b, 1)) << (8 * ((b - f) % 4));
                 v[u] = u32x4{w[0], w[1], w[2], w[3]};
             }
         }
@@ -505,9 +507,9 @@ __global__ void __launch_bounds__(kTileThreads) file_encode_tiled_kernel(EncTile
         for (int i = 0; i < K; ++i) {
             uint8_t *dst = col + uint64_t(i) * a.shard_stride;
             if (hi)
-                __builtin_nontemporal_store(x[i], reinterpret_cast<u32x4 *>(dst));
+                __builtin_nontemporal_store(x[i], reinterpret_cast<u32x4 *>(RSAMD_G(dst, 16)));
             else
-                __builtin_nontemporal_store(u32x2{x[i][0], x[i][1]}, reinterpret_cast<u32x2 *>(dst));
+                __builtin_nontemporal_store(u32x2{x[i][0], x[i][1]}, reinterpret_cast<u32x2 *>(RSAMD_G(dst, 8)));
         }
         if (M == 0) continue;
         u32x4 acc[M > 0 ? M : 1];
@@ -523,9 +525,9 @@ __global__ void __launch_bounds__(kTileThreads) file_encode_tiled_kernel(EncTile
         for (int p = 0; p < M; ++p) {
             uint8_t *dst = col + uint64_t(K + p) * a.shard_stride;
             if (hi)
-                __builtin_nontemporal_store(acc[p], reinterpret_cast<u32x4 *>(dst));
+                __builtin_nontemporal_store(acc[p], reinterpret_cast<u32x4 *>(RSAMD_G(dst, 16)));
             else
-                __builtin_nontemporal_store(u32x2{acc[p][0], acc[p][1]}, reinterpret_cast<u32x2 *>(dst));
+                __builtin_nontemporal_store(u32x2{acc[p][0], acc[p][1]}, reinterpret_cast<u32x2 *>(RSAMD_G(dst, 8)));
         }
     }
 }
@@ -560,16 +562,16 @@ __global__ void __launch_bounds__(kThreads) split_merge_kernel(CopyArgs a) {
         const uint64_t n = a.S - c < W ? a.S - c : W;  // bytes of this word inside the shard
         if (SPLIT) {
             if (W == 8 && n == 8) {
-                *reinterpret_cast<u32x2 *>(sh) = load8<IO_PLAIN8>(a.file, a.file_len, f);
+                *reinterpret_cast<u32x2 *>(RSAMD_G(sh, 8)) = load8<IO_PLAIN8>(a.file, a.file_len, f);
             } else {
-                for (uint64_t b = 0; b < n; ++b) sh[b] = f + b < a.file_len ? a.file[f + b] : 0;
+                for (uint64_t b = 0; b < n; ++b) *RSAMD_G(sh + b, 1) = f + b < a.file_len ? *RSAMD_G(a.file + (f + b), 1) : 0;
             }
         } else {
             if (W == 8 && n == 8) {
-                store8<IO_PLAIN8>(a.file_out, a.file_len, f, *reinterpret_cast<const u32x2 *>(sh));
+                store8<IO_PLAIN8>(a.file_out, a.file_len, f, *reinterpret_cast<const u32x2 *>(RSAMD_G(sh, 8)));
             } else {
                 for (uint64_t b = 0; b < n; ++b)
-                    if (f + b < a.file_len) a.file_out[f + b] = sh[b];
+                    if (f + b < a.file_len) *RSAMD_G(a.file_out + (f + b), 1) = *RSAMD_G(sh + b, 1);
             }
         }
     }
@@ -796,21 +798,22 @@ namespace {
 //     and the rebuilt data units to the file.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t load_run8(const uint8_t *p, uint64_t f, uint64_t len) {
-    if (f + 8 <= len) return __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(p + f));
+    if (f + 8 <= len) return __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(RSAMD_G(p + f, 8)));
     uint64_t v = 0;
-    for (uint64_t b = f; b < len && b < f + 8; ++b) v |= uint64_t(p[b]) << (8 * (b - f));
+    for (uint64_t b = f; b < len && b < f + 8; ++b) v |= uint64_t(*RSAMD_G(p + b, 1)) << (8 * (b - f));
     return v;
 }
 
 __device__ __forceinline__ void store_run8(uint8_t *p, uint64_t f, uint64_t len, uint64_t v) {
     if (f + 8 <= len) {
-        __builtin_nontemporal_store(v, reinterpret_cast<uint64_t *>(p + f));
+        __builtin_nontemporal_store(v, reinterpret_cast<uint64_t *>(RSAMD_G(p + f, 8)));
         return;
     }
-    for (uint64_t b = f; b < len && b < f + 8; ++b) p[b] = uint8_t(v >> (8 * (b - f)));
+    for (uint64_t b = f; b < len && b < f + 8; ++b) *RSAMD_G(p + b, 1) = uint8_t(v >> (8 * (b - f)));
 }
 
 __device__ __forceinline__ void fold_unit(const uint32_t *t, uint64_t x, uint32_t &lo, uint32_t &hi) {
+    t = RSAMD_G(t, 20);
     uint32_t a, b, c;
     terms(t, selectors(uint32_t(x)), a, b, c);
     lo = xor3(lo, a, b) ^ c;
@@ -835,14 +838,14 @@ __global__ void __launch_bounds__(kThreads) file_direct_encode_kernel(FileDirect
         uint32_t lo[M > 0 ? M : 1] = {}, hi[M > 0 ? M : 1] = {};
         for (int i = 0; i < a.k; ++i) {
             const uint64_t x = load_run8(a.file, (r * uint64_t(a.k) + uint64_t(i)) * a.block + w, a.file_len);
-            __builtin_nontemporal_store(x, reinterpret_cast<uint64_t *>(a.out[i] + c));
+            __builtin_nontemporal_store(x, reinterpret_cast<uint64_t *>(RSAMD_G(a.out[i] + c, 8)));
 #pragma unroll
             for (int p = 0; p < M; ++p) fold_unit(a.tabs + (i * M + p) * 5, x, lo[p], hi[p]);
         }
 #pragma unroll
         for (int p = 0; p < M; ++p)
             __builtin_nontemporal_store(uint64_t(lo[p]) | (uint64_t(hi[p]) << 32),
-                                        reinterpret_cast<uint64_t *>(a.out[a.k + p] + c));
+                                        reinterpret_cast<uint64_t *>(RSAMD_G(a.out[a.k + p] + c, 8)));
     }
 }
 
@@ -852,7 +855,7 @@ __device__ __forceinline__ void decode_unit(const FileDirect &a, uint64_t c, uin
     const uint64_t row0 = r * uint64_t(a.k) * a.block + w;
     uint32_t lo[E > 0 ? E : 1] = {}, hi[E > 0 ? E : 1] = {};
     for (int i = 0; i < a.k; ++i) {
-        const uint64_t x = __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(a.in[i] + c));
+        const uint64_t x = __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(RSAMD_G(a.in[i] + c, 8)));
 #pragma unroll
         for (int p = 0; p < E; ++p) fold_unit(a.tabs + (i * E + p) * 5, x, lo[p], hi[p]);
         const int d = a.in_shard[i];
@@ -861,7 +864,7 @@ __device__ __forceinline__ void decode_unit(const FileDirect &a, uint64_t c, uin
 #pragma unroll
     for (int p = 0; p < E; ++p) {
         const uint64_t y = uint64_t(lo[p]) | (uint64_t(hi[p]) << 32);
-        __builtin_nontemporal_store(y, reinterpret_cast<uint64_t *>(a.out[p] + c));
+        __builtin_nontemporal_store(y, reinterpret_cast<uint64_t *>(RSAMD_G(a.out[p] + c, 8)));
         const int d = a.out_shard[p];
         if (d < a.k) store_run8(a.file_out, row0 + uint64_t(d) * a.block, a.file_len, y);
     }
@@ -898,12 +901,12 @@ __device__ __forceinline__ void lds_run_out(uint8_t *dst, const uint8_t *lds, ui
     const bool v16 = reinterpret_cast<uintptr_t>(dst) % 16 == 0 && reinterpret_cast<uintptr_t>(lds) % 16 == 0;
     if (v16) {
         for (b = uint64_t(threadIdx.x) * 16; b + 16 <= n; b += uint64_t(kThreads) * 16)
-            __builtin_nontemporal_store(*reinterpret_cast<const u32x4 *>(lds + b), reinterpret_cast<u32x4 *>(dst + b));
+            __builtin_nontemporal_store(*reinterpret_cast<const u32x4 *>(lds + b), reinterpret_cast<u32x4 *>(RSAMD_G(dst + b, 16)));
         b = n / 16 * 16;
     }
     for (uint64_t q = b + uint64_t(threadIdx.x) * 8; q + 8 <= n; q += uint64_t(kThreads) * 8)
-        __builtin_nontemporal_store(*reinterpret_cast<const uint64_t *>(lds + q), reinterpret_cast<uint64_t *>(dst + q));
-    for (uint64_t q = n / 8 * 8 + threadIdx.x; q < n; q += kThreads) dst[q] = lds[q];
+        __builtin_nontemporal_store(*reinterpret_cast<const uint64_t *>(lds + q), reinterpret_cast<uint64_t *>(RSAMD_G(dst + q, 8)));
+    for (uint64_t q = n / 8 * 8 + threadIdx.x; q < n; q += kThreads) *RSAMD_G(dst + q, 1) = lds[q];
 }
 
 template <int E>
@@ -919,7 +922,7 @@ __global__ void __launch_bounds__(kThreads) file_direct_decode_tiled_kernel(File
             const uint64_t rr = cc / blk, w = cc - rr * blk, frow = rr * k * blk + w;
             uint32_t lo[E > 0 ? E : 1] = {}, hi[E > 0 ? E : 1] = {};
             for (int i = 0; i < a.k; ++i) {
-                const uint64_t x = __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(a.in[i] + c0 + cc));
+                const uint64_t x = __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(RSAMD_G(a.in[i] + (c0 + cc), 8)));
 #pragma unroll
                 for (int p = 0; p < E; ++p) fold_unit(a.tabs + (i * E + p) * 5, x, lo[p], hi[p]);
                 const int d = a.in_shard[i];
@@ -1037,3 +1040,5 @@ hipError_t launch_split(const FileGeom &g, hipStream_t s) { return launch_split_
 hipError_t launch_merge(const FileGeom &g, hipStream_t s) { return launch_split_merge(g, false, s); }
 
 }  // namespace rsamd
+
+RSAMD_BOUNDS_TU(layout)

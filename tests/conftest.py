@@ -49,6 +49,30 @@ def native():
     return _lib.load()
 
 
+@pytest.fixture(autouse=True)
+def bounds_check(request):
+    """Against the bounds-checking build (make -C csrc bounds; RSAMD_TEST_LIB
+    names lib/bounds/librsamd.so): after every GPU test, no kernel access may
+    have fallen outside the buffers its call declared (csrc/bounds.hpp).  A
+    no-op with the product library, which does not export rs_bounds_report."""
+    yield
+    if "gpu" not in request.fixturenames:
+        return
+    import ctypes as C
+    from rsamd import _lib
+    lib = _lib.load()
+    if not hasattr(lib, "rs_bounds_report"):
+        return
+    import torch
+    torch.cuda.synchronize()
+    n, addr, ln, where = C.c_ulonglong(), C.c_ulonglong(), C.c_ulonglong(), C.c_uint()
+    lib.rs_bounds_report(C.byref(n), C.byref(addr), C.byref(ln), C.byref(where))
+    unit = {1: "kernels.hip", 2: "layout.hip", 9: "host check of a declared range (bounds.hpp)"}.get(
+        where.value // 100000, "?")
+    assert n.value == 0, (f"{n.value} kernel access(es) outside the call's buffers; first: {ln.value} B at "
+                          f"{addr.value:#x}, {unit}:{where.value % 100000}")
+
+
 @pytest.fixture(scope="session")
 def gpu(native):
     """Skip-free GPU gate: a gpu-marked test on a box without a device is an error."""
