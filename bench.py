@@ -379,6 +379,10 @@ def run(args, live_traffic=None):
                 # also as a fraction of the measured device copy kernel
                 "frac_of_copy_kernel": (round(achieved / extra["copy_kernel_GBps"], 4)
                                         if extra.get("copy_kernel_GBps") else None),
+                # north_star's decode target (configs[2], >= 0.50 on 2 erasures) and the
+                # other configs, here so a record that keeps only this object has them
+                # (ReedSolomon.java:175-272; full legs in `extra`)
+                **decode_summary(extra),
             },
             "cpu_baseline": cpu,
             "extra": extra,
@@ -386,6 +390,32 @@ def run(args, live_traffic=None):
         print(json.dumps(line), flush=True)
     parallel.shutdown(r)
     return 0
+
+
+def decode_summary(extra):
+    """Short roofline keys for the decode legs and configs[2]-[4] (fractions of
+    8 TB/s; None where the leg did not run, e.g. at N > 1)."""
+    g = extra.get
+    d01 = g("decode_0_1_hbm_frac") or g("decode_0_1_all_ranks_hbm_frac_per_gpu")
+    return {
+        "decode_0_frac": g("decode_0_hbm_frac"),
+        "decode_0_1_frac": d01,
+        "decode_0_5_frac": g("decode_0_5_hbm_frac"),
+        "decode_patterns_min": g("decode_patterns_min"),
+        "decode_2_erasures_target_0_50_met": (d01 >= 0.50 and (g("decode_0_5_hbm_frac") or 1) >= 0.50)
+        if d01 is not None else None,
+        "configs": {
+            "c2_dec1": g("decode_0_hbm_frac"), "c2_dec2": d01,
+            "c3_enc": g("cfg3_strong_encode_hbm_frac_per_gpu"), "c3_dec4": g("cfg3_strong_decode_hbm_frac_per_gpu"),
+            "c3_enc_pad": g("cfg3_strong_stride_rec_encode_hbm_frac_per_gpu"),
+            "c3_dec4_pad": g("cfg3_strong_stride_rec_decode_hbm_frac_per_gpu"),
+            "c3_enc_granule": g("cfg3_strong_granule32K_encode_hbm_frac_per_gpu"),
+            "c3_dec4_granule": g("cfg3_strong_granule32K_decode_hbm_frac_per_gpu"),
+            "c4_enc": g("cfg4_4p2_4KiB_x1M_encode_hbm_frac"), "c4_dec2": g("cfg4_4p2_4KiB_x1M_decode_hbm_frac"),
+            "c4_enc_granule": g("granule_4p2_4KiB_x1M_encode_hbm_frac"),
+            "c4_dec2_granule": g("granule_4p2_4KiB_x1M_decode_hbm_frac"),
+        },
+    }
 
 
 def device_refusal(backend, world, ranks):
@@ -635,7 +665,8 @@ def cfg3_strong(torch, rsamd, parallel, r, rdev, dev, stream, total, iters):
     most = parallel.stripe_partition(total, r.world, 0)[1]  # rank 0 holds the largest share
     rs = rsamd.ReedSolomon.create(k, m)
     lay = StripeLayout.packed(count, k + m, S)
-    pool = rdev.DeviceBuffer(lay.nbytes, contiguous=True)
+    rlay = StripeLayout.recommended(count, k + m, S)  # rs_shard_stride_recommended (include/rs_amd.h)
+    pool = rdev.DeviceBuffer(max(lay.nbytes, rlay.nbytes), contiguous=True)
     base = pool.data_ptr()
     rdev.fill_synthetic(base, k, lay, SEED, start, stream)
     n = max(3, iters // 2)
@@ -654,6 +685,20 @@ def cfg3_strong(torch, rsamd, parallel, r, rdev, dev, stream, total, iters):
     flag = torch.zeros(1, dtype=torch.int32, device=dev)
     rdev.verify(rs, base, lay, flag.data_ptr(), stream)
     out["cfg3_strong_verified"] = parallel.all_ranks_true(r, int(flag.item()) == 0)
+    # the same [stripe][shard][stride] layout at the recommended shard stride
+    if rlay.shard_stride != lay.shard_stride:
+        rdev.fill_synthetic(base, k, rlay, SEED, start, stream)
+        out["cfg3_strong_stride_rec"] = rlay.shard_stride
+        t = timed_all_ranks(torch, parallel, r, lambda: rdev.encode(rs, base, rlay, stream), n)
+        out["cfg3_strong_stride_rec_encode_hbm_frac_per_gpu"] = round((k + m) * S * most / t / 1e9 / HBM_PEAK_GBPS, 4)
+        t = timed_all_ranks(torch, parallel, r, lambda: rdev.decode(rs, base, present, rlay, stream), n)
+        out["cfg3_strong_stride_rec_decode_hbm_frac_per_gpu"] = round((k + len(miss)) * S * most / t / 1e9 /
+                                                                      HBM_PEAK_GBPS, 4)
+        rdev.fill_synthetic(base, len(miss), rlay, SEED ^ 0xBAD, 0, stream)
+        rdev.decode(rs, base, present, rlay, stream)
+        flag.zero_()
+        rdev.verify(rs, base, rlay, flag.data_ptr(), stream)
+        out["cfg3_strong_stride_rec_verified"] = parallel.all_ranks_true(r, int(flag.item()) == 0)
     # the same stripes in the granule layout, on the same pool
     glay = rdev.GranuleLayout.make(count, k + m, S)
     rdev.fill_synthetic(base, k, glay, SEED, start, stream)
@@ -820,6 +865,59 @@ def packed_headline_leg(torch, rsamd, rdev, dev, stream):
 def chunk_group_legs(torch, rsamd, rdev, dev, stream, B=4 << 20):
     out = chunk_group_leg(torch, rsamd, rdev, dev, stream, B, 1000)
     out.update(chunk_group_leg(torch, rsamd, rdev, dev, stream, B, 1024))
+    out.update(chunk_group_shard_major_leg(torch, rsamd, rdev, dev, stream, B))
+    return out
+
+
+def chunk_group_shard_major_leg(torch, rsamd, rdev, dev, stream, B):
+    """Row f2 in the layout the master's loop implies (MasterImpl.java:733-743,
+    794-839): it reads group g's chunk from every present server, and the
+    offline set is the same for every group (it only grows when a read fails
+    mid-loop), so a batching master holds one array per server with the B
+    groups' 1000-byte chunks back to back, [server][group * 1000].  A run of
+    groups with one pattern is then ONE stripe of B * 1000-byte shards
+    (rs_decode_groups_shard_major_dev).  Encode, decodes {0}, {0,1}, {0,5} with
+    the per-group flags passed as the master would (B x 6 host flags, run
+    detection inside the timed calls), and a set that grows at group B/2 + 1
+    (two runs, the second 8 bytes off a 16-byte boundary).  Each decode is
+    verified after the absent chunks were overwritten."""
+    import numpy as np
+    from rsamd.device import StripeLayout
+    from rsamd.recovery import recover_groups_shard_major_dev
+    k, m, S, T = 4, 2, 1000, 6
+    name = "chunk_groups_4p2_1000B_x4M_shard_major"
+    rs = rsamd.ReedSolomon.create(k, m)
+    lay = StripeLayout.recommended(1, T, S * B)  # one stripe: server stride = the recommended shard stride
+    pool = rdev.DeviceBuffer(lay.nbytes, contiguous=True)
+    buf, base = pool.tensor(), pool.data_ptr()
+    out = {name + "_layout": f"[server][group * 1000], server stride {lay.shard_stride}"}
+    rdev.fill_synthetic(base, k, lay, SEED, 0, stream)
+    t = timed(torch, stream, lambda: rdev.encode(rs, base, lay, stream), 10)
+    out[name + "_encode_GiBps"] = round(k * S * B / t / 2**30, 2)
+    out[name + "_encode_hbm_frac"] = round(T * S * B / t / 1e9 / HBM_PEAK_GBPS, 4)
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    view = buf[: T * lay.shard_stride].view(T, lay.shard_stride)
+    cases = {"0": [(0, B, (0,))], "0_1": [(0, B, (0, 1))], "0_5": [(0, B, (0, 5))],
+             "grows": [(0, B // 2 + 1, (0,)), (B // 2 + 1, B, (0, 3))]}
+    for tag, runs in cases.items():
+        pres = np.ones((B, T), bool)
+        erased = 0
+        for g0, g1, miss in runs:
+            pres[g0:g1, list(miss)] = False
+            erased += (g1 - g0) * len(miss)
+        alg = (k * B + erased) * S
+        t = timed(torch, stream, lambda: recover_groups_shard_major_dev(base, lay.shard_stride, pres, S, stream), 10)
+        out[name + f"_decode_{tag}_hbm_frac"] = round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)
+        for g0, g1, miss in runs:
+            for j in miss:
+                view[j, g0 * S: g1 * S].fill_(0x3C)
+        recover_groups_shard_major_dev(base, lay.shard_stride, pres, S, stream)
+        flag.zero_()
+        rdev.verify(rs, base, lay, flag.data_ptr(), stream)
+        out[name + f"_decode_{tag}_verified"] = int(flag.item()) == 0
+    del buf, view
+    pool.free()
+    torch.cuda.empty_cache()
     return out
 
 

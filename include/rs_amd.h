@@ -57,6 +57,15 @@ enum {
 
 typedef struct rs_codec rs_codec;
 
+/* ABI version of this header.  It goes up whenever an existing entry point's
+ * arguments change, so a dynamic binder (ctypes, JNA, dlsym) can refuse a
+ * library it was not written for: bind only if rs_abi_version() equals the
+ * RS_AMD_ABI_VERSION the binding was written against.
+ *   3: rs_granule_copy_shard takes n_stripes after granule (round 3).
+ *   4: rs_abi_version (this), rs_shard_stride_recommended. */
+#define RS_AMD_ABI_VERSION 4
+RS_API int rs_abi_version(void);
+
 /* ---------------------------------------------------------------------------
  * Codec lifetime -- replaces ReedSolomon.create / the 3-arg constructor
  * (ReedSolomon.java:30-57).  Builds the systematic generator matrix
@@ -187,6 +196,35 @@ RS_API int rs_decode_batch_masked_bits_dev(const rs_codec *codec, uint8_t *dev_b
                                            const uint32_t *dev_present_bits, size_t n_stripes,
                                            size_t shard_len, size_t shard_stride, size_t stripe_stride,
                                            int32_t *dev_bad_count, void *stream);
+
+/* The master's recovery loop batched in its own layout (SURVEY.md 8f row f2;
+ * MasterImpl.recoverOfflineChunkserver, MasterImpl.java:733-743, 794-839,
+ * with ChunkserverDiskRecoveryMachine.java:34-48 per chunk group).  The
+ * master reads chunk group g's chunk from every present chunkserver; a
+ * batching master keeps ONE array per server with the groups back to back:
+ * chunk g of server s at dev_base + s*server_stride + g*chunk_len (shard-major,
+ * [server][group*chunk]).  The offline set is the same for every group and
+ * only grows when a read fails mid-loop, so the groups form a few runs of one
+ * presence pattern each, and a run of n groups is byte for byte ONE stripe of
+ * n*chunk_len-byte shards: one launch at the headline kernels' rate instead
+ * of n 1000-byte stripes.  present holds n_groups x (k+m) HOST flags (group g's
+ * pattern); every absent chunk of every group is rebuilt in place, survivors
+ * the first k present (ReedSolomon.java:210-223).  RS_E_NOT_ENOUGH (nothing
+ * enqueued) when any group has fewer than k present; RS_E_INVALID when
+ * server_stride < n_groups*chunk_len.  Full rate with dev_base, server_stride
+ * and each run's first byte 16-byte aligned (chunk_len 1000: runs starting at
+ * an even group). */
+RS_API int rs_decode_groups_shard_major_dev(const rs_codec *codec, uint8_t *dev_base, size_t server_stride,
+                                            size_t chunk_len, size_t n_groups, const uint8_t *present,
+                                            void *stream);
+
+/* The shard stride a [stripe][shard][stride] batch of total_shards shards of
+ * shard_len bytes should use (the stride measured fastest on MI355X for that
+ * geometry): shard_len rounded up to 256 bytes, plus a pad
+ * where shards a power of two apart contend for the same HBM channels.  Pass
+ * it as shard_stride (and total_shards times it as stripe_stride) to the
+ * batch entry points.  0 when total_shards < 1 or shard_len == 0. */
+RS_API size_t rs_shard_stride_recommended(int total_shards, size_t shard_len);
 
 /* Verify parity of every stripe: dev_mismatch (a device int) is OR-ed with 1
  * when any parity byte differs.  The caller zeroes it first. */

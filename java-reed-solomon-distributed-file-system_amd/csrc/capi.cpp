@@ -816,6 +816,8 @@ int rs_codec_decode_matrix(const rs_codec *c, const uint8_t *present, int nshard
 
 const char *rs_last_error_message(void) { return rsamd::host::last_error(); }
 
+int rs_abi_version(void) { return RS_AMD_ABI_VERSION; }
+
 void rs_thread_release(void) { rsamd::host::release_thread_contexts(); }
 
 int rs_device_count(void) {
@@ -922,6 +924,83 @@ int rs_decode_batch_dev(const rs_codec *codec, uint8_t *dev_base, const uint8_t 
     Geometry g{dev_base, n_stripes, 0, shard_len, shard_stride, stripe_stride, c->total()};
     for (const DevPlan &p : plans)
         RS_HIP(rsamd::launch_gf(g, p, Mode::Code, nullptr, static_cast<hipStream_t>(stream)));
+    return RS_OK;
+}
+
+int rs_decode_groups_shard_major_dev(const rs_codec *codec, uint8_t *dev_base, size_t server_stride, size_t chunk_len,
+                                     size_t n_groups, const uint8_t *present, void *stream) {
+    const Codec *c = impl(codec);
+    if (!c) return fail(RS_E_INVALID, "codec is NULL");
+    if (!present) return fail(RS_E_INVALID, "present must not be NULL");
+    if (n_groups == 0 || chunk_len == 0) return RS_OK;
+    if (!dev_base) return fail(RS_E_INVALID, "NULL device base");
+    const int T = c->total(), k = c->k();
+    if (server_stride < n_groups * chunk_len)
+        return fail(RS_E_INVALID, "server_stride " + std::to_string(server_stride) + " is smaller than n_groups * chunk_len");
+    // Runs of consecutive groups with one presence pattern (the master's
+    // offline set only grows, MasterImpl.java:794-806: one or a few runs).
+    // Every group is checked before anything is enqueued.
+    struct Run {
+        size_t g0, n;
+        std::shared_ptr<const Plan> plan;  // null: every shard present
+    };
+    std::vector<Run> runs;
+    const size_t rowb = size_t(T);
+    auto same_flags = [&](const uint8_t *a, const uint8_t *b) {
+        for (int i = 0; i < T; ++i)
+            if ((a[i] != 0) != (b[i] != 0)) return false;
+        return true;
+    };
+    for (size_t g = 0; g < n_groups;) {
+        const uint8_t *p = present + g * rowb;
+        int np = 0;
+        for (int i = 0; i < T; ++i) np += p[i] ? 1 : 0;
+        if (np < k) return fail(RS_E_NOT_ENOUGH, "Not enough shards present");
+        // Extend the run: byte-identical rows by memcmp blocks that double
+        // while they match and halve when they do not (rows [g, g+n) all equal
+        // row g, so rows [g+n, g+n+a) are compared with rows [g, g+a), a <= n:
+        // 4 M groups cost about one pass over the flags), then row by row for
+        // flags that differ only in their nonzero value.
+        size_t n = 1;
+        while (g + n < n_groups) {
+            size_t a = n;
+            while (g + n < n_groups) {
+                a = std::min(a, n_groups - g - n);
+                if (std::memcmp(present + (g + n) * rowb, p, a * rowb) == 0) {
+                    n += a;
+                    a = n;
+                } else if (a > 1) {
+                    a /= 2;
+                } else {
+                    break;
+                }
+            }
+            if (g + n < n_groups && same_flags(present + (g + n) * rowb, p))
+                ++n;
+            else
+                break;
+        }
+        Run r{g, n, nullptr};
+        if (np < T) {
+            int rc = c->decode_plan(p, &r.plan);
+            if (rc) return fail(rc, rc == RS_E_SINGULAR ? "Matrix is singular" : "Not enough shards present");
+        }
+        runs.push_back(r);
+        g += n;
+    }
+    int rc = need_device();
+    if (rc) return rc;
+    bounds::Scope bs(stream);
+    allow_batch(dev_base, 1, n_groups * chunk_len, server_stride, 0, T);
+    for (const Run &r : runs) {
+        if (!r.plan) continue;
+        std::vector<DevPlan> plans;
+        RS_HIP(r.plan->device_plans(&plans));
+        // the run is ONE stripe of n * chunk_len-byte shards, server_stride apart
+        Geometry g{dev_base + r.g0 * chunk_len, 1, 0, r.n * chunk_len, server_stride, server_stride * size_t(T), T};
+        for (const DevPlan &p : plans)
+            RS_HIP(rsamd::launch_gf(g, p, Mode::Code, nullptr, static_cast<hipStream_t>(stream)));
+    }
     return RS_OK;
 }
 
@@ -1159,6 +1238,12 @@ int rs_check_buffers_and_sizes(const rs_codec *codec, int nshards, const int64_t
                                int64_t byte_count) {
     if (!codec) return fail(RS_E_INVALID, "NULL codec");
     return check_buffers_and_sizes(*codec->impl, nullptr, nshards, shard_lens, offset, byte_count, false);
+}
+
+size_t rs_shard_stride_recommended(int total_shards, size_t shard_len) {
+    if (total_shards < 1 || shard_len == 0) return 0;
+    if (total_shards >= 8 && shard_len >= (size_t(1) << 20)) return round_up(shard_len, 4096) + 4096;
+    return round_up(shard_len, 256);
 }
 
 size_t rs_granule_recommended(int total_shards) {

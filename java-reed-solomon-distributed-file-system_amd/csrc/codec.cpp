@@ -167,9 +167,6 @@ hipError_t Plan::device_plans(std::vector<DevPlan> *out) const {
     for (int g = 0; g < groups(); ++g) {
         const int nout = std::min<int>(kMaxOut, int(out_idx_.size()) - g * kMaxOut);
         out->push_back(dev_plan_at(static_cast<uint8_t *>(it->second) + offs[g], nin, nout));
-        bool run = true;  // consecutive ascending output shards
-        for (int q = 1; q < nout; ++q) run = run && out_idx_[g * kMaxOut + q] == out_idx_[g * kMaxOut] + q;
-        out->back().out_first = run ? out_idx_[g * kMaxOut] : -1;
     }
     return hipSuccess;
 }

@@ -5,6 +5,7 @@
 #include "host.hpp"
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -27,6 +28,7 @@ namespace host {
 
 namespace {
 void release_all(std::map<int, ThreadCtx *> &ctx);
+void orphan(std::map<int, ThreadCtx *> &&ctx);
 
 // This thread's contexts (device -> context), released when the thread exits
 // (JVM and gRPC worker pools create and retire threads) or by rs_thread_release.
@@ -34,11 +36,20 @@ void release_all(std::map<int, ThreadCtx *> &ctx);
 // exit() (glibc runs them before the atexit handlers), where the HIP runtime
 // may already be shutting down.  Whichever thread loaded the library (a JVM
 // loads it from a worker) is released like any other.
+//
+// The exiting thread makes no HIP call: its contexts go to the reaper thread
+// (orphan), which frees them from a live thread.  Thread-local destructors run
+// in the reverse order of their first use, across libraries, so the HIP
+// runtime's own per-thread state (created lazily, by the first stream or
+// launch of the thread, after this object) may already be gone when this
+// destructor runs; streams and events destroyed from here went through it.
+// Both GPU faults of rounds 3 and 4 surfaced a few calls after worker threads
+// had exited that way.
 bool on_main_thread() { return pid_t(syscall(SYS_gettid)) == getpid(); }
 struct ThreadContexts {
     std::map<int, ThreadCtx *> m;
     ~ThreadContexts() {
-        if (!on_main_thread() && !process_exiting()) release_all(m);
+        if (!on_main_thread() && !process_exiting() && !m.empty()) orphan(std::move(m));
     }
 };
 
@@ -174,6 +185,49 @@ void release_all(std::map<int, ThreadCtx *> &ctx) {
 }
 }  // namespace
 
+namespace {
+// The reaper: one long-lived thread, started by the first exiting worker,
+// that releases orphaned contexts.  It never touches a ThreadCtx of its own
+// and stops releasing once exit() has begun (as ~Codec does).
+struct Orphanage {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::map<int, ThreadCtx *>> q;
+    bool started = false;
+};
+
+Orphanage &orphanage() {
+    static Orphanage *o = new Orphanage;  // never destroyed: the reaper may outlive exit()
+    return *o;
+}
+
+void reaper() {
+    Orphanage &o = orphanage();
+    for (;;) {
+        std::map<int, ThreadCtx *> m;
+        {
+            std::unique_lock<std::mutex> lock(o.mu);
+            o.cv.wait(lock, [&] { return !o.q.empty(); });
+            m = std::move(o.q.front());
+            o.q.pop_front();
+        }
+        if (process_exiting()) return;
+        release_all(m);
+    }
+}
+
+void orphan(std::map<int, ThreadCtx *> &&ctx) {
+    Orphanage &o = orphanage();
+    std::lock_guard<std::mutex> lock(o.mu);
+    o.q.push_back(std::move(ctx));
+    if (!o.started) {
+        o.started = true;
+        std::thread(reaper).detach();
+    }
+    o.cv.notify_one();
+}
+}  // namespace
+
 void release_thread_contexts() { release_all(t_ctx.m); }
 
 int grow(uint8_t **buf, size_t *cap, size_t want) {
@@ -241,23 +295,32 @@ size_t chunk_bytes(size_t total, int nslots, bool pinned) {
 }
 
 namespace {
-bool registry_holds(const void *p);  // below: locked for a call by HostRegistration
+struct HostRegistry;
+HostRegistry &host_registry();
+std::mutex &registry_mutex(HostRegistry &reg);
+bool registry_holds_locked(HostRegistry &reg, const void *p);  // below: locked for a call by HostRegistration
 }
 
 // True when every non-null pointer is page-locked host memory known to HIP
 // and stays so for the call: memory that HostRegistration locked for another
 // thread's call reads as pinned too, but is unlocked when that call ends, so
 // it counts as pageable here (the caller then locks it and shares that
-// registration by reference count).
+// registration by reference count).  The registry's lock is held across each
+// pointer's attribute query and registry lookup: a registration released
+// between the two would otherwise read as the caller's own pinning, and the
+// call would run on pages nobody keeps locked.
 bool all_pinned(const uint8_t *const *ptrs, int n) {
+    HostRegistry &reg = host_registry();
+    std::lock_guard<std::mutex> guard(registry_mutex(reg));
     for (int i = 0; i < n; ++i) {
         if (!ptrs[i]) continue;
+        if (registry_holds_locked(reg, ptrs[i])) return false;
         hipPointerAttribute_t attr;
         if (hipPointerGetAttributes(&attr, ptrs[i]) != hipSuccess) {
             (void)hipGetLastError();  // pageable memory: clear the sticky error
             return false;
         }
-        if (attr.type != hipMemoryTypeHost || registry_holds(ptrs[i])) return false;
+        if (attr.type != hipMemoryTypeHost) return false;
     }
     return true;
 }
@@ -288,10 +351,10 @@ HostRegistry &host_registry() {
     return *r;
 }
 
-bool registry_holds(const void *p) {
-    HostRegistry &reg = host_registry();
+std::mutex &registry_mutex(HostRegistry &reg) { return reg.mu; }
+
+bool registry_holds_locked(HostRegistry &reg, const void *p) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    std::lock_guard<std::mutex> guard(reg.mu);
     auto next = reg.regs.upper_bound(a);
     if (next == reg.regs.begin()) return false;
     const auto prev = std::prev(next);

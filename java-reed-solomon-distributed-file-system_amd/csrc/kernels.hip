@@ -767,7 +767,7 @@ struct GroupArgs {
     // one plan for every stripe (MASKED = false)
     const uint32_t *tabs;     // tabs[nin][MS][5]
     const int32_t *in_idx;
-    const int32_t *out_idx;   // ascending
+    const int32_t *out_idx;   // ascending: every Plan lists its outputs in shard order (codec.cpp)
     // a record per stripe (MASKED = true), as MaskedArgs
     const uint8_t *records;
     uint64_t rec_stride;

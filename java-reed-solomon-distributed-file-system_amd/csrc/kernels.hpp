@@ -21,10 +21,6 @@ struct DevPlan {
     const int32_t *in_idx = nullptr;
     const int32_t *out_idx = nullptr;
     int nin = 0, nout = 0;
-    // out_idx[0] when the outputs are consecutive shards in ascending order
-    // (encode: k..k+m-1; decode {0,1}: 0, 1), else -1.  Host-side; selects the
-    // line-owner kernel for back-to-back chunk groups (kernels.hip).
-    int out_first = -1;
 };
 
 // Stripe-batched layout: shard s of stripe t at base + t*stripe_stride + s*shard_stride,

@@ -13,6 +13,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_ROOT, "lib", "librsamd.so")
 CSRC = os.path.join(PKG_ROOT, "csrc")
 
+ABI_VERSION = 4  # include/rs_amd.h RS_AMD_ABI_VERSION, which SIGNATURES follows
 u8p = C.POINTER(C.c_uint8)
 u8pp = C.POINTER(u8p)
 
@@ -27,6 +28,7 @@ SIGNATURES = {
     "rs_codec_matrix": (C.c_int, [C.c_void_p, u8p]),
     "rs_codec_decode_matrix": (C.c_int, [C.c_void_p, u8p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
                                          C.POINTER(C.c_int), u8p]),
+    "rs_abi_version": (C.c_int, []),
     "rs_last_error_message": (C.c_char_p, []),
     "rs_thread_release": (None, []),
     "rs_device_count": (C.c_int, []),
@@ -50,6 +52,9 @@ SIGNATURES = {
                                                C.c_void_p]),
     "rs_decode_granule_masked_bits_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t,
                                                     C.c_size_t, C.c_void_p, C.c_void_p]),
+    "rs_decode_groups_shard_major_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t, u8p,
+                                                   C.c_void_p]),
+    "rs_shard_stride_recommended": (C.c_size_t, [C.c_int, C.c_size_t]),
     "rs_verify_batch_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t,
                                       C.c_void_p, C.c_void_p]),
     "rs_file_layout": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
@@ -94,6 +99,9 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        if lib.rs_abi_version() != ABI_VERSION:
+            raise OSError(f"{LIB_PATH} has ABI version {lib.rs_abi_version()}; this binding was written for "
+                          f"{ABI_VERSION} (include/rs_amd.h RS_AMD_ABI_VERSION): rebuild it")
         _lib = lib
     return _lib
 

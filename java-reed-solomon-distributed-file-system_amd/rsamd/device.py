@@ -33,6 +33,13 @@ class StripeLayout:
         stride = (shard_len + align - 1) // align * align + pad
         return StripeLayout(n_stripes, shard_len, stride, stride * total_shards)
 
+    @staticmethod
+    def recommended(n_stripes: int, total_shards: int, shard_len: int) -> "StripeLayout":
+        """Packed shards at rs_shard_stride_recommended's stride (a pad where
+        shards a power of two apart contend for HBM channels)."""
+        stride = int(_lib.load().rs_shard_stride_recommended(total_shards, shard_len))
+        return StripeLayout(n_stripes, shard_len, stride, stride * total_shards)
+
     @property
     def nbytes(self) -> int:
         return self.n_stripes * self.stripe_stride

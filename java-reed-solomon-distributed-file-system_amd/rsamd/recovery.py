@@ -5,14 +5,21 @@ server/Chunkserver/ChunkserverDiskRecoveryMachine.java:14-57 one call at a
 time (same checks, messages and quirks; decodeMissing runs on the GPU).  The
 master drives it once per 6 x 1000-byte chunk group (MasterImpl.java:794-839);
 recover_chunk_groups_dev does all of a server's chunk groups in one batched
-launch, each group with its own presence pattern (rs_decode_batch_masked_dev).
+launch, each group with its own presence pattern (rs_decode_batch_masked_dev),
+in the group-major layout [group][server][chunk]; recover_groups_shard_major_dev
+takes the layout the master's loop itself implies -- one array per server,
+groups back to back -- where a run of groups with one pattern is one long
+stripe (rs_decode_groups_shard_major_dev).
 """
 from __future__ import annotations
 
 import numpy as np
 
-from .codec import IllegalArgumentException, RS_E_INVALID, RS_E_NOT_ENOUGH
-from .device import StripeLayout, decode_masked
+import ctypes as C
+
+from . import _lib
+from .codec import IllegalArgumentException, RS_E_INVALID, RS_E_NOT_ENOUGH, check
+from .device import StripeLayout, _stream_handle, decode_masked
 from .layout import DATA_SHARD_COUNT, PARITY_SHARD_COUNT, TOTAL_SHARD_COUNT, _codec
 
 
@@ -70,3 +77,22 @@ def recover_chunk_groups_dev(dev_base: int, present, lay: StripeLayout, stream=N
     ConfigVariables.BLOCK_SIZE bytes in the DFS); present is (groups, k+m).
     """
     decode_masked(_codec(data_shards, parity_shards), dev_base, present, lay, stream)
+
+
+def recover_groups_shard_major_dev(dev_base: int, server_stride: int, present, chunk_len: int = 1000, stream=None,
+                                   data_shards: int = DATA_SHARD_COUNT,
+                                   parity_shards: int = PARITY_SHARD_COUNT) -> None:
+    """MasterImpl.recoverOfflineChunkserver (MasterImpl.java:733-743, 794-839)
+    over n_groups chunk groups at once, in the master's own layout: chunk g of
+    server s at dev_base + s*server_stride + g*chunk_len.  present is
+    (n_groups, k+m): group g's servers that answered (the offline set, grown
+    where a read failed mid-loop).  Every absent chunk is rebuilt in place, as
+    ChunkserverDiskRecoveryMachine.recoverChunkserverDiskData does per group
+    (:34-48); each run of groups with one pattern is one launch."""
+    p = np.ascontiguousarray(np.asarray(present, dtype=bool)).view(np.uint8)
+    T = data_shards + parity_shards
+    if p.ndim != 2 or p.shape[1] != T:
+        raise ValueError(f"present must be (n_groups, {T}), got {p.shape}")
+    check(_lib.load().rs_decode_groups_shard_major_dev(
+        _codec(data_shards, parity_shards).handle, C.c_void_p(dev_base), server_stride, chunk_len, p.shape[0],
+        p.ctypes.data_as(_lib.u8p), C.c_void_p(_stream_handle(stream))))

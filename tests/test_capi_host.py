@@ -283,3 +283,37 @@ def test_decode_plan_cache_eviction_keeps_plans_exact(oracle_lib):
         surv, miss, rows = rs.decode_matrix(p)
         osurv, omiss, orows = oc.decode_rows(p)
         assert surv == osurv[:k] and miss == omiss and np.array_equal(rows, orows), idx
+
+
+def test_abi_version_and_stride_recommendation(native):
+    """rs_abi_version matches the header's RS_AMD_ABI_VERSION and the binding's;
+    rs_shard_stride_recommended is a 256-multiple >= shard_len (0 for bad args)."""
+    import re
+    from rsamd import _lib
+    text = open(HEADER).read()
+    want = int(re.search(r"#define RS_AMD_ABI_VERSION (\d+)", text).group(1))
+    assert native.rs_abi_version() == want == _lib.ABI_VERSION
+    for T, S in [(6, 1 << 20), (14, 4 << 20), (6, 1000), (6, 4096), (14, 1 << 20), (20, 12345)]:
+        st = native.rs_shard_stride_recommended(T, S)
+        assert st >= S and st % 256 == 0, (T, S, st)
+    assert native.rs_shard_stride_recommended(0, 4096) == 0
+    assert native.rs_shard_stride_recommended(6, 0) == 0
+
+
+def test_shard_major_argument_errors(native):
+    """rs_decode_groups_shard_major_dev validates every group before any work:
+    a group below k present shards is RS_E_NOT_ENOUGH, a short server stride
+    RS_E_INVALID (no device needed to see either)."""
+    import ctypes as C
+    import rsamd
+    from rsamd import _lib
+    rs = rsamd.ReedSolomon.create(4, 2)
+    pres = np.ones((3, 6), np.uint8)
+    pres[1, :3] = 0
+    u8 = _lib.u8p
+    rc = native.rs_decode_groups_shard_major_dev(rs.handle, C.c_void_p(1 << 20), 3000, 1000, 3,
+                                                pres.ctypes.data_as(u8), None)
+    assert rc == -6 and "Not enough shards present" in _lib.last_error()
+    rc = native.rs_decode_groups_shard_major_dev(rs.handle, C.c_void_p(1 << 20), 2999, 1000, 3,
+                                                pres.ctypes.data_as(u8), None)
+    assert rc == -10

@@ -294,3 +294,63 @@ def test_bits_full_size_small_objects(gpu):
     assert torch.equal(buf, ref) and int(bad.item()) == 0
     del buf, ref, mask
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("pad", [0, 8, 256])
+def test_shard_major_groups_like_the_master(gpu, oracle_lib, pad):
+    """The master's recovery loop batched in its own layout
+    (MasterImpl.java:733-743, 794-839): one array per server, 1000-byte chunk
+    groups back to back (rs_decode_groups_shard_major_dev).  Offline sets {0}
+    and {0,5} for every group, a set that grows mid-loop (a read fails at an
+    odd group, so the second run starts 8 bytes off a 16-byte boundary), and
+    groups that need nothing before the failure.  Parity from the oracle on the
+    long stripe (a run of groups is one stripe of N*1000-byte shards); every
+    byte, server pads included, must come back as encoded."""
+    import torch
+    from rsamd.recovery import recover_groups_shard_major_dev
+    k, m, chunk, N = 4, 2, 1000, 2049
+    T = k + m
+    L = N * chunk
+    stride = L + pad
+    rng = np.random.default_rng(pad + 1)
+    rows = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)] + [np.zeros(L, np.uint8) for _ in range(m)]
+    oracle_lib.Codec(k, m).encode_parity(rows, 0, L)
+    want = np.full(T * stride, 0x77, np.uint8)
+    for s in range(T):
+        want[s * stride: s * stride + L] = rows[s]
+    j = 1001
+    cases = {
+        "offline_0": [(0, N, (0,))],
+        "offline_0_5": [(0, N, (0, 5))],
+        "grows_mid_loop": [(0, j, (0,)), (j, N, (0, 3))],
+        "fails_after_clean_run": [(0, j, ()), (j, N, (2,))],
+    }
+    st = torch.cuda.current_stream()
+    for name, runs in cases.items():
+        host = want.copy()
+        present = np.ones((N, T), bool)
+        for g0, g1, miss in runs:
+            for s in miss:
+                present[g0:g1, s] = False
+                host[s * stride + g0 * chunk: s * stride + g1 * chunk] = 0x3C
+        dev = torch.from_numpy(host).to("cuda:0")
+        recover_groups_shard_major_dev(dev.data_ptr(), stride, present, chunk, st)
+        torch.cuda.synchronize()
+        got = dev.cpu().numpy()
+        assert np.array_equal(got, want), (name, int(np.flatnonzero(got != want)[0]))
+
+
+def test_shard_major_not_enough_touches_nothing(gpu):
+    import torch
+    from rsamd.codec import IllegalArgumentException
+    from rsamd.recovery import recover_groups_shard_major_dev
+    N, T = 64, 6
+    host = np.arange(N * 1000 * T, dtype=np.uint64).astype(np.uint8)
+    dev = torch.from_numpy(host).to("cuda:0")
+    present = np.ones((N, T), bool)
+    present[:10, 1] = False
+    present[40, :3] = False  # undecodable
+    with pytest.raises(IllegalArgumentException):
+        recover_groups_shard_major_dev(dev.data_ptr(), N * 1000, present)
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy(), host)

@@ -18,6 +18,8 @@ Workloads (bench.py's configs):
   cgmaskbits / cgmaskbits1k   4+2 x 1000 B x 4 M chunk groups, stride 1000 / 1024, bitmasks
   cgenc / cgdec01             the same groups at stride 1000: encode / uniform {0,1} decode (line-owner kernel)
   cgdec05 / cgdec15           ... uniform {0,5} / {1,5} decodes
+  cgsmenc / cgsmdec01 / cgsmdec05  the same 4 M groups shard-major ([server][group*1000], one
+                                   array per server): encode, decodes via rs_decode_groups_shard_major_dev
   fenc       4 GiB file -> 4+2 shards (fused)            alg file + 6 S
   fdec_05    4+2 shards {0,5} -> 4 GiB file (tiled)      alg 4 S + file
 """
@@ -136,6 +138,24 @@ def main():
             fn = lambda: rdev.decode(rs, buf.data_ptr(), pres, lay, st)  # noqa: E731
         alg = 6 * S * B
         kernel = "gf_group8_kernel<4, 2, false>"
+    elif name in ("cgsmenc", "cgsmdec01", "cgsmdec05"):
+        # the master's chunk groups in its own layout: one array per server
+        from rsamd.recovery import recover_groups_shard_major_dev
+        k, m, S, B = 4, 2, 1000, 4 << 20
+        rs = rsamd.ReedSolomon.create(k, m)
+        lay = StripeLayout.recommended(1, 6, S * B)
+        buf = torch.empty(lay.nbytes, dtype=torch.uint8, device="cuda:0")
+        rdev.fill_synthetic(buf.data_ptr(), k, lay, SEED, 0, st)
+        rdev.encode(rs, buf.data_ptr(), lay, st)
+        if name == "cgsmenc":
+            fn = lambda: rdev.encode(rs, buf.data_ptr(), lay, st)  # noqa: E731
+            kernel = "gf_vec_kernel<4, 2, false>"
+        else:
+            miss = (0, 1) if name == "cgsmdec01" else (0, 5)
+            pres = np.tile(np.array([i not in miss for i in range(6)]), (B, 1))
+            fn = lambda: recover_groups_shard_major_dev(buf.data_ptr(), lay.shard_stride, pres, S, st)  # noqa: E731
+            kernel = "gf_vec_kernel<4, 2, false>"
+        alg = 6 * S * B
     elif name == "ver104":
         k, m, S, B = 10, 4, 4 << 20, 128
         rs, lay, buf = stripes(k, m, S, B)
