@@ -789,6 +789,9 @@ typedef uint32_t u32x2a __attribute__((ext_vector_type(2)));
 // wave at 4+2 x 1000 B.  Three or four outputs hold up to 32 accumulator
 // registers per lane: a budget of 5 waves per SIMD, unspilled.
 constexpr uint32_t kGroupMaxLen = 1792;
+#ifndef RSAMD_GROUP_FOREIGN
+#define RSAMD_GROUP_FOREIGN 1  // A/B: 0 = never write foreign bytes back (a run's ragged ends as 8-byte stores)
+#endif
 #ifndef RSAMD_GROUP_FOREIGN_LDS
 #define RSAMD_GROUP_FOREIGN_LDS 1  // foreign bytes of a survivor's line from LDS: 0 never, 1 per-group records, 2 always
 #endif
@@ -919,8 +922,8 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MS >
         uint8_t *r0 = sb + uint64_t(s0) * len, *r1 = sb + uint64_t(s1 + 1) * len;
         uint8_t *l0 = r0 - (reinterpret_cast<uintptr_t>(r0) & 127u);  // pointer arithmetic keeps the
         uint8_t *l1 = r1 + ((128u - (reinterpret_cast<uintptr_t>(r1) & 127u)) & 127u);  // global address space
-        head[p] = s0 > 0 || !prev_busy;
-        tail[p] = s1 + 1 < T || !next_busy;
+        head[p] = RSAMD_GROUP_FOREIGN && (s0 > 0 || !prev_busy);
+        tail[p] = RSAMD_GROUP_FOREIGN && (s1 + 1 < T || !next_busy);
         uint8_t *q = lane < 16 ? l0 + 8u * lane : r1 + 8u * (lane - 16);
         fin[p] = lane < 16 ? (head[p] && q < r0) : (lane < 32 && tail[p] && q < l1);
         foff[p] = run_lds[p] + uint32_t(q - l0);
@@ -1797,10 +1800,25 @@ hipError_t launch_gf_tables(const Geometry &g, const DevPlan &p, Mode mode, int 
     if (g.n_stripes == 0 || g.len == 0 || p.nout == 0) return hipSuccess;
     if (p.nout > kMaxOut || p.nin < 1) return hipErrorInvalidValue;
     uint8_t *base = g.base + g.col0;
+    // (one stripe: its stripe stride is never used)
     const bool aligned = (reinterpret_cast<uintptr_t>(base) % 16 == 0) && g.shard_stride % 16 == 0 &&
-                         g.stripe_stride % 16 == 0;
+                         (g.n_stripes == 1 || g.stripe_stride % 16 == 0);
     const bool aligned8 = (reinterpret_cast<uintptr_t>(base) % 8 == 0) && g.shard_stride % 8 == 0 &&
-                          g.stripe_stride % 8 == 0;
+                          (g.n_stripes == 1 || g.stripe_stride % 8 == 0);
+    // A batch 8 bytes off a 16-byte boundary with 16-byte strides (a shard-major
+    // recovery run that starts at an odd 1000-byte group,
+    // rs_decode_groups_shard_major_dev): the first 8 columns on the byte
+    // kernel, the rest on the 16-byte kernels, instead of all of it on the
+    // 8-byte kernels (0.67 of peak for a 2 GB run).
+    if (!aligned && reinterpret_cast<uintptr_t>(base) % 16 == 8 && g.shard_stride % 16 == 0 &&
+        (g.n_stripes == 1 || g.stripe_stride % 16 == 0) && g.len >= kSmallBytes) {
+        hipError_t e = launch_bytes(g, p, g.col0, 8, mode, mismatch, s);
+        if (e != hipSuccess) return e;
+        Geometry rest = g;
+        rest.col0 += 8;
+        rest.len -= 8;
+        return launch_gf_tables(rest, p, mode, mismatch, s);
+    }
     if (aligned8 && !aligned && mode == Mode::Code && uint64_t(g.n_stripes) * g.len > kSmallBytes &&
         group8_geometry(g, p.nin, p.nout)) {
         GroupArgs a{};

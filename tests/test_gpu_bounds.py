@@ -31,10 +31,10 @@ class Tight:
     """nbytes of HBM with GUARD canary bytes on each side, or (guard=False)
     exactly nbytes, ending at the end of its own allocation."""
 
-    def __init__(self, nbytes, guard=True):
+    def __init__(self, nbytes, guard=True, off=0):
         from rsamd.device import DeviceBuffer
-        self.n, self.g = nbytes, (GUARD if guard else 0)
-        self.buf = DeviceBuffer(max(1, nbytes + 2 * self.g), contiguous=False)
+        self.n, self.g = nbytes, (GUARD if guard else 0) + off  # off: the buffer's start past an aligned one
+        self.buf = DeviceBuffer(max(1, nbytes + 2 * self.g - off), contiguous=False)
         self.t = self.buf.tensor()
         self.t.fill_(CANARY)
 
@@ -45,7 +45,7 @@ class Tight:
         return self.t[self.g: self.g + self.n]
 
     def check(self):
-        if self.g:
+        if self.g >= GUARD:
             head = self.t[: self.g].cpu().numpy()
             tail = self.t[self.g + self.n:].cpu().numpy()
             assert (head == CANARY).all(), f"write before the buffer at {int(np.argmax(head != CANARY)) - self.g}"
@@ -118,15 +118,17 @@ def test_file_paths_no_slack(gpu, oracle_lib, guard, k, m, block, n, stride_mode
 
 
 @pytest.mark.parametrize("guard", [False, True], ids=["no-slack", "canary"])
-@pytest.mark.parametrize("k,m,S,B,stride", [
-    (4, 2, 309_000, 1, 309_248),   # the faulting test's write_missing launch: one ragged stripe
-    (4, 2, 309_000, 3, 309_000),   # 8-aligned stride
-    (4, 2, 4096 + 8, 7, 4096 + 16),
-    (4, 2, 1000, 4099, 1000),      # the master's chunk groups, back to back: line-owner kernel
-    (4, 2, 24, 5, 24),             # below the vector width: byte kernel only
-    (10, 4, 65536 + 24, 3, 65536 + 32),
+@pytest.mark.parametrize("k,m,S,B,stride,off", [
+    (4, 2, 309_000, 1, 309_248, 0),   # the faulting test's write_missing launch: one ragged stripe
+    (4, 2, 309_000, 3, 309_000, 0),   # 8-aligned stride
+    (4, 2, 4096 + 8, 7, 4096 + 16, 0),
+    (4, 2, 1000, 4099, 1000, 0),      # the master's chunk groups, back to back: line-owner kernel
+    (4, 2, 24, 5, 24, 0),             # below the vector width: byte kernel only
+    (10, 4, 65536 + 24, 3, 65536 + 32, 0),
+    (4, 2, 1_048_000, 1, 1_048_576, 8),  # 8 bytes off 16 with 16-byte strides: 8-column peel + 16-byte kernels
+    (4, 2, 65_536, 5, 65_536, 8),        # the same over several stripes
 ])
-def test_stripe_batches_no_slack(gpu, oracle_lib, guard, k, m, S, B, stride):
+def test_stripe_batches_no_slack(gpu, oracle_lib, guard, k, m, S, B, stride, off):
     import torch
     import rsamd
     from rsamd import device
@@ -135,7 +137,7 @@ def test_stripe_batches_no_slack(gpu, oracle_lib, guard, k, m, S, B, stride):
     T = k + m
     lay = StripeLayout(B, S, stride, T * stride)
     nbytes = (B - 1) * lay.stripe_stride + (T - 1) * stride + S
-    buf = Tight(nbytes, guard)
+    buf = Tight(nbytes, guard, off)
     st = torch.cuda.current_stream()
     data = _bytes(B * k * S, S + B)
     host = np.zeros(nbytes, np.uint8)

@@ -3,7 +3,7 @@
 # Steps, run in the order given, each under its own time limit; the chain stops
 # at the first failure (nothing more touches the GPU after a fault or timeout):
 #   tests      pytest -m gpu (one process)              -> pytest_gpu_TAG.log
-#   bounds     pytest -m gpu against the bounds-checking build (lib/bounds)
+#   bounds     pytest -m gpu against the bounds-checking build (lib/bounds), serialised
 #   smoke      __graft_entry__.smoke()                  -> smoke_TAG.log
 #   bench      bench.py at N = 1 (live PMC passes)      -> bench_TAG.json
 #   prof       rocprofv3 --kernel-trace --stats of the headline -> prof_TAG/
@@ -31,6 +31,8 @@ for step in "$@"; do
           > $out/pytest_gpu_$tag.log 2>&1 || { echo "pytest failed"; tail -40 $out/pytest_gpu_$tag.log; exit 1; }
       tail -1 $out/pytest_gpu_$tag.log ;;
     bounds)
+      # kernels and copies serialised: a fault surfaces at the call that made it
+      AMD_SERIALIZE_KERNEL=3 AMD_SERIALIZE_COPY=3 \
       RSAMD_TEST_LIB=java-reed-solomon-distributed-file-system_amd/lib/bounds/librsamd.so \
         timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
           > $out/pytest_bounds_$tag.log 2>&1 || { echo "bounds pytest failed"; tail -40 $out/pytest_bounds_$tag.log; exit 1; }
@@ -65,6 +67,18 @@ for step in "$@"; do
         python3 tools/pmc_summary.py "$W" "$kern" "$alg" "$out/pmcw_${tag}_${W}_FETCH_SIZE" \
             "$out/pmcw_${tag}_${W}_WRITE_SIZE" "$out/pmc_traffic_$tag.json" || exit 1
       done ;;
+    pmcw:*)  # pmcw:WORKLOAD[:LIB] -> FETCH/WRITE passes of one tools/pmc_workloads.py workload
+      spec=${step#pmcw:}; W=${spec%%:*}; L=""; [ "$spec" != "$W" ] && L=${spec#*:}
+      sfx=$W; [ -n "$L" ] && sfx=${W}_$(basename $(dirname $L))
+      for C in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$out/pmcw_${tag}_${sfx}_$C" -o run -- \
+            python3 tools/pmc_workloads.py $W $L > "$out/pmcw_${tag}_${sfx}_$C.log" 2>&1 || { tail -20 "$out/pmcw_${tag}_${sfx}_$C.log"; exit 1; }
+      done
+      meta=$(grep '^{' "$out/pmcw_${tag}_${sfx}_FETCH_SIZE.log" | tail -1)
+      kern=$(python3 -c "import json,sys; print(json.loads(sys.argv[1])['kernel'])" "$meta")
+      alg=$(python3 -c "import json,sys; print(json.loads(sys.argv[1])['alg_bytes_per_launch'])" "$meta")
+      python3 tools/pmc_summary.py "$sfx" "$kern" "$alg" "$out/pmcw_${tag}_${sfx}_FETCH_SIZE" \
+          "$out/pmcw_${tag}_${sfx}_WRITE_SIZE" "$out/pmc_traffic_$tag.json" || exit 1 ;;
     probe:*)
       np=$((np + 1))
       timeout -k 10 600 python3 ${step#probe:} > $out/probe_${tag}_$np.txt 2>&1 \

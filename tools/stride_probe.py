@@ -7,6 +7,9 @@ shard), the batch is one rs_dev_alloc pool, encoded and decoded (the first m
 data shards) in alternation over --rounds rounds; fractions of 8 TB/s of
 (k+m)*S*B and (k+e)*S*B.
   python tools/stride_probe.py --shapes 10:4:4096:1024 4:2:1024:4096 --pads 0 256 1024 4096 8192
+--offsets O ...: one pool per shape (allocated once, --extra-MiB larger), the
+batch placed O KiB past its start, so the only thing that changes between
+variants is the batch's address; the pool's base address is printed.
 """
 import argparse
 import json
@@ -41,6 +44,8 @@ def main():
     ap.add_argument("--shapes", nargs="+", default=["10:4:4096:1024"])
     ap.add_argument("--pads", nargs="+", type=int, default=[0, 4096])
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--offsets", nargs="*", type=int, default=None, help="KiB offsets of the batch in one pool")
+    ap.add_argument("--extra-MiB", type=int, default=512)
     a = ap.parse_args()
     import torch
     import rsamd
@@ -52,6 +57,26 @@ def main():
         S = skib << 10
         rs = rsamd.ReedSolomon.create(k, m)
         present = [i >= m for i in range(k + m)]  # the first m data shards rebuilt
+        if a.offsets is not None:
+            lay = StripeLayout.packed(B, k + m, S, pad=a.pads[0])
+            pool = DeviceBuffer(lay.nbytes + (a.extra_MiB << 20))
+            res = {o: {"enc": [], "dec": []} for o in a.offsets}
+            for r in range(a.rounds):
+                for o in a.offsets:
+                    base = pool.data_ptr() + (o << 10)
+                    device.fill_synthetic(base, k, lay, 7, 0, st)
+                    te = timed(torch, st, lambda: device.encode(rs, base, lay, st))
+                    td = timed(torch, st, lambda: device.decode(rs, base, present, lay, st))
+                    res[o]["enc"].append((k + m) * S * B / te / 1e9 / PEAK)
+                    res[o]["dec"].append((k + m) * S * B / td / 1e9 / PEAK)
+            for o in a.offsets:
+                print(json.dumps({"shape": shape, "pad": a.pads[0], "pool_base": hex(pool.data_ptr()),
+                                  "contiguous": pool.contiguous, "offset_KiB": o,
+                                  "encode": [round(x, 4) for x in res[o]["enc"]],
+                                  "decode_first_m": [round(x, 4) for x in res[o]["dec"]]}), flush=True)
+            pool.free()
+            torch.cuda.empty_cache()
+            continue
         res = {p: {"enc": [], "dec": []} for p in a.pads}
         for r in range(a.rounds):
             for p in a.pads:
