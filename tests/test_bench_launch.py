@@ -189,3 +189,24 @@ def test_link_bound():
     assert abs(bench.link_bound_GiBps(link2, 1.0, 1.0) - 44e9 / 2**30) < 0.01
     link3 = dict(link, kernel={"h2d_GBps": 30.0, "d2h_GBps": 30.0, "both_h2d_GBps": 20.0, "both_d2h_GBps": 20.0})
     assert bench.link_bound_GiBps(link3, 1.0, 0.5) == bench.link_bound_GiBps(link, 1.0, 0.5)
+
+
+def test_decode_summary_keys():
+    """roofline's short decode / configs keys (what a record that keeps only the
+    parsed line shows): taken from the extra legs at N = 1, the all-ranks
+    {0,1} leg at N > 1, None where a leg did not run."""
+    sys.path.insert(0, ROOT)
+    import bench
+    ex = {"decode_0_hbm_frac": 0.87, "decode_0_1_hbm_frac": 0.86, "decode_0_5_hbm_frac": 0.85,
+          "decode_patterns_min": 0.84, "cfg3_strong_encode_hbm_frac_per_gpu": 0.77,
+          "granule_4p2_4KiB_x1M_encode_hbm_frac": 0.87}
+    s = bench.decode_summary(ex)
+    assert (s["decode_0_frac"], s["decode_0_1_frac"], s["decode_0_5_frac"], s["decode_patterns_min"]) == \
+        (0.87, 0.86, 0.85, 0.84)
+    assert s["decode_2_erasures_target_0_50_met"] is True
+    assert s["configs"]["c3_enc"] == 0.77 and s["configs"]["c4_enc_granule"] == 0.87
+    assert s["configs"]["c3_enc_pad"] is None
+    n8 = bench.decode_summary({"decode_0_1_all_ranks_hbm_frac_per_gpu": 0.45})
+    assert n8["decode_0_1_frac"] == 0.45 and n8["decode_0_frac"] is None
+    assert n8["decode_2_erasures_target_0_50_met"] is False
+    assert bench.decode_summary({})["decode_2_erasures_target_0_50_met"] is None
