@@ -29,6 +29,7 @@ namespace host {
 namespace {
 void release_all(std::map<int, ThreadCtx *> &ctx);
 void orphan(std::map<int, ThreadCtx *> &&ctx);
+ThreadCtx *adopt_idle(int dev);
 
 // This thread's contexts (device -> context), released when the thread exits
 // (JVM and gRPC worker pools create and retire threads) or by rs_thread_release.
@@ -38,7 +39,8 @@ void orphan(std::map<int, ThreadCtx *> &&ctx);
 // loads it from a worker) is released like any other.
 //
 // The exiting thread makes no HIP call: its contexts go to the reaper thread
-// (orphan), which frees them from a live thread.  Thread-local destructors run
+// (orphan), which frees their buffers from a live thread and keeps their
+// streams and events for the next new thread (adopt_idle).  Thread-local destructors run
 // in the reverse order of their first use, across libraries, so the HIP
 // runtime's own per-thread state (created lazily, by the first stream or
 // launch of the thread, after this object) may already be gone when this
@@ -128,7 +130,14 @@ int thread_ctx(ThreadCtx **out) {
     RS_HIP(hipGetDevice(&dev));
     auto it = t_ctx.m.find(dev);
     if (it == t_ctx.m.end()) {
-        auto *c = new ThreadCtx;
+        ThreadCtx *c = adopt_idle(dev);  // a retired thread's streams and events, if any
+        if (c) {
+            it = t_ctx.m.emplace(dev, c).first;
+            *out = c;
+            bounds::allow(c->flag, 256);
+            return RS_OK;
+        }
+        c = new ThreadCtx;
         hipError_t e = create_pipeline_streams(c);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ready, hipEventDisableTiming);
         for (int b = 0; b < kStageBufs && e == hipSuccess; ++b) {
@@ -149,6 +158,26 @@ int thread_ctx(ThreadCtx **out) {
 }
 
 namespace {
+// A context's buffers (staging, mirrors, zero-copy and masked slots, plan
+// images): the memory a retired thread should give back.  Streams, events
+// and the flag stay.
+void free_buffers(ThreadCtx *c) {
+    for (MaskedSlot &sl : c->masked) {
+        if (sl.done) (void)hipEventSynchronize(sl.done);
+        if (sl.dev) (void)hipFree(sl.dev);
+        if (sl.host) (void)hipHostFree(sl.host);
+        sl.dev = sl.host = nullptr;
+        sl.dev_cap = sl.host_cap = 0;
+    }
+    if (c->mirror) (void)hipHostFree(c->mirror);
+    if (c->stage) (void)hipFree(c->stage);
+    if (c->plan) (void)hipFree(c->plan);
+    if (c->file) (void)hipFree(c->file);
+    if (c->zc) (void)hipHostFree(c->zc);
+    c->mirror = c->stage = c->plan = c->file = c->zc = c->zc_dev = nullptr;
+    c->mirror_cap = c->stage_cap = c->plan_cap = c->file_cap = c->zc_cap = 0;
+}
+
 void release_all(std::map<int, ThreadCtx *> &ctx) {
     if (ctx.empty()) return;  // a thread that never coded makes no HIP call here
     int cur = 0;
@@ -156,6 +185,7 @@ void release_all(std::map<int, ThreadCtx *> &ctx) {
     for (auto &kv : ctx) {
         ThreadCtx *c = kv.second;
         (void)hipSetDevice(kv.first);
+        free_buffers(c);
         if (c->stream) (void)hipStreamDestroy(c->stream);
         if (c->stream2) (void)hipStreamDestroy(c->stream2);
         if (c->stream3) (void)hipStreamDestroy(c->stream3);
@@ -165,16 +195,8 @@ void release_all(std::map<int, ThreadCtx *> &ctx) {
             if (c->freed[b]) (void)hipEventDestroy(c->freed[b]);
             if (c->loaded[b]) (void)hipEventDestroy(c->loaded[b]);
         }
-        if (c->mirror) (void)hipHostFree(c->mirror);
-        if (c->stage) (void)hipFree(c->stage);
-        if (c->plan) (void)hipFree(c->plan);
         if (c->flag) (void)hipFree(c->flag);
-        if (c->file) (void)hipFree(c->file);
-        if (c->zc) (void)hipHostFree(c->zc);
         for (MaskedSlot &sl : c->masked) {
-            if (sl.done) (void)hipEventSynchronize(sl.done);
-            if (sl.dev) (void)hipFree(sl.dev);
-            if (sl.host) (void)hipHostFree(sl.host);
             if (sl.done) (void)hipEventDestroy(sl.done);
             if (sl.uploaded) (void)hipEventDestroy(sl.uploaded);
         }
@@ -194,6 +216,7 @@ struct Orphanage {
     std::condition_variable cv;
     std::deque<std::map<int, ThreadCtx *>> q;
     bool started = false;
+    std::map<int, std::vector<ThreadCtx *>> idle;  // device -> retired contexts, buffers freed
 };
 
 Orphanage &orphanage() {
@@ -212,8 +235,30 @@ void reaper() {
             o.q.pop_front();
         }
         if (process_exiting()) return;
-        release_all(m);
+        // Give the memory back and keep the streams and events for the next
+        // new thread (thread_ctx): a JVM or gRPC pool that retires and
+        // creates workers then makes no stream churn at all.
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        for (auto &kv : m) {
+            (void)hipSetDevice(kv.first);
+            free_buffers(kv.second);
+        }
+        (void)hipSetDevice(cur);
+        std::lock_guard<std::mutex> lock(o.mu);
+        for (auto &kv : m) o.idle[kv.first].push_back(kv.second);
     }
+}
+
+// A retired context for this device, or nullptr.
+ThreadCtx *adopt_idle(int dev) {
+    Orphanage &o = orphanage();
+    std::lock_guard<std::mutex> lock(o.mu);
+    auto it = o.idle.find(dev);
+    if (it == o.idle.end() || it->second.empty()) return nullptr;
+    ThreadCtx *c = it->second.back();
+    it->second.pop_back();
+    return c;
 }
 
 void orphan(std::map<int, ThreadCtx *> &&ctx) {

@@ -110,3 +110,38 @@ def test_thread_exit_releases_its_staging(gpu, oracle_lib):
                 break
             time.sleep(0.05)
         assert free1 - seen["mid"] >= 0.8 * held, (free0, seen["mid"], free1)
+
+
+def test_retired_contexts_are_reused(gpu, oracle_lib):
+    """Workers that come and go (a JVM / gRPC pool): each exiting thread's
+    contexts go to the reaper, which frees their buffers and keeps their
+    streams for the next new thread (host.cpp orphan / adopt_idle).  Six
+    short-lived workers in turn, alternating calls on the direct path (6 MiB
+    per shard, page-locked for the call) and on the zero-copy staging buffer
+    (40 KB), all bit-exact."""
+    import rsamd
+    rs = rsamd.ReedSolomon.create(4, 2)
+    oc = oracle_lib.Codec(4, 2)
+    errors = []
+
+    def work(seed, n):
+        try:
+            rng = np.random.default_rng(seed)
+            sh = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(4)] + [np.zeros(n, np.uint8)
+                                                                                 for _ in range(2)]
+            ref = [a.copy() for a in sh]
+            oc.encode_parity(ref, 0, n)
+            rs.encodeParity(sh, 0, n)
+            assert all(np.array_equal(a, b) for a, b in zip(sh, ref)), seed
+            sh[1][:] = 0
+            sh[5][:] = 0
+            rs.decodeMissing(sh, [True, False, True, True, True, False], 0, n)
+            assert all(np.array_equal(a, b) for a, b in zip(sh, ref)), seed
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    for seed in range(6):
+        t = threading.Thread(target=work, args=(seed, (6 << 20) + seed if seed % 2 else 40_000 + seed))
+        t.start()
+        t.join()
+    assert not errors, errors
