@@ -959,12 +959,12 @@ int rs_decode_groups_shard_major_dev(const rs_codec *codec, uint8_t *dev_base, s
         // Extend the run: byte-identical rows by memcmp blocks that double
         // while they match and halve when they do not (rows [g, g+n) all equal
         // row g, so rows [g+n, g+n+a) are compared with rows [g, g+a), a <= n:
-        // 4 M groups cost about one pass over the flags), then row by row for
-        // flags that differ only in their nonzero value.
-        size_t n = 1;
+        // 4 M groups cost about one pass over the flags); from the first row
+        // that differs in bytes, row by row on the flags' meaning (nonzero).
+        size_t n = 1, a = 1;
+        bool exact = true;
         while (g + n < n_groups) {
-            size_t a = n;
-            while (g + n < n_groups) {
+            if (exact) {
                 a = std::min(a, n_groups - g - n);
                 if (std::memcmp(present + (g + n) * rowb, p, a * rowb) == 0) {
                     n += a;
@@ -972,13 +972,13 @@ int rs_decode_groups_shard_major_dev(const rs_codec *codec, uint8_t *dev_base, s
                 } else if (a > 1) {
                     a /= 2;
                 } else {
-                    break;
+                    exact = false;
                 }
-            }
-            if (g + n < n_groups && same_flags(present + (g + n) * rowb, p))
+            } else if (same_flags(present + (g + n) * rowb, p)) {
                 ++n;
-            else
+            } else {
                 break;
+            }
         }
         Run r{g, n, nullptr};
         if (np < T) {

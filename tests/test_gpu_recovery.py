@@ -354,3 +354,34 @@ def test_shard_major_not_enough_touches_nothing(gpu):
         recover_groups_shard_major_dev(dev.data_ptr(), N * 1000, present)
     torch.cuda.synchronize()
     assert np.array_equal(dev.cpu().numpy(), host)
+
+
+def test_shard_major_any_nonzero_flag(gpu, oracle_lib):
+    """The C entry point reads a flag as present when nonzero, as the Java
+    boolean[] is read (rows with different nonzero bytes but the same pattern
+    are one run): random nonzero values in every present flag, two runs."""
+    import ctypes as C
+    import torch
+    import rsamd
+    from rsamd import _lib
+    k, m, chunk, N = 4, 2, 1000, 1026
+    T, L = k + m, N * chunk
+    rng = np.random.default_rng(9)
+    rows = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)] + [np.zeros(L, np.uint8) for _ in range(m)]
+    oracle_lib.Codec(k, m).encode_parity(rows, 0, L)
+    want = np.concatenate(rows)
+    flags = rng.integers(1, 256, (N, T), dtype=np.uint8)
+    flags[:500, 0] = 0
+    flags[500:, 2] = 0
+    flags[500:, 5] = 0
+    host = want.copy()
+    host[0: 500 * chunk] = 0x3C
+    for s in (2, 5):
+        host[s * L + 500 * chunk: (s + 1) * L] = 0x3C
+    dev = torch.from_numpy(host).to("cuda:0")
+    rs = rsamd.ReedSolomon.create(k, m)
+    rc = _lib.load().rs_decode_groups_shard_major_dev(rs.handle, C.c_void_p(dev.data_ptr()), L, chunk, N,
+                                                      flags.ctypes.data_as(_lib.u8p), None)
+    assert rc == 0, _lib.last_error()
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy(), want)
