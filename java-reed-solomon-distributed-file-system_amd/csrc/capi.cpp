@@ -935,6 +935,8 @@ int rs_decode_groups_shard_major_dev(const rs_codec *codec, uint8_t *dev_base, s
     if (n_groups == 0 || chunk_len == 0) return RS_OK;
     if (!dev_base) return fail(RS_E_INVALID, "NULL device base");
     const int T = c->total(), k = c->k();
+    if (n_groups > SIZE_MAX / chunk_len || server_stride > SIZE_MAX / size_t(T))
+        return fail(RS_E_INVALID, "n_groups * chunk_len or server_stride * total overflows");
     if (server_stride < n_groups * chunk_len)
         return fail(RS_E_INVALID, "server_stride " + std::to_string(server_stride) + " is smaller than n_groups * chunk_len");
     // Runs of consecutive groups with one presence pattern (the master's

@@ -317,3 +317,7 @@ def test_shard_major_argument_errors(native):
     rc = native.rs_decode_groups_shard_major_dev(rs.handle, C.c_void_p(1 << 20), 2999, 1000, 3,
                                                 pres.ctypes.data_as(u8), None)
     assert rc == -10
+    # n_groups * chunk_len past SIZE_MAX is rejected, not wrapped
+    rc = native.rs_decode_groups_shard_major_dev(rs.handle, C.c_void_p(1 << 20), 1 << 20, 1 << 40, 1 << 30,
+                                                pres.ctypes.data_as(u8), None)
+    assert rc == -10 and "overflows" in _lib.last_error()
