@@ -10,6 +10,7 @@
 #   rehearse   bench.py --gpus 2 and --gpus 4 with every leg, wall times -> bench{2,4}_TAG.json
 #   pmc        FETCH/WRITE_SIZE passes of the chunk-group kernels -> pmc_traffic_TAG.json
 #   probe:ARGS python3 ARGS (a tools/ probe)            -> probe_TAG_N.txt
+#   kprobe:ARGS the same under rocprofv3 --kernel-trace --stats -> kprobe_TAG_N/, kprobe_TAG_N.txt
 set -o pipefail
 tag=${1:?tag}
 shift
@@ -84,6 +85,12 @@ for step in "$@"; do
       timeout -k 10 600 python3 ${step#probe:} > $out/probe_${tag}_$np.txt 2>&1 \
           || { echo "probe failed"; tail -30 $out/probe_${tag}_$np.txt; exit 1; }
       tail -5 $out/probe_${tag}_$np.txt ;;
+    kprobe:*)  # a tools/ probe under rocprofv3 --kernel-trace --stats -> kprobe_TAG_N/ + .txt
+      np=$((np + 1))
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kprobe_${tag}_$np" -o run -- \
+          python3 ${step#kprobe:} > $out/kprobe_${tag}_$np.txt 2>&1 \
+          || { echo "kprobe failed"; tail -30 $out/kprobe_${tag}_$np.txt; exit 1; }
+      grep '^{' $out/kprobe_${tag}_$np.txt | tail -12 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   echo "   $step: $(( $(date +%s) - t0 )) s"

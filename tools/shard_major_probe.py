@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""Shard-major chunk-group recovery, run by run: why does an offline set that
+grows mid-loop (two runs) read below either run alone?
+
+4+2 x 1000 B x B groups in the master's layout [server][group * 1000]
+(rs_decode_groups_shard_major_dev).  Each case is a list of (g0, g1, missing)
+runs; fractions of 8 TB/s of (k * B + erased chunks) * 1000 B.  Run it under
+rocprofv3 --kernel-trace --stats to see each run's kernels.
+  python tools/shard_major_probe.py [--groups 4194304] [--rounds 2]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                "java-reed-solomon-distributed-file-system_amd"))
+PEAK = 8000.0
+
+
+def timed(torch, st, fn, iters=8, warm_s=0.4):
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < warm_s:
+        for _ in range(4):
+            fn()
+        torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record(st)
+    for _ in range(iters):
+        fn()
+    e.record(st)
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e-3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--groups", type=int, default=4 << 20)
+    ap.add_argument("--rounds", type=int, default=2)
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    import rsamd
+    from rsamd import device
+    from rsamd.device import DeviceBuffer, StripeLayout
+    from rsamd.recovery import recover_groups_shard_major_dev
+    k, m, S, T, B = 4, 2, 1000, 6, a.groups
+    h = B // 2
+    cases = {
+        "full_0": [(0, B, (0,))],
+        "full_03": [(0, B, (0, 3))],
+        "h1odd_0": [(0, h + 1, (0,))],
+        "h1even_0": [(0, h, (0,))],
+        "h2odd_03": [(h + 1, B, (0, 3))],
+        "h2even_03": [(h, B, (0, 3))],
+        "h2odd_0": [(h + 1, B, (0,))],
+        "grows_odd": [(0, h + 1, (0,)), (h + 1, B, (0, 3))],
+        "grows_even": [(0, h, (0,)), (h, B, (0, 3))],
+        "split_same_odd": [(0, h + 1, (0, 3)), (h + 1, B, (0, 5))],
+    }
+    st = torch.cuda.current_stream()
+    rs = rsamd.ReedSolomon.create(k, m)
+    lay = StripeLayout.recommended(1, T, S * B)
+    pool = DeviceBuffer(lay.nbytes)
+    base = pool.data_ptr()
+    device.fill_synthetic(base, k, lay, 7, 0, st)
+    device.encode(rs, base, lay, st)
+    res = {c: [] for c in cases}
+    for _ in range(a.rounds):
+        for name, runs in cases.items():
+            pres = np.ones((B, T), bool)
+            erased = 0
+            for g0, g1, miss in runs:
+                pres[g0:g1, list(miss)] = False
+                erased += (g1 - g0) * len(miss)
+            t = timed(torch, st, lambda: recover_groups_shard_major_dev(base, lay.shard_stride, pres, S, st))
+            res[name].append(((k * B + erased) * S / t / 1e9 / PEAK, t * 1e3))
+    for name in cases:
+        print(json.dumps({"case": name, "runs": [[g0, g1, list(mi)] for g0, g1, mi in cases[name]],
+                          "frac": [round(f, 4) for f, _ in res[name]],
+                          "ms": [round(t, 3) for _, t in res[name]]}), flush=True)
+    pool.free()
+
+
+if __name__ == "__main__":
+    main()
