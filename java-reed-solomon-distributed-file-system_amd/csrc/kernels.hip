@@ -53,6 +53,7 @@ constexpr int kWave = 64;      // vector kernels: one wave per block
 // into launches of at most this many blocks.
 constexpr size_t kMaxGridBlocks = size_t(UINT32_MAX) / kWave;
 constexpr uint64_t kSmallBytes = 16384;  // columns below which a ragged launch uses the byte kernel alone
+constexpr uint64_t kLinePeelMinBytes = uint64_t(256) << 20;  // head peel (launch_gf_tables) from this many columns
 // Division by a launch-invariant divisor with a multiply-high (Granlund and
 // Montgomery): q = (t + ((n - t) >> s1)) >> s2, t = mulhi(n, m), exact for all
 // 32-bit n.  The block -> (stripe, chunk) map divides wave-uniform values, and
@@ -1805,18 +1806,45 @@ hipError_t launch_gf_tables(const Geometry &g, const DevPlan &p, Mode mode, int 
                          (g.n_stripes == 1 || g.stripe_stride % 16 == 0);
     const bool aligned8 = (reinterpret_cast<uintptr_t>(base) % 8 == 0) && g.shard_stride % 8 == 0 &&
                           (g.n_stripes == 1 || g.stripe_stride % 8 == 0);
-    // A batch 8 bytes off a 16-byte boundary with 16-byte strides (a shard-major
-    // recovery run that starts at an odd 1000-byte group,
-    // rs_decode_groups_shard_major_dev): the first 8 columns on the byte
-    // kernel, the rest on the 16-byte kernels, instead of all of it on the
-    // 8-byte kernels (0.67 of peak for a 2 GB run).
-    if (!aligned && reinterpret_cast<uintptr_t>(base) % 16 == 8 && g.shard_stride % 16 == 0 &&
-        (g.n_stripes == 1 || g.stripe_stride % 16 == 0) && g.len >= kSmallBytes) {
-        hipError_t e = launch_bytes(g, p, g.col0, 8, mode, mismatch, s);
+    // Head peel: the first columns on the byte kernel, so the rest starts on a
+    // boundary every shard shares (strides its multiples).
+    //  * For batches of >= 256 MiB of columns: a wave's 1 KiB (else a 128-B
+    //    line, for strides that are line but not 1 KiB multiples), so each
+    //    wave covers whole lines instead of sharing a partial line with each
+    //    neighbour; at most 1/1024 of a shard is peeled.  4+2 x 1 MiB x 1024
+    //    stripes 16 / 112 / 1008 B past a line: 0.72 / 0.71 / 0.71 of peak
+    //    unpeeled, 0.855 / 0.855 / 0.865 peeled to 1 KiB (0.848 / 0.848 /
+    //    0.864 to 128 B; 0.867 line-aligned).  A shard-major recovery run that
+    //    starts at group 2 M + 1 (rs_decode_groups_shard_major_dev) 0.674 ->
+    //    0.795 (profiles/r4/line_peel_r4p.txt).
+    //  * Else 16 B for a batch 8 bytes off (then the 16-byte kernels, not the
+    //    8-byte ones).
+    // RSAMD_LINE_PEEL (TUNING builds): 0 = no line peel, A = peel to A only.
+    const uintptr_t addr = reinterpret_cast<uintptr_t>(base);
+    auto strides_multiple = [&](size_t a) {
+        return g.shard_stride % a == 0 && (g.n_stripes == 1 || g.stripe_stride % a == 0);
+    };
+    size_t peel = 0;
+    if (uint64_t(g.n_stripes) * g.len >= kLinePeelMinBytes) {
+        const size_t forced = tuning_size("RSAMD_LINE_PEEL", SIZE_MAX);
+        const size_t order[2] = {forced != SIZE_MAX ? forced : 1024, forced != SIZE_MAX ? forced : 128};
+        for (size_t line : order) {
+            if (line == 0 || !strides_multiple(line)) continue;
+            if (addr % line == 0) break;  // already on the boundary
+            const size_t n = line - addr % line;
+            if (n * 1024 <= g.len) {
+                peel = n;
+                break;
+            }
+        }
+    }
+    if (!peel && addr % 16 == 8 && strides_multiple(16) && g.len >= kSmallBytes) peel = 8;
+    if (peel) {
+        hipError_t e = launch_bytes(g, p, g.col0, peel, mode, mismatch, s);
         if (e != hipSuccess) return e;
         Geometry rest = g;
-        rest.col0 += 8;
-        rest.len -= 8;
+        rest.col0 += peel;
+        rest.len -= peel;
         return launch_gf_tables(rest, p, mode, mismatch, s);
     }
     if (aligned8 && !aligned && mode == Mode::Code && uint64_t(g.n_stripes) * g.len > kSmallBytes &&

@@ -1,0 +1,101 @@
+"""The head peel of launch_gf_tables (kernels.hip): a batch of >= 256 MiB of
+columns whose base is not on a 1 KiB / 128 B boundary codes its first columns
+on the byte kernel and the rest on the 16-byte kernels from the boundary.
+Results must not depend on where the batch sits: every byte at every offset
+equals the line-aligned batch, which is checked against the oracle."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+K, M, S, B = 4, 2, 1 << 20, 256  # 256 MiB of columns: the peel's threshold
+T = K + M
+
+
+def _oracle_stripe(oracle_lib, host, lay, t):
+    rows = [host[t * lay.stripe_stride + i * lay.shard_stride:][:S].copy() for i in range(K)]
+    rows += [np.zeros(S, np.uint8) for _ in range(M)]
+    oracle_lib.Codec(K, M).encode_parity(rows, 0, S)
+    return rows[K:]
+
+
+def test_misaligned_batches_equal_the_aligned_batch(gpu, oracle_lib):
+    import torch
+    import rsamd
+    from rsamd import device
+    from rsamd.device import StripeLayout
+    rs = rsamd.ReedSolomon.create(K, M)
+    lay = StripeLayout.packed(B, T, S)
+    st = torch.cuda.current_stream()
+    pool = torch.empty(lay.nbytes + 4096, dtype=torch.uint8, device="cuda:0")
+    base0 = pool.data_ptr()
+    assert base0 % 4096 == 0
+    device.fill_synthetic(base0, K, lay, 0xD15C, 0, st)
+    device.encode(rs, base0, lay, st)
+    want = pool[: lay.nbytes].clone()
+    host = want.cpu().numpy()
+    for t in (0, 1, B - 1):
+        for p, par in enumerate(_oracle_stripe(oracle_lib, host, lay, t)):
+            off = t * lay.stripe_stride + (K + p) * lay.shard_stride
+            assert np.array_equal(host[off: off + S], par), (t, p)
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    view = lambda o: pool[o: o + lay.nbytes].view(B, T, lay.shard_stride)  # noqa: E731
+    for o in (8, 16, 112, 1008, 2056):
+        b = base0 + o
+        v = view(o)
+        pool.fill_(0x5A)
+        device.fill_synthetic(b, K, lay, 0xD15C, 0, st)
+        device.encode(rs, b, lay, st)
+        assert torch.equal(pool[o: o + lay.nbytes], want), ("encode", o)
+        # decode {0,1}: the peeled head columns come back too
+        v[:, 0:2, :S].fill_(0x3C)
+        device.decode(rs, b, [False, False, True, True, True, True], lay, st)
+        assert torch.equal(pool[o: o + lay.nbytes], want), ("decode", o)
+        # verify passes, then sees one wrong byte inside the peeled head
+        flag.zero_()
+        device.verify(rs, b, lay, flag.data_ptr(), st)
+        assert int(flag.item()) == 0, o
+        v[7, K + 1, 3] ^= 1
+        device.verify(rs, b, lay, flag.data_ptr(), st)
+        assert int(flag.item()) != 0, o
+        v[7, K + 1, 3] ^= 1
+        # nothing outside the batch was written
+        assert int((pool[:o] != 0x5A).sum()) == 0 and int((pool[o + lay.nbytes:] != 0x5A).sum()) == 0
+    del pool, want
+    torch.cuda.empty_cache()
+
+
+def test_shard_major_run_past_a_line_at_scale(gpu, oracle_lib):
+    """The master's offline set grows at odd group 300 033 of 600 064 (the
+    second run, 300 MB per server, starts 1000 B past a 1 KiB boundary):
+    every chunk comes back, and the groups around the failure match the
+    oracle's parity."""
+    import torch
+    import rsamd
+    from rsamd import device
+    from rsamd.device import StripeLayout
+    from rsamd.recovery import recover_groups_shard_major_dev
+    chunk, N, j = 1000, 600_064, 300_033
+    rs = rsamd.ReedSolomon.create(K, M)
+    lay = StripeLayout(1, N * chunk, N * chunk, T * N * chunk)
+    st = torch.cuda.current_stream()
+    buf = torch.empty(lay.nbytes, dtype=torch.uint8, device="cuda:0")
+    device.fill_synthetic(buf.data_ptr(), K, lay, 0x6A57E2, 0, st)
+    device.encode(rs, buf.data_ptr(), lay, st)
+    want = buf.clone()
+    v = buf.view(T, N * chunk)
+    present = np.ones((N, T), bool)
+    for g0, g1, miss in [(0, j, (0,)), (j, N, (0, 3))]:
+        present[g0:g1, list(miss)] = False
+        for s in miss:
+            v[s, g0 * chunk: g1 * chunk].fill_(0x3C)
+    recover_groups_shard_major_dev(buf.data_ptr(), N * chunk, present, chunk, st)
+    assert torch.equal(buf, want)
+    w = want.view(T, N, chunk)[:, j - 2: j + 3].cpu().numpy()
+    for g in range(5):
+        rows = [w[i, g].copy() for i in range(K)] + [np.zeros(chunk, np.uint8) for _ in range(M)]
+        oracle_lib.Codec(K, M).encode_parity(rows, 0, chunk)
+        for p in range(M):
+            assert np.array_equal(w[K + p, g], rows[K + p]), (g, p)
+    del buf, want, v
+    torch.cuda.empty_cache()
