@@ -1721,6 +1721,44 @@ hipError_t launch_masked8(const Geometry &g, const MaskedPlan &p, const MaskedRe
     return hipSuccess;
 }
 
+// Columns to code on the byte kernel before the vector kernels (0: none).
+size_t head_peel(const Geometry &g) {
+    // Head peel: the first columns on the byte kernel, so the rest starts on a
+    // boundary every shard shares (strides its multiples).
+    //  * For batches of >= 256 MiB of columns: a wave's 1 KiB (else a 128-B
+    //    line, for strides that are line but not 1 KiB multiples), so each
+    //    wave covers whole lines instead of sharing a partial line with each
+    //    neighbour; at most 1/1024 of a shard is peeled.  4+2 x 1 MiB x 1024
+    //    stripes 16 / 112 / 1008 B past a line: 0.72 / 0.71 / 0.71 of peak
+    //    unpeeled, 0.855 / 0.855 / 0.865 peeled to 1 KiB (0.848 / 0.848 /
+    //    0.864 to 128 B; 0.867 line-aligned).  A shard-major recovery run that
+    //    starts at group 2 M + 1 (rs_decode_groups_shard_major_dev) 0.674 ->
+    //    0.795 (profiles/r4/line_peel_r4p.txt).
+    //  * Else 16 B for a batch 8 bytes off (then the 16-byte kernels, not the
+    //    8-byte ones).
+    // RSAMD_LINE_PEEL (TUNING builds): 0 = no line peel, A = peel to A only.
+    const uintptr_t addr = reinterpret_cast<uintptr_t>(g.base + g.col0);
+    auto strides_multiple = [&](size_t a) {
+        return g.shard_stride % a == 0 && (g.n_stripes == 1 || g.stripe_stride % a == 0);
+    };
+    size_t peel = 0;
+    if (uint64_t(g.n_stripes) * g.len >= kLinePeelMinBytes) {
+        const size_t forced = tuning_size("RSAMD_LINE_PEEL", SIZE_MAX);
+        const size_t order[2] = {forced != SIZE_MAX ? forced : 1024, forced != SIZE_MAX ? forced : 128};
+        for (size_t line : order) {
+            if (line == 0 || !strides_multiple(line)) continue;
+            if (addr % line == 0) break;  // already on the boundary
+            const size_t n = line - addr % line;
+            if (n * 1024 <= g.len) {
+                peel = n;
+                break;
+            }
+        }
+    }
+    if (!peel && addr % 16 == 8 && strides_multiple(16) && g.len >= kSmallBytes) peel = 8;
+    return peel;
+}
+
 }  // namespace
 
 MaskedRecordLayout masked_record_layout(int nin, int mslots) {
@@ -1737,8 +1775,9 @@ hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t 
     if (p.mslots < 1 || p.mslots > kMaxOut || p.nin < 1) return hipErrorInvalidValue;
     const MaskedRecordLayout l = masked_record_layout(p.nin, p.mslots);
     uint8_t *base = g.base + g.col0;
+    // (one stripe: its stripe stride is never used)
     const bool aligned = (reinterpret_cast<uintptr_t>(base) % 16 == 0) && g.shard_stride % 16 == 0 &&
-                         g.stripe_stride % 16 == 0;
+                         (g.n_stripes == 1 || g.stripe_stride % 16 == 0);
     // Patterns per logical stripe: the vector kernels need every 1 KiB chunk
     // inside one pattern (rows of whole 1 KiB chunks, patterns of whole rows
     // or of whole chunks) and the batch's chunk count in 32 bits.
@@ -1748,7 +1787,17 @@ hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t 
                                      (pb % g.len == 0 || g.len % pb == 0) &&
                                      g.n_stripes * (g.len / chunk_bytes) <= UINT32_MAX);
     const bool aligned8 = (reinterpret_cast<uintptr_t>(base) % 8 == 0) && g.shard_stride % 8 == 0 &&
-                          g.stripe_stride % 8 == 0;
+                          (g.n_stripes == 1 || g.stripe_stride % 8 == 0);
+    // Head peel as launch_gf_tables (per-stripe patterns only: granule
+    // patterns are tied to the columns' 1 KiB chunks).
+    if (const size_t peel = pb == 0 ? head_peel(g) : 0) {
+        hipError_t e = launch_masked_bytes(g, p, l, g.col0, peel, s);
+        if (e != hipSuccess) return e;
+        Geometry rest = g;
+        rest.col0 += peel;
+        rest.len -= peel;
+        return launch_gf_masked(rest, p, s);
+    }
     // (the line-owner kernel reads a stripe's outputs off its bitmask: a
     // pattern table, and every pattern's absent shards in one launch group)
     if (aligned8 && !aligned && pb == 0 && p.mask_table && g.total > 0 && p.mslots >= g.total - p.nin &&
@@ -1806,39 +1855,8 @@ hipError_t launch_gf_tables(const Geometry &g, const DevPlan &p, Mode mode, int 
                          (g.n_stripes == 1 || g.stripe_stride % 16 == 0);
     const bool aligned8 = (reinterpret_cast<uintptr_t>(base) % 8 == 0) && g.shard_stride % 8 == 0 &&
                           (g.n_stripes == 1 || g.stripe_stride % 8 == 0);
-    // Head peel: the first columns on the byte kernel, so the rest starts on a
-    // boundary every shard shares (strides its multiples).
-    //  * For batches of >= 256 MiB of columns: a wave's 1 KiB (else a 128-B
-    //    line, for strides that are line but not 1 KiB multiples), so each
-    //    wave covers whole lines instead of sharing a partial line with each
-    //    neighbour; at most 1/1024 of a shard is peeled.  4+2 x 1 MiB x 1024
-    //    stripes 16 / 112 / 1008 B past a line: 0.72 / 0.71 / 0.71 of peak
-    //    unpeeled, 0.855 / 0.855 / 0.865 peeled to 1 KiB (0.848 / 0.848 /
-    //    0.864 to 128 B; 0.867 line-aligned).  A shard-major recovery run that
-    //    starts at group 2 M + 1 (rs_decode_groups_shard_major_dev) 0.674 ->
-    //    0.795 (profiles/r4/line_peel_r4p.txt).
-    //  * Else 16 B for a batch 8 bytes off (then the 16-byte kernels, not the
-    //    8-byte ones).
-    // RSAMD_LINE_PEEL (TUNING builds): 0 = no line peel, A = peel to A only.
-    const uintptr_t addr = reinterpret_cast<uintptr_t>(base);
-    auto strides_multiple = [&](size_t a) {
-        return g.shard_stride % a == 0 && (g.n_stripes == 1 || g.stripe_stride % a == 0);
-    };
-    size_t peel = 0;
-    if (uint64_t(g.n_stripes) * g.len >= kLinePeelMinBytes) {
-        const size_t forced = tuning_size("RSAMD_LINE_PEEL", SIZE_MAX);
-        const size_t order[2] = {forced != SIZE_MAX ? forced : 1024, forced != SIZE_MAX ? forced : 128};
-        for (size_t line : order) {
-            if (line == 0 || !strides_multiple(line)) continue;
-            if (addr % line == 0) break;  // already on the boundary
-            const size_t n = line - addr % line;
-            if (n * 1024 <= g.len) {
-                peel = n;
-                break;
-            }
-        }
-    }
-    if (!peel && addr % 16 == 8 && strides_multiple(16) && g.len >= kSmallBytes) peel = 8;
+    // Head peel (head_peel): the rest starts on a boundary every shard shares.
+    const size_t peel = head_peel(g);
     if (peel) {
         hipError_t e = launch_bytes(g, p, g.col0, peel, mode, mismatch, s);
         if (e != hipSuccess) return e;

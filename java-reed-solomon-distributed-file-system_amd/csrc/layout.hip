@@ -438,8 +438,8 @@ struct EncTileArgs {
     uint32_t xcd_span;     // block order (file_block)
 };
 
-template <int K, int M>
-__global__ void __launch_bounds__(kTileThreads) file_encode_tiled_kernel(EncTileArgs a) {
+template <int K, int M, int THREADS, int SLOTS>
+__global__ void __launch_bounds__(THREADS) file_encode_tiled_kernel(EncTileArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
     const uint64_t r0 = uint64_t(file_block(a.xcd_span)) * a.rows;
     const uint32_t rows = uint32_t(min(uint64_t(a.rows), a.n_rows - r0));
@@ -455,12 +455,12 @@ __global__ void __launch_bounds__(kTileThreads) file_encode_tiled_kernel(EncTile
 #pragma unroll
             for (int j = 0; j < 5; ++j) T[p][i][j] = *RSAMD_G(a.tabs + ((i * M + p) * 5 + j), 4);
 
-    // Phase 1: run <= kTileSlots * 256 * 16 * K bytes, so 2K loads per thread.
-    constexpr int NL = kTileSlots * K;
+    // Phase 1: run <= SLOTS * THREADS * 16 * K bytes, so SLOTS * K loads per thread.
+    constexpr int NL = SLOTS * K;
     u32x4 v[NL];
 #pragma unroll
     for (int u = 0; u < NL; ++u) {
-        const uint32_t t = (u * kTileThreads + threadIdx.x) * 16;
+        const uint32_t t = (u * THREADS + threadIdx.x) * 16;
         const uint64_t f = f0 + t;
         v[u] = u32x4{0, 0, 0, 0};
         if (t < run) {
@@ -475,16 +475,16 @@ __global__ void __launch_bounds__(kTileThreads) file_encode_tiled_kernel(EncTile
     }
 #pragma unroll
     for (int u = 0; u < NL; ++u) {
-        const uint32_t t = (u * kTileThreads + threadIdx.x) * 16;
+        const uint32_t t = (u * THREADS + threadIdx.x) * 16;
         if (t < run) *reinterpret_cast<u32x4 *>(tile + t) = v[u];
     }
     __syncthreads();
 
-    // Phase 2: columns c of the tile's span, kTileSlots vectors per thread.
+    // Phase 2: columns c of the tile's span, SLOTS vectors per thread.
     const uint64_t col0 = r0 * a.block;
 #pragma unroll
-    for (int u = 0; u < kTileSlots; ++u) {
-        const uint32_t c = (u * kTileThreads + threadIdx.x) * 16;
+    for (int u = 0; u < SLOTS; ++u) {
+        const uint32_t c = (u * THREADS + threadIdx.x) * 16;
         if (c >= span) continue;
         const bool hi = c + 16 <= span;  // else only the 8-byte half [c, c+8) exists
         u32x4 x[K];
@@ -651,29 +651,28 @@ bool file_fusable(const FileGeom &g, bool encode) {
 
 namespace {
 
-// Decode tile shape: THREADS x SLOTS 16-byte columns per shard.
+// Tile shape: THREADS x SLOTS 16-byte columns per shard.  TUNING builds read
+// "threads,slots" from `env` at each launch (sweeps change it between legs).
 struct DecTile {
     int threads, slots;
 };
 
-DecTile dec_tile() {
-    static const DecTile v = [] {
-        const char *e = tuning_env("RSAMD_DEC_TILE");  // "threads,slots" (A/B)
-        DecTile d{kDecTileThreads, kDecTileSlots};
-        if (e) {
-            int t = 0, sl = 0;
-            if (std::sscanf(e, "%d,%d", &t, &sl) == 2 && (t == 128 || t == 256 || t == 512) && (sl == 1 || sl == 2))
-                d = {t, sl};
-        }
-        return d;
-    }();
-    return v;
+DecTile tile_shape(const char *env, DecTile dflt) {
+    const char *e = tuning_env(env);
+    if (e) {
+        int t = 0, sl = 0;
+        if (std::sscanf(e, "%d,%d", &t, &sl) == 2 && (t == 128 || t == 256 || t == 512) && (sl == 1 || sl == 2))
+            return {t, sl};
+    }
+    return dflt;
 }
 
+DecTile dec_tile() { return tile_shape("RSAMD_DEC_TILE", {kDecTileThreads, kDecTileSlots}); }
+DecTile enc_tile() { return tile_shape("RSAMD_ENC_TILE", {kTileThreads, kTileSlots}); }
+
 template <int K, int E>
-hipError_t launch_tiled_t(const TileArgs &a, uint64_t tiles, hipStream_t s) {
+hipError_t launch_tiled_t(const TileArgs &a, uint64_t tiles, DecTile d, hipStream_t s) {
     const size_t lds = size_t(K) * a.rows * a.block + tuning_size("RSAMD_FILE_TILE_LDS_PAD", 0);
-    const DecTile d = dec_tile();
     const dim3 grid{unsigned(tiles)}, blk{unsigned(d.threads)};
 #define RSAMD_DEC_TILE(T, SL)                                                                   \
     if (d.threads == T && d.slots == SL) {                                                      \
@@ -691,10 +690,19 @@ hipError_t launch_tiled_t(const TileArgs &a, uint64_t tiles, hipStream_t s) {
 }
 
 template <int K, int M>
-hipError_t launch_enc_tiled_t(const EncTileArgs &a, uint64_t tiles, hipStream_t s) {
+hipError_t launch_enc_tiled_t(const EncTileArgs &a, uint64_t tiles, DecTile d, hipStream_t s) {
     const size_t lds = size_t(K) * a.rows * a.block + tuning_size("RSAMD_FILE_TILE_LDS_PAD", 0);
-    hipLaunchKernelGGL((file_encode_tiled_kernel<K, M>), dim3(unsigned(tiles)), dim3(kTileThreads), lds, s, a);
-    return hipGetLastError();
+    const dim3 grid{unsigned(tiles)}, blk{unsigned(d.threads)};
+#define RSAMD_ENC_TILE(T, SL)                                                                   \
+    if (d.threads == T && d.slots == SL) {                                                      \
+        hipLaunchKernelGGL((file_encode_tiled_kernel<K, M, T, SL>), grid, blk, lds, s, a);      \
+        return hipGetLastError();                                                               \
+    }
+    RSAMD_ENC_TILE(256, 2)
+    RSAMD_ENC_TILE(512, 2)
+    RSAMD_ENC_TILE(512, 1)
+#undef RSAMD_ENC_TILE
+    return hipErrorInvalidValue;
 }
 
 // A tile spans R * block <= slots * threads * 16 columns (R even, >= 2), so
@@ -715,19 +723,20 @@ hipError_t launch_file_encode_fused(const FileGeom &g, const DevPlan *parity0, h
     // (profiles/r1/file_decode_ab/).
     // RSAMD_FILE_ENCODE=1 selects it (A/B).
     const char *mode = tuning_env("RSAMD_FILE_ENCODE");
-    uint32_t R = tile_rows(g);
-    if (R && (g.S / g.block + R - 1) / R * uint64_t(kTileThreads) > UINT32_MAX) R = 0;  // grid > 2^32 work-items
+    const DecTile d = enc_tile();
+    uint32_t R = tile_rows(g, d.threads, d.slots);
+    if (R && (g.S / g.block + R - 1) / R * uint64_t(d.threads) > UINT32_MAX) R = 0;  // grid > 2^32 work-items
     if (R && aligned(g.file, 16) && mode && mode[0] == '1') {
         EncTileArgs a{g.file, g.file_len, g.shards, g.shard_stride, g.S / g.block, uint32_t(g.block), R,
                       uint32_t((uint64_t(1) << 32) / g.block + 1), parity0 ? parity0->tabs : nullptr, 0};
         const uint64_t tiles = (a.n_rows + R - 1) / R;
         a.xcd_span = file_xcd_span(tiles);
         switch (parity0 ? parity0->nout : 0) {
-        case 0: return launch_enc_tiled_t<4, 0>(a, tiles, s);
-        case 1: return launch_enc_tiled_t<4, 1>(a, tiles, s);
-        case 2: return launch_enc_tiled_t<4, 2>(a, tiles, s);
-        case 3: return launch_enc_tiled_t<4, 3>(a, tiles, s);
-        case 4: return launch_enc_tiled_t<4, 4>(a, tiles, s);
+        case 0: return launch_enc_tiled_t<4, 0>(a, tiles, d, s);
+        case 1: return launch_enc_tiled_t<4, 1>(a, tiles, d, s);
+        case 2: return launch_enc_tiled_t<4, 2>(a, tiles, d, s);
+        case 3: return launch_enc_tiled_t<4, 3>(a, tiles, d, s);
+        case 4: return launch_enc_tiled_t<4, 4>(a, tiles, d, s);
         }
         return hipErrorInvalidValue;
     }
@@ -747,8 +756,9 @@ hipError_t launch_file_encode_fused(const FileGeom &g, const DevPlan *parity0, h
 
 hipError_t launch_file_decode_fused(const FileGeom &g, const FileDecodePlan &p, hipStream_t s) {
     if (g.S == 0 || g.file_len == 0) return hipSuccess;
-    uint32_t R = tile_rows(g, dec_tile().threads, dec_tile().slots);
-    if (R && (g.S / g.block + R - 1) / R * uint64_t(dec_tile().threads) > UINT32_MAX) R = 0;  // grid > 2^32 work-items
+    const DecTile d = dec_tile();
+    uint32_t R = tile_rows(g, d.threads, d.slots);
+    if (R && (g.S / g.block + R - 1) / R * uint64_t(d.threads) > UINT32_MAX) R = 0;  // grid > 2^32 work-items
     const char *mode = tuning_env("RSAMD_FILE_DECODE");
     if (R && !(mode && mode[0] == '0')) {  // RSAMD_FILE_DECODE=0 selects the untiled kernel (A/B only)
         TileArgs a{g.file_out, g.file_len, g.shards, g.shard_stride, g.S / g.block, uint32_t(g.block), R,
@@ -757,11 +767,11 @@ hipError_t launch_file_decode_fused(const FileGeom &g, const FileDecodePlan &p, 
         const uint64_t tiles = (a.n_rows + R - 1) / R;
         a.xcd_span = file_xcd_span(tiles);
         switch (p.n_missing_data) {
-        case 0: return launch_tiled_t<4, 0>(a, tiles, s);
-        case 1: return launch_tiled_t<4, 1>(a, tiles, s);
-        case 2: return launch_tiled_t<4, 2>(a, tiles, s);
-        case 3: return launch_tiled_t<4, 3>(a, tiles, s);
-        case 4: return launch_tiled_t<4, 4>(a, tiles, s);
+        case 0: return launch_tiled_t<4, 0>(a, tiles, d, s);
+        case 1: return launch_tiled_t<4, 1>(a, tiles, d, s);
+        case 2: return launch_tiled_t<4, 2>(a, tiles, d, s);
+        case 3: return launch_tiled_t<4, 3>(a, tiles, d, s);
+        case 4: return launch_tiled_t<4, 4>(a, tiles, d, s);
         }
         return hipErrorInvalidValue;
     }

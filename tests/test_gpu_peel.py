@@ -99,3 +99,39 @@ def test_shard_major_run_past_a_line_at_scale(gpu, oracle_lib):
             assert np.array_equal(w[K + p, g], rows[K + p]), (g, p)
     del buf, want, v
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("o", [8, 112])
+def test_masked_patterns_on_a_misaligned_batch(gpu, o):
+    """Per-stripe presence patterns (host flags and device bitmasks) on a
+    batch o bytes past a line: the masked launches peel their head too."""
+    import itertools
+    import torch
+    import rsamd
+    from rsamd import device
+    from rsamd.device import StripeLayout, presence_bits
+    rs = rsamd.ReedSolomon.create(K, M)
+    lay = StripeLayout.packed(B, T, S)
+    st = torch.cuda.current_stream()
+    pool = torch.full((lay.nbytes + 4096,), 0x5A, dtype=torch.uint8, device="cuda:0")
+    b = pool.data_ptr() + o
+    device.fill_synthetic(b, K, lay, 0xBEEF, 0, st)
+    device.encode(rs, b, lay, st)
+    want = pool.clone()
+    allp = np.array([[i not in miss for i in range(T)] for e in range(M + 1)
+                     for miss in itertools.combinations(range(T), e)], dtype=bool)
+    pats = allp[np.random.default_rng(o).integers(0, len(allp), B)]
+    v = pool[o: o + lay.nbytes].view(B, T, lay.shard_stride)
+    mask = torch.from_numpy(~pats).to("cuda:0")
+    for bits in (False, True):
+        v.masked_fill_(mask[:, :, None], 0x3C)
+        if bits:
+            words = torch.from_numpy(presence_bits(pats).view(np.int32)).to("cuda:0")
+            bad = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+            device.decode_masked_bits(rs, b, words.data_ptr(), lay, bad.data_ptr(), st)
+            assert int(bad.item()) == 0
+        else:
+            device.decode_masked(rs, b, pats, lay, st)
+        assert torch.equal(pool, want), bits
+    del pool, want, v, mask
+    torch.cuda.empty_cache()
