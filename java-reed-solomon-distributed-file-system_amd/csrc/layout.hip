@@ -661,7 +661,7 @@ DecTile tile_shape(const char *env, DecTile dflt) {
     const char *e = tuning_env(env);
     if (e) {
         int t = 0, sl = 0;
-        if (std::sscanf(e, "%d,%d", &t, &sl) == 2 && (t == 128 || t == 256 || t == 512) && (sl == 1 || sl == 2))
+        if (std::sscanf(e, "%d,%d", &t, &sl) == 2 && (t == 128 || t == 256 || t == 512 || t == 1024) && (sl == 1 || sl == 2))
             return {t, sl};
     }
     return dflt;
@@ -685,6 +685,7 @@ hipError_t launch_tiled_t(const TileArgs &a, uint64_t tiles, DecTile d, hipStrea
     RSAMD_DEC_TILE(128, 2)
     RSAMD_DEC_TILE(512, 2)
     RSAMD_DEC_TILE(128, 1)
+    RSAMD_DEC_TILE(1024, 1)
 #undef RSAMD_DEC_TILE
     return hipErrorInvalidValue;
 }
@@ -701,6 +702,7 @@ hipError_t launch_enc_tiled_t(const EncTileArgs &a, uint64_t tiles, DecTile d, h
     RSAMD_ENC_TILE(256, 2)
     RSAMD_ENC_TILE(512, 2)
     RSAMD_ENC_TILE(512, 1)
+    RSAMD_ENC_TILE(1024, 1)
 #undef RSAMD_ENC_TILE
     return hipErrorInvalidValue;
 }

@@ -20,12 +20,17 @@ PEAK = 8000.0
 ENC = [("untiled", {}),
        ("tiled_256x2_R8", {"RSAMD_FILE_ENCODE": "1", "RSAMD_ENC_TILE": "256,2"}),
        ("tiled_512x2_R16", {"RSAMD_FILE_ENCODE": "1", "RSAMD_ENC_TILE": "512,2"}),
-       ("tiled_512x1_R8", {"RSAMD_FILE_ENCODE": "1", "RSAMD_ENC_TILE": "512,1"})]
+       ("tiled_512x1_R8", {"RSAMD_FILE_ENCODE": "1", "RSAMD_ENC_TILE": "512,1"}),
+       ("tiled_512x1_R8_lds48K", {"RSAMD_FILE_ENCODE": "1", "RSAMD_ENC_TILE": "512,1", "RSAMD_FILE_TILE_LDS_PAD": "16000"}),
+       ("tiled_512x1_R8_lds64K", {"RSAMD_FILE_ENCODE": "1", "RSAMD_ENC_TILE": "512,1", "RSAMD_FILE_TILE_LDS_PAD": "32000"}),
+       ("tiled_1024x1_R16", {"RSAMD_FILE_ENCODE": "1", "RSAMD_ENC_TILE": "1024,1"})]
 DEC = [("tiled_512x1_R8", {"RSAMD_DEC_TILE": "512,1"}),
        ("tiled_512x2_R16", {"RSAMD_DEC_TILE": "512,2"}),
        ("tiled_256x2_R8", {"RSAMD_DEC_TILE": "256,2"}),
-       ("tiled_256x1_R4", {"RSAMD_DEC_TILE": "256,1"})]
-KNOBS = ("RSAMD_FILE_ENCODE", "RSAMD_ENC_TILE", "RSAMD_DEC_TILE")
+       ("tiled_256x1_R4", {"RSAMD_DEC_TILE": "256,1"}),
+       ("tiled_512x1_R8_lds48K", {"RSAMD_DEC_TILE": "512,1", "RSAMD_FILE_TILE_LDS_PAD": "16000"}),
+       ("tiled_1024x1_R16", {"RSAMD_DEC_TILE": "1024,1"})]
+KNOBS = ("RSAMD_FILE_ENCODE", "RSAMD_ENC_TILE", "RSAMD_DEC_TILE", "RSAMD_FILE_TILE_LDS_PAD")
 
 
 def timed(torch, st, fn, iters=5, warm_s=0.4):
