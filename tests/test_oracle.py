@@ -3,7 +3,11 @@ against it.
 
 Evidence used:
   * the literal LOG/EXP tables of Galois.java:58-169 (tests/golden/galois_tables.json);
-  * the upstream Backblaze 5+5 known-answer vector;
+  * the upstream Backblaze 5+5 known-answer vector, and the upstream library's
+    Galois / Matrix known answers (multiply, exp, 3x3 and 5x5 inverses,
+    a 2x2 product), recalled from its published tests -- none of these is in
+    /root/reference, so they cross-check the oracle built from its literal
+    tables rather than replace the fixtures;
   * the reference's own round-trip tests, ReedSolomonTest.java:70-93 (0 erasures
     and erasures {0 (DataDiskOne), 5 (ParityDiskTwo)}), on seeded data instead
     of 200 MB of unseeded java.util.Random;
@@ -49,6 +53,26 @@ def test_galois_scalar_semantics(oracle_lib):
     out = (C.c_int * 256)()
     n = L.orc_all_possible_polynomials(out)
     assert list(out)[:n] == [29, 43, 45, 77, 95, 99, 101, 105, 113, 135, 141, 169, 195, 207, 231, 245]
+
+
+def test_upstream_galois_and_matrix_known_answers(oracle_lib):
+    """The Galois / Matrix known answers of the JavaReedSolomon library the
+    reference vendors (Galois.java, Matrix.java:191-344), recalled from its
+    published tests; both restatements must give them."""
+    L = oracle_lib.lib()
+    for f in (nr.gal_multiply, L.orc_gal_multiply):
+        assert (f(3, 4), f(7, 7), f(23, 45)) == (12, 21, 41)
+    for f in (nr.gal_exp, L.orc_gal_exp):
+        assert (f(2, 2), f(5, 20), f(13, 7)) == (4, 235, 43)
+    m = np.array([[56, 23, 98], [3, 100, 200], [45, 201, 123]], np.uint8)
+    m5 = np.array([[1, 0, 0, 0, 0], [0, 1, 0, 0, 0], [0, 0, 0, 1, 0], [0, 0, 0, 0, 1], [7, 7, 6, 6, 1]], np.uint8)
+    for inv in (nr.matrix_invert, oracle_lib.matrix_invert):
+        assert inv(m).tolist() == [[175, 133, 33], [130, 13, 245], [112, 35, 126]]
+        assert inv(m5).tolist() == [[1, 0, 0, 0, 0], [0, 1, 0, 0, 0], [123, 123, 1, 122, 122],
+                                    [0, 0, 1, 0, 0], [0, 0, 0, 1, 0]]
+    assert nr.matrix_times(m, nr.matrix_invert(m)).tolist() == np.eye(3, dtype=int).tolist()
+    assert nr.matrix_times(np.array([[1, 2], [3, 4]], np.uint8),
+                           np.array([[5, 6], [7, 8]], np.uint8)).tolist() == [[11, 22], [19, 42]]
 
 
 def test_known_answer_5_5(oracle_lib):
