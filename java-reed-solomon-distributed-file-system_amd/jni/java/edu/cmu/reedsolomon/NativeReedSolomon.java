@@ -65,6 +65,20 @@ public final class NativeReedSolomon implements AutoCloseable {
     }
 
     /**
+     * MasterImpl.recoverOfflineChunkserver's loop (MasterImpl.java:794-839)
+     * over chunk groups a GPU-side service keeps in HBM in the master's own
+     * layout: chunk g of server s at devBase + s * serverStride + g * chunkLen.
+     * present holds nGroups * getTotalShardCount() flags, group after group
+     * (nonzero: the server answered).  Every absent chunk is rebuilt in place;
+     * each run of groups with one offline set is one launch on the given HIP
+     * stream (0: the default stream).
+     */
+    public void recoverGroupsShardMajorDevice(long devBase, long serverStride, int chunkLen, long nGroups,
+                                              byte[] present, long stream) {
+        nativeRecoverGroupsShardMajorDevice(handle, devBase, serverStride, chunkLen, nGroups, present, stream);
+    }
+
+    /**
      * Frees the calling thread's GPU contexts (HIP streams, device and pinned
      * staging buffers); call from worker threads before a pool retires them.
      */
@@ -89,4 +103,7 @@ public final class NativeReedSolomon implements AutoCloseable {
     private static native void nativeDecodeMaskedBitsDevice(long h, long devBase, long devBits, long nStripes,
                                                             long shardLen, long shardStride, long stripeStride,
                                                             long devBad, long stream);
+    private static native void nativeRecoverGroupsShardMajorDevice(long h, long devBase, long serverStride,
+                                                                   int chunkLen, long nGroups, byte[] present,
+                                                                   long stream);
 }

@@ -154,3 +154,13 @@ JNIEXPORT void JNICALL Java_edu_cmu_reedsolomon_NativeReedSolomon_nativeDecodeMa
         if (c) (*env)->ThrowNew(env, c, rs_last_error_message());
     }
 }
+
+/* The master's recovery loop over device-resident chunk groups in its own
+ * layout, [server][group * chunkLen] (rs_decode_groups_shard_major_dev). */
+JNIEXPORT void JNICALL Java_edu_cmu_reedsolomon_NativeReedSolomon_nativeRecoverGroupsShardMajorDevice(
+        JNIEnv *env, jclass cls, jlong h, jlong devBase, jlong serverStride, jint chunkLen, jlong nGroups,
+        jbyteArray present, jlong stream) {
+    jenv je;
+    rsj_recover_groups_shard_major(wrap(&je, env), rsj_librsamd_backend(), CODEC(h), devBase, serverStride, chunkLen,
+                                   nGroups, present, stream);
+}

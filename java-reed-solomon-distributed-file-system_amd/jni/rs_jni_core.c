@@ -31,7 +31,8 @@
 const rsj_backend *rsj_librsamd_backend(void) {
     static const rsj_backend b = {rs_encode_parity,           rs_decode_missing,         rs_is_parity_correct,
                                   rs_code_some_shards,        rs_check_some_shards,      rs_check_buffers_and_sizes,
-                                  rs_codec_total_shard_count, rs_codec_data_shard_count, rs_last_error_message};
+                                  rs_codec_total_shard_count, rs_codec_data_shard_count, rs_last_error_message,
+                                  rs_decode_groups_shard_major_dev};
     return &b;
 }
 
@@ -465,4 +466,49 @@ int rsj_check_some_shards(rsj_env *e, const rsj_backend *b, rsj_obj rows, rsj_ob
                           rsj_obj to_check, int32_t ncheck, int32_t offset, int32_t count) {
     const int r = loop_call(e, b, rows, inputs, nin, to_check, ncheck, offset, count, 1);
     return r > 0;
+}
+
+void rsj_recover_groups_shard_major(rsj_env *e, const rsj_backend *b, const rs_codec *c, int64_t dev_base,
+                                    int64_t server_stride, int32_t chunk_len, int64_t n_groups, rsj_obj present,
+                                    int64_t stream) {
+    if (!present) {
+        e->throw_new(e, NPE, "present is null");
+        return;
+    }
+    if (server_stride < 0 || chunk_len < 0 || n_groups < 0) {
+        e->throw_new(e, IAE, "negative size");
+        return;
+    }
+    const int total = b->total_shards(c);
+    const int n = e->array_length(e, present);
+    if (total <= 0 || n_groups > INT32_MAX / total || (int64_t)n != n_groups * total) {
+        char msg[128];
+        snprintf(msg, sizeof msg, "present has %d flags; n_groups * total shards is %lld", n,
+                 (long long)n_groups * (total > 0 ? total : 0));
+        e->throw_new(e, IAE, msg);
+        return;
+    }
+    /* Pinned for the call, or copied out when the JVM will not pin. */
+    int is_copy = 0;
+    uint8_t *pinned = n ? e->critical_get(e, present, &is_copy) : NULL, *copy = NULL;
+    static const uint8_t none = 0;
+    const uint8_t *flags = pinned ? pinned : &none;
+    if (n && !pinned) {
+        copy = (uint8_t *)malloc((size_t)n);
+        if (!copy) {
+            e->throw_new(e, "java/lang/OutOfMemoryError", "present flags");
+            return;
+        }
+        e->byte_region_get(e, present, 0, n, copy);
+        if (e->exception_pending(e)) {
+            free(copy);
+            return;
+        }
+        flags = copy;
+    }
+    const int rc = b->decode_groups_shard_major(c, (uint8_t *)(uintptr_t)dev_base, (size_t)server_stride,
+                                                (size_t)chunk_len, (size_t)n_groups, flags, (void *)(uintptr_t)stream);
+    if (pinned) e->critical_release(e, present, pinned, RSJ_ABORT);
+    free(copy);
+    if (rc) throw_rc(e, b, rc);
 }

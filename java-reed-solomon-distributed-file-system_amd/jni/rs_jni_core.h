@@ -74,6 +74,7 @@ typedef struct rsj_backend {
     int (*total_shards)(const rs_codec *);
     int (*data_shards)(const rs_codec *);
     const char *(*last_error)(void);
+    int (*decode_groups_shard_major)(const rs_codec *, uint8_t *, size_t, size_t, size_t, const uint8_t *, void *);
 } rsj_backend;
 
 const rsj_backend *rsj_librsamd_backend(void);
@@ -91,6 +92,15 @@ void rsj_code_some_shards(rsj_env *e, const rsj_backend *b, rsj_obj rows, rsj_ob
                           rsj_obj outputs, int32_t nout, int32_t offset, int32_t count);
 int rsj_check_some_shards(rsj_env *e, const rsj_backend *b, rsj_obj rows, rsj_obj inputs, int32_t nin,
                           rsj_obj to_check, int32_t ncheck, int32_t offset, int32_t count);
+/* MasterImpl.recoverOfflineChunkserver's loop (MasterImpl.java:794-839) over
+ * chunk groups a GPU-side service keeps in HBM in the master's own layout
+ * (rs_decode_groups_shard_major_dev): chunk g of server s at
+ * dev_base + s*server_stride + g*chunk_len; present is a byte[] of
+ * n_groups * total flags, group after group (nonzero = the server answered).
+ * The flags are pinned for the call (it only enqueues kernels on `stream`). */
+void rsj_recover_groups_shard_major(rsj_env *e, const rsj_backend *b, const rs_codec *c, int64_t dev_base,
+                                    int64_t server_stride, int32_t chunk_len, int64_t n_groups, rsj_obj present,
+                                    int64_t stream);
 
 #ifdef __cplusplus
 }

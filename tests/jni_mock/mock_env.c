@@ -244,9 +244,31 @@ static int fake_check(const uint8_t *const *rows, const uint8_t *const *in, int 
     return 0;
 }
 
+/* shard-major recovery: records its arguments and the flags it was handed */
+static struct {
+    const rs_codec *c;
+    uint64_t base, stride, chunk, n;
+    void *stream;
+    uint8_t flags[4096];
+    int rc;
+} SM;
+static int fake_shard_major(const rs_codec *c, uint8_t *base, size_t stride, size_t chunk, size_t n,
+                            const uint8_t *present, void *stream) {
+    SM.c = c;
+    SM.base = (uint64_t)(uintptr_t)base;
+    SM.stride = stride;
+    SM.chunk = chunk;
+    SM.n = n;
+    SM.stream = stream;
+    const size_t nf = n * (size_t)rs_codec_total_shard_count(c);
+    memcpy(SM.flags, present, nf < sizeof SM.flags ? nf : sizeof SM.flags);
+    return SM.rc;
+}
+
 static const rsj_backend FAKE = {fake_encode,       fake_decode,         fake_verify,
                                  fake_code,         fake_check,          rs_check_buffers_and_sizes,
-                                 rs_codec_total_shard_count, fake_data_shards, rs_last_error_message};
+                                 rs_codec_total_shard_count, fake_data_shards, rs_last_error_message,
+                                 fake_shard_major};
 
 static const rsj_backend *backend(int real) { return real ? rsj_librsamd_backend() : &FAKE; }
 
@@ -269,3 +291,17 @@ int mock_check_some_shards(int real, mobj *rows, mobj *in, int32_t nin, mobj *ch
                            int32_t cnt) {
     return rsj_check_some_shards(&ENV, backend(real), rows, in, nin, chk, nchk, off, cnt);
 }
+void mock_recover_groups_shard_major(int real, const rs_codec *c, int64_t base, int64_t stride, int32_t chunk,
+                                     int64_t n, mobj *present, int64_t stream) {
+    rsj_recover_groups_shard_major(&ENV, backend(real), c, base, stride, chunk, n, present, stream);
+}
+/* the fake's record: out[0..4] = base, stride, chunk, n, stream; flags copied to `flags` */
+void mock_shard_major_record(uint64_t *out, uint8_t *flags, int nflags) {
+    out[0] = SM.base;
+    out[1] = SM.stride;
+    out[2] = SM.chunk;
+    out[3] = SM.n;
+    out[4] = (uint64_t)(uintptr_t)SM.stream;
+    memcpy(flags, SM.flags, nflags < (int)sizeof SM.flags ? (size_t)nflags : sizeof SM.flags);
+}
+void mock_shard_major_rc(int rc) { SM.rc = rc; }

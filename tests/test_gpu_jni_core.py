@@ -85,3 +85,34 @@ def test_code_some_shards_through_shim(gpu, oracle_lib, jvm, cnt):
         assert np.array_equal(jvm.read(outs[p], S), want[p]), p
     assert jvm.lib.mock_check_some_shards(1, R, I, nin, jvm.objects(outs), nout, off, cnt) == 1
     jvm.assert_clean()
+
+
+def test_recover_groups_shard_major_through_shim(gpu, oracle_lib, native, jvm):
+    """NativeReedSolomon.recoverGroupsShardMajorDevice's marshalling over the
+    real entry point: the master's layout on the GPU, a byte[] of flags with
+    the offline set growing mid-loop, every chunk back as the oracle encoded
+    it, the flags array released untouched."""
+    import torch
+    k, m, chunk, N, j = 4, 2, 1000, 3001, 1501
+    T, L = k + m, N * chunk
+    h = C.c_void_p()
+    assert native.rs_codec_create(k, m, C.byref(h)) == 0
+    rng = np.random.default_rng(21)
+    rows = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)] + [np.zeros(L, np.uint8) for _ in range(m)]
+    oracle_lib.Codec(k, m).encode_parity(rows, 0, L)
+    want = np.concatenate(rows)
+    flags = np.ones((N, T), np.uint8)
+    flags[:j, 1] = 0
+    flags[j:, [1, 4]] = 0
+    host = want.copy()
+    host[1 * L: 2 * L] = 0x3C
+    host[4 * L + j * chunk: 5 * L] = 0x3C
+    dev = torch.from_numpy(host).to("cuda:0")
+    fl = jvm.bytes(flags.ravel())
+    jvm.lib.mock_recover_groups_shard_major(1, h, dev.data_ptr(), L, chunk, N, fl, 0)
+    assert jvm.exception() == ("", "")
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy(), want)
+    assert np.array_equal(jvm.read(fl, N * T), flags.ravel())
+    jvm.assert_clean()
+    native.rs_codec_destroy(h)

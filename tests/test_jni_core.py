@@ -51,6 +51,10 @@ def build_mock():
         ("mock_is_parity_correct", C.c_int, [C.c_int, P, P, C.c_int32, C.c_int32, P]),
         ("mock_code_some_shards", None, [C.c_int, P, P, C.c_int32, P, C.c_int32, C.c_int32, C.c_int32]),
         ("mock_check_some_shards", C.c_int, [C.c_int, P, P, C.c_int32, P, C.c_int32, C.c_int32, C.c_int32]),
+        ("mock_recover_groups_shard_major", None,
+         [C.c_int, P, C.c_int64, C.c_int64, C.c_int32, C.c_int64, P, C.c_int64]),
+        ("mock_shard_major_record", None, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint8), C.c_int]),
+        ("mock_shard_major_rc", None, [C.c_int]),
     ]:
         fn = getattr(lib, name)
         fn.restype, fn.argtypes = res, args
@@ -388,4 +392,54 @@ def test_real_backend_without_gpu_throws_illegal_state(jvm, codec42, native):
     assert jvm.exception()[0] == ISE
     for i in range(6):
         assert np.array_equal(jvm.read(arrs[i], 100), data[i])
+    jvm.assert_clean()
+
+
+# ---- recoverGroupsShardMajorDevice (rs_decode_groups_shard_major_dev) ----
+
+@pytest.mark.parametrize("pin", ["critical", "copy_fallback"])
+def test_shard_major_marshalling(jvm, codec42, pin):
+    """The flags reach the entry point as one byte per shard per group, with
+    the device pointer, strides and stream as given; the array is released
+    without a copy-back (or copied out when the JVM will not pin it)."""
+    n = 7
+    flags = np.random.default_rng(3).integers(0, 3, n * 6).astype(np.uint8)
+    jvm.lib.mock_shard_major_rc(0)
+    jvm.lib.mock_fail_critical(1 if pin == "copy_fallback" else 0)
+    jvm.lib.mock_recover_groups_shard_major(0, codec42, 1 << 40, 123456, 1000, n, jvm.bytes(flags), 0xABC)
+    jvm.lib.mock_fail_critical(0)
+    assert jvm.exception() == ("", "")
+    rec = (C.c_uint64 * 5)()
+    got = (C.c_uint8 * len(flags))()
+    jvm.lib.mock_shard_major_record(rec, got, len(flags))
+    assert list(rec) == [1 << 40, 123456, 1000, n, 0xABC]
+    assert bytes(got) == flags.tobytes()
+    st = jvm.assert_clean()
+    assert st["commits"] == 0
+
+
+def test_shard_major_argument_errors(jvm, codec42):
+    jvm.lib.mock_recover_groups_shard_major(0, codec42, 1 << 20, 6000, 1000, 2, None, 0)
+    assert jvm.exception() == (NPE, "present is null")
+    jvm.lib.mock_reset()
+    jvm.lib.mock_recover_groups_shard_major(0, codec42, 1 << 20, 6000, 1000, 2, jvm.bytes(np.ones(11, np.uint8)), 0)
+    assert jvm.exception() == (IAE, "present has 11 flags; n_groups * total shards is 12")
+    jvm.lib.mock_reset()
+    jvm.lib.mock_recover_groups_shard_major(0, codec42, 1 << 20, -1, 1000, 2, jvm.bytes(np.ones(12, np.uint8)), 0)
+    assert jvm.exception() == (IAE, "negative size")
+    jvm.lib.mock_reset()
+    jvm.lib.mock_shard_major_rc(-9)  # RS_E_HIP from the entry point -> IllegalStateException
+    jvm.lib.mock_recover_groups_shard_major(0, codec42, 1 << 20, 6000, 1000, 2, jvm.bytes(np.ones(12, np.uint8)), 0)
+    assert jvm.exception()[0] == ISE
+    jvm.lib.mock_shard_major_rc(0)
+    jvm.assert_clean()
+
+
+def test_shard_major_real_backend_rejects_before_any_work(jvm, codec42):
+    """Through librsamd (no device needed: every group is validated first):
+    a group with fewer than k servers is the reference's exception."""
+    flags = np.ones((3, 6), np.uint8)
+    flags[1, :3] = 0
+    jvm.lib.mock_recover_groups_shard_major(1, codec42, 1 << 20, 3000, 1000, 3, jvm.bytes(flags.ravel()), 0)
+    assert jvm.exception() == (IAE, "Not enough shards present")
     jvm.assert_clean()
