@@ -20,6 +20,10 @@ Workloads (bench.py's configs):
   cgdec05 / cgdec15           ... uniform {0,5} / {1,5} decodes
   cgsmenc / cgsmdec01 / cgsmdec05  the same 4 M groups shard-major ([server][group*1000], one
                                    array per server): encode, decodes via rs_decode_groups_shard_major_dev
+  cgsmh2odd  ... {0,3} lost from group 2 M + 1 on only (one run 112 B past a line; the head
+             peel of a TUNING build is RSAMD_LINE_PEEL)    alg 6 S (B - 2 M - 1)
+  enc42off   4+2 x 1 MiB x 1024 packed, 16 B past a line, encode (with a TUNING build:
+             RSAMD_LINE_PEEL=0 codes it unpeeled, unset peels to 1 KiB)  alg 6 S B
   fenc       4 GiB file -> 4+2 shards (fused)            alg file + 6 S
   fdec_05    4+2 shards {0,5} -> 4 GiB file (tiled)      alg 4 S + file
 """
@@ -80,6 +84,16 @@ def main():
             fn = lambda: rdev.encode(rs, buf.data_ptr(), lay, st)  # noqa: E731
             alg = (k + m) * S * B
             kernel = f"gf_vec_kernel<{k}, {m}, false>"
+    elif name == "enc42off":
+        k, m, S, B = 4, 2, 1 << 20, 1024
+        rs = rsamd.ReedSolomon.create(k, m)
+        lay = StripeLayout.packed(B, k + m, S)
+        pool = torch.empty(lay.nbytes + 4096, dtype=torch.uint8, device="cuda:0")
+        b = pool.data_ptr() + 16
+        rdev.fill_synthetic(b, k, lay, SEED, 0, st)
+        fn = lambda: rdev.encode(rs, b, lay, st)  # noqa: E731
+        alg = (k + m) * S * B
+        kernel = f"gf_vec_kernel<{k}, {m}, false>"
     elif name == "maskbits":
         k, m, S, B = 4, 2, 4096, 1 << 20
         rs, lay, buf = stripes(k, m, S, B)
@@ -138,7 +152,7 @@ def main():
             fn = lambda: rdev.decode(rs, buf.data_ptr(), pres, lay, st)  # noqa: E731
         alg = 6 * S * B
         kernel = "gf_group8_kernel<4, 2, false>"
-    elif name in ("cgsmenc", "cgsmdec01", "cgsmdec05"):
+    elif name in ("cgsmenc", "cgsmdec01", "cgsmdec05", "cgsmh2odd"):
         # the master's chunk groups in its own layout: one array per server
         from rsamd.recovery import recover_groups_shard_major_dev
         k, m, S, B = 4, 2, 1000, 4 << 20
@@ -147,15 +161,22 @@ def main():
         buf = torch.empty(lay.nbytes, dtype=torch.uint8, device="cuda:0")
         rdev.fill_synthetic(buf.data_ptr(), k, lay, SEED, 0, st)
         rdev.encode(rs, buf.data_ptr(), lay, st)
+        alg = 6 * S * B
         if name == "cgsmenc":
             fn = lambda: rdev.encode(rs, buf.data_ptr(), lay, st)  # noqa: E731
             kernel = "gf_vec_kernel<4, 2, false>"
+        elif name == "cgsmh2odd":
+            g0 = B // 2 + 1
+            pres = np.ones((B, 6), bool)
+            pres[g0:, [0, 3]] = False
+            fn = lambda: recover_groups_shard_major_dev(buf.data_ptr(), lay.shard_stride, pres, S, st)  # noqa: E731
+            kernel = "gf_vec_kernel<4, 2, false>"
+            alg = 6 * S * (B - g0)
         else:
             miss = (0, 1) if name == "cgsmdec01" else (0, 5)
             pres = np.tile(np.array([i not in miss for i in range(6)]), (B, 1))
             fn = lambda: recover_groups_shard_major_dev(buf.data_ptr(), lay.shard_stride, pres, S, st)  # noqa: E731
             kernel = "gf_vec_kernel<4, 2, false>"
-        alg = 6 * S * B
     elif name == "ver104":
         k, m, S, B = 10, 4, 4 << 20, 128
         rs, lay, buf = stripes(k, m, S, B)
