@@ -11,6 +11,7 @@
 #   pmc        FETCH/WRITE_SIZE passes of the chunk-group kernels -> pmc_traffic_TAG.json
 #   probe:ARGS python3 ARGS (a tools/ probe)            -> probe_TAG_N.txt
 #   kprobe:ARGS the same under rocprofv3 --kernel-trace --stats -> kprobe_TAG_N/, kprobe_TAG_N.txt
+#   pmcc:W:C1,C2,...  one rocprofv3 --pmc pass of the given counters over pmc_workloads.py W -> pmcc_TAG.txt
 set -o pipefail
 tag=${1:?tag}
 shift
@@ -80,6 +81,14 @@ for step in "$@"; do
       alg=$(python3 -c "import json,sys; print(json.loads(sys.argv[1])['alg_bytes_per_launch'])" "$meta")
       python3 tools/pmc_summary.py "$sfx" "$kern" "$alg" "$out/pmcw_${tag}_${sfx}_FETCH_SIZE" \
           "$out/pmcw_${tag}_${sfx}_WRITE_SIZE" "$out/pmc_traffic_$tag.json" || exit 1 ;;
+    pmcc:*)  # pmcc:WORKLOAD:C1,C2,... -> one rocprofv3 --pmc pass of tools/pmc_workloads.py WORKLOAD
+      np=$((np + 1))
+      spec=${step#pmcc:}; W=${spec%%:*}; CS=${spec#*:}
+      timeout -s KILL 120 rocprofv3 --pmc ${CS//,/ } --output-format csv -d "$out/pmcc_${tag}_$np" -o run -- \
+          python3 tools/pmc_workloads.py $W > "$out/pmcc_${tag}_$np.log" 2>&1 || { tail -20 "$out/pmcc_${tag}_$np.log"; exit 1; }
+      meta=$(grep '^{' "$out/pmcc_${tag}_$np.log" | tail -1)
+      kern=$(python3 -c "import json,sys; print(json.loads(sys.argv[1])['kernel'])" "$meta")
+      echo "$meta $(python3 tools/pmc_counters.py "$out/pmcc_${tag}_$np" "$kern")" | tee -a $out/pmcc_$tag.txt ;;
     probe:*)
       np=$((np + 1))
       timeout -k 10 600 python3 ${step#probe:} > $out/probe_${tag}_$np.txt 2>&1 \
