@@ -488,27 +488,17 @@ void rsj_recover_groups_shard_major(rsj_env *e, const rsj_backend *b, const rs_c
         e->throw_new(e, IAE, msg);
         return;
     }
-    /* Pinned for the call, or copied out when the JVM will not pin. */
+    /* Pinned for the call (or the JVM's own copy: the flags are only read). */
     int is_copy = 0;
-    uint8_t *pinned = n ? e->critical_get(e, present, &is_copy) : NULL, *copy = NULL;
-    static const uint8_t none = 0;
-    const uint8_t *flags = pinned ? pinned : &none;
+    uint8_t *pinned = n ? e->critical_get(e, present, &is_copy) : NULL;
     if (n && !pinned) {
-        copy = (uint8_t *)malloc((size_t)n);
-        if (!copy) {
-            e->throw_new(e, "java/lang/OutOfMemoryError", "present flags");
-            return;
-        }
-        e->byte_region_get(e, present, 0, n, copy);
-        if (e->exception_pending(e)) {
-            free(copy);
-            return;
-        }
-        flags = copy;
+        if (!e->exception_pending(e)) e->throw_new(e, "java/lang/OutOfMemoryError", "GetPrimitiveArrayCritical failed");
+        return;
     }
+    static const uint8_t none = 0;
     const int rc = b->decode_groups_shard_major(c, (uint8_t *)(uintptr_t)dev_base, (size_t)server_stride,
-                                                (size_t)chunk_len, (size_t)n_groups, flags, (void *)(uintptr_t)stream);
+                                                (size_t)chunk_len, (size_t)n_groups, pinned ? pinned : &none,
+                                                (void *)(uintptr_t)stream);
     if (pinned) e->critical_release(e, present, pinned, RSJ_ABORT);
-    free(copy);
     if (rc) throw_rc(e, b, rc);
 }

@@ -97,7 +97,8 @@ int rsj_check_some_shards(rsj_env *e, const rsj_backend *b, rsj_obj rows, rsj_ob
  * (rs_decode_groups_shard_major_dev): chunk g of server s at
  * dev_base + s*server_stride + g*chunk_len; present is a byte[] of
  * n_groups * total flags, group after group (nonzero = the server answered).
- * The flags are pinned for the call (it only enqueues kernels on `stream`). */
+ * The flags are pinned for the call (it only enqueues kernels on `stream`);
+ * a failed pin is OutOfMemoryError, as for the shard arrays. */
 void rsj_recover_groups_shard_major(rsj_env *e, const rsj_backend *b, const rs_codec *c, int64_t dev_base,
                                     int64_t server_stride, int32_t chunk_len, int64_t n_groups, rsj_obj present,
                                     int64_t stream);
