@@ -1,6 +1,8 @@
 // codec.cpp -- see codec.hpp.
 #include "codec.hpp"
 
+#include <algorithm>
+
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
@@ -136,6 +138,13 @@ Plan::~Plan() {
 }
 
 hipError_t Plan::device_plans(std::vector<DevPlan> *out) const {
+    // The line-owner kernel (gf_group8_kernel) finds runs of consecutive
+    // output shards off out_idx and needs it ascending; every plan the codec
+    // builds is (encode: the parity rows in order; decode: the absent shards in
+    // index order), and a plan that is not never reaches a kernel.
+    if (!std::is_sorted(out_idx_.begin(), out_idx_.end()) ||
+        std::adjacent_find(out_idx_.begin(), out_idx_.end()) != out_idx_.end())
+        return hipErrorInvalidValue;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
