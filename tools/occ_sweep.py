@@ -51,7 +51,11 @@ SHAPES = [("4p2g_enc", 4, 2, 1 << 20, 4096, None, 64 << 10),
           ("4p2g128_dec05", 4, 2, 1 << 20, 4096, (0, 5), 128 << 10),
           ("10p4g16_enc", 10, 4, 4 << 20, 128, None, 16 << 10),
           ("10p4g64_enc", 10, 4, 4 << 20, 128, None, 64 << 10),
-          ("10p4g64_dec0123", 10, 4, 4 << 20, 128, (0, 1, 2, 3), 64 << 10)]
+          ("10p4g64_dec0123", 10, 4, 4 << 20, 128, (0, 1, 2, 3), 64 << 10),
+          # one stripe of 4 GB shards: the master's chunk groups shard-major (4 M x 1000 B)
+          ("4p2_1x4G_enc", 4, 2, 4096000000, 1, None, 0),
+          ("4p2_1x4G_dec0", 4, 2, 4096000000, 1, (0,), 0),
+          ("4p2_1x4G_dec01", 4, 2, 4096000000, 1, (0, 1), 0)]
 
 
 def main():
