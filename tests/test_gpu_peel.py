@@ -12,22 +12,27 @@ K, M, S, B = 4, 2, 1 << 20, 256  # 256 MiB of columns: the peel's threshold
 T = K + M
 
 
-def _oracle_stripe(oracle_lib, host, lay, t):
+def _oracle_stripe(oracle_lib, host, lay, t, K=K, M=M):
     rows = [host[t * lay.stripe_stride + i * lay.shard_stride:][:S].copy() for i in range(K)]
     rows += [np.zeros(S, np.uint8) for _ in range(M)]
     oracle_lib.Codec(K, M).encode_parity(rows, 0, S)
     return rows[K:]
 
 
-def test_misaligned_batches_equal_the_aligned_batch(gpu, oracle_lib):
+# (k, m, shard-stride pad, offsets): 1 KiB-multiple strides peel to 1 KiB; a
+# 128-B pad leaves line-multiple strides only, so those batches peel to 128 B
+@pytest.mark.parametrize("K,M,pad,offsets", [(4, 2, 0, (8, 16, 112, 1008, 2056)), (4, 2, 128, (48, 8)),
+                                             (10, 4, 0, (16, 1000))], ids=["4p2", "4p2_pad128", "10p4"])
+def test_misaligned_batches_equal_the_aligned_batch(gpu, oracle_lib, K, M, pad, offsets):
     import torch
     import rsamd
     from rsamd import device
     from rsamd.device import StripeLayout
+    T = K + M
     rs = rsamd.ReedSolomon.create(K, M)
-    lay = StripeLayout.packed(B, T, S)
+    lay = StripeLayout.packed(B, T, S, pad=pad)
     st = torch.cuda.current_stream()
-    pool = torch.empty(lay.nbytes + 4096, dtype=torch.uint8, device="cuda:0")
+    pool = torch.full((lay.nbytes + 4096,), 0x5A, dtype=torch.uint8, device="cuda:0")  # pads keep 0x5A
     base0 = pool.data_ptr()
     assert base0 % 4096 == 0
     device.fill_synthetic(base0, K, lay, 0xD15C, 0, st)
@@ -35,12 +40,13 @@ def test_misaligned_batches_equal_the_aligned_batch(gpu, oracle_lib):
     want = pool[: lay.nbytes].clone()
     host = want.cpu().numpy()
     for t in (0, 1, B - 1):
-        for p, par in enumerate(_oracle_stripe(oracle_lib, host, lay, t)):
+        for p, par in enumerate(_oracle_stripe(oracle_lib, host, lay, t, K, M)):
             off = t * lay.stripe_stride + (K + p) * lay.shard_stride
             assert np.array_equal(host[off: off + S], par), (t, p)
     flag = torch.zeros(1, dtype=torch.int32, device="cuda:0")
     view = lambda o: pool[o: o + lay.nbytes].view(B, T, lay.shard_stride)  # noqa: E731
-    for o in (8, 16, 112, 1008, 2056):
+    present = [i >= 2 for i in range(T)]
+    for o in offsets:
         b = base0 + o
         v = view(o)
         pool.fill_(0x5A)
@@ -49,7 +55,7 @@ def test_misaligned_batches_equal_the_aligned_batch(gpu, oracle_lib):
         assert torch.equal(pool[o: o + lay.nbytes], want), ("encode", o)
         # decode {0,1}: the peeled head columns come back too
         v[:, 0:2, :S].fill_(0x3C)
-        device.decode(rs, b, [False, False, True, True, True, True], lay, st)
+        device.decode(rs, b, present, lay, st)
         assert torch.equal(pool[o: o + lay.nbytes], want), ("decode", o)
         # verify passes, then sees one wrong byte inside the peeled head
         flag.zero_()
