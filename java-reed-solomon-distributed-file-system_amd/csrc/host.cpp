@@ -5,6 +5,7 @@
 #include "host.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -411,7 +412,14 @@ void release_locked(HostRegistry &reg, std::vector<uintptr_t> &held) {
     for (uintptr_t ps : held) {
         auto it = reg.regs.find(ps);
         if (it != reg.regs.end() && --it->second.second == 0) {
-            (void)hipHostUnregister(reinterpret_cast<void *>(ps));
+            const hipError_t e = hipHostUnregister(reinterpret_cast<void *>(ps));
+            if (e != hipSuccess) {  // never seen; said once, as it would leave the pages locked
+                (void)hipGetLastError();
+                static std::atomic<bool> said{false};
+                if (!said.exchange(true))
+                    std::fprintf(stderr, "librsamd: hipHostUnregister(%p) failed: %s\n", reinterpret_cast<void *>(ps),
+                                 hipGetErrorString(e));
+            }
             reg.regs.erase(it);
         }
     }

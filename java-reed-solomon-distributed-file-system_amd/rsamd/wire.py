@@ -108,7 +108,11 @@ def recover_offline_chunks(chunk_maps: Sequence[Optional[Mapping[str, bytes]]], 
     if groups == 0:
         return {}
     stride = (block + 15) // 16 * 16
-    host = np.zeros((groups, total, stride), dtype=np.uint8)
+    # Staged through page-locked host buffers (torch's pinned allocator): the
+    # copies are plain DMA, with no pageable copy for the runtime to lock in
+    # place.
+    host_t = torch.zeros(groups * total * stride, dtype=torch.uint8, pin_memory=True)
+    host = host_t.numpy().reshape(groups, total, stride)
     present = np.zeros((groups, total), dtype=bool)
     for s in range(total):
         if s in offline or not chunk_maps[s]:
@@ -117,9 +121,10 @@ def recover_offline_chunks(chunk_maps: Sequence[Optional[Mapping[str, bytes]]], 
             g = chunk_index(name) // total
             host[g, s, :block] = np.frombuffer(bytes(data), dtype=np.uint8)
             present[g, s] = True
-    dev = torch.from_numpy(host.reshape(-1)).to("cuda")
+    dev = host_t.to("cuda")
     lay = StripeLayout(groups, block, stride, stride * total)
     recover_chunk_groups_dev(dev.data_ptr(), present, lay, torch.cuda.current_stream(), data_shards, parity_shards)
-    out = dev.cpu().numpy().reshape(groups, total, stride)
+    host_t.copy_(dev)  # synchronous: the recovered chunks are in host_t on return
+    out = host
     return {f"{file_path_version}-{g * total + s}": out[g, s, :block].tobytes()
             for g in range(groups) for s in offline}
