@@ -1,0 +1,65 @@
+"""Seeded random cases of the client's file path (ReedSolomonEncoder.java:56-85,
+ReedSolomonDecoder.java:62-103) through rs_file_encode / rs_file_decode and
+their device forms, against the oracle's restatement, bit-exact: data and
+parity shards of the padded, block-interleaved file; the file rebuilt from
+the first k present shards with every absent shard filled in place
+(decodeMissing semantics); random k, m, block sizes (multiples of 8 and not,
+1 byte included), file sizes from empty to ~300 KB and random erasure sets.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+BLOCKS = [1000, 8, 16, 24, 999, 7, 4096, 1, 1000, 520]
+
+
+@pytest.mark.parametrize("case", range(24))
+def test_file_paths_random(gpu, oracle_lib, case):
+    import torch
+    import rsamd
+    from rsamd.layout import ReedSolomonDecoder, ReedSolomonEncoder, decode_file_dev, encode_file_dev, file_layout
+    rng = np.random.default_rng(9000 + case)
+    k = int(rng.integers(1, 11))
+    m = int(rng.integers(0, 5))
+    block = BLOCKS[case % len(BLOCKS)]
+    n = int(rng.choice([0, 1, block, k * block, k * block + 1, int(rng.integers(1, 300_001))]))
+    data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    oc = oracle_lib.Codec(k, m)
+    ref = oc.file_encode(data, block)  # (k + m, S)
+
+    enc = ReedSolomonEncoder(data, k, m, block)
+    enc.encode()
+    got = np.stack(enc.getShards()) if ref.shape[1] else np.zeros_like(ref)
+    assert np.array_equal(got, ref), (k, m, block, n)
+    if n == 0:
+        return
+    S = ref.shape[1]
+    e = int(rng.integers(0, m + 1))
+    miss = sorted(int(x) for x in rng.choice(k + m, e, replace=False)) if e else []
+    present = [i not in miss for i in range(k + m)]
+    sh = [ref[i].copy() for i in range(k + m)]
+    for j in miss:
+        sh[j][:] = 0
+    out = ReedSolomonDecoder(sh, present, S, n, k, m, block).getFileData()
+    assert out == data, (k, m, block, n, miss)
+    assert all(np.array_equal(a, b) for a, b in zip(sh, ref)), (k, m, block, n, miss)  # filled in place
+    assert oc.file_decode(ref, present, n, block) == data
+
+    # the device forms on the same case: shards at a 256-rounded stride
+    rs = rsamd.ReedSolomon.create(k, m)
+    padded, S2 = file_layout(rs, n, block)
+    assert S2 == S
+    stride = (S + 255) // 256 * 256
+    st = torch.cuda.current_stream()
+    fdev = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to("cuda:0")
+    sdev = torch.zeros((k + m) * stride, dtype=torch.uint8, device="cuda:0")
+    encode_file_dev(rs, fdev.data_ptr(), n, sdev.data_ptr(), stride, block, st)
+    v = sdev.view(k + m, stride)
+    assert np.array_equal(v[:, :S].cpu().numpy(), ref), (k, m, block, n)
+    for j in miss:
+        v[j, :S] = 0
+    odev = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
+    decode_file_dev(rs, sdev.data_ptr(), S, stride, present, odev.data_ptr(), n, block, True, st)
+    assert odev.cpu().numpy().tobytes() == data, (k, m, block, n, miss)
+    assert np.array_equal(v[:, :S].cpu().numpy(), ref), (k, m, block, n, miss)  # write_missing
