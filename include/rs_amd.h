@@ -90,6 +90,13 @@ RS_API const char *rs_last_error_message(void);
 RS_API void rs_thread_release(void);
 /* Number of visible HIP devices (0 when none). */
 RS_API int rs_device_count(void);
+/* The host-memory registry of the direct path (pageable caller buffers are
+ * page-locked for one call): out[0] = registrations held now (0 whenever no
+ * host call is running), out[1] = their pages, out[2] = hipHostUnregister
+ * failures since load.  Writes min(n, 3) values; returns 3.  A check for
+ * tests and services: a registration that outlives its call would leave the
+ * runtime tracking pages the caller may free. */
+RS_API int rs_host_registry_state(int64_t *out, int n);
 
 /* ---------------------------------------------------------------------------
  * Host-buffer API (JNI-facing).  Shards are caller-owned host arrays,

@@ -820,6 +820,8 @@ int rs_abi_version(void) { return RS_AMD_ABI_VERSION; }
 
 void rs_thread_release(void) { rsamd::host::release_thread_contexts(); }
 
+int rs_host_registry_state(int64_t *out, int n) { return rsamd::host::registry_state(out, n); }
+
 int rs_device_count(void) {
     int n = 0;
     return hipGetDeviceCount(&n) == hipSuccess ? n : 0;

@@ -392,6 +392,8 @@ struct HostRegistry {
     std::map<uintptr_t, std::pair<uintptr_t, int>> regs;  // page start -> (page end, references)
 };
 
+std::atomic<int64_t> g_unregister_failures{0};
+
 HostRegistry &host_registry() {
     static HostRegistry *r = new HostRegistry;  // never destroyed: no HIP calls at exit
     return *r;
@@ -415,6 +417,7 @@ void release_locked(HostRegistry &reg, std::vector<uintptr_t> &held) {
             const hipError_t e = hipHostUnregister(reinterpret_cast<void *>(ps));
             if (e != hipSuccess) {  // never seen; said once, as it would leave the pages locked
                 (void)hipGetLastError();
+                g_unregister_failures.fetch_add(1);
                 static std::atomic<bool> said{false};
                 if (!said.exchange(true))
                     std::fprintf(stderr, "librsamd: hipHostUnregister(%p) failed: %s\n", reinterpret_cast<void *>(ps),
@@ -478,6 +481,18 @@ bool HostRegistration::lock(const std::vector<std::pair<const uint8_t *, size_t>
         held_.push_back(ps);
     }
     return true;
+}
+
+int registry_state(int64_t *out, int n) {
+    int64_t v[3] = {0, 0, g_unregister_failures.load()};
+    {
+        HostRegistry &reg = host_registry();
+        std::lock_guard<std::mutex> guard(reg.mu);
+        v[0] = int64_t(reg.regs.size());
+        for (const auto &kv : reg.regs) v[1] += int64_t((kv.second.first - kv.first) / 4096);
+    }
+    for (int i = 0; out && i < n && i < 3; ++i) out[i] = v[i];
+    return 3;
 }
 
 HostRegistration::~HostRegistration() {

@@ -91,6 +91,10 @@ size_t chunk_bytes(size_t total, int nslots, bool pinned);
 bool all_pinned(const uint8_t *const *ptrs, int n);
 inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// rs_host_registry_state: registrations held now, their pages, and
+// hipHostUnregister failures since load.
+int registry_state(int64_t *out, int n);
+
 // Page-locks pageable caller ranges for the duration of one pipelined call
 // (host.cpp: a process-wide, reference-counted registry of page ranges).
 class HostRegistration {

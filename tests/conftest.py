@@ -61,6 +61,12 @@ def bounds_check(request):
     import ctypes as C
     from rsamd import _lib
     lib = _lib.load()
+    # Every build: no page registration of the direct path outlives its call
+    # (a stale one would leave the runtime tracking pages the caller may free),
+    # and no hipHostUnregister failed.
+    st = (C.c_int64 * 3)()
+    lib.rs_host_registry_state(st, 3)
+    assert st[0] == 0 and st[2] == 0, f"host registry after the test: {st[0]} held ({st[1]} pages), {st[2]} unregister failures"
     if not hasattr(lib, "rs_bounds_report"):
         return
     import torch

@@ -321,3 +321,15 @@ def test_shard_major_argument_errors(native):
     rc = native.rs_decode_groups_shard_major_dev(rs.handle, C.c_void_p(1 << 20), 1 << 20, 1 << 40, 1 << 30,
                                                 pres.ctypes.data_as(u8), None)
     assert rc == -10 and "overflows" in _lib.last_error()
+
+
+def test_host_registry_state_idle(native):
+    """rs_host_registry_state: no registration held while no host call runs
+    (the same check follows every GPU test, tests/conftest.py)."""
+    import ctypes as C
+    out = (C.c_int64 * 3)(-1, -1, -1)
+    assert native.rs_host_registry_state(out, 3) == 3
+    assert list(out) == [0, 0, 0]
+    one = (C.c_int64 * 1)(-1)
+    assert native.rs_host_registry_state(one, 1) == 3 and one[0] == 0
+    assert native.rs_host_registry_state(None, 0) == 3
