@@ -218,9 +218,11 @@ RS_API int rs_decode_batch_masked_bits_dev(const rs_codec *codec, uint8_t *dev_b
  * pattern); every absent chunk of every group is rebuilt in place, survivors
  * the first k present (ReedSolomon.java:210-223).  RS_E_NOT_ENOUGH (nothing
  * enqueued) when any group has fewer than k present; RS_E_INVALID when
- * server_stride < n_groups*chunk_len.  Full rate with dev_base, server_stride
- * and each run's first byte 16-byte aligned (chunk_len 1000: runs starting at
- * an even group). */
+ * server_stride < n_groups*chunk_len.  Full rate with dev_base and
+ * server_stride 1 KiB aligned; a run that starts mid-line peels its first
+ * bytes onto a byte kernel.  Flags that form more than 64 runs (patterns that
+ * change every few groups) are decoded in one launch of the per-stripe pattern
+ * kernels instead, the groups read as stripes of chunk_len-byte shards. */
 RS_API int rs_decode_groups_shard_major_dev(const rs_codec *codec, uint8_t *dev_base, size_t server_stride,
                                             size_t chunk_len, size_t n_groups, const uint8_t *present,
                                             void *stream);

@@ -949,6 +949,13 @@ int rs_decode_groups_shard_major_dev(const rs_codec *codec, uint8_t *dev_base, s
         std::shared_ptr<const Plan> plan;  // null: every shard present
     };
     std::vector<Run> runs;
+    // Flags that change every few groups (not the master's loop) would make
+    // thousands of small launches: past kMaxRuns runs the groups go to the
+    // per-stripe pattern kernels instead, the layout read as n_groups stripes
+    // of chunk_len-byte shards (stripe stride chunk_len, shard stride
+    // server_stride) -- one launch, every group checked before it.
+    constexpr size_t kMaxRuns = 64;
+    bool per_group = false;
     const size_t rowb = size_t(T);
     auto same_flags = [&](const uint8_t *a, const uint8_t *b) {
         for (int i = 0; i < T; ++i)
@@ -956,6 +963,10 @@ int rs_decode_groups_shard_major_dev(const rs_codec *codec, uint8_t *dev_base, s
         return true;
     };
     for (size_t g = 0; g < n_groups;) {
+        if (runs.size() == kMaxRuns) {
+            per_group = true;
+            break;
+        }
         const uint8_t *p = present + g * rowb;
         int np = 0;
         for (int i = 0; i < T; ++i) np += p[i] ? 1 : 0;
@@ -992,10 +1003,15 @@ int rs_decode_groups_shard_major_dev(const rs_codec *codec, uint8_t *dev_base, s
         runs.push_back(r);
         g += n;
     }
+    if (per_group && n_groups > size_t(INT32_MAX)) return fail(RS_E_INVALID, "too many groups");
     int rc = need_device();
     if (rc) return rc;
     bounds::Scope bs(stream);
     allow_batch(dev_base, 1, n_groups * chunk_len, server_stride, 0, T);
+    if (per_group) {
+        const Geometry geo{dev_base, n_groups, 0, chunk_len, server_stride, chunk_len, T};
+        return decode_masked_dev(*c, present, n_groups, geo, 0, static_cast<hipStream_t>(stream));
+    }
     for (const Run &r : runs) {
         if (!r.plan) continue;
         std::vector<DevPlan> plans;

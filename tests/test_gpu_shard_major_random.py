@@ -55,3 +55,39 @@ def test_shard_major_random(gpu, oracle_lib, case):
         s, off = divmod(i, stride)
         raise AssertionError(f"k={k} m={m} chunk={chunk} pad={pad} N={N} runs={bounds}: first wrong byte "
                              f"server {s} offset {off} (group {off // chunk})")
+
+
+@pytest.mark.parametrize("chunk,pad", [(1000, 0), (13, 8), (4096, 256)])
+def test_shard_major_many_runs(gpu, oracle_lib, chunk, pad):
+    """Flags that change every group or few groups (more than the 64 runs the
+    call codes one by one) go to the per-stripe pattern kernels in one launch:
+    same results, against the oracle, with random bytes in every chunk."""
+    import torch
+    from rsamd.recovery import recover_groups_shard_major_dev
+    rng = np.random.default_rng(chunk + pad)
+    k, m = 4, 2
+    T = k + m
+    N = 3001
+    L = N * chunk
+    stride = L + pad
+    rows = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(T)]
+    oracle_lib.Codec(k, m).encode_parity(rows, 0, L)
+    want = rng.integers(0, 256, T * stride, dtype=np.uint8)
+    for s in range(T):
+        want[s * stride: s * stride + L] = rows[s]
+    present = np.ones((N, T), bool)
+    host = want.copy()
+    g = 0
+    while g < N:
+        n = int(rng.integers(1, 4))
+        e = int(rng.integers(0, m + 1))
+        miss = [int(x) for x in rng.choice(T, e, replace=False)] if e else []
+        present[g: g + n, miss] = False
+        for s in miss:
+            host[s * stride + g * chunk: s * stride + min(N, g + n) * chunk] = 0x3C
+        g += n
+    dev = torch.from_numpy(host).to("cuda:0")
+    recover_groups_shard_major_dev(dev.data_ptr(), stride, present, chunk, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    got = dev.cpu().numpy()
+    assert np.array_equal(got, want), int(np.flatnonzero(got != want)[0])
