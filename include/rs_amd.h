@@ -220,9 +220,10 @@ RS_API int rs_decode_batch_masked_bits_dev(const rs_codec *codec, uint8_t *dev_b
  * enqueued) when any group has fewer than k present; RS_E_INVALID when
  * server_stride < n_groups*chunk_len.  Full rate with dev_base and
  * server_stride 1 KiB aligned; a run that starts mid-line peels its first
- * bytes onto a byte kernel.  Flags that form more than 64 runs (patterns that
- * change every few groups) are decoded in one launch of the per-stripe pattern
- * kernels instead, the groups read as stripes of chunk_len-byte shards. */
+ * bytes onto a byte kernel.  Flags that form many runs (more than one per
+ * 128 MiB of the batch, at least 8: patterns that change every few groups)
+ * are decoded in one launch of the per-stripe pattern kernels instead, the
+ * groups read as stripes of chunk_len-byte shards. */
 RS_API int rs_decode_groups_shard_major_dev(const rs_codec *codec, uint8_t *dev_base, size_t server_stride,
                                             size_t chunk_len, size_t n_groups, const uint8_t *present,
                                             void *stream);

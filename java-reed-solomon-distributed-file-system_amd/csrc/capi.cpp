@@ -950,11 +950,15 @@ int rs_decode_groups_shard_major_dev(const rs_codec *codec, uint8_t *dev_base, s
     };
     std::vector<Run> runs;
     // Flags that change every few groups (not the master's loop) would make
-    // thousands of small launches: past kMaxRuns runs the groups go to the
-    // per-stripe pattern kernels instead, the layout read as n_groups stripes
-    // of chunk_len-byte shards (stripe stride chunk_len, shard stride
-    // server_stride) -- one launch, every group checked before it.
-    constexpr size_t kMaxRuns = 64;
+    // many small launches: past max_runs runs the groups go to the per-stripe
+    // pattern kernels instead, the layout read as n_groups stripes of
+    // chunk_len-byte shards (stripe stride chunk_len, shard stride
+    // server_stride) -- one launch, every group checked before it.  That
+    // launch reads 0.53 of peak against 0.85 for runs (4 M groups, a random
+    // pattern each: profiles/r4/shard_major_runs_r4zk.txt), and a run costs
+    // about 15 us of launches, so runs pay while they number fewer than one
+    // per ~160 MB of the batch: one per 128 MiB, at least 8.
+    const size_t max_runs = std::min<size_t>(4096, std::max<size_t>(8, ((n_groups * chunk_len) >> 27) * size_t(T)));
     bool per_group = false;
     const size_t rowb = size_t(T);
     auto same_flags = [&](const uint8_t *a, const uint8_t *b) {
@@ -963,7 +967,7 @@ int rs_decode_groups_shard_major_dev(const rs_codec *codec, uint8_t *dev_base, s
         return true;
     };
     for (size_t g = 0; g < n_groups;) {
-        if (runs.size() == kMaxRuns) {
+        if (runs.size() == max_runs) {
             per_group = true;
             break;
         }

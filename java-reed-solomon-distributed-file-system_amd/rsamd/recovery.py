@@ -88,8 +88,8 @@ def recover_groups_shard_major_dev(dev_base: int, server_stride: int, present, c
     (n_groups, k+m): group g's servers that answered (the offline set, grown
     where a read failed mid-loop).  Every absent chunk is rebuilt in place, as
     ChunkserverDiskRecoveryMachine.recoverChunkserverDiskData does per group
-    (:34-48); each run of groups with one pattern is one launch (past 64 runs,
-    one launch of the per-stripe pattern kernels for every group)."""
+    (:34-48); each run of groups with one pattern is one launch (past one run per
+    128 MiB of the batch, one launch of the per-stripe pattern kernels)."""
     p = np.ascontiguousarray(np.asarray(present, dtype=bool)).view(np.uint8)
     T = data_shards + parity_shards
     if p.ndim != 2 or p.shape[1] != T:

@@ -85,11 +85,23 @@ def main():
         else:
             os.environ["RSAMD_LINE_PEEL"] = str(v)
 
+    # a random pattern per group (<= 2 erasures): past 64 runs the call takes
+    # the per-stripe pattern kernels over the same layout
+    import itertools
+    allp = np.array([[i not in miss for i in range(T)] for e in range(3)
+                     for miss in itertools.combinations(range(T), e)], dtype=bool)
+    rnd = allp[np.random.default_rng(5).integers(0, len(allp), B)]
+    cases["random_per_group"] = "random"
     res = {(c, v): [] for c in cases for v in a.peels}
     for _ in range(a.rounds):
         for name, runs in cases.items():
             pres = np.ones((B, T), bool)
             alg = 0
+            if runs == "random":
+                pres = rnd
+                e = (~rnd).sum(axis=1)
+                alg = int(((k + e) * (e > 0)).sum()) * S
+                runs = []
             for g0, g1, miss in runs:
                 pres[g0:g1, list(miss)] = False
                 alg += (g1 - g0) * (k + len(miss)) * S
@@ -100,7 +112,8 @@ def main():
     for name in cases:
         for v in a.peels:
             print(json.dumps({"case": name, "line_peel": v,
-                              "runs": [[g0, g1, list(mi)] for g0, g1, mi in cases[name]],
+                              "runs": "random" if cases[name] == "random" else
+                              [[g0, g1, list(mi)] for g0, g1, mi in cases[name]],
                               "frac": [round(f, 4) for f, _ in res[(name, v)]],
                               "ms": [round(t, 3) for _, t in res[(name, v)]]}), flush=True)
     pool.free()
