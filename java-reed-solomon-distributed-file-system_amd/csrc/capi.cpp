@@ -88,43 +88,60 @@ uint8_t *host_dev_addr(const void *p) {
 //   256 KiB 93.5 -> 54.7 / 96.3 -> 50.5;  1 MiB 291 -> 122;  4 MiB 696 -> 371 us.
 size_t direct_min_bytes() { return rsamd::tuning_size("RSAMD_DIRECT_MIN", size_t(64) << 10); }
 
-int run_direct(ThreadCtx *ctx, const std::vector<DevPlan> &plans, const std::vector<int> &in_slots,
-               const std::vector<int> &out_slots, uint8_t *const *host, size_t offset, size_t count, Mode mode,
-               bool *taken) {
-    *taken = false;
-    if (!direct_enabled() || plans.empty()) return RS_OK;
+// True when every range starts and ends on a page boundary, so page-locking
+// it covers no byte outside it (run_direct_interior's rule; the file calls
+// lock caller memory only then).
+bool whole_pages(const std::vector<std::pair<const uint8_t *, size_t>> &ranges) {
+    for (const auto &r : ranges)
+        if (reinterpret_cast<uintptr_t>(r.first) % 4096 || (reinterpret_cast<uintptr_t>(r.first) + r.second) % 4096)
+            return false;
+    return true;
+}
+
+// The direct kernels' plans for columns [offset, offset+count) of the slots:
+// false (nothing enqueued) when a shard has no device address, a plan is
+// wider than kMaxDirectIn inputs, or the addresses share no 8-byte residue.
+bool direct_plans(const std::vector<DevPlan> &plans, const std::vector<int> &in_slots,
+                  const std::vector<int> &out_slots, uint8_t *const *host, size_t offset,
+                  std::vector<rsamd::DirectPlan> *out) {
+    if (!direct_enabled() || plans.empty()) return false;
     std::vector<rsamd::DirectPlan> dp(plans.size());
     // The range's own first byte: a call locked for its range only has no
     // device mapping before host[slot] + offset.
-    auto dev_addr = [&](int slot, uint8_t **out) {
-        *out = host_dev_addr(host[slot] + offset);
-        return *out != nullptr;
+    auto dev_addr = [&](int slot, uint8_t **a) {
+        *a = host_dev_addr(host[slot] + offset);
+        return *a != nullptr;
     };
     for (size_t g = 0; g < plans.size(); ++g) {
         const DevPlan &p = plans[g];
-        if (p.nin > rsamd::kMaxDirectIn || p.nin > int(in_slots.size())) return RS_OK;
+        if (p.nin > rsamd::kMaxDirectIn || p.nin > int(in_slots.size())) return false;
         dp[g].nin = p.nin;
         dp[g].nout = p.nout;
         dp[g].tabs = p.tabs;
         for (int i = 0; i < p.nin; ++i) {
             uint8_t *a = nullptr;
-            if (!dev_addr(in_slots[i], &a)) return RS_OK;
+            if (!dev_addr(in_slots[i], &a)) return false;
             dp[g].in[i] = a;
         }
         for (int q = 0; q < p.nout; ++q) {
             const size_t o = g * size_t(rsamd::kMaxOut) + size_t(q);
-            if (o >= out_slots.size() || !dev_addr(out_slots[o], &dp[g].out[q])) return RS_OK;
+            if (o >= out_slots.size() || !dev_addr(out_slots[o], &dp[g].out[q])) return false;
         }
     }
     // Every address must share one residue modulo 8 (launch_gf_direct's
-    // narrowest vector), checked before anything is enqueued.
+    // narrowest vector).
     const uintptr_t r8 = reinterpret_cast<uintptr_t>(dp[0].in[0]) % 8;
     for (const rsamd::DirectPlan &d : dp) {
         for (int i = 0; i < d.nin; ++i)
-            if (reinterpret_cast<uintptr_t>(d.in[i]) % 8 != r8) return RS_OK;
+            if (reinterpret_cast<uintptr_t>(d.in[i]) % 8 != r8) return false;
         for (int q = 0; q < d.nout; ++q)
-            if (reinterpret_cast<uintptr_t>(d.out[q]) % 8 != r8) return RS_OK;
+            if (reinterpret_cast<uintptr_t>(d.out[q]) % 8 != r8) return false;
     }
+    *out = std::move(dp);
+    return true;
+}
+
+int launch_direct(ThreadCtx *ctx, const std::vector<rsamd::DirectPlan> &dp, size_t count, Mode mode) {
     for (const rsamd::DirectPlan &d : dp) {
         for (int i = 0; i < d.nin; ++i) bounds::allow(d.in[i], count);
         for (int q = 0; q < d.nout; ++q) bounds::allow(d.out[q], count);
@@ -136,8 +153,86 @@ int run_direct(ThreadCtx *ctx, const std::vector<DevPlan> &plans, const std::vec
             return hip_fail(e, "launch_gf_direct");
         }
     }
-    *taken = true;
     RS_HIP(hipStreamSynchronize(ctx->stream));
+    return RS_OK;
+}
+
+// Caller-pinned arrays: [offset, offset+count) coded in place by the direct
+// kernels.  *taken = false (nothing enqueued) when direct_plans refuses.
+int run_direct(ThreadCtx *ctx, const std::vector<DevPlan> &plans, const std::vector<int> &in_slots,
+               const std::vector<int> &out_slots, uint8_t *const *host, size_t offset, size_t count, Mode mode,
+               bool *taken) {
+    *taken = false;
+    std::vector<rsamd::DirectPlan> dp;
+    if (!direct_plans(plans, in_slots, out_slots, host, offset, &dp)) return RS_OK;
+    *taken = true;
+    return launch_direct(ctx, dp, count, mode);
+}
+
+// Pageable caller arrays.  Only the pages wholly inside every slot's range
+// are page-locked, and their columns coded in place by the direct kernels;
+// the columns at either end (less than a page per slot) are copied through
+// the zero-copy staging buffer and coded there, in the same launch sequence
+// and under the same synchronisation.  A page-lock therefore never covers a
+// byte the caller did not pass: the runtime page-locks the pages of its own
+// pageable copies too, and a lock of ours that reached into a neighbouring
+// allocation could be dropped under one of those.  *taken =
+// false (nothing enqueued) when the interior is under a page or the direct
+// kernels cannot take it.
+int run_direct_interior(ThreadCtx *ctx, const std::vector<DevPlan> &plans, int nslots,
+                        const std::vector<int> &in_slots, const std::vector<int> &out_slots, uint8_t *const *host,
+                        size_t offset, size_t count, Mode mode, bool *taken) {
+    *taken = false;
+    constexpr uintptr_t kPage = 4096;
+    std::vector<int> slots = in_slots;
+    if (mode == Mode::Code) slots.insert(slots.end(), out_slots.begin(), out_slots.end());
+    size_t lo = 0, hi = count;
+    for (int sl : slots) {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(host[sl] + offset);
+        const uintptr_t first = (a + kPage - 1) & ~(kPage - 1), end = (a + count) & ~(kPage - 1);
+        if (end <= first) return RS_OK;  // no whole page inside this slot's range
+        lo = std::max<size_t>(lo, first - a);
+        hi = std::min<size_t>(hi, end - a);
+    }
+    if (hi <= lo) return RS_OK;
+    std::vector<rsamd::DirectPlan> dp;
+    HostRegistration reg;
+    std::vector<std::pair<const uint8_t *, size_t>> ranges;
+    for (int sl : slots) ranges.push_back({host[sl] + offset + lo, hi - lo});
+    if (!reg.lock(ranges)) return RS_OK;
+    if (!direct_plans(plans, in_slots, out_slots, host, offset + lo, &dp)) return RS_OK;
+    const size_t ends = lo + (count - hi);
+    const size_t stride = round_up(std::max<size_t>(ends, 1), 256);
+    if (ends) {
+        int rc = zero_copy_buffer(ctx, stride * size_t(nslots));
+        if (rc) return rc;
+        for (int sl : in_slots) {
+            std::memcpy(ctx->zc + size_t(sl) * stride, host[sl] + offset, lo);
+            std::memcpy(ctx->zc + size_t(sl) * stride + lo, host[sl] + offset + hi, count - hi);
+        }
+        Geometry g;
+        g.base = ctx->zc_dev;
+        g.n_stripes = 1;
+        g.col0 = 0;
+        g.len = ends;
+        g.shard_stride = stride;
+        g.stripe_stride = stride * size_t(nslots);
+        for (const DevPlan &p : plans) {
+            const hipError_t e = rsamd::launch_gf(g, p, mode, ctx->flag, ctx->stream);
+            if (e != hipSuccess) {
+                (void)hipStreamSynchronize(ctx->stream);
+                return hip_fail(e, "launch_gf (direct call's ends)");
+            }
+        }
+    }
+    *taken = true;
+    int rc = launch_direct(ctx, dp, hi - lo, mode);  // synchronises the stream: the ends too
+    if (rc) return rc;
+    if (ends && mode == Mode::Code)
+        for (int sl : out_slots) {
+            std::memcpy(host[sl] + offset, ctx->zc + size_t(sl) * stride, lo);
+            std::memcpy(host[sl] + offset + hi, ctx->zc + size_t(sl) * stride + lo, count - hi);
+        }
     return RS_OK;
 }
 
@@ -156,19 +251,12 @@ int run_host(const std::vector<DevPlan> &plans, int nslots, const std::vector<in
     // per-buffer pointer queries.  Larger pageable calls lock the caller's
     // ranges for the call and take the direct path (or the pipeline).
     const size_t dmin = direct_min_bytes();
-    bool pinned = count >= std::min(dmin, size_t(1) << 20) && all_pinned(host, nslots);
-    HostRegistration reg;
-    if (!pinned && (count > chunk_bytes(count, nslots, false) || count >= dmin)) {
-        std::vector<std::pair<const uint8_t *, size_t>> ranges;
-        for (int sl : in_slots) ranges.push_back({host[sl] + offset, count});
-        if (mode == Mode::Code)
-            for (int sl : out_slots) ranges.push_back({host[sl] + offset, count});
-        pinned = reg.lock(ranges);
-    }
+    const bool pinned = count >= std::min(dmin, size_t(1) << 20) && all_pinned(host, nslots);
     if (mode == Mode::Verify) RS_HIP(hipMemsetAsync(ctx->flag, 0, sizeof(int), ctx->stream));
-    if (pinned) {
+    if (pinned || count >= dmin) {
         bool taken = false;
-        rc = run_direct(ctx, plans, in_slots, out_slots, host, offset, count, mode, &taken);
+        rc = pinned ? run_direct(ctx, plans, in_slots, out_slots, host, offset, count, mode, &taken)
+                    : run_direct_interior(ctx, plans, nslots, in_slots, out_slots, host, offset, count, mode, &taken);
         if (rc) return rc;
         if (taken) {
             if (mode == Mode::Verify) {
@@ -516,7 +604,7 @@ int file_decode_chunked(const Codec &c, uint8_t *const *shards, const int64_t *l
         std::vector<std::pair<const uint8_t *, size_t>> ranges;
         for (int i = 0; i < T; ++i) ranges.push_back({shards[i], size_t(S)});
         ranges.push_back({file_out, size_t(file_size)});
-        pinned = reg.lock(ranges);
+        pinned = whole_pages(ranges) && reg.lock(ranges);
     }
     const FileChunks f = file_chunks(k, T, size_t(S), blk, pinned);
     std::vector<int> surv, missing;
@@ -1160,7 +1248,7 @@ int rs_file_encode(const rs_codec *codec, const uint8_t *file, int64_t file_len,
         std::vector<std::pair<const uint8_t *, size_t>> ranges;
         for (int i = 0; i < nshards; ++i) ranges.push_back({shards_out[i], size_t(S)});
         ranges.push_back({file, size_t(file_len)});
-        pinned = reg.lock(ranges);
+        pinned = whole_pages(ranges) && reg.lock(ranges);
     }
     if (pinned) {
         bool taken = false;

@@ -371,20 +371,23 @@ bool all_pinned(const uint8_t *const *ptrs, int n) {
     return true;
 }
 
-// Page-locks pageable caller buffers for the duration of one pipelined call
+// Page-locks pageable caller memory for the duration of one call
 // (hipHostRegister: ~0.2 ms per 64 MiB the first time a range is seen,
-// microseconds after), so the pipeline DMAs them directly, full duplex,
-// instead of staging them through pinned mirrors with host memcpy
-// (tools/reg_probe.py: 4+2 x 64 MiB encode 35 -> 43.5 GiB/s).
+// microseconds after) so the direct kernels code it in place.  Since the
+// end of round 4 only ranges made of whole pages of the caller's own bytes
+// are locked (capi.cpp run_direct_interior, whole_pages): a lock rounded out
+// to pages reached into neighbouring allocations, which the runtime locks
+// for its own pageable copies, and every GPU fault of rounds 3 and 4 surfaced
+// in such a copy after calls that had locked NumPy memory.
 //
 // Registrations go through a process-wide registry of page ranges: calls on
 // the same caller buffers (several threads, or one array passed twice) share
 // one registration by reference count, and a range that partly overlaps a
 // registered one is not registered again -- registering the same pages twice
 // and unregistering one while the other is in use aborts inside the HIP
-// runtime.  All or nothing: if any range cannot be locked the call uses the
-// mirrors.  The destructor releases after run_chunks has drained both
-// streams, also on its error paths.  RSAMD_HOST_REGISTER=0 turns it off.
+// runtime.  All or nothing: if any range cannot be locked the call is staged.
+// The destructor releases after the call's kernels have completed, also on
+// its error paths.  RSAMD_HOST_REGISTER=0 (TUNING builds) turns it off.
 namespace {
 
 struct HostRegistry {
@@ -523,6 +526,20 @@ int run_chunks(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinned, c
     return rc;
 }
 
+int zero_copy_buffer(ThreadCtx *ctx, size_t buf_bytes) {
+    if (ctx->zc_cap < buf_bytes) {
+        if (ctx->zc) RS_HIP(hipHostFree(ctx->zc));
+        ctx->zc = ctx->zc_dev = nullptr;
+        ctx->zc_cap = 0;
+        RS_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->zc), buf_bytes,
+                             hipHostMallocMapped | hipHostMallocCoherent));
+        ctx->zc_cap = buf_bytes;
+        RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->zc_dev), ctx->zc, 0));
+    }
+    bounds::allow(ctx->zc_dev, ctx->zc_cap);
+    return RS_OK;
+}
+
 namespace {
 
 // Single-chunk calls (<= 4 MiB per shard) skip the DMA pipeline: the inputs
@@ -542,16 +559,8 @@ size_t zero_copy_limit() {
 }
 
 int run_zero_copy(ThreadCtx *ctx, size_t buf_bytes, const ChunkIo &io, const ChunkCode &code) {
-    if (ctx->zc_cap < buf_bytes) {
-        if (ctx->zc) RS_HIP(hipHostFree(ctx->zc));
-        ctx->zc = ctx->zc_dev = nullptr;
-        ctx->zc_cap = 0;
-        RS_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->zc), buf_bytes,
-                             hipHostMallocMapped | hipHostMallocCoherent));
-        ctx->zc_cap = buf_bytes;
-        RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->zc_dev), ctx->zc, 0));
-    }
-    bounds::allow(ctx->zc_dev, ctx->zc_cap);
+    int zrc = zero_copy_buffer(ctx, buf_bytes);
+    if (zrc) return zrc;
     std::vector<Xfer> in, out;
     io(0, &in, &out);
     // Host copies on the calling thread; the copy pool only above 2 MiB (its

@@ -82,6 +82,9 @@ void release_thread_contexts();
 // Device / pinned-host buffers that only grow.
 int grow(uint8_t **buf, size_t *cap, size_t want);
 int grow_pinned(uint8_t **buf, size_t *cap, size_t want);
+// The context's coherent, device-mapped host buffer (zc / zc_dev) with at
+// least buf_bytes.
+int zero_copy_buffer(ThreadCtx *ctx, size_t buf_bytes);
 
 // ---- the chunked pipeline --------------------------------------------------
 // Bytes per slot per chunk for a call of `total` bytes per slot and `nslots`
