@@ -66,8 +66,9 @@ def test_direct_encode_verify_decode(gpu, oracle_lib, page, gap, offset):
 
 
 def test_direct_pageable_registered(gpu, oracle_lib):
-    """Pageable numpy shards of a multi-chunk call are page-locked for the call
-    (HostRegistration, mapped) and then coded in place."""
+    """Pageable numpy shards of a multi-chunk call: the pages wholly inside
+    them are page-locked for the call (HostRegistration, mapped) and coded in
+    place, the ragged ends through the staging buffer in the same launches."""
     import rsamd
     rs = rsamd.ReedSolomon.create(10, 4)
     n = (3 << 20) + 4096 + 5
@@ -86,8 +87,8 @@ def test_direct_pageable_registered(gpu, oracle_lib):
 
 
 def test_direct_pageable_offset_range(gpu, oracle_lib):
-    """A pageable call on a range far into its arrays: only the range's pages
-    are locked, so the kernel's addresses come from the range's first byte."""
+    """A pageable call on a range far into its arrays: only whole pages inside
+    the range are locked, so the kernel's addresses come from inside it."""
     import rsamd
     rs = rsamd.ReedSolomon.create(4, 2)
     n, off, cnt = 12 << 20, (3 << 20) + 5, (4 << 20) + 3

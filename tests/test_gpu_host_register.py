@@ -1,9 +1,10 @@
-"""GPU tests of the host-buffer pipeline's per-call page-locking
-(host.cpp HostRegistration): pageable caller ranges are registered with
-hipHostRegister for the duration of a pipelined call, all or nothing, with the
-pinned mirrors as the fallback.  Registration collisions must never change a
-byte: threads sharing the same input arrays, shards that are slices of one
-allocation (shared pages), and the same array passed twice.
+"""GPU tests of the host calls' per-call page-locking (host.cpp
+HostRegistration): the pages wholly inside pageable caller ranges are
+registered with hipHostRegister for the duration of one call, all or nothing,
+with the staged paths as the fallback (capi.cpp run_direct_interior).
+Registration collisions must never change a byte: threads sharing the same
+input arrays, shards that are slices of one allocation (shared pages), and the
+same array passed twice.
 """
 import threading
 
