@@ -203,3 +203,30 @@ def test_direct_file_paths(gpu, oracle_lib, k, m, n, file_off, pinned, misses):
         file_decode_into(rs, sh, [i not in miss for i in range(k + m)], S, out)
         assert np.array_equal(out, fbuf), miss
         assert np.array_equal(np.stack(sh), ref), miss  # absent shards rebuilt in place
+
+
+@pytest.mark.parametrize("n,off", [((64 << 10) + 4100, 3), ((1 << 20) + 7, 4095), (5 << 20, 0)])
+def test_direct_interior_and_ends(gpu, oracle_lib, n, off):
+    """Pageable calls: the pages wholly inside the range are coded in place,
+    the ends (under a page per shard) through the staging buffer in the same
+    launches.  Encode, decode and verify must be exact at both ends and
+    inside, and a wrong parity byte is found wherever it is."""
+    import rsamd
+    rs = rsamd.ReedSolomon.create(4, 2)
+    rng = np.random.default_rng(n + off)
+    cnt = n - off - 1
+    sh = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(4)] + [np.zeros(n, np.uint8) for _ in range(2)]
+    ref = [a.copy() for a in sh]
+    oracle_lib.Codec(4, 2).encode_parity(ref, off, cnt)
+    rs.encodeParity(sh, off, cnt)
+    assert all(np.array_equal(a, b) for a, b in zip(sh, ref))
+    assert rs.isParityCorrect(sh, off, cnt)
+    for where in (off, off + cnt - 1, off + cnt // 2, off + 4095 if cnt > 8192 else off + 1):
+        sh[5][where] ^= 0x5A
+        assert not rs.isParityCorrect(sh, off, cnt), where
+        sh[5][where] ^= 0x5A
+    for miss in ((0, 5), (1, 2)):
+        for j in miss:
+            sh[j][off:off + cnt] = 0x33
+        rs.decodeMissing(sh, [i not in miss for i in range(6)], off, cnt)
+        assert all(np.array_equal(a, b) for a, b in zip(sh, ref)), miss
