@@ -88,6 +88,16 @@ uint8_t *host_dev_addr(const void *p) {
 //   256 KiB 93.5 -> 54.7 / 96.3 -> 50.5;  1 MiB 291 -> 122;  4 MiB 696 -> 371 us.
 size_t direct_min_bytes() { return rsamd::tuning_size("RSAMD_DIRECT_MIN", size_t(64) << 10); }
 
+// The same for pageable arrays, which the direct path takes only through
+// run_direct_interior (its ends cost a staged kernel and two memcpys per
+// call): 4+2 x 64 KiB pageable ran 48 us that way against ~40 us staged
+// (bench_r4zm.json cfg0 legs), while from 256 KiB the direct kernels win
+// clearly (93.5 -> 54.7 us, direct_small_r3s2k.txt).  TUNING builds:
+// RSAMD_DIRECT_PAGEABLE_MIN.
+size_t direct_pageable_min_bytes() {
+    return std::max(direct_min_bytes(), rsamd::tuning_size("RSAMD_DIRECT_PAGEABLE_MIN", size_t(256) << 10));
+}
+
 // True when every range starts and ends on a page boundary, so page-locking
 // it covers no byte outside it (run_direct_interior's rule; the file calls
 // lock caller memory only then).
@@ -253,7 +263,7 @@ int run_host(const std::vector<DevPlan> &plans, int nslots, const std::vector<in
     const size_t dmin = direct_min_bytes();
     const bool pinned = count >= std::min(dmin, size_t(1) << 20) && all_pinned(host, nslots);
     if (mode == Mode::Verify) RS_HIP(hipMemsetAsync(ctx->flag, 0, sizeof(int), ctx->stream));
-    if (pinned || count >= dmin) {
+    if (pinned || count >= direct_pageable_min_bytes()) {
         bool taken = false;
         rc = pinned ? run_direct(ctx, plans, in_slots, out_slots, host, offset, count, mode, &taken)
                     : run_direct_interior(ctx, plans, nslots, in_slots, out_slots, host, offset, count, mode, &taken);

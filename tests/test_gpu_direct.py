@@ -205,7 +205,7 @@ def test_direct_file_paths(gpu, oracle_lib, k, m, n, file_off, pinned, misses):
         assert np.array_equal(np.stack(sh), ref), miss  # absent shards rebuilt in place
 
 
-@pytest.mark.parametrize("n,off", [((64 << 10) + 4100, 3), ((1 << 20) + 7, 4095), (5 << 20, 0)])
+@pytest.mark.parametrize("n,off", [((64 << 10) + 4100, 3), ((256 << 10) + 8200, 3), ((1 << 20) + 7, 4095), (5 << 20, 0)])
 def test_direct_interior_and_ends(gpu, oracle_lib, n, off):
     """Pageable calls: the pages wholly inside the range are coded in place,
     the ends (under a page per shard) through the staging buffer in the same
