@@ -108,6 +108,32 @@ bool whole_pages(const std::vector<std::pair<const uint8_t *, size_t>> &ranges) 
     return true;
 }
 
+// One caller array of a block-row call (the host file calls): row r spans
+// [p + r*per_row, p + (r+1)*per_row), clipped to len.
+struct RowArray {
+    const uint8_t *p;
+    size_t len, per_row;
+};
+
+// The rows [*r0, *r1) of [0, rows) whose bytes lie, in every array, inside
+// the pages wholly within that array (so locking them covers no byte the
+// caller did not pass); false when there are none.
+bool interior_rows(const std::vector<RowArray> &arrays, size_t rows, size_t *r0, size_t *r1) {
+    constexpr uintptr_t kPage = 4096;
+    size_t lo = 0, hi = rows;
+    for (const RowArray &a : arrays) {
+        if (a.len == 0) continue;
+        const uintptr_t p = reinterpret_cast<uintptr_t>(a.p);
+        const uintptr_t first = (p + kPage - 1) & ~(kPage - 1), end = (p + a.len) & ~(kPage - 1);
+        if (end <= first) return false;
+        lo = std::max(lo, (first - p + a.per_row - 1) / a.per_row);
+        hi = std::min(hi, (end - p) / a.per_row);
+    }
+    *r0 = lo;
+    *r1 = hi;
+    return hi > lo;
+}
+
 // The direct kernels' plans for columns [offset, offset+count) of the slots:
 // false (nothing enqueued) when a shard has no device address, a plan is
 // wider than kMaxDirectIn inputs, or the addresses share no 8-byte residue.
@@ -540,6 +566,59 @@ int file_encode_direct(const Codec &c, const uint8_t *file, size_t file_len, siz
     return RS_OK;
 }
 
+// The staged form of the host file encode: chunks of block rows through
+// run_chunks.  file_len fills every row but the last (the padded layout).
+int file_encode_staged(const Codec &c, const uint8_t *file, size_t file_len, size_t blk, uint8_t *const *shards,
+                       size_t S, ThreadCtx *ctx, bool pinned) {
+    const size_t kb = size_t(c.k()) * blk;
+    const FileChunks f = file_chunks(c.k(), c.total(), S, blk, pinned);
+    auto flen_of = [&](size_t r0, size_t rc_rows) {  // every row holds file bytes
+        return std::min(rc_rows * kb, file_len - r0 * kb);
+    };
+    auto io = [&](size_t j, std::vector<Xfer> *in, std::vector<Xfer> *out) {
+        const size_t r0 = j * f.R, rc_rows = std::min(f.R, f.rows - r0);
+        in->push_back({const_cast<uint8_t *>(file) + r0 * kb, 0, flen_of(r0, rc_rows)});
+        for (int i = 0; i < c.total(); ++i)
+            out->push_back({shards[i] + r0 * blk, f.fbytes + size_t(i) * f.sstride, rc_rows * blk});
+    };
+    auto code = [&](size_t j, uint8_t *buf, hipStream_t st) -> int {
+        const size_t r0 = j * f.R, rc_rows = std::min(f.R, f.rows - r0);
+        return file_encode_dev(c, buf, flen_of(r0, rc_rows), blk, buf + f.fbytes, f.sstride, st);
+    };
+    return run_chunks(ctx, f.n, f.buf_bytes, pinned, io, code);
+}
+
+// Pageable host file encode: file_decode_interior's split -- the block rows
+// inside whole pages of the file and of every shard coded in place, the rows
+// either side staged.
+int file_encode_interior(const Codec &c, const uint8_t *file, size_t file_len, size_t blk, uint8_t *const *shards,
+                         size_t S, ThreadCtx *ctx, bool *taken) {
+    *taken = false;
+    const int T = c.total();
+    const size_t kb = size_t(c.k()) * blk, rows = S / blk;
+    std::vector<RowArray> arrays{{file, file_len, kb}};
+    for (int i = 0; i < T; ++i) arrays.push_back({shards[i], S, blk});
+    size_t r0 = 0, r1 = 0;
+    if (!interior_rows(arrays, rows, &r0, &r1)) return RS_OK;
+    std::vector<std::pair<const uint8_t *, size_t>> ranges;
+    for (const RowArray &a : arrays) ranges.push_back({a.p + r0 * a.per_row, (r1 - r0) * a.per_row});
+    HostRegistration reg;
+    if (!reg.lock(ranges)) return RS_OK;
+    std::vector<uint8_t *> sh(T);
+    for (int i = 0; i < T; ++i) sh[i] = shards[i] + r0 * blk;
+    int rc = file_encode_direct(c, file + r0 * kb, (r1 - r0) * kb, blk, sh.data(), (r1 - r0) * blk, ctx, taken);
+    if (rc || !*taken) return rc;
+    for (const auto &piece : {std::make_pair(size_t(0), r0), std::make_pair(r1, rows)}) {
+        const size_t a = piece.first, b = piece.second;
+        if (b <= a) continue;
+        for (int i = 0; i < T; ++i) sh[i] = shards[i] + a * blk;
+        rc = file_encode_staged(c, file + a * kb, std::min((b - a) * kb, file_len - a * kb), blk, sh.data(),
+                                (b - a) * blk, ctx, false);
+        if (rc) return rc;
+    }
+    return RS_OK;
+}
+
 int file_decode_direct(const Codec &c, uint8_t *const *shards, const uint8_t *present, const std::vector<int> &surv,
                        const std::vector<int> &missing, size_t blk, uint8_t *file_out, size_t file_size,
                        size_t cols, ThreadCtx *ctx, bool *taken) {
@@ -578,6 +657,81 @@ int file_decode_direct(const Codec &c, uint8_t *const *shards, const uint8_t *pr
     return RS_OK;
 }
 
+// Block rows a file decode must code: all of them when a shard is rebuilt,
+// else only those holding file bytes.
+size_t file_rows_needed(int k, size_t S, size_t blk, const std::vector<int> &missing, size_t file_size) {
+    const size_t rows = S / blk, kb = size_t(k) * blk;
+    return missing.empty() ? std::min(rows, (file_size + kb - 1) / kb) : rows;
+}
+
+// The staged form of the host file decode (rs_file_decode's whole-shard
+// case): chunks of block rows through run_chunks.
+int file_decode_staged(const Codec &c, uint8_t *const *shards, size_t S, const uint8_t *present,
+                       const std::vector<int> &surv, const std::vector<int> &missing, size_t blk, uint8_t *file_out,
+                       size_t file_size, ThreadCtx *ctx, bool pinned) {
+    const size_t kb = size_t(c.k()) * blk;
+    const FileChunks f = file_chunks(c.k(), c.total(), S, blk, pinned);
+    const size_t rows_needed = file_rows_needed(c.k(), S, blk, missing, file_size);
+    if (rows_needed == 0) return RS_OK;
+    auto flen_of = [&](size_t r0, size_t rc_rows) {
+        const size_t fo = r0 * kb;
+        return file_size > fo ? std::min(rc_rows * kb, file_size - fo) : size_t(0);
+    };
+    auto io = [&](size_t j, std::vector<Xfer> *in, std::vector<Xfer> *out) {
+        const size_t r0 = j * f.R, rc_rows = std::min(f.R, f.rows - r0), n = rc_rows * blk;
+        for (int sidx : surv) in->push_back({shards[sidx] + r0 * blk, f.fbytes + size_t(sidx) * f.sstride, n});
+        for (int sidx : missing) out->push_back({shards[sidx] + r0 * blk, f.fbytes + size_t(sidx) * f.sstride, n});
+        const size_t flen = flen_of(r0, rc_rows);
+        if (flen) out->push_back({file_out + r0 * kb, 0, flen});
+    };
+    auto code = [&](size_t j, uint8_t *buf, hipStream_t st) -> int {
+        const size_t r0 = j * f.R, rc_rows = std::min(f.R, f.rows - r0);
+        return file_decode_dev(c, buf + f.fbytes, rc_rows * blk, f.sstride, present, blk, buf, flen_of(r0, rc_rows),
+                               true, st);
+    };
+    return run_chunks(ctx, (rows_needed + f.R - 1) / f.R, f.buf_bytes, pinned, io, code);
+}
+
+// Pageable host file decode: the block rows whose bytes lie inside whole
+// pages of every array (survivors, rebuilt shards, file) are page-locked and
+// coded in place by the direct kernel; the few rows either side (under a page
+// of each array) are staged.  As run_direct_interior, no lock covers a byte
+// the caller did not pass.  *taken = false, nothing done,
+// when there is no such interior or the direct kernel cannot take it.
+int file_decode_interior(const Codec &c, uint8_t *const *shards, size_t S, const uint8_t *present,
+                         const std::vector<int> &surv, const std::vector<int> &missing, size_t blk, uint8_t *file_out,
+                         size_t file_size, size_t rows_needed, ThreadCtx *ctx, bool *taken) {
+    *taken = false;
+    const int T = c.total();
+    const size_t kb = size_t(c.k()) * blk;
+    std::vector<RowArray> arrays;
+    for (int i : surv) arrays.push_back({shards[i], rows_needed * blk, blk});
+    for (int i : missing) arrays.push_back({shards[i], S, blk});
+    arrays.push_back({file_out, file_size, kb});
+    size_t r0 = 0, r1 = 0;
+    if (!interior_rows(arrays, rows_needed, &r0, &r1)) return RS_OK;
+    std::vector<std::pair<const uint8_t *, size_t>> ranges;
+    for (const RowArray &a : arrays)
+        if (a.len) ranges.push_back({a.p + r0 * a.per_row, (r1 - r0) * a.per_row});
+    HostRegistration reg;
+    if (!reg.lock(ranges)) return RS_OK;
+    auto fsz = [&](size_t a, size_t b) { return file_size > a * kb ? std::min(file_size - a * kb, (b - a) * kb) : 0; };
+    std::vector<uint8_t *> sh(T);
+    for (int i = 0; i < T; ++i) sh[i] = shards[i] + r0 * blk;
+    int rc = file_decode_direct(c, sh.data(), present, surv, missing, blk, file_out + r0 * kb, fsz(r0, r1),
+                                (r1 - r0) * blk, ctx, taken);
+    if (rc || !*taken) return rc;
+    for (const auto &piece : {std::make_pair(size_t(0), r0), std::make_pair(r1, rows_needed)}) {
+        const size_t a = piece.first, b = piece.second;
+        if (b <= a) continue;
+        for (int i = 0; i < T; ++i) sh[i] = shards[i] + a * blk;
+        rc = file_decode_staged(c, sh.data(), (b - a) * blk, present, surv, missing, blk, file_out + a * kb,
+                                fsz(a, b), ctx, false);
+        if (rc) return rc;
+    }
+    return RS_OK;
+}
+
 // rs_file_decode when byteCntInShard is the whole shard: one pass per chunk
 // -- upload the first k present shards, rebuild every absent shard and merge
 // the data shards into the file chunk on the GPU, download the rebuilt shards
@@ -605,48 +759,35 @@ int file_decode_chunked(const Codec &c, uint8_t *const *shards, const int64_t *l
     ThreadCtx *ctx = nullptr;
     rc = thread_ctx(&ctx);
     if (rc) return rc;
-    const size_t blk = size_t(block), kb = size_t(k) * blk;
+    const size_t blk = size_t(block);
     std::vector<const uint8_t *> bufs(shards, shards + T);
     bufs.push_back(file_out);
     bool pinned = all_pinned(bufs.data(), int(bufs.size()));
     HostRegistration reg;
-    if (!pinned && (file_chunks(k, T, size_t(S), blk, false).n > 1 || size_t(S) >= direct_min_bytes())) {
+    const bool big = file_chunks(k, T, size_t(S), blk, false).n > 1 || size_t(S) >= direct_min_bytes();
+    if (!pinned && big) {
         std::vector<std::pair<const uint8_t *, size_t>> ranges;
         for (int i = 0; i < T; ++i) ranges.push_back({shards[i], size_t(S)});
         ranges.push_back({file_out, size_t(file_size)});
         pinned = whole_pages(ranges) && reg.lock(ranges);
     }
-    const FileChunks f = file_chunks(k, T, size_t(S), blk, pinned);
     std::vector<int> surv, missing;
     for (int i = 0; i < T; ++i) {
         if (present[i] && int(surv.size()) < k) surv.push_back(i);
         if (!present[i]) missing.push_back(i);
     }
-    // Nothing to rebuild: only the rows holding file bytes are needed.
-    const size_t rows_needed = missing.empty() ? std::min(f.rows, (size_t(file_size) + kb - 1) / kb) : f.rows;
+    const size_t rows_needed = file_rows_needed(k, size_t(S), blk, missing, size_t(file_size));
+    bool taken = false;
     if (pinned) {  // direct path: the survivors, rebuilt shards and file coded in place
-        bool taken = false;
         rc = file_decode_direct(c, shards, present, surv, missing, blk, file_out, size_t(file_size),
                                 rows_needed * blk, ctx, &taken);
-        if (rc || taken) return rc;
+    } else if (big && size_t(S) >= direct_pageable_min_bytes()) {
+        rc = file_decode_interior(c, shards, size_t(S), present, surv, missing, blk, file_out, size_t(file_size),
+                                  rows_needed, ctx, &taken);
     }
-    auto flen_of = [&](size_t r0, size_t rc_rows) {
-        const size_t fo = r0 * kb;
-        return size_t(file_size) > fo ? std::min(rc_rows * kb, size_t(file_size) - fo) : size_t(0);
-    };
-    auto io = [&](size_t j, std::vector<Xfer> *in, std::vector<Xfer> *out) {
-        const size_t r0 = j * f.R, rc_rows = std::min(f.R, f.rows - r0), n = rc_rows * blk;
-        for (int sidx : surv) in->push_back({shards[sidx] + r0 * blk, f.fbytes + size_t(sidx) * f.sstride, n});
-        for (int sidx : missing) out->push_back({shards[sidx] + r0 * blk, f.fbytes + size_t(sidx) * f.sstride, n});
-        const size_t flen = flen_of(r0, rc_rows);
-        if (flen) out->push_back({file_out + r0 * kb, 0, flen});
-    };
-    auto code = [&](size_t j, uint8_t *buf, hipStream_t st) -> int {
-        const size_t r0 = j * f.R, rc_rows = std::min(f.R, f.rows - r0);
-        return file_decode_dev(c, buf + f.fbytes, rc_rows * blk, f.sstride, present, blk, buf, flen_of(r0, rc_rows),
-                               true, st);
-    };
-    return run_chunks(ctx, (rows_needed + f.R - 1) / f.R, f.buf_bytes, pinned, io, code);
+    if (rc || taken) return rc;
+    return file_decode_staged(c, shards, size_t(S), present, surv, missing, blk, file_out, size_t(file_size), ctx,
+                              pinned);
 }
 
 // Next staging slot of this thread with >= bytes on both sides, once the
@@ -1249,37 +1390,25 @@ int rs_file_encode(const rs_codec *codec, const uint8_t *file, int64_t file_len,
     ThreadCtx *ctx = nullptr;
     rc = thread_ctx(&ctx);
     if (rc) return rc;
-    const size_t k = size_t(c->k()), blk = size_t(block);
+    const size_t blk = size_t(block);
     std::vector<const uint8_t *> bufs(shards_out, shards_out + nshards);
     bufs.push_back(file);
     bool pinned = all_pinned(bufs.data(), int(bufs.size()));
     HostRegistration reg;
-    if (!pinned && (file_chunks(c->k(), c->total(), size_t(S), blk, false).n > 1 || size_t(S) >= direct_min_bytes())) {
+    const bool big = file_chunks(c->k(), c->total(), size_t(S), blk, false).n > 1 || size_t(S) >= direct_min_bytes();
+    if (!pinned && big) {
         std::vector<std::pair<const uint8_t *, size_t>> ranges;
         for (int i = 0; i < nshards; ++i) ranges.push_back({shards_out[i], size_t(S)});
         ranges.push_back({file, size_t(file_len)});
         pinned = whole_pages(ranges) && reg.lock(ranges);
     }
-    if (pinned) {
-        bool taken = false;
+    bool taken = false;
+    if (pinned)
         rc = file_encode_direct(*c, file, size_t(file_len), blk, shards_out, size_t(S), ctx, &taken);
-        if (rc || taken) return rc;
-    }
-    const FileChunks f = file_chunks(c->k(), c->total(), size_t(S), blk, pinned);
-    auto flen_of = [&](size_t r0, size_t rc_rows) {  // every row holds file bytes
-        return std::min(rc_rows * k * blk, size_t(file_len) - r0 * k * blk);
-    };
-    auto io = [&](size_t j, std::vector<Xfer> *in, std::vector<Xfer> *out) {
-        const size_t r0 = j * f.R, rc_rows = std::min(f.R, f.rows - r0);
-        in->push_back({const_cast<uint8_t *>(file) + r0 * k * blk, 0, flen_of(r0, rc_rows)});
-        for (int i = 0; i < c->total(); ++i)
-            out->push_back({shards_out[i] + r0 * blk, f.fbytes + size_t(i) * f.sstride, rc_rows * blk});
-    };
-    auto code = [&](size_t j, uint8_t *buf, hipStream_t st) -> int {
-        const size_t r0 = j * f.R, rc_rows = std::min(f.R, f.rows - r0);
-        return file_encode_dev(*c, buf, flen_of(r0, rc_rows), blk, buf + f.fbytes, f.sstride, st);
-    };
-    return run_chunks(ctx, f.n, f.buf_bytes, pinned, io, code);
+    else if (big && size_t(S) >= direct_pageable_min_bytes())
+        rc = file_encode_interior(*c, file, size_t(file_len), blk, shards_out, size_t(S), ctx, &taken);
+    if (rc || taken) return rc;
+    return file_encode_staged(*c, file, size_t(file_len), blk, shards_out, size_t(S), ctx, pinned);
 }
 
 int rs_file_decode(const rs_codec *codec, uint8_t *const *shards, int nshards, const int64_t *shard_lens,

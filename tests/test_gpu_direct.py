@@ -205,6 +205,59 @@ def test_direct_file_paths(gpu, oracle_lib, k, m, n, file_off, pinned, misses):
         assert np.array_equal(np.stack(sh), ref), miss  # absent shards rebuilt in place
 
 
+@pytest.mark.parametrize("k,m,n,block,offs", [
+    (4, 2, 12_000_007, 1000, (24, 16, 4088, 8, 0, 4000, 2000)),     # offsets of file, shard 0 .. 5
+    (4, 2, 4_096_000, 1000, (0,) * 7),                               # whole pages: locked whole
+    (10, 4, 30_000_001, 4096, (8, 40, 4056, 0, 8, 16, 24, 32, 48, 56, 64, 72, 80, 88, 96)),
+    (4, 2, 3_000_000, 8, (16, 8, 0, 8, 16, 24, 32)),                # 512 rows per page
+    (4, 2, 3_000_000, 1000, (3, 8, 0, 8, 16, 24, 32)),              # file not 8-aligned: staged
+    (4, 2, 3_000_000, 999, (8, 8, 0, 8, 16, 24, 32)),               # block not a multiple of 8: staged
+])
+def test_direct_file_interior(gpu, oracle_lib, k, m, n, block, offs):
+    """Pageable host file calls (ReedSolomonEncoder.java:56-85,
+    ReedSolomonDecoder.java:36,62-103): the block rows inside whole pages of
+    the file and of every shard are page-locked and coded in place, the rows
+    either side staged (capi.cpp file_encode_interior / file_decode_interior).
+    Shards and file exact against the oracle, and no byte around any array
+    written."""
+    import rsamd
+    from rsamd.layout import file_decode_into, file_encode_into, file_layout
+    rs = rsamd.ReedSolomon.create(k, m)
+    oc = oracle_lib.Codec(k, m)
+    rng = np.random.default_rng(n + block)
+    _, S = file_layout(rs, n, block)
+    guard = 8192
+
+    def place(size, off):  # a view `off` bytes past a page inside a guarded pageable buffer
+        raw = np.full(size + off + 2 * guard + 4096, 0xA5, np.uint8)
+        start = (-raw.ctypes.data) % 4096 + guard + off
+        return raw, raw[start:start + size]
+
+    def guards_intact(raw, view):
+        a = view.ctypes.data - raw.ctypes.data
+        return bool((raw[:a] == 0xA5).all() and (raw[a + len(view):] == 0xA5).all())
+
+    fraw, fbuf = place(n, offs[0])
+    fbuf[:] = rng.integers(0, 256, n, dtype=np.uint8)
+    shs = [place(S, o) for o in offs[1:]]
+    sh = [v for _, v in shs]
+    for a in sh:
+        a[:] = 0xEE  # every byte must be written
+    file_encode_into(rs, fbuf, sh, block)
+    ref = oc.file_encode(fbuf.tobytes(), block)
+    assert np.array_equal(np.stack(sh), ref)
+    assert all(guards_intact(r, v) for r, v in shs) and guards_intact(fraw, fbuf)
+    miss = tuple(int(x) for x in rng.choice(k + m, m, replace=False))
+    for j in miss:
+        sh[j][:] = 0
+    oraw, out = place(n, offs[0] + 8 if offs[0] % 8 == 0 else offs[0])
+    out[:] = 0x33
+    file_decode_into(rs, sh, [i not in miss for i in range(k + m)], S, out, block)
+    assert np.array_equal(out, fbuf), miss
+    assert np.array_equal(np.stack(sh), ref), miss  # absent shards rebuilt in place
+    assert all(guards_intact(r, v) for r, v in shs) and guards_intact(oraw, out)
+
+
 @pytest.mark.parametrize("n,off", [((64 << 10) + 4100, 3), ((256 << 10) + 8200, 3), ((1 << 20) + 7, 4095), (5 << 20, 0)])
 def test_direct_interior_and_ends(gpu, oracle_lib, n, off):
     """Pageable calls: the pages wholly inside the range are coded in place,
