@@ -258,6 +258,59 @@ def test_direct_file_interior(gpu, oracle_lib, k, m, n, block, offs):
     assert all(guards_intact(r, v) for r, v in shs) and guards_intact(oraw, out)
 
 
+def test_direct_file_interior_threads(gpu, oracle_lib):
+    """Four threads at once, each encoding and decoding its own file, with
+    every file and shard a slice of ONE pageable buffer, packed back to back
+    at 8-byte-aligned odd offsets so neighbouring slices share pages.  Each
+    call locks only pages wholly inside its own slices, so no two calls' locks
+    overlap; every result is exact and the registry ends empty (conftest)."""
+    import threading
+    import rsamd
+    from rsamd.layout import file_decode_into, file_encode_into, file_layout
+    k, m, n, block = 4, 2, 3_000_104, 1000
+    rs = rsamd.ReedSolomon.create(k, m)
+    oc = oracle_lib.Codec(k, m)
+    _, S = file_layout(rs, n, block)
+    per = n + 2 * n + (k + m) * S + 8 * (k + m + 2)  # file, decoded file, shards (+ 8-byte gaps)
+    big = np.empty(4 * per + 4096, np.uint8)
+    rng = np.random.default_rng(11)
+    jobs = []
+    pos = (-big.ctypes.data) % 4096 + 24
+    for t in range(4):
+        f = big[pos:pos + n]; pos += n + 8
+        out = big[pos:pos + n]; pos += n + 8
+        sh = []
+        for _ in range(k + m):
+            sh.append(big[pos:pos + S]); pos += S + 8
+        f[:] = rng.integers(0, 256, n, dtype=np.uint8)
+        jobs.append((f, out, sh, (t % (k + m), (t + 3) % (k + m))))
+    refs = [oc.file_encode(f.tobytes(), block) for f, _, _, _ in jobs]
+    errors = []
+
+    def work(j):
+        f, out, sh, miss = jobs[j]
+        try:
+            for _ in range(3):
+                file_encode_into(rs, f, sh, block)
+                if not np.array_equal(np.stack(sh), refs[j]):
+                    errors.append((j, "encode"))
+                for s in miss:
+                    sh[s][:] = 0
+                out[:] = 0
+                file_decode_into(rs, sh, [i not in miss for i in range(k + m)], S, out, block)
+                if not np.array_equal(out, f) or not np.array_equal(np.stack(sh), refs[j]):
+                    errors.append((j, "decode", miss))
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append((j, repr(e)))
+
+    ts = [threading.Thread(target=work, args=(j,)) for j in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+
+
 @pytest.mark.parametrize("n,off", [((64 << 10) + 4100, 3), ((256 << 10) + 8200, 3), ((1 << 20) + 7, 4095), (5 << 20, 0)])
 def test_direct_interior_and_ends(gpu, oracle_lib, n, off):
     """Pageable calls: the pages wholly inside the range are coded in place,
