@@ -111,3 +111,67 @@ def test_device_batch_random(gpu, oracle_lib, case):
     pres = np.array([_random_present(rng, k, m) for _ in range(B)], dtype=bool)
     run(lambda p: device.decode_masked(rs, p, pres, lay, st),
         lambda v: _oracle_batch(oc, v, lambda t, sh: oc.decode_missing(sh, list(pres[t]), 0, S)))
+
+
+@pytest.mark.parametrize("case", range(16))
+def test_host_api_random_large(gpu, oracle_lib, case):
+    """The same host calls at sizes that take the direct path (capi.cpp
+    run_direct / run_direct_interior): shards of 256 KiB to 3 MiB, pageable
+    NumPy arrays (pages inside the range locked and coded in place, the ends
+    staged) or page-locked ones, each shard a view at a random offset of its
+    own buffer (common residues modulo 16 or 8, and none: the staged
+    pipeline), k up to 20 and m up to 8 (several launch groups)."""
+    import torch
+    import rsamd
+    rng = np.random.default_rng(3000 + case)
+    k = int(rng.integers(1, 21))
+    m = int(rng.integers(0, 9))
+    n = int(rng.integers(256 << 10, 3 << 20))
+    off = int(rng.integers(0, 5000))
+    cnt = int(rng.integers(n // 2, n - off + 1))
+    pinned = case % 4 == 3
+    residue = [16, 8, 1][case % 3]  # shard start offsets are multiples of this
+
+    def buf(nbytes):
+        if pinned:
+            return torch.empty(nbytes, dtype=torch.uint8, pin_memory=True).numpy()
+        return np.empty(nbytes, np.uint8)
+
+    def shard_views():
+        out = []
+        for _ in range(k + m):
+            o = int(rng.integers(0, 4096 // residue)) * residue
+            b = buf(n + o)
+            out.append(b[o:o + n])
+        return out
+
+    src = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k + m)]
+    rs = rsamd.ReedSolomon.create(k, m)
+    oc = oracle_lib.Codec(k, m)
+    desc = f"k={k} m={m} n={n} off={off} cnt={cnt} pinned={pinned} residue={residue}"
+
+    got = shard_views()
+    for g, s in zip(got, src):
+        g[:] = s
+    ref = [s.copy() for s in src]
+    rs.encodeParity(got, off, cnt)
+    oc.encode_parity(ref, off, cnt)
+    for i, (a, b) in enumerate(zip(got, ref)):
+        np.testing.assert_array_equal(a, b, err_msg=f"encode {desc} shard {i}")
+    assert rs.isParityCorrect(got, off, cnt)
+    if m:
+        j = int(rng.choice([off, off + cnt - 1, int(rng.integers(off, off + cnt))]))
+        s = k + int(rng.integers(0, m))
+        got[s][j] ^= 0x41
+        assert not rs.isParityCorrect(got, off, cnt), desc
+        got[s][j] ^= 0x41
+
+    present = _random_present(rng, k, m)
+    got2 = shard_views()
+    for g, s in zip(got2, src):
+        g[:] = s
+    ref = [s.copy() for s in src]
+    rs.decodeMissing(got2, present, off, cnt)
+    oc.decode_missing(ref, present, off, cnt)
+    for i, (a, b) in enumerate(zip(got2, ref)):
+        np.testing.assert_array_equal(a, b, err_msg=f"decode {desc} present={present} shard {i}")
