@@ -63,3 +63,46 @@ def test_file_paths_random(gpu, oracle_lib, case):
     decode_file_dev(rs, sdev.data_ptr(), S, stride, present, odev.data_ptr(), n, block, True, st)
     assert odev.cpu().numpy().tobytes() == data, (k, m, block, n, miss)
     assert np.array_equal(v[:, :S].cpu().numpy(), ref), (k, m, block, n, miss)  # write_missing
+
+
+@pytest.mark.parametrize("case", range(10))
+def test_file_host_random_large(gpu, oracle_lib, case):
+    """Host file calls at sizes that take the direct path (shards of 256 KiB
+    and more): pageable file, shards and output, each a view at a random
+    offset (8-byte aligned, or not for one case in four: staged), so the
+    block rows inside whole pages are coded in place and the rows either side
+    staged (capi.cpp file_encode_interior / file_decode_interior); random k,
+    m, block and erasures, against the oracle."""
+    from rsamd.layout import file_decode_into, file_encode_into, file_layout
+    import rsamd
+    rng = np.random.default_rng(9500 + case)
+    k = int(rng.integers(1, 11))
+    m = int(rng.integers(0, 5))
+    block = int(rng.choice([1000, 8, 4096, 520, 24, 1000]))
+    n = int(rng.integers(max(1, k) * (256 << 10), max(1, k) * (1 << 20)))
+    step = 1 if case % 4 == 3 else 8
+
+    def view(size):
+        o = int(rng.integers(0, 4096 // step)) * step
+        return np.empty(size + o, np.uint8)[o:o + size]
+
+    rs = rsamd.ReedSolomon.create(k, m)
+    oc = oracle_lib.Codec(k, m)
+    _, S = file_layout(rs, n, block)
+    f = view(n)
+    f[:] = rng.integers(0, 256, n, dtype=np.uint8)
+    sh = [view(S) for _ in range(k + m)]
+    for a in sh:
+        a[:] = 0xEE
+    file_encode_into(rs, f, sh, block)
+    ref = oc.file_encode(f.tobytes(), block)
+    assert np.array_equal(np.stack(sh), ref), (k, m, block, n)
+    e = int(rng.integers(0, m + 1))
+    miss = sorted(int(x) for x in rng.choice(k + m, e, replace=False)) if e else []
+    for j in miss:
+        sh[j][:] = 0
+    out = view(n)
+    out[:] = 0x33
+    file_decode_into(rs, sh, [i not in miss for i in range(k + m)], S, out, block)
+    assert np.array_equal(out, f), (k, m, block, n, miss)
+    assert np.array_equal(np.stack(sh), ref), (k, m, block, n, miss)
