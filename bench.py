@@ -1407,8 +1407,10 @@ def host_inclusive(rsamd, k, m, link=None):
     del pin
     out["host_inclusive_note"] = (f"{k}+{m}, {n >> 20} MiB host shards per call, pageable unless 'pinned' "
                                   f"(file legs: a {len(data) >> 20} MiB file); PCIe-bound, never the bench value; "
-                                  f"calls of >= 64 KiB per shard are coded in place across the link by one kernel "
-                                  f"(the direct path: pageable arrays page-locked for the call, no copies)")
+                                  f"pinned calls of >= 64 KiB per shard are coded in place across the link by one "
+                                  f"kernel (the direct path, no copies); pageable ones are staged through the "
+                                  f"library's pinned buffers (page-locking them for the call is opt-in, "
+                                  f"rs_set_host_register, and not timed here)")
     # Each leg against the link bound of its traffic (bytes up / down per user byte):
     # encode k up, m down per k user bytes; decode {0,1} k up, 2 down; file encode
     # 1 up, (k+m)/k down; file decode {0,k+m-1} 1 up (the k survivors), 1 + 2/k down

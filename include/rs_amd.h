@@ -97,6 +97,17 @@ RS_API int rs_device_count(void);
  * tests and services: a registration that outlives its call would leave the
  * runtime tracking pages the caller may free. */
 RS_API int rs_host_registry_state(int64_t *out, int n);
+/* Page-locking of pageable caller buffers for one call (the direct path on
+ * pageable memory: only pages wholly inside the caller's ranges are locked,
+ * the ends are staged).  OFF by default since the end of round 4: every GPU
+ * fault seen in the test suites (five, none in our kernels' accesses) came at
+ * a runtime pageable copy in a process that had page-locked NumPy memory, so
+ * pageable calls are staged through the library's own pinned buffers unless
+ * a service turns this on.  Buffers the caller page-locked itself
+ * (hipHostMalloc, hipHostRegister, pinned tensors) take the direct path
+ * either way.  Process-wide; returns the previous setting (0 or 1), or the
+ * current one when enable < 0. */
+RS_API int rs_set_host_register(int enable);
 
 /* ---------------------------------------------------------------------------
  * Host-buffer API (JNI-facing).  Shards are caller-owned host arrays,

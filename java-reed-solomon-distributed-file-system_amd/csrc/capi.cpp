@@ -289,7 +289,7 @@ int run_host(const std::vector<DevPlan> &plans, int nslots, const std::vector<in
     const size_t dmin = direct_min_bytes();
     const bool pinned = count >= std::min(dmin, size_t(1) << 20) && all_pinned(host, nslots);
     if (mode == Mode::Verify) RS_HIP(hipMemsetAsync(ctx->flag, 0, sizeof(int), ctx->stream));
-    if (pinned || count >= direct_pageable_min_bytes()) {
+    if (pinned || (count >= direct_pageable_min_bytes() && set_host_register(-1))) {
         bool taken = false;
         rc = pinned ? run_direct(ctx, plans, in_slots, out_slots, host, offset, count, mode, &taken)
                     : run_direct_interior(ctx, plans, nslots, in_slots, out_slots, host, offset, count, mode, &taken);
@@ -1060,6 +1060,8 @@ int rs_abi_version(void) { return RS_AMD_ABI_VERSION; }
 void rs_thread_release(void) { rsamd::host::release_thread_contexts(); }
 
 int rs_host_registry_state(int64_t *out, int n) { return rsamd::host::registry_state(out, n); }
+
+int rs_set_host_register(int enable) { return rsamd::host::set_host_register(enable); }
 
 int rs_device_count(void) {
     int n = 0;

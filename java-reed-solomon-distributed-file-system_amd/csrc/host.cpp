@@ -387,7 +387,8 @@ bool all_pinned(const uint8_t *const *ptrs, int n) {
 // and unregistering one while the other is in use aborts inside the HIP
 // runtime.  All or nothing: if any range cannot be locked the call is staged.
 // The destructor releases after the call's kernels have completed, also on
-// its error paths.  RSAMD_HOST_REGISTER=0 (TUNING builds) turns it off.
+// its error paths.  Off unless rs_set_host_register(1) (TUNING builds:
+// RSAMD_HOST_REGISTER=1 at load).
 namespace {
 
 struct HostRegistry {
@@ -434,12 +435,25 @@ void release_locked(HostRegistry &reg, std::vector<uintptr_t> &held) {
 
 }  // namespace
 
-bool HostRegistration::lock(const std::vector<std::pair<const uint8_t *, size_t>> &ranges) {
-    static const bool enabled = [] {
+namespace {
+// Off by default (include/rs_amd.h rs_set_host_register); a TUNING build's
+// RSAMD_HOST_REGISTER=1 sets the initial value.
+std::atomic<int> &host_register_flag() {
+    static std::atomic<int> *f = new std::atomic<int>([] {
         const char *e = tuning_env("RSAMD_HOST_REGISTER");
-        return !(e && e[0] == '0');
-    }();
-    if (!enabled) return false;
+        return e && e[0] == '1' ? 1 : 0;
+    }());
+    return *f;
+}
+}  // namespace
+
+int set_host_register(int enable) {
+    if (enable < 0) return host_register_flag().load();
+    return host_register_flag().exchange(enable ? 1 : 0);
+}
+
+bool HostRegistration::lock(const std::vector<std::pair<const uint8_t *, size_t>> &ranges) {
+    if (!host_register_flag().load()) return false;
     // The call's page ranges, sorted and merged: shards that are slices of
     // one allocation (sharing boundary pages) become one registration.
     constexpr uintptr_t kPage = 4096;

@@ -97,6 +97,9 @@ inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // rs_host_registry_state: registrations held now, their pages, and
 // hipHostUnregister failures since load.
 int registry_state(int64_t *out, int n);
+// rs_set_host_register: page-locking of pageable caller memory on or off
+// (off by default); returns the previous setting, or the current one for < 0.
+int set_host_register(int enable);
 
 // Page-locks pageable caller ranges for the duration of one pipelined call
 // (host.cpp: a process-wide, reference-counted registry of page ranges).

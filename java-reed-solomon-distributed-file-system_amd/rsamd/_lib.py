@@ -32,6 +32,7 @@ SIGNATURES = {
     "rs_last_error_message": (C.c_char_p, []),
     "rs_thread_release": (None, []),
     "rs_host_registry_state": (C.c_int, [C.POINTER(C.c_int64), C.c_int]),
+    "rs_set_host_register": (C.c_int, [C.c_int]),
     "rs_device_count": (C.c_int, []),
     "rs_encode_parity": (C.c_int, [C.c_void_p, u8pp, C.c_int, C.POINTER(C.c_int64), C.c_int32, C.c_int32]),
     "rs_decode_missing": (C.c_int, [C.c_void_p, u8pp, C.c_int, C.POINTER(C.c_int64), u8p, C.c_int32, C.c_int32]),

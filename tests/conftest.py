@@ -81,10 +81,15 @@ def bounds_check(request):
 
 @pytest.fixture(scope="session")
 def gpu(native):
-    """Skip-free GPU gate: a gpu-marked test on a box without a device is an error."""
+    """Skip-free GPU gate: a gpu-marked test on a box without a device is an error.
+    RSAMD_TEST_HOST_REGISTER=1 runs the session with page-locking of pageable
+    caller memory on (rs_set_host_register, off by default): the opt-in direct
+    path on pageable arrays, tested in a run of its own (tools/gpu_run.sh
+    hostreg)."""
     n = native.rs_device_count()
     if n < 1:
         pytest.fail("no HIP device visible to librsamd.so (gpu tests need an MI355X)")
+    native.rs_set_host_register(1 if os.environ.get("RSAMD_TEST_HOST_REGISTER") == "1" else 0)
     import torch
     assert torch.cuda.is_available(), "torch sees no GPU"
     return torch.device("cuda:0")
