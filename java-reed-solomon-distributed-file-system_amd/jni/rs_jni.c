@@ -115,6 +115,14 @@ JNIEXPORT void JNICALL Java_edu_cmu_reedsolomon_NativeReedSolomon_nativeThreadRe
     rs_thread_release();
 }
 
+/* NativeReedSolomon.setHostRegister: opt in to page-locking the (pageable)
+ * Java arrays of large calls for the call (include/rs_amd.h
+ * rs_set_host_register; off by default).  Returns the previous setting. */
+JNIEXPORT jboolean JNICALL Java_edu_cmu_reedsolomon_NativeReedSolomon_nativeSetHostRegister(JNIEnv *env, jclass cls,
+                                                                                           jboolean on) {
+    return rs_set_host_register(on ? 1 : 0) ? JNI_TRUE : JNI_FALSE;
+}
+
 /* ---- GpuCodingLoop: drop-in CodingLoop plugin (CodingLoop.java:79-117) ---- */
 
 JNIEXPORT void JNICALL Java_edu_cmu_reedsolomon_GpuCodingLoop_nativeCodeSomeShards(
