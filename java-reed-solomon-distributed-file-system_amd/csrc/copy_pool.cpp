@@ -1,5 +1,6 @@
 // copy_pool.cpp -- see copy_pool.hpp.
 #include "copy_pool.hpp"
+#include "tuning.hpp"
 
 #include <algorithm>
 #include <cstring>
@@ -13,7 +14,8 @@ constexpr size_t kPiece = size_t(1) << 20;  // bytes per work item
 CopyPool &CopyPool::get() {
     static CopyPool *pool = [] {
         const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-        return new CopyPool(int(std::min(15u, std::max(2u, hw / 2))));  // + the caller: <= 16 copying threads
+        // + the caller: <= 16 copying threads (TUNING builds: RSAMD_COPY_THREADS)
+        return new CopyPool(int(tuning_size("RSAMD_COPY_THREADS", std::min(15u, std::max(2u, hw / 2)))));
     }();
     return *pool;
 }

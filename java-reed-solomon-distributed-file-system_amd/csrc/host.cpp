@@ -336,7 +336,9 @@ size_t chunks_per_call() {
 size_t chunk_bytes(size_t total, int nslots, bool pinned) {
     const size_t per = chunks_per_call();
     size_t c = std::max(kMinChunk * 8 / per, (total / per + 255) / 256 * 256);
-    if (!pinned) c = std::min(c, std::max<size_t>(size_t(1) << 20, kMirrorBytes / size_t(std::max(1, nslots))));
+    // TUNING builds: RSAMD_MIRROR_BYTES overrides the mirror size per buffer
+    static const size_t mirror = rsamd::tuning_size("RSAMD_MIRROR_BYTES", kMirrorBytes);
+    if (!pinned) c = std::min(c, std::max<size_t>(size_t(1) << 20, mirror / size_t(std::max(1, nslots))));
     return std::min(kChunk, c);
 }
 
