@@ -99,14 +99,16 @@ RS_API int rs_device_count(void);
 RS_API int rs_host_registry_state(int64_t *out, int n);
 /* Page-locking of pageable caller buffers for one call (the direct path on
  * pageable memory: only pages wholly inside the caller's ranges are locked,
- * the ends are staged).  OFF by default since the end of round 4: every GPU
- * fault seen in the test suites (five, none in our kernels' accesses) came at
- * a runtime pageable copy in a process that had page-locked NumPy memory, so
- * pageable calls are staged through the library's own pinned buffers unless
- * a service turns this on.  Buffers the caller page-locked itself
- * (hipHostMalloc, hipHostRegister, pinned tensors) take the direct path
- * either way.  Process-wide; returns the previous setting (0 or 1), or the
- * current one when enable < 0. */
+ * the ends are staged).  OFF, and refused in product builds since the end of
+ * round 4: every GPU fault seen in the test suites (five, none in our
+ * kernels' accesses) came at a runtime pageable copy in a process that had
+ * page-locked NumPy memory, and one run with it on returned a wrong file
+ * encode, so pageable calls are always staged through the library's own
+ * pinned buffers.  Buffers the caller page-locked itself (hipHostMalloc,
+ * hipHostRegister, pinned tensors) take the direct path.  Product builds:
+ * enable > 0 returns RS_E_INVALID; 0 or < 0 return 0.  TUNING builds (for the
+ * investigation only): process-wide switch, returns the previous setting, or
+ * the current one when enable < 0. */
 RS_API int rs_set_host_register(int enable);
 
 /* ---------------------------------------------------------------------------

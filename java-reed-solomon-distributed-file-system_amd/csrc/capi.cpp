@@ -1061,7 +1061,15 @@ void rs_thread_release(void) { rsamd::host::release_thread_contexts(); }
 
 int rs_host_registry_state(int64_t *out, int n) { return rsamd::host::registry_state(out, n); }
 
-int rs_set_host_register(int enable) { return rsamd::host::set_host_register(enable); }
+int rs_set_host_register(int enable) {
+#if !RSAMD_TUNING_ENV
+    // Product builds never page-lock pageable caller memory:
+    // the faults, and one wrong result with it on, are not explained.
+    if (enable > 0)
+        return fail(RS_E_INVALID, "page-locking pageable caller memory is off in product builds (DESIGN.md 5.3)");
+#endif
+    return rsamd::host::set_host_register(enable);
+}
 
 int rs_device_count(void) {
     int n = 0;

@@ -87,11 +87,10 @@ public final class NativeReedSolomon implements AutoCloseable {
     }
 
     /**
-     * Opt in (or out) of page-locking the Java arrays of large calls for the
-     * duration of each call, so the GPU codes them in place across the link
-     * (about 1.4x the staged rate on 64 MiB shards).  Off by default: see
-     * rs_set_host_register in rs_amd.h.  Process-wide; returns the previous
-     * setting.
+     * Page-locking the Java arrays of large calls for each call (the GPU would
+     * code them in place across the link).  Off, and refused by product
+     * builds (UnsupportedOperationException): see rs_set_host_register in
+     * rs_amd.h.  setHostRegister(false) always succeeds.
      */
     public static boolean setHostRegister(boolean on) {
         return nativeSetHostRegister(on);

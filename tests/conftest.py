@@ -83,13 +83,16 @@ def bounds_check(request):
 def gpu(native):
     """Skip-free GPU gate: a gpu-marked test on a box without a device is an error.
     RSAMD_TEST_HOST_REGISTER=1 runs the session with page-locking of pageable
-    caller memory on (rs_set_host_register, off by default): the opt-in direct
-    path on pageable arrays, tested in a run of its own (tools/gpu_run.sh
-    hostreg)."""
+    caller memory on (rs_set_host_register; refused by product builds, so
+    with the TUNING build): the investigation's direct path on pageable
+    arrays, in a run of its own (tools/gpu_run.sh hostreg)."""
     n = native.rs_device_count()
     if n < 1:
         pytest.fail("no HIP device visible to librsamd.so (gpu tests need an MI355X)")
-    native.rs_set_host_register(1 if os.environ.get("RSAMD_TEST_HOST_REGISTER") == "1" else 0)
+    if os.environ.get("RSAMD_TEST_HOST_REGISTER") == "1":
+        assert native.rs_set_host_register(1) >= 0, "page-locking needs the TUNING build (RSAMD_TEST_LIB)"
+    else:
+        native.rs_set_host_register(0)
     import torch
     assert torch.cuda.is_available(), "torch sees no GPU"
     return torch.device("cuda:0")

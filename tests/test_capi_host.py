@@ -333,3 +333,13 @@ def test_host_registry_state_idle(native):
     one = (C.c_int64 * 1)(-1)
     assert native.rs_host_registry_state(one, 1) == 3 and one[0] == 0
     assert native.rs_host_registry_state(None, 0) == 3
+
+
+def test_host_register_refused_by_product(native):
+    """rs_set_host_register: the product library never page-locks pageable
+    caller memory: turning it on is refused with
+    RS_E_INVALID, turning it off or querying returns 0 (off)."""
+    assert native.rs_set_host_register(1) < 0
+    assert "product builds" in native.rs_last_error_message().decode()
+    assert native.rs_set_host_register(-1) == 0
+    assert native.rs_set_host_register(0) == 0

@@ -41,8 +41,8 @@ for step in "$@"; do
           > $out/pytest_bounds_$tag.log 2>&1 || { echo "bounds pytest failed"; tail -40 $out/pytest_bounds_$tag.log; exit 1; }
       tail -1 $out/pytest_bounds_$tag.log ;;
     hostreg)
-      # the opt-in page-locking of pageable caller memory (rs_set_host_register), in a process of its own
-      RSAMD_TEST_HOST_REGISTER=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_direct.py \
+      # page-locking of pageable caller memory (rs_set_host_register: TUNING build only), a process of its own
+      RSAMD_TEST_LIB=build/ab/tuning/librsamd.so RSAMD_TEST_HOST_REGISTER=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_direct.py \
           tests/test_gpu_host_register.py tests/test_gpu_random.py tests/test_gpu_file_random.py \
           -m gpu -x -v --timeout 300 --timeout-method thread \
           > $out/pytest_hostreg_$tag.log 2>&1 || { echo "hostreg pytest failed"; tail -40 $out/pytest_hostreg_$tag.log; exit 1; }
