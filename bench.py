@@ -1409,8 +1409,8 @@ def host_inclusive(rsamd, k, m, link=None):
                                   f"(file legs: a {len(data) >> 20} MiB file); PCIe-bound, never the bench value; "
                                   f"pinned calls of >= 64 KiB per shard are coded in place across the link by one "
                                   f"kernel (the direct path, no copies); pageable ones are staged through the "
-                                  f"library's pinned buffers (page-locking them for the call is opt-in, "
-                                  f"rs_set_host_register, and not timed here)")
+                                  f"library's pinned buffers (product builds never page-lock caller memory, "
+                                  f"DESIGN.md 5.3)")
     # Each leg against the link bound of its traffic (bytes up / down per user byte):
     # encode k up, m down per k user bytes; decode {0,1} k up, 2 down; file encode
     # 1 up, (k+m)/k down; file decode {0,k+m-1} 1 up (the k survivors), 1 + 2/k down
