@@ -62,8 +62,10 @@ typedef struct rs_codec rs_codec;
  * library it was not written for: bind only if rs_abi_version() equals the
  * RS_AMD_ABI_VERSION the binding was written against.
  *   3: rs_granule_copy_shard takes n_stripes after granule (round 3).
- *   4: rs_abi_version (this), rs_shard_stride_recommended. */
-#define RS_AMD_ABI_VERSION 4
+ *   4: rs_abi_version (this), rs_shard_stride_recommended.
+ *   5: rs_set_host_register and rs_host_registry_state removed: the library
+ *      no longer page-locks caller memory (round 5). */
+#define RS_AMD_ABI_VERSION 5
 RS_API int rs_abi_version(void);
 
 /* ---------------------------------------------------------------------------
@@ -90,32 +92,15 @@ RS_API const char *rs_last_error_message(void);
 RS_API void rs_thread_release(void);
 /* Number of visible HIP devices (0 when none). */
 RS_API int rs_device_count(void);
-/* The host-memory registry of the direct path (pageable caller buffers are
- * page-locked for one call): out[0] = registrations held now (0 whenever no
- * host call is running), out[1] = their pages, out[2] = hipHostUnregister
- * failures since load.  Writes min(n, 3) values; returns 3.  A check for
- * tests and services: a registration that outlives its call would leave the
- * runtime tracking pages the caller may free. */
-RS_API int rs_host_registry_state(int64_t *out, int n);
-/* Page-locking of pageable caller buffers for one call (the direct path on
- * pageable memory: only pages wholly inside the caller's ranges are locked,
- * the ends are staged).  OFF, and refused in product builds since the end of
- * round 4: every GPU fault seen in the test suites (five, none in our
- * kernels' accesses) came at a runtime pageable copy in a process that had
- * page-locked NumPy memory, and one run with it on returned a wrong file
- * encode, so pageable calls are always staged through the library's own
- * pinned buffers.  Buffers the caller page-locked itself (hipHostMalloc,
- * hipHostRegister, pinned tensors) take the direct path.  Product builds:
- * enable > 0 returns RS_E_INVALID; 0 or < 0 return 0.  TUNING builds (for the
- * investigation only): process-wide switch, returns the previous setting, or
- * the current one when enable < 0. */
-RS_API int rs_set_host_register(int enable);
-
 /* ---------------------------------------------------------------------------
  * Host-buffer API (JNI-facing).  Shards are caller-owned host arrays,
- * mutated in place.  Each call stages [offset, offset+byte_count) of the
- * shards to the GPU, codes them there and copies the outputs back.
- * shard_lens[i] is the Java array length of shards[i] (for the size checks).
+ * mutated in place.  shard_lens[i] is the Java array length of shards[i]
+ * (for the size checks).  The library never page-locks caller memory:
+ *  - arrays the caller page-locked itself (hipHostMalloc, hipHostRegister,
+ *    pinned tensors) are coded in place across the link by one kernel;
+ *  - pageable arrays (JVM heap arrays through JNI) are copied chunk by chunk
+ *    into the library's own device-mapped pinned slots, coded there by the
+ *    same kernels and copied back, the copies overlapped with the link.
  * ------------------------------------------------------------------------- */
 
 /* ReedSolomon.encodeParity(byte[][] shards, int offset, int byteCount)

@@ -88,64 +88,22 @@ uint8_t *host_dev_addr(const void *p) {
 //   256 KiB 93.5 -> 54.7 / 96.3 -> 50.5;  1 MiB 291 -> 122;  4 MiB 696 -> 371 us.
 size_t direct_min_bytes() { return rsamd::tuning_size("RSAMD_DIRECT_MIN", size_t(64) << 10); }
 
-// The same for pageable arrays, which the direct path takes only through
-// run_direct_interior (its ends cost a staged kernel and two memcpys per
-// call): 4+2 x 64 KiB pageable ran 48 us that way against ~40 us staged
-// (bench_r4zm.json cfg0 legs), while from 256 KiB the direct kernels win
-// clearly (93.5 -> 54.7 us, direct_small_r3s2k.txt).  TUNING builds:
-// RSAMD_DIRECT_PAGEABLE_MIN.
-size_t direct_pageable_min_bytes() {
-    return std::max(direct_min_bytes(), rsamd::tuning_size("RSAMD_DIRECT_PAGEABLE_MIN", size_t(256) << 10));
-}
-
-// True when every range starts and ends on a page boundary, so page-locking
-// it covers no byte outside it (run_direct_interior's rule; the file calls
-// lock caller memory only then).
-bool whole_pages(const std::vector<std::pair<const uint8_t *, size_t>> &ranges) {
-    for (const auto &r : ranges)
-        if (reinterpret_cast<uintptr_t>(r.first) % 4096 || (reinterpret_cast<uintptr_t>(r.first) + r.second) % 4096)
-            return false;
-    return true;
-}
-
-// One caller array of a block-row call (the host file calls): row r spans
-// [p + r*per_row, p + (r+1)*per_row), clipped to len.
-struct RowArray {
-    const uint8_t *p;
-    size_t len, per_row;
-};
-
-// The rows [*r0, *r1) of [0, rows) whose bytes lie, in every array, inside
-// the pages wholly within that array (so locking them covers no byte the
-// caller did not pass); false when there are none.
-bool interior_rows(const std::vector<RowArray> &arrays, size_t rows, size_t *r0, size_t *r1) {
-    constexpr uintptr_t kPage = 4096;
-    size_t lo = 0, hi = rows;
-    for (const RowArray &a : arrays) {
-        if (a.len == 0) continue;
-        const uintptr_t p = reinterpret_cast<uintptr_t>(a.p);
-        const uintptr_t first = (p + kPage - 1) & ~(kPage - 1), end = (p + a.len) & ~(kPage - 1);
-        if (end <= first) return false;
-        lo = std::max(lo, (first - p + a.per_row - 1) / a.per_row);
-        hi = std::min(hi, (end - p) / a.per_row);
-    }
-    *r0 = lo;
-    *r1 = hi;
-    return hi > lo;
-}
+// Bytes per shard from which a pageable call takes the mirrored pipeline
+// instead of the single zero-copy staging pass (TUNING builds:
+// RSAMD_MIRROR_MIN, read per call).
+size_t mirror_min_bytes() { return rsamd::tuning_size("RSAMD_MIRROR_MIN", size_t(256) << 10); }
 
 // The direct kernels' plans for columns [offset, offset+count) of the slots:
 // false (nothing enqueued) when a shard has no device address, a plan is
 // wider than kMaxDirectIn inputs, or the addresses share no 8-byte residue.
+// addr(slot) gives a slot's device address (nullptr: none).
 bool direct_plans(const std::vector<DevPlan> &plans, const std::vector<int> &in_slots,
-                  const std::vector<int> &out_slots, uint8_t *const *host, size_t offset,
+                  const std::vector<int> &out_slots, const std::function<uint8_t *(int)> &addr,
                   std::vector<rsamd::DirectPlan> *out) {
     if (!direct_enabled() || plans.empty()) return false;
     std::vector<rsamd::DirectPlan> dp(plans.size());
-    // The range's own first byte: a call locked for its range only has no
-    // device mapping before host[slot] + offset.
     auto dev_addr = [&](int slot, uint8_t **a) {
-        *a = host_dev_addr(host[slot] + offset);
+        *a = addr(slot);
         return *a != nullptr;
     };
     for (size_t g = 0; g < plans.size(); ++g) {
@@ -200,76 +158,46 @@ int run_direct(ThreadCtx *ctx, const std::vector<DevPlan> &plans, const std::vec
                bool *taken) {
     *taken = false;
     std::vector<rsamd::DirectPlan> dp;
-    if (!direct_plans(plans, in_slots, out_slots, host, offset, &dp)) return RS_OK;
+    if (!direct_plans(plans, in_slots, out_slots, [&](int sl) { return host_dev_addr(host[sl] + offset); }, &dp))
+        return RS_OK;
     *taken = true;
     return launch_direct(ctx, dp, count, mode);
 }
 
-// Pageable caller arrays.  Only the pages wholly inside every slot's range
-// are page-locked, and their columns coded in place by the direct kernels;
-// the columns at either end (less than a page per slot) are copied through
-// the zero-copy staging buffer and coded there, in the same launch sequence
-// and under the same synchronisation.  A page-lock therefore never covers a
-// byte the caller did not pass: the runtime page-locks the pages of its own
-// pageable copies too, and a lock of ours that reached into a neighbouring
-// allocation could be dropped under one of those.  *taken =
-// false (nothing enqueued) when the interior is under a page or the direct
-// kernels cannot take it.
-int run_direct_interior(ThreadCtx *ctx, const std::vector<DevPlan> &plans, int nslots,
-                        const std::vector<int> &in_slots, const std::vector<int> &out_slots, uint8_t *const *host,
-                        size_t offset, size_t count, Mode mode, bool *taken) {
+// Pageable caller arrays (JNI heap arrays): copied chunk by chunk into the
+// context's device-mapped pinned slots and coded there in place by the direct
+// kernels, the copies overlapped with the link (host.hpp run_mirrored).  The
+// library never page-locks caller memory.  *taken = false
+// (nothing done) when a plan is wider than the direct kernels take.
+constexpr size_t kMirrorAlign = 4096;  // slots on page boundaries: the kernels' waves move whole lines
+
+int run_mirror_host(ThreadCtx *ctx, const std::vector<DevPlan> &plans, int nslots, const std::vector<int> &in_slots,
+                    const std::vector<int> &out_slots, uint8_t *const *host, size_t offset, size_t count, Mode mode,
+                    bool *taken) {
     *taken = false;
-    constexpr uintptr_t kPage = 4096;
-    std::vector<int> slots = in_slots;
-    if (mode == Mode::Code) slots.insert(slots.end(), out_slots.begin(), out_slots.end());
-    size_t lo = 0, hi = count;
-    for (int sl : slots) {
-        const uintptr_t a = reinterpret_cast<uintptr_t>(host[sl] + offset);
-        const uintptr_t first = (a + kPage - 1) & ~(kPage - 1), end = (a + count) & ~(kPage - 1);
-        if (end <= first) return RS_OK;  // no whole page inside this slot's range
-        lo = std::max<size_t>(lo, first - a);
-        hi = std::min<size_t>(hi, end - a);
-    }
-    if (hi <= lo) return RS_OK;
-    std::vector<rsamd::DirectPlan> dp;
-    HostRegistration reg;
-    std::vector<std::pair<const uint8_t *, size_t>> ranges;
-    for (int sl : slots) ranges.push_back({host[sl] + offset + lo, hi - lo});
-    if (!reg.lock(ranges)) return RS_OK;
-    if (!direct_plans(plans, in_slots, out_slots, host, offset + lo, &dp)) return RS_OK;
-    const size_t ends = lo + (count - hi);
-    const size_t stride = round_up(std::max<size_t>(ends, 1), 256);
-    if (ends) {
-        int rc = zero_copy_buffer(ctx, stride * size_t(nslots));
-        if (rc) return rc;
-        for (int sl : in_slots) {
-            std::memcpy(ctx->zc + size_t(sl) * stride, host[sl] + offset, lo);
-            std::memcpy(ctx->zc + size_t(sl) * stride + lo, host[sl] + offset + hi, count - hi);
-        }
-        Geometry g;
-        g.base = ctx->zc_dev;
-        g.n_stripes = 1;
-        g.col0 = 0;
-        g.len = ends;
-        g.shard_stride = stride;
-        g.stripe_stride = stride * size_t(nslots);
-        for (const DevPlan &p : plans) {
-            const hipError_t e = rsamd::launch_gf(g, p, mode, ctx->flag, ctx->stream);
-            if (e != hipSuccess) {
-                (void)hipStreamSynchronize(ctx->stream);
-                return hip_fail(e, "launch_gf (direct call's ends)");
-            }
-        }
-    }
+    if (!direct_enabled() || plans.empty()) return RS_OK;
+    for (const DevPlan &p : plans)
+        if (p.nin > rsamd::kMaxDirectIn) return RS_OK;
+    const size_t chunk = mirror_chunk_bytes(count, nslots, kMirrorAlign);
+    const std::vector<size_t> cb = ramp_bounds(count, chunk, kMirrorAlign);
+    size_t widest = 0;
+    for (size_t j = 0; j + 1 < cb.size(); ++j) widest = std::max(widest, cb[j + 1] - cb[j]);
+    const size_t slot_stride = round_up(widest, kMirrorAlign);
+    auto io = [&](size_t j, std::vector<Xfer> *in, std::vector<Xfer> *out) {
+        const size_t lo = cb[j], n = cb[j + 1] - lo;
+        for (int s : in_slots) in->push_back({host[s] + offset + lo, size_t(s) * slot_stride, n});
+        if (mode == Mode::Code)
+            for (int s : out_slots) out->push_back({host[s] + offset + lo, size_t(s) * slot_stride, n});
+    };
+    auto code = [&](size_t j, uint8_t *dev, hipStream_t st) -> int {
+        std::vector<rsamd::DirectPlan> dp;
+        if (!direct_plans(plans, in_slots, out_slots, [&](int sl) { return dev + size_t(sl) * slot_stride; }, &dp))
+            return fail(RS_E_HIP, "direct plans over the mirror slots");
+        for (const rsamd::DirectPlan &d : dp) RS_HIP(rsamd::launch_gf_direct(d, cb[j + 1] - cb[j], mode, ctx->flag, st));
+        return RS_OK;
+    };
     *taken = true;
-    int rc = launch_direct(ctx, dp, hi - lo, mode);  // synchronises the stream: the ends too
-    if (rc) return rc;
-    if (ends && mode == Mode::Code)
-        for (int sl : out_slots) {
-            std::memcpy(host[sl] + offset, ctx->zc + size_t(sl) * stride, lo);
-            std::memcpy(host[sl] + offset + hi, ctx->zc + size_t(sl) * stride + lo, count - hi);
-        }
-    return RS_OK;
+    return run_mirrored(ctx, cb.size() - 1, slot_stride * size_t(nslots), io, code);
 }
 
 // Stage [offset, offset+count) of the host shards (slot-indexed), run every
@@ -284,15 +212,16 @@ int run_host(const std::vector<DevPlan> &plans, int nslots, const std::vector<in
     int rc = thread_ctx(&ctx);
     if (rc) return rc;
     // Small calls stay on the zero-copy staging path (direct_min_bytes): skip the
-    // per-buffer pointer queries.  Larger pageable calls lock the caller's
-    // ranges for the call and take the direct path (or the pipeline).
+    // per-buffer pointer queries.  Larger calls: caller-pinned arrays are coded
+    // in place by the direct kernels, pageable ones through the mirrored
+    // pipeline (or, for plans the direct kernels cannot take, the DMA pipeline).
     const size_t dmin = direct_min_bytes();
     const bool pinned = count >= std::min(dmin, size_t(1) << 20) && all_pinned(host, nslots);
     if (mode == Mode::Verify) RS_HIP(hipMemsetAsync(ctx->flag, 0, sizeof(int), ctx->stream));
-    if (pinned || (count >= direct_pageable_min_bytes() && set_host_register(-1))) {
+    if (pinned || count >= mirror_min_bytes()) {
         bool taken = false;
         rc = pinned ? run_direct(ctx, plans, in_slots, out_slots, host, offset, count, mode, &taken)
-                    : run_direct_interior(ctx, plans, nslots, in_slots, out_slots, host, offset, count, mode, &taken);
+                    : run_mirror_host(ctx, plans, nslots, in_slots, out_slots, host, offset, count, mode, &taken);
         if (rc) return rc;
         if (taken) {
             if (mode == Mode::Verify) {
@@ -588,34 +517,90 @@ int file_encode_staged(const Codec &c, const uint8_t *file, size_t file_len, siz
     return run_chunks(ctx, f.n, f.buf_bytes, pinned, io, code);
 }
 
-// Pageable host file encode: file_decode_interior's split -- the block rows
-// inside whole pages of the file and of every shard coded in place, the rows
-// either side staged.
-int file_encode_interior(const Codec &c, const uint8_t *file, size_t file_len, size_t blk, uint8_t *const *shards,
+// Mirrored form of the host file calls (pageable callers, host.hpp
+// run_mirrored): chunks of block rows, each slot laid out as [the rows' file
+// bytes][shard 0 .. total-1 columns of the rows], page-aligned, coded in the
+// slot by the fused direct file kernels.  Rows per chunk, the chunk
+// boundaries (in rows) and the slot layout:
+struct MirrorRows {
+    std::vector<size_t> bounds;
+    size_t fstride = 0, sstride = 0, buf_bytes = 0;
+};
+
+MirrorRows mirror_rows(int k, int total, size_t rows, size_t blk) {
+    MirrorRows r;
+    // a row is k*blk file bytes plus total*blk shard bytes: k + total slots of blk
+    const size_t per = mirror_chunk_bytes(rows * blk, k + total, blk);
+    r.bounds = ramp_bounds(rows, std::max<size_t>(1, per / blk), 1);
+    size_t widest = 0;
+    for (size_t j = 0; j + 1 < r.bounds.size(); ++j) widest = std::max(widest, r.bounds[j + 1] - r.bounds[j]);
+    r.fstride = round_up(widest * size_t(k) * blk, kMirrorAlign);
+    r.sstride = round_up(widest * blk, kMirrorAlign);
+    r.buf_bytes = r.fstride + r.sstride * size_t(total);
+    return r;
+}
+
+// *taken = false (nothing done) when the direct file kernel cannot take the
+// code or the block size (more than kMaxOut parity shards, k above
+// kMaxDirectIn, blocks that are not 8-byte multiples).
+int file_encode_mirrored(const Codec &c, const uint8_t *file, size_t file_len, size_t blk, uint8_t *const *shards,
                          size_t S, ThreadCtx *ctx, bool *taken) {
     *taken = false;
+    if (!direct_enabled() || c.m() > rsamd::kMaxOut || c.k() > rsamd::kMaxDirectIn || blk % 8) return RS_OK;
     const int T = c.total();
-    const size_t kb = size_t(c.k()) * blk, rows = S / blk;
-    std::vector<RowArray> arrays{{file, file_len, kb}};
-    for (int i = 0; i < T; ++i) arrays.push_back({shards[i], S, blk});
-    size_t r0 = 0, r1 = 0;
-    if (!interior_rows(arrays, rows, &r0, &r1)) return RS_OK;
-    std::vector<std::pair<const uint8_t *, size_t>> ranges;
-    for (const RowArray &a : arrays) ranges.push_back({a.p + r0 * a.per_row, (r1 - r0) * a.per_row});
-    HostRegistration reg;
-    if (!reg.lock(ranges)) return RS_OK;
-    std::vector<uint8_t *> sh(T);
-    for (int i = 0; i < T; ++i) sh[i] = shards[i] + r0 * blk;
-    int rc = file_encode_direct(c, file + r0 * kb, (r1 - r0) * kb, blk, sh.data(), (r1 - r0) * blk, ctx, taken);
-    if (rc || !*taken) return rc;
-    for (const auto &piece : {std::make_pair(size_t(0), r0), std::make_pair(r1, rows)}) {
-        const size_t a = piece.first, b = piece.second;
-        if (b <= a) continue;
-        for (int i = 0; i < T; ++i) sh[i] = shards[i] + a * blk;
-        rc = file_encode_staged(c, file + a * kb, std::min((b - a) * kb, file_len - a * kb), blk, sh.data(),
-                                (b - a) * blk, ctx, false);
-        if (rc) return rc;
+    const size_t kb = size_t(c.k()) * blk;
+    const MirrorRows mr = mirror_rows(c.k(), T, S / blk, blk);
+    const uint32_t *tabs = nullptr;
+    if (c.m() > 0) {
+        std::vector<DevPlan> plans;
+        RS_HIP(c.encode_plan().device_plans(&plans));
+        tabs = plans[0].tabs;
     }
+    auto flen_of = [&](size_t j) { return std::min((mr.bounds[j + 1] - mr.bounds[j]) * kb, file_len - mr.bounds[j] * kb); };
+    auto io = [&](size_t j, std::vector<Xfer> *in, std::vector<Xfer> *out) {
+        const size_t r0 = mr.bounds[j], nr = mr.bounds[j + 1] - r0;
+        in->push_back({const_cast<uint8_t *>(file) + r0 * kb, 0, flen_of(j)});
+        for (int i = 0; i < T; ++i) out->push_back({shards[i] + r0 * blk, mr.fstride + size_t(i) * mr.sstride, nr * blk});
+    };
+    auto code = [&](size_t j, uint8_t *dev, hipStream_t st) -> int {
+        rsamd::FileDirect d;
+        d.k = c.k();
+        d.nout = c.m();
+        d.block = blk;
+        d.units = (mr.bounds[j + 1] - mr.bounds[j]) * blk / 8;
+        d.file_len = flen_of(j);
+        d.file = dev;
+        d.tabs = tabs;
+        for (int i = 0; i < T; ++i) d.out[i] = dev + mr.fstride + size_t(i) * mr.sstride;
+        RS_HIP(rsamd::launch_file_encode_direct(d, st));
+        return RS_OK;
+    };
+    *taken = true;
+    return run_mirrored(ctx, mr.bounds.size() - 1, mr.buf_bytes, io, code);
+}
+
+// The fused direct decode's shape for a presence pattern (no pointers): the
+// survivors are the first k present shards, the outputs every absent one.
+// RS_OK with *ok = false when the direct kernel cannot take it.
+// *keep holds the decode plan (and so d->tabs) for the caller's kernels.
+int file_decode_shape(const Codec &c, const uint8_t *present, const std::vector<int> &surv,
+                      const std::vector<int> &missing, size_t blk, rsamd::FileDirect *d,
+                      std::shared_ptr<const Plan> *keep, bool *ok) {
+    *ok = false;
+    if (!direct_enabled() || missing.size() > size_t(rsamd::kMaxOut) || c.k() > rsamd::kMaxDirectIn) return RS_OK;
+    d->k = c.k();
+    d->nout = int(missing.size());
+    d->block = blk;
+    if (!missing.empty()) {
+        int rc = c.decode_plan(present, keep);
+        if (rc) return fail(rc, rc == RS_E_SINGULAR ? "Matrix is singular" : "Not enough shards present");
+        std::vector<DevPlan> plans;
+        RS_HIP((*keep)->device_plans(&plans));
+        d->tabs = plans[0].tabs;
+    }
+    for (int i = 0; i < d->k; ++i) d->in_shard[i] = surv[i];
+    for (int q = 0; q < d->nout; ++q) d->out_shard[q] = missing[q];
+    *ok = true;
     return RS_OK;
 }
 
@@ -623,29 +608,17 @@ int file_decode_direct(const Codec &c, uint8_t *const *shards, const uint8_t *pr
                        const std::vector<int> &missing, size_t blk, uint8_t *file_out, size_t file_size,
                        size_t cols, ThreadCtx *ctx, bool *taken) {
     *taken = false;
-    if (!direct_enabled() || missing.size() > size_t(rsamd::kMaxOut) || c.k() > rsamd::kMaxDirectIn) return RS_OK;
     rsamd::FileDirect d;
-    d.k = c.k();
-    d.nout = int(missing.size());
-    d.block = blk;
+    std::shared_ptr<const Plan> plan;
+    bool ok = false;
+    int rc0 = file_decode_shape(c, present, surv, missing, blk, &d, &plan, &ok);
+    if (rc0 || !ok) return rc0;
     d.units = cols / 8;
     d.file_len = file_size;
-    std::shared_ptr<const Plan> plan;
-    std::vector<DevPlan> plans;
-    if (!missing.empty()) {  // survivors = the first k present, outputs = every absent shard
-        int rc = c.decode_plan(present, &plan);
-        if (rc) return fail(rc, rc == RS_E_SINGULAR ? "Matrix is singular" : "Not enough shards present");
-        RS_HIP(plan->device_plans(&plans));
-        d.tabs = plans[0].tabs;
-    }
-    for (int i = 0; i < d.k; ++i) {
-        d.in_shard[i] = surv[i];
+    for (int i = 0; i < d.k; ++i)
         if (!(d.in[i] = host_dev_addr(shards[surv[i]]))) return RS_OK;
-    }
-    for (int q = 0; q < d.nout; ++q) {
-        d.out_shard[q] = missing[q];
+    for (int q = 0; q < d.nout; ++q)
         if (!(d.out[q] = host_dev_addr(shards[missing[q]]))) return RS_OK;
-    }
     if (file_size && !(d.file_out = host_dev_addr(file_out))) return RS_OK;
     if (!rsamd::file_direct_ok(d, false)) return RS_OK;
     bounds::allow(d.file_out, file_size);
@@ -692,44 +665,47 @@ int file_decode_staged(const Codec &c, uint8_t *const *shards, size_t S, const u
     return run_chunks(ctx, (rows_needed + f.R - 1) / f.R, f.buf_bytes, pinned, io, code);
 }
 
-// Pageable host file decode: the block rows whose bytes lie inside whole
-// pages of every array (survivors, rebuilt shards, file) are page-locked and
-// coded in place by the direct kernel; the few rows either side (under a page
-// of each array) are staged.  As run_direct_interior, no lock covers a byte
-// the caller did not pass.  *taken = false, nothing done,
-// when there is no such interior or the direct kernel cannot take it.
-int file_decode_interior(const Codec &c, uint8_t *const *shards, size_t S, const uint8_t *present,
+// Mirrored form of the host file decode (pageable callers; MirrorRows):
+// the survivors' rows copied in, the fused direct decode kernel rebuilds the
+// absent shards' rows and writes the rows' file bytes in the slot, both copied
+// out.  *taken = false (nothing done) when the direct kernel cannot take the
+// pattern or the block size.
+int file_decode_mirrored(const Codec &c, uint8_t *const *shards, size_t S, const uint8_t *present,
                          const std::vector<int> &surv, const std::vector<int> &missing, size_t blk, uint8_t *file_out,
                          size_t file_size, size_t rows_needed, ThreadCtx *ctx, bool *taken) {
     *taken = false;
+    if (blk % 8) return RS_OK;
+    rsamd::FileDirect shape;
+    std::shared_ptr<const Plan> plan;
+    bool ok = false;
+    int rc = file_decode_shape(c, present, surv, missing, blk, &shape, &plan, &ok);
+    if (rc || !ok) return rc;
+    (void)S;
     const int T = c.total();
     const size_t kb = size_t(c.k()) * blk;
-    std::vector<RowArray> arrays;
-    for (int i : surv) arrays.push_back({shards[i], rows_needed * blk, blk});
-    for (int i : missing) arrays.push_back({shards[i], S, blk});
-    arrays.push_back({file_out, file_size, kb});
-    size_t r0 = 0, r1 = 0;
-    if (!interior_rows(arrays, rows_needed, &r0, &r1)) return RS_OK;
-    std::vector<std::pair<const uint8_t *, size_t>> ranges;
-    for (const RowArray &a : arrays)
-        if (a.len) ranges.push_back({a.p + r0 * a.per_row, (r1 - r0) * a.per_row});
-    HostRegistration reg;
-    if (!reg.lock(ranges)) return RS_OK;
-    auto fsz = [&](size_t a, size_t b) { return file_size > a * kb ? std::min(file_size - a * kb, (b - a) * kb) : 0; };
-    std::vector<uint8_t *> sh(T);
-    for (int i = 0; i < T; ++i) sh[i] = shards[i] + r0 * blk;
-    int rc = file_decode_direct(c, sh.data(), present, surv, missing, blk, file_out + r0 * kb, fsz(r0, r1),
-                                (r1 - r0) * blk, ctx, taken);
-    if (rc || !*taken) return rc;
-    for (const auto &piece : {std::make_pair(size_t(0), r0), std::make_pair(r1, rows_needed)}) {
-        const size_t a = piece.first, b = piece.second;
-        if (b <= a) continue;
-        for (int i = 0; i < T; ++i) sh[i] = shards[i] + a * blk;
-        rc = file_decode_staged(c, sh.data(), (b - a) * blk, present, surv, missing, blk, file_out + a * kb,
-                                fsz(a, b), ctx, false);
-        if (rc) return rc;
-    }
-    return RS_OK;
+    const MirrorRows mr = mirror_rows(c.k(), T, rows_needed, blk);
+    auto flen_of = [&](size_t j) {
+        const size_t fo = mr.bounds[j] * kb;
+        return file_size > fo ? std::min((mr.bounds[j + 1] - mr.bounds[j]) * kb, file_size - fo) : size_t(0);
+    };
+    auto io = [&](size_t j, std::vector<Xfer> *in, std::vector<Xfer> *out) {
+        const size_t r0 = mr.bounds[j], n = (mr.bounds[j + 1] - r0) * blk;
+        for (int sidx : surv) in->push_back({shards[sidx] + r0 * blk, mr.fstride + size_t(sidx) * mr.sstride, n});
+        for (int sidx : missing) out->push_back({shards[sidx] + r0 * blk, mr.fstride + size_t(sidx) * mr.sstride, n});
+        if (const size_t flen = flen_of(j)) out->push_back({file_out + r0 * kb, 0, flen});
+    };
+    auto code = [&](size_t j, uint8_t *dev, hipStream_t st) -> int {
+        rsamd::FileDirect d = shape;
+        d.units = (mr.bounds[j + 1] - mr.bounds[j]) * blk / 8;
+        d.file_len = flen_of(j);
+        d.file_out = dev;
+        for (int i = 0; i < d.k; ++i) d.in[i] = dev + mr.fstride + size_t(surv[i]) * mr.sstride;
+        for (int q = 0; q < d.nout; ++q) d.out[q] = dev + mr.fstride + size_t(missing[q]) * mr.sstride;
+        RS_HIP(rsamd::launch_file_decode_direct(d, st));
+        return RS_OK;
+    };
+    *taken = true;
+    return run_mirrored(ctx, mr.bounds.size() - 1, mr.buf_bytes, io, code);
 }
 
 // rs_file_decode when byteCntInShard is the whole shard: one pass per chunk
@@ -762,15 +738,8 @@ int file_decode_chunked(const Codec &c, uint8_t *const *shards, const int64_t *l
     const size_t blk = size_t(block);
     std::vector<const uint8_t *> bufs(shards, shards + T);
     bufs.push_back(file_out);
-    bool pinned = all_pinned(bufs.data(), int(bufs.size()));
-    HostRegistration reg;
+    const bool pinned = all_pinned(bufs.data(), int(bufs.size()));
     const bool big = file_chunks(k, T, size_t(S), blk, false).n > 1 || size_t(S) >= direct_min_bytes();
-    if (!pinned && big) {
-        std::vector<std::pair<const uint8_t *, size_t>> ranges;
-        for (int i = 0; i < T; ++i) ranges.push_back({shards[i], size_t(S)});
-        ranges.push_back({file_out, size_t(file_size)});
-        pinned = whole_pages(ranges) && reg.lock(ranges);
-    }
     std::vector<int> surv, missing;
     for (int i = 0; i < T; ++i) {
         if (present[i] && int(surv.size()) < k) surv.push_back(i);
@@ -781,8 +750,8 @@ int file_decode_chunked(const Codec &c, uint8_t *const *shards, const int64_t *l
     if (pinned) {  // direct path: the survivors, rebuilt shards and file coded in place
         rc = file_decode_direct(c, shards, present, surv, missing, blk, file_out, size_t(file_size),
                                 rows_needed * blk, ctx, &taken);
-    } else if (big && size_t(S) >= direct_pageable_min_bytes()) {
-        rc = file_decode_interior(c, shards, size_t(S), present, surv, missing, blk, file_out, size_t(file_size),
+    } else if (big && size_t(S) >= mirror_min_bytes()) {
+        rc = file_decode_mirrored(c, shards, size_t(S), present, surv, missing, blk, file_out, size_t(file_size),
                                   rows_needed, ctx, &taken);
     }
     if (rc || taken) return rc;
@@ -1058,18 +1027,6 @@ const char *rs_last_error_message(void) { return rsamd::host::last_error(); }
 int rs_abi_version(void) { return RS_AMD_ABI_VERSION; }
 
 void rs_thread_release(void) { rsamd::host::release_thread_contexts(); }
-
-int rs_host_registry_state(int64_t *out, int n) { return rsamd::host::registry_state(out, n); }
-
-int rs_set_host_register(int enable) {
-#if !RSAMD_TUNING_ENV
-    // Product builds never page-lock pageable caller memory:
-    // the faults, and one wrong result with it on, are not explained.
-    if (enable > 0)
-        return fail(RS_E_INVALID, "page-locking pageable caller memory is off in product builds (DESIGN.md 5.3)");
-#endif
-    return rsamd::host::set_host_register(enable);
-}
 
 int rs_device_count(void) {
     int n = 0;
@@ -1403,20 +1360,13 @@ int rs_file_encode(const rs_codec *codec, const uint8_t *file, int64_t file_len,
     const size_t blk = size_t(block);
     std::vector<const uint8_t *> bufs(shards_out, shards_out + nshards);
     bufs.push_back(file);
-    bool pinned = all_pinned(bufs.data(), int(bufs.size()));
-    HostRegistration reg;
+    const bool pinned = all_pinned(bufs.data(), int(bufs.size()));
     const bool big = file_chunks(c->k(), c->total(), size_t(S), blk, false).n > 1 || size_t(S) >= direct_min_bytes();
-    if (!pinned && big) {
-        std::vector<std::pair<const uint8_t *, size_t>> ranges;
-        for (int i = 0; i < nshards; ++i) ranges.push_back({shards_out[i], size_t(S)});
-        ranges.push_back({file, size_t(file_len)});
-        pinned = whole_pages(ranges) && reg.lock(ranges);
-    }
     bool taken = false;
     if (pinned)
         rc = file_encode_direct(*c, file, size_t(file_len), blk, shards_out, size_t(S), ctx, &taken);
-    else if (big && size_t(S) >= direct_pageable_min_bytes())
-        rc = file_encode_interior(*c, file, size_t(file_len), blk, shards_out, size_t(S), ctx, &taken);
+    else if (big && size_t(S) >= mirror_min_bytes())
+        rc = file_encode_mirrored(*c, file, size_t(file_len), blk, shards_out, size_t(S), ctx, &taken);
     if (rc || taken) return rc;
     return file_encode_staged(*c, file, size_t(file_len), blk, shards_out, size_t(S), ctx, pinned);
 }

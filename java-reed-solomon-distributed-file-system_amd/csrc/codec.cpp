@@ -15,12 +15,22 @@ namespace rsamd {
 namespace {
 std::atomic<bool> g_exiting{false};
 const bool g_exit_hook = [] {
-    std::atexit([] { g_exiting.store(true); });
+    // Under exit_mutex: a thread that makes HIP calls holding it (the reaper,
+    // host.cpp) either finishes them before exit() goes on or sees the flag.
+    std::atexit([] {
+        std::lock_guard<std::mutex> lock(exit_mutex());
+        g_exiting.store(true);
+    });
     return true;
 }();
 }  // namespace
 
 bool process_exiting() { return g_exiting.load(); }
+
+std::mutex &exit_mutex() {
+    static std::mutex *mu = new std::mutex;  // never destroyed: used from atexit
+    return *mu;
+}
 
 hipError_t upload(int dev, void *dst, const void *src, size_t n) {
     // One non-blocking stream per device, created on first use and kept for the

@@ -61,6 +61,9 @@ hipError_t upload(int dev, void *dst, const void *src, size_t n);
 void free_device(int dev, void *p);
 // True once exit() has begun (an atexit hook): device frees are skipped then.
 bool process_exiting();
+// Held by the exit hook while it sets process_exiting(): hold it around HIP
+// calls made from a thread that may outlive exit() and check the flag inside.
+std::mutex &exit_mutex();
 // Frees p later, in a batch with other deferred frees (codec.cpp).
 void free_device_deferred(int dev, void *p);
 void flush_deferred_frees();

@@ -5,11 +5,55 @@
 #include <algorithm>
 #include <cstring>
 
+#include <immintrin.h>
+
 namespace rsamd {
 
 namespace {
 constexpr size_t kPiece = size_t(1) << 20;  // bytes per work item
+
+// Streaming (non-temporal) copy: the destination's lines are written without
+// being read first and without displacing the cache.  Every pool copy is
+// between caller memory and the pinned mirror, which the GPU reads (or has
+// written) across the link, so no CPU cache would keep either side.  The
+// sfence makes the stores globally visible before the piece is reported done.
+__attribute__((target("avx2"))) void copy_stream(uint8_t *dst, const uint8_t *src, size_t n) {
+    size_t head = (32 - reinterpret_cast<uintptr_t>(dst) % 32) % 32;
+    if (head > n) head = n;
+    std::memcpy(dst, src, head);
+    dst += head;
+    src += head;
+    n -= head;
+    for (; n >= 128; n -= 128, dst += 128, src += 128) {
+        const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(src));
+        const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(src + 32));
+        const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(src + 64));
+        const __m256i d = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(src + 96));
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(dst), a);
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(dst + 32), b);
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(dst + 64), c);
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(dst + 96), d);
+    }
+    std::memcpy(dst, src, n);
+    _mm_sfence();
 }
+
+// TUNING builds: RSAMD_COPY_NT=0 copies with memcpy instead (A/B).
+bool use_stream() {
+    static const bool on = [] {
+        const char *e = tuning_env("RSAMD_COPY_NT");
+        return __builtin_cpu_supports("avx2") && !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+void copy_piece(const CopyJob &j) {
+    if (j.n >= 4096 && use_stream())
+        copy_stream(static_cast<uint8_t *>(j.dst), static_cast<const uint8_t *>(j.src), j.n);
+    else
+        std::memcpy(j.dst, j.src, j.n);
+}
+}  // namespace
 
 CopyPool &CopyPool::get() {
     static CopyPool *pool = [] {
@@ -34,7 +78,7 @@ void CopyPool::run() {
         Piece p = queue_.front();
         queue_.pop_front();
         lock.unlock();
-        std::memcpy(p.job.dst, p.job.src, p.job.n);
+        copy_piece(p.job);
         lock.lock();
         if (--*p.pending == 0) done_cv_.notify_all();
     }
@@ -62,7 +106,7 @@ void CopyPool::copy(const std::vector<CopyJob> &jobs) {
             Piece p = queue_.front();
             queue_.pop_front();
             lock.unlock();
-            std::memcpy(p.job.dst, p.job.src, p.job.n);
+            copy_piece(p.job);
             lock.lock();
             if (--*p.pending == 0) done_cv_.notify_all();
             continue;

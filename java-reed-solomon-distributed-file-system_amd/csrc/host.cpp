@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -175,8 +176,9 @@ void free_buffers(ThreadCtx *c) {
     if (c->plan) (void)hipFree(c->plan);
     if (c->file) (void)hipFree(c->file);
     if (c->zc) (void)hipHostFree(c->zc);
-    c->mirror = c->stage = c->plan = c->file = c->zc = c->zc_dev = nullptr;
-    c->mirror_cap = c->stage_cap = c->plan_cap = c->file_cap = c->zc_cap = 0;
+    if (c->mbuf) (void)hipHostFree(c->mbuf);
+    c->mirror = c->stage = c->plan = c->file = c->zc = c->zc_dev = c->mbuf = c->mbuf_dev = nullptr;
+    c->mirror_cap = c->stage_cap = c->plan_cap = c->file_cap = c->zc_cap = c->mbuf_cap = 0;
 }
 
 void release_all(std::map<int, ThreadCtx *> &ctx) {
@@ -197,6 +199,8 @@ void release_all(std::map<int, ThreadCtx *> &ctx) {
             if (c->loaded[b]) (void)hipEventDestroy(c->loaded[b]);
         }
         if (c->flag) (void)hipFree(c->flag);
+        for (hipEvent_t &ev : c->mdone)
+            if (ev) (void)hipEventDestroy(ev);
         for (MaskedSlot &sl : c->masked) {
             if (sl.done) (void)hipEventDestroy(sl.done);
             if (sl.uploaded) (void)hipEventDestroy(sl.uploaded);
@@ -235,17 +239,20 @@ void reaper() {
             m = std::move(o.q.front());
             o.q.pop_front();
         }
-        if (process_exiting()) return;
         // Give the memory back and keep the streams and events for the next
         // new thread (thread_ctx): a JVM or gRPC pool that retires and
-        // creates workers then makes no stream churn at all.
-        int cur = 0;
-        (void)hipGetDevice(&cur);
+        // creates workers then makes no stream churn at all.  Each context is
+        // freed under exit_mutex with the exit flag checked inside it, so no
+        // free runs once exit() has begun (codec.cpp).
         for (auto &kv : m) {
+            std::lock_guard<std::mutex> exit_lock(exit_mutex());
+            if (process_exiting()) return;
+            int cur = 0;
+            (void)hipGetDevice(&cur);
             (void)hipSetDevice(kv.first);
             free_buffers(kv.second);
+            (void)hipSetDevice(cur);
         }
-        (void)hipSetDevice(cur);
         std::lock_guard<std::mutex> lock(o.mu);
         for (auto &kv : m) o.idle[kv.first].push_back(kv.second);
     }
@@ -342,27 +349,12 @@ size_t chunk_bytes(size_t total, int nslots, bool pinned) {
     return std::min(kChunk, c);
 }
 
-namespace {
-struct HostRegistry;
-HostRegistry &host_registry();
-std::mutex &registry_mutex(HostRegistry &reg);
-bool registry_holds_locked(HostRegistry &reg, const void *p);  // below: locked for a call by HostRegistration
-}
-
-// True when every non-null pointer is page-locked host memory known to HIP
-// and stays so for the call: memory that HostRegistration locked for another
-// thread's call reads as pinned too, but is unlocked when that call ends, so
-// it counts as pageable here (the caller then locks it and shares that
-// registration by reference count).  The registry's lock is held across each
-// pointer's attribute query and registry lookup: a registration released
-// between the two would otherwise read as the caller's own pinning, and the
-// call would run on pages nobody keeps locked.
+// True when every non-null pointer is page-locked host memory known to HIP:
+// pinned by the caller (torch pin_memory, hipHostMalloc, a pooled direct
+// buffer).  The library itself never page-locks caller memory.
 bool all_pinned(const uint8_t *const *ptrs, int n) {
-    HostRegistry &reg = host_registry();
-    std::lock_guard<std::mutex> guard(registry_mutex(reg));
     for (int i = 0; i < n; ++i) {
         if (!ptrs[i]) continue;
-        if (registry_holds_locked(reg, ptrs[i])) return false;
         hipPointerAttribute_t attr;
         if (hipPointerGetAttributes(&attr, ptrs[i]) != hipSuccess) {
             (void)hipGetLastError();  // pageable memory: clear the sticky error
@@ -371,154 +363,6 @@ bool all_pinned(const uint8_t *const *ptrs, int n) {
         if (attr.type != hipMemoryTypeHost) return false;
     }
     return true;
-}
-
-// Page-locks pageable caller memory for the duration of one call
-// (hipHostRegister: ~0.2 ms per 64 MiB the first time a range is seen,
-// microseconds after) so the direct kernels code it in place.  Since the
-// end of round 4 only ranges made of whole pages of the caller's own bytes
-// are locked (capi.cpp run_direct_interior, whole_pages): a lock rounded out
-// to pages reached into neighbouring allocations, which the runtime locks
-// for its own pageable copies, and every GPU fault of rounds 3 and 4 surfaced
-// in such a copy after calls that had locked NumPy memory.
-//
-// Registrations go through a process-wide registry of page ranges: calls on
-// the same caller buffers (several threads, or one array passed twice) share
-// one registration by reference count, and a range that partly overlaps a
-// registered one is not registered again -- registering the same pages twice
-// and unregistering one while the other is in use aborts inside the HIP
-// runtime.  All or nothing: if any range cannot be locked the call is staged.
-// The destructor releases after the call's kernels have completed, also on
-// its error paths.  Off unless rs_set_host_register(1) (TUNING builds:
-// RSAMD_HOST_REGISTER=1 at load).
-namespace {
-
-struct HostRegistry {
-    std::mutex mu;
-    std::map<uintptr_t, std::pair<uintptr_t, int>> regs;  // page start -> (page end, references)
-};
-
-std::atomic<int64_t> g_unregister_failures{0};
-
-HostRegistry &host_registry() {
-    static HostRegistry *r = new HostRegistry;  // never destroyed: no HIP calls at exit
-    return *r;
-}
-
-std::mutex &registry_mutex(HostRegistry &reg) { return reg.mu; }
-
-bool registry_holds_locked(HostRegistry &reg, const void *p) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    auto next = reg.regs.upper_bound(a);
-    if (next == reg.regs.begin()) return false;
-    const auto prev = std::prev(next);
-    return a >= prev->first && a < prev->second.first;
-}
-
-// Drops this call's references; the last one unregisters.  Caller holds reg.mu.
-void release_locked(HostRegistry &reg, std::vector<uintptr_t> &held) {
-    for (uintptr_t ps : held) {
-        auto it = reg.regs.find(ps);
-        if (it != reg.regs.end() && --it->second.second == 0) {
-            const hipError_t e = hipHostUnregister(reinterpret_cast<void *>(ps));
-            if (e != hipSuccess) {  // never seen; said once, as it would leave the pages locked
-                (void)hipGetLastError();
-                g_unregister_failures.fetch_add(1);
-                static std::atomic<bool> said{false};
-                if (!said.exchange(true))
-                    std::fprintf(stderr, "librsamd: hipHostUnregister(%p) failed: %s\n", reinterpret_cast<void *>(ps),
-                                 hipGetErrorString(e));
-            }
-            reg.regs.erase(it);
-        }
-    }
-    held.clear();
-}
-
-}  // namespace
-
-namespace {
-// Off by default (include/rs_amd.h rs_set_host_register); a TUNING build's
-// RSAMD_HOST_REGISTER=1 sets the initial value.
-std::atomic<int> &host_register_flag() {
-    static std::atomic<int> *f = new std::atomic<int>([] {
-        const char *e = tuning_env("RSAMD_HOST_REGISTER");
-        return e && e[0] == '1' ? 1 : 0;
-    }());
-    return *f;
-}
-}  // namespace
-
-int set_host_register(int enable) {
-    if (enable < 0) return host_register_flag().load();
-    return host_register_flag().exchange(enable ? 1 : 0);
-}
-
-bool HostRegistration::lock(const std::vector<std::pair<const uint8_t *, size_t>> &ranges) {
-    if (!host_register_flag().load()) return false;
-    // The call's page ranges, sorted and merged: shards that are slices of
-    // one allocation (sharing boundary pages) become one registration.
-    constexpr uintptr_t kPage = 4096;
-    std::vector<std::pair<uintptr_t, uintptr_t>> pages;
-    for (const auto &r : ranges) {
-        if (!r.first || r.second == 0) continue;
-        const uintptr_t a = reinterpret_cast<uintptr_t>(r.first);
-        pages.push_back({a & ~(kPage - 1), (a + r.second + kPage - 1) & ~(kPage - 1)});
-    }
-    std::sort(pages.begin(), pages.end());
-    std::vector<std::pair<uintptr_t, uintptr_t>> merged;
-    for (const auto &pr : pages) {
-        if (!merged.empty() && pr.first <= merged.back().second)
-            merged.back().second = std::max(merged.back().second, pr.second);
-        else
-            merged.push_back(pr);
-    }
-    HostRegistry &reg = host_registry();
-    std::lock_guard<std::mutex> guard(reg.mu);
-    for (const auto &pr : merged) {
-        const uintptr_t ps = pr.first, pe = pr.second;
-        auto next = reg.regs.upper_bound(ps);  // first registration starting after ps
-        if (next != reg.regs.begin()) {
-            auto prev = std::prev(next);
-            if (prev->second.first >= pe) {  // already covered: share it
-                ++prev->second.second;
-                held_.push_back(prev->first);
-                continue;
-            }
-            if (prev->second.first > ps) {  // partial overlap
-                release_locked(reg, held_);
-                return false;
-            }
-        }
-        if ((next != reg.regs.end() && next->first < pe) ||
-            hipHostRegister(reinterpret_cast<void *>(ps), pe - ps, hipHostRegisterMapped) != hipSuccess) {
-            (void)hipGetLastError();
-            release_locked(reg, held_);
-            return false;
-        }
-        reg.regs.emplace(ps, std::make_pair(pe, 1));
-        held_.push_back(ps);
-    }
-    return true;
-}
-
-int registry_state(int64_t *out, int n) {
-    int64_t v[3] = {0, 0, g_unregister_failures.load()};
-    {
-        HostRegistry &reg = host_registry();
-        std::lock_guard<std::mutex> guard(reg.mu);
-        v[0] = int64_t(reg.regs.size());
-        for (const auto &kv : reg.regs) v[1] += int64_t((kv.second.first - kv.first) / 4096);
-    }
-    for (int i = 0; out && i < n && i < 3; ++i) out[i] = v[i];
-    return 3;
-}
-
-HostRegistration::~HostRegistration() {
-    if (held_.empty()) return;
-    HostRegistry &reg = host_registry();
-    std::lock_guard<std::mutex> guard(reg.mu);
-    release_locked(reg, held_);
 }
 
 namespace {
@@ -686,6 +530,232 @@ int run_chunks_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinn
 }
 
 }  // namespace
+
+// ---------------------------------------------------------------------------
+// The mirrored pipeline (host.hpp).  Slot b of ctx->mbuf holds one chunk laid
+// out as the caller's code expects; a chunk's life is
+//   copy-in (pool, caller -> slot) -> kernels over the slot's device address
+//   (ctx->stream, event mdone[b]) -> copy-out (pool, slot -> caller).
+// The copy batch issued before chunk j's launch holds chunk j's inputs and
+// the outputs of every earlier chunk whose kernels have completed; only the
+// chunk that last used slot b must have been drained before the slot is
+// refilled, so the CPU runs up to kMirrorBufs - 1 chunks ahead of the GPU.
+// ---------------------------------------------------------------------------
+namespace {
+// Pinned bytes per slot (TUNING builds: RSAMD_MIRROR_BYTES).
+size_t mirror_slot_bytes() {
+    static const size_t v = rsamd::tuning_size("RSAMD_MIRROR_BYTES", size_t(24) << 20);
+    return v;
+}
+
+int mirror_buffer(ThreadCtx *ctx, size_t bytes) {
+    if (ctx->mbuf_cap < bytes) {
+        if (ctx->mbuf) RS_HIP(hipHostFree(ctx->mbuf));
+        ctx->mbuf = ctx->mbuf_dev = nullptr;
+        ctx->mbuf_cap = 0;
+        RS_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->mbuf), bytes, hipHostMallocDefault));
+        ctx->mbuf_cap = bytes;
+        RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->mbuf_dev), ctx->mbuf, 0));
+    }
+    for (hipEvent_t &ev : ctx->mdone)
+        if (!ev) RS_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    bounds::allow(ctx->mbuf_dev, ctx->mbuf_cap);
+    return RS_OK;
+}
+
+// TUNING builds: RSAMD_TRACE=<file> appends one JSON line per mirrored call
+// with every chunk's copy batch (host ns from the call's start), launch, and
+// kernel start / end (GPU events, on the same clock through a reference event
+// synchronised at the start), and which chunks each batch drained.
+struct MirrorTrace {
+    const char *path = nullptr;
+    std::chrono::steady_clock::time_point t0;
+    hipEvent_t ref = nullptr;
+    std::vector<hipEvent_t> ks, ke;
+    std::vector<int64_t> cb, ce, launched;
+    std::vector<std::vector<size_t>> drained;
+    int64_t now() const {
+        return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    }
+    void begin(hipStream_t s, size_t n) {
+        path = tuning_env("RSAMD_TRACE");
+        if (!path) return;
+        (void)hipEventCreate(&ref);
+        ks.assign(n, nullptr);
+        ke.assign(n, nullptr);
+        for (size_t j = 0; j < n; ++j) {
+            (void)hipEventCreate(&ks[j]);
+            (void)hipEventCreate(&ke[j]);
+        }
+        cb.assign(n, 0);
+        ce.assign(n, 0);
+        launched.assign(n, 0);
+        drained.assign(n, {});
+        (void)hipStreamSynchronize(s);
+        (void)hipEventRecord(ref, s);
+        (void)hipEventSynchronize(ref);
+        t0 = std::chrono::steady_clock::now();
+    }
+    void end(hipStream_t s, size_t bytes) {
+        if (!path) return;
+        (void)hipStreamSynchronize(s);
+        const int64_t total = now();
+        FILE *f = std::fopen(path, "a");
+        if (f) {
+            std::fprintf(f, "{\"bytes\": %zu, \"total_ns\": %lld, \"chunks\": [", bytes, (long long)total);
+            for (size_t j = 0; j < cb.size(); ++j) {
+                float a = 0, b = 0;
+                (void)hipEventElapsedTime(&a, ref, ks[j]);
+                (void)hipEventElapsedTime(&b, ref, ke[j]);
+                std::fprintf(f, "%s{\"j\": %zu, \"copy\": [%lld, %lld], \"launch\": %lld, \"kernel\": [%lld, %lld], \"drained\": [",
+                             j ? ", " : "", j, (long long)cb[j], (long long)ce[j], (long long)launched[j],
+                             (long long)(a * 1e6), (long long)(b * 1e6));
+                for (size_t q = 0; q < drained[j].size(); ++q) std::fprintf(f, "%s%zu", q ? ", " : "", drained[j][q]);
+                std::fprintf(f, "]}");
+            }
+            std::fprintf(f, "]}\n");
+            std::fclose(f);
+        }
+        for (hipEvent_t e : ks) (void)hipEventDestroy(e);
+        for (hipEvent_t e : ke) (void)hipEventDestroy(e);
+        (void)hipEventDestroy(ref);
+    }
+};
+
+int run_mirrored_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, const ChunkIo &io,
+                      const ChunkCode &code) {
+    const int nbuf = int(std::min<size_t>(kMirrorBufs, std::max<size_t>(1, n_chunks)));
+    int rc = mirror_buffer(ctx, buf_bytes * size_t(nbuf));
+    if (rc) return rc;
+    MirrorTrace tr;
+    tr.begin(ctx->stream, n_chunks);
+    // Chunks alternate between two streams, so one chunk's kernel starts while
+    // the previous one drains: a direct kernel over a few MiB spends ~60 us
+    // filling and emptying the link (4+2, 24 MiB slots: 338 us per 14.8 MiB
+    // chunk on one stream, 73 us of it fixed; tools/host_legs.py --trace,
+    // profiles/r5/).  stream2 first waits for what the caller queued on
+    // stream (the verify flag's reset).  TUNING builds: RSAMD_MIRROR_STREAMS=1.
+    const int nstreams = int(std::min<size_t>(2, std::max<size_t>(1, rsamd::tuning_size("RSAMD_MIRROR_STREAMS", 2))));
+    hipStream_t ss[2] = {ctx->stream, ctx->stream2};
+    if (nstreams > 1) {
+        RS_HIP(hipEventRecord(ctx->ready, ctx->stream));
+        RS_HIP(hipStreamWaitEvent(ctx->stream2, ctx->ready, 0));
+    }
+    rsamd::CopyPool &pool = rsamd::CopyPool::get();
+    struct Pending {
+        size_t j;
+        std::vector<Xfer> out;
+    };
+    std::deque<Pending> pending;  // launched, slot not yet released: outputs not copied out (chunk order)
+    std::vector<rsamd::CopyJob> jobs;
+    std::vector<Xfer> in, out;
+    size_t batch = 0;  // the chunk whose copy batch is being built (trace)
+    auto drain_front = [&]() {
+        const Pending &p = pending.front();
+        if (tr.path) tr.drained[batch].push_back(p.j);
+        const uint8_t *slot = ctx->mbuf + (p.j % size_t(nbuf)) * buf_bytes;
+        for (const Xfer &x : p.out) jobs.push_back({x.host, slot + x.off, x.n});
+        pending.pop_front();
+    };
+    auto done = [&](size_t j) {  // chunk j's kernels have completed
+        const hipError_t e = hipEventQuery(ctx->mdone[j % size_t(nbuf)]);
+        if (e == hipErrorNotReady) (void)hipGetLastError();
+        return e == hipSuccess;
+    };
+    for (size_t j = 0; j < n_chunks; ++j) {
+        const size_t b = j % size_t(nbuf);
+        batch = j;
+        jobs.clear();
+        // the slot's previous chunk first (waited for), then whatever else is done
+        while (!pending.empty() && pending.front().j + size_t(nbuf) <= j) {
+            RS_HIP(hipEventSynchronize(ctx->mdone[pending.front().j % size_t(nbuf)]));
+            drain_front();
+        }
+        while (!pending.empty() && done(pending.front().j)) drain_front();
+        in.clear();
+        out.clear();
+        io(j, &in, &out);
+        uint8_t *slot = ctx->mbuf + b * buf_bytes;
+        for (const Xfer &x : in) jobs.push_back({slot + x.off, x.host, x.n});
+        if (tr.path) tr.cb[j] = tr.now();
+        pool.copy(jobs);
+        hipStream_t st = ss[j % size_t(nstreams)];
+        if (tr.path) {
+            tr.ce[j] = tr.now();
+            (void)hipEventRecord(tr.ks[j], st);
+        }
+        rc = code(j, ctx->mbuf_dev + b * buf_bytes, st);
+        if (rc) return rc;
+        if (tr.path) {
+            (void)hipEventRecord(tr.ke[j], st);
+            tr.launched[j] = tr.now();
+        }
+        RS_HIP(hipEventRecord(ctx->mdone[b], st));
+        // (also with no outputs -- verify: the slot's inputs may not be
+        // refilled before the chunk's kernels have read them)
+        pending.push_back({j, out});
+    }
+    batch = n_chunks - 1;
+    while (!pending.empty()) {
+        jobs.clear();
+        RS_HIP(hipEventSynchronize(ctx->mdone[pending.front().j % size_t(nbuf)]));
+        drain_front();
+        while (!pending.empty() && done(pending.front().j)) drain_front();
+        pool.copy(jobs);
+    }
+    if (nstreams > 1) {  // stream carries on behind both (the caller reads the verify flag next)
+        RS_HIP(hipEventRecord(ctx->ready, ctx->stream2));
+        RS_HIP(hipStreamWaitEvent(ctx->stream, ctx->ready, 0));
+    }
+    RS_HIP(hipStreamSynchronize(ctx->stream));
+    tr.end(ctx->stream, buf_bytes);
+    return RS_OK;
+}
+}  // namespace
+
+size_t mirror_chunk_bytes(size_t total, int nslots, size_t granule) {
+    granule = std::max<size_t>(1, granule);
+    // 8 chunks per call when they fit the slot, never under 256 KiB per slot
+    size_t c = std::max<size_t>(size_t(256) << 10, total / 8);
+    c = std::min(c, mirror_slot_bytes() / size_t(std::max(1, nslots)));
+    c = std::max(granule, c / granule * granule);
+    return c;
+}
+
+std::vector<size_t> ramp_bounds(size_t total, size_t chunk, size_t granule) {
+    granule = std::max<size_t>(1, granule);
+    chunk = std::max(granule, chunk / granule * granule);
+    auto g = [&](size_t x) { return std::max(granule, x / granule * granule); };
+    std::vector<size_t> sizes;
+    const size_t q = g(chunk / 4), h = g(chunk / 2);
+    if (total <= 2 * (q + h)) {  // short call: up to 4 equal chunks
+        const size_t n = std::max<size_t>(1, std::min<size_t>(4, total / granule));
+        const size_t each = g((total + n - 1) / n);
+        for (size_t done = 0; done < total; done += each) sizes.push_back(std::min(each, total - done));
+    } else {  // a quarter and a half chunk either side of whole chunks
+        // (granule-sized pieces up to the last one, which takes the remainder)
+        const size_t mid = total - 2 * (q + h), nbody = (mid + chunk - 1) / chunk;
+        const size_t each = g(mid / nbody);
+        sizes = {q, h};
+        for (size_t i = 0; i < nbody && each * (i + 1) <= mid; ++i) sizes.push_back(each);
+        sizes.push_back(h);
+        size_t sum = 0;
+        for (size_t x : sizes) sum += x;
+        sizes.push_back(total - sum);
+    }
+    std::vector<size_t> b{0};
+    for (size_t x : sizes) b.push_back(b.back() + x);
+    return b;
+}
+
+int run_mirrored(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, const ChunkIo &io, const ChunkCode &code) {
+    const int rc = run_mirrored_impl(ctx, n_chunks, buf_bytes, io, code);
+    if (rc) {  // nothing of the call left in flight
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipStreamSynchronize(ctx->stream2);
+    }
+    return rc;
+}
 
 }  // namespace host
 

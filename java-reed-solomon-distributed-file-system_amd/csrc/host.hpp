@@ -47,6 +47,10 @@ struct MaskedSlot {
 #define RSAMD_STAGE_BUFS 3  // A/B builds: make KDEFS=-DRSAMD_STAGE_BUFS=n
 #endif
 constexpr int kStageBufs = RSAMD_STAGE_BUFS;  // staging buffers of the host-buffer pipeline
+#ifndef RSAMD_MIRROR_BUFS
+#define RSAMD_MIRROR_BUFS 4  // A/B builds: make KDEFS=-DRSAMD_MIRROR_BUFS=n
+#endif
+constexpr int kMirrorBufs = RSAMD_MIRROR_BUFS;  // slots of the mirrored pipeline (run_mirrored)
 
 struct ThreadCtx {
     hipStream_t stream = nullptr;   // host pipeline: kernels, in chunk order
@@ -68,6 +72,10 @@ struct ThreadCtx {
     uint8_t *zc = nullptr;      // small calls: coherent, device-mapped host buffer the kernels use directly
     uint8_t *zc_dev = nullptr;  // its device address
     size_t zc_cap = 0;
+    uint8_t *mbuf = nullptr;      // run_mirrored: kMirrorBufs device-mapped pinned slots
+    uint8_t *mbuf_dev = nullptr;  // their device address
+    size_t mbuf_cap = 0;
+    hipEvent_t mdone[kMirrorBufs] = {};  // slot b's kernels done (its outputs may be drained)
     // rs_decode_batch_masked_dev: two staging slots used in turn, so a call's
     // host-side preparation overlaps the previous call's kernels.
     MaskedSlot masked[2];
@@ -90,31 +98,10 @@ int zero_copy_buffer(ThreadCtx *ctx, size_t buf_bytes);
 // Bytes per slot per chunk for a call of `total` bytes per slot and `nslots`
 // slots per buffer.
 size_t chunk_bytes(size_t total, int nslots, bool pinned);
-// True when every non-null pointer is page-locked host memory known to HIP.
+// True when every non-null pointer is page-locked host memory known to HIP
+// (the caller's own pinning: the library never page-locks caller memory).
 bool all_pinned(const uint8_t *const *ptrs, int n);
 inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
-
-// rs_host_registry_state: registrations held now, their pages, and
-// hipHostUnregister failures since load.
-int registry_state(int64_t *out, int n);
-// rs_set_host_register: page-locking of pageable caller memory on or off
-// (off by default); returns the previous setting, or the current one for < 0.
-int set_host_register(int enable);
-
-// Page-locks pageable caller ranges for the duration of one pipelined call
-// (host.cpp: a process-wide, reference-counted registry of page ranges).
-class HostRegistration {
-public:
-    HostRegistration() = default;
-    HostRegistration(const HostRegistration &) = delete;
-    HostRegistration &operator=(const HostRegistration &) = delete;
-    ~HostRegistration();
-    // All or nothing: false (and nothing held) if any range cannot be locked.
-    bool lock(const std::vector<std::pair<const uint8_t *, size_t>> &ranges);
-
-private:
-    std::vector<uintptr_t> held_;  // registry keys this call references
-};
 
 // One host <-> device transfer of a chunk: host bytes [host, host + n) and
 // bytes [off, off + n) of the chunk's staging buffer.
@@ -132,6 +119,28 @@ using ChunkCode = std::function<int(size_t j, uint8_t *buf, hipStream_t s)>;
 // or out of caller memory is still in flight when the caller gets control.
 int run_chunks(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinned, const ChunkIo &io,
                const ChunkCode &code);
+
+// ---- the mirrored pipeline (pageable callers) ----------------------------------
+// Pageable caller memory (JVM heap arrays through JNI) cannot be read by the
+// GPU, and the library does not page-lock it.  Its bytes are
+// copied by the copy pool into device-mapped pinned slots that the direct
+// kernels code in place across the link, and the outputs copied back out,
+// chunk by chunk: chunk j's inputs are copied while the GPU codes chunk j-1 and
+// chunk j-2's outputs are drained, so the CPU copies hide behind the link.
+//
+// Per-slot chunk bytes for a call of `total` bytes per slot over `nslots`
+// slots (multiples of `granule`, at least one granule).
+size_t mirror_chunk_bytes(size_t total, int nslots, size_t granule);
+// Chunk boundaries over [0, total) in units of `granule`: chunks of `chunk`
+// bytes, the first and last two shorter (a quarter, a half), so the pipeline
+// fills and drains quickly.  bounds.front() == 0, bounds.back() == total.
+std::vector<size_t> ramp_bounds(size_t total, size_t chunk, size_t granule);
+// Runs bounds.size() - 1 chunks through the slots: io(j) names chunk j's host
+// inputs and outputs (offsets into a slot of buf_bytes), code(j, dev, s)
+// enqueues its kernels on s over the slot's device address.  Returns once
+// every output is in caller memory; on an error, once nothing of the call is
+// in flight.
+int run_mirrored(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, const ChunkIo &io, const ChunkCode &code);
 
 }  // namespace host
 }  // namespace rsamd

@@ -1042,6 +1042,7 @@ struct MaskedByteArgs {
     int mask_bits;
     int32_t *bad;
     uint64_t pat_bytes, row_bytes;  // MaskedPlan::pattern_bytes (0: per stripe); the view's full shard length
+    uint64_t count_col;             // per-stripe patterns: the column whose thread counts an undecodable stripe
 };
 
 __global__ void __launch_bounds__(kThreads) gf_masked_byte_kernel(MaskedByteArgs a) {
@@ -1050,7 +1051,7 @@ __global__ void __launch_bounds__(kThreads) gf_masked_byte_kernel(MaskedByteArgs
         const uint64_t stripe = idx / a.ncols;
         const uint64_t col = a.col0 + (idx - stripe * a.ncols);
         uint64_t pat = stripe;
-        bool first = col == 0;
+        bool first = col == a.count_col;
         if (a.pat_bytes) {
             const uint64_t x = stripe * a.row_bytes + col;
             pat = x / a.pat_bytes;
@@ -1666,11 +1667,16 @@ Lanes8 lanes8(size_t len, bool u16) {
     return Lanes8{uint32_t(len / 8), 0, len / 8 * 8};
 }
 
+// `counts`: this launch covers the first column of its call's range, and
+// counts each undecodable stripe there (per-stripe patterns).  A launch that
+// codes a tail or a head peel's remainder does not: every stripe is counted
+// once per call (include/rs_amd.h rs_decode_batch_masked_bits_dev).
 hipError_t launch_masked_bytes(const Geometry &g, const MaskedPlan &p, const MaskedRecordLayout &l, size_t col0,
-                               size_t ncols, hipStream_t s) {
+                               size_t ncols, bool counts, hipStream_t s) {
     MaskedByteArgs a{g.base, p.records, p.rec_stride, p.plan_ids, g.stripe_stride, g.shard_stride, col0, ncols,
                      uint64_t(g.n_stripes) * ncols, uint32_t(l.in_idx), uint32_t(l.out_idx), uint32_t(l.tabs),
-                     p.nin, p.mslots, p.mask_table, p.mask_bits, p.bad, p.pattern_bytes, g.col0 + g.len};
+                     p.nin, p.mslots, p.mask_table, p.mask_bits, p.bad, p.pattern_bytes, g.col0 + g.len,
+                     counts ? uint64_t(col0) : UINT64_MAX};
     if (a.total == 0) return hipSuccess;
     const unsigned grid = unsigned(std::min<uint64_t>((a.total + kThreads - 1) / kThreads, 65536));
     hipLaunchKernelGGL(gf_masked_byte_kernel, dim3(grid), dim3(kThreads), 0, s, a);
@@ -1717,7 +1723,7 @@ hipError_t launch_masked8(const Geometry &g, const MaskedPlan &p, const MaskedRe
             if (e != hipSuccess) return e;
         }
     }
-    if (n.covered < g.len) return launch_masked_bytes(g, p, l, g.col0 + n.covered, g.len - n.covered, s);
+    if (n.covered < g.len) return launch_masked_bytes(g, p, l, g.col0 + n.covered, g.len - n.covered, false, s);
     return hipSuccess;
 }
 
@@ -1791,12 +1797,14 @@ hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t 
     // Head peel as launch_gf_tables (per-stripe patterns only: granule
     // patterns are tied to the columns' 1 KiB chunks).
     if (const size_t peel = pb == 0 ? head_peel(g) : 0) {
-        hipError_t e = launch_masked_bytes(g, p, l, g.col0, peel, s);
+        hipError_t e = launch_masked_bytes(g, p, l, g.col0, peel, true, s);
         if (e != hipSuccess) return e;
         Geometry rest = g;
         rest.col0 += peel;
         rest.len -= peel;
-        return launch_gf_masked(rest, p, s);
+        MaskedPlan rp = p;
+        rp.bad = nullptr;  // counted by the peel's launch
+        return launch_gf_masked(rest, rp, s);
     }
     // (the line-owner kernel reads a stripe's outputs off its bitmask: a
     // pattern table, and every pattern's absent shards in one launch group)
@@ -1817,7 +1825,8 @@ hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t 
     if (aligned8 && pb == 0 && (!aligned || small_with_tail8(g.len)) && g.len / 8 <= UINT32_MAX - kWave &&
         masked8_enabled())
         return launch_masked8(g, p, l, s);
-    if (!aligned || !pat_vec || g.len / 16 > UINT32_MAX - kWave) return launch_masked_bytes(g, p, l, g.col0, g.len, s);
+    if (!aligned || !pat_vec || g.len / 16 > UINT32_MAX - kWave)
+        return launch_masked_bytes(g, p, l, g.col0, g.len, true, s);
     const uint32_t nvec = uint32_t(g.len / 16);
     if (nvec > 0) {
         const uint32_t chunks = (nvec + kWave - 1) / kWave;
@@ -1837,7 +1846,7 @@ hipError_t launch_gf_masked(const Geometry &g, const MaskedPlan &p, hipStream_t 
         }
     }
     const size_t tail = g.len % 16;
-    if (tail) return launch_masked_bytes(g, p, l, g.col0 + size_t(nvec) * 16, tail, s);
+    if (tail) return launch_masked_bytes(g, p, l, g.col0 + size_t(nvec) * 16, tail, false, s);
     return hipSuccess;
 }
 

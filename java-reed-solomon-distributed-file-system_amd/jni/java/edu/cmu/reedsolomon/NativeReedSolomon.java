@@ -86,16 +86,6 @@ public final class NativeReedSolomon implements AutoCloseable {
         nativeThreadRelease();
     }
 
-    /**
-     * Page-locking the Java arrays of large calls for each call (the GPU would
-     * code them in place across the link).  Off, and refused by product
-     * builds (UnsupportedOperationException): see rs_set_host_register in
-     * rs_amd.h.  setHostRegister(false) always succeeds.
-     */
-    public static boolean setHostRegister(boolean on) {
-        return nativeSetHostRegister(on);
-    }
-
     @Override
     public synchronized void close() {
         if (handle != 0) {
@@ -106,7 +96,6 @@ public final class NativeReedSolomon implements AutoCloseable {
 
     private static native long nativeCreate(int k, int m);
     private static native void nativeThreadRelease();
-    private static native boolean nativeSetHostRegister(boolean on);
     private static native void nativeDestroy(long h);
     private static native void nativeEncodeParity(long h, byte[][] shards, int offset, int byteCount);
     private static native void nativeDecodeMissing(long h, byte[][] shards, boolean[] present, int offset, int byteCount);

@@ -115,20 +115,6 @@ JNIEXPORT void JNICALL Java_edu_cmu_reedsolomon_NativeReedSolomon_nativeThreadRe
     rs_thread_release();
 }
 
-/* NativeReedSolomon.setHostRegister: page-locking the (pageable) Java arrays
- * of large calls for the call (include/rs_amd.h rs_set_host_register).
- * Product builds refuse to turn it on: UnsupportedOperationException. */
-JNIEXPORT jboolean JNICALL Java_edu_cmu_reedsolomon_NativeReedSolomon_nativeSetHostRegister(JNIEnv *env, jclass cls,
-                                                                                           jboolean on) {
-    const int rc = rs_set_host_register(on ? 1 : 0);
-    if (rc < 0) {
-        jclass ex = (*env)->FindClass(env, "java/lang/UnsupportedOperationException");
-        if (ex) (*env)->ThrowNew(env, ex, rs_last_error_message());
-        return JNI_FALSE;
-    }
-    return rc ? JNI_TRUE : JNI_FALSE;
-}
-
 /* ---- GpuCodingLoop: drop-in CodingLoop plugin (CodingLoop.java:79-117) ---- */
 
 JNIEXPORT void JNICALL Java_edu_cmu_reedsolomon_GpuCodingLoop_nativeCodeSomeShards(

@@ -488,17 +488,26 @@ void rsj_recover_groups_shard_major(rsj_env *e, const rsj_backend *b, const rs_c
         e->throw_new(e, IAE, msg);
         return;
     }
-    /* Pinned for the call (or the JVM's own copy: the flags are only read). */
-    int is_copy = 0;
-    uint8_t *pinned = n ? e->critical_get(e, present, &is_copy) : NULL;
-    if (n && !pinned) {
-        if (!e->exception_pending(e)) e->throw_new(e, "java/lang/OutOfMemoryError", "GetPrimitiveArrayCritical failed");
+    /* Copied out (GetByteArrayRegion), not pinned: the call can block (plan
+     * uploads, waits on the previous call's event), and a critical region
+     * held that long stalls the GC.  The library reads the flags on the host
+     * only. */
+    uint8_t *flags = n ? (uint8_t *)malloc((size_t)n) : NULL;
+    if (n && !flags) {
+        e->throw_new(e, "java/lang/OutOfMemoryError", "present flags");
         return;
+    }
+    if (n) {
+        e->byte_region_get(e, present, 0, n, flags);
+        if (e->exception_pending(e)) {
+            free(flags);
+            return;
+        }
     }
     static const uint8_t none = 0;
     const int rc = b->decode_groups_shard_major(c, (uint8_t *)(uintptr_t)dev_base, (size_t)server_stride,
-                                                (size_t)chunk_len, (size_t)n_groups, pinned ? pinned : &none,
+                                                (size_t)chunk_len, (size_t)n_groups, flags ? flags : &none,
                                                 (void *)(uintptr_t)stream);
-    if (pinned) e->critical_release(e, present, pinned, RSJ_ABORT);
+    free(flags);
     if (rc) throw_rc(e, b, rc);
 }

@@ -13,7 +13,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_ROOT, "lib", "librsamd.so")
 CSRC = os.path.join(PKG_ROOT, "csrc")
 
-ABI_VERSION = 4  # include/rs_amd.h RS_AMD_ABI_VERSION, which SIGNATURES follows
+ABI_VERSION = 5  # include/rs_amd.h RS_AMD_ABI_VERSION, which SIGNATURES follows
 u8p = C.POINTER(C.c_uint8)
 u8pp = C.POINTER(u8p)
 
@@ -31,8 +31,6 @@ SIGNATURES = {
     "rs_abi_version": (C.c_int, []),
     "rs_last_error_message": (C.c_char_p, []),
     "rs_thread_release": (None, []),
-    "rs_host_registry_state": (C.c_int, [C.POINTER(C.c_int64), C.c_int]),
-    "rs_set_host_register": (C.c_int, [C.c_int]),
     "rs_device_count": (C.c_int, []),
     "rs_encode_parity": (C.c_int, [C.c_void_p, u8pp, C.c_int, C.POINTER(C.c_int64), C.c_int32, C.c_int32]),
     "rs_decode_missing": (C.c_int, [C.c_void_p, u8pp, C.c_int, C.POINTER(C.c_int64), u8p, C.c_int32, C.c_int32]),

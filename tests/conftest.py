@@ -61,12 +61,6 @@ def bounds_check(request):
     import ctypes as C
     from rsamd import _lib
     lib = _lib.load()
-    # Every build: no page registration of the direct path outlives its call
-    # (a stale one would leave the runtime tracking pages the caller may free),
-    # and no hipHostUnregister failed.
-    st = (C.c_int64 * 3)()
-    lib.rs_host_registry_state(st, 3)
-    assert st[0] == 0 and st[2] == 0, f"host registry after the test: {st[0]} held ({st[1]} pages), {st[2]} unregister failures"
     if not hasattr(lib, "rs_bounds_report"):
         return
     import torch
@@ -81,18 +75,10 @@ def bounds_check(request):
 
 @pytest.fixture(scope="session")
 def gpu(native):
-    """Skip-free GPU gate: a gpu-marked test on a box without a device is an error.
-    RSAMD_TEST_HOST_REGISTER=1 runs the session with page-locking of pageable
-    caller memory on (rs_set_host_register; refused by product builds, so
-    with the TUNING build): the investigation's direct path on pageable
-    arrays, in a run of its own (tools/gpu_run.sh hostreg)."""
+    """Skip-free GPU gate: a gpu-marked test on a box without a device is an error."""
     n = native.rs_device_count()
     if n < 1:
         pytest.fail("no HIP device visible to librsamd.so (gpu tests need an MI355X)")
-    if os.environ.get("RSAMD_TEST_HOST_REGISTER") == "1":
-        assert native.rs_set_host_register(1) >= 0, "page-locking needs the TUNING build (RSAMD_TEST_LIB)"
-    else:
-        native.rs_set_host_register(0)
     import torch
     assert torch.cuda.is_available(), "torch sees no GPU"
     return torch.device("cuda:0")

@@ -192,8 +192,8 @@ def test_link_bound():
 
 
 def test_decode_summary_keys():
-    """roofline's short decode / configs keys (what a record that keeps only the
-    parsed line shows): taken from the extra legs at N = 1, the all-ranks
+    """roofline's short decode / config keys, all scalars (what a record that
+    keeps only the parsed line's scalar keys shows): taken from the extra legs at N = 1, the all-ranks
     {0,1} leg at N > 1, None where a leg did not run."""
     sys.path.insert(0, ROOT)
     import bench
@@ -204,8 +204,10 @@ def test_decode_summary_keys():
     assert (s["decode_0_frac"], s["decode_0_1_frac"], s["decode_0_5_frac"], s["decode_patterns_min"]) == \
         (0.87, 0.86, 0.85, 0.84)
     assert s["decode_2_erasures_target_0_50_met"] is True
-    assert s["configs"]["c3_enc"] == 0.77 and s["configs"]["c4_enc_granule"] == 0.87
-    assert s["configs"]["c3_enc_pad"] is None
+    assert s["c3_enc_frac"] == 0.77 and s["c4_enc_granule_frac"] == 0.87
+    assert s["c3_enc_pad_frac"] is None
+    # every key is a scalar: a record that drops nested objects keeps them all
+    assert all(not isinstance(v, (dict, list)) for v in s.values())
     n8 = bench.decode_summary({"decode_0_1_all_ranks_hbm_frac_per_gpu": 0.45})
     assert n8["decode_0_1_frac"] == 0.45 and n8["decode_0_frac"] is None
     assert n8["decode_2_erasures_target_0_50_met"] is False

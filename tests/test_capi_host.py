@@ -323,23 +323,12 @@ def test_shard_major_argument_errors(native):
     assert rc == -10 and "overflows" in _lib.last_error()
 
 
-def test_host_registry_state_idle(native):
-    """rs_host_registry_state: no registration held while no host call runs
-    (the same check follows every GPU test, tests/conftest.py)."""
+def test_no_page_locking_entry_points(native):
+    """ABI 5: the library never page-locks caller memory, and
+    the switch and registry query of rounds 3-4 are gone from the exports."""
     import ctypes as C
-    out = (C.c_int64 * 3)(-1, -1, -1)
-    assert native.rs_host_registry_state(out, 3) == 3
-    assert list(out) == [0, 0, 0]
-    one = (C.c_int64 * 1)(-1)
-    assert native.rs_host_registry_state(one, 1) == 3 and one[0] == 0
-    assert native.rs_host_registry_state(None, 0) == 3
-
-
-def test_host_register_refused_by_product(native):
-    """rs_set_host_register: the product library never page-locks pageable
-    caller memory: turning it on is refused with
-    RS_E_INVALID, turning it off or querying returns 0 (off)."""
-    assert native.rs_set_host_register(1) < 0
-    assert "product builds" in native.rs_last_error_message().decode()
-    assert native.rs_set_host_register(-1) == 0
-    assert native.rs_set_host_register(0) == 0
+    from rsamd import _lib
+    raw = C.CDLL(_lib.LIB_PATH)
+    for name in ("rs_set_host_register", "rs_host_registry_state"):
+        assert not hasattr(raw, name), name
+    assert native.rs_abi_version() == 5

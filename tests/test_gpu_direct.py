@@ -10,6 +10,7 @@ staged copies); here each geometry is chosen so that the path is known.
 """
 import numpy as np
 import pytest
+from bytes_report import assert_same
 
 pytestmark = pytest.mark.gpu
 
@@ -50,7 +51,7 @@ def test_direct_encode_verify_decode(gpu, oracle_lib, page, gap, offset):
     oracle_lib.Codec(4, 2).encode_parity(ref, offset, count)
     rs.encodeParity(sh, offset, count)
     for a, b in zip(sh, ref):  # parity in range, every byte outside it untouched
-        assert np.array_equal(a, b)
+        assert_same([a], [b], '')
     assert rs.isParityCorrect(sh, offset, count)
     for pos in (offset, offset + 1, offset + count // 2, offset + count - 1):  # head, body, tail bytes
         sh[5][pos] ^= 0x10
@@ -62,7 +63,7 @@ def test_direct_encode_verify_decode(gpu, oracle_lib, page, gap, offset):
             sh[j][offset:offset + count] = 0
         rs.decodeMissing(sh, [i not in miss for i in range(6)], offset, count)
         for a, b in zip(sh, ref):
-            assert np.array_equal(a, b), miss
+            assert_same([a], [b], miss)
 
 
 def test_direct_pageable_registered(gpu, oracle_lib):
@@ -77,12 +78,12 @@ def test_direct_pageable_registered(gpu, oracle_lib):
     ref = [a.copy() for a in sh]
     oracle_lib.Codec(10, 4).encode_parity(ref, 0, n)
     rs.encodeParity(sh, 0, n)
-    assert all(np.array_equal(a, b) for a, b in zip(sh, ref))
+    assert_same(sh, ref, '')
     miss = (0, 3, 7, 12)
     for j in miss:
         sh[j][:] = 0
     rs.decodeMissing(sh, [i not in miss for i in range(14)], 0, n)
-    assert all(np.array_equal(a, b) for a, b in zip(sh, ref))
+    assert_same(sh, ref, '')
     assert rs.isParityCorrect(sh, 0, n)
 
 
@@ -101,7 +102,7 @@ def test_direct_pageable_offset_range(gpu, oracle_lib):
     assert rs.isParityCorrect(sh, off, cnt)
     sh[2][off:off + cnt] = 0
     rs.decodeMissing(sh, [True, True, False, True, True, True], off, cnt)
-    assert all(np.array_equal(a, b) for a, b in zip(sh, ref))
+    assert_same(sh, ref, '')
 
 
 @pytest.mark.parametrize("nin,nout", [(7, 9), (32, 2), (33, 1)])
@@ -124,7 +125,7 @@ def test_direct_code_some_shards(gpu, oracle_lib, nin, nout):
     ref = [o.copy() for o in outs]
     oracle_lib.code_some_shards(7, rows, inputs, ref, off, n - off)
     rsamd.codeSomeShards(rows, inputs, nin, outs, nout, off, n - off)
-    assert all(np.array_equal(a, b) for a, b in zip(outs, ref))
+    assert_same(outs, ref, '')
     assert rsamd.checkSomeShards(rows, inputs, nin, outs, nout, off, n - off)
     outs[-1][n - 1] ^= 1  # the last byte of the range
     assert not rsamd.checkSomeShards(rows, inputs, nin, outs, nout, off, n - off)
@@ -150,7 +151,7 @@ def test_direct_threads(gpu, oracle_lib):
                 ref = [a.copy() for a in sh]
                 oc.encode_parity(ref, 0, n)
                 rs.encodeParity(sh, 0, n)
-                assert all(np.array_equal(a, b) for a, b in zip(sh, ref))
+                assert_same(sh, ref, '')
                 sh[0][:] = rng.integers(0, 256, n, dtype=np.uint8)
         except Exception as e:  # noqa: BLE001
             errors.append(e)
@@ -194,15 +195,15 @@ def test_direct_file_paths(gpu, oracle_lib, k, m, n, file_off, pinned, misses):
         a[:] = 0xEE  # every byte must be written
     file_encode_into(rs, fbuf, sh)
     ref = oc.file_encode(fbuf.tobytes())
-    assert np.array_equal(np.stack(sh), ref)
+    assert_same(sh, ref, '')
     for miss in misses:
         for j in miss:
             sh[j][:] = 0
         out = alloc(n + 64)[8:8 + n]
         out[:] = 0x33
         file_decode_into(rs, sh, [i not in miss for i in range(k + m)], S, out)
-        assert np.array_equal(out, fbuf), miss
-        assert np.array_equal(np.stack(sh), ref), miss  # absent shards rebuilt in place
+        assert_same([out], [fbuf], miss)
+        assert_same(sh, ref, miss)  # absent shards rebuilt in place
 
 
 @pytest.mark.parametrize("k,m,n,block,offs", [
@@ -245,7 +246,7 @@ def test_direct_file_interior(gpu, oracle_lib, k, m, n, block, offs):
         a[:] = 0xEE  # every byte must be written
     file_encode_into(rs, fbuf, sh, block)
     ref = oc.file_encode(fbuf.tobytes(), block)
-    assert np.array_equal(np.stack(sh), ref)
+    assert_same(sh, ref, '')
     assert all(guards_intact(r, v) for r, v in shs) and guards_intact(fraw, fbuf)
     miss = tuple(int(x) for x in rng.choice(k + m, m, replace=False))
     for j in miss:
@@ -253,17 +254,17 @@ def test_direct_file_interior(gpu, oracle_lib, k, m, n, block, offs):
     oraw, out = place(n, offs[0] + 8 if offs[0] % 8 == 0 else offs[0])
     out[:] = 0x33
     file_decode_into(rs, sh, [i not in miss for i in range(k + m)], S, out, block)
-    assert np.array_equal(out, fbuf), miss
-    assert np.array_equal(np.stack(sh), ref), miss  # absent shards rebuilt in place
+    assert_same([out], [fbuf], miss)
+    assert_same(sh, ref, miss)  # absent shards rebuilt in place
     assert all(guards_intact(r, v) for r, v in shs) and guards_intact(oraw, out)
 
 
 def test_direct_file_interior_threads(gpu, oracle_lib):
     """Four threads at once, each encoding and decoding its own file, with
     every file and shard a slice of ONE pageable buffer, packed back to back
-    at 8-byte-aligned odd offsets so neighbouring slices share pages.  Each
-    call locks only pages wholly inside its own slices, so no two calls' locks
-    overlap; every result is exact and the registry ends empty (conftest)."""
+    at 8-byte-aligned odd offsets so neighbouring slices share pages (the
+    mirrored pipeline: each thread's chunks through its own slots); every
+    result is exact."""
     import threading
     import rsamd
     from rsamd.layout import file_decode_into, file_encode_into, file_layout
@@ -313,10 +314,10 @@ def test_direct_file_interior_threads(gpu, oracle_lib):
 
 @pytest.mark.parametrize("n,off", [((64 << 10) + 4100, 3), ((256 << 10) + 8200, 3), ((1 << 20) + 7, 4095), (5 << 20, 0)])
 def test_direct_interior_and_ends(gpu, oracle_lib, n, off):
-    """Pageable calls: the pages wholly inside the range are coded in place,
-    the ends (under a page per shard) through the staging buffer in the same
-    launches.  Encode, decode and verify must be exact at both ends and
-    inside, and a wrong parity byte is found wherever it is."""
+    """Pageable calls at ragged offsets and lengths (the mirrored pipeline's
+    ramped chunks, or the zero-copy pass under 256 KiB per shard).  Encode,
+    decode and verify must be exact at both ends and inside, and a wrong
+    parity byte is found wherever it is."""
     import rsamd
     rs = rsamd.ReedSolomon.create(4, 2)
     rng = np.random.default_rng(n + off)
@@ -325,7 +326,7 @@ def test_direct_interior_and_ends(gpu, oracle_lib, n, off):
     ref = [a.copy() for a in sh]
     oracle_lib.Codec(4, 2).encode_parity(ref, off, cnt)
     rs.encodeParity(sh, off, cnt)
-    assert all(np.array_equal(a, b) for a, b in zip(sh, ref))
+    assert_same(sh, ref, '')
     assert rs.isParityCorrect(sh, off, cnt)
     for where in (off, off + cnt - 1, off + cnt // 2, off + 4095 if cnt > 8192 else off + 1):
         sh[5][where] ^= 0x5A
@@ -335,4 +336,4 @@ def test_direct_interior_and_ends(gpu, oracle_lib, n, off):
         for j in miss:
             sh[j][off:off + cnt] = 0x33
         rs.decodeMissing(sh, [i not in miss for i in range(6)], off, cnt)
-        assert all(np.array_equal(a, b) for a, b in zip(sh, ref)), miss
+        assert_same(sh, ref, miss)

@@ -8,6 +8,7 @@ the first k present shards with every absent shard filled in place
 """
 import numpy as np
 import pytest
+from bytes_report import assert_same
 
 pytestmark = pytest.mark.gpu
 
@@ -31,7 +32,7 @@ def test_file_paths_random(gpu, oracle_lib, case):
     enc = ReedSolomonEncoder(data, k, m, block)
     enc.encode()
     got = np.stack(enc.getShards()) if ref.shape[1] else np.zeros_like(ref)
-    assert np.array_equal(got, ref), (k, m, block, n)
+    assert_same([got], [ref], (k, m, block, n))
     if n == 0:
         return
     S = ref.shape[1]
@@ -43,7 +44,7 @@ def test_file_paths_random(gpu, oracle_lib, case):
         sh[j][:] = 0
     out = ReedSolomonDecoder(sh, present, S, n, k, m, block).getFileData()
     assert out == data, (k, m, block, n, miss)
-    assert all(np.array_equal(a, b) for a, b in zip(sh, ref)), (k, m, block, n, miss)  # filled in place
+    assert_same(sh, ref, (k, m, block, n, miss))  # filled in place
     assert oc.file_decode(ref, present, n, block) == data
 
     # the device forms on the same case: shards at a 256-rounded stride
@@ -96,7 +97,7 @@ def test_file_host_random_large(gpu, oracle_lib, case):
         a[:] = 0xEE
     file_encode_into(rs, f, sh, block)
     ref = oc.file_encode(f.tobytes(), block)
-    assert np.array_equal(np.stack(sh), ref), (k, m, block, n)
+    assert_same(sh, ref, (k, m, block, n))
     e = int(rng.integers(0, m + 1))
     miss = sorted(int(x) for x in rng.choice(k + m, e, replace=False)) if e else []
     for j in miss:
@@ -104,5 +105,5 @@ def test_file_host_random_large(gpu, oracle_lib, case):
     out = view(n)
     out[:] = 0x33
     file_decode_into(rs, sh, [i not in miss for i in range(k + m)], S, out, block)
-    assert np.array_equal(out, f), (k, m, block, n, miss)
-    assert np.array_equal(np.stack(sh), ref), (k, m, block, n, miss)
+    assert_same([out], [f], (k, m, block, n, miss))
+    assert_same(sh, ref, (k, m, block, n, miss))

@@ -1,15 +1,15 @@
-"""GPU tests of the host calls' per-call page-locking (host.cpp
-HostRegistration): the pages wholly inside pageable caller ranges are
-registered with hipHostRegister for the duration of one call, all or nothing,
-with the staged paths as the fallback (capi.cpp run_direct_interior).
-Registration collisions must never change a byte: threads sharing the same
-input arrays, shards that are slices of one allocation (shared pages), and the
-same array passed twice.
+"""GPU tests of the host calls on pageable caller memory (JVM heap arrays
+through JNI), which go through the mirrored pipeline (host.hpp run_mirrored:
+chunks copied into the thread's device-mapped pinned slots, coded there by the
+direct kernels, copied back).  Sharing must never change a byte: threads
+passing the same input arrays, shards that are slices of one allocation
+(shared pages), and the same array passed twice.
 """
 import threading
 
 import numpy as np
 import pytest
+from bytes_report import assert_same
 
 pytestmark = pytest.mark.gpu
 
@@ -52,18 +52,17 @@ def test_shards_are_slices_of_one_allocation(gpu, oracle_lib):
     ref = [s.copy() for s in sh]
     oracle_lib.Codec(4, 2).encode_parity(ref, 0, N)
     rs.encodeParity(sh, 0, N)
-    assert all(np.array_equal(a, b) for a, b in zip(sh, ref))
+    assert_same(sh, ref, '')
     sh[1][:] = 0
     sh[4][:] = 0
     rs.decodeMissing(sh, [True, False, True, True, False, True], 0, N)
-    assert all(np.array_equal(a, b) for a, b in zip(sh, ref))
+    assert_same(sh, ref, '')
     assert rs.isParityCorrect(sh, 0, N)
 
 
 def test_same_array_twice_as_input(gpu, oracle_lib):
-    """CodingLoop-level call with one input array passed twice: its range is
-    registered once and the second registration collides -- the call falls
-    back to the mirrors and the bytes are still right."""
+    """CodingLoop-level call with one input array passed twice (two slots of
+    the mirror hold the same bytes)."""
     import rsamd
     rng = np.random.default_rng(33)
     a = rng.integers(0, 256, N, dtype=np.uint8)
@@ -73,16 +72,13 @@ def test_same_array_twice_as_input(gpu, oracle_lib):
     ref = [np.zeros(N, np.uint8)]
     oracle_lib.code_some_shards(7, rows, [a, b, a], ref, 0, N)
     rsamd.codeSomeShards(rows, [a, b, a], 3, out, 1, 0, N)
-    assert np.array_equal(out[0], ref[0])
+    assert_same([out[0]], [ref[0]], '')
 
 
 def test_threads_check_the_same_shards(gpu, oracle_lib):
     """Several threads run isParityCorrect on the SAME pageable shards (every
-    slot an input).  Memory another thread's call has locked reads as pinned;
-    each call must still take its own reference on the registration (host.cpp
-    all_pinned / registry_holds), or the first call to finish would unlock the
-    pages under the others' kernels.  Then decodes of the same shards into
-    per-thread copies of the absent ones."""
+    slot an input; each thread has its own mirror slots and stream), then
+    decodes of the same shards into per-thread copies of the absent ones."""
     import rsamd
     rs = rsamd.ReedSolomon.create(4, 2)
     rng = np.random.default_rng(33)

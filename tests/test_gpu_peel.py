@@ -71,11 +71,13 @@ def test_misaligned_batches_equal_the_aligned_batch(gpu, oracle_lib, K, M, pad, 
     torch.cuda.empty_cache()
 
 
-def test_shard_major_run_past_a_line_at_scale(gpu, oracle_lib):
+@pytest.mark.parametrize("pad", [0, 4096 + 8])
+def test_shard_major_run_past_a_line_at_scale(gpu, oracle_lib, pad):
     """The master's offline set grows at odd group 300 033 of 600 064 (the
     second run, 300 MB per server, starts 1000 B past a 1 KiB boundary):
     every chunk comes back, and the groups around the failure match the
-    oracle's parity."""
+    oracle's parity.  With a pad after each server's array, its sentinel
+    bytes (and every byte at the runs' group boundaries) come back unchanged."""
     import torch
     import rsamd
     from rsamd import device
@@ -83,21 +85,24 @@ def test_shard_major_run_past_a_line_at_scale(gpu, oracle_lib):
     from rsamd.recovery import recover_groups_shard_major_dev
     chunk, N, j = 1000, 600_064, 300_033
     rs = rsamd.ReedSolomon.create(K, M)
-    lay = StripeLayout(1, N * chunk, N * chunk, T * N * chunk)
+    stride = N * chunk + pad
+    lay = StripeLayout(1, N * chunk, stride, T * stride)
     st = torch.cuda.current_stream()
-    buf = torch.empty(lay.nbytes, dtype=torch.uint8, device="cuda:0")
+    buf = torch.full((lay.nbytes,), 0xA5, dtype=torch.uint8, device="cuda:0")
     device.fill_synthetic(buf.data_ptr(), K, lay, 0x6A57E2, 0, st)
     device.encode(rs, buf.data_ptr(), lay, st)
     want = buf.clone()
-    v = buf.view(T, N * chunk)
+    v = buf.view(T, stride)
     present = np.ones((N, T), bool)
     for g0, g1, miss in [(0, j, (0,)), (j, N, (0, 3))]:
         present[g0:g1, list(miss)] = False
         for s in miss:
             v[s, g0 * chunk: g1 * chunk].fill_(0x3C)
-    recover_groups_shard_major_dev(buf.data_ptr(), N * chunk, present, chunk, st)
+    recover_groups_shard_major_dev(buf.data_ptr(), stride, present, chunk, st)
     assert torch.equal(buf, want)
-    w = want.view(T, N, chunk)[:, j - 2: j + 3].cpu().numpy()
+    if pad:
+        assert int((buf.view(T, stride)[:, N * chunk:] != 0xA5).sum()) == 0
+    w = want.view(T, stride)[:, : N * chunk].reshape(T, N, chunk)[:, j - 2: j + 3].cpu().numpy()
     for g in range(5):
         rows = [w[i, g].copy() for i in range(K)] + [np.zeros(chunk, np.uint8) for _ in range(M)]
         oracle_lib.Codec(K, M).encode_parity(rows, 0, chunk)
@@ -139,5 +144,25 @@ def test_masked_patterns_on_a_misaligned_batch(gpu, o):
         else:
             device.decode_masked(rs, b, pats, lay, st)
         assert torch.equal(pool, want), bits
-    del pool, want, v, mask
+    # Undecodable stripes (fewer than k shards present) through the peeled
+    # launch: each is counted exactly once and left untouched; the rest decode.
+    rng = np.random.default_rng(o + 1)
+    undec = np.sort(rng.choice(B, 7, replace=False))
+    pats2 = pats.copy()
+    pats2[undec] = np.array([i < K - 1 for i in range(T)])  # k - 1 present
+    v.masked_fill_(mask[:, :, None], 0x3C)
+    before = pool.clone()
+    words = torch.from_numpy(presence_bits(pats2).view(np.int32)).to("cuda:0")
+    bad = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    device.decode_masked_bits(rs, b, words.data_ptr(), lay, bad.data_ptr(), st)
+    assert int(bad.item()) == len(undec), (int(bad.item()), len(undec))
+    got = pool[o: o + lay.nbytes].view(B, T * lay.shard_stride)
+    ok = np.setdiff1d(np.arange(B), undec)
+    ref = want[o: o + lay.nbytes].view(B, T * lay.shard_stride)
+    old = before[o: o + lay.nbytes].view(B, T * lay.shard_stride)
+    idx = torch.from_numpy(ok).to("cuda:0")
+    assert torch.equal(got[idx], ref[idx])
+    idx = torch.from_numpy(undec).to("cuda:0")
+    assert torch.equal(got[idx], old[idx])
+    del pool, want, v, mask, before, got, ref, old
     torch.cuda.empty_cache()

@@ -15,6 +15,13 @@ Every byte outside the coded range and every present shard must be unchanged.
 """
 import numpy as np
 import pytest
+from bytes_report import describe
+
+
+def assert_equal_bytes(got, want, msg):
+    d = describe(got, want)
+    assert d is None, f"{msg}: {d}"
+
 
 pytestmark = pytest.mark.gpu
 
@@ -43,7 +50,7 @@ def test_host_api_random(gpu, oracle_lib, case):
     rs.encodeParity(got, off, cnt)
     oc.encode_parity(ref, off, cnt)
     for i, (a, b) in enumerate(zip(got, ref)):
-        np.testing.assert_array_equal(a, b, err_msg=f"encode k={k} m={m} n={n} off={off} cnt={cnt} shard {i}")
+        assert_equal_bytes(a, b, f"encode k={k} m={m} n={n} off={off} cnt={cnt} shard {i}")
     assert rs.isParityCorrect(got, off, cnt) == oc.is_parity_correct(ref, off, cnt) == True  # noqa: E712
     if m and cnt:
         bad = [s.copy() for s in got]
@@ -57,7 +64,7 @@ def test_host_api_random(gpu, oracle_lib, case):
     rs.decodeMissing(got, present, off, cnt)
     oc.decode_missing(ref, present, off, cnt)
     for i, (a, b) in enumerate(zip(got, ref)):
-        np.testing.assert_array_equal(a, b, err_msg=f"decode k={k} m={m} n={n} off={off} cnt={cnt} "
+        assert_equal_bytes(a, b, f"decode k={k} m={m} n={n} off={off} cnt={cnt} "
                                                     f"present={present} shard {i}")
 
 
@@ -157,7 +164,7 @@ def test_host_api_random_large(gpu, oracle_lib, case):
     rs.encodeParity(got, off, cnt)
     oc.encode_parity(ref, off, cnt)
     for i, (a, b) in enumerate(zip(got, ref)):
-        np.testing.assert_array_equal(a, b, err_msg=f"encode {desc} shard {i}")
+        assert_equal_bytes(a, b, f"encode {desc} shard {i}")
     assert rs.isParityCorrect(got, off, cnt)
     if m:
         j = int(rng.choice([off, off + cnt - 1, int(rng.integers(off, off + cnt))]))
@@ -174,4 +181,4 @@ def test_host_api_random_large(gpu, oracle_lib, case):
     rs.decodeMissing(got2, present, off, cnt)
     oc.decode_missing(ref, present, off, cnt)
     for i, (a, b) in enumerate(zip(got2, ref)):
-        np.testing.assert_array_equal(a, b, err_msg=f"decode {desc} present={present} shard {i}")
+        assert_equal_bytes(a, b, f"decode {desc} present={present} shard {i}")

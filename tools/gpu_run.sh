@@ -4,7 +4,7 @@
 # at the first failure (nothing more touches the GPU after a fault or timeout):
 #   tests      pytest -m gpu (one process)              -> pytest_gpu_TAG.log
 #   bounds     pytest -m gpu against the bounds-checking build (lib/bounds), serialised
-#   hostreg    the host-path test files with page-locking of pageable memory on -> pytest_hostreg_TAG.log
+#   hosttests  the host-buffer test files only           -> pytest_host_TAG.log
 #   smoke      __graft_entry__.smoke()                  -> smoke_TAG.log
 #   bench      bench.py at N = 1 (live PMC passes)      -> bench_TAG.json
 #   prof       rocprofv3 --kernel-trace --stats of the headline -> prof_TAG/
@@ -40,13 +40,13 @@ for step in "$@"; do
         timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
           > $out/pytest_bounds_$tag.log 2>&1 || { echo "bounds pytest failed"; tail -40 $out/pytest_bounds_$tag.log; exit 1; }
       tail -1 $out/pytest_bounds_$tag.log ;;
-    hostreg)
-      # page-locking of pageable caller memory (rs_set_host_register: TUNING build only), a process of its own
-      RSAMD_TEST_LIB=build/ab/tuning/librsamd.so RSAMD_TEST_HOST_REGISTER=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_direct.py \
-          tests/test_gpu_host_register.py tests/test_gpu_random.py tests/test_gpu_file_random.py \
-          -m gpu -x -v --timeout 300 --timeout-method thread \
-          > $out/pytest_hostreg_$tag.log 2>&1 || { echo "hostreg pytest failed"; tail -40 $out/pytest_hostreg_$tag.log; exit 1; }
-      tail -1 $out/pytest_hostreg_$tag.log ;;
+    hosttests)
+      # the host-buffer paths only (direct, mirrored, staged; file layout), product library
+      timeout -k 10 600 python -u -m pytest tests/test_gpu_direct.py tests/test_gpu_host_pageable.py \
+          tests/test_gpu_random.py tests/test_gpu_file_random.py tests/test_gpu_jni_core.py -m gpu -x -v \
+          --timeout 300 --timeout-method thread > $out/pytest_host_$tag.log 2>&1 \
+          || { echo "host pytest failed"; tail -40 $out/pytest_host_$tag.log; exit 1; }
+      tail -1 $out/pytest_host_$tag.log ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke_$tag.log 2>&1 \
           || { echo "smoke failed"; cat $out/smoke_$tag.log; exit 1; }
