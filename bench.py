@@ -443,7 +443,11 @@ def decode_summary(extra):
         "host_file_enc_GiBps": g("host_inclusive_file_encode_GiBps"),
         "host_file_enc_link_frac": g("host_inclusive_file_encode_frac_of_link_bound"),
         "host_file_dec_link_frac": g("host_inclusive_file_decode_0_5_frac_of_link_bound"),
+        "host_file_enc_all_gpu_link_frac": g("host_inclusive_file_encode_frac_of_all_gpu_link_bound"),
+        "host_file_dec_all_gpu_link_frac": g("host_inclusive_file_decode_0_5_frac_of_all_gpu_link_bound"),
         "host_pinned_enc_link_frac": g("host_inclusive_pinned_encode_frac_of_link_bound"),
+        "host_pinned_file_enc_link_frac": g("host_inclusive_pinned_file_encode_frac_of_link_bound"),
+        "host_pinned_file_dec_link_frac": g("host_inclusive_pinned_file_decode_0_5_frac_of_link_bound"),
     }
 
 
@@ -1433,26 +1437,48 @@ def host_inclusive(rsamd, k, m, link=None):
         a[:] = b
     out["host_inclusive_pinned_encode_GiBps"] = rate(lambda: rs.encodeParity(pin, 0, n), k * n)
     out["host_inclusive_pinned_decode_0_1_GiBps"] = rate(lambda: rs.decodeMissing(pin, present, 0, n), k * n)
-    del pin
+    # the file calls on pinned buffers (the direct kernels plus the split / merge on the host)
+    pfile = torch.empty(len(data), dtype=torch.uint8, pin_memory=True).numpy()
+    pfile[:] = data
+    pfsh = [torch.empty(S, dtype=torch.uint8, pin_memory=True).numpy() for _ in range(k + m)]
+    pfout = torch.empty(len(data), dtype=torch.uint8, pin_memory=True).numpy()
+    out["host_inclusive_pinned_file_encode_GiBps"] = rate(lambda: file_encode_into(rs, pfile, pfsh), len(data))
+    out["host_inclusive_pinned_file_decode_0_%d_GiBps" % (k + m - 1)] = rate(
+        lambda: file_decode_into(rs, pfsh, fpresent, S, pfout), len(data))
+    pinned_file_ok = np.array_equal(pfout, data) and all(np.array_equal(a, b) for a, b in zip(pfsh, fsh))
+    out["host_inclusive_file_legs_bit_exact"] = bool(pinned_file_ok and np.array_equal(fout, data))
+    del pin, pfile, pfsh, pfout
     out["host_inclusive_note"] = (f"{k}+{m}, {n >> 20} MiB host shards per call, pageable unless 'pinned' "
                                   f"(file legs: a {len(data) >> 20} MiB file); PCIe-bound, never the bench value; "
                                   f"pinned calls of >= 64 KiB per shard are coded in place across the link by one "
-                                  f"kernel (the direct path, no copies); pageable ones are staged through the "
-                                  f"library's pinned buffers (product builds never page-lock caller memory, "
-                                  f"DESIGN.md 5.3)")
-    # Each leg against the link bound of its traffic (bytes up / down per user byte):
-    # encode k up, m down per k user bytes; decode {0,1} k up, 2 down; file encode
-    # 1 up, (k+m)/k down; file decode {0,k+m-1} 1 up (the k survivors), 1 + 2/k down
-    # (the file, and both absent shards rebuilt in place as decodeMissing does).
+                                  f"kernel (the direct path, no copies); pageable ones go through the "
+                                  f"mirrored pipeline (copied chunk by chunk into the library's device-mapped "
+                                  f"pinned slots, overlapped with the link; the library never page-locks caller "
+                                  f"memory, DESIGN.md 5.3); pageable file calls keep the split / merge on the "
+                                  f"CPU, so only coded bytes cross the link")
+    # Each leg against the link bound of the bytes it must move (up / down per
+    # user byte): encode k up, m down per k user bytes; decode {0,1} k up, 2
+    # down.  The pageable file calls keep the layout on the CPU (capi.cpp
+    # file_encode_mirrored / file_decode_mirrored), so only coded bytes cross:
+    # file encode 1 up (the data), m/k down (parity); file decode {0,k+m-1} 1 up
+    # (the k survivors), 2/k down (the rebuilt shards).  Their *_all_gpu_* keys
+    # keep round 4's bound, where the GPU also did the layout and moved every
+    # shard (file encode (k+m)/k down; file decode 1 + 2/k down: the file too).
+    fdec = "host_inclusive_file_decode_0_%d_GiBps" % (k + m - 1)
     legs = {"host_inclusive_encode_GiBps": (1.0, m / k), "host_inclusive_pinned_encode_GiBps": (1.0, m / k),
             "host_inclusive_decode_0_1_GiBps": (1.0, 2 / k), "host_inclusive_pinned_decode_0_1_GiBps": (1.0, 2 / k),
-            "host_inclusive_file_encode_GiBps": (1.0, (k + m) / k),
-            "host_inclusive_file_decode_0_%d_GiBps" % (k + m - 1): (1.0, 1.0 + 2.0 / k)}
+            "host_inclusive_file_encode_GiBps": (1.0, m / k), fdec: (1.0, 2.0 / k),
+            "host_inclusive_pinned_file_encode_GiBps": (1.0, m / k),
+            "host_inclusive_pinned_" + fdec[len("host_inclusive_"):]: (1.0, 2.0 / k)}
     for key, (up, down) in legs.items():
         bound = link_bound_GiBps(link, up, down)
         if bound and key in out:
             out[key.replace("_GiBps", "_link_bound_GiBps")] = bound
             out[key.replace("_GiBps", "_frac_of_link_bound")] = round(out[key] / bound, 4)
+    for key, (up, down) in (("host_inclusive_file_encode_GiBps", (1.0, (k + m) / k)), (fdec, (1.0, 1.0 + 2.0 / k))):
+        bound = link_bound_GiBps(link, up, down)
+        if bound and key in out:
+            out[key.replace("_GiBps", "_frac_of_all_gpu_link_bound")] = round(out[key] / bound, 4)
     return out
 
 

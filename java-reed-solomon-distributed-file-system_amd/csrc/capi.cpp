@@ -462,11 +462,68 @@ FileChunks file_chunks(int k, int total, size_t S, size_t block, bool pinned) {
     return f;
 }
 
-// Direct path of the host file calls (layout.hpp FileDirect): page-locked file
-// and shards coded in place across the link by one kernel, as run_direct does
-// for shards.  *taken = false, nothing enqueued, when the code or a pointer
-// does not fit the direct kernels (more than kMaxOut outputs, k above
-// kMaxDirectIn, no device address, not 8-byte aligned): the call is staged.
+// ReedSolomonEncoder's split (ReedSolomonEncoder.java:56-60, the arraycopy
+// per block) of block rows [r0, r1) as copy jobs: data shard i's block of row
+// r is file bytes [(r k + i) blk, +blk), zeros past the file's end (the
+// padding).  Row r goes to dst[i] + r * blk and, with dst2, to dst2[i] +
+// (r - row2) * blk as well (one read, two writes).
+void split_jobs(const uint8_t *file, size_t file_len, size_t blk, int k, uint8_t *const *dst, uint8_t *const *dst2,
+                size_t row2, size_t r0, size_t r1, std::vector<rsamd::CopyJob> *jobs) {
+    const size_t kb = size_t(k) * blk;
+    const size_t full = std::min(r1, std::max(r0, file_len / kb));  // rows wholly inside the file
+    for (int i = 0; i < k; ++i) {
+        uint8_t *a = dst[i] + r0 * blk, *b = dst2 ? dst2[i] + (r0 - row2) * blk : nullptr;  // row r0's blocks
+        if (full > r0) {
+            rsamd::CopyJob job{a, file + (r0 * size_t(k) + size_t(i)) * blk, blk, full - r0, blk, kb};
+            job.dst2 = b;
+            job.dst2_stride = blk;
+            jobs->push_back(job);
+        }
+        for (size_t r = full; r < r1; ++r) {  // the last row: the file's bytes, then the padding's zeros
+            const size_t f0 = (r * size_t(k) + size_t(i)) * blk;
+            const size_t have = f0 < file_len ? std::min(blk, file_len - f0) : 0;
+            for (uint8_t *d : {a, b}) {
+                if (!d) continue;
+                d += (r - r0) * blk;
+                if (have) jobs->push_back({d, file + f0, have});
+                if (have < blk) jobs->push_back({d + have, nullptr, blk - have});
+            }
+        }
+    }
+}
+
+// ReedSolomonDecoder's merge and trim (ReedSolomonDecoder.java:62-66, 92-103)
+// of block rows [r0, r1) as copy jobs: data shard d's block of row r is file
+// bytes [(r k + d) blk, +blk), clipped to the file.  src[d] holds shard d's
+// bytes from row r0 on; shards with only[d] == false are skipped.
+void merge_jobs(int k, size_t blk, uint8_t *file_out, size_t file_size, const uint8_t *const *src,
+                const std::vector<bool> &only, size_t r0, size_t r1, std::vector<rsamd::CopyJob> *jobs) {
+    const size_t kb = size_t(k) * blk;
+    for (int d = 0; d < k; ++d) {
+        if (!only[d]) continue;
+        for (size_t r = r0; r < r1;) {
+            const size_t f0 = (r * size_t(k) + size_t(d)) * blk;
+            if (f0 >= file_size) break;
+            if (f0 + blk <= file_size) {  // whole blocks up to the first that crosses the file's end
+                const size_t last = std::min(r1, (file_size - size_t(d) * blk - blk) / kb + 1);
+                jobs->push_back({file_out + f0, src[d] + (r - r0) * blk, blk, last - r, kb, blk});
+                r = last;
+            } else {
+                jobs->push_back({file_out + f0, src[d] + (r - r0) * blk, file_size - f0});
+                ++r;
+            }
+        }
+    }
+}
+
+// Direct path of the host file calls on caller-pinned memory (layout.hpp
+// FileDirect): the fused kernel reads the file in place across the link and
+// writes the parity shards in place, while the copy pool splits the file into
+// the data shards on the host (they are the file's own bytes: only coded bytes
+// cross the link, 1.5 file sizes for 4+2 instead of 2.5).  *taken = false,
+// nothing enqueued, when the code or a pointer does not fit the direct kernels
+// (more than kMaxOut outputs, k above kMaxDirectIn, no device address, not
+// 8-byte aligned): the call is staged.
 int file_encode_direct(const Codec &c, const uint8_t *file, size_t file_len, size_t blk, uint8_t *const *shards,
                        size_t S, ThreadCtx *ctx, bool *taken) {
     *taken = false;
@@ -479,18 +536,21 @@ int file_encode_direct(const Codec &c, const uint8_t *file, size_t file_len, siz
     d.file_len = file_len;
     d.file = host_dev_addr(file);
     if (!d.file) return RS_OK;
-    for (int i = 0; i < c.total(); ++i)
+    for (int i = c.k(); i < c.total(); ++i)  // data shards (out[0 .. k)) stay null: split on the host
         if (!(d.out[i] = host_dev_addr(shards[i]))) return RS_OK;
     if (c.m() > 0) {
         std::vector<DevPlan> plans;
         RS_HIP(c.encode_plan().device_plans(&plans));
         d.tabs = plans[0].tabs;
     }
-    if (!rsamd::file_direct_ok(d, true)) return RS_OK;
+    if (!rsamd::file_direct_ok(d)) return RS_OK;
     bounds::allow(d.file, file_len);
-    for (int i = 0; i < c.total(); ++i) bounds::allow(d.out[i], S);
-    RS_HIP(rsamd::launch_file_encode_direct(d, ctx->stream));
+    for (int i = c.k(); i < c.total(); ++i) bounds::allow(d.out[i], S);
+    if (c.m() > 0) RS_HIP(rsamd::launch_file_encode_direct(d, ctx->stream));
     *taken = true;
+    std::vector<rsamd::CopyJob> jobs;
+    split_jobs(file, file_len, blk, c.k(), shards, nullptr, 0, 0, S / blk, &jobs);
+    rsamd::CopyPool::get().copy(jobs);
     RS_HIP(hipStreamSynchronize(ctx->stream));
     return RS_OK;
 }
@@ -518,115 +578,115 @@ int file_encode_staged(const Codec &c, const uint8_t *file, size_t file_len, siz
 }
 
 // Mirrored form of the host file calls (pageable callers, host.hpp
-// run_mirrored): chunks of block rows, each slot laid out as [the rows' file
-// bytes][shard 0 .. total-1 columns of the rows], page-aligned, coded in the
-// slot by the fused direct file kernels.  Rows per chunk, the chunk
-// boundaries (in rows) and the slot layout:
-struct MirrorRows {
-    std::vector<size_t> bounds;
-    size_t fstride = 0, sstride = 0, buf_bytes = 0;
-};
-
-MirrorRows mirror_rows(int k, int total, size_t rows, size_t blk) {
-    MirrorRows r;
-    // a row is k*blk file bytes plus total*blk shard bytes: k + total slots of blk
-    const size_t per = mirror_chunk_bytes(rows * blk, k + total, blk);
-    r.bounds = ramp_bounds(rows, std::max<size_t>(1, per / blk), 1);
+// run_mirrored) -- the file layout on the CPU, the coding on the GPU.  A
+// file's data shards are its own bytes rearranged (ReedSolomonEncoder.java:
+// 56-60 splits, ReedSolomonDecoder.java:92-103 merges), so they need not
+// cross the link in both directions: the CPU moves them between the caller's
+// file and shard arrays (the same pass that fills the pinned slots), and only
+// the bytes the GPU codes cross the link -- data in, parity (or rebuilt shards)
+// out: a 4+2 file encode moves 1.5 file sizes across the link instead of 2.5.
+// The slots hold shard columns of whole block rows (one slot per shard,
+// page-aligned), coded by the shard direct kernels.
+//
+// Chunk boundaries in block rows, and the slot stride, for `nslots` slots.
+std::vector<size_t> mirror_row_bounds(size_t rows, size_t blk, int nslots, size_t *slot_stride) {
+    const size_t per = mirror_chunk_bytes(rows * blk, nslots, blk);
+    std::vector<size_t> b = ramp_bounds(rows, std::max<size_t>(1, per / blk), 1);
     size_t widest = 0;
-    for (size_t j = 0; j + 1 < r.bounds.size(); ++j) widest = std::max(widest, r.bounds[j + 1] - r.bounds[j]);
-    r.fstride = round_up(widest * size_t(k) * blk, kMirrorAlign);
-    r.sstride = round_up(widest * blk, kMirrorAlign);
-    r.buf_bytes = r.fstride + r.sstride * size_t(total);
-    return r;
+    for (size_t j = 0; j + 1 < b.size(); ++j) widest = std::max(widest, b[j + 1] - b[j]);
+    *slot_stride = round_up(widest * blk, kMirrorAlign);
+    return b;
 }
 
-// *taken = false (nothing done) when the direct file kernel cannot take the
-// code or the block size (more than kMaxOut parity shards, k above
-// kMaxDirectIn, blocks that are not 8-byte multiples).
-int file_encode_mirrored(const Codec &c, const uint8_t *file, size_t file_len, size_t blk, uint8_t *const *shards,
-                         size_t S, ThreadCtx *ctx, bool *taken) {
-    *taken = false;
-    if (!direct_enabled() || c.m() > rsamd::kMaxOut || c.k() > rsamd::kMaxDirectIn || blk % 8) return RS_OK;
-    const int T = c.total();
-    const size_t kb = size_t(c.k()) * blk;
-    const MirrorRows mr = mirror_rows(c.k(), T, S / blk, blk);
-    const uint32_t *tabs = nullptr;
-    if (c.m() > 0) {
-        std::vector<DevPlan> plans;
-        RS_HIP(c.encode_plan().device_plans(&plans));
-        tabs = plans[0].tabs;
-    }
-    auto flen_of = [&](size_t j) { return std::min((mr.bounds[j + 1] - mr.bounds[j]) * kb, file_len - mr.bounds[j] * kb); };
-    auto io = [&](size_t j, std::vector<Xfer> *in, std::vector<Xfer> *out) {
-        const size_t r0 = mr.bounds[j], nr = mr.bounds[j + 1] - r0;
-        in->push_back({const_cast<uint8_t *>(file) + r0 * kb, 0, flen_of(j)});
-        for (int i = 0; i < T; ++i) out->push_back({shards[i] + r0 * blk, mr.fstride + size_t(i) * mr.sstride, nr * blk});
-    };
-    auto code = [&](size_t j, uint8_t *dev, hipStream_t st) -> int {
-        rsamd::FileDirect d;
-        d.k = c.k();
-        d.nout = c.m();
-        d.block = blk;
-        d.units = (mr.bounds[j + 1] - mr.bounds[j]) * blk / 8;
-        d.file_len = flen_of(j);
-        d.file = dev;
-        d.tabs = tabs;
-        for (int i = 0; i < T; ++i) d.out[i] = dev + mr.fstride + size_t(i) * mr.sstride;
-        RS_HIP(rsamd::launch_file_encode_direct(d, st));
-        return RS_OK;
-    };
-    *taken = true;
-    return run_mirrored(ctx, mr.bounds.size() - 1, mr.buf_bytes, io, code);
-}
-
-// The fused direct decode's shape for a presence pattern (no pointers): the
-// survivors are the first k present shards, the outputs every absent one.
-// RS_OK with *ok = false when the direct kernel cannot take it.
-// *keep holds the decode plan (and so d->tabs) for the caller's kernels.
-int file_decode_shape(const Codec &c, const uint8_t *present, const std::vector<int> &surv,
-                      const std::vector<int> &missing, size_t blk, rsamd::FileDirect *d,
-                      std::shared_ptr<const Plan> *keep, bool *ok) {
-    *ok = false;
-    if (!direct_enabled() || missing.size() > size_t(rsamd::kMaxOut) || c.k() > rsamd::kMaxDirectIn) return RS_OK;
-    d->k = c.k();
-    d->nout = int(missing.size());
-    d->block = blk;
-    if (!missing.empty()) {
-        int rc = c.decode_plan(present, keep);
-        if (rc) return fail(rc, rc == RS_E_SINGULAR ? "Matrix is singular" : "Not enough shards present");
-        std::vector<DevPlan> plans;
-        RS_HIP((*keep)->device_plans(&plans));
-        d->tabs = plans[0].tabs;
-    }
-    for (int i = 0; i < d->k; ++i) d->in_shard[i] = surv[i];
-    for (int q = 0; q < d->nout; ++q) d->out_shard[q] = missing[q];
-    *ok = true;
+// Codes chunk j's columns of the slots: every launch group of `plans` over the
+// slot-indexed shards.
+int code_slots(const std::vector<DevPlan> &plans, const std::vector<int> &in_slots, const std::vector<int> &out_slots,
+               uint8_t *dev, size_t slot_stride, size_t n, Mode mode, int *flag, hipStream_t st) {
+    std::vector<rsamd::DirectPlan> dp;
+    if (!direct_plans(plans, in_slots, out_slots, [&](int sl) { return dev + size_t(sl) * slot_stride; }, &dp))
+        return fail(RS_E_HIP, "direct plans over the mirror slots");
+    for (const rsamd::DirectPlan &d : dp) RS_HIP(rsamd::launch_gf_direct(d, n, mode, flag, st));
     return RS_OK;
 }
 
-int file_decode_direct(const Codec &c, uint8_t *const *shards, const uint8_t *present, const std::vector<int> &surv,
-                       const std::vector<int> &missing, size_t blk, uint8_t *file_out, size_t file_size,
-                       size_t cols, ThreadCtx *ctx, bool *taken) {
+// File encode: the CPU splits each chunk's block rows into the caller's data
+// shards and the data slots at once; the GPU codes the parity slots, which are
+// copied out.  *taken = false (nothing done) when the direct kernels cannot
+// take the code (more than kMaxDirectIn data shards).
+int file_encode_mirrored(const Codec &c, const uint8_t *file, size_t file_len, size_t blk, uint8_t *const *shards,
+                         size_t S, ThreadCtx *ctx, bool *taken) {
     *taken = false;
-    rsamd::FileDirect d;
-    std::shared_ptr<const Plan> plan;
-    bool ok = false;
-    int rc0 = file_decode_shape(c, present, surv, missing, blk, &d, &plan, &ok);
-    if (rc0 || !ok) return rc0;
-    d.units = cols / 8;
-    d.file_len = file_size;
-    for (int i = 0; i < d.k; ++i)
-        if (!(d.in[i] = host_dev_addr(shards[surv[i]]))) return RS_OK;
-    for (int q = 0; q < d.nout; ++q)
-        if (!(d.out[q] = host_dev_addr(shards[missing[q]]))) return RS_OK;
-    if (file_size && !(d.file_out = host_dev_addr(file_out))) return RS_OK;
-    if (!rsamd::file_direct_ok(d, false)) return RS_OK;
-    bounds::allow(d.file_out, file_size);
-    for (int i = 0; i < d.k; ++i) bounds::allow(d.in[i], cols);
-    for (int q = 0; q < d.nout; ++q) bounds::allow(d.out[q], cols);
-    RS_HIP(rsamd::launch_file_decode_direct(d, ctx->stream));
+    const int k = c.k(), T = c.total();
+    if (!direct_enabled() || k > rsamd::kMaxDirectIn) return RS_OK;
+    std::vector<DevPlan> plans;
+    if (c.m() > 0) RS_HIP(c.encode_plan().device_plans(&plans));
+    std::vector<int> in_slots(k), out_slots(c.m());
+    for (int i = 0; i < k; ++i) in_slots[i] = i;
+    for (int p = 0; p < c.m(); ++p) out_slots[p] = k + p;
+    size_t ss = 0;
+    const std::vector<size_t> cb = mirror_row_bounds(S / blk, blk, T, &ss);
+    auto io = [&](size_t j, std::vector<Xfer> *, std::vector<Xfer> *out) {
+        const size_t r0 = cb[j], n = (cb[j + 1] - r0) * blk;
+        for (int p = 0; p < c.m(); ++p) out->push_back({shards[k + p] + r0 * blk, size_t(k + p) * ss, n});
+    };
+    auto side = [&](size_t j, uint8_t *slot, std::vector<rsamd::CopyJob> *before, std::vector<rsamd::CopyJob> *) {
+        std::vector<uint8_t *> sl(k);
+        for (int i = 0; i < k; ++i) sl[i] = slot + size_t(i) * ss;  // slot i holds the chunk's rows from cb[j]
+        split_jobs(file, file_len, blk, k, shards, sl.data(), cb[j], cb[j], cb[j + 1], before);
+    };
+    auto code = [&](size_t j, uint8_t *dev, hipStream_t st) -> int {
+        if (plans.empty()) return RS_OK;  // no parity: the split is the whole call
+        return code_slots(plans, in_slots, out_slots, dev, ss, (cb[j + 1] - cb[j]) * blk, Mode::Code, nullptr, st);
+    };
     *taken = true;
+    return run_mirrored(ctx, cb.size() - 1, ss * size_t(T), io, code, side);
+}
+
+// Direct path of the host file decode on caller-pinned memory: the absent
+// shards rebuilt in place across the link by the shard direct kernels (the
+// survivors read, the rebuilt shards written: only coded bytes cross the
+// link), while the copy pool merges the present data shards into the file;
+// the rebuilt data shards are merged once the kernels are done.  *taken =
+// false, nothing enqueued, when the direct kernels cannot take the plan or a
+// shard has no device address.
+int file_decode_pinned(const Codec &c, uint8_t *const *shards, const uint8_t *present, const std::vector<int> &missing,
+                       size_t blk, uint8_t *file_out, size_t file_size, size_t rows_needed, ThreadCtx *ctx,
+                       bool *taken) {
+    *taken = false;
+    const int k = c.k();
+    std::shared_ptr<const Plan> plan;
+    std::vector<rsamd::DirectPlan> dp;
+    if (!missing.empty()) {
+        int rc = c.decode_plan(present, &plan);
+        if (rc) return fail(rc, rc == RS_E_SINGULAR ? "Matrix is singular" : "Not enough shards present");
+        std::vector<DevPlan> plans;
+        RS_HIP(plan->device_plans(&plans));
+        if (!direct_plans(plans, plan->in_idx(), plan->out_idx(), [&](int sl) { return host_dev_addr(shards[sl]); },
+                          &dp))
+            return RS_OK;
+    }
+    const size_t n = rows_needed * blk;
+    for (const rsamd::DirectPlan &d : dp) {
+        for (int i = 0; i < d.nin; ++i) bounds::allow(d.in[i], n);
+        for (int q = 0; q < d.nout; ++q) bounds::allow(d.out[q], n);
+        RS_HIP(rsamd::launch_gf_direct(d, n, Mode::Code, nullptr, ctx->stream));
+    }
+    *taken = true;
+    std::vector<const uint8_t *> src(shards, shards + k);
+    std::vector<bool> now(static_cast<size_t>(k), false), later(static_cast<size_t>(k), false);
+    for (int d = 0; d < k; ++d) {
+        if (present[d])
+            now[d] = true;
+        else
+            later[d] = true;
+    }
+    std::vector<rsamd::CopyJob> jobs;
+    merge_jobs(k, blk, file_out, file_size, src.data(), now, 0, rows_needed, &jobs);
+    rsamd::CopyPool::get().copy(jobs);
     RS_HIP(hipStreamSynchronize(ctx->stream));
+    jobs.clear();
+    merge_jobs(k, blk, file_out, file_size, src.data(), later, 0, rows_needed, &jobs);
+    rsamd::CopyPool::get().copy(jobs);
     return RS_OK;
 }
 
@@ -665,47 +725,56 @@ int file_decode_staged(const Codec &c, uint8_t *const *shards, size_t S, const u
     return run_chunks(ctx, (rows_needed + f.R - 1) / f.R, f.buf_bytes, pinned, io, code);
 }
 
-// Mirrored form of the host file decode (pageable callers; MirrorRows):
-// the survivors' rows copied in, the fused direct decode kernel rebuilds the
-// absent shards' rows and writes the rows' file bytes in the slot, both copied
-// out.  *taken = false (nothing done) when the direct kernel cannot take the
-// pattern or the block size.
-int file_decode_mirrored(const Codec &c, uint8_t *const *shards, size_t S, const uint8_t *present,
-                         const std::vector<int> &surv, const std::vector<int> &missing, size_t blk, uint8_t *file_out,
-                         size_t file_size, size_t rows_needed, ThreadCtx *ctx, bool *taken) {
+// File decode: the survivors' rows go to their slots, the GPU rebuilds the
+// absent shards' slots, which are copied out to the caller's arrays; the CPU
+// merges each chunk's data shards into the file (present ones from the
+// caller's arrays, rebuilt ones from their slots) behind the chunk's kernels.
+// With no shard absent there is nothing to code and the merge is the call.
+// *taken = false (nothing done) when the direct kernels cannot take the code.
+int file_decode_mirrored(const Codec &c, uint8_t *const *shards, const uint8_t *present, const std::vector<int> &surv,
+                         const std::vector<int> &missing, size_t blk, uint8_t *file_out, size_t file_size,
+                         size_t rows_needed, ThreadCtx *ctx, bool *taken) {
     *taken = false;
-    if (blk % 8) return RS_OK;
-    rsamd::FileDirect shape;
+    const int k = c.k(), T = c.total();
+    if (!direct_enabled() || k > rsamd::kMaxDirectIn) return RS_OK;
     std::shared_ptr<const Plan> plan;
-    bool ok = false;
-    int rc = file_decode_shape(c, present, surv, missing, blk, &shape, &plan, &ok);
-    if (rc || !ok) return rc;
-    (void)S;
-    const int T = c.total();
-    const size_t kb = size_t(c.k()) * blk;
-    const MirrorRows mr = mirror_rows(c.k(), T, rows_needed, blk);
-    auto flen_of = [&](size_t j) {
-        const size_t fo = mr.bounds[j] * kb;
-        return file_size > fo ? std::min((mr.bounds[j + 1] - mr.bounds[j]) * kb, file_size - fo) : size_t(0);
+    std::vector<DevPlan> plans;
+    if (!missing.empty()) {
+        int rc = c.decode_plan(present, &plan);
+        if (rc) return fail(rc, rc == RS_E_SINGULAR ? "Matrix is singular" : "Not enough shards present");
+        RS_HIP(plan->device_plans(&plans));
+    }
+    size_t ss = 0;
+    const std::vector<size_t> cb = mirror_row_bounds(rows_needed, blk, T, &ss);
+    // the chunk's data shards into the file: present ones from the caller's
+    // arrays, rebuilt ones from their slots
+    const std::vector<bool> all(size_t(k), true);
+    auto merge = [&](size_t r0, size_t r1, const uint8_t *slot, std::vector<rsamd::CopyJob> *jobs) {
+        std::vector<const uint8_t *> src(k);
+        for (int d = 0; d < k; ++d) src[d] = present[d] ? shards[d] + r0 * blk : slot + size_t(d) * ss;
+        merge_jobs(k, blk, file_out, file_size, src.data(), all, r0, r1, jobs);
     };
+    if (missing.empty()) {  // nothing to rebuild: the merge alone (mergeShardsToFile)
+        std::vector<rsamd::CopyJob> jobs;
+        merge(0, rows_needed, nullptr, &jobs);
+        rsamd::CopyPool::get().copy(jobs);
+        *taken = true;
+        return RS_OK;
+    }
     auto io = [&](size_t j, std::vector<Xfer> *in, std::vector<Xfer> *out) {
-        const size_t r0 = mr.bounds[j], n = (mr.bounds[j + 1] - r0) * blk;
-        for (int sidx : surv) in->push_back({shards[sidx] + r0 * blk, mr.fstride + size_t(sidx) * mr.sstride, n});
-        for (int sidx : missing) out->push_back({shards[sidx] + r0 * blk, mr.fstride + size_t(sidx) * mr.sstride, n});
-        if (const size_t flen = flen_of(j)) out->push_back({file_out + r0 * kb, 0, flen});
+        const size_t r0 = cb[j], n = (cb[j + 1] - r0) * blk;
+        for (int sidx : surv) in->push_back({shards[sidx] + r0 * blk, size_t(sidx) * ss, n});
+        for (int sidx : missing) out->push_back({shards[sidx] + r0 * blk, size_t(sidx) * ss, n});
+    };
+    auto side = [&](size_t j, uint8_t *slot, std::vector<rsamd::CopyJob> *, std::vector<rsamd::CopyJob> *after) {
+        merge(cb[j], cb[j + 1], slot, after);
     };
     auto code = [&](size_t j, uint8_t *dev, hipStream_t st) -> int {
-        rsamd::FileDirect d = shape;
-        d.units = (mr.bounds[j + 1] - mr.bounds[j]) * blk / 8;
-        d.file_len = flen_of(j);
-        d.file_out = dev;
-        for (int i = 0; i < d.k; ++i) d.in[i] = dev + mr.fstride + size_t(surv[i]) * mr.sstride;
-        for (int q = 0; q < d.nout; ++q) d.out[q] = dev + mr.fstride + size_t(missing[q]) * mr.sstride;
-        RS_HIP(rsamd::launch_file_decode_direct(d, st));
-        return RS_OK;
+        return code_slots(plans, plan->in_idx(), plan->out_idx(), dev, ss, (cb[j + 1] - cb[j]) * blk, Mode::Code,
+                          nullptr, st);
     };
     *taken = true;
-    return run_mirrored(ctx, mr.bounds.size() - 1, mr.buf_bytes, io, code);
+    return run_mirrored(ctx, cb.size() - 1, ss * size_t(T), io, code, side);
 }
 
 // rs_file_decode when byteCntInShard is the whole shard: one pass per chunk
@@ -747,12 +816,12 @@ int file_decode_chunked(const Codec &c, uint8_t *const *shards, const int64_t *l
     }
     const size_t rows_needed = file_rows_needed(k, size_t(S), blk, missing, size_t(file_size));
     bool taken = false;
-    if (pinned) {  // direct path: the survivors, rebuilt shards and file coded in place
-        rc = file_decode_direct(c, shards, present, surv, missing, blk, file_out, size_t(file_size),
-                                rows_needed * blk, ctx, &taken);
+    if (pinned) {  // direct path: the absent shards rebuilt in place, the file merged on the host
+        rc = file_decode_pinned(c, shards, present, missing, blk, file_out, size_t(file_size), rows_needed, ctx,
+                                &taken);
     } else if (big && size_t(S) >= mirror_min_bytes()) {
-        rc = file_decode_mirrored(c, shards, size_t(S), present, surv, missing, blk, file_out, size_t(file_size),
-                                  rows_needed, ctx, &taken);
+        rc = file_decode_mirrored(c, shards, present, surv, missing, blk, file_out, size_t(file_size), rows_needed,
+                                  ctx, &taken);
     }
     if (rc || taken) return rc;
     return file_decode_staged(c, shards, size_t(S), present, surv, missing, blk, file_out, size_t(file_size), ctx,

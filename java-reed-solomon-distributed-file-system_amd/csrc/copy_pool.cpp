@@ -15,8 +15,9 @@ constexpr size_t kPiece = size_t(1) << 20;  // bytes per work item
 // Streaming (non-temporal) copy: the destination's lines are written without
 // being read first and without displacing the cache.  Every pool copy is
 // between caller memory and the pinned mirror, which the GPU reads (or has
-// written) across the link, so no CPU cache would keep either side.  The
-// sfence makes the stores globally visible before the piece is reported done.
+// written) across the link, so no CPU cache would keep either side.
+// copy_piece's sfence makes the stores globally visible before the piece is
+// reported done.
 __attribute__((target("avx2"))) void copy_stream(uint8_t *dst, const uint8_t *src, size_t n) {
     size_t head = (32 - reinterpret_cast<uintptr_t>(dst) % 32) % 32;
     if (head > n) head = n;
@@ -35,7 +36,6 @@ __attribute__((target("avx2"))) void copy_stream(uint8_t *dst, const uint8_t *sr
         _mm256_stream_si256(reinterpret_cast<__m256i *>(dst + 96), d);
     }
     std::memcpy(dst, src, n);
-    _mm_sfence();
 }
 
 // TUNING builds: RSAMD_COPY_NT=0 copies with memcpy instead (A/B).
@@ -47,11 +47,32 @@ bool use_stream() {
     return on;
 }
 
-void copy_piece(const CopyJob &j) {
-    if (j.n >= 4096 && use_stream())
-        copy_stream(static_cast<uint8_t *>(j.dst), static_cast<const uint8_t *>(j.src), j.n);
+// Rows shorter than this are copied with plain stores (TUNING builds:
+// RSAMD_COPY_NT_MIN): a streaming store that fills only part of a line
+// (a short row's head and tail) costs the line a read-modify-write.
+size_t stream_min() {
+    static const size_t v = tuning_size("RSAMD_COPY_NT_MIN", 256);
+    return v;
+}
+
+void copy_row(uint8_t *dst, const uint8_t *src, size_t n) {
+    if (!src)
+        std::memset(dst, 0, n);
+    else if (n >= stream_min() && use_stream())
+        copy_stream(dst, src, n);
     else
-        std::memcpy(j.dst, j.src, j.n);
+        std::memcpy(dst, src, n);
+}
+
+void copy_piece(const CopyJob &j) {
+    uint8_t *d = static_cast<uint8_t *>(j.dst), *d2 = static_cast<uint8_t *>(j.dst2);
+    const uint8_t *s = static_cast<const uint8_t *>(j.src);
+    for (size_t r = 0; r < j.rows; ++r) {
+        const uint8_t *src = s ? s + r * j.src_stride : nullptr;
+        copy_row(d + r * j.dst_stride, src, j.n);
+        if (d2) copy_row(d2 + r * j.dst2_stride, src, j.n);
+    }
+    _mm_sfence();
 }
 }  // namespace
 
@@ -88,13 +109,30 @@ void CopyPool::copy(const std::vector<CopyJob> &jobs) {
     size_t pending = 0;
     {
         std::lock_guard<std::mutex> lock(mu_);
-        for (const CopyJob &j : jobs)
-            for (size_t off = 0; off < j.n; off += kPiece) {
-                const size_t n = std::min(kPiece, j.n - off);
-                queue_.push_back({{static_cast<uint8_t *>(j.dst) + off, static_cast<const uint8_t *>(j.src) + off, n},
-                                  &pending});
+        for (const CopyJob &j : jobs) {
+            if (j.n == 0 || j.rows == 0) continue;
+            const uint8_t *src = static_cast<const uint8_t *>(j.src);
+            uint8_t *dst = static_cast<uint8_t *>(j.dst);
+            uint8_t *dst2 = static_cast<uint8_t *>(j.dst2);
+            if (j.rows == 1) {
+                for (size_t off = 0; off < j.n; off += kPiece) {
+                    CopyJob piece{dst + off, src ? src + off : nullptr, std::min(kPiece, j.n - off)};
+                    piece.dst2 = dst2 ? dst2 + off : nullptr;
+                    queue_.push_back({piece, &pending});
+                    ++pending;
+                }
+                continue;
+            }
+            // rows: pieces of about kPiece bytes of whole rows
+            const size_t per = std::max<size_t>(1, kPiece / j.n);
+            for (size_t r = 0; r < j.rows; r += per) {
+                CopyJob piece{dst + r * j.dst_stride, src ? src + r * j.src_stride : nullptr, j.n,
+                              std::min(per, j.rows - r), j.dst_stride, j.src_stride,
+                              dst2 ? dst2 + r * j.dst2_stride : nullptr, j.dst2_stride};
+                queue_.push_back({piece, &pending});
                 ++pending;
             }
+        }
     }
     if (pending == 0) return;
     work_cv_.notify_all();

@@ -18,10 +18,19 @@
 
 namespace rsamd {
 
+// n bytes from src to dst, or `rows` rows of n bytes each, row r at
+// src + r * src_stride and dst + r * dst_stride (block rows of a file and the
+// columns of a shard).  src == nullptr writes zeros (a file's padding).  With
+// dst2, every row also goes to dst2 + r * dst2_stride, from the same thread
+// right after the first (the second read hits the core's cache).
 struct CopyJob {
     void *dst;
     const void *src;
     size_t n;
+    size_t rows = 1;
+    size_t dst_stride = 0, src_stride = 0;
+    void *dst2 = nullptr;
+    size_t dst2_stride = 0;
 };
 
 class CopyPool {

@@ -539,12 +539,23 @@ int run_chunks_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinn
 // The copy batch issued before chunk j's launch holds chunk j's inputs and
 // the outputs of every earlier chunk whose kernels have completed; only the
 // chunk that last used slot b must have been drained before the slot is
-// refilled, so the CPU runs up to kMirrorBufs - 1 chunks ahead of the GPU.
+// refilled, so the CPU runs up to nbuf - 1 chunks ahead of the GPU.
 // ---------------------------------------------------------------------------
 namespace {
 // Pinned bytes per slot (TUNING builds: RSAMD_MIRROR_BYTES).
+// 48 MiB: a direct kernel over a chunk costs ~70 us on top of its bytes, so
+// larger chunks run closer to the link (4+2 x 64 MiB, no host copies: 0.893 of
+// the link bound at 24 MiB slots, 0.953 at 48 MiB; with the copies 0.853 /
+// 0.888; 16 MiB 0.832; profiles/r5/host_legs_r5d.txt, r5e).
 size_t mirror_slot_bytes() {
-    static const size_t v = rsamd::tuning_size("RSAMD_MIRROR_BYTES", size_t(24) << 20);
+    static const size_t v = rsamd::tuning_size("RSAMD_MIRROR_BYTES", size_t(48) << 20);
+    return v;
+}
+
+// Slots in use (<= kMirrorBufs; TUNING builds: RSAMD_MIRROR_NBUF).  Three let
+// the CPU copy one chunk in and drain one out while the GPU codes a third.
+int mirror_nbuf() {
+    static const int v = int(std::max<size_t>(2, std::min<size_t>(kMirrorBufs, rsamd::tuning_size("RSAMD_MIRROR_NBUF", 3))));
     return v;
 }
 
@@ -553,7 +564,19 @@ int mirror_buffer(ThreadCtx *ctx, size_t bytes) {
         if (ctx->mbuf) RS_HIP(hipHostFree(ctx->mbuf));
         ctx->mbuf = ctx->mbuf_dev = nullptr;
         ctx->mbuf_cap = 0;
-        RS_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->mbuf), bytes, hipHostMallocDefault));
+        // TUNING builds: RSAMD_MIRROR_ALLOC 0 = hipHostMallocDefault, 1 = non-coherent,
+        // 2 = coherent, 3 = mapped, pages placed by the
+        // calling thread's NUMA policy (A/B of where and how the slots are pinned).
+        // The default places the slots by the caller's policy: a service bound to
+        // the GPU's NUMA node (as bench.py binds its host legs) gets them there,
+        // 4+2 x 64 MiB pageable encode 0.853 -> 0.882 of the link bound, file
+        // encode 0.852 -> 0.861, file decode 0.733 -> 0.779 (profiles/r5/host_legs_r5e.txt).
+        const size_t how = rsamd::tuning_size("RSAMD_MIRROR_ALLOC", 3);
+        const unsigned flags = how == 1 ? (hipHostMallocMapped | hipHostMallocNonCoherent)
+                             : how == 2 ? (hipHostMallocMapped | hipHostMallocCoherent)
+                             : how == 3 ? (hipHostMallocMapped | hipHostMallocNumaUser)
+                                        : hipHostMallocDefault;
+        RS_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->mbuf), bytes, flags));
         ctx->mbuf_cap = bytes;
         RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->mbuf_dev), ctx->mbuf, 0));
     }
@@ -623,19 +646,19 @@ struct MirrorTrace {
 };
 
 int run_mirrored_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, const ChunkIo &io,
-                      const ChunkCode &code) {
-    const int nbuf = int(std::min<size_t>(kMirrorBufs, std::max<size_t>(1, n_chunks)));
+                      const ChunkCode &code, const ChunkSide &side) {
+    const int nbuf = int(std::min<size_t>(size_t(mirror_nbuf()), std::max<size_t>(1, n_chunks)));
     int rc = mirror_buffer(ctx, buf_bytes * size_t(nbuf));
     if (rc) return rc;
     MirrorTrace tr;
     tr.begin(ctx->stream, n_chunks);
-    // Chunks alternate between two streams, so one chunk's kernel starts while
-    // the previous one drains: a direct kernel over a few MiB spends ~60 us
-    // filling and emptying the link (4+2, 24 MiB slots: 338 us per 14.8 MiB
-    // chunk on one stream, 73 us of it fixed; tools/host_legs.py --trace,
-    // profiles/r5/).  stream2 first waits for what the caller queued on
-    // stream (the verify flag's reset).  TUNING builds: RSAMD_MIRROR_STREAMS=1.
-    const int nstreams = int(std::min<size_t>(2, std::max<size_t>(1, rsamd::tuning_size("RSAMD_MIRROR_STREAMS", 2))));
+    // One stream: chunks alternating over two streams (one chunk's kernel
+    // starting while the previous one drains) ran two kernels at a time at the
+    // same aggregate rate (0.831 / 0.805 of the link bound, 0.893 / 0.888 without
+    // host copies; profiles/r5/host_legs_r5d.txt, r5e).  TUNING builds:
+    // RSAMD_MIRROR_STREAMS=2; stream2 then first waits for what the caller
+    // queued on stream (the verify flag's reset).
+    const int nstreams = int(std::min<size_t>(2, std::max<size_t>(1, rsamd::tuning_size("RSAMD_MIRROR_STREAMS", 1))));
     hipStream_t ss[2] = {ctx->stream, ctx->stream2};
     if (nstreams > 1) {
         RS_HIP(hipEventRecord(ctx->ready, ctx->stream));
@@ -645,6 +668,7 @@ int run_mirrored_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, const C
     struct Pending {
         size_t j;
         std::vector<Xfer> out;
+        std::vector<rsamd::CopyJob> after;  // side copies behind the chunk's kernels
     };
     std::deque<Pending> pending;  // launched, slot not yet released: outputs not copied out (chunk order)
     std::vector<rsamd::CopyJob> jobs;
@@ -655,6 +679,7 @@ int run_mirrored_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, const C
         if (tr.path) tr.drained[batch].push_back(p.j);
         const uint8_t *slot = ctx->mbuf + (p.j % size_t(nbuf)) * buf_bytes;
         for (const Xfer &x : p.out) jobs.push_back({x.host, slot + x.off, x.n});
+        jobs.insert(jobs.end(), p.after.begin(), p.after.end());
         pending.pop_front();
     };
     auto done = [&](size_t j) {  // chunk j's kernels have completed
@@ -677,8 +702,13 @@ int run_mirrored_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, const C
         io(j, &in, &out);
         uint8_t *slot = ctx->mbuf + b * buf_bytes;
         for (const Xfer &x : in) jobs.push_back({slot + x.off, x.host, x.n});
+        std::vector<rsamd::CopyJob> after;
+        if (side) side(j, slot, &jobs, &after);
         if (tr.path) tr.cb[j] = tr.now();
-        pool.copy(jobs);
+        // TUNING builds: RSAMD_MIRROR_NOCOPY=1 skips the host copies (wrong
+        // results; the kernels' rate on the slots without CPU memory traffic)
+        static const bool nocopy = rsamd::tuning_size("RSAMD_MIRROR_NOCOPY", 0) != 0;
+        if (!nocopy) pool.copy(jobs);
         hipStream_t st = ss[j % size_t(nstreams)];
         if (tr.path) {
             tr.ce[j] = tr.now();
@@ -693,7 +723,7 @@ int run_mirrored_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, const C
         RS_HIP(hipEventRecord(ctx->mdone[b], st));
         // (also with no outputs -- verify: the slot's inputs may not be
         // refilled before the chunk's kernels have read them)
-        pending.push_back({j, out});
+        pending.push_back({j, out, std::move(after)});
     }
     batch = n_chunks - 1;
     while (!pending.empty()) {
@@ -701,7 +731,7 @@ int run_mirrored_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, const C
         RS_HIP(hipEventSynchronize(ctx->mdone[pending.front().j % size_t(nbuf)]));
         drain_front();
         while (!pending.empty() && done(pending.front().j)) drain_front();
-        pool.copy(jobs);
+        if (!rsamd::tuning_size("RSAMD_MIRROR_NOCOPY", 0)) pool.copy(jobs);
     }
     if (nstreams > 1) {  // stream carries on behind both (the caller reads the verify flag next)
         RS_HIP(hipEventRecord(ctx->ready, ctx->stream2));
@@ -748,8 +778,9 @@ std::vector<size_t> ramp_bounds(size_t total, size_t chunk, size_t granule) {
     return b;
 }
 
-int run_mirrored(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, const ChunkIo &io, const ChunkCode &code) {
-    const int rc = run_mirrored_impl(ctx, n_chunks, buf_bytes, io, code);
+int run_mirrored(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, const ChunkIo &io, const ChunkCode &code,
+                 const ChunkSide &side) {
+    const int rc = run_mirrored_impl(ctx, n_chunks, buf_bytes, io, code, side);
     if (rc) {  // nothing of the call left in flight
         (void)hipStreamSynchronize(ctx->stream);
         (void)hipStreamSynchronize(ctx->stream2);

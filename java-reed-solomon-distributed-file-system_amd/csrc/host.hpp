@@ -13,6 +13,8 @@
 #include <utility>
 #include <vector>
 
+#include "copy_pool.hpp"
+
 namespace rsamd {
 namespace host {
 
@@ -140,7 +142,14 @@ std::vector<size_t> ramp_bounds(size_t total, size_t chunk, size_t granule);
 // enqueues its kernels on s over the slot's device address.  Returns once
 // every output is in caller memory; on an error, once nothing of the call is
 // in flight.
-int run_mirrored(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, const ChunkIo &io, const ChunkCode &code);
+// side(j, slot, before, after), when given, adds host copies of chunk j that
+// are not slot transfers (a file split into its data shards, shards merged into
+// a file): `before` run in the batch with chunk j's inputs, `after` in the
+// batch that drains its outputs; slot is chunk j's slot (host address).
+using ChunkSide = std::function<void(size_t j, uint8_t *slot, std::vector<rsamd::CopyJob> *before,
+                                     std::vector<rsamd::CopyJob> *after)>;
+int run_mirrored(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, const ChunkIo &io, const ChunkCode &code,
+                 const ChunkSide &side = nullptr);
 
 }  // namespace host
 }  // namespace rsamd

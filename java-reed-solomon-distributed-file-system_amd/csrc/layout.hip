@@ -793,35 +793,22 @@ hipError_t launch_file_decode_fused(const FileGeom &g, const FileDecodePlan &p, 
 namespace {
 
 // ---------------------------------------------------------------------------
-// Direct file kernels: the host file API (rs_file_encode / rs_file_decode,
-// capi.cpp) on page-locked caller buffers, coded in place across the link
-// like kernels.hip gf_direct_kernel -- no staging buffers, no copy engine, H2D
-// and D2H at once.  One thread codes one 8-byte column unit of every shard
-// (block % 8 == 0, so a unit never crosses a block and its bytes of data shard
-// i are one 8-byte run of the file); runtime k, the output count a template
-// argument, so nothing is indexed dynamically in registers:
-//   encode: for each data shard i, load its file run (zero past file_len:
-//     the pad, ReedSolomonEncoder.java:76-85), store it to shard i and fold
-//     it into the M parity units, then store those.
-//   decode: for each survivor (the plan's first k present shards), load its
-//     unit, fold it into the E rebuilt units and, if it is a data shard, store
-//     it to its file run (trimmed at file_size); then store the rebuilt units
-//     to their shards (decodeMissing fills them in, ReedSolomonDecoder.java:36)
-//     and the rebuilt data units to the file.
+// Direct file encode kernel: rs_file_encode (capi.cpp file_encode_direct) on
+// page-locked caller buffers, coded in place across the link like kernels.hip
+// gf_direct_kernel -- no staging buffers, no copy engine, H2D and D2H at once.
+// One thread codes one 8-byte column unit of every shard (block % 8 == 0, so
+// a unit never crosses a block and its bytes of data shard i are one 8-byte
+// run of the file); runtime k, the output count a template argument, so
+// nothing is indexed dynamically in registers: for each data shard i, load its
+// file run (zero past file_len: the pad, ReedSolomonEncoder.java:76-85), store
+// it to shard i unless the host splits the data shards (out[i] null) and fold
+// it into the M parity units, then store those.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t load_run8(const uint8_t *p, uint64_t f, uint64_t len) {
     if (f + 8 <= len) return __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(RSAMD_G(p + f, 8)));
     uint64_t v = 0;
     for (uint64_t b = f; b < len && b < f + 8; ++b) v |= uint64_t(*RSAMD_G(p + b, 1)) << (8 * (b - f));
     return v;
-}
-
-__device__ __forceinline__ void store_run8(uint8_t *p, uint64_t f, uint64_t len, uint64_t v) {
-    if (f + 8 <= len) {
-        __builtin_nontemporal_store(v, reinterpret_cast<uint64_t *>(RSAMD_G(p + f, 8)));
-        return;
-    }
-    for (uint64_t b = f; b < len && b < f + 8; ++b) *RSAMD_G(p + b, 1) = uint8_t(v >> (8 * (b - f)));
 }
 
 __device__ __forceinline__ void fold_unit(const uint32_t *t, uint64_t x, uint32_t &lo, uint32_t &hi) {
@@ -850,7 +837,8 @@ __global__ void __launch_bounds__(kThreads) file_direct_encode_kernel(FileDirect
         uint32_t lo[M > 0 ? M : 1] = {}, hi[M > 0 ? M : 1] = {};
         for (int i = 0; i < a.k; ++i) {
             const uint64_t x = load_run8(a.file, (r * uint64_t(a.k) + uint64_t(i)) * a.block + w, a.file_len);
-            __builtin_nontemporal_store(x, reinterpret_cast<uint64_t *>(RSAMD_G(a.out[i] + c, 8)));
+            if (a.out[i])  // (null: the caller splits the data shards on the host, capi.cpp file_encode_direct)
+                __builtin_nontemporal_store(x, reinterpret_cast<uint64_t *>(RSAMD_G(a.out[i] + c, 8)));
 #pragma unroll
             for (int p = 0; p < M; ++p) fold_unit(a.tabs + (i * M + p) * 5, x, lo[p], hi[p]);
         }
@@ -859,106 +847,6 @@ __global__ void __launch_bounds__(kThreads) file_direct_encode_kernel(FileDirect
             __builtin_nontemporal_store(uint64_t(lo[p]) | (uint64_t(hi[p]) << 32),
                                         reinterpret_cast<uint64_t *>(RSAMD_G(a.out[a.k + p] + c, 8)));
     }
-}
-
-// One 8-byte unit of the decode: column c (w = c % block) of block row r.
-template <int E>
-__device__ __forceinline__ void decode_unit(const FileDirect &a, uint64_t c, uint64_t r, uint64_t w) {
-    const uint64_t row0 = r * uint64_t(a.k) * a.block + w;
-    uint32_t lo[E > 0 ? E : 1] = {}, hi[E > 0 ? E : 1] = {};
-    for (int i = 0; i < a.k; ++i) {
-        const uint64_t x = __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(RSAMD_G(a.in[i] + c, 8)));
-#pragma unroll
-        for (int p = 0; p < E; ++p) fold_unit(a.tabs + (i * E + p) * 5, x, lo[p], hi[p]);
-        const int d = a.in_shard[i];
-        if (d < a.k) store_run8(a.file_out, row0 + uint64_t(d) * a.block, a.file_len, x);
-    }
-#pragma unroll
-    for (int p = 0; p < E; ++p) {
-        const uint64_t y = uint64_t(lo[p]) | (uint64_t(hi[p]) << 32);
-        __builtin_nontemporal_store(y, reinterpret_cast<uint64_t *>(RSAMD_G(a.out[p] + c, 8)));
-        const int d = a.out_shard[p];
-        if (d < a.k) store_run8(a.file_out, row0 + uint64_t(d) * a.block, a.file_len, y);
-    }
-}
-
-// Units in rotated column order, as the encode.  One wave per block row (so
-// that a wave writes the row's k * block contiguous file bytes instead of k
-// runs of 512 bytes that start anywhere in a line) read 27.6-27.8 GiB/s
-// against 29.2-29.3 (direct_file_r3s2m.txt) and was dropped.
-template <int E>
-__global__ void __launch_bounds__(kThreads) file_direct_decode_kernel(FileDirect a) {
-    const uint64_t step = uint64_t(gridDim.x) * kThreads;
-    for (uint64_t u = uint64_t(blockIdx.x) * kThreads + threadIdx.x; u < a.units; u += step) {
-        const uint64_t c = rotated_column(u, a), r = c / a.block;
-        decode_unit<E>(a, c, r, c - r * a.block);
-    }
-}
-
-// Tiled form: a workgroup owns R whole block rows at a time.  Phase 1 codes
-// the tile's units and parks every data unit (survivor or rebuilt) at its
-// place in an LDS copy of the tile's file bytes, and the rebuilt units in LDS
-// copies of their shard runs; phase 2 writes each as ONE contiguous run of
-// 16-byte stores (8-byte at an 8-byte-aligned start), so every line but the
-// two at a run's ends is written whole, where the untiled form writes k runs
-// of 512 bytes per wave that start anywhere in a line.  LDS: (k + E) * R *
-// block bytes, R = the rows that fit kDecTileLds.  256 MiB file, {0,5}: 30.0 /
-// 30.1 GiB/s (numpy / pinned) against 29.2 / 29.1 untiled, 0.94 of the link
-// bound (tools/direct_file_probe.py --rows 0,1, profiles/r3/direct_file_r3s2p.txt).
-constexpr size_t kDecTileLds = 65536;
-
-__device__ __forceinline__ void lds_run_out(uint8_t *dst, const uint8_t *lds, uint64_t n) {
-    // dst and lds are 8-byte aligned; 16-byte vectors when both are 16-byte aligned.
-    uint64_t b = 0;
-    const bool v16 = reinterpret_cast<uintptr_t>(dst) % 16 == 0 && reinterpret_cast<uintptr_t>(lds) % 16 == 0;
-    if (v16) {
-        for (b = uint64_t(threadIdx.x) * 16; b + 16 <= n; b += uint64_t(kThreads) * 16)
-            __builtin_nontemporal_store(*reinterpret_cast<const u32x4 *>(lds + b), reinterpret_cast<u32x4 *>(RSAMD_G(dst + b, 16)));
-        b = n / 16 * 16;
-    }
-    for (uint64_t q = b + uint64_t(threadIdx.x) * 8; q + 8 <= n; q += uint64_t(kThreads) * 8)
-        __builtin_nontemporal_store(*reinterpret_cast<const uint64_t *>(lds + q), reinterpret_cast<uint64_t *>(RSAMD_G(dst + q, 8)));
-    for (uint64_t q = n / 8 * 8 + threadIdx.x; q < n; q += kThreads) *RSAMD_G(dst + q, 1) = lds[q];
-}
-
-template <int E>
-__global__ void __launch_bounds__(kThreads) file_direct_decode_tiled_kernel(FileDirect a, uint32_t R) {
-    extern __shared__ __align__(16) uint8_t lds[];
-    const uint64_t blk = a.block, k = uint64_t(a.k);
-    const uint64_t rows = a.units * 8 / blk, tiles = (rows + R - 1) / R;
-    const uint64_t fstride = uint64_t(R) * k * blk;  // LDS bytes of the file tile
-    for (uint64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
-        const uint64_t r0 = t * R, nrows = rows - r0 < R ? rows - r0 : R;
-        const uint64_t c0 = r0 * blk, ncols = nrows * blk, f0 = r0 * k * blk;
-        for (uint64_t cc = uint64_t(threadIdx.x) * 8; cc < ncols; cc += uint64_t(kThreads) * 8) {
-            const uint64_t rr = cc / blk, w = cc - rr * blk, frow = rr * k * blk + w;
-            uint32_t lo[E > 0 ? E : 1] = {}, hi[E > 0 ? E : 1] = {};
-            for (int i = 0; i < a.k; ++i) {
-                const uint64_t x = __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(RSAMD_G(a.in[i] + (c0 + cc), 8)));
-#pragma unroll
-                for (int p = 0; p < E; ++p) fold_unit(a.tabs + (i * E + p) * 5, x, lo[p], hi[p]);
-                const int d = a.in_shard[i];
-                if (d < a.k) *reinterpret_cast<uint64_t *>(lds + frow + uint64_t(d) * blk) = x;
-            }
-#pragma unroll
-            for (int p = 0; p < E; ++p) {
-                const uint64_t y = uint64_t(lo[p]) | (uint64_t(hi[p]) << 32);
-                *reinterpret_cast<uint64_t *>(lds + fstride + uint64_t(p) * R * blk + cc) = y;
-                const int d = a.out_shard[p];
-                if (d < a.k) *reinterpret_cast<uint64_t *>(lds + frow + uint64_t(d) * blk) = y;
-            }
-        }
-        __syncthreads();
-        if (f0 < a.file_len) lds_run_out(a.file_out + f0, lds, a.file_len - f0 < nrows * k * blk ? a.file_len - f0 : nrows * k * blk);
-#pragma unroll
-        for (int p = 0; p < E; ++p) lds_run_out(a.out[p] + c0, lds + fstride + uint64_t(p) * R * blk, ncols);
-        __syncthreads();
-    }
-}
-
-uint32_t dec_tile_rows(const FileDirect &d) {
-    const uint64_t per_row = uint64_t(d.k + d.nout) * d.block;
-    return uint32_t(std::min<uint64_t>(tuning_size("RSAMD_DEC_TILE_LDS", kDecTileLds) / per_row, d.units * 8 / d.block));
 }
 
 // 128 x 256 threads.  256 MiB file, 4+2, GiB/s (tools/direct_file_probe.py,
@@ -976,25 +864,20 @@ unsigned file_direct_grid(uint64_t units) {
 
 }  // namespace
 
-bool file_direct_ok(const FileDirect &d, bool encode) {
-    const int nptr = encode ? d.k + d.nout : d.nout;
+bool file_direct_ok(const FileDirect &d) {
     bool ok = d.k >= 1 && d.k <= kMaxDirectIn && d.nout >= 0 && d.nout <= kMaxOut && d.block >= 8 &&
-              d.block % 8 == 0 && d.units * 8 % d.block == 0 && aligned(encode ? d.file : d.file_out, 8);
-    for (int i = 0; ok && !encode && i < d.k; ++i) ok = aligned(d.in[i], 8);
-    for (int i = 0; ok && i < nptr; ++i) ok = aligned(d.out[i], 8);
+              d.block % 8 == 0 && d.units * 8 % d.block == 0 && aligned(d.file, 8);
+    for (int i = 0; ok && i < d.k + d.nout; ++i) ok = aligned(d.out[i], 8);
     return ok;
 }
 
 // The rotation of rotated_column: bytes from the first shard's address to the
 // widest power-of-two boundary (<= 4 KiB) every shard address agrees on.
-static uint64_t file_direct_rot(const FileDirect &d, bool encode) {
+static uint64_t file_direct_rot(const FileDirect &d) {
     std::vector<const void *> ptrs;
-    if (encode) {
-        for (int i = 0; i < d.k + d.nout; ++i) ptrs.push_back(d.out[i]);
-    } else {
-        for (int i = 0; i < d.k; ++i) ptrs.push_back(d.in[i]);
-        for (int i = 0; i < d.nout; ++i) ptrs.push_back(d.out[i]);
-    }
+    for (int i = 0; i < d.k + d.nout; ++i)
+        if (d.out[i]) ptrs.push_back(d.out[i]);
+    if (ptrs.empty()) return 0;
     for (uintptr_t A = 4096; A > 8; A >>= 1) {
         const uintptr_t r = reinterpret_cast<uintptr_t>(ptrs[0]) % A;
         bool same = true;
@@ -1005,10 +888,10 @@ static uint64_t file_direct_rot(const FileDirect &d, bool encode) {
 }
 
 hipError_t launch_file_encode_direct(const FileDirect &d0, hipStream_t s) {
-    if (!file_direct_ok(d0, true)) return hipErrorInvalidValue;
+    if (!file_direct_ok(d0)) return hipErrorInvalidValue;
     if (d0.units == 0) return hipSuccess;
     FileDirect d = d0;
-    d.rot = file_direct_rot(d, true);
+    d.rot = file_direct_rot(d);
     const dim3 grid(file_direct_grid(d.units));
     switch (d.nout) {
     case 0: hipLaunchKernelGGL((file_direct_encode_kernel<0>), grid, dim3(kThreads), 0, s, d); break;
@@ -1016,34 +899,6 @@ hipError_t launch_file_encode_direct(const FileDirect &d0, hipStream_t s) {
     case 2: hipLaunchKernelGGL((file_direct_encode_kernel<2>), grid, dim3(kThreads), 0, s, d); break;
     case 3: hipLaunchKernelGGL((file_direct_encode_kernel<3>), grid, dim3(kThreads), 0, s, d); break;
     default: hipLaunchKernelGGL((file_direct_encode_kernel<4>), grid, dim3(kThreads), 0, s, d); break;
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_file_decode_direct(const FileDirect &d0, hipStream_t s) {
-    if (!file_direct_ok(d0, false)) return hipErrorInvalidValue;
-    if (d0.units == 0) return hipSuccess;
-    FileDirect d = d0;
-    d.rot = file_direct_rot(d, false);
-    const dim3 grid(file_direct_grid(d.units));
-    const uint32_t R = dec_tile_rows(d);
-    if (R >= 1 && tuning_size("RSAMD_DEC_TILED", 1)) {
-        const size_t lds = size_t(d.k + d.nout) * R * d.block;
-        switch (d.nout) {
-        case 0: hipLaunchKernelGGL((file_direct_decode_tiled_kernel<0>), grid, dim3(kThreads), lds, s, d, R); break;
-        case 1: hipLaunchKernelGGL((file_direct_decode_tiled_kernel<1>), grid, dim3(kThreads), lds, s, d, R); break;
-        case 2: hipLaunchKernelGGL((file_direct_decode_tiled_kernel<2>), grid, dim3(kThreads), lds, s, d, R); break;
-        case 3: hipLaunchKernelGGL((file_direct_decode_tiled_kernel<3>), grid, dim3(kThreads), lds, s, d, R); break;
-        default: hipLaunchKernelGGL((file_direct_decode_tiled_kernel<4>), grid, dim3(kThreads), lds, s, d, R); break;
-        }
-        return hipGetLastError();
-    }
-    switch (d.nout) {
-    case 0: hipLaunchKernelGGL((file_direct_decode_kernel<0>), grid, dim3(kThreads), 0, s, d); break;
-    case 1: hipLaunchKernelGGL((file_direct_decode_kernel<1>), grid, dim3(kThreads), 0, s, d); break;
-    case 2: hipLaunchKernelGGL((file_direct_decode_kernel<2>), grid, dim3(kThreads), 0, s, d); break;
-    case 3: hipLaunchKernelGGL((file_direct_decode_kernel<3>), grid, dim3(kThreads), 0, s, d); break;
-    default: hipLaunchKernelGGL((file_direct_decode_kernel<4>), grid, dim3(kThreads), 0, s, d); break;
     }
     return hipGetLastError();
 }

@@ -42,32 +42,26 @@ bool file_fusable(const FileGeom &g, bool encode);
 hipError_t launch_file_encode_fused(const FileGeom &g, const DevPlan *parity0, hipStream_t s);
 // k survivors -> file (missing data shards computed in registers, nothing else written).
 hipError_t launch_file_decode_fused(const FileGeom &g, const FileDecodePlan &p, hipStream_t s);
-// The host file API's direct path: a file and shards in page-locked host
+// The host file encode's direct path: a file and shards in page-locked host
 // memory (device addresses from hipHostGetDevicePointer), coded in place
-// across the link by one kernel (layout.hip file_direct_*_kernel).  Every
-// pointer 8-byte aligned, block % 8 == 0, units = S / 8.
-//   encode: file (file_len unpadded bytes) -> out[0 .. k) data shards and
-//           out[k .. k + nout) parity shards; tabs = the encode plan's [k][nout][5]
-//   decode: in[0 .. k) survivors (shard in_shard[i]) -> out[0 .. nout) the
-//           absent shards (shard out_shard[p]) and file_out (file_len bytes,
-//           trimmed); tabs = the decode plan's [k][nout][5]
+// across the link by one kernel (layout.hip file_direct_encode_kernel).
+// Every pointer 8-byte aligned, block % 8 == 0, units = S / 8.  file
+// (file_len unpadded bytes) -> out[0 .. k) data shards (each may be null: the
+// caller splits them on the host) and out[k .. k + nout) parity shards; tabs =
+// the encode plan's [k][nout][5].  (The host file decode rebuilds shards with
+// the shard direct kernels and merges on the host: capi.cpp file_decode_pinned.)
 struct FileDirect {
     const uint8_t *file = nullptr;
-    uint8_t *file_out = nullptr;
     uint64_t file_len = 0;
     uint64_t units = 0;
     uint64_t block = 0;
-    const uint8_t *in[kMaxDirectIn] = {};
     uint8_t *out[kMaxDirectIn + kMaxOut] = {};
-    int32_t in_shard[kMaxDirectIn] = {};
-    int32_t out_shard[kMaxOut] = {};
     const uint32_t *tabs = nullptr;
     int k = 0, nout = 0;
-    uint64_t rot = 0;  // set by the launchers (layout.hip rotated_column)
+    uint64_t rot = 0;  // set by the launcher (layout.hip rotated_column)
 };
-bool file_direct_ok(const FileDirect &d, bool encode);
+bool file_direct_ok(const FileDirect &d);
 hipError_t launch_file_encode_direct(const FileDirect &d, hipStream_t s);
-hipError_t launch_file_decode_direct(const FileDirect &d, hipStream_t s);
 // Generic permutation copies (any k, block, alignment).
 hipError_t launch_split(const FileGeom &g, hipStream_t s);
 hipError_t launch_merge(const FileGeom &g, hipStream_t s);

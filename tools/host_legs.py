@@ -45,10 +45,19 @@ def child(trace):
             os.environ["RSAMD_TRACE"] = trace
         for _ in range(3):
             rs.encodeParity(sh, 0, n)
+        from rsamd.layout import file_encode_into, file_layout
+        data = rng.integers(0, 256, k * n, dtype=np.uint8)
+        _, S = file_layout(rs, len(data))
+        fsh = [np.zeros(S, np.uint8) for _ in range(k + m)]
+        for _ in range(2):
+            file_encode_into(rs, data, fsh)
         os.environ.pop("RSAMD_TRACE", None)
+        fref = c_ref.Codec(k, m).file_encode(data.tobytes(), 1000)
+        out["pageable_file_encode_vs_oracle"] = bool(np.array_equal(np.stack(fsh), fref))
         ref = [a.copy() for a in sh[:k]] + [np.zeros(n, np.uint8) for _ in range(m)]
         c_ref.Codec(k, m).encode_parity(ref, 0, n)
-        out["pageable_encode_vs_oracle"] = all(np.array_equal(a, b) for a, b in zip(sh, ref))
+        out["pageable_encode_vs_oracle"] = (all(np.array_equal(a, b) for a, b in zip(sh, ref))
+                                            if not os.environ.get("RSAMD_MIRROR_NOCOPY") else "skipped (NOCOPY)")
     out["numa"] = extra.get("host_legs_numa")
     out["link"] = link
     print(json.dumps(out), flush=True)
