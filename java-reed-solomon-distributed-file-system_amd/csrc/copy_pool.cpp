@@ -64,13 +64,73 @@ void copy_row(uint8_t *dst, const uint8_t *src, size_t n) {
         std::memcpy(dst, src, n);
 }
 
+// Destination bytes [x0, x0 + len) of a gather whose destination is `rows`
+// rows of n bytes back to back, row r's source at src + r * src_stride.
+void gather_plain(uint8_t *dst, const uint8_t *src, size_t n, size_t src_stride, size_t x0, size_t len) {
+    while (len) {
+        const size_t r = x0 / n, c = x0 % n, take = std::min(len, n - c);
+        std::memcpy(dst + x0, src + r * src_stride + c, take);
+        x0 += take;
+        len -= take;
+    }
+}
+
+// A gather into a contiguous destination (a file's block rows into one
+// shard's column run: rows of n >= 32 bytes, sources src_stride apart) as
+// whole 32-byte streaming stores along the destination.  Copying row by row
+// instead leaves each short row's first and last line partly written by
+// streaming stores, which costs those lines a read-modify-write.  A vector
+// that straddles two rows is assembled from both.
+__attribute__((target("avx2"))) void gather_stream(uint8_t *dst, const uint8_t *src, size_t n, size_t rows,
+                                                   size_t src_stride) {
+    const size_t total = n * rows;
+    size_t x = std::min(total, (32 - reinterpret_cast<uintptr_t>(dst) % 32) % 32);
+    gather_plain(dst, src, n, src_stride, 0, x);
+    size_t r = x / n, c = x % n;
+    const uint8_t *sp = src + r * src_stride + c;
+    for (; x + 32 <= total; x += 32) {
+        __m256i v;
+        if (c + 32 <= n) {
+            v = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(sp));
+            sp += 32;
+            c += 32;
+        } else {  // the vector's bytes end one row and start the next
+            alignas(32) uint8_t tmp[32];
+            const size_t a = n - c;
+            std::memcpy(tmp, sp, a);
+            ++r;
+            sp = src + r * src_stride;
+            std::memcpy(tmp + a, sp, 32 - a);
+            sp += 32 - a;
+            c = 32 - a;
+            v = _mm256_load_si256(reinterpret_cast<const __m256i *>(tmp));
+        }
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(dst + x), v);
+        if (c == n) {
+            ++r;
+            c = 0;
+            sp = src + r * src_stride;
+        }
+    }
+    gather_plain(dst, src, n, src_stride, x, total - x);
+}
+
 void copy_piece(const CopyJob &j) {
     uint8_t *d = static_cast<uint8_t *>(j.dst), *d2 = static_cast<uint8_t *>(j.dst2);
     const uint8_t *s = static_cast<const uint8_t *>(j.src);
-    for (size_t r = 0; r < j.rows; ++r) {
-        const uint8_t *src = s ? s + r * j.src_stride : nullptr;
-        copy_row(d + r * j.dst_stride, src, j.n);
-        if (d2) copy_row(d2 + r * j.dst2_stride, src, j.n);
+    // rows into a contiguous destination: along the destination
+    auto gathers = [&](size_t dst_stride) {
+        return s && j.rows > 1 && dst_stride == j.n && j.n >= 32 && use_stream() && !tuning_size("RSAMD_COPY_ROWWISE", 0);
+    };
+    if (gathers(j.dst_stride) && (!d2 || gathers(j.dst2_stride))) {
+        gather_stream(d, s, j.n, j.rows, j.src_stride);
+        if (d2) gather_stream(d2, s, j.n, j.rows, j.src_stride);  // the source again, from this core's cache
+    } else {
+        for (size_t r = 0; r < j.rows; ++r) {
+            const uint8_t *src = s ? s + r * j.src_stride : nullptr;
+            copy_row(d + r * j.dst_stride, src, j.n);
+            if (d2) copy_row(d2 + r * j.dst2_stride, src, j.n);
+        }
     }
     _mm_sfence();
 }
