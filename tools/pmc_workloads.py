@@ -12,6 +12,7 @@ Workloads (bench.py's configs):
   enc104p / dec104p   enc104 / dec104 with a 4 KiB pad between shards
   enc104     10+4 x 4 MiB x 128, encode                 alg 14 S B
   enc104k / enc104kg  10+4 x 4 MiB x 1024 encode, packed / granule layout (32 KiB)  alg 14 S B
+  enc104kc   enc104k on a pool from rs_dev_alloc (physically contiguous, as bench.py allocates)
   dec104     10+4 x 4 MiB x 128, decode {0,1,2,3}       alg 14 S B
   enc42_4k   4+2 x 4 KiB x 1 M, encode                  alg 6 S B
   maskbits   4+2 x 4 KiB x 1 M, per-stripe bitmasks      alg (4 * stripes with a loss + erased shards) S
@@ -85,11 +86,13 @@ def main():
             fn = lambda: rdev.encode(rs, buf.data_ptr(), lay, st)  # noqa: E731
             alg = (k + m) * S * B
             kernel = f"gf_vec_kernel<{k}, {m}, false>"
-    elif name in ("enc104k", "enc104kg"):
+    elif name in ("enc104k", "enc104kg", "enc104kc"):
         k, m, S, B = 10, 4, 4 << 20, 1024
         rs = rsamd.ReedSolomon.create(k, m)
-        lay = StripeLayout.packed(B, k + m, S) if name == "enc104k" else rdev.GranuleLayout.make(B, k + m, S)
-        buf = torch.empty(lay.nbytes, dtype=torch.uint8, device="cuda:0")
+        lay = rdev.GranuleLayout.make(B, k + m, S) if name == "enc104kg" else StripeLayout.packed(B, k + m, S)
+        # enc104kc: the pool as bench.py allocates it (rs_dev_alloc, one physically contiguous range)
+        buf = (rdev.DeviceBuffer(lay.nbytes, contiguous=True) if name == "enc104kc"
+               else torch.empty(lay.nbytes, dtype=torch.uint8, device="cuda:0"))
         rdev.fill_synthetic(buf.data_ptr(), k, lay, SEED, 0, st)
         fn = lambda: rdev.encode(rs, buf.data_ptr(), lay, st)  # noqa: E731
         alg = (k + m) * S * B

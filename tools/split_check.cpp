@@ -14,8 +14,11 @@
 //   * every locked range, rounded to pages as HostRegistration::lock rounds
 //     it, lies inside its own array;
 //   * the interior's file bytes are all real file bytes (no padding row).
-// Build: make -C tools/split_check (see tools/split_check.mk); prints one
-// line per geometry and exits 1 on the first violation.
+// Round 5 removed the path; this checker builds against the tree before the
+// removal (capi.cpp of commit 4f31d22: `git show 4f31d22:java-reed-solomon-
+// distributed-file-system_amd/csrc/capi.cpp`), linked with that tree's other
+// objects; it prints one line per geometry and exits 1 on any violation
+// (profiles/r5/split_check_r5.txt).
 #include "../java-reed-solomon-distributed-file-system_amd/csrc/capi.cpp"
 
 #include <cinttypes>
