@@ -176,9 +176,8 @@ void free_buffers(ThreadCtx *c) {
     if (c->plan) (void)hipFree(c->plan);
     if (c->file) (void)hipFree(c->file);
     if (c->zc) (void)hipHostFree(c->zc);
-    if (c->mbuf) (void)hipHostFree(c->mbuf);
-    c->mirror = c->stage = c->plan = c->file = c->zc = c->zc_dev = c->mbuf = c->mbuf_dev = nullptr;
-    c->mirror_cap = c->stage_cap = c->plan_cap = c->file_cap = c->zc_cap = c->mbuf_cap = 0;
+    c->mirror = c->stage = c->plan = c->file = c->zc = c->zc_dev = nullptr;
+    c->mirror_cap = c->stage_cap = c->plan_cap = c->file_cap = c->zc_cap = 0;
 }
 
 void release_all(std::map<int, ThreadCtx *> &ctx) {
@@ -199,8 +198,6 @@ void release_all(std::map<int, ThreadCtx *> &ctx) {
             if (c->loaded[b]) (void)hipEventDestroy(c->loaded[b]);
         }
         if (c->flag) (void)hipFree(c->flag);
-        for (hipEvent_t &ev : c->mdone)
-            if (ev) (void)hipEventDestroy(ev);
         for (MaskedSlot &sl : c->masked) {
             if (sl.done) (void)hipEventDestroy(sl.done);
             if (sl.uploaded) (void)hipEventDestroy(sl.uploaded);
@@ -532,10 +529,10 @@ int run_chunks_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinn
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// The mirrored pipeline (host.hpp).  Slot b of ctx->mbuf holds one chunk laid
-// out as the caller's code expects; a chunk's life is
+// The mirrored pipeline (host.hpp).  Slot b of the call's slot set holds one
+// chunk laid out as the caller's code expects; a chunk's life is
 //   copy-in (pool, caller -> slot) -> kernels over the slot's device address
-//   (ctx->stream, event mdone[b]) -> copy-out (pool, slot -> caller).
+//   (ctx->stream, event done[b]) -> copy-out (pool, slot -> caller).
 // The copy batch issued before chunk j's launch holds chunk j's inputs and
 // the outputs of every earlier chunk whose kernels have completed; only the
 // chunk that last used slot b must have been drained before the slot is
@@ -559,31 +556,99 @@ int mirror_nbuf() {
     return v;
 }
 
-int mirror_buffer(ThreadCtx *ctx, size_t bytes) {
-    if (ctx->mbuf_cap < bytes) {
-        if (ctx->mbuf) RS_HIP(hipHostFree(ctx->mbuf));
-        ctx->mbuf = ctx->mbuf_dev = nullptr;
-        ctx->mbuf_cap = 0;
+// The slots, shared by the process's threads: a call takes an idle set of
+// its device for its duration (or makes one), so the pinned memory follows the
+// number of concurrent large pageable calls, not the number of threads that
+// ever made one (a JVM's I/O pool); at most kIdleSets idle sets per device are
+// kept, the rest freed when returned.
+struct MirrorSet {
+    int dev = 0;
+    uint8_t *buf = nullptr, *dev_ptr = nullptr;  // host and device addresses of the slots
+    size_t cap = 0;
+    hipEvent_t done[kMirrorBufs] = {};  // slot b's kernels done (its outputs may be drained)
+};
+
+constexpr size_t kIdleSets = 4;
+
+struct MirrorPool {
+    std::mutex mu;
+    std::map<int, std::vector<MirrorSet *>> idle;  // device -> idle sets
+};
+
+MirrorPool &mirror_pool() {
+    static MirrorPool *p = new MirrorPool;  // never destroyed: no HIP calls at exit
+    return *p;
+}
+
+void free_set(MirrorSet *s) {
+    if (s->buf) (void)hipHostFree(s->buf);
+    for (hipEvent_t &ev : s->done)
+        if (ev) (void)hipEventDestroy(ev);
+    delete s;
+}
+
+// An idle set of the current device with at least `bytes` of slots (the
+// largest idle one, grown if needed), or a new one.
+int acquire_set(size_t bytes, MirrorSet **out) {
+    *out = nullptr;
+    int dev = 0;
+    RS_HIP(hipGetDevice(&dev));
+    MirrorSet *s = nullptr;
+    {
+        MirrorPool &p = mirror_pool();
+        std::lock_guard<std::mutex> lock(p.mu);
+        std::vector<MirrorSet *> &v = p.idle[dev];
+        if (!v.empty()) {
+            auto best = std::max_element(v.begin(), v.end(), [](MirrorSet *a, MirrorSet *b) { return a->cap < b->cap; });
+            s = *best;
+            v.erase(best);
+        }
+    }
+    if (!s) {
+        s = new MirrorSet;
+        s->dev = dev;
+    }
+    *out = s;  // (returned by release_set also on the error paths below)
+    if (s->cap < bytes) {
+        if (s->buf) RS_HIP(hipHostFree(s->buf));
+        s->buf = s->dev_ptr = nullptr;
+        s->cap = 0;
         // TUNING builds: RSAMD_MIRROR_ALLOC 0 = hipHostMallocDefault, 1 = non-coherent,
-        // 2 = coherent, 3 = mapped, pages placed by the
-        // calling thread's NUMA policy (A/B of where and how the slots are pinned).
-        // The default places the slots by the caller's policy: a service bound to
-        // the GPU's NUMA node (as bench.py binds its host legs) gets them there,
-        // 4+2 x 64 MiB pageable encode 0.853 -> 0.882 of the link bound, file
-        // encode 0.852 -> 0.861, file decode 0.733 -> 0.779 (profiles/r5/host_legs_r5e.txt).
+        // 2 = coherent, 3 = mapped, pages placed by the calling thread's NUMA policy
+        // (A/B of where and how the slots are pinned).  The default places the slots
+        // by the caller's policy: a service bound to the GPU's NUMA node (as bench.py
+        // binds its host legs) gets them there, 4+2 x 64 MiB pageable encode 0.853 ->
+        // 0.882 of the link bound, file encode 0.852 -> 0.861, file decode 0.733 ->
+        // 0.779 (profiles/r5/host_legs_r5e.txt).
         const size_t how = rsamd::tuning_size("RSAMD_MIRROR_ALLOC", 3);
         const unsigned flags = how == 1 ? (hipHostMallocMapped | hipHostMallocNonCoherent)
                              : how == 2 ? (hipHostMallocMapped | hipHostMallocCoherent)
                              : how == 3 ? (hipHostMallocMapped | hipHostMallocNumaUser)
                                         : hipHostMallocDefault;
-        RS_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->mbuf), bytes, flags));
-        ctx->mbuf_cap = bytes;
-        RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->mbuf_dev), ctx->mbuf, 0));
+        RS_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->buf), bytes, flags));
+        s->cap = bytes;
+        RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&s->dev_ptr), s->buf, 0));
     }
-    for (hipEvent_t &ev : ctx->mdone)
+    for (hipEvent_t &ev : s->done)
         if (!ev) RS_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    bounds::allow(ctx->mbuf_dev, ctx->mbuf_cap);
+    bounds::allow(s->dev_ptr, s->cap);
     return RS_OK;
+}
+
+// Back to the pool once nothing of the call uses it (the caller has
+// synchronised); beyond kIdleSets idle sets per device it is freed.
+void release_set(MirrorSet *s) {
+    if (!s) return;
+    {
+        MirrorPool &p = mirror_pool();
+        std::lock_guard<std::mutex> lock(p.mu);
+        std::vector<MirrorSet *> &v = p.idle[s->dev];
+        if (v.size() < kIdleSets || process_exiting()) {
+            v.push_back(s);
+            return;
+        }
+    }
+    free_set(s);
 }
 
 // TUNING builds: RSAMD_TRACE=<file> appends one JSON line per mirrored call
@@ -645,11 +710,9 @@ struct MirrorTrace {
     }
 };
 
-int run_mirrored_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, const ChunkIo &io,
-                      const ChunkCode &code, const ChunkSide &side) {
-    const int nbuf = int(std::min<size_t>(size_t(mirror_nbuf()), std::max<size_t>(1, n_chunks)));
-    int rc = mirror_buffer(ctx, buf_bytes * size_t(nbuf));
-    if (rc) return rc;
+int run_mirrored_impl(ThreadCtx *ctx, MirrorSet *ms, int nbuf, size_t n_chunks, size_t buf_bytes,
+                      const ChunkIo &io, const ChunkCode &code, const ChunkSide &side) {
+    int rc = RS_OK;
     MirrorTrace tr;
     tr.begin(ctx->stream, n_chunks);
     // One stream: chunks alternating over two streams (one chunk's kernel
@@ -677,13 +740,13 @@ int run_mirrored_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, const C
     auto drain_front = [&]() {
         const Pending &p = pending.front();
         if (tr.path) tr.drained[batch].push_back(p.j);
-        const uint8_t *slot = ctx->mbuf + (p.j % size_t(nbuf)) * buf_bytes;
+        const uint8_t *slot = ms->buf + (p.j % size_t(nbuf)) * buf_bytes;
         for (const Xfer &x : p.out) jobs.push_back({x.host, slot + x.off, x.n});
         jobs.insert(jobs.end(), p.after.begin(), p.after.end());
         pending.pop_front();
     };
     auto done = [&](size_t j) {  // chunk j's kernels have completed
-        const hipError_t e = hipEventQuery(ctx->mdone[j % size_t(nbuf)]);
+        const hipError_t e = hipEventQuery(ms->done[j % size_t(nbuf)]);
         if (e == hipErrorNotReady) (void)hipGetLastError();
         return e == hipSuccess;
     };
@@ -693,14 +756,14 @@ int run_mirrored_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, const C
         jobs.clear();
         // the slot's previous chunk first (waited for), then whatever else is done
         while (!pending.empty() && pending.front().j + size_t(nbuf) <= j) {
-            RS_HIP(hipEventSynchronize(ctx->mdone[pending.front().j % size_t(nbuf)]));
+            RS_HIP(hipEventSynchronize(ms->done[pending.front().j % size_t(nbuf)]));
             drain_front();
         }
         while (!pending.empty() && done(pending.front().j)) drain_front();
         in.clear();
         out.clear();
         io(j, &in, &out);
-        uint8_t *slot = ctx->mbuf + b * buf_bytes;
+        uint8_t *slot = ms->buf + b * buf_bytes;
         for (const Xfer &x : in) jobs.push_back({slot + x.off, x.host, x.n});
         std::vector<rsamd::CopyJob> after;
         if (side) side(j, slot, &jobs, &after);
@@ -714,13 +777,13 @@ int run_mirrored_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, const C
             tr.ce[j] = tr.now();
             (void)hipEventRecord(tr.ks[j], st);
         }
-        rc = code(j, ctx->mbuf_dev + b * buf_bytes, st);
+        rc = code(j, ms->dev_ptr + b * buf_bytes, st);
         if (rc) return rc;
         if (tr.path) {
             (void)hipEventRecord(tr.ke[j], st);
             tr.launched[j] = tr.now();
         }
-        RS_HIP(hipEventRecord(ctx->mdone[b], st));
+        RS_HIP(hipEventRecord(ms->done[b], st));
         // (also with no outputs -- verify: the slot's inputs may not be
         // refilled before the chunk's kernels have read them)
         pending.push_back({j, out, std::move(after)});
@@ -728,7 +791,7 @@ int run_mirrored_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, const C
     batch = n_chunks - 1;
     while (!pending.empty()) {
         jobs.clear();
-        RS_HIP(hipEventSynchronize(ctx->mdone[pending.front().j % size_t(nbuf)]));
+        RS_HIP(hipEventSynchronize(ms->done[pending.front().j % size_t(nbuf)]));
         drain_front();
         while (!pending.empty() && done(pending.front().j)) drain_front();
         if (!rsamd::tuning_size("RSAMD_MIRROR_NOCOPY", 0)) pool.copy(jobs);
@@ -780,11 +843,15 @@ std::vector<size_t> ramp_bounds(size_t total, size_t chunk, size_t granule) {
 
 int run_mirrored(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, const ChunkIo &io, const ChunkCode &code,
                  const ChunkSide &side) {
-    const int rc = run_mirrored_impl(ctx, n_chunks, buf_bytes, io, code, side);
-    if (rc) {  // nothing of the call left in flight
+    const int nbuf = int(std::min<size_t>(size_t(mirror_nbuf()), std::max<size_t>(1, n_chunks)));
+    MirrorSet *ms = nullptr;
+    int rc = acquire_set(buf_bytes * size_t(nbuf), &ms);
+    if (!rc) rc = run_mirrored_impl(ctx, ms, nbuf, n_chunks, buf_bytes, io, code, side);
+    if (rc) {  // nothing of the call left in flight before the slots go back
         (void)hipStreamSynchronize(ctx->stream);
         (void)hipStreamSynchronize(ctx->stream2);
     }
+    release_set(ms);
     return rc;
 }
 

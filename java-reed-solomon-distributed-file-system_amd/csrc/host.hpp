@@ -74,10 +74,6 @@ struct ThreadCtx {
     uint8_t *zc = nullptr;      // small calls: coherent, device-mapped host buffer the kernels use directly
     uint8_t *zc_dev = nullptr;  // its device address
     size_t zc_cap = 0;
-    uint8_t *mbuf = nullptr;      // run_mirrored: kMirrorBufs device-mapped pinned slots
-    uint8_t *mbuf_dev = nullptr;  // their device address
-    size_t mbuf_cap = 0;
-    hipEvent_t mdone[kMirrorBufs] = {};  // slot b's kernels done (its outputs may be drained)
     // rs_decode_batch_masked_dev: two staging slots used in turn, so a call's
     // host-side preparation overlaps the previous call's kernels.
     MaskedSlot masked[2];

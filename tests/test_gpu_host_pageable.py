@@ -104,3 +104,36 @@ def test_threads_check_the_same_shards(gpu, oracle_lib):
     for t in ts:
         t.join()
     assert not errors, errors
+
+
+def test_many_threads_borrow_slot_sets(gpu, oracle_lib):
+    """Eight threads at once, each encoding then decoding its own pageable
+    shards of a different size: more concurrent calls than the pool keeps idle
+    slot sets (host.cpp MirrorPool), every result exact, and again once the
+    pool has trimmed back."""
+    import rsamd
+    rs = rsamd.ReedSolomon.create(4, 2)
+    errors = []
+
+    def work(t):
+        try:
+            n = (1 << 20) * (t + 1) + 13 * t
+            rng = np.random.default_rng(100 + t)
+            sh = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(4)] + [np.zeros(n, np.uint8) for _ in range(2)]
+            ref = [a.copy() for a in sh]
+            oracle_lib.Codec(4, 2).encode_parity(ref, 0, n)
+            rs.encodeParity(sh, 0, n)
+            assert_same(sh, ref, f"thread {t} encode")
+            sh[t % 6][:] = 0
+            rs.decodeMissing(sh, [i != t % 6 for i in range(6)], 0, n)
+            assert_same(sh, ref, f"thread {t} decode")
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    for _ in range(2):
+        ts = [threading.Thread(target=work, args=(t,)) for t in range(8)]
+        for th in ts:
+            th.start()
+        for th in ts:
+            th.join()
+        assert not errors, errors
