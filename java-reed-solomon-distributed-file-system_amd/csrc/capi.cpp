@@ -467,29 +467,37 @@ FileChunks file_chunks(int k, int total, size_t S, size_t block, bool pinned) {
 // r is file bytes [(r k + i) blk, +blk), zeros past the file's end (the
 // padding).  Row r goes to dst[i] + r * blk and, with dst2, to dst2[i] +
 // (r - row2) * blk as well (one read, two writes).
+// Rows per block of the split / merge jobs: each block's jobs, one per shard,
+// are queued together, so the copy threads work on one ~1 MB stretch of the
+// file at a time and read it from DRAM once, in order (4 shards x 1000-B
+// blocks, split and tee: +10-25% over one job per shard on a CPU test box,
+// tests/native; TUNING builds: RSAMD_COPY_ROW_BLOCK, 0 = one block).
+size_t row_block() { return rsamd::tuning_size("RSAMD_COPY_ROW_BLOCK", 256); }
+
 void split_jobs(const uint8_t *file, size_t file_len, size_t blk, int k, uint8_t *const *dst, uint8_t *const *dst2,
                 size_t row2, size_t r0, size_t r1, std::vector<rsamd::CopyJob> *jobs) {
     const size_t kb = size_t(k) * blk;
     const size_t full = std::min(r1, std::max(r0, file_len / kb));  // rows wholly inside the file
-    for (int i = 0; i < k; ++i) {
-        uint8_t *a = dst[i] + r0 * blk, *b = dst2 ? dst2[i] + (r0 - row2) * blk : nullptr;  // row r0's blocks
-        if (full > r0) {
-            rsamd::CopyJob job{a, file + (r0 * size_t(k) + size_t(i)) * blk, blk, full - r0, blk, kb};
-            job.dst2 = b;
+    const size_t rb = row_block() ? row_block() : std::max<size_t>(1, r1 - r0);
+    for (size_t b0 = r0; b0 < full; b0 += rb) {
+        const size_t b1 = std::min(full, b0 + rb);
+        for (int i = 0; i < k; ++i) {
+            rsamd::CopyJob job{dst[i] + b0 * blk, file + (b0 * size_t(k) + size_t(i)) * blk, blk, b1 - b0, blk, kb};
+            job.dst2 = dst2 ? dst2[i] + (b0 - row2) * blk : nullptr;
             job.dst2_stride = blk;
             jobs->push_back(job);
         }
-        for (size_t r = full; r < r1; ++r) {  // the last row: the file's bytes, then the padding's zeros
+    }
+    for (size_t r = full; r < r1; ++r)  // the last row: the file's bytes, then the padding's zeros
+        for (int i = 0; i < k; ++i) {
             const size_t f0 = (r * size_t(k) + size_t(i)) * blk;
             const size_t have = f0 < file_len ? std::min(blk, file_len - f0) : 0;
-            for (uint8_t *d : {a, b}) {
+            for (uint8_t *d : {dst[i] + r * blk, dst2 ? dst2[i] + (r - row2) * blk : nullptr}) {
                 if (!d) continue;
-                d += (r - r0) * blk;
                 if (have) jobs->push_back({d, file + f0, have});
                 if (have < blk) jobs->push_back({d + have, nullptr, blk - have});
             }
         }
-    }
 }
 
 // ReedSolomonDecoder's merge and trim (ReedSolomonDecoder.java:62-66, 92-103)
@@ -499,18 +507,22 @@ void split_jobs(const uint8_t *file, size_t file_len, size_t blk, int k, uint8_t
 void merge_jobs(int k, size_t blk, uint8_t *file_out, size_t file_size, const uint8_t *const *src,
                 const std::vector<bool> &only, size_t r0, size_t r1, std::vector<rsamd::CopyJob> *jobs) {
     const size_t kb = size_t(k) * blk;
-    for (int d = 0; d < k; ++d) {
-        if (!only[d]) continue;
-        for (size_t r = r0; r < r1;) {
-            const size_t f0 = (r * size_t(k) + size_t(d)) * blk;
-            if (f0 >= file_size) break;
-            if (f0 + blk <= file_size) {  // whole blocks up to the first that crosses the file's end
-                const size_t last = std::min(r1, (file_size - size_t(d) * blk - blk) / kb + 1);
-                jobs->push_back({file_out + f0, src[d] + (r - r0) * blk, blk, last - r, kb, blk});
-                r = last;
-            } else {
-                jobs->push_back({file_out + f0, src[d] + (r - r0) * blk, file_size - f0});
-                ++r;
+    const size_t rb = row_block() ? row_block() : std::max<size_t>(1, r1 - r0);
+    for (size_t b0 = r0; b0 < r1; b0 += rb) {  // blocks of rows, every shard's jobs of a block together
+        const size_t b1 = std::min(r1, b0 + rb);
+        for (int d = 0; d < k; ++d) {
+            if (!only[d]) continue;
+            for (size_t r = b0; r < b1;) {
+                const size_t f0 = (r * size_t(k) + size_t(d)) * blk;
+                if (f0 >= file_size) break;
+                if (f0 + blk <= file_size) {  // whole blocks up to the first that crosses the file's end
+                    const size_t last = std::min(b1, (file_size - size_t(d) * blk - blk) / kb + 1);
+                    jobs->push_back({file_out + f0, src[d] + (r - r0) * blk, blk, last - r, kb, blk});
+                    r = last;
+                } else {
+                    jobs->push_back({file_out + f0, src[d] + (r - r0) * blk, file_size - f0});
+                    ++r;
+                }
             }
         }
     }
