@@ -68,12 +68,12 @@ def test_file_paths_random(gpu, oracle_lib, case):
 
 @pytest.mark.parametrize("case", range(10))
 def test_file_host_random_large(gpu, oracle_lib, case):
-    """Host file calls at sizes that take the direct path (shards of 256 KiB
-    and more): pageable file, shards and output, each a view at a random
-    offset (8-byte aligned, or not for one case in four: staged), so the
-    block rows inside whole pages are coded in place and the rows either side
-    staged (capi.cpp file_encode_interior / file_decode_interior); random k,
-    m, block and erasures, against the oracle."""
+    """Host file calls at sizes that take the mirrored pipeline (shards of
+    256 KiB and more): pageable file, shards and output, each a view at a
+    random offset (8-byte aligned, or not for one case in four), split and
+    merged on the host around the GPU's coding (capi.cpp file_encode_mirrored /
+    file_decode_mirrored); random k, m, block and erasures, against the
+    oracle."""
     from rsamd.layout import file_decode_into, file_encode_into, file_layout
     import rsamd
     rng = np.random.default_rng(9500 + case)
@@ -107,3 +107,47 @@ def test_file_host_random_large(gpu, oracle_lib, case):
     file_decode_into(rs, sh, [i not in miss for i in range(k + m)], S, out, block)
     assert_same([out], [f], (k, m, block, n, miss))
     assert_same(sh, ref, (k, m, block, n, miss))
+
+
+@pytest.mark.parametrize("case", range(8))
+def test_file_host_odd_blocks_pageable_and_pinned(gpu, oracle_lib, case):
+    """The host file calls with blocks that are not 8-byte multiples (999,
+    1001, 13, 4097) and files that end mid-row, on pageable arrays (the
+    mirrored pipeline) and on caller-pinned ones (the direct kernels plus the
+    host split / merge; odd blocks fall back to the staged pipeline there),
+    every erasure count up to m, against the oracle."""
+    import torch
+    from rsamd.layout import file_decode_into, file_encode_into, file_layout
+    import rsamd
+    rng = np.random.default_rng(9600 + case)
+    k, m = [(4, 2), (3, 2), (6, 3), (2, 1)][case % 4]
+    block = [999, 1001, 13, 4097][(case // 2) % 4]
+    pinned = case % 2 == 1
+    n = int(rng.integers(k * (300 << 10), k * (900 << 10)))
+    rs = rsamd.ReedSolomon.create(k, m)
+    oc = oracle_lib.Codec(k, m)
+    _, S = file_layout(rs, n, block)
+
+    def buf(size):
+        if pinned:
+            return torch.empty(size, dtype=torch.uint8, pin_memory=True).numpy()
+        o = int(rng.integers(0, 64))
+        return np.empty(size + o, np.uint8)[o:o + size]
+
+    f = buf(n)
+    f[:] = rng.integers(0, 256, n, dtype=np.uint8)
+    sh = [buf(S) for _ in range(k + m)]
+    for a in sh:
+        a[:] = 0xEE
+    file_encode_into(rs, f, sh, block)
+    ref = oc.file_encode(f.tobytes(), block)
+    assert_same(sh, ref, (k, m, block, n, pinned))
+    for e in range(m + 1):
+        miss = sorted(int(x) for x in rng.choice(k + m, e, replace=False)) if e else []
+        for j in miss:
+            sh[j][:] = 0
+        out = buf(n)
+        out[:] = 0x33
+        file_decode_into(rs, sh, [i not in miss for i in range(k + m)], S, out, block)
+        assert_same([out], [f], (k, m, block, n, miss, pinned))
+        assert_same(sh, ref, (k, m, block, n, miss, pinned))
