@@ -704,9 +704,13 @@ struct MirrorTrace {
             std::fprintf(f, "]}\n");
             std::fclose(f);
         }
-        for (hipEvent_t e : ks) (void)hipEventDestroy(e);
-        for (hipEvent_t e : ke) (void)hipEventDestroy(e);
-        (void)hipEventDestroy(ref);
+    }
+    ~MirrorTrace() {  // also when the call returned early with an error
+        for (hipEvent_t e : ks)
+            if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : ke)
+            if (e) (void)hipEventDestroy(e);
+        if (ref) (void)hipEventDestroy(ref);
     }
 };
 
@@ -728,6 +732,9 @@ int run_mirrored_impl(ThreadCtx *ctx, MirrorSet *ms, int nbuf, size_t n_chunks, 
         RS_HIP(hipStreamWaitEvent(ctx->stream2, ctx->ready, 0));
     }
     rsamd::CopyPool &pool = rsamd::CopyPool::get();
+    // TUNING builds: RSAMD_MIRROR_NOCOPY=1 skips the host copies (wrong
+    // results; the kernels' rate on the slots without CPU memory traffic)
+    const bool nocopy = rsamd::tuning_size("RSAMD_MIRROR_NOCOPY", 0) != 0;
     struct Pending {
         size_t j;
         std::vector<Xfer> out;
@@ -768,9 +775,6 @@ int run_mirrored_impl(ThreadCtx *ctx, MirrorSet *ms, int nbuf, size_t n_chunks, 
         std::vector<rsamd::CopyJob> after;
         if (side) side(j, slot, &jobs, &after);
         if (tr.path) tr.cb[j] = tr.now();
-        // TUNING builds: RSAMD_MIRROR_NOCOPY=1 skips the host copies (wrong
-        // results; the kernels' rate on the slots without CPU memory traffic)
-        static const bool nocopy = rsamd::tuning_size("RSAMD_MIRROR_NOCOPY", 0) != 0;
         if (!nocopy) pool.copy(jobs);
         hipStream_t st = ss[j % size_t(nstreams)];
         if (tr.path) {
@@ -794,7 +798,7 @@ int run_mirrored_impl(ThreadCtx *ctx, MirrorSet *ms, int nbuf, size_t n_chunks, 
         RS_HIP(hipEventSynchronize(ms->done[pending.front().j % size_t(nbuf)]));
         drain_front();
         while (!pending.empty() && done(pending.front().j)) drain_front();
-        if (!rsamd::tuning_size("RSAMD_MIRROR_NOCOPY", 0)) pool.copy(jobs);
+        if (!nocopy) pool.copy(jobs);
     }
     if (nstreams > 1) {  // stream carries on behind both (the caller reads the verify flag next)
         RS_HIP(hipEventRecord(ctx->ready, ctx->stream2));
