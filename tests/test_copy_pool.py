@@ -1,7 +1,8 @@
-"""The host copy pool (csrc/copy_pool.cpp) on the CPU: its streaming gather
-of strided rows into contiguous destinations, the tee to a second
-destination and zero fills, against plain copies (tests/native/
-copy_pool_check.cpp, compiled here with g++)."""
+"""The host side of the mirrored pipeline on the CPU: the copy pool's
+streaming gather of strided rows into contiguous destinations, the tee to a
+second destination and zero fills, against plain copies (tests/native/
+copy_pool_check.cpp, compiled here with g++); and the pipeline's chunking
+(tests/native/ramp_check.cpp, linked with the product library's objects)."""
 import os
 import subprocess
 
@@ -17,3 +18,21 @@ def test_copy_pool_gathers_and_tees(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:]
     assert "0 bad" in r.stdout
+
+
+def test_mirrored_chunking(tmp_path):
+    obj = os.path.join(ROOT, "java-reed-solomon-distributed-file-system_amd", "build")
+    objs = [os.path.join(obj, o) for o in ("host.o", "codec.o", "gf256.o", "copy_pool.o", "kernels.o", "layout.o")]
+    if not all(os.path.exists(o) for o in objs):
+        import pytest
+        pytest.skip("product objects not built (make -C java-...-amd/csrc)")
+    exe = str(tmp_path / "ramp_check")
+    cc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
+    subprocess.run([cc, "-O2", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-DRSAMD_TUNING_ENV=0", "-DRSAMD_BOUNDS=0",
+                    "-I", CSRC, "-c", os.path.join(ROOT, "tests", "native", "ramp_check.cpp"),
+                    "-o", str(tmp_path / "ramp_check.o")], check=True)
+    subprocess.run([cc, "--offload-arch=gfx950", str(tmp_path / "ramp_check.o")] + objs + ["-pthread", "-o", exe],
+                   check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:]
+    assert " 0 bad" in r.stdout
