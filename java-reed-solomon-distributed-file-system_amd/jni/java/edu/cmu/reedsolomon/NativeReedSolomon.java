@@ -50,6 +50,48 @@ public final class NativeReedSolomon implements AutoCloseable {
     }
 
     /**
+     * The padded shard length of a file (ReedSolomonEncoder.pad,
+     * ReedSolomonEncoder.java:76-85): the file padded with zeros to a multiple
+     * of dataShardCount * blockSize, divided by dataShardCount.
+     */
+    public int shardLengthForFile(int fileLength, int blockSize) {
+        if (blockSize < 1) throw new IllegalArgumentException("block size must be positive");
+        long mult = (long) dataShardCount * blockSize;
+        long padded = fileLength % mult == 0 ? fileLength : (fileLength / mult + 1) * mult;
+        return (int) (padded / dataShardCount);
+    }
+
+    /**
+     * ReedSolomonEncoder.encode() (ReedSolomonEncoder.java:56-74): pads the
+     * file, splits it into blockSize-byte blocks round-robin over the data
+     * shards (block b to shard b % k at (b / k) * blockSize) and encodes the
+     * parity.  The split runs in the native library, so only the file and the
+     * parity cross the link.  Returns the k + m shards.
+     */
+    public byte[][] encodeFile(byte[] fileData, int blockSize) {
+        byte[][] shards = new byte[getTotalShardCount()][shardLengthForFile(fileData.length, blockSize)];
+        nativeEncodeFile(handle, fileData, blockSize, shards);
+        return shards;
+    }
+
+    /** encodeFile into caller-allocated shards of at least shardLengthForFile bytes each. */
+    public void encodeFile(byte[] fileData, int blockSize, byte[][] shards) {
+        nativeEncodeFile(handle, fileData, blockSize, shards);
+    }
+
+    /**
+     * new ReedSolomonDecoder(shards, shardPresent, byteCntInShard, fileSize)
+     * (ReedSolomonDecoder.java:33-39, 62-66, 92-103): decodeMissing(shards,
+     * shardPresent, 0, byteCntInShard) in place, then the data shards merged
+     * and trimmed to fileSize.  Returns the file.
+     */
+    public byte[] decodeFile(byte[][] shards, boolean[] shardPresent, int byteCntInShard, int blockSize, int fileSize) {
+        byte[] fileData = new byte[fileSize];
+        nativeDecodeFile(handle, shards, shardPresent, byteCntInShard, blockSize, fileData, fileSize);
+        return fileData;
+    }
+
+    /**
      * Device-resident per-stripe recovery (rs_decode_batch_masked_bits_dev):
      * stripes [stripe][shard][shardStride] at device address devBase, one
      * uint32 presence bitmask per stripe at devBits (bit i = shard i present),
@@ -100,6 +142,9 @@ public final class NativeReedSolomon implements AutoCloseable {
     private static native void nativeEncodeParity(long h, byte[][] shards, int offset, int byteCount);
     private static native void nativeDecodeMissing(long h, byte[][] shards, boolean[] present, int offset, int byteCount);
     private static native boolean nativeIsParityCorrect(long h, byte[][] shards, int first, int byteCount, byte[] temp);
+    private static native void nativeEncodeFile(long h, byte[] file, int blockSize, byte[][] shards);
+    private static native void nativeDecodeFile(long h, byte[][] shards, boolean[] present, int byteCntInShard,
+                                                int blockSize, byte[] fileOut, int fileSize);
     private static native void nativeDecodeMaskedBitsDevice(long h, long devBase, long devBits, long nStripes,
                                                             long shardLen, long shardStride, long stripeStride,
                                                             long devBad, long stream);

@@ -109,6 +109,25 @@ JNIEXPORT jboolean JNICALL Java_edu_cmu_reedsolomon_NativeReedSolomon_nativeIsPa
                : JNI_FALSE;
 }
 
+/* ReedSolomonEncoder.encode() / new ReedSolomonDecoder(shards, shardPresent,
+ * byteCntInShard, fileSize) (ReedSolomonEncoder.java:56-85,
+ * ReedSolomonDecoder.java:33-39): the split / merge runs in librsamd, so only
+ * coded bytes cross the link (rs_file_encode / rs_file_decode). */
+JNIEXPORT void JNICALL Java_edu_cmu_reedsolomon_NativeReedSolomon_nativeEncodeFile(JNIEnv *env, jclass cls, jlong h,
+                                                                                   jbyteArray file, jint block,
+                                                                                   jobjectArray shards) {
+    jenv je;
+    rsj_file_encode(wrap(&je, env), rsj_librsamd_backend(), CODEC(h), file, block, shards);
+}
+
+JNIEXPORT void JNICALL Java_edu_cmu_reedsolomon_NativeReedSolomon_nativeDecodeFile(
+    JNIEnv *env, jclass cls, jlong h, jobjectArray shards, jbooleanArray present, jint byteCntInShard, jint block,
+    jbyteArray fileOut, jint fileSize) {
+    jenv je;
+    rsj_file_decode(wrap(&je, env), rsj_librsamd_backend(), CODEC(h), shards, present, byteCntInShard, block, fileOut,
+                    fileSize);
+}
+
 /* Frees this thread's device contexts (streams, staging buffers); for worker
  * threads a pool is about to retire. */
 JNIEXPORT void JNICALL Java_edu_cmu_reedsolomon_NativeReedSolomon_nativeThreadRelease(JNIEnv *env, jclass cls) {

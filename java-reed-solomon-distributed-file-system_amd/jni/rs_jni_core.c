@@ -3,12 +3,13 @@
  *
  * How a call reaches the GPU: the range [offset, offset + count) is coded in
  * slices of RSJ_SLICE_BYTES per shard.  For each slice every Java array is
- * pinned with GetPrimitiveArrayCritical, librsamd codes the slice straight
- * from/to the pinned memory (registering it for DMA), and the arrays are
- * released -- outputs with mode 0 (commit), inputs with JNI_ABORT -- before
- * the next slice.  So no critical region lasts longer than one slice (a few
- * ms), the garbage collector can run between slices, and no byte is copied on
- * the host.  Calls of more than one slice are validated up front (same checks
+ * pinned with GetPrimitiveArrayCritical, librsamd codes the slice from and to
+ * those arrays (pageable memory: its mirrored pipeline; the
+ * library never page-locks them), and the arrays are released -- outputs with
+ * mode 0 (commit), inputs with JNI_ABORT -- before the next slice.  So no
+ * critical region lasts longer than one slice (a few ms), the garbage
+ * collector can run between slices, and the shim itself copies no byte.
+ * Calls of more than one slice are validated up front (same checks
  * and order as the reference), so a later slice never fails after an earlier
  * one was written.  If the JVM answers a critical get with a COPY of the array
  * (isCopy), pinning per slice would copy whole arrays each time: the call then
@@ -32,7 +33,8 @@ const rsj_backend *rsj_librsamd_backend(void) {
     static const rsj_backend b = {rs_encode_parity,           rs_decode_missing,         rs_is_parity_correct,
                                   rs_code_some_shards,        rs_check_some_shards,      rs_check_buffers_and_sizes,
                                   rs_codec_total_shard_count, rs_codec_data_shard_count, rs_last_error_message,
-                                  rs_decode_groups_shard_major_dev};
+                                  rs_decode_groups_shard_major_dev, rs_file_layout,          rs_file_encode,
+                                  rs_file_decode};
     return &b;
 }
 
@@ -510,4 +512,204 @@ void rsj_recover_groups_shard_major(rsj_env *e, const rsj_backend *b, const rs_c
                                                 (void *)(uintptr_t)stream);
     free(flags);
     if (rc) throw_rc(e, b, rc);
+}
+
+/* ---- client file layout natives (ReedSolomonEncoder / ReedSolomonDecoder) ---- */
+
+typedef struct {
+    int op;                 /* OP_ENCODE or OP_DECODE */
+    int32_t block;
+    int64_t file_len;       /* encode: the file's length; decode: fileSize */
+    int32_t byte_cnt;       /* decode, whole call: byteCntInShard */
+    const uint8_t *present; /* decode */
+} file_op;
+
+/* The whole call: the arrays as Java holds them, every argument passed on, so
+ * the library makes every check itself. */
+static int file_whole(const rsj_backend *b, const rs_codec *c, const file_op *op, arrays *s, uint8_t *f) {
+    if (op->op == OP_ENCODE) return b->file_encode(c, f, op->file_len, op->block, s->ptr, s->n, s->len);
+    return b->file_decode(c, s->ptr, s->n, s->len, op->present, op->byte_cnt, op->block, f, op->file_len);
+}
+
+/* Block rows [r0, r1) of a sliced call: row r0 of every shard at sh[i], the
+ * file's row r0 at f (only the file's own bytes in those rows are read or
+ * written; NULL when the rows hold none). */
+static int file_rows(const rsj_backend *b, const rs_codec *c, const file_op *op, uint8_t *const *sh, int n,
+                     uint8_t *f, int64_t r0, int64_t r1) {
+    const int64_t kb = (int64_t)b->data_shards(c) * op->block, len = (r1 - r0) * op->block;
+    int64_t fl = op->file_len - r0 * kb;
+    if (fl < 0) fl = 0;
+    if (fl > (r1 - r0) * kb) fl = (r1 - r0) * kb;
+    int64_t lens[RSJ_MAX_SHARDS];
+    for (int i = 0; i < n; i++) lens[i] = len;
+    if (op->op == OP_ENCODE) return b->file_encode(c, fl ? f : NULL, fl, op->block, sh, n, lens);
+    return b->file_decode(c, sh, n, lens, op->present, (int32_t)len, op->block, fl ? f : NULL, fl);
+}
+
+static int64_t slice_rows(int32_t block) {
+    const int64_t per = (int64_t)RSJ_SLICE_BYTES / block;
+    return per > 0 ? per : 1;
+}
+
+/* Runs a file call over the shard arrays s (roles: what each is) and the file
+ * array f (f_role: read for encode, written for decode), whole when rows fit
+ * one slice, else slice by slice (pinned, or copied through C buffers when
+ * the JVM copies).  Leaves an exception pending on failure. */
+static void file_call(rsj_env *e, const rsj_backend *b, const rs_codec *c, const file_op *op, arrays *s,
+                      const int *role, rsj_obj f, int f_role, int64_t rows) {
+    const int64_t blk = op->block, kb = (int64_t)b->data_shards(c) * blk, per = slice_rows(op->block);
+    const int multi = rows > per;
+    int mode_of[RSJ_MAX_SHARDS];
+    for (int i = 0; i < s->n; i++) mode_of[i] = (role[i] & ROLE_OUT) ? RSJ_COMMIT : RSJ_ABORT;
+    const int f_mode = f_role == ROLE_OUT ? RSJ_COMMIT : RSJ_ABORT;
+    const int64_t f_len = e->array_length(e, f);
+    uint8_t *mem = NULL, *fbuf = NULL, *buf[RSJ_MAX_SHARDS], *at[RSJ_MAX_SHARDS];
+    int64_t r0 = 0;
+    do {  /* at least once: a call with no rows still gets the library's checks */
+        const int64_t r1 = !multi ? rows : (r0 + per < rows ? r0 + per : rows);
+        int rc;
+        if (!mem) {
+            int f_copy = 0;
+            const int copied = pin(e, s);
+            uint8_t *fp = e->critical_get(e, f, &f_copy);
+            if (!pinned_ok(s) || (!fp && f_len > 0)) {
+                if (fp) e->critical_release(e, f, fp, RSJ_ABORT);
+                unpin(e, s, NULL, RSJ_ABORT);
+                e->throw_new(e, "java/lang/OutOfMemoryError", "GetPrimitiveArrayCritical failed");
+                return;
+            }
+            if ((copied || f_copy) && multi && r0 == 0) {  /* the JVM copies: slice through C buffers instead */
+                e->critical_release(e, f, fp, RSJ_ABORT);
+                unpin(e, s, NULL, RSJ_ABORT);
+                mem = (uint8_t *)malloc((size_t)(s->n * per * blk + per * kb));
+                if (!mem) {
+                    e->throw_new(e, "java/lang/OutOfMemoryError", "slice buffers");
+                    return;
+                }
+                for (int i = 0; i < s->n; i++) buf[i] = mem + (size_t)(i * per * blk);
+                fbuf = mem + (size_t)(s->n * per * blk);
+                continue;
+            }
+            if (!multi) {
+                rc = file_whole(b, c, op, s, fp);
+            } else {
+                for (int i = 0; i < s->n; i++) at[i] = s->ptr[i] + r0 * blk;
+                rc = file_rows(b, c, op, at, s->n, (fp && r0 * kb < f_len) ? fp + r0 * kb : NULL, r0, r1);
+            }
+            if (fp) e->critical_release(e, f, fp, rc ? RSJ_ABORT : f_mode);
+            unpin(e, s, rc ? NULL : mode_of, RSJ_ABORT);  /* on an error nothing was written */
+        } else {
+            const int32_t len = (int32_t)((r1 - r0) * blk);
+            int64_t fl = op->file_len - r0 * kb;
+            if (fl < 0) fl = 0;
+            if (fl > (r1 - r0) * kb) fl = (r1 - r0) * kb;
+            for (int i = 0; i < s->n; i++)
+                if (role[i] & ROLE_IN) e->byte_region_get(e, s->arr[i], (int)(r0 * blk), len, buf[i]);
+            if (f_role == ROLE_IN && fl) e->byte_region_get(e, f, (int)(r0 * kb), (int)fl, fbuf);
+            if (e->exception_pending(e)) {
+                free(mem);
+                return;
+            }
+            rc = file_rows(b, c, op, buf, s->n, fbuf, r0, r1);
+            if (!rc) {
+                for (int i = 0; i < s->n; i++)
+                    if (role[i] & ROLE_OUT) e->byte_region_set(e, s->arr[i], (int)(r0 * blk), len, buf[i]);
+                if (f_role == ROLE_OUT && fl) e->byte_region_set(e, f, (int)(r0 * kb), (int)fl, fbuf);
+            }
+        }
+        if (rc) {
+            free(mem);
+            throw_rc(e, b, rc);
+            return;
+        }
+        if (mem && e->exception_pending(e)) {
+            free(mem);
+            return;
+        }
+        r0 = r1;
+    } while (r0 < rows);
+    free(mem);
+}
+
+void rsj_file_encode(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj file, int32_t block, rsj_obj shards) {
+    if (!file) {
+        e->throw_new(e, NPE, "fileData is null");
+        return;
+    }
+    arrays s;
+    if (take_shards(e, b, c, shards, &s)) return;
+    const int64_t flen = e->array_length(e, file);
+    int64_t padded = 0, S = 0;
+    int rc = b->file_layout(c, flen, block, &padded, &S);
+    if (rc) {
+        throw_rc(e, b, rc);
+        drop_refs(e, &s);
+        return;
+    }
+    /* checked up front (a sliced call hands the library slices only): every
+     * shard holds the padded length / k, as the reference allocates them
+     * (ReedSolomonEncoder.java:63) */
+    for (int i = 0; i < s.n; i++)
+        if (s.len[i] < S) {
+            char msg[96];
+            snprintf(msg, sizeof msg, "shard %d is shorter than %lld", i, (long long)S);
+            e->throw_new(e, IAE, msg);
+            drop_refs(e, &s);
+            return;
+        }
+    int role[RSJ_MAX_SHARDS];
+    for (int i = 0; i < s.n; i++) role[i] = ROLE_OUT; /* data shards from the file, parity coded */
+    const file_op op = {OP_ENCODE, block, flen, 0, NULL};
+    file_call(e, b, c, &op, &s, role, file, ROLE_IN, S / block);
+    drop_refs(e, &s);
+}
+
+void rsj_file_decode(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj shards, rsj_obj present,
+                     int32_t byte_cnt, int32_t block, rsj_obj file_out, int32_t file_size) {
+    arrays s;
+    if (take_shards(e, b, c, shards, &s)) return;
+    /* decodeMissing's checks first (ReedSolomonDecoder.java:36 -> ReedSolomon.java:185-194) */
+    int rc = b->check_buffers_and_sizes(c, s.n, s.len, 0, byte_cnt);
+    if (rc) {
+        throw_rc(e, b, rc);
+        drop_refs(e, &s);
+        return;
+    }
+    if (!present || !file_out) {
+        e->throw_new(e, NPE, present ? "fileOut is null" : "shardPresent is null");
+        drop_refs(e, &s);
+        return;
+    }
+    const int np = e->array_length(e, present);
+    if (np < s.n) {
+        throw_index(e, np, np);
+        drop_refs(e, &s);
+        return;
+    }
+    uint8_t pres[RSJ_MAX_SHARDS];
+    e->bool_region_get(e, present, 0, s.n, pres);
+    if (e->exception_pending(e)) {
+        drop_refs(e, &s);
+        return;
+    }
+    const int fo_len = e->array_length(e, file_out);
+    if (file_size > fo_len) { /* the trimmed copy would run past fileOut (ReedSolomonDecoder.java:63-64) */
+        throw_index(e, fo_len, fo_len);
+        drop_refs(e, &s);
+        return;
+    }
+    int role[RSJ_MAX_SHARDS], n_present = 0;
+    for (int i = 0; i < s.n; i++) {
+        role[i] = pres[i] ? ROLE_IN : ROLE_OUT;
+        n_present += pres[i] ? 1 : 0;
+    }
+    /* sliced only when every slice is a valid call on its own: whole shards
+     * decoded, whole block rows, enough survivors and a file that fits;
+     * anything else goes to the library whole, which reports it */
+    const int64_t L = s.n ? s.len[0] : 0, k = b->data_shards(c);
+    const int sliceable = block >= 1 && byte_cnt == L && L % block == 0 && n_present >= k && file_size >= 0 &&
+                          (int64_t)file_size <= k * L;
+    const file_op op = {OP_DECODE, block, file_size, byte_cnt, pres};
+    file_call(e, b, c, &op, &s, role, file_out, ROLE_OUT, sliceable ? L / block : 0);
+    drop_refs(e, &s);
 }

@@ -75,6 +75,10 @@ typedef struct rsj_backend {
     int (*data_shards)(const rs_codec *);
     const char *(*last_error)(void);
     int (*decode_groups_shard_major)(const rs_codec *, uint8_t *, size_t, size_t, size_t, const uint8_t *, void *);
+    int (*file_layout)(const rs_codec *, int64_t, int32_t, int64_t *, int64_t *);
+    int (*file_encode)(const rs_codec *, const uint8_t *, int64_t, int32_t, uint8_t *const *, int, const int64_t *);
+    int (*file_decode)(const rs_codec *, uint8_t *const *, int, const int64_t *, const uint8_t *, int32_t, int32_t,
+                       uint8_t *, int64_t);
 } rsj_backend;
 
 const rsj_backend *rsj_librsamd_backend(void);
@@ -102,6 +106,25 @@ int rsj_check_some_shards(rsj_env *e, const rsj_backend *b, rsj_obj rows, rsj_ob
 void rsj_recover_groups_shard_major(rsj_env *e, const rsj_backend *b, const rs_codec *c, int64_t dev_base,
                                     int64_t server_stride, int32_t chunk_len, int64_t n_groups, rsj_obj present,
                                     int64_t stream);
+
+/* The client's file layout (ReedSolomonEncoder.java:56-85,
+ * ReedSolomonDecoder.java:33-39, 62-66, 92-103) through rs_file_encode /
+ * rs_file_decode, so only coded bytes cross the link and the split / merge
+ * runs in the library instead of the Java per-byte loops.
+ *   encode: the whole byte[] file, padded with zeros to a multiple of
+ *     k * block, split into the data shards and the parity encoded, into
+ *     `shards` (k+m byte[] of at least padded / k bytes each; bytes past that
+ *     are untouched).
+ *   decode: decodeMissing(shards, present, 0, byte_cnt) in place, then the
+ *     data shards merged and trimmed to file_size into file_out (a byte[] of
+ *     at least file_size bytes).
+ * Large calls are coded in slices of whole block rows (RSJ_SLICE_BYTES of
+ * each shard, rounded down to the block), pinned slice by slice like the
+ * shard calls and validated up front, so a later slice never fails after an
+ * earlier one was written. */
+void rsj_file_encode(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj file, int32_t block, rsj_obj shards);
+void rsj_file_decode(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj shards, rsj_obj present,
+                     int32_t byte_cnt, int32_t block, rsj_obj file_out, int32_t file_size);
 
 #ifdef __cplusplus
 }

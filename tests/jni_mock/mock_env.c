@@ -265,10 +265,65 @@ static int fake_shard_major(const rs_codec *c, uint8_t *base, size_t stride, siz
     return SM.rc;
 }
 
+/* file layout: the real split / merge (ReedSolomonEncoder.java:62-74,
+ * ReedSolomonDecoder.java:92-103) around the fake parity and decode above;
+ * every call's file length and first shard length are recorded */
+static struct {
+    int calls;
+    int64_t file_len[64], shard_len[64];
+} FC;
+static void file_record(int64_t flen, int64_t slen) {
+    if (FC.calls < 64) {
+        FC.file_len[FC.calls] = flen;
+        FC.shard_len[FC.calls] = slen;
+    }
+    FC.calls++;
+}
+static int fake_file_encode(const rs_codec *c, const uint8_t *file, int64_t flen, int32_t block, uint8_t *const *sh,
+                            int n, const int64_t *lens) {
+    int64_t padded = 0, S = 0;
+    int rc = rs_file_layout(c, flen, block, &padded, &S);
+    if (rc) return rc;
+    file_record(flen, n ? lens[0] : -1);
+    const int k = rs_codec_data_shard_count(c);
+    for (int64_t blk = 0; blk < padded / block; blk++)
+        for (int32_t i = 0; i < block; i++) {
+            const int64_t at = blk * block + i;
+            sh[blk % k][(blk / k) * block + i] = at < flen ? file[at] : 0;
+        }
+    return fake_encode(c, sh, n, lens, 0, (int32_t)S);
+}
+static int fake_file_decode(const rs_codec *c, uint8_t *const *sh, int n, const int64_t *lens, const uint8_t *pres,
+                            int32_t cnt, int32_t block, uint8_t *out, int64_t fsize) {
+    int rc = rs_check_buffers_and_sizes(c, n, lens, 0, cnt);
+    if (rc) return rc;
+    const int k = rs_codec_data_shard_count(c);
+    int np = 0;
+    for (int i = 0; i < n; i++) np += pres[i] ? 1 : 0;
+    if (np < k) return RS_E_NOT_ENOUGH;
+    if (block < 1 || lens[0] % block || fsize < 0 || fsize > k * lens[0]) return RS_E_INVALID;
+    file_record(fsize, lens[0]);
+    if (np < n) fake_decode(c, sh, n, lens, pres, 0, cnt);
+    for (int64_t at = 0; at < fsize; at++) {
+        const int64_t blk = at / block;
+        out[at] = sh[blk % k][(blk / k) * block + at % block];
+    }
+    return 0;
+}
+void mock_file_record(int64_t *out, int max) {
+    out[0] = FC.calls;
+    for (int i = 0; i < FC.calls && i < 64 && 2 * i + 2 < max; i++) {
+        out[1 + 2 * i] = FC.file_len[i];
+        out[2 + 2 * i] = FC.shard_len[i];
+    }
+    FC.calls = 0;
+}
+
 static const rsj_backend FAKE = {fake_encode,       fake_decode,         fake_verify,
                                  fake_code,         fake_check,          rs_check_buffers_and_sizes,
                                  rs_codec_total_shard_count, fake_data_shards, rs_last_error_message,
-                                 fake_shard_major};
+                                 fake_shard_major,  rs_file_layout,      fake_file_encode,
+                                 fake_file_decode};
 
 static const rsj_backend *backend(int real) { return real ? rsj_librsamd_backend() : &FAKE; }
 
@@ -305,3 +360,10 @@ void mock_shard_major_record(uint64_t *out, uint8_t *flags, int nflags) {
     memcpy(flags, SM.flags, nflags < (int)sizeof SM.flags ? (size_t)nflags : sizeof SM.flags);
 }
 void mock_shard_major_rc(int rc) { SM.rc = rc; }
+void mock_file_encode(int real, const rs_codec *c, mobj *file, int32_t block, mobj *shards) {
+    rsj_file_encode(&ENV, backend(real), c, file, block, shards);
+}
+void mock_file_decode(int real, const rs_codec *c, mobj *shards, mobj *present, int32_t cnt, int32_t block, mobj *out,
+                      int32_t fsize) {
+    rsj_file_decode(&ENV, backend(real), c, shards, present, cnt, block, out, fsize);
+}

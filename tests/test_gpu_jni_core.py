@@ -116,3 +116,38 @@ def test_recover_groups_shard_major_through_shim(gpu, oracle_lib, native, jvm):
     assert np.array_equal(jvm.read(fl, N * T), flags.ravel())
     jvm.assert_clean()
     native.rs_codec_destroy(h)
+
+
+@pytest.mark.parametrize("k,m,block,flen", [(4, 2, 1000, 90999), (4, 2, 1000, 4000 * (SLICE // 1000 + 7) + 1234),
+                                            (10, 4, 1024, 3 * 1024 * 1024 + 5)])
+def test_file_encode_decode_through_shim(gpu, oracle_lib, native, jvm, k, m, block, flen):
+    """NativeReedSolomon.encodeFile / decodeFile's marshalling over
+    rs_file_encode / rs_file_decode: the Java file in, the k+m shards out as
+    the oracle's pad + split + encode writes them (ReedSolomonEncoder.java:
+    56-85); then {0, k+m-1} erased, the shards rebuilt in place and the file
+    back trimmed (ReedSolomonDecoder.java:33-39, 92-103).  The second case
+    is more than one slice of block rows per shard."""
+    h = C.c_void_p()
+    assert native.rs_codec_create(k, m, C.byref(h)) == 0
+    try:
+        data = np.random.default_rng(flen).integers(0, 256, flen, dtype=np.uint8)
+        ref = oracle_lib.Codec(k, m).file_encode(data.tobytes(), block)
+        S = ref.shape[1]
+        arrs = [jvm.bytes(np.full(S, 0xA5, np.uint8)) for _ in range(k + m)]
+        jvm.lib.mock_file_encode(1, h, jvm.bytes(data), block, jvm.objects(arrs))
+        assert jvm.exception() == ("", "")
+        for i in range(k + m):
+            assert np.array_equal(jvm.read(arrs[i], S), ref[i]), i
+        jvm.assert_clean()
+        present = [i not in (0, k + m - 1) for i in range(k + m)]
+        for i in (0, k + m - 1):
+            arrs[i] = jvm.bytes(np.zeros(S, np.uint8))
+        out = jvm.bytes(np.full(flen, 0x11, np.uint8))
+        jvm.lib.mock_file_decode(1, h, jvm.objects(arrs), jvm.bools(present), S, block, out, flen)
+        assert jvm.exception() == ("", "")
+        assert np.array_equal(jvm.read(out, flen), data)
+        for i in range(k + m):
+            assert np.array_equal(jvm.read(arrs[i], S), ref[i]), i
+        jvm.assert_clean()
+    finally:
+        native.rs_codec_destroy(h)

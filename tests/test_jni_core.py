@@ -55,6 +55,9 @@ def build_mock():
          [C.c_int, P, C.c_int64, C.c_int64, C.c_int32, C.c_int64, P, C.c_int64]),
         ("mock_shard_major_record", None, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint8), C.c_int]),
         ("mock_shard_major_rc", None, [C.c_int]),
+        ("mock_file_encode", None, [C.c_int, P, P, C.c_int32, P]),
+        ("mock_file_decode", None, [C.c_int, P, P, P, C.c_int32, C.c_int32, P, C.c_int32]),
+        ("mock_file_record", None, [C.POINTER(C.c_int64), C.c_int]),
     ]:
         fn = getattr(lib, name)
         fn.restype, fn.argtypes = res, args
@@ -441,4 +444,161 @@ def test_shard_major_real_backend_rejects_before_any_work(jvm, codec42):
     flags[1, :3] = 0
     jvm.lib.mock_recover_groups_shard_major(1, codec42, 1 << 20, 3000, 1000, 3, jvm.bytes(flags.ravel()), 0)
     assert jvm.exception() == (IAE, "Not enough shards present")
+    jvm.assert_clean()
+
+
+# ---- the client's file layout: rsj_file_encode / rsj_file_decode ----
+
+def file_calls(jvm):
+    """(file length, shard length) of every backend file call since the last read."""
+    rec = (C.c_int64 * 129)()
+    jvm.lib.mock_file_record(rec, 129)
+    return [(rec[1 + 2 * i], rec[2 + 2 * i]) for i in range(min(rec[0], 64))]
+
+
+def split_file(data, k, m, block):
+    """ReedSolomonEncoder.pad + splitFileToShards (ReedSolomonEncoder.java:62-85), numpy."""
+    kb = k * block
+    padded = len(data) if len(data) % kb == 0 else (len(data) // kb + 1) * kb
+    buf = np.zeros(padded, np.uint8)
+    buf[:len(data)] = data
+    rows = buf.reshape(-1, k, block)
+    return [np.ascontiguousarray(rows[:, i, :]).ravel() for i in range(k)] + [np.zeros(padded // k, np.uint8)
+                                                                             for _ in range(m)]
+
+
+def merge_file(shards, k, block, size):
+    """mergeShardsToFile + trimPadding (ReedSolomonDecoder.java:62-66, 92-103), numpy."""
+    S = len(shards[0])
+    return np.stack([s.reshape(-1, block) for s in shards[:k]], axis=1).ravel()[:size] if S else np.zeros(0, np.uint8)
+
+
+@pytest.fixture(scope="module")
+def codec21(native):
+    h = C.c_void_p()
+    assert native.rs_codec_create(2, 1, C.byref(h)) == 0
+    yield h
+    native.rs_codec_destroy(h)
+
+
+FILE_CASES = [(4, 2, 1000, 90999, 0), (4, 2, 1000, 92000, 0), (4, 2, 1000, 0, 0), (4, 2, 8, 4001, 1),
+              (2, 1, 4096, 2 * SLICE + 3 * 4096 * 2 + 77, 0), (2, 1, 4096, 2 * SLICE + 3 * 4096 * 2 + 77, 1),
+              (2, 1, 3000, 4 * SLICE + 5, 0)]
+
+
+@pytest.mark.parametrize("k,m,block,flen,copy", FILE_CASES)
+def test_file_encode_marshalling(jvm, codec42, codec21, k, m, block, flen, copy):
+    """The whole file in, every shard out (data split + parity), committed;
+    a file of more than one slice of block rows per shard goes to the library
+    in slices of whole rows, the last one holding the ragged end."""
+    codec = codec42 if k == 4 else codec21
+    data = np.random.default_rng(flen).integers(0, 256, flen, dtype=np.uint8)
+    want = split_file(data, k, m, block)
+    S = len(want[0])
+    want = fake_parity(want, k, m, 0, S)
+    arrs = [jvm.bytes(np.full(S, 0xC3, np.uint8)) for _ in range(k + m)]
+    jvm.lib.mock_force_copy(copy)
+    jvm.lib.mock_file_encode(0, codec, jvm.bytes(data), block, jvm.objects(arrs))
+    jvm.lib.mock_force_copy(0)
+    assert jvm.exception() == ("", "")
+    for i in range(k + m):
+        assert np.array_equal(jvm.read(arrs[i], S), want[i]), i
+    st = jvm.assert_clean()
+    rows, per = S // block, max(1, SLICE // block)
+    calls = file_calls(jvm)
+    if rows <= per:
+        assert calls == [(flen, S)]  # one call, with the arrays' own lengths
+    else:
+        n = -(-rows // per)
+        assert [c[1] for c in calls] == [per * block] * (n - 1) + [(rows - (n - 1) * per) * block]
+        assert sum(c[0] for c in calls) == flen
+        if copy:
+            assert st["bytes_in"] == flen and st["bytes_out"] == (k + m) * S
+        else:
+            assert st["critical_gets"] == (k + m + 1) * n and st["commits"] == (k + m) * n
+            assert st["bytes_in"] == 0 and st["bytes_out"] == 0
+
+
+@pytest.mark.parametrize("k,m,block,flen,copy", FILE_CASES)
+def test_file_decode_marshalling(jvm, codec42, codec21, k, m, block, flen, copy):
+    """Survivors in, the absent shards rebuilt in place and the trimmed file
+    out, sliced like the encode; only the rebuilt shards and the file are
+    committed."""
+    codec = codec42 if k == 4 else codec21
+    data = np.random.default_rng(flen + 1).integers(0, 256, flen, dtype=np.uint8)
+    shards = split_file(data, k, m, block)
+    S = len(shards[0])
+    shards = fake_parity(shards, k, m, 0, S)
+    present = [i != 0 for i in range(k + m)]
+    want = fake_decode(shards, present, 0, S)
+    arrs = [jvm.bytes(shards[i] if present[i] else np.zeros(S, np.uint8)) for i in range(k + m)]
+    out = jvm.bytes(np.full(flen + 3, 0x77, np.uint8))
+    jvm.lib.mock_force_copy(copy)
+    jvm.lib.mock_file_decode(0, codec, jvm.objects(arrs), jvm.bools(present), S, block, out, flen)
+    jvm.lib.mock_force_copy(0)
+    assert jvm.exception() == ("", "")
+    for i in range(k + m):
+        assert np.array_equal(jvm.read(arrs[i], S), want[i]), i
+    got = jvm.read(out, flen + 3)
+    assert np.array_equal(got[:flen], merge_file(want, k, block, flen)) and (got[flen:] == 0x77).all()
+    st = jvm.assert_clean()
+    rows, per = S // block, max(1, SLICE // block)
+    calls = file_calls(jvm)
+    if rows > per:
+        n = -(-rows // per)
+        assert len(calls) == n and sum(c[0] for c in calls) == flen
+        if copy:
+            assert st["bytes_in"] == (k + m - 1) * S + k + m and st["bytes_out"] == S + flen
+        else:
+            assert st["commits"] == 2 * n and st["aborts"] == (k + m - 1) * n
+
+
+def test_file_argument_errors(jvm, codec42):
+    """The library's own checks and texts (real backend; none needs a device)
+    and the shim's: a null file is NullPointerException, a fileOut shorter than
+    fileSize ArrayIndexOutOfBoundsException, and nothing is written."""
+    def enc(file, block, arrs):
+        jvm.lib.mock_reset()
+        jvm.lib.mock_file_encode(1, codec42, file, block, jvm.objects(arrs))
+        jvm.assert_clean()
+        return jvm.exception()
+
+    data = jvm.bytes(np.arange(9000) % 251)
+    full = [jvm.bytes(np.zeros(3000, np.uint8)) for _ in range(6)]
+    assert enc(None, 1000, full)[0] == NPE
+    assert enc(data, 1000, full[:5]) == (IAE, "wrong number of shards: 5")
+    assert enc(data, 0, full) == (IAE, "block size must be positive")
+    short = full[:5] + [jvm.bytes(np.zeros(2999, np.uint8))]
+    assert enc(data, 1000, short) == (IAE, "shard 5 is shorter than 3000")
+    assert all((jvm.read(a, 3000) == 0).all() for a in full)
+
+    def dec(arrs, present, cnt, block, out, size, real=1):
+        jvm.lib.mock_reset()
+        jvm.lib.mock_file_decode(real, codec42, jvm.objects(arrs), present, cnt, block, out, size)
+        jvm.assert_clean()
+        return jvm.exception()
+
+    out = jvm.bytes(np.zeros(12000, np.uint8))
+    ok = jvm.bools([True] * 6)
+    assert dec(full, ok, 3001, 1000, out, 9000) == (IAE, "buffers to small: 30010")
+    assert dec(full, None, 3000, 1000, out, 9000)[0] == NPE
+    assert dec(full, ok, 3000, 1000, None, 9000)[0] == NPE
+    assert dec(full, jvm.bools([True] * 5), 3000, 1000, out, 9000) == (AIOOBE, "Index 5 out of bounds for length 5")
+    assert dec(full, ok, 3000, 1000, jvm.bytes(np.zeros(8999, np.uint8)), 9000) == (
+        AIOOBE, "Index 8999 out of bounds for length 8999")
+    assert dec(full, jvm.bools([False, False, False, True, True, True]), 3000, 1000, out, 9000) == (
+        IAE, "Not enough shards present")
+    assert dec(full, ok, 3000, 1000, out, 12001)[0] == AIOOBE  # fileOut holds 12000
+    assert dec(full, ok, 3000, 1000, jvm.bytes(np.zeros(12001, np.uint8)), 12001) == (
+        IAE, "file size exceeds k * shard length")
+    assert (jvm.read(out, 12000) == 0).all()
+
+
+def test_file_real_backend_without_gpu_throws_illegal_state(jvm, codec42, native):
+    if native.rs_device_count() > 0:
+        pytest.skip("a GPU is visible: tests/test_gpu_jni_core.py covers the real backend")
+    arrs = [jvm.bytes(np.zeros(1000, np.uint8)) for _ in range(6)]
+    jvm.lib.mock_file_encode(1, codec42, jvm.bytes(np.ones(4000, np.uint8)), 1000, jvm.objects(arrs))
+    assert jvm.exception()[0] == ISE
+    assert all((jvm.read(a, 1000) == 0).all() for a in arrs)
     jvm.assert_clean()
