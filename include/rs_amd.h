@@ -64,8 +64,9 @@ typedef struct rs_codec rs_codec;
  *   3: rs_granule_copy_shard takes n_stripes after granule (round 3).
  *   4: rs_abi_version (this), rs_shard_stride_recommended.
  *   5: rs_set_host_register and rs_host_registry_state removed: the library
- *      no longer page-locks caller memory (round 5). */
-#define RS_AMD_ABI_VERSION 5
+ *      no longer page-locks caller memory (round 5).
+ *   6: rs_host_alloc / rs_host_free (caller-owned pinned buffers). */
+#define RS_AMD_ABI_VERSION 6
 RS_API int rs_abi_version(void);
 
 /* ---------------------------------------------------------------------------
@@ -352,6 +353,19 @@ RS_API int rs_file_decode_dev(const rs_codec *codec, uint8_t *dev_shards, size_t
  * ------------------------------------------------------------------------- */
 RS_API int rs_dev_alloc(void **out, size_t bytes, int contiguous, int *got_contiguous);
 RS_API int rs_dev_free(void *ptr);
+
+/* ---------------------------------------------------------------------------
+ * Pinned host memory for callers that can keep their shards and files in it
+ * (no Java counterpart; a JVM reaches it as direct ByteBuffers,
+ * NativeReedSolomon.allocatePinned).  Page-locked, mapped for the device,
+ * pages placed by the calling thread's NUMA policy.  Host calls on arrays in
+ * it are coded in place across the link with no host copies (DESIGN.md 5.2:
+ * 1.00 of the link bound for 4+2 x 64 MiB encodeParity, against 0.86-0.90
+ * for pageable arrays).  Free with rs_host_free.  RS_E_NO_DEVICE without a
+ * GPU, RS_E_HIP when the allocation fails.
+ * ------------------------------------------------------------------------- */
+RS_API int rs_host_alloc(void **out, size_t bytes);
+RS_API int rs_host_free(void *ptr);
 
 /* ---------------------------------------------------------------------------
  * Benchmark/test support (not part of the reference API).

@@ -1526,6 +1526,23 @@ int rs_dev_free(void *ptr) {
     return RS_OK;
 }
 
+// Caller-owned pinned buffers: the same flags as the mirror slots (mapped,
+// pages placed by the calling thread's NUMA policy), so shards the caller
+// keeps here take the in-place direct path (all_pinned).
+int rs_host_alloc(void **out, size_t bytes) {
+    if (!out) return fail(RS_E_INVALID, "out must not be NULL");
+    *out = nullptr;
+    int rc = need_device();
+    if (rc) return rc;
+    RS_HIP(hipHostMalloc(out, std::max<size_t>(bytes, 1), hipHostMallocMapped | hipHostMallocNumaUser));
+    return RS_OK;
+}
+
+int rs_host_free(void *ptr) {
+    if (ptr) RS_HIP(hipHostFree(ptr));
+    return RS_OK;
+}
+
 int rs_check_buffers_and_sizes(const rs_codec *codec, int nshards, const int64_t *shard_lens, int64_t offset,
                                int64_t byte_count) {
     if (!codec) return fail(RS_E_INVALID, "NULL codec");

@@ -1,5 +1,7 @@
 package edu.cmu.reedsolomon;
 
+import java.nio.ByteBuffer;
+
 /**
  * GPU-backed drop-in for {@code ReedSolomon} (ReedSolomon.java:13-344 of the
  * reference): same factory, getters and coding methods, same exceptions and
@@ -92,6 +94,48 @@ public final class NativeReedSolomon implements AutoCloseable {
     }
 
     /**
+     * A direct ByteBuffer over pinned host memory (rs_host_alloc: page-locked,
+     * mapped for the GPU, on the calling thread's NUMA node).  Shards and files
+     * kept in such buffers are coded in place across the link with no host
+     * copies (the ByteBuffer overloads below).  Free it with freePinned; the
+     * garbage collector does not.
+     */
+    public static ByteBuffer allocatePinned(int capacity) {
+        return nativeAllocatePinned(capacity);
+    }
+
+    /** Frees a buffer from allocatePinned; the buffer must not be used afterwards. */
+    public static void freePinned(ByteBuffer buffer) {
+        nativeFreePinned(buffer);
+    }
+
+    /**
+     * encodeParity over direct ByteBuffers (any direct buffer; pinned ones
+     * from allocatePinned take the in-place path).  Each shard's length is
+     * its capacity; position and limit are ignored.  Same checks, exceptions
+     * and messages as the byte[][] form.
+     */
+    public void encodeParity(ByteBuffer[] shards, int offset, int byteCount) {
+        nativeEncodeParityDirect(handle, shards, offset, byteCount);
+    }
+
+    /** decodeMissing over direct ByteBuffers (see encodeParity(ByteBuffer[], int, int)). */
+    public void decodeMissing(ByteBuffer[] shards, boolean[] shardPresent, int offset, int byteCount) {
+        nativeDecodeMissingDirect(handle, shards, shardPresent, offset, byteCount);
+    }
+
+    /** encodeFile over direct ByteBuffers: the first fileLength bytes of fileData. */
+    public void encodeFile(ByteBuffer fileData, int fileLength, int blockSize, ByteBuffer[] shards) {
+        nativeEncodeFileDirect(handle, fileData, fileLength, blockSize, shards);
+    }
+
+    /** decodeFile over direct ByteBuffers: fileSize bytes into fileOut. */
+    public void decodeFile(ByteBuffer[] shards, boolean[] shardPresent, int byteCntInShard, int blockSize,
+                           ByteBuffer fileOut, int fileSize) {
+        nativeDecodeFileDirect(handle, shards, shardPresent, byteCntInShard, blockSize, fileOut, fileSize);
+    }
+
+    /**
      * Device-resident per-stripe recovery (rs_decode_batch_masked_bits_dev):
      * stripes [stripe][shard][shardStride] at device address devBase, one
      * uint32 presence bitmask per stripe at devBits (bit i = shard i present),
@@ -145,6 +189,16 @@ public final class NativeReedSolomon implements AutoCloseable {
     private static native void nativeEncodeFile(long h, byte[] file, int blockSize, byte[][] shards);
     private static native void nativeDecodeFile(long h, byte[][] shards, boolean[] present, int byteCntInShard,
                                                 int blockSize, byte[] fileOut, int fileSize);
+    private static native ByteBuffer nativeAllocatePinned(int capacity);
+    private static native void nativeFreePinned(ByteBuffer buffer);
+    private static native void nativeEncodeParityDirect(long h, ByteBuffer[] shards, int offset, int byteCount);
+    private static native void nativeDecodeMissingDirect(long h, ByteBuffer[] shards, boolean[] present, int offset,
+                                                         int byteCount);
+    private static native void nativeEncodeFileDirect(long h, ByteBuffer file, int fileLength, int blockSize,
+                                                      ByteBuffer[] shards);
+    private static native void nativeDecodeFileDirect(long h, ByteBuffer[] shards, boolean[] present,
+                                                      int byteCntInShard, int blockSize, ByteBuffer fileOut,
+                                                      int fileSize);
     private static native void nativeDecodeMaskedBitsDevice(long h, long devBase, long devBits, long nStripes,
                                                             long shardLen, long shardStride, long stripeStride,
                                                             long devBad, long stream);

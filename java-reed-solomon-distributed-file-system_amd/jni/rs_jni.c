@@ -57,10 +57,21 @@ static void j_throw_new(rsj_env *e, const char *cls, const char *msg) {
     if (c) (*J(e))->ThrowNew(J(e), c, msg);
 }
 
+static uint8_t *j_direct_address(rsj_env *e, rsj_obj b) {
+    return (uint8_t *)(*J(e))->GetDirectBufferAddress(J(e), (jobject)b);
+}
+static int64_t j_direct_capacity(rsj_env *e, rsj_obj b) {
+    return (int64_t)(*J(e))->GetDirectBufferCapacity(J(e), (jobject)b);
+}
+static rsj_obj j_new_direct(rsj_env *e, void *p, int64_t cap) {
+    return (*J(e))->NewDirectByteBuffer(J(e), p, (jlong)cap);
+}
+
 static rsj_env *wrap(jenv *je, JNIEnv *env) {
     rsj_env base = {NULL,           j_array_length,    j_object_element,   j_delete_local,
                     j_ensure_local_capacity, j_critical_get, j_critical_release, j_byte_region_get,
-                    j_byte_region_set, j_bool_region_get, j_exception_pending, j_throw_new};
+                    j_byte_region_set, j_bool_region_get, j_exception_pending, j_throw_new,
+                    j_direct_address, j_direct_capacity, j_new_direct};
     je->base = base;
     je->env = env;
     return &je->base;
@@ -126,6 +137,46 @@ JNIEXPORT void JNICALL Java_edu_cmu_reedsolomon_NativeReedSolomon_nativeDecodeFi
     jenv je;
     rsj_file_decode(wrap(&je, env), rsj_librsamd_backend(), CODEC(h), shards, present, byteCntInShard, block, fileOut,
                     fileSize);
+}
+
+/* Direct ByteBuffers: pinned ones from allocatePinned (rs_host_alloc) are
+ * coded in place across the link; any direct buffer is accepted. */
+JNIEXPORT jobject JNICALL Java_edu_cmu_reedsolomon_NativeReedSolomon_nativeAllocatePinned(JNIEnv *env, jclass cls,
+                                                                                        jint capacity) {
+    jenv je;
+    return (jobject)rsj_alloc_pinned(wrap(&je, env), rsj_librsamd_backend(), capacity);
+}
+
+JNIEXPORT void JNICALL Java_edu_cmu_reedsolomon_NativeReedSolomon_nativeFreePinned(JNIEnv *env, jclass cls,
+                                                                                 jobject buf) {
+    jenv je;
+    rsj_free_pinned(wrap(&je, env), rsj_librsamd_backend(), buf);
+}
+
+JNIEXPORT void JNICALL Java_edu_cmu_reedsolomon_NativeReedSolomon_nativeEncodeParityDirect(
+    JNIEnv *env, jclass cls, jlong h, jobjectArray shards, jint offset, jint count) {
+    jenv je;
+    rsj_encode_parity_direct(wrap(&je, env), rsj_librsamd_backend(), CODEC(h), shards, offset, count);
+}
+
+JNIEXPORT void JNICALL Java_edu_cmu_reedsolomon_NativeReedSolomon_nativeDecodeMissingDirect(
+    JNIEnv *env, jclass cls, jlong h, jobjectArray shards, jbooleanArray present, jint offset, jint count) {
+    jenv je;
+    rsj_decode_missing_direct(wrap(&je, env), rsj_librsamd_backend(), CODEC(h), shards, present, offset, count);
+}
+
+JNIEXPORT void JNICALL Java_edu_cmu_reedsolomon_NativeReedSolomon_nativeEncodeFileDirect(
+    JNIEnv *env, jclass cls, jlong h, jobject file, jint fileLength, jint block, jobjectArray shards) {
+    jenv je;
+    rsj_file_encode_direct(wrap(&je, env), rsj_librsamd_backend(), CODEC(h), file, fileLength, block, shards);
+}
+
+JNIEXPORT void JNICALL Java_edu_cmu_reedsolomon_NativeReedSolomon_nativeDecodeFileDirect(
+    JNIEnv *env, jclass cls, jlong h, jobjectArray shards, jbooleanArray present, jint byteCntInShard, jint block,
+    jobject fileOut, jint fileSize) {
+    jenv je;
+    rsj_file_decode_direct(wrap(&je, env), rsj_librsamd_backend(), CODEC(h), shards, present, byteCntInShard, block,
+                           fileOut, fileSize);
 }
 
 /* Frees this thread's device contexts (streams, staging buffers); for worker

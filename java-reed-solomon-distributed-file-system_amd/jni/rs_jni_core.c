@@ -34,7 +34,7 @@ const rsj_backend *rsj_librsamd_backend(void) {
                                   rs_code_some_shards,        rs_check_some_shards,      rs_check_buffers_and_sizes,
                                   rs_codec_total_shard_count, rs_codec_data_shard_count, rs_last_error_message,
                                   rs_decode_groups_shard_major_dev, rs_file_layout,          rs_file_encode,
-                                  rs_file_decode};
+                                  rs_file_decode,             rs_host_alloc,             rs_host_free};
     return &b;
 }
 
@@ -712,4 +712,170 @@ void rsj_file_decode(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_ob
     const file_op op = {OP_DECODE, block, file_size, byte_cnt, pres};
     file_call(e, b, c, &op, &s, role, file_out, ROLE_OUT, sliceable ? L / block : 0);
     drop_refs(e, &s);
+}
+
+/* ---- direct ByteBuffers ---- */
+
+rsj_obj rsj_alloc_pinned(rsj_env *e, const rsj_backend *b, int32_t capacity) {
+    if (capacity < 0) {
+        e->throw_new(e, IAE, "capacity is negative");
+        return NULL;
+    }
+    void *p = NULL;
+    const int rc = b->host_alloc(&p, (size_t)capacity);
+    if (rc) {
+        if (rc == RS_E_HIP) e->throw_new(e, "java/lang/OutOfMemoryError", b->last_error());
+        else throw_rc(e, b, rc);
+        return NULL;
+    }
+    rsj_obj buf = e->new_direct(e, p, capacity);
+    if (!buf) b->host_free(p); /* NewDirectByteBuffer threw */
+    return buf;
+}
+
+void rsj_free_pinned(rsj_env *e, const rsj_backend *b, rsj_obj buf) {
+    if (!buf) return;
+    uint8_t *p = e->direct_address(e, buf);
+    if (!p) {
+        e->throw_new(e, IAE, "not a direct buffer");
+        return;
+    }
+    const int rc = b->host_free(p);
+    if (rc) throw_rc(e, b, rc);
+}
+
+/* The first n elements of a ByteBuffer[] by address and capacity (local
+ * references dropped as soon as the address is read: a direct buffer's
+ * memory does not move). */
+static int take_direct(rsj_env *e, rsj_obj outer, int n, uint8_t **ptr, int64_t *len) {
+    if (n > RSJ_MAX_SHARDS) n = RSJ_MAX_SHARDS;
+    for (int i = 0; i < n; i++) {
+        rsj_obj x = e->object_element(e, outer, i);
+        if (e->exception_pending(e)) return -1;
+        if (!x) {
+            e->throw_new(e, NPE, "ByteBuffer element is null");
+            return -1;
+        }
+        ptr[i] = e->direct_address(e, x);
+        len[i] = ptr[i] ? e->direct_capacity(e, x) : 0;
+        e->delete_local(e, x);
+        if (!ptr[i]) {
+            char msg[64];
+            snprintf(msg, sizeof msg, "shard %d is not a direct buffer", i);
+            e->throw_new(e, IAE, msg);
+            return -1;
+        }
+    }
+    return 0;
+}
+
+/* shards.length != totalShardCount first (ReedSolomon.java:280-282), then the elements. */
+static int take_direct_shards(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj shards, uint8_t **ptr,
+                              int64_t *len, int *n) {
+    if (!shards) {
+        e->throw_new(e, NPE, "shards is null");
+        return -1;
+    }
+    *n = e->array_length(e, shards);
+    if (*n != b->total_shards(c)) {
+        int64_t none = 0;
+        throw_rc(e, b, b->check_buffers_and_sizes(c, *n, &none, 0, 0));
+        return -1;
+    }
+    return take_direct(e, shards, *n, ptr, len);
+}
+
+static int take_present(rsj_env *e, rsj_obj present, int n, uint8_t *pres) {
+    if (!present) {
+        e->throw_new(e, NPE, "shardPresent is null");
+        return -1;
+    }
+    const int np = e->array_length(e, present);
+    if (np < n) {
+        throw_index(e, np, np);
+        return -1;
+    }
+    e->bool_region_get(e, present, 0, n, pres);
+    return e->exception_pending(e) ? -1 : 0;
+}
+
+void rsj_encode_parity_direct(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj shards, int32_t offset,
+                              int32_t count) {
+    uint8_t *ptr[RSJ_MAX_SHARDS];
+    int64_t len[RSJ_MAX_SHARDS];
+    int n = 0;
+    if (take_direct_shards(e, b, c, shards, ptr, len, &n)) return;
+    const int rc = b->encode_parity(c, ptr, n, len, offset, count);
+    if (rc) throw_rc(e, b, rc);
+}
+
+void rsj_decode_missing_direct(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj shards, rsj_obj present,
+                               int32_t offset, int32_t count) {
+    uint8_t *ptr[RSJ_MAX_SHARDS], pres[RSJ_MAX_SHARDS];
+    int64_t len[RSJ_MAX_SHARDS];
+    int n = 0;
+    if (take_direct_shards(e, b, c, shards, ptr, len, &n)) return;
+    /* checkBuffersAndSizes first (ReedSolomon.java:185), then shardPresent[i] (:190-194) */
+    int rc = b->check_buffers_and_sizes(c, n, len, offset, count);
+    if (rc) {
+        throw_rc(e, b, rc);
+        return;
+    }
+    if (take_present(e, present, n, pres)) return;
+    rc = b->decode_missing(c, ptr, n, len, pres, offset, count);
+    if (rc) throw_rc(e, b, rc);
+}
+
+void rsj_file_encode_direct(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj file, int32_t file_len,
+                            int32_t block, rsj_obj shards) {
+    if (!file) {
+        e->throw_new(e, NPE, "fileData is null");
+        return;
+    }
+    uint8_t *f = e->direct_address(e, file);
+    if (!f) {
+        e->throw_new(e, IAE, "fileData is not a direct buffer");
+        return;
+    }
+    if (file_len > e->direct_capacity(e, file)) {
+        const int64_t cap = e->direct_capacity(e, file);
+        throw_index(e, cap, cap);
+        return;
+    }
+    uint8_t *ptr[RSJ_MAX_SHARDS];
+    int64_t len[RSJ_MAX_SHARDS];
+    int n = 0;
+    if (take_direct_shards(e, b, c, shards, ptr, len, &n)) return;
+    const int rc = b->file_encode(c, f, file_len, block, ptr, n, len);
+    if (rc) throw_rc(e, b, rc);
+}
+
+void rsj_file_decode_direct(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj shards, rsj_obj present,
+                            int32_t byte_cnt, int32_t block, rsj_obj file_out, int32_t file_size) {
+    uint8_t *ptr[RSJ_MAX_SHARDS], pres[RSJ_MAX_SHARDS];
+    int64_t len[RSJ_MAX_SHARDS];
+    int n = 0;
+    if (take_direct_shards(e, b, c, shards, ptr, len, &n)) return;
+    int rc = b->check_buffers_and_sizes(c, n, len, 0, byte_cnt);
+    if (rc) {
+        throw_rc(e, b, rc);
+        return;
+    }
+    if (take_present(e, present, n, pres)) return;
+    if (!file_out) {
+        e->throw_new(e, NPE, "fileOut is null");
+        return;
+    }
+    uint8_t *f = e->direct_address(e, file_out);
+    if (!f) {
+        e->throw_new(e, IAE, "fileOut is not a direct buffer");
+        return;
+    }
+    const int64_t cap = e->direct_capacity(e, file_out);
+    if (file_size > cap) {
+        throw_index(e, cap, cap);
+        return;
+    }
+    rc = b->file_decode(c, ptr, n, len, pres, byte_cnt, block, f, file_size);
+    if (rc) throw_rc(e, b, rc);
 }

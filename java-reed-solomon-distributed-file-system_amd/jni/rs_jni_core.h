@@ -57,6 +57,9 @@ struct rsj_env {
     void (*bool_region_get)(rsj_env *e, rsj_obj arr, int start, int len, uint8_t *dst);
     int (*exception_pending)(rsj_env *e);
     void (*throw_new)(rsj_env *e, const char *cls, const char *msg);
+    uint8_t *(*direct_address)(rsj_env *e, rsj_obj buf); /* NULL: not a direct buffer */
+    int64_t (*direct_capacity)(rsj_env *e, rsj_obj buf);
+    rsj_obj (*new_direct)(rsj_env *e, void *p, int64_t capacity); /* a new local reference, or NULL */
 };
 
 /* The coding entry points (librsamd.so's by default; tests substitute fakes). */
@@ -79,6 +82,8 @@ typedef struct rsj_backend {
     int (*file_encode)(const rs_codec *, const uint8_t *, int64_t, int32_t, uint8_t *const *, int, const int64_t *);
     int (*file_decode)(const rs_codec *, uint8_t *const *, int, const int64_t *, const uint8_t *, int32_t, int32_t,
                        uint8_t *, int64_t);
+    int (*host_alloc)(void **, size_t);
+    int (*host_free)(void *);
 } rsj_backend;
 
 const rsj_backend *rsj_librsamd_backend(void);
@@ -125,6 +130,25 @@ void rsj_recover_groups_shard_major(rsj_env *e, const rsj_backend *b, const rs_c
 void rsj_file_encode(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj file, int32_t block, rsj_obj shards);
 void rsj_file_decode(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj shards, rsj_obj present,
                      int32_t byte_cnt, int32_t block, rsj_obj file_out, int32_t file_size);
+
+/* Direct ByteBuffers (no Java counterpart): shards and files the caller keeps
+ * outside the Java heap, reached by address with no pinning and no slicing.
+ * Buffers from rsj_alloc_pinned (rs_host_alloc) are page-locked, so the
+ * library codes them in place across the link; other direct buffers
+ * (ByteBuffer.allocateDirect) are pageable and take the mirrored pipeline.
+ * A buffer's length is its capacity; an element that is not a direct buffer
+ * is IllegalArgumentException ("shard i is not a direct buffer"). */
+rsj_obj rsj_alloc_pinned(rsj_env *e, const rsj_backend *b, int32_t capacity);
+void rsj_free_pinned(rsj_env *e, const rsj_backend *b, rsj_obj buf);
+void rsj_encode_parity_direct(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj shards, int32_t offset,
+                              int32_t count);
+void rsj_decode_missing_direct(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj shards, rsj_obj present,
+                               int32_t offset, int32_t count);
+/* file: the first file_len bytes of a direct buffer; file_out receives file_size bytes */
+void rsj_file_encode_direct(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj file, int32_t file_len,
+                            int32_t block, rsj_obj shards);
+void rsj_file_decode_direct(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj shards, rsj_obj present,
+                            int32_t byte_cnt, int32_t block, rsj_obj file_out, int32_t file_size);
 
 #ifdef __cplusplus
 }

@@ -13,7 +13,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_ROOT, "lib", "librsamd.so")
 CSRC = os.path.join(PKG_ROOT, "csrc")
 
-ABI_VERSION = 5  # include/rs_amd.h RS_AMD_ABI_VERSION, which SIGNATURES follows
+ABI_VERSION = 6  # include/rs_amd.h RS_AMD_ABI_VERSION, which SIGNATURES follows
 u8p = C.POINTER(C.c_uint8)
 u8pp = C.POINTER(u8p)
 
@@ -73,6 +73,8 @@ SIGNATURES = {
                                         C.c_int, C.c_void_p, C.c_int, C.c_void_p]),
     "rs_dev_alloc": (C.c_int, [C.POINTER(C.c_void_p), C.c_size_t, C.c_int, C.POINTER(C.c_int)]),
     "rs_dev_free": (C.c_int, [C.c_void_p]),
+    "rs_host_alloc": (C.c_int, [C.POINTER(C.c_void_p), C.c_size_t]),
+    "rs_host_free": (C.c_int, [C.c_void_p]),
 }
 
 _lib = None

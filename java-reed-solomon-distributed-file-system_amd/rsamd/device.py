@@ -269,3 +269,33 @@ def view_shards(buf: np.ndarray, lay: StripeLayout, total: int) -> np.ndarray:
     v = buf[: lay.nbytes].reshape(lay.n_stripes, lay.stripe_stride)
     v = v[:, : total * lay.shard_stride].reshape(lay.n_stripes, total, lay.shard_stride)
     return v[:, :, : lay.shard_len]
+
+
+class HostBuffer:
+    """Pinned host memory from rs_host_alloc (page-locked, mapped for the
+    device, placed by the calling thread's NUMA policy): shards and files kept
+    here are coded in place across the link by the host calls, with no host
+    copies.  `.array` is a NumPy uint8 view (valid while the buffer lives);
+    freed by free() or when collected."""
+
+    def __init__(self, nbytes: int):
+        import numpy as np
+        p = C.c_void_p()
+        check(_lib.load().rs_host_alloc(C.byref(p), nbytes))
+        self._ptr, self.nbytes = p.value, nbytes
+        self.array = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(max(nbytes, 1),))[:nbytes]
+
+    def data_ptr(self) -> int:
+        return self._ptr
+
+    def free(self) -> None:
+        if self._ptr:
+            self.array = None
+            check(_lib.load().rs_host_free(C.c_void_p(self._ptr)))
+            self._ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:  # noqa: BLE001  (interpreter shutdown)
+            pass

@@ -20,7 +20,7 @@
 
 #include "rs_jni_core.h"
 
-enum { K_BYTES = 1, K_BOOLS = 2, K_OBJECTS = 3 };
+enum { K_BYTES = 1, K_BOOLS = 2, K_OBJECTS = 3, K_DIRECT = 4 };
 
 typedef struct mobj {
     int kind, len;
@@ -60,6 +60,14 @@ mobj *mock_new_objects(int len) {
     o->kind = K_OBJECTS;
     o->len = len;
     o->elems = (mobj **)calloc((size_t)(len > 0 ? len : 1), sizeof(mobj *));
+    return o;
+}
+/* a direct ByteBuffer over caller memory (data not owned) */
+mobj *mock_new_direct(uint8_t *p, int cap) {
+    mobj *o = (mobj *)calloc(1, sizeof *o);
+    o->kind = K_DIRECT;
+    o->len = cap;
+    o->data = p;
     return o;
 }
 void mock_set(mobj *outer, int i, mobj *inner) { outer->elems[i] = inner; }
@@ -169,9 +177,25 @@ static void m_throw_new(rsj_env *e, const char *cls, const char *msg) {
     strncpy(S.exc_msg, msg ? msg : "", sizeof S.exc_msg - 1);
 }
 
+static uint8_t *m_direct_address(rsj_env *e, rsj_obj b) {
+    jni_call(0);
+    return ((mobj *)b)->kind == K_DIRECT ? ((mobj *)b)->data : NULL;
+}
+static int64_t m_direct_capacity(rsj_env *e, rsj_obj b) {
+    jni_call(0);
+    return ((mobj *)b)->kind == K_DIRECT ? ((mobj *)b)->len : -1;
+}
+static rsj_obj m_new_direct(rsj_env *e, void *p, int64_t cap) {
+    jni_call(0);
+    S.live_refs++; /* the returned local reference (the Java caller takes it over) */
+    if (S.live_refs > S.max_live_refs) S.max_live_refs = S.live_refs;
+    return mock_new_direct((uint8_t *)p, (int)cap);
+}
+
 static rsj_env ENV = {NULL,           m_array_length,    m_object_element,   m_delete_local,
                       m_ensure_local_capacity, m_critical_get, m_critical_release, m_byte_region_get,
-                      m_byte_region_set, m_bool_region_get, m_exception_pending, m_throw_new};
+                      m_byte_region_set, m_bool_region_get, m_exception_pending, m_throw_new,
+                      m_direct_address, m_direct_capacity, m_new_direct};
 
 /* ---- fake backend: real argument checks from librsamd, fake coding ---- */
 
@@ -310,6 +334,20 @@ static int fake_file_decode(const rs_codec *c, uint8_t *const *sh, int n, const 
     }
     return 0;
 }
+/* pinned host memory: plain malloc, counted */
+static int host_live;
+static int fake_host_alloc(void **out, size_t n) {
+    *out = malloc(n ? n : 1);
+    if (!*out) return RS_E_HIP;
+    host_live++;
+    return 0;
+}
+static int fake_host_free(void *p) {
+    free(p);
+    host_live--;
+    return 0;
+}
+int mock_host_live(void) { return host_live; }
 void mock_file_record(int64_t *out, int max) {
     out[0] = FC.calls;
     for (int i = 0; i < FC.calls && i < 64 && 2 * i + 2 < max; i++) {
@@ -323,7 +361,7 @@ static const rsj_backend FAKE = {fake_encode,       fake_decode,         fake_ve
                                  fake_code,         fake_check,          rs_check_buffers_and_sizes,
                                  rs_codec_total_shard_count, fake_data_shards, rs_last_error_message,
                                  fake_shard_major,  rs_file_layout,      fake_file_encode,
-                                 fake_file_decode};
+                                 fake_file_decode,  fake_host_alloc,     fake_host_free};
 
 static const rsj_backend *backend(int real) { return real ? rsj_librsamd_backend() : &FAKE; }
 
@@ -366,4 +404,21 @@ void mock_file_encode(int real, const rs_codec *c, mobj *file, int32_t block, mo
 void mock_file_decode(int real, const rs_codec *c, mobj *shards, mobj *present, int32_t cnt, int32_t block, mobj *out,
                       int32_t fsize) {
     rsj_file_decode(&ENV, backend(real), c, shards, present, cnt, block, out, fsize);
+}
+mobj *mock_alloc_pinned(int real, int32_t cap) { return (mobj *)rsj_alloc_pinned(&ENV, backend(real), cap); }
+void mock_free_pinned(int real, mobj *buf) { rsj_free_pinned(&ENV, backend(real), buf); }
+/* the Java caller dropping its local reference to a buffer from new_direct */
+void mock_drop_local(void) { S.live_refs--; }
+void mock_encode_parity_direct(int real, const rs_codec *c, mobj *shards, int32_t off, int32_t cnt) {
+    rsj_encode_parity_direct(&ENV, backend(real), c, shards, off, cnt);
+}
+void mock_decode_missing_direct(int real, const rs_codec *c, mobj *shards, mobj *present, int32_t off, int32_t cnt) {
+    rsj_decode_missing_direct(&ENV, backend(real), c, shards, present, off, cnt);
+}
+void mock_file_encode_direct(int real, const rs_codec *c, mobj *file, int32_t flen, int32_t block, mobj *shards) {
+    rsj_file_encode_direct(&ENV, backend(real), c, file, flen, block, shards);
+}
+void mock_file_decode_direct(int real, const rs_codec *c, mobj *shards, mobj *present, int32_t cnt, int32_t block,
+                             mobj *out, int32_t fsize) {
+    rsj_file_decode_direct(&ENV, backend(real), c, shards, present, cnt, block, out, fsize);
 }

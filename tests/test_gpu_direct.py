@@ -337,3 +337,42 @@ def test_direct_interior_and_ends(gpu, oracle_lib, n, off):
             sh[j][off:off + cnt] = 0x33
         rs.decodeMissing(sh, [i not in miss for i in range(6)], off, cnt)
         assert_same(sh, ref, miss)
+
+
+def test_host_buffer_shards_and_file(gpu, oracle_lib):
+    """Shards and a file kept in rs_host_alloc memory (rsamd.device.HostBuffer,
+    the pinned buffers NativeReedSolomon.allocatePinned hands a JVM): encode,
+    decode {0, 5} and the file calls in place, against the oracle."""
+    import rsamd
+    from rsamd.device import HostBuffer
+    from rsamd.layout import file_decode_into, file_encode_into, file_layout
+    k, m, n = 4, 2, (8 << 20) + 40
+    rs = rsamd.ReedSolomon.create(k, m)
+    bufs = [HostBuffer(n) for _ in range(k + m)]
+    sh = [b.array for b in bufs]
+    rng = np.random.default_rng(77)
+    for a in sh:
+        a[:] = rng.integers(0, 256, n, dtype=np.uint8)
+    ref = [a.copy() for a in sh]
+    oracle_lib.Codec(k, m).encode_parity(ref, 0, n)
+    rs.encodeParity(sh, 0, n)
+    assert_same(sh, ref, "encode")
+    for j in (0, 5):
+        sh[j][:] = 0
+    rs.decodeMissing(sh, [i not in (0, 5) for i in range(k + m)], 0, n)
+    assert_same(sh, ref, "decode {0,5}")
+    flen = 3 * (4 << 20) + 999
+    fbuf = HostBuffer(flen)
+    fbuf.array[:] = rng.integers(0, 256, flen, dtype=np.uint8)
+    _, S = file_layout(rs, flen)
+    fsh = [HostBuffer(S) for _ in range(k + m)]
+    file_encode_into(rs, fbuf.array, [b.array for b in fsh])
+    want = oracle_lib.Codec(k, m).file_encode(fbuf.array.tobytes(), 1000)
+    assert_same([b.array for b in fsh], list(want), "file encode")
+    out = HostBuffer(flen)
+    for j in (0, 5):
+        fsh[j].array[:] = 0
+    file_decode_into(rs, [b.array for b in fsh], [i not in (0, 5) for i in range(k + m)], S, out.array)
+    assert np.array_equal(out.array, fbuf.array)
+    for b in bufs + fsh + [fbuf, out]:
+        b.free()

@@ -151,3 +151,55 @@ def test_file_encode_decode_through_shim(gpu, oracle_lib, native, jvm, k, m, blo
         jvm.assert_clean()
     finally:
         native.rs_codec_destroy(h)
+
+
+def test_direct_buffers_through_shim(gpu, oracle_lib, native, jvm):
+    """NativeReedSolomon.allocatePinned / freePinned and the ByteBuffer
+    overloads over librsamd: shards and a file in pinned direct buffers from
+    the shim's own allocator, coded in place, against the oracle."""
+    k, m, n = 4, 2, (4 << 20) + 24
+    h = C.c_void_p()
+    assert native.rs_codec_create(k, m, C.byref(h)) == 0
+
+    def view(buf, size):
+        return np.ctypeslib.as_array(C.cast(jvm.lib.mock_data(buf), C.POINTER(C.c_uint8)), shape=(size,))
+
+    try:
+        bufs = [jvm.lib.mock_alloc_pinned(1, n) for _ in range(k + m)]
+        assert all(bufs) and jvm.exception() == ("", "")
+        rng = np.random.default_rng(5)
+        for b in bufs:
+            view(b, n)[:] = rng.integers(0, 256, n, dtype=np.uint8)
+        ref = [view(b, n).copy() for b in bufs]
+        oracle_lib.Codec(k, m).encode_parity(ref, 0, n)
+        jvm.lib.mock_encode_parity_direct(1, h, jvm.objects(bufs), 0, n)
+        assert jvm.exception() == ("", "")
+        assert all(np.array_equal(view(b, n), r) for b, r in zip(bufs, ref))
+        for j in (0, 5):
+            view(bufs[j], n)[:] = 0
+        jvm.lib.mock_decode_missing_direct(1, h, jvm.objects(bufs), jvm.bools([i not in (0, 5) for i in range(6)]), 0,
+                                           n)
+        assert jvm.exception() == ("", "")
+        assert all(np.array_equal(view(b, n), r) for b, r in zip(bufs, ref))
+        # the file calls: 3 shards' worth of file, 1000-byte blocks
+        flen = 3 * n + 7
+        S = -(-flen // 4000) * 1000
+        fb = jvm.lib.mock_alloc_pinned(1, flen)
+        view(fb, flen)[:] = rng.integers(0, 256, flen, dtype=np.uint8)
+        fsh = [jvm.lib.mock_alloc_pinned(1, S) for _ in range(k + m)]
+        jvm.lib.mock_file_encode_direct(1, h, fb, flen, 1000, jvm.objects(fsh))
+        assert jvm.exception() == ("", "")
+        want = oracle_lib.Codec(k, m).file_encode(view(fb, flen).tobytes(), 1000)
+        assert all(np.array_equal(view(b, S), w) for b, w in zip(fsh, want))
+        out = jvm.lib.mock_alloc_pinned(1, flen)
+        view(fsh[0], S)[:] = 0
+        jvm.lib.mock_file_decode_direct(1, h, jvm.objects(fsh), jvm.bools([False] + [True] * 5), S, 1000, out, flen)
+        assert jvm.exception() == ("", "")
+        assert np.array_equal(view(out, flen), view(fb, flen))
+        for b in bufs + fsh + [fb, out]:
+            jvm.lib.mock_drop_local()
+            jvm.lib.mock_free_pinned(1, b)
+        assert jvm.exception() == ("", "")
+        jvm.assert_clean()
+    finally:
+        native.rs_codec_destroy(h)

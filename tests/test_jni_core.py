@@ -58,6 +58,12 @@ def build_mock():
         ("mock_file_encode", None, [C.c_int, P, P, C.c_int32, P]),
         ("mock_file_decode", None, [C.c_int, P, P, P, C.c_int32, C.c_int32, P, C.c_int32]),
         ("mock_file_record", None, [C.POINTER(C.c_int64), C.c_int]),
+        ("mock_new_direct", P, [P, C.c_int]), ("mock_host_live", C.c_int, []), ("mock_drop_local", None, []),
+        ("mock_alloc_pinned", P, [C.c_int, C.c_int32]), ("mock_free_pinned", None, [C.c_int, P]),
+        ("mock_encode_parity_direct", None, [C.c_int, P, P, C.c_int32, C.c_int32]),
+        ("mock_decode_missing_direct", None, [C.c_int, P, P, P, C.c_int32, C.c_int32]),
+        ("mock_file_encode_direct", None, [C.c_int, P, P, C.c_int32, C.c_int32, P]),
+        ("mock_file_decode_direct", None, [C.c_int, P, P, P, C.c_int32, C.c_int32, P, C.c_int32]),
     ]:
         fn = getattr(lib, name)
         fn.restype, fn.argtypes = res, args
@@ -90,6 +96,10 @@ class Jvm:
         for i, e in enumerate(elems):
             self.lib.mock_set(o, i, e)
         return o
+
+    def direct(self, arr):
+        """A direct ByteBuffer over a NumPy array's memory (the array must outlive it)."""
+        return self.lib.mock_new_direct(arr.ctypes.data, len(arr))
 
     def read(self, o, n):
         return np.ctypeslib.as_array(C.cast(self.lib.mock_data(o), C.POINTER(C.c_uint8)), shape=(n,)).copy()
@@ -601,4 +611,101 @@ def test_file_real_backend_without_gpu_throws_illegal_state(jvm, codec42, native
     jvm.lib.mock_file_encode(1, codec42, jvm.bytes(np.ones(4000, np.uint8)), 1000, jvm.objects(arrs))
     assert jvm.exception()[0] == ISE
     assert all((jvm.read(a, 1000) == 0).all() for a in arrs)
+    jvm.assert_clean()
+
+
+# ---- direct ByteBuffers: pinned allocation and the ByteBuffer overloads ----
+
+def test_direct_encode_decode_marshalling(jvm, codec42):
+    """Shards by address and capacity: no critical region, no copy, no local
+    reference left; the backend writes the caller's memory in place."""
+    S, off, cnt = 5000, 7, 4000
+    data = [np.random.default_rng(i).integers(0, 256, S, dtype=np.uint8) for i in range(6)]
+    bufs = [d.copy() for d in data]
+    jvm.lib.mock_encode_parity_direct(0, codec42, jvm.objects([jvm.direct(b) for b in bufs]), off, cnt)
+    assert jvm.exception() == ("", "")
+    want = fake_parity(data, 4, 2, off, cnt)
+    assert all(np.array_equal(b, w) for b, w in zip(bufs, want))
+    present = [True, False, True, True, True, False]
+    jvm.lib.mock_decode_missing_direct(0, codec42, jvm.objects([jvm.direct(b) for b in bufs]), jvm.bools(present),
+                                       off, cnt)
+    assert jvm.exception() == ("", "")
+    want = fake_decode(want, present, off, cnt)
+    assert all(np.array_equal(b, w) for b, w in zip(bufs, want))
+    st = jvm.assert_clean()
+    assert st["critical_gets"] == 0 and st["bytes_in"] == 6 and st["bytes_out"] == 0  # (the 6 flags)
+
+
+def test_direct_argument_errors(jvm, codec42):
+    bufs = [np.zeros(100, np.uint8) for _ in range(6)]
+
+    def enc(elems, off=0, cnt=10, real=1):
+        jvm.lib.mock_reset()
+        jvm.lib.mock_encode_parity_direct(real, codec42, elems, off, cnt)
+        jvm.assert_clean()
+        return jvm.exception()
+
+    D = [jvm.direct(b) for b in bufs]
+    assert enc(None)[0] == NPE
+    assert enc(jvm.objects(D[:5])) == (IAE, "wrong number of shards: 5")
+    assert enc(jvm.objects(D[:2] + [jvm.bytes(bufs[2])] + D[3:])) == (IAE, "shard 2 is not a direct buffer")
+    assert enc(jvm.objects(D[:5] + [None]))[0] == NPE
+    assert enc(jvm.objects(D), 95, 10) == (IAE, "buffers to small: 1095")
+    jvm.lib.mock_reset()
+    jvm.lib.mock_decode_missing_direct(1, codec42, jvm.objects(D), jvm.bools([True] * 5), 0, 10)
+    assert jvm.exception() == (AIOOBE, "Index 5 out of bounds for length 5")
+    jvm.assert_clean()
+    assert all((b == 0).all() for b in bufs)
+
+
+def test_direct_file_marshalling(jvm, codec42):
+    k, m, block, flen = 4, 2, 1000, 90999
+    data = np.random.default_rng(4).integers(0, 256, flen + 50, dtype=np.uint8)  # capacity past the file
+    want = split_file(data[:flen], k, m, block)
+    S = len(want[0])
+    want = fake_parity(want, k, m, 0, S)
+    bufs = [np.full(S, 0xC3, np.uint8) for _ in range(k + m)]
+    jvm.lib.mock_file_encode_direct(0, codec42, jvm.direct(data), flen, block, jvm.objects([jvm.direct(b) for b in bufs]))
+    assert jvm.exception() == ("", "")
+    assert all(np.array_equal(b, w) for b, w in zip(bufs, want))
+    present = [False, True, True, True, True, True]
+    out = np.full(flen + 3, 0x77, np.uint8)
+    jvm.lib.mock_file_decode_direct(0, codec42, jvm.objects([jvm.direct(b) for b in bufs]), jvm.bools(present), S,
+                                    block, jvm.direct(out), flen)
+    assert jvm.exception() == ("", "")
+    dec = fake_decode(want, present, 0, S)
+    assert np.array_equal(out[:flen], merge_file(dec, k, block, flen)) and (out[flen:] == 0x77).all()
+    st = jvm.assert_clean()
+    assert st["critical_gets"] == 0
+    # the file length past the buffer, a heap array where a direct buffer belongs
+    jvm.lib.mock_file_encode_direct(1, codec42, jvm.direct(data), len(data) + 1, block,
+                                    jvm.objects([jvm.direct(b) for b in bufs]))
+    assert jvm.exception() == (AIOOBE, f"Index {len(data)} out of bounds for length {len(data)}")
+    jvm.lib.mock_reset()
+    jvm.lib.mock_file_encode_direct(1, codec42, jvm.bytes(data), flen, block, jvm.objects([jvm.direct(b) for b in bufs]))
+    assert jvm.exception() == (IAE, "fileData is not a direct buffer")
+    jvm.lib.mock_reset()
+    jvm.lib.mock_file_decode_direct(1, codec42, jvm.objects([jvm.direct(b) for b in bufs]), jvm.bools(present), S,
+                                    block, jvm.direct(out[:flen - 1]), flen)
+    assert jvm.exception() == (AIOOBE, f"Index {flen - 1} out of bounds for length {flen - 1}")
+    jvm.assert_clean()
+
+
+def test_alloc_free_pinned(jvm, native):
+    """allocatePinned hands back a direct buffer of the asked capacity over
+    the backend's allocation (one new local reference, which the Java caller
+    owns); freePinned returns it."""
+    buf = jvm.lib.mock_alloc_pinned(0, 4096)
+    assert buf and jvm.exception() == ("", "") and jvm.lib.mock_host_live() == 1
+    assert jvm.stats()["live_refs"] == 1
+    jvm.lib.mock_drop_local()
+    jvm.lib.mock_free_pinned(0, buf)
+    assert jvm.lib.mock_host_live() == 0 and jvm.exception() == ("", "")
+    assert not jvm.lib.mock_alloc_pinned(0, -1) and jvm.exception() == (IAE, "capacity is negative")
+    jvm.lib.mock_reset()
+    jvm.lib.mock_free_pinned(0, jvm.bytes(np.zeros(4)))
+    assert jvm.exception() == (IAE, "not a direct buffer")
+    jvm.lib.mock_reset()
+    if native.rs_device_count() == 0:  # the real allocator needs a device
+        assert not jvm.lib.mock_alloc_pinned(1, 4096) and jvm.exception()[0] == ISE
     jvm.assert_clean()
