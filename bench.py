@@ -1393,9 +1393,11 @@ def link_bound_GiBps(link, up, down):
 
 
 def host_inclusive(rsamd, k, m, link=None):
-    """Rates of the JNI-facing host-buffer API: H2D + kernel + D2H on pageable
-    buffers, chunked and overlapped on three streams (host.cpp run_chunks),
-    each next to the bound of the link measured in this run (host_link)."""
+    """Rates of the JNI-facing host-buffer API on pageable buffers (the
+    mirrored pipeline, host.cpp run_mirrored) and on the library's own pinned
+    buffers (rs_host_alloc, what NativeReedSolomon.allocatePinned hands a JVM:
+    coded in place across the link), each next to the bound of the link
+    measured in this run (host_link)."""
     import numpy as np
     from rsamd.layout import file_encode_into, file_layout
     n = 64 << 20
@@ -1429,26 +1431,34 @@ def host_inclusive(rsamd, k, m, link=None):
     fout = np.empty(len(data), np.uint8)
     out["host_inclusive_file_decode_0_%d_GiBps" % (k + m - 1)] = rate(
         lambda: file_decode_into(rs, fsh, fpresent, S, fout), len(data))
-    # the same calls on pinned (page-locked) host buffers, where
-    # the two streams' H2D and D2H overlap as DMA
-    import torch
-    pin = [torch.empty(n, dtype=torch.uint8, pin_memory=True).numpy() for _ in range(k + m)]
+    # the same calls on pinned (page-locked) host buffers from the
+    # library's allocator (rsamd.device.HostBuffer = rs_host_alloc)
+    from rsamd.device import HostBuffer
+    held = []
+
+    def pinned(nbytes):
+        held.append(HostBuffer(nbytes))
+        return held[-1].array
+
+    pin = [pinned(n) for _ in range(k + m)]
     for a, b in zip(pin, sh):
         a[:] = b
     out["host_inclusive_pinned_encode_GiBps"] = rate(lambda: rs.encodeParity(pin, 0, n), k * n)
     out["host_inclusive_pinned_decode_0_1_GiBps"] = rate(lambda: rs.decodeMissing(pin, present, 0, n), k * n)
     # the file calls on pinned buffers (the direct kernels plus the split / merge on the host)
-    pfile = torch.empty(len(data), dtype=torch.uint8, pin_memory=True).numpy()
+    pfile = pinned(len(data))
     pfile[:] = data
-    pfsh = [torch.empty(S, dtype=torch.uint8, pin_memory=True).numpy() for _ in range(k + m)]
-    pfout = torch.empty(len(data), dtype=torch.uint8, pin_memory=True).numpy()
+    pfsh = [pinned(S) for _ in range(k + m)]
+    pfout = pinned(len(data))
     out["host_inclusive_pinned_file_encode_GiBps"] = rate(lambda: file_encode_into(rs, pfile, pfsh), len(data))
     out["host_inclusive_pinned_file_decode_0_%d_GiBps" % (k + m - 1)] = rate(
         lambda: file_decode_into(rs, pfsh, fpresent, S, pfout), len(data))
     pinned_file_ok = np.array_equal(pfout, data) and all(np.array_equal(a, b) for a, b in zip(pfsh, fsh))
     out["host_inclusive_file_legs_bit_exact"] = bool(pinned_file_ok and np.array_equal(fout, data))
     del pin, pfile, pfsh, pfout
-    out["host_inclusive_note"] = (f"{k}+{m}, {n >> 20} MiB host shards per call, pageable unless 'pinned' "
+    for b in held:
+        b.free()
+    out["host_inclusive_note"] = (f"{k}+{m}, {n >> 20} MiB host shards per call, pageable unless 'pinned' (rs_host_alloc) "
                                   f"(file legs: a {len(data) >> 20} MiB file); PCIe-bound, never the bench value; "
                                   f"pinned calls of >= 64 KiB per shard are coded in place across the link by one "
                                   f"kernel (the direct path, no copies); pageable ones go through the "
@@ -1531,10 +1541,11 @@ def host_inclusive_all_ranks(rsamd, parallel, r, k, m, link=None, n=64 << 20, re
     then pageable), bracketed by barriers; aggregate user bytes over the
     slowest rank's time.  Bound by the node's PCIe / host memory, not HBM."""
     import numpy as np
-    import torch
+    from rsamd.device import HostBuffer
     rng = np.random.default_rng(100 + r.rank)
     rs = rsamd.ReedSolomon.create(k, m)
-    pin = [torch.empty(n, dtype=torch.uint8, pin_memory=True).numpy() for _ in range(k + m)]
+    held = [HostBuffer(n) for _ in range(k + m)]  # rs_host_alloc: the library's pinned buffers
+    pin = [b.array for b in held]
     for a in pin[:k]:
         a[:] = rng.integers(0, 256, n, dtype=np.uint8)
     pageable = [a.copy() for a in pin]
@@ -1556,6 +1567,8 @@ def host_inclusive_all_ranks(rsamd, parallel, r, k, m, link=None, n=64 << 20, re
         out["host_inclusive_pinned_encode_all_ranks_frac_of_N_links"] = round(
             out["host_inclusive_pinned_encode_all_ranks_GiBps"] / (r.world * bound), 4)
     del pin, pageable
+    for b in held:
+        b.free()
     return out
 
 
