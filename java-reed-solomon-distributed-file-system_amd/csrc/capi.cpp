@@ -79,13 +79,12 @@ uint8_t *host_dev_addr(const void *p) {
     return static_cast<uint8_t *>(d);
 }
 
-// Bytes per shard from which a pageable call is page-locked for the call and
-// coded by the direct kernel instead of being copied through the zero-copy
-// staging buffer (TUNING builds: RSAMD_DIRECT_MIN, read per call).  4+2
-// encodeParity per call, pageable / pinned, staged -> direct
-// (tools/direct_small_probe.py, profiles/r3/direct_small_r3s2k.txt):
-//   4 KiB 26.6 -> 31.5 / 26.3 -> 29.7 us;  64 KiB 39.8 -> 38.3 / 38.8 -> 31.8 us;
-//   256 KiB 93.5 -> 54.7 / 96.3 -> 50.5;  1 MiB 291 -> 122;  4 MiB 696 -> 371 us.
+// Bytes per shard from which a caller-pinned call is coded in place by the
+// direct kernel instead of being copied through the zero-copy staging buffer
+// (TUNING builds: RSAMD_DIRECT_MIN, read per call).  4+2 encodeParity per
+// call on pinned shards, staged -> direct (tools/direct_small_probe.py,
+// profiles/r3/direct_small_r3s2k.txt): 4 KiB 26.3 -> 29.7 us, 64 KiB
+// 38.8 -> 31.8 us, 256 KiB 96.3 -> 50.5 us.
 size_t direct_min_bytes() { return rsamd::tuning_size("RSAMD_DIRECT_MIN", size_t(64) << 10); }
 
 // Bytes per shard from which a pageable call takes the mirrored pipeline

@@ -709,3 +709,26 @@ def test_alloc_free_pinned(jvm, native):
     if native.rs_device_count() == 0:  # the real allocator needs a device
         assert not jvm.lib.mock_alloc_pinned(1, 4096) and jvm.exception()[0] == ISE
     jvm.assert_clean()
+
+
+def test_file_decode_sliced_short_file(jvm, codec21):
+    """A sliced decode whose fileSize ends in the first slice: every slice
+    still rebuilds the absent shard (the reference decodes all byteCntInShard
+    bytes before it trims), the later slices write no file bytes."""
+    k, m, block = 2, 1, 4096
+    S = 2 * SLICE + 3 * block
+    rng = np.random.default_rng(8)
+    shards = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)] + [np.zeros(S, np.uint8)]
+    shards = fake_parity(shards, k, m, 0, S)
+    present = [True, False, True]
+    arrs = [jvm.bytes(s if p else np.zeros(S, np.uint8)) for s, p in zip(shards, present)]
+    out = jvm.bytes(np.full(10, 0x77, np.uint8))
+    jvm.lib.mock_file_decode(0, codec21, jvm.objects(arrs), jvm.bools(present), S, block, out, 5)
+    assert jvm.exception() == ("", "")
+    want = fake_decode(shards, present, 0, S)
+    assert np.array_equal(jvm.read(arrs[1], S), want[1])
+    got = jvm.read(out, 10)
+    assert np.array_equal(got[:5], want[0][:5]) and (got[5:] == 0x77).all()
+    calls = file_calls(jvm)
+    assert [c[0] for c in calls] == [5, 0, 0] and sum(c[1] for c in calls) == S
+    jvm.assert_clean()
