@@ -421,8 +421,8 @@ int run_zero_copy(ThreadCtx *ctx, size_t buf_bytes, const ChunkIo &io, const Chu
     std::vector<Xfer> in, out;
     io(0, &in, &out);
     // Host copies on the calling thread; the copy pool only above 2 MiB (its
-    // wake-up costs more than a small memcpy).
-    const bool use_pool = buf_bytes > (size_t(2) << 20);
+    // wake-up costs more than a small memcpy; TUNING builds: RSAMD_ZC_POOL_MIN).
+    const bool use_pool = buf_bytes > tuning_size("RSAMD_ZC_POOL_MIN", size_t(2) << 20);
     std::vector<rsamd::CopyJob> jobs;
     for (const Xfer &x : in) jobs.push_back({ctx->zc + x.off, x.host, x.n});
     if (use_pool) {
