@@ -3,6 +3,7 @@
 #include "tuning.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 
 #include <immintrin.h>
@@ -145,7 +146,23 @@ CopyPool &CopyPool::get() {
     return *pool;
 }
 
+// An idle thread (a worker with nothing queued, a caller waiting for its
+// batch's last pieces) polls for this long before it sleeps on a condition
+// variable: the mirrored pipeline hands the pool a batch per chunk, and a
+// sleeping thread's wake-up costs more than a small chunk's copy (TUNING
+// builds: RSAMD_POOL_SPIN_US).
+template <class Ready>
+void spin_until(int us, Ready ready) {
+    if (us <= 0) return;
+    const auto end = std::chrono::steady_clock::now() + std::chrono::microseconds(us);
+    while (!ready()) {
+        for (int i = 0; i < 32; ++i) _mm_pause();
+        if (std::chrono::steady_clock::now() > end) return;
+    }
+}
+
 CopyPool::CopyPool(int n) {
+    spin_us_ = int(tuning_size("RSAMD_POOL_SPIN_US", 0));
     for (int i = 0; i < n; ++i) {
         threads_.emplace_back([this] { run(); });
         threads_.back().detach();
@@ -153,20 +170,22 @@ CopyPool::CopyPool(int n) {
 }
 
 void CopyPool::run() {
-    std::unique_lock<std::mutex> lock(mu_);
     for (;;) {
+        spin_until(spin_us_, [this] { return queued_.load(std::memory_order_acquire) != 0; });
+        std::unique_lock<std::mutex> lock(mu_);
         work_cv_.wait(lock, [this] { return !queue_.empty(); });
         Piece p = queue_.front();
         queue_.pop_front();
+        queued_.fetch_sub(1, std::memory_order_relaxed);
         lock.unlock();
         copy_piece(p.job);
         lock.lock();
-        if (--*p.pending == 0) done_cv_.notify_all();
+        if (p.pending->fetch_sub(1, std::memory_order_acq_rel) == 1) done_cv_.notify_all();
     }
 }
 
 void CopyPool::copy(const std::vector<CopyJob> &jobs) {
-    size_t pending = 0;
+    std::atomic<size_t> pending{0};
     {
         std::lock_guard<std::mutex> lock(mu_);
         for (const CopyJob &j : jobs) {
@@ -179,7 +198,7 @@ void CopyPool::copy(const std::vector<CopyJob> &jobs) {
                     CopyJob piece{dst + off, src ? src + off : nullptr, std::min(kPiece, j.n - off)};
                     piece.dst2 = dst2 ? dst2 + off : nullptr;
                     queue_.push_back({piece, &pending});
-                    ++pending;
+                    pending.fetch_add(1, std::memory_order_relaxed);
                 }
                 continue;
             }
@@ -190,26 +209,31 @@ void CopyPool::copy(const std::vector<CopyJob> &jobs) {
                               std::min(per, j.rows - r), j.dst_stride, j.src_stride,
                               dst2 ? dst2 + r * j.dst2_stride : nullptr, j.dst2_stride};
                 queue_.push_back({piece, &pending});
-                ++pending;
+                pending.fetch_add(1, std::memory_order_relaxed);
             }
         }
+        queued_.store(queue_.size(), std::memory_order_release);
     }
-    if (pending == 0) return;
+    if (pending.load(std::memory_order_relaxed) == 0) return;
     work_cv_.notify_all();
     // The caller works too: take this batch's pieces (or anyone's) until the
     // queue is empty, then wait for the pieces still being copied.
     std::unique_lock<std::mutex> lock(mu_);
-    while (pending > 0) {
+    while (pending.load(std::memory_order_acquire) > 0) {
         if (!queue_.empty()) {
             Piece p = queue_.front();
             queue_.pop_front();
+            queued_.fetch_sub(1, std::memory_order_relaxed);
             lock.unlock();
             copy_piece(p.job);
             lock.lock();
-            if (--*p.pending == 0) done_cv_.notify_all();
+            if (p.pending->fetch_sub(1, std::memory_order_acq_rel) == 1) done_cv_.notify_all();
             continue;
         }
-        done_cv_.wait(lock, [&] { return pending == 0 || !queue_.empty(); });
+        lock.unlock();
+        spin_until(spin_us_, [&] { return pending.load(std::memory_order_acquire) == 0; });
+        lock.lock();
+        done_cv_.wait(lock, [&] { return pending.load(std::memory_order_acquire) == 0 || !queue_.empty(); });
     }
 }
 

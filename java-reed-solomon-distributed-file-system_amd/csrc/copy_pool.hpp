@@ -8,6 +8,7 @@
 // way -- tools/memcpy_probe.cpp).
 #pragma once
 
+#include <atomic>
 #include <condition_variable>
 #include <cstddef>
 #include <cstdint>
@@ -52,11 +53,13 @@ private:
 
     struct Piece {
         CopyJob job;
-        size_t *pending;  // the batch's counter (guarded by mu_)
+        std::atomic<size_t> *pending;  // the batch's counter (decremented under mu_)
     };
     std::mutex mu_;
     std::condition_variable work_cv_, done_cv_;
     std::deque<Piece> queue_;
+    std::atomic<size_t> queued_{0};  // queue_.size(), readable without mu_ (the spinners poll it)
+    int spin_us_ = 0;                // how long an idle thread polls before it sleeps
     std::vector<std::thread> threads_;
 };
 

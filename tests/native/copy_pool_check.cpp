@@ -3,11 +3,15 @@
 // a file's block rows into shard columns), with a second destination (the
 // tee into the pinned slots), random row lengths, strides and alignments;
 // every byte is compared with a plain copy and nothing past the destination
-// may be written.  Built and run by tests/test_copy_pool.py.
+// may be written.  Then several threads hand the pool batches at once (the
+// process-wide pool serves every concurrent call), each batch checked.  Built
+// and run by tests/test_copy_pool.py, with and without idle spinning.
 #include "copy_pool.hpp"
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <random>
+#include <thread>
 #include <vector>
 int main() {  // copy_pool.cpp gathers, tees, zero fills: every byte against a plain copy
     std::mt19937_64 rng(1);
@@ -34,6 +38,32 @@ int main() {  // copy_pool.cpp gathers, tees, zero fills: every byte against a p
         }
         if (dst[doff + n * rows] != 0xEE || (doff && dst[doff - 1] != 0xEE)) { ++bad; printf("overrun n=%zu\n", n); }
     }
+    // concurrent callers: 6 threads x 300 batches of 1-6 jobs, 1 B to 3 MiB each
+    std::atomic<int> cbad{0}, ccases{0};
+    std::vector<std::thread> ts;
+    for (int t = 0; t < 6; ++t)
+        ts.emplace_back([&, t] {
+            std::mt19937_64 r(100 + t);
+            for (int it = 0; it < 300; ++it) {
+                const int nj = 1 + int(r() % 6);
+                std::vector<std::vector<uint8_t>> srcs(nj), dsts(nj);
+                std::vector<rsamd::CopyJob> jobs;
+                for (int q = 0; q < nj; ++q) {
+                    const size_t n = 1 + r() % ((r() % 4 == 0) ? (3u << 20) : 70000u);
+                    srcs[q].resize(n);
+                    for (size_t x = 0; x < n; x += 8) srcs[q][x] = uint8_t(r());
+                    dsts[q].assign(n + 1, 0xEE);
+                    jobs.push_back({dsts[q].data(), srcs[q].data(), n});
+                }
+                rsamd::CopyPool::get().copy(jobs);
+                ++ccases;
+                for (int q = 0; q < nj; ++q)
+                    if (memcmp(dsts[q].data(), srcs[q].data(), srcs[q].size()) || dsts[q].back() != 0xEE) ++cbad;
+            }
+        });
+    for (auto &th : ts) th.join();
+    printf("%d concurrent batches, %d bad\n", ccases.load(), cbad.load());
+    bad += cbad.load();
     printf("%d cases, %d bad\n", cases, bad);
     return bad != 0;
 }

@@ -10,12 +10,20 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "java-reed-solomon-distributed-file-system_amd", "csrc")
 
 
-def test_copy_pool_gathers_and_tees(tmp_path):
+import pytest
+
+
+@pytest.mark.parametrize("spin_us", [None, 50])
+def test_copy_pool_gathers_and_tees(tmp_path, spin_us):
+    """None: the product build; 50: a TUNING build whose idle threads poll
+    50 us before they sleep (RSAMD_POOL_SPIN_US)."""
     exe = str(tmp_path / "copy_pool_check")
-    subprocess.run(["g++", "-O2", "-std=c++17", "-DRSAMD_TUNING_ENV=0", "-I", CSRC,
+    tuning = "0" if spin_us is None else "1"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-DRSAMD_TUNING_ENV=" + tuning, "-I", CSRC,
                     os.path.join(ROOT, "tests", "native", "copy_pool_check.cpp"),
                     os.path.join(CSRC, "copy_pool.cpp"), "-pthread", "-o", exe], check=True)
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    env = dict(os.environ, RSAMD_POOL_SPIN_US=str(spin_us or 0))
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout[-2000:]
     assert "0 bad" in r.stdout
 
@@ -24,7 +32,6 @@ def test_mirrored_chunking(tmp_path):
     obj = os.path.join(ROOT, "java-reed-solomon-distributed-file-system_amd", "build")
     objs = [os.path.join(obj, o) for o in ("host.o", "codec.o", "gf256.o", "copy_pool.o", "kernels.o", "layout.o")]
     if not all(os.path.exists(o) for o in objs):
-        import pytest
         pytest.skip("product objects not built (make -C java-...-amd/csrc)")
     exe = str(tmp_path / "ramp_check")
     cc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
