@@ -184,6 +184,11 @@ void CopyPool::run() {
     }
 }
 
+void CopyPool::copy_here(const std::vector<CopyJob> &jobs) {
+    for (const CopyJob &j : jobs)
+        if (j.n && j.rows) copy_piece(j);
+}
+
 void CopyPool::copy(const std::vector<CopyJob> &jobs) {
     std::atomic<size_t> pending{0};
     {
