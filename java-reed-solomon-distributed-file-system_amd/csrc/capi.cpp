@@ -89,8 +89,11 @@ size_t direct_min_bytes() { return rsamd::tuning_size("RSAMD_DIRECT_MIN", size_t
 
 // Bytes per shard from which a pageable call takes the mirrored pipeline
 // instead of the single zero-copy staging pass (TUNING builds:
-// RSAMD_MIRROR_MIN, read per call).
-size_t mirror_min_bytes() { return rsamd::tuning_size("RSAMD_MIRROR_MIN", size_t(256) << 10); }
+// RSAMD_MIRROR_MIN, read per call).  Below 1 MiB the pipeline's per-chunk
+// latency outweighs its overlap: 4+2 encodeParity per call, zero-copy /
+// mirrored, 256 KiB shards 84 / 181-251 us, 512 KiB 145-169 / 208-287 us;
+// even at 1 MiB (profiles/r5/host_sizes_r5u.txt, host_sizes_r5v.txt).
+size_t mirror_min_bytes() { return rsamd::tuning_size("RSAMD_MIRROR_MIN", size_t(1) << 20); }
 
 // The direct kernels' plans for columns [offset, offset+count) of the slots:
 // false (nothing enqueued) when a shard has no device address, a plan is

@@ -149,8 +149,10 @@ CopyPool &CopyPool::get() {
 // An idle thread (a worker with nothing queued, a caller waiting for its
 // batch's last pieces) polls for this long before it sleeps on a condition
 // variable: the mirrored pipeline hands the pool a batch per chunk, and a
-// sleeping thread's wake-up costs more than a small chunk's copy (TUNING
-// builds: RSAMD_POOL_SPIN_US).
+// sleeping thread's wake-up costs more than a small chunk's copy.  4+2
+// pageable encodeParity per call, 0 -> 50 us (profiles/r5/host_sizes_r5v.txt):
+// 1 MiB shards 309-378 -> 235-269 us, 2 MiB 465-547 -> 354-394, 4 MiB
+// 620-656 -> 556-567; 200 us is no better (TUNING builds: RSAMD_POOL_SPIN_US).
 template <class Ready>
 void spin_until(int us, Ready ready) {
     if (us <= 0) return;
@@ -162,7 +164,7 @@ void spin_until(int us, Ready ready) {
 }
 
 CopyPool::CopyPool(int n) {
-    spin_us_ = int(tuning_size("RSAMD_POOL_SPIN_US", 0));
+    spin_us_ = int(tuning_size("RSAMD_POOL_SPIN_US", 50));
     for (int i = 0; i < n; ++i) {
         threads_.emplace_back([this] { run(); });
         threads_.back().detach();
@@ -182,11 +184,6 @@ void CopyPool::run() {
         lock.lock();
         if (p.pending->fetch_sub(1, std::memory_order_acq_rel) == 1) done_cv_.notify_all();
     }
-}
-
-void CopyPool::copy_here(const std::vector<CopyJob> &jobs) {
-    for (const CopyJob &j : jobs)
-        if (j.n && j.rows) copy_piece(j);
 }
 
 void CopyPool::copy(const std::vector<CopyJob> &jobs) {

@@ -45,10 +45,6 @@ public:
     // threads at once.
     void copy(const std::vector<CopyJob> &jobs);
 
-    // The same copies on the calling thread alone (streaming stores as in the
-    // pool's pieces), for batches too small to be worth waking the pool.
-    static void copy_here(const std::vector<CopyJob> &jobs);
-
     int workers() const { return int(threads_.size()); }
 
 private:

@@ -422,15 +422,12 @@ int run_zero_copy(ThreadCtx *ctx, size_t buf_bytes, const ChunkIo &io, const Chu
     io(0, &in, &out);
     // Host copies on the calling thread; the copy pool only above 2 MiB (its
     // wake-up costs more than a small memcpy; TUNING builds: RSAMD_ZC_POOL_MIN).
-    // TUNING builds: RSAMD_ZC_NT=1 copies on the calling thread with the pool's
-    // streaming stores instead of memcpy.
+    // (Streaming stores on the calling thread instead of memcpy: no better,
+    // profiles/r5/host_sizes_r5v.txt.)
     const bool use_pool = buf_bytes > tuning_size("RSAMD_ZC_POOL_MIN", size_t(2) << 20);
-    const bool nt = tuning_size("RSAMD_ZC_NT", 0) != 0;
     auto copy = [&](const std::vector<rsamd::CopyJob> &jobs) {
         if (use_pool) {
             rsamd::CopyPool::get().copy(jobs);
-        } else if (nt) {
-            rsamd::CopyPool::copy_here(jobs);
         } else {
             for (const rsamd::CopyJob &j : jobs) std::memcpy(j.dst, j.src, j.n);
         }

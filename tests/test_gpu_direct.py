@@ -312,10 +312,11 @@ def test_direct_file_interior_threads(gpu, oracle_lib):
     assert not errors, errors
 
 
-@pytest.mark.parametrize("n,off", [((64 << 10) + 4100, 3), ((256 << 10) + 8200, 3), ((1 << 20) + 7, 4095), (5 << 20, 0)])
+@pytest.mark.parametrize("n,off", [((64 << 10) + 4100, 3), ((256 << 10) + 8200, 3), ((1 << 20) + 7, 4095),
+                                   ((1 << 20) + 8200, 3), (5 << 20, 0)])
 def test_direct_interior_and_ends(gpu, oracle_lib, n, off):
     """Pageable calls at ragged offsets and lengths (the mirrored pipeline's
-    ramped chunks, or the zero-copy pass under 256 KiB per shard).  Encode,
+    ramped chunks from 1 MiB per shard, or the zero-copy pass below).  Encode,
     decode and verify must be exact at both ends and inside, and a wrong
     parity byte is found wherever it is."""
     import rsamd

@@ -69,7 +69,7 @@ def test_file_paths_random(gpu, oracle_lib, case):
 @pytest.mark.parametrize("case", range(10))
 def test_file_host_random_large(gpu, oracle_lib, case):
     """Host file calls at sizes that take the mirrored pipeline (shards of
-    256 KiB and more): pageable file, shards and output, each a view at a
+    1 MiB and more): pageable file, shards and output, each a view at a
     random offset (8-byte aligned, or not for one case in four), split and
     merged on the host around the GPU's coding (capi.cpp file_encode_mirrored /
     file_decode_mirrored); random k, m, block and erasures, against the
@@ -80,7 +80,7 @@ def test_file_host_random_large(gpu, oracle_lib, case):
     k = int(rng.integers(1, 11))
     m = int(rng.integers(0, 5))
     block = int(rng.choice([1000, 8, 4096, 520, 24, 1000]))
-    n = int(rng.integers(max(1, k) * (256 << 10), max(1, k) * (1 << 20)))
+    n = int(rng.integers(max(1, k) * (1 << 20), max(1, k) * (3 << 20)))
     step = 1 if case % 4 == 3 else 8
 
     def view(size):

@@ -76,6 +76,7 @@ class Jvm:
     def __init__(self, lib):
         self.lib = lib
         lib.mock_reset()
+        lib.mock_file_record((C.c_int64 * 129)(), 129)  # drop earlier tests' file-call records
 
     def bytes(self, arr):
         arr = np.ascontiguousarray(arr, dtype=np.uint8)
