@@ -558,39 +558,12 @@ int file_encode_direct(const Codec &c, const uint8_t *file, size_t file_len, siz
         d.tabs = plans[0].tabs;
     }
     if (!rsamd::file_direct_ok(d)) return RS_OK;
-    // The host split is the slower side (it reads and writes every data byte;
-    // the link carries the file up and the parity down), so the kernel also
-    // writes the data shards of the first `ra` block rows into the caller's
-    // pinned shards, and the host splits the rest beside it (TUNING builds:
-    // RSAMD_FILE_GPU_ROWS_PCT, the kernel's share of the rows).
-    const size_t rows = S / blk, kb = size_t(c.k()) * blk;
-    size_t ra = c.m() > 0 ? rows * std::min<size_t>(rsamd::tuning_size("RSAMD_FILE_GPU_ROWS_PCT", 0), 100) / 100 : 0;
-    rsamd::FileDirect a = d, b = d;
-    if (ra > 0) {
-        for (int i = 0; i < c.k(); ++i)
-            if (!(a.out[i] = host_dev_addr(shards[i]))) ra = 0;
-    }
-    if (ra > 0) {
-        a.units = ra * blk / 8;
-        a.file_len = std::min(file_len, ra * kb);
-        b.file = d.file + ra * kb;
-        for (int i = c.k(); i < c.total(); ++i) b.out[i] = d.out[i] + ra * blk;
-        b.units = (rows - ra) * blk / 8;
-        b.file_len = file_len - a.file_len;
-        if (!rsamd::file_direct_ok(a) || !rsamd::file_direct_ok(b)) ra = 0;
-    }
     bounds::allow(d.file, file_len);
-    for (int i = 0; i < c.total(); ++i)
-        if (i >= c.k() || ra > 0) bounds::allow(i < c.k() ? a.out[i] : d.out[i], S);
-    if (ra > 0) {
-        RS_HIP(rsamd::launch_file_encode_direct(a, ctx->stream));
-        RS_HIP(rsamd::launch_file_encode_direct(b, ctx->stream));
-    } else if (c.m() > 0) {
-        RS_HIP(rsamd::launch_file_encode_direct(d, ctx->stream));
-    }
+    for (int i = c.k(); i < c.total(); ++i) bounds::allow(d.out[i], S);
+    if (c.m() > 0) RS_HIP(rsamd::launch_file_encode_direct(d, ctx->stream));
     *taken = true;
     std::vector<rsamd::CopyJob> jobs;
-    split_jobs(file, file_len, blk, c.k(), shards, nullptr, 0, ra, rows, &jobs);
+    split_jobs(file, file_len, blk, c.k(), shards, nullptr, 0, 0, S / blk, &jobs);
     rsamd::CopyPool::get().copy(jobs);
     RS_HIP(hipStreamSynchronize(ctx->stream));
     return RS_OK;
