@@ -20,6 +20,9 @@ def main():
     ap.add_argument("--calls", type=int, default=10)
     a = ap.parse_args()
     import numpy as np
+    from rsamd import _lib
+    if os.environ.get("RSAMD_TEST_LIB"):
+        _lib.LIB_PATH = os.path.abspath(os.environ["RSAMD_TEST_LIB"])
     import rsamd
     from rsamd.device import HostBuffer
     from rsamd.layout import file_encode_into, file_layout
@@ -36,7 +39,7 @@ def main():
     for _ in range(a.calls):
         file_encode_into(rs, f.array, views)
     t = (time.perf_counter() - t0) / a.calls
-    print(json.dumps({"file_MiB": n >> 20, "calls": a.calls, "ms_per_call": round(t * 1e3, 3),
+    print(json.dumps({"env": {x: os.environ[x] for x in os.environ if x.startswith("RSAMD_")}, "file_MiB": n >> 20, "calls": a.calls, "ms_per_call": round(t * 1e3, 3),
                       "GiBps": round(n / t / 2**30, 2)}), flush=True)
 
 
