@@ -830,22 +830,64 @@ __device__ __forceinline__ uint64_t rotated_column(uint64_t u, const FileDirect 
 }
 
 template <int M>
+__device__ __forceinline__ void file_direct_unit(const FileDirect &a, uint64_t c) {
+    const uint64_t r = c / a.block, w = c - r * a.block;
+    uint32_t lo[M > 0 ? M : 1] = {}, hi[M > 0 ? M : 1] = {};
+    for (int i = 0; i < a.k; ++i) {
+        const uint64_t x = load_run8(a.file, (r * uint64_t(a.k) + uint64_t(i)) * a.block + w, a.file_len);
+        if (a.out[i])  // (null: the caller splits the data shards on the host, capi.cpp file_encode_direct)
+            __builtin_nontemporal_store(x, reinterpret_cast<uint64_t *>(RSAMD_G(a.out[i] + c, 8)));
+#pragma unroll
+        for (int p = 0; p < M; ++p) fold_unit(a.tabs + (i * M + p) * 5, x, lo[p], hi[p]);
+    }
+#pragma unroll
+    for (int p = 0; p < M; ++p)
+        __builtin_nontemporal_store(uint64_t(lo[p]) | (uint64_t(hi[p]) << 32),
+                                    reinterpret_cast<uint64_t *>(RSAMD_G(a.out[a.k + p] + c, 8)));
+}
+
+template <int M>
 __global__ void __launch_bounds__(kThreads) file_direct_encode_kernel(FileDirect a) {
     const uint64_t step = uint64_t(gridDim.x) * kThreads;
-    for (uint64_t u = uint64_t(blockIdx.x) * kThreads + threadIdx.x; u < a.units; u += step) {
-        const uint64_t c = rotated_column(u, a), r = c / a.block, w = c - r * a.block;
-        uint32_t lo[M > 0 ? M : 1] = {}, hi[M > 0 ? M : 1] = {};
-        for (int i = 0; i < a.k; ++i) {
-            const uint64_t x = load_run8(a.file, (r * uint64_t(a.k) + uint64_t(i)) * a.block + w, a.file_len);
-            if (a.out[i])  // (null: the caller splits the data shards on the host, capi.cpp file_encode_direct)
-                __builtin_nontemporal_store(x, reinterpret_cast<uint64_t *>(RSAMD_G(a.out[i] + c, 8)));
+    for (uint64_t u = uint64_t(blockIdx.x) * kThreads + threadIdx.x; u < a.units; u += step)
+        file_direct_unit<M>(a, rotated_column(u, a));
+}
+
+// Tiled form: a workgroup takes tile_rows block rows, loads their file bytes
+// (one contiguous run of tile_rows * k * block bytes, 64-byte aligned when the
+// file is) into LDS with coalesced 8-byte loads, then codes the tile's columns
+// from LDS and writes each output's tile_rows * block bytes as one run.  Over
+// the link every read and write is then whole 64-byte lines: 1000-byte blocks
+// had cut the column order's runs at every block edge (44.5 GiB/s against 51
+// for 1024-byte blocks, profiles/r5/pfile_block_r5z.txt).  4+2, 256 MiB pinned
+// file, 1000-byte blocks: 44.4 -> 51.2-51.7 GiB/s, 0.98 of the link bound
+// (profiles/r5/pfile_tiled_r5z.txt).
+template <int M>
+__global__ void __launch_bounds__(kThreads) file_direct_tiled_kernel(FileDirect a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t tile_bytes[];  // tile_rows * k * block bytes
+    uint64_t *tile = reinterpret_cast<uint64_t *>(tile_bytes);
+    const uint64_t kb = uint64_t(a.k) * a.block, rows = a.units * 8 / a.block;
+    const uint64_t ntiles = (rows + a.tile_rows - 1) / a.tile_rows;
+    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint64_t r0 = t * a.tile_rows, nr = min(a.tile_rows, rows - r0);
+        __syncthreads();  // the previous tile's LDS reads are done
+        for (uint64_t q = threadIdx.x; q < nr * kb / 8; q += kThreads)
+            tile[q] = load_run8(a.file, r0 * kb + q * 8, a.file_len);  // (zeros past the file: its padding)
+        __syncthreads();
+        for (uint64_t u = threadIdx.x; u < nr * a.block / 8; u += kThreads) {
+            const uint64_t cl = u * 8, r = cl / a.block, w = cl - r * a.block, c = r0 * a.block + cl;
+            uint32_t lo[M > 0 ? M : 1] = {}, hi[M > 0 ? M : 1] = {};
+            for (int i = 0; i < a.k; ++i) {
+                const uint64_t x = tile[((r * uint64_t(a.k) + uint64_t(i)) * a.block + w) / 8];
+                if (a.out[i]) __builtin_nontemporal_store(x, reinterpret_cast<uint64_t *>(RSAMD_G(a.out[i] + c, 8)));
 #pragma unroll
-            for (int p = 0; p < M; ++p) fold_unit(a.tabs + (i * M + p) * 5, x, lo[p], hi[p]);
+                for (int p = 0; p < M; ++p) fold_unit(a.tabs + (i * M + p) * 5, x, lo[p], hi[p]);
+            }
+#pragma unroll
+            for (int p = 0; p < M; ++p)
+                __builtin_nontemporal_store(uint64_t(lo[p]) | (uint64_t(hi[p]) << 32),
+                                            reinterpret_cast<uint64_t *>(RSAMD_G(a.out[a.k + p] + c, 8)));
         }
-#pragma unroll
-        for (int p = 0; p < M; ++p)
-            __builtin_nontemporal_store(uint64_t(lo[p]) | (uint64_t(hi[p]) << 32),
-                                        reinterpret_cast<uint64_t *>(RSAMD_G(a.out[a.k + p] + c, 8)));
     }
 }
 
@@ -863,6 +905,19 @@ unsigned file_direct_grid(uint64_t units) {
 }
 
 }  // namespace
+
+// Block rows per workgroup of the tiled kernel: as many as fit 64 KiB of LDS,
+// rounded down to a multiple that keeps every tile's runs on 64-byte lines
+// (1000-byte blocks, k = 4: 16 rows, 64000 bytes); 0 (the column kernel) when
+// not one row fits.  TUNING builds: RSAMD_FILE_DIRECT_TILE=0 turns it off.
+static uint64_t file_tile_rows(int k, uint64_t block) {
+    if (!tuning_size("RSAMD_FILE_DIRECT_TILE", 1)) return 0;
+    const uint64_t kb = uint64_t(k) * block, fit = (uint64_t(64) << 10) / kb;
+    uint64_t g = 64, b = block;
+    while (b) { const uint64_t t = g % b; g = b; b = t; }  // gcd(64, block)
+    const uint64_t align = 64 / g;
+    return fit >= align ? fit / align * align : fit;
+}
 
 bool file_direct_ok(const FileDirect &d) {
     bool ok = d.k >= 1 && d.k <= kMaxDirectIn && d.nout >= 0 && d.nout <= kMaxOut && d.block >= 8 &&
@@ -892,6 +947,20 @@ hipError_t launch_file_encode_direct(const FileDirect &d0, hipStream_t s) {
     if (d0.units == 0) return hipSuccess;
     FileDirect d = d0;
     d.rot = file_direct_rot(d);
+    d.tile_rows = file_tile_rows(d.k, d.block);
+    if (d.tile_rows) {
+        const uint64_t rows = d.units * 8 / d.block, ntiles = (rows + d.tile_rows - 1) / d.tile_rows;
+        const dim3 grid(unsigned(std::min<uint64_t>(ntiles, tuning_size("RSAMD_FILE_TILE_BLOCKS", 512))));
+        const size_t lds = size_t(d.tile_rows * d.k * d.block);
+        switch (d.nout) {
+        case 0: hipLaunchKernelGGL((file_direct_tiled_kernel<0>), grid, dim3(kThreads), lds, s, d); break;
+        case 1: hipLaunchKernelGGL((file_direct_tiled_kernel<1>), grid, dim3(kThreads), lds, s, d); break;
+        case 2: hipLaunchKernelGGL((file_direct_tiled_kernel<2>), grid, dim3(kThreads), lds, s, d); break;
+        case 3: hipLaunchKernelGGL((file_direct_tiled_kernel<3>), grid, dim3(kThreads), lds, s, d); break;
+        default: hipLaunchKernelGGL((file_direct_tiled_kernel<4>), grid, dim3(kThreads), lds, s, d); break;
+        }
+        return hipGetLastError();
+    }
     const dim3 grid(file_direct_grid(d.units));
     switch (d.nout) {
     case 0: hipLaunchKernelGGL((file_direct_encode_kernel<0>), grid, dim3(kThreads), 0, s, d); break;

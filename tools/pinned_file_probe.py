@@ -18,6 +18,7 @@ sys.path.insert(0, os.path.join(ROOT, "java-reed-solomon-distributed-file-system
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=10)
+    ap.add_argument("--block", type=int, default=1000)
     a = ap.parse_args()
     import numpy as np
     from rsamd import _lib
@@ -30,16 +31,16 @@ def main():
     rs = rsamd.ReedSolomon.create(k, m)
     f = HostBuffer(n)
     f.array[:] = np.random.default_rng(1).integers(0, 256, n, dtype=np.uint8)
-    _, S = file_layout(rs, n)
+    _, S = file_layout(rs, n, a.block)
     sh = [HostBuffer(S) for _ in range(k + m)]
     views = [b.array for b in sh]
     for _ in range(3):
-        file_encode_into(rs, f.array, views)
+        file_encode_into(rs, f.array, views, a.block)
     t0 = time.perf_counter()
     for _ in range(a.calls):
-        file_encode_into(rs, f.array, views)
+        file_encode_into(rs, f.array, views, a.block)
     t = (time.perf_counter() - t0) / a.calls
-    print(json.dumps({"env": {x: os.environ[x] for x in os.environ if x.startswith("RSAMD_")}, "file_MiB": n >> 20, "calls": a.calls, "ms_per_call": round(t * 1e3, 3),
+    print(json.dumps({"env": {x: os.environ[x] for x in os.environ if x.startswith("RSAMD_")}, "file_MiB": n >> 20, "block": a.block, "calls": a.calls, "ms_per_call": round(t * 1e3, 3),
                       "GiBps": round(n / t / 2**30, 2)}), flush=True)
 
 
