@@ -683,41 +683,10 @@ int file_decode_pinned(const Codec &c, uint8_t *const *shards, const uint8_t *pr
     for (const rsamd::DirectPlan &d : dp) {
         for (int i = 0; i < d.nin; ++i) bounds::allow(d.in[i], n);
         for (int q = 0; q < d.nout; ++q) bounds::allow(d.out[q], n);
-    }
-    // The rebuild runs in pieces of block rows, an event after each, so the
-    // rebuilt data shards' rows are merged as their piece lands instead of all
-    // after the last kernel (the present shards are merged first, beside the
-    // kernels).  About 8 MiB of rows per piece, at most 8 pieces (TUNING
-    // builds: RSAMD_DECODE_PIECES).
-    const size_t want = std::max<size_t>(1, std::min<size_t>(8, n / (size_t(8) << 20)));
-    const size_t pieces = dp.empty() ? 1 : std::min(rows_needed, std::max<size_t>(1, rsamd::tuning_size("RSAMD_DECODE_PIECES", want)));
-    std::vector<size_t> pb(pieces + 1);
-    for (size_t j = 0; j <= pieces; ++j) pb[j] = rows_needed * j / pieces;
-    std::vector<hipEvent_t> ev(dp.empty() ? 0 : pieces, nullptr);
-    auto destroy = [&]() {
-        for (hipEvent_t &e : ev)
-            if (e) (void)hipEventDestroy(e);
-    };
-    for (size_t j = 0; j < ev.size(); ++j) {
-        if (hipEventCreateWithFlags(&ev[j], hipEventDisableTiming) != hipSuccess) {
-            destroy();
-            return hip_fail(hipGetLastError(), "hipEventCreateWithFlags");
-        }
-        const size_t off = pb[j] * blk, len = (pb[j + 1] - pb[j]) * blk;
-        for (const rsamd::DirectPlan &d : dp) {
-            rsamd::DirectPlan dj = d;
-            for (int i = 0; i < dj.nin; ++i) dj.in[i] += off;
-            for (int q = 0; q < dj.nout; ++q) dj.out[q] += off;
-            const hipError_t e = rsamd::launch_gf_direct(dj, len, Mode::Code, nullptr, ctx->stream);
-            if (e != hipSuccess) {
-                (void)hipStreamSynchronize(ctx->stream);
-                destroy();
-                return hip_fail(e, "launch_gf_direct");
-            }
-        }
-        (void)hipEventRecord(ev[j], ctx->stream);
+        RS_HIP(rsamd::launch_gf_direct(d, n, Mode::Code, nullptr, ctx->stream));
     }
     *taken = true;
+    std::vector<const uint8_t *> src(shards, shards + k);
     std::vector<bool> now(static_cast<size_t>(k), false), later(static_cast<size_t>(k), false);
     for (int d = 0; d < k; ++d) {
         if (present[d])
@@ -726,24 +695,13 @@ int file_decode_pinned(const Codec &c, uint8_t *const *shards, const uint8_t *pr
             later[d] = true;
     }
     std::vector<rsamd::CopyJob> jobs;
-    std::vector<const uint8_t *> src(shards, shards + k);
     merge_jobs(k, blk, file_out, file_size, src.data(), now, 0, rows_needed, &jobs);
     rsamd::CopyPool::get().copy(jobs);
-    int rc = RS_OK;
-    for (size_t j = 0; j < ev.size() && rc == RS_OK; ++j) {
-        const hipError_t e = hipEventSynchronize(ev[j]);
-        if (e != hipSuccess) {
-            rc = hip_fail(e, "hipEventSynchronize");
-            break;
-        }
-        for (int d = 0; d < k; ++d) src[d] = shards[d] + pb[j] * blk;  // (merge_jobs: src at row r0)
-        jobs.clear();
-        merge_jobs(k, blk, file_out, file_size, src.data(), later, pb[j], pb[j + 1], &jobs);
-        rsamd::CopyPool::get().copy(jobs);
-    }
-    (void)hipStreamSynchronize(ctx->stream);
-    destroy();
-    return rc;
+    RS_HIP(hipStreamSynchronize(ctx->stream));
+    jobs.clear();
+    merge_jobs(k, blk, file_out, file_size, src.data(), later, 0, rows_needed, &jobs);
+    rsamd::CopyPool::get().copy(jobs);
+    return RS_OK;
 }
 
 // Block rows a file decode must code: all of them when a shard is rebuilt,
