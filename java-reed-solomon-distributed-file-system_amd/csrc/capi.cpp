@@ -530,6 +530,28 @@ void merge_jobs(int k, size_t blk, uint8_t *file_out, size_t file_size, const ui
     }
 }
 
+// Data shard d's rows [a0, a1) copied from src to dst (both at row a0) and
+// merged into the file in the same pass: each row is read once and written
+// twice (ReedSolomonDecoder.java:92-103's merge; the rows whose file block is
+// cut by the file's end, or lies past it, get their file bytes clipped).
+void tee_jobs(int k, size_t blk, uint8_t *file_out, size_t file_size, int d, const uint8_t *src, uint8_t *dst,
+              size_t a0, size_t a1, std::vector<rsamd::CopyJob> *jobs) {
+    const size_t kb = size_t(k) * blk, lead = size_t(d + 1) * blk;
+    const size_t whole_rows = file_size >= lead ? (file_size - lead) / kb + 1 : 0;  // rows with a whole file block
+    const size_t w1 = std::min(a1, std::max(a0, whole_rows));
+    if (w1 > a0) {
+        rsamd::CopyJob j{dst, src, blk, w1 - a0, blk, blk};
+        j.dst2 = file_out + (a0 * size_t(k) + size_t(d)) * blk;
+        j.dst2_stride = kb;
+        jobs->push_back(j);
+    }
+    if (a1 > w1) {
+        jobs->push_back({dst + (w1 - a0) * blk, src + (w1 - a0) * blk, (a1 - w1) * blk});
+        const size_t f0 = (w1 * size_t(k) + size_t(d)) * blk;
+        if (f0 < file_size) jobs->push_back({file_out + f0, src + (w1 - a0) * blk, std::min(blk, file_size - f0)});
+    }
+}
+
 // Direct path of the host file calls on caller-pinned memory (layout.hpp
 // FileDirect): the fused kernel reads the file in place across the link and
 // writes the parity shards in place, while the copy pool splits the file into
@@ -775,13 +797,32 @@ int file_decode_mirrored(const Codec &c, uint8_t *const *shards, const uint8_t *
         *taken = true;
         return RS_OK;
     }
+    // Data shards go to the file in the pass that moves them anyway (TUNING
+    // builds: RSAMD_DECODE_TEE=0 merges them in a pass of their own): present
+    // ones from the caller's arrays into their slots and the file, rebuilt ones
+    // from their slots into the caller's arrays and the file.
+    const bool tee = rsamd::tuning_size("RSAMD_DECODE_TEE", 1) != 0;
     auto io = [&](size_t j, std::vector<Xfer> *in, std::vector<Xfer> *out) {
         const size_t r0 = cb[j], n = (cb[j + 1] - r0) * blk;
-        for (int sidx : surv) in->push_back({shards[sidx] + r0 * blk, size_t(sidx) * ss, n});
-        for (int sidx : missing) out->push_back({shards[sidx] + r0 * blk, size_t(sidx) * ss, n});
+        for (int sidx : surv)
+            if (!tee || sidx >= k) in->push_back({shards[sidx] + r0 * blk, size_t(sidx) * ss, n});
+        for (int sidx : missing)
+            if (!tee || sidx >= k) out->push_back({shards[sidx] + r0 * blk, size_t(sidx) * ss, n});
     };
-    auto side = [&](size_t j, uint8_t *slot, std::vector<rsamd::CopyJob> *, std::vector<rsamd::CopyJob> *after) {
-        merge(cb[j], cb[j + 1], slot, after);
+    auto side = [&](size_t j, uint8_t *slot, std::vector<rsamd::CopyJob> *before, std::vector<rsamd::CopyJob> *after) {
+        const size_t r0 = cb[j], r1 = cb[j + 1];
+        if (!tee) return merge(r0, r1, slot, after);
+        const size_t rb = row_block() ? row_block() : std::max<size_t>(1, r1 - r0);
+        for (size_t b0 = r0; b0 < r1; b0 += rb) {  // blocks of rows, every shard's jobs of a block together
+            const size_t b1 = std::min(r1, b0 + rb);
+            for (int d = 0; d < k; ++d) {
+                uint8_t *mine = shards[d] + b0 * blk, *sl = slot + size_t(d) * ss + (b0 - r0) * blk;
+                if (present[d])
+                    tee_jobs(k, blk, file_out, file_size, d, mine, sl, b0, b1, before);
+                else
+                    tee_jobs(k, blk, file_out, file_size, d, sl, mine, b0, b1, after);
+            }
+        }
     };
     auto code = [&](size_t j, uint8_t *dev, hipStream_t st) -> int {
         return code_slots(plans, plan->in_idx(), plan->out_idx(), dev, ss, (cb[j + 1] - cb[j]) * blk, Mode::Code,
