@@ -126,6 +126,11 @@ void copy_piece(const CopyJob &j) {
     if (gathers(j.dst_stride) && (!d2 || gathers(j.dst2_stride))) {
         gather_stream(d, s, j.n, j.rows, j.src_stride);
         if (d2) gather_stream(d2, s, j.n, j.rows, j.src_stride);  // the source again, from this core's cache
+    } else if (s && d2 && j.rows > 1 && j.src_stride == j.n && j.dst_stride == j.n && use_stream()) {
+        // a contiguous run teed into rows (a decode's data shard into its slot
+        // and the file): the run in one stream, then the rows from this core's cache
+        copy_stream(d, s, j.n * j.rows);
+        for (size_t r = 0; r < j.rows; ++r) copy_row(d2 + r * j.dst2_stride, s + r * j.n, j.n);
     } else {
         for (size_t r = 0; r < j.rows; ++r) {
             const uint8_t *src = s ? s + r * j.src_stride : nullptr;

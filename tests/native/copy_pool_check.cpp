@@ -38,6 +38,27 @@ int main() {  // copy_pool.cpp gathers, tees, zero fills: every byte against a p
         }
         if (dst[doff + n * rows] != 0xEE || (doff && dst[doff - 1] != 0xEE)) { ++bad; printf("overrun n=%zu\n", n); }
     }
+    // a contiguous run teed into strided rows (a decode's data shard into its
+    // slot and the file): every byte of both destinations, nothing past them
+    for (int it = 0; it < 600; ++it) {
+        const size_t n = 8 + rng() % 3000, rows = 1 + rng() % 400, d2stride = n + rng() % 5000;
+        const size_t soff = rng() % 64, doff = rng() % 64, d2off = rng() % 64;
+        std::vector<uint8_t> src(soff + n * rows), dst(doff + n * rows + 64, 0xEE), dst2(d2off + d2stride * rows + 64, 0xDD);
+        for (auto &b : src) b = uint8_t(rng());
+        rsamd::CopyJob j{dst.data() + doff, src.data() + soff, n, rows, n, n};
+        j.dst2 = dst2.data() + d2off;
+        j.dst2_stride = d2stride;
+        rsamd::CopyPool::get().copy({j});
+        ++cases;
+        if (memcmp(dst.data() + doff, src.data() + soff, n * rows) || dst[doff + n * rows] != 0xEE) {
+            ++bad;
+            printf("tee run n=%zu rows=%zu\n", n, rows);
+        }
+        for (size_t r = 0; r < rows; ++r) {
+            if (memcmp(dst2.data() + d2off + r * d2stride, src.data() + soff + r * n, n)) { ++bad; printf("tee rows n=%zu r=%zu\n", n, r); break; }
+            if (r + 1 < rows && d2stride > n && dst2[d2off + r * d2stride + n] != 0xDD) { ++bad; printf("tee gap n=%zu\n", n); break; }
+        }
+    }
     // concurrent callers: 6 threads x 300 batches of 1-6 jobs, 1 B to 3 MiB each
     std::atomic<int> cbad{0}, ccases{0};
     std::vector<std::thread> ts;
