@@ -151,3 +151,45 @@ def test_file_host_odd_blocks_pageable_and_pinned(gpu, oracle_lib, case):
         file_decode_into(rs, sh, [i not in miss for i in range(k + m)], S, out, block)
         assert_same([out], [f], (k, m, block, n, miss, pinned))
         assert_same(sh, ref, (k, m, block, n, miss, pinned))
+
+
+PINNED_GEOMS = [(4, 2, 1000), (1, 1, 8), (10, 4, 1000), (3, 3, 520), (6, 1, 4096), (2, 4, 24), (7, 2, 8192),
+                (5, 3, 16), (4, 2, 1000), (9, 4, 4096), (1, 4, 1000), (8, 2, 8), (4, 1, 65536), (2, 2, 40000)]
+
+
+@pytest.mark.parametrize("case", range(len(PINNED_GEOMS)))
+def test_file_pinned_random(gpu, oracle_lib, case):
+    """Files and shards in the library's pinned buffers (rs_host_alloc): the
+    encode's tiled kernel (layout.hip file_direct_tiled_kernel; 64 KiB of
+    block rows per workgroup, one row when a row is larger, the column kernel
+    past that) across k, m and block sizes, then a decode with random
+    erasures, against the oracle."""
+    import rsamd
+    from rsamd.device import HostBuffer
+    from rsamd.layout import file_decode_into, file_encode_into, file_layout
+    k, m, block = PINNED_GEOMS[case]
+    rng = np.random.default_rng(9700 + case)
+    kb = k * block
+    n = int(rng.integers(kb, max(kb + 1, 3_000_000 // kb * kb))) + int(rng.integers(0, 2)) * kb * 40
+    rs = rsamd.ReedSolomon.create(k, m)
+    oc = oracle_lib.Codec(k, m)
+    _, S = file_layout(rs, n, block)
+    f = HostBuffer(n)
+    f.array[:] = rng.integers(0, 256, n, dtype=np.uint8)
+    sh = [HostBuffer(S) for _ in range(k + m)]
+    views = [b.array for b in sh]
+    for v in views:
+        v[:] = 0xEE
+    file_encode_into(rs, f.array, views, block)
+    ref = oc.file_encode(f.array.tobytes(), block)
+    assert_same(views, list(ref), (k, m, block, n))
+    e = int(rng.integers(1, m + 1))
+    miss = sorted(int(x) for x in rng.choice(k + m, e, replace=False))
+    for j in miss:
+        views[j][:] = 0
+    out = HostBuffer(n)
+    file_decode_into(rs, views, [i not in miss for i in range(k + m)], S, out.array, block)
+    assert np.array_equal(out.array, f.array), (k, m, block, n, miss)
+    assert_same(views, list(ref), (k, m, block, n, miss))
+    for b in sh + [f, out]:
+        b.free()
