@@ -203,3 +203,43 @@ def test_direct_buffers_through_shim(gpu, oracle_lib, native, jvm):
         jvm.assert_clean()
     finally:
         native.rs_codec_destroy(h)
+
+
+def test_pageable_direct_buffers_through_shim(gpu, oracle_lib, native, jvm):
+    """ByteBuffer.allocateDirect-style buffers (pageable C memory, here NumPy
+    arrays) through the ByteBuffer overloads: the mirrored pipeline, same
+    bytes as the oracle."""
+    k, m, n = 4, 2, (3 << 20) + 40
+    h = C.c_void_p()
+    assert native.rs_codec_create(k, m, C.byref(h)) == 0
+    try:
+        rng = np.random.default_rng(6)
+        bufs = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)] + [np.zeros(n, np.uint8) for _ in range(m)]
+        ref = [b.copy() for b in bufs]
+        oracle_lib.Codec(k, m).encode_parity(ref, 0, n)
+        jvm.lib.mock_encode_parity_direct(1, h, jvm.objects([jvm.direct(b) for b in bufs]), 0, n)
+        assert jvm.exception() == ("", "")
+        assert all(np.array_equal(b, r) for b, r in zip(bufs, ref))
+        for j in (1, 4):
+            bufs[j][:] = 0
+        jvm.lib.mock_decode_missing_direct(1, h, jvm.objects([jvm.direct(b) for b in bufs]),
+                                           jvm.bools([j not in (1, 4) for j in range(6)]), 0, n)
+        assert jvm.exception() == ("", "")
+        assert all(np.array_equal(b, r) for b, r in zip(bufs, ref))
+        flen = 4 * n - 3
+        f = rng.integers(0, 256, flen + 9, dtype=np.uint8)  # capacity past the file
+        S = -(-flen // 4000) * 1000
+        fsh = [np.zeros(S, np.uint8) for _ in range(k + m)]
+        jvm.lib.mock_file_encode_direct(1, h, jvm.direct(f), flen, 1000, jvm.objects([jvm.direct(b) for b in fsh]))
+        assert jvm.exception() == ("", "")
+        want = oracle_lib.Codec(k, m).file_encode(f[:flen].tobytes(), 1000)
+        assert all(np.array_equal(b, w) for b, w in zip(fsh, want))
+        out = np.zeros(flen, np.uint8)
+        fsh[2][:] = 0
+        jvm.lib.mock_file_decode_direct(1, h, jvm.objects([jvm.direct(b) for b in fsh]),
+                                        jvm.bools([j != 2 for j in range(6)]), S, 1000, jvm.direct(out), flen)
+        assert jvm.exception() == ("", "")
+        assert np.array_equal(out, f[:flen])
+        jvm.assert_clean()
+    finally:
+        native.rs_codec_destroy(h)
