@@ -1029,6 +1029,101 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MS >
     }
 }
 
+// Span-owner kernel (uniform plans; A/B against the line-owner kernel above):
+// a workgroup owns `groups` consecutive chunk groups whose bytes fill whole
+// 128-byte lines (4+2 x 1000 B: 8 groups, 48000 bytes, 375 lines), so every
+// line it reads or writes is its own.  Phase 0 loads, as 16-byte pieces, the
+// lines holding survivor bytes and, of the lines it will write, the bytes of
+// shards it does not rebuild; phase 1 codes 8-byte columns from LDS into the
+// output shards' places in LDS; phase 2 stores every line that holds an
+// output byte whole.  No foreign bytes, no per-wave phases: four waves share
+// each phase.
+struct SpanArgs {
+    uint8_t *lo, *hi;       // the batch's bytes: [lo, hi), lo 128-aligned
+    uint32_t len, total;    // shard length (a multiple of 8), shards per group
+    uint32_t glen;          // total * len
+    uint32_t groups;        // groups per span (groups * glen a multiple of 128)
+    uint64_t n_spans;
+    uint32_t in_mask, out_mask;  // survivors, outputs (bit s = shard s)
+    const uint32_t *tabs;   // tabs[4][MS][5]
+    const int32_t *in_idx, *out_idx;
+};
+
+template <int MS>
+__global__ void __launch_bounds__(kThreads) gf_span_kernel(SpanArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr int K = 4;
+    const uint32_t span = a.groups * a.glen;
+    int sidx[K], oidx[MS];
+#pragma unroll
+    for (int i = 0; i < K; ++i) sidx[i] = *RSAMD_G(a.in_idx + i, 4);
+#pragma unroll
+    for (int p = 0; p < MS; ++p) oidx[p] = *RSAMD_G(a.out_idx + p, 4);
+    const __attribute__((address_space(4))) uint32_t *ctabs =
+        (const __attribute__((address_space(4))) uint32_t *)(RSAMD_G(a.tabs, K * MS * 20));
+    // shard role of span offset o: bit 0 survivor, bit 1 output
+    auto role = [&](uint32_t o) -> uint32_t {
+        const uint32_t sh = (o % a.glen) / a.len;
+        return ((a.in_mask >> sh) & 1u) | (((a.out_mask >> sh) & 1u) << 1);
+    };
+    for (uint64_t w = blockIdx.x; w < a.n_spans; w += gridDim.x) {
+        uint8_t *sp = a.lo + w * uint64_t(span);
+        const uint32_t nb = uint32_t(min(uint64_t(span), uint64_t(a.hi - sp)));  // a multiple of 8
+        __syncthreads();  // the previous span's stores have read LDS
+        for (uint32_t q = threadIdx.x * 16u; q < nb; q += kThreads * 16u) {
+            const uint32_t l0 = q & ~127u, l1 = min(l0 + 127u, nb - 1u);
+            const bool written = ((role(l0) | role(l1)) & 2u) != 0;
+            const uint32_t r0 = role(q), r1 = q + 8u < nb ? role(q + 8u) : 2u;  // (past the batch: as an output, not loaded)
+            const bool need0 = (r0 & 1u) || (written && !(r0 & 2u));
+            const bool need1 = (r1 & 1u) || (written && !(r1 & 2u));
+            if (need0 && need1) {
+                *reinterpret_cast<u32x4 *>(lds + q) = load_stream(sp + q);
+            } else if (need0) {
+                *reinterpret_cast<u32x2a *>(lds + q) = *reinterpret_cast<const u32x2a *>(RSAMD_G(sp + q, 8));
+            } else if (need1) {
+                *reinterpret_cast<u32x2a *>(lds + q + 8u) = *reinterpret_cast<const u32x2a *>(RSAMD_G(sp + q + 8u, 8));
+            }
+        }
+        __syncthreads();
+        const uint32_t nw = a.len / 8u, units = nb / a.glen * nw;
+        for (uint32_t u = threadIdx.x; u < units; u += kThreads) {
+            const uint32_t j = u / nw, v = u - j * nw, gb = j * a.glen + 8u * v;
+            u32x2a x[K];
+#pragma unroll
+            for (int i = 0; i < K; ++i) x[i] = *reinterpret_cast<const u32x2a *>(lds + gb + uint32_t(sidx[i]) * a.len);
+            uint32_t acc[MS][2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    const Sel sl = selectors(x[i][h]);
+#pragma unroll
+                    for (int p = 0; p < MS; ++p) {
+                        uint32_t t0, t1, t2, tp[5];
+#pragma unroll
+                        for (int jj = 0; jj < 5; ++jj) tp[jj] = ctabs[(i * MS + p) * 5 + jj];
+                        terms(tp, sl, t0, t1, t2);
+                        acc[p][h] = i == 0 ? xor3(t0, t1, t2) : xor3(acc[p][h], t0, t1) ^ t2;
+                    }
+                }
+            }
+#pragma unroll
+            for (int p = 0; p < MS; ++p)
+                *reinterpret_cast<u32x2a *>(lds + gb + uint32_t(oidx[p]) * a.len) = u32x2a{acc[p][0], acc[p][1]};
+        }
+        __syncthreads();
+        for (uint32_t q = threadIdx.x * 16u; q < nb; q += kThreads * 16u) {
+            const uint32_t l0 = q & ~127u, l1 = min(l0 + 127u, nb - 1u);
+            if (!((role(l0) | role(l1)) & 2u)) continue;
+            const u32x4 v = *reinterpret_cast<const u32x4 *>(lds + q);
+            if (q + 16u <= nb)
+                __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(RSAMD_G(sp + q, 16)));
+            else
+                __builtin_nontemporal_store(u32x2a{v[0], v[1]}, reinterpret_cast<u32x2a *>(RSAMD_G(sp + q, 8)));
+        }
+    }
+}
+
 // Masked byte kernel: any alignment, and the <16-byte tails.
 struct MaskedByteArgs {
     uint8_t *base;
@@ -1616,8 +1711,63 @@ bool group8_geometry(const Geometry &g, int nin, int ms) {
            group8_enabled();
 }
 
+// The span-owner kernel's groups per workgroup: the fewest whose bytes fill
+// whole lines, times as many as fit `budget` bytes of LDS; 0 when none fit.
+uint32_t span_groups(size_t glen, size_t budget) {
+    size_t g0 = 1;
+    while ((g0 * glen) % 128) ++g0;  // <= 16 for a multiple of 8
+    return uint32_t(budget / (g0 * glen) * g0);
+}
+
+template <int MS>
+hipError_t launch_span_t(const SpanArgs &a, size_t lds, hipStream_t s) {
+    const dim3 grid(unsigned(std::min<uint64_t>(a.n_spans, uint64_t(1) << 20)));
+    hipLaunchKernelGGL((gf_span_kernel<MS>), grid, dim3(kThreads), lds, s, a);
+    return hipGetLastError();
+}
+
+// TUNING builds: RSAMD_GROUP_SPAN=<LDS bytes per workgroup> takes uniform
+// plans on 128-byte-aligned batches to the span-owner kernel (0: off).
+bool launch_span(const Geometry &g, const GroupArgs &ga, int ms, hipStream_t s, hipError_t *err) {
+    const size_t budget = tuning_size("RSAMD_GROUP_SPAN", 0);
+    const size_t glen = size_t(g.total) * g.len;
+    if (!budget || reinterpret_cast<uintptr_t>(g.base) % 128 || g.total > 32 || ms < 1 || ms > 4) return false;
+    const uint32_t G = span_groups(glen, std::min<size_t>(budget, 65536));
+    if (G == 0) return false;
+    SpanArgs a{};
+    a.lo = g.base;
+    a.hi = g.base + g.n_stripes * g.stripe_stride;
+    a.len = uint32_t(g.len);
+    a.total = uint32_t(g.total);
+    a.glen = uint32_t(glen);
+    a.groups = G;
+    a.n_spans = (g.n_stripes + G - 1) / G;
+    a.tabs = ga.tabs;
+    a.in_idx = ga.in_idx;
+    a.out_idx = ga.out_idx;
+    int32_t in_idx[4], out_idx[4];
+    if (hipMemcpy(in_idx, ga.in_idx, sizeof in_idx, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(out_idx, ga.out_idx, size_t(ms) * 4, hipMemcpyDeviceToHost) != hipSuccess) {
+        *err = hipGetLastError();
+        return true;
+    }
+    for (int i = 0; i < 4; ++i) a.in_mask |= 1u << in_idx[i];
+    for (int p = 0; p < ms; ++p) a.out_mask |= 1u << out_idx[p];
+    bounds::allow(a.lo, size_t(a.hi - a.lo));
+    const size_t lds = size_t(G) * glen;
+    switch (ms) {
+    case 1: *err = launch_span_t<1>(a, lds, s); break;
+    case 2: *err = launch_span_t<2>(a, lds, s); break;
+    case 3: *err = launch_span_t<3>(a, lds, s); break;
+    default: *err = launch_span_t<4>(a, lds, s); break;
+    }
+    return true;
+}
+
 template <bool MASKED>
 hipError_t launch_group8(const Geometry &g, GroupArgs a, int ms, hipStream_t s) {
+    hipError_t span_err = hipSuccess;
+    if (!MASKED && launch_span(g, a, ms, s, &span_err)) return span_err;
     const size_t lds = group8_lds(g.len, 4, ms, MASKED);
     a.stripe_stride = g.stripe_stride;
     a.lo = g.base;
