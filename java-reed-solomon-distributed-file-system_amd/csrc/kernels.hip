@@ -1049,11 +1049,17 @@ struct SpanArgs {
     const int32_t *in_idx, *out_idx;
 };
 
-template <int MS>
+// LEN and T fixed at compile time (the DFS's 1000-byte chunks, 6 servers):
+// every offset-to-shard division is a multiply.  A workgroup first works out,
+// once, what each 16-byte piece of a span needs (the pattern is the same in
+// every span of a uniform plan), then walks its spans (a persistent grid).
+template <int MS, int LEN, int T>
 __global__ void __launch_bounds__(kThreads) gf_span_kernel(SpanArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int K = 4;
-    const uint32_t span = a.groups * a.glen;
+    constexpr uint32_t GLEN = uint32_t(LEN) * T;
+    const uint32_t span = a.groups * GLEN, npieces = span / 16u;
+    uint8_t *flags = lds + span;  // per piece: bit 0 load low half, bit 1 load high half, bit 2 store
     int sidx[K], oidx[MS];
 #pragma unroll
     for (int i = 0; i < K; ++i) sidx[i] = *RSAMD_G(a.in_idx + i, 4);
@@ -1061,36 +1067,39 @@ __global__ void __launch_bounds__(kThreads) gf_span_kernel(SpanArgs a) {
     for (int p = 0; p < MS; ++p) oidx[p] = *RSAMD_G(a.out_idx + p, 4);
     const __attribute__((address_space(4))) uint32_t *ctabs =
         (const __attribute__((address_space(4))) uint32_t *)(RSAMD_G(a.tabs, K * MS * 20));
-    // shard role of span offset o: bit 0 survivor, bit 1 output
-    auto role = [&](uint32_t o) -> uint32_t {
-        const uint32_t sh = (o % a.glen) / a.len;
+    auto role = [&](uint32_t o) -> uint32_t {  // bit 0 survivor, bit 1 output
+        const uint32_t sh = (o % GLEN) / uint32_t(LEN);
         return ((a.in_mask >> sh) & 1u) | (((a.out_mask >> sh) & 1u) << 1);
     };
+    for (uint32_t pi = threadIdx.x; pi < npieces; pi += kThreads) {
+        const uint32_t q = pi * 16u, l0 = q & ~127u, l1 = l0 + 127u;
+        const bool written = ((role(l0) | role(l1)) & 2u) != 0;
+        const uint32_t r0 = role(q), r1 = role(q + 8u);
+        flags[pi] = uint8_t(((r0 & 1u) || (written && !(r0 & 2u)) ? 1u : 0u) |
+                            ((r1 & 1u) || (written && !(r1 & 2u)) ? 2u : 0u) | (written ? 4u : 0u));
+    }
     for (uint64_t w = blockIdx.x; w < a.n_spans; w += gridDim.x) {
         uint8_t *sp = a.lo + w * uint64_t(span);
-        const uint32_t nb = uint32_t(min(uint64_t(span), uint64_t(a.hi - sp)));  // a multiple of 8
-        __syncthreads();  // the previous span's stores have read LDS
-        for (uint32_t q = threadIdx.x * 16u; q < nb; q += kThreads * 16u) {
-            const uint32_t l0 = q & ~127u, l1 = min(l0 + 127u, nb - 1u);
-            const bool written = ((role(l0) | role(l1)) & 2u) != 0;
-            const uint32_t r0 = role(q), r1 = q + 8u < nb ? role(q + 8u) : 2u;  // (past the batch: as an output, not loaded)
-            const bool need0 = (r0 & 1u) || (written && !(r0 & 2u));
-            const bool need1 = (r1 & 1u) || (written && !(r1 & 2u));
-            if (need0 && need1) {
+        const uint32_t nb = uint32_t(min(uint64_t(span), uint64_t(a.hi - sp)));  // whole groups
+        __syncthreads();  // the flags are written / the previous span's stores have read LDS
+        for (uint32_t pi = threadIdx.x; pi * 16u < nb; pi += kThreads) {
+            const uint32_t q = pi * 16u, f = flags[pi];
+            if ((f & 3u) == 3u) {
                 *reinterpret_cast<u32x4 *>(lds + q) = load_stream(sp + q);
-            } else if (need0) {
+            } else if (f & 1u) {
                 *reinterpret_cast<u32x2a *>(lds + q) = *reinterpret_cast<const u32x2a *>(RSAMD_G(sp + q, 8));
-            } else if (need1) {
+            } else if (f & 2u) {
                 *reinterpret_cast<u32x2a *>(lds + q + 8u) = *reinterpret_cast<const u32x2a *>(RSAMD_G(sp + q + 8u, 8));
             }
         }
         __syncthreads();
-        const uint32_t nw = a.len / 8u, units = nb / a.glen * nw;
+        constexpr uint32_t NW = uint32_t(LEN) / 8u;
+        const uint32_t units = nb / GLEN * NW;
         for (uint32_t u = threadIdx.x; u < units; u += kThreads) {
-            const uint32_t j = u / nw, v = u - j * nw, gb = j * a.glen + 8u * v;
+            const uint32_t j = u / NW, v = u - j * NW, gb = j * GLEN + 8u * v;
             u32x2a x[K];
 #pragma unroll
-            for (int i = 0; i < K; ++i) x[i] = *reinterpret_cast<const u32x2a *>(lds + gb + uint32_t(sidx[i]) * a.len);
+            for (int i = 0; i < K; ++i) x[i] = *reinterpret_cast<const u32x2a *>(lds + gb + uint32_t(sidx[i]) * LEN);
             uint32_t acc[MS][2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
@@ -1109,17 +1118,14 @@ __global__ void __launch_bounds__(kThreads) gf_span_kernel(SpanArgs a) {
             }
 #pragma unroll
             for (int p = 0; p < MS; ++p)
-                *reinterpret_cast<u32x2a *>(lds + gb + uint32_t(oidx[p]) * a.len) = u32x2a{acc[p][0], acc[p][1]};
+                *reinterpret_cast<u32x2a *>(lds + gb + uint32_t(oidx[p]) * LEN) = u32x2a{acc[p][0], acc[p][1]};
         }
         __syncthreads();
-        for (uint32_t q = threadIdx.x * 16u; q < nb; q += kThreads * 16u) {
-            const uint32_t l0 = q & ~127u, l1 = min(l0 + 127u, nb - 1u);
-            if (!((role(l0) | role(l1)) & 2u)) continue;
+        for (uint32_t pi = threadIdx.x; pi * 16u < nb; pi += kThreads) {
+            if (!(flags[pi] & 4u)) continue;
+            const uint32_t q = pi * 16u;
             const u32x4 v = *reinterpret_cast<const u32x4 *>(lds + q);
-            if (q + 16u <= nb)
-                __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(RSAMD_G(sp + q, 16)));
-            else
-                __builtin_nontemporal_store(u32x2a{v[0], v[1]}, reinterpret_cast<u32x2a *>(RSAMD_G(sp + q, 8)));
+            __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(RSAMD_G(sp + q, 16)));
         }
     }
 }
@@ -1721,8 +1727,9 @@ uint32_t span_groups(size_t glen, size_t budget) {
 
 template <int MS>
 hipError_t launch_span_t(const SpanArgs &a, size_t lds, hipStream_t s) {
-    const dim3 grid(unsigned(std::min<uint64_t>(a.n_spans, uint64_t(1) << 20)));
-    hipLaunchKernelGGL((gf_span_kernel<MS>), grid, dim3(kThreads), lds, s, a);
+    // persistent: a few workgroups per CU, each working out its piece flags once
+    const dim3 grid(unsigned(std::min<uint64_t>(a.n_spans, tuning_size("RSAMD_GROUP_SPAN_WGS", 1024))));
+    hipLaunchKernelGGL((gf_span_kernel<MS, 1000, 6>), grid, dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
 
@@ -1731,7 +1738,8 @@ hipError_t launch_span_t(const SpanArgs &a, size_t lds, hipStream_t s) {
 bool launch_span(const Geometry &g, const GroupArgs &ga, int ms, hipStream_t s, hipError_t *err) {
     const size_t budget = tuning_size("RSAMD_GROUP_SPAN", 0);
     const size_t glen = size_t(g.total) * g.len;
-    if (!budget || reinterpret_cast<uintptr_t>(g.base) % 128 || g.total > 32 || ms < 1 || ms > 4) return false;
+    if (!budget || reinterpret_cast<uintptr_t>(g.base) % 128 || g.total != 6 || g.len != 1000 || ms < 1 || ms > 4)
+        return false;
     const uint32_t G = span_groups(glen, std::min<size_t>(budget, 65536));
     if (G == 0) return false;
     SpanArgs a{};
@@ -1754,7 +1762,7 @@ bool launch_span(const Geometry &g, const GroupArgs &ga, int ms, hipStream_t s, 
     for (int i = 0; i < 4; ++i) a.in_mask |= 1u << in_idx[i];
     for (int p = 0; p < ms; ++p) a.out_mask |= 1u << out_idx[p];
     bounds::allow(a.lo, size_t(a.hi - a.lo));
-    const size_t lds = size_t(G) * glen;
+    const size_t lds = size_t(G) * glen + size_t(G) * glen / 16;  // the span, then its piece flags
     switch (ms) {
     case 1: *err = launch_span_t<1>(a, lds, s); break;
     case 2: *err = launch_span_t<2>(a, lds, s); break;
