@@ -1029,107 +1029,6 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MS >
     }
 }
 
-// Span-owner kernel (uniform plans; A/B against the line-owner kernel above):
-// a workgroup owns `groups` consecutive chunk groups whose bytes fill whole
-// 128-byte lines (4+2 x 1000 B: 8 groups, 48000 bytes, 375 lines), so every
-// line it reads or writes is its own.  Phase 0 loads, as 16-byte pieces, the
-// lines holding survivor bytes and, of the lines it will write, the bytes of
-// shards it does not rebuild; phase 1 codes 8-byte columns from LDS into the
-// output shards' places in LDS; phase 2 stores every line that holds an
-// output byte whole.  No foreign bytes, no per-wave phases: four waves share
-// each phase.
-struct SpanArgs {
-    uint8_t *lo, *hi;       // the batch's bytes: [lo, hi), lo 128-aligned
-    uint32_t len, total;    // shard length (a multiple of 8), shards per group
-    uint32_t glen;          // total * len
-    uint32_t groups;        // groups per span (groups * glen a multiple of 128)
-    uint64_t n_spans;
-    uint32_t in_mask, out_mask;  // survivors, outputs (bit s = shard s)
-    const uint32_t *tabs;   // tabs[4][MS][5]
-    const int32_t *in_idx, *out_idx;
-};
-
-// LEN and T fixed at compile time (the DFS's 1000-byte chunks, 6 servers):
-// every offset-to-shard division is a multiply.  A workgroup first works out,
-// once, what each 16-byte piece of a span needs (the pattern is the same in
-// every span of a uniform plan), then walks its spans (a persistent grid).
-template <int MS, int LEN, int T>
-__global__ void __launch_bounds__(kThreads) gf_span_kernel(SpanArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    constexpr int K = 4;
-    constexpr uint32_t GLEN = uint32_t(LEN) * T;
-    const uint32_t span = a.groups * GLEN, npieces = span / 16u;
-    uint8_t *flags = lds + span;  // per piece: bit 0 load low half, bit 1 load high half, bit 2 store
-    int sidx[K], oidx[MS];
-#pragma unroll
-    for (int i = 0; i < K; ++i) sidx[i] = *RSAMD_G(a.in_idx + i, 4);
-#pragma unroll
-    for (int p = 0; p < MS; ++p) oidx[p] = *RSAMD_G(a.out_idx + p, 4);
-    const __attribute__((address_space(4))) uint32_t *ctabs =
-        (const __attribute__((address_space(4))) uint32_t *)(RSAMD_G(a.tabs, K * MS * 20));
-    auto role = [&](uint32_t o) -> uint32_t {  // bit 0 survivor, bit 1 output
-        const uint32_t sh = (o % GLEN) / uint32_t(LEN);
-        return ((a.in_mask >> sh) & 1u) | (((a.out_mask >> sh) & 1u) << 1);
-    };
-    for (uint32_t pi = threadIdx.x; pi < npieces; pi += kThreads) {
-        const uint32_t q = pi * 16u, l0 = q & ~127u, l1 = l0 + 127u;
-        const bool written = ((role(l0) | role(l1)) & 2u) != 0;
-        const uint32_t r0 = role(q), r1 = role(q + 8u);
-        flags[pi] = uint8_t(((r0 & 1u) || (written && !(r0 & 2u)) ? 1u : 0u) |
-                            ((r1 & 1u) || (written && !(r1 & 2u)) ? 2u : 0u) | (written ? 4u : 0u));
-    }
-    for (uint64_t w = blockIdx.x; w < a.n_spans; w += gridDim.x) {
-        uint8_t *sp = a.lo + w * uint64_t(span);
-        const uint32_t nb = uint32_t(min(uint64_t(span), uint64_t(a.hi - sp)));  // whole groups
-        __syncthreads();  // the flags are written / the previous span's stores have read LDS
-        for (uint32_t pi = threadIdx.x; pi * 16u < nb; pi += kThreads) {
-            const uint32_t q = pi * 16u, f = flags[pi];
-            if ((f & 3u) == 3u) {
-                *reinterpret_cast<u32x4 *>(lds + q) = load_stream(sp + q);
-            } else if (f & 1u) {
-                *reinterpret_cast<u32x2a *>(lds + q) = *reinterpret_cast<const u32x2a *>(RSAMD_G(sp + q, 8));
-            } else if (f & 2u) {
-                *reinterpret_cast<u32x2a *>(lds + q + 8u) = *reinterpret_cast<const u32x2a *>(RSAMD_G(sp + q + 8u, 8));
-            }
-        }
-        __syncthreads();
-        constexpr uint32_t NW = uint32_t(LEN) / 8u;
-        const uint32_t units = nb / GLEN * NW;
-        for (uint32_t u = threadIdx.x; u < units; u += kThreads) {
-            const uint32_t j = u / NW, v = u - j * NW, gb = j * GLEN + 8u * v;
-            u32x2a x[K];
-#pragma unroll
-            for (int i = 0; i < K; ++i) x[i] = *reinterpret_cast<const u32x2a *>(lds + gb + uint32_t(sidx[i]) * LEN);
-            uint32_t acc[MS][2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-#pragma unroll
-                for (int i = 0; i < K; ++i) {
-                    const Sel sl = selectors(x[i][h]);
-#pragma unroll
-                    for (int p = 0; p < MS; ++p) {
-                        uint32_t t0, t1, t2, tp[5];
-#pragma unroll
-                        for (int jj = 0; jj < 5; ++jj) tp[jj] = ctabs[(i * MS + p) * 5 + jj];
-                        terms(tp, sl, t0, t1, t2);
-                        acc[p][h] = i == 0 ? xor3(t0, t1, t2) : xor3(acc[p][h], t0, t1) ^ t2;
-                    }
-                }
-            }
-#pragma unroll
-            for (int p = 0; p < MS; ++p)
-                *reinterpret_cast<u32x2a *>(lds + gb + uint32_t(oidx[p]) * LEN) = u32x2a{acc[p][0], acc[p][1]};
-        }
-        __syncthreads();
-        for (uint32_t pi = threadIdx.x; pi * 16u < nb; pi += kThreads) {
-            if (!(flags[pi] & 4u)) continue;
-            const uint32_t q = pi * 16u;
-            const u32x4 v = *reinterpret_cast<const u32x4 *>(lds + q);
-            __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(RSAMD_G(sp + q, 16)));
-        }
-    }
-}
-
 // Masked byte kernel: any alignment, and the <16-byte tails.
 struct MaskedByteArgs {
     uint8_t *base;
@@ -1717,65 +1616,8 @@ bool group8_geometry(const Geometry &g, int nin, int ms) {
            group8_enabled();
 }
 
-// The span-owner kernel's groups per workgroup: the fewest whose bytes fill
-// whole lines, times as many as fit `budget` bytes of LDS; 0 when none fit.
-uint32_t span_groups(size_t glen, size_t budget) {
-    size_t g0 = 1;
-    while ((g0 * glen) % 128) ++g0;  // <= 16 for a multiple of 8
-    return uint32_t(budget / (g0 * glen) * g0);
-}
-
-template <int MS>
-hipError_t launch_span_t(const SpanArgs &a, size_t lds, hipStream_t s) {
-    // persistent: a few workgroups per CU, each working out its piece flags once
-    const dim3 grid(unsigned(std::min<uint64_t>(a.n_spans, tuning_size("RSAMD_GROUP_SPAN_WGS", 1024))));
-    hipLaunchKernelGGL((gf_span_kernel<MS, 1000, 6>), grid, dim3(kThreads), lds, s, a);
-    return hipGetLastError();
-}
-
-// TUNING builds: RSAMD_GROUP_SPAN=<LDS bytes per workgroup> takes uniform
-// plans on 128-byte-aligned batches to the span-owner kernel (0: off).
-bool launch_span(const Geometry &g, const GroupArgs &ga, int ms, hipStream_t s, hipError_t *err) {
-    const size_t budget = tuning_size("RSAMD_GROUP_SPAN", 0);
-    const size_t glen = size_t(g.total) * g.len;
-    if (!budget || reinterpret_cast<uintptr_t>(g.base) % 128 || g.total != 6 || g.len != 1000 || ms < 1 || ms > 4)
-        return false;
-    const uint32_t G = span_groups(glen, std::min<size_t>(budget, 65536));
-    if (G == 0) return false;
-    SpanArgs a{};
-    a.lo = g.base;
-    a.hi = g.base + g.n_stripes * g.stripe_stride;
-    a.len = uint32_t(g.len);
-    a.total = uint32_t(g.total);
-    a.glen = uint32_t(glen);
-    a.groups = G;
-    a.n_spans = (g.n_stripes + G - 1) / G;
-    a.tabs = ga.tabs;
-    a.in_idx = ga.in_idx;
-    a.out_idx = ga.out_idx;
-    int32_t in_idx[4], out_idx[4];
-    if (hipMemcpy(in_idx, ga.in_idx, sizeof in_idx, hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(out_idx, ga.out_idx, size_t(ms) * 4, hipMemcpyDeviceToHost) != hipSuccess) {
-        *err = hipGetLastError();
-        return true;
-    }
-    for (int i = 0; i < 4; ++i) a.in_mask |= 1u << in_idx[i];
-    for (int p = 0; p < ms; ++p) a.out_mask |= 1u << out_idx[p];
-    bounds::allow(a.lo, size_t(a.hi - a.lo));
-    const size_t lds = size_t(G) * glen + size_t(G) * glen / 16;  // the span, then its piece flags
-    switch (ms) {
-    case 1: *err = launch_span_t<1>(a, lds, s); break;
-    case 2: *err = launch_span_t<2>(a, lds, s); break;
-    case 3: *err = launch_span_t<3>(a, lds, s); break;
-    default: *err = launch_span_t<4>(a, lds, s); break;
-    }
-    return true;
-}
-
 template <bool MASKED>
 hipError_t launch_group8(const Geometry &g, GroupArgs a, int ms, hipStream_t s) {
-    hipError_t span_err = hipSuccess;
-    if (!MASKED && launch_span(g, a, ms, s, &span_err)) return span_err;
     const size_t lds = group8_lds(g.len, 4, ms, MASKED);
     a.stripe_stride = g.stripe_stride;
     a.lo = g.base;
