@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Pageable host calls by size: 4+2 encodeParity per call at 64 KiB .. 64 MiB
-per shard (the DFS client's files are split into shards of a quarter of the
+"""Pageable host calls by size: 4+2 encodeParity per call at 16 KiB .. 64 MiB
+per shard, and the client's file calls (encode, decode {0,5}) on 1 .. 64 MiB
+files (the DFS client's files are split into shards of a quarter of the
 file, so mid sizes are the common case), GiB/s of data shards and us per
 call, bound to the GPU's NUMA node as bench.py binds its host legs.  One child
 process per TUNING variant; each prints one JSON line.
@@ -13,6 +14,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FILE_SIZES = [1 << 20, 4 << 20, 16 << 20, 64 << 20]
 SIZES = [16 << 10, 32 << 10, 64 << 10, 128 << 10, 192 << 10, 256 << 10, 512 << 10, 1 << 20, 2 << 20, 4 << 20, 16 << 20, 64 << 20]
 
 
@@ -47,6 +49,29 @@ def child():
             c_ref.Codec(k, m).encode_parity(ref, 0, S)
             assert all(np.array_equal(a, b) for a, b in zip(sh, ref)), S
             out[f"{S >> 10}K"] = {"us": round(t * 1e6, 1), "GiBps": round(k * S / t / 2**30, 2)}
+        # the client's file calls (1000-byte blocks): encode, then decode {0, 5}
+        from rsamd.layout import file_decode_into, file_encode_into, file_layout
+        for F in FILE_SIZES:
+            rng = np.random.default_rng(F)
+            data = rng.integers(0, 256, F, dtype=np.uint8)
+            _, S = file_layout(rs, F)
+            fsh = [np.zeros(S, np.uint8) for _ in range(k + m)]
+            fout = np.zeros(F, np.uint8)
+            reps = max(5, min(100, (256 << 20) // F))
+            pres = [i not in (0, 5) for i in range(k + m)]
+            row = {}
+            for name, fn in (("enc", lambda: file_encode_into(rs, data, fsh)),
+                             ("dec05", lambda: file_decode_into(rs, fsh, pres, S, fout))):
+                for _ in range(3):
+                    fn()
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    fn()
+                t = (time.perf_counter() - t0) / reps
+                row[name] = {"us": round(t * 1e6, 1), "GiBps": round(F / t / 2**30, 2)}
+            ref = c_ref.Codec(k, m).file_encode(data.tobytes(), 1000)
+            assert np.array_equal(np.stack(fsh), ref) and np.array_equal(fout, data), F
+            out[f"file_{F >> 10}K"] = row
     print(json.dumps(out), flush=True)
 
 
