@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Concurrency stress of the host paths (the process-wide copy pool with its
+polling threads, the mirrored pipeline's shared slot sets, the zero-copy
+path): T threads at once, each making random pageable calls -- encodeParity /
+decodeMissing at random sizes (4 KiB .. 24 MiB per shard) and offsets, and
+file encode / decode at random sizes and blocks -- for a fixed time, every
+result checked against the oracle.  Prints one JSON line per thread and a
+summary; exits 1 on any mismatch.
+  python tools/host_stress.py [--threads 8] [--seconds 60]"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "java-reed-solomon-distributed-file-system_amd"))
+
+
+def worker(tid, seconds, oracle, res):
+    import numpy as np
+    import rsamd
+    from rsamd.layout import file_decode_into, file_encode_into, file_layout
+    rng = np.random.default_rng(1000 + tid)
+    calls = bad = 0
+    t_end = time.time() + seconds
+    while time.time() < t_end:
+        k = int(rng.choice([4, 4, 10, 3, 6]))
+        m = int(rng.choice([2, 2, 4, 1, 3]))
+        rs = rsamd.ReedSolomon.create(k, m)
+        oc = oracle.Codec(k, m)
+        if rng.random() < 0.6:
+            n = int(rng.choice([4 << 10, 64 << 10, 300 << 10, 1 << 20, 3 << 20, 24 << 20]))
+            n += int(rng.integers(0, 4096))
+            off = int(rng.integers(0, 64))
+            cnt = n - off - int(rng.integers(0, 64))
+            sh = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)] + [np.zeros(n, np.uint8) for _ in range(m)]
+            ref = [a.copy() for a in sh]
+            oc.encode_parity(ref, off, cnt)
+            rs.encodeParity(sh, off, cnt)
+            ok = all(np.array_equal(a, b) for a, b in zip(sh, ref))
+            e = int(rng.integers(1, m + 1))
+            miss = sorted(int(x) for x in rng.choice(k + m, e, replace=False))
+            for j in miss:
+                sh[j][off:off + cnt] = 0
+            rs.decodeMissing(sh, [i not in miss for i in range(k + m)], off, cnt)
+            ok = ok and all(np.array_equal(a, b) for a, b in zip(sh, ref))
+        else:
+            block = int(rng.choice([1000, 1000, 4096, 520, 8]))
+            n = int(rng.choice([90_999, 1 << 20, 5 << 20, 20 << 20])) + int(rng.integers(0, 5000))
+            data = rng.integers(0, 256, n, dtype=np.uint8)
+            _, S = file_layout(rs, n, block)
+            sh = [np.full(S, 0xEE, np.uint8) for _ in range(k + m)]
+            file_encode_into(rs, data, sh, block)
+            ref = oc.file_encode(data.tobytes(), block)
+            ok = all(np.array_equal(a, b) for a, b in zip(sh, ref))
+            e = int(rng.integers(1, m + 1))
+            miss = sorted(int(x) for x in rng.choice(k + m, e, replace=False))
+            for j in miss:
+                sh[j][:] = 0
+            out = np.zeros(n, np.uint8)
+            file_decode_into(rs, sh, [i not in miss for i in range(k + m)], S, out, block)
+            ok = ok and np.array_equal(out, data) and all(np.array_equal(a, b) for a, b in zip(sh, ref))
+        calls += 1
+        bad += 0 if ok else 1
+    res[tid] = {"thread": tid, "calls": calls, "bad": bad}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--seconds", type=float, default=60)
+    a = ap.parse_args()
+    import torch
+    torch.cuda.init()
+    from oracle import c_ref
+    res = {}
+    ts = [threading.Thread(target=worker, args=(t, a.seconds, c_ref, res)) for t in range(a.threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for t in sorted(res):
+        print(json.dumps(res[t]), flush=True)
+    total = sum(r["calls"] for r in res.values())
+    bad = sum(r["bad"] for r in res.values())
+    print(json.dumps({"threads": a.threads, "seconds": a.seconds, "calls": total, "bad": bad,
+                      "all_threads_finished": len(res) == a.threads}), flush=True)
+    return 1 if bad or len(res) != a.threads else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
