@@ -73,6 +73,9 @@ def main():
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--seconds", type=float, default=60)
     a = ap.parse_args()
+    from rsamd import _lib
+    if os.environ.get("RSAMD_TEST_LIB"):  # e.g. the bounds-checking build
+        _lib.LIB_PATH = os.path.abspath(os.environ["RSAMD_TEST_LIB"])
     import torch
     torch.cuda.init()
     from oracle import c_ref
@@ -86,9 +89,16 @@ def main():
         print(json.dumps(res[t]), flush=True)
     total = sum(r["calls"] for r in res.values())
     bad = sum(r["bad"] for r in res.values())
+    oob = None
+    lib = _lib.load()
+    if hasattr(lib, "rs_bounds_report"):  # the bounds build: kernel accesses outside their declared buffers
+        import ctypes as C
+        n, addr, ln, where = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint32()
+        lib.rs_bounds_report(C.byref(n), C.byref(addr), C.byref(ln), C.byref(where))
+        oob = n.value
     print(json.dumps({"threads": a.threads, "seconds": a.seconds, "calls": total, "bad": bad,
-                      "all_threads_finished": len(res) == a.threads}), flush=True)
-    return 1 if bad or len(res) != a.threads else 0
+                      "all_threads_finished": len(res) == a.threads, "bounds_violations": oob}), flush=True)
+    return 1 if bad or oob or len(res) != a.threads else 0
 
 
 if __name__ == "__main__":
