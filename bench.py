@@ -310,6 +310,7 @@ def run(args, live_traffic=None):
                 link = host_link(torch)
                 extra.update(host_inclusive(rsamd, k, m, link))
                 extra.update(config0_single_stripe(rsamd, k, m))
+                extra.update(host_by_size(rsamd, k, m))
         else:
             # every rank at once: the node's aggregate host <-> device rate
             with gpu_numa_bound(torch, parallel, extra):
@@ -448,6 +449,8 @@ def decode_summary(extra):
         "host_pinned_enc_link_frac": g("host_inclusive_pinned_encode_frac_of_link_bound"),
         "host_pinned_file_enc_link_frac": g("host_inclusive_pinned_file_encode_frac_of_link_bound"),
         "host_pinned_file_dec_link_frac": g("host_inclusive_pinned_file_decode_0_5_frac_of_link_bound"),
+        "host_enc_64K_us": g("host_enc_64K_us"), "host_enc_1M_us": g("host_enc_1024K_us"),
+        "host_enc_4M_us": g("host_enc_4096K_us"),
     }
 
 
@@ -1532,6 +1535,32 @@ def config0_single_stripe(rsamd, k, m, S=64 << 10, reps=200):
         np.array_equal(sh[0], data[0])
     out["cfg0_note"] = (f"one {k}+{m} stripe of {S >> 10} KiB shards per call, host buffers; GPU = host API "
                         f"(H2D + kernel + D2H), CPU = oracle scalar port, 1 thread")
+    return out
+
+
+def host_by_size(rsamd, k, m, sizes=(64 << 10, 1 << 20, 4 << 20, 16 << 20)):
+    """Pageable encodeParity per call by shard size (the mid sizes a DFS
+    client's files give: the shards are a quarter of the file), microseconds
+    per call, each result checked against the oracle (tools/host_sizes.py is
+    the full sweep)."""
+    import numpy as np
+    from oracle import c_ref
+    rs = rsamd.ReedSolomon.create(k, m)
+    out, ok = {}, True
+    for S in sizes:
+        rng = np.random.default_rng(S)
+        sh = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
+        reps = max(5, min(100, (128 << 20) // (k * S)))
+        for _ in range(3):
+            rs.encodeParity(sh, 0, S)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            rs.encodeParity(sh, 0, S)
+        out[f"host_enc_{S >> 10}K_us"] = round((time.perf_counter() - t0) / reps * 1e6, 1)
+        ref = [a.copy() for a in sh[:k]] + [np.zeros(S, np.uint8) for _ in range(m)]
+        c_ref.Codec(k, m).encode_parity(ref, 0, S)
+        ok = ok and all(np.array_equal(a, b) for a, b in zip(sh, ref))
+    out["host_by_size_bit_exact"] = bool(ok)
     return out
 
 
