@@ -41,7 +41,11 @@ def main():
     cases = bad = 0
     first_bad = None
     t_end = time.time() + a.seconds
+    t_note = time.time() + 30
     while time.time() < t_end:
+        if time.time() > t_note:  # a progress line every 30 s (a silent GPU run reads as hung)
+            print(json.dumps({"progress_cases": cases, "bad": bad}), flush=True)
+            t_note = time.time() + 30
         k = int(rng.integers(1, 17))
         m = int(rng.integers(1, 5))
         T = k + m
