@@ -388,8 +388,12 @@ int zero_copy_buffer(ThreadCtx *ctx, size_t buf_bytes) {
         if (ctx->zc) RS_HIP(hipHostFree(ctx->zc));
         ctx->zc = ctx->zc_dev = nullptr;
         ctx->zc_cap = 0;
-        RS_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->zc), buf_bytes,
-                             hipHostMallocMapped | hipHostMallocCoherent));
+        // TUNING builds: RSAMD_ZC_ALLOC 1 = mapped + the caller's NUMA policy, 2 = mapped non-coherent
+        const size_t how = tuning_size("RSAMD_ZC_ALLOC", 0);
+        const unsigned flags = how == 1 ? (hipHostMallocMapped | hipHostMallocNumaUser)
+                             : how == 2 ? (hipHostMallocMapped | hipHostMallocNonCoherent)
+                                        : (hipHostMallocMapped | hipHostMallocCoherent);
+        RS_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->zc), buf_bytes, flags));
         ctx->zc_cap = buf_bytes;
         RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->zc_dev), ctx->zc, 0));
     }
