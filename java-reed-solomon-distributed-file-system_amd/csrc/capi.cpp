@@ -591,6 +591,69 @@ int file_encode_direct(const Codec &c, const uint8_t *file, size_t file_len, siz
     return RS_OK;
 }
 
+// Small pageable files (one zero-copy pass): the file is copied into the
+// context's device-mapped buffer, the fused direct kernel codes the parity
+// there (reading the file over the link, writing only the parity back), and
+// the host splits the data shards from the caller's file while it runs -- the
+// link carries the file and the parity instead of the file and every shard
+// (TUNING builds: RSAMD_FILE_ZC_SPLIT=0 keeps the all-GPU pass).  *taken =
+// false when the kernel cannot take the geometry (block % 8, k, m, size).
+int file_encode_zc_split(const Codec &c, const uint8_t *file, size_t file_len, size_t blk, uint8_t *const *shards,
+                         size_t S, ThreadCtx *ctx, bool *taken) {
+    *taken = false;
+    const int k = c.k(), m = c.m();
+    if (!rsamd::tuning_size("RSAMD_FILE_ZC_SPLIT", 1) || !direct_enabled() || m < 1 || m > rsamd::kMaxOut ||
+        k > rsamd::kMaxDirectIn || blk % 8 || S % 8)
+        return RS_OK;
+    const size_t fbytes = round_up(std::max<size_t>(file_len, 1), 256), stride = round_up(S, 256);
+    const size_t need = fbytes + size_t(m) * stride;
+    if (need > (size_t(64) << 20)) return RS_OK;
+    int rc = zero_copy_buffer(ctx, need);
+    if (rc) return rc;
+    rsamd::FileDirect d;
+    d.k = k;
+    d.nout = m;
+    d.block = blk;
+    d.units = S / 8;
+    d.file_len = file_len;
+    d.file = ctx->zc_dev;
+    for (int p = 0; p < m; ++p) d.out[k + p] = ctx->zc_dev + fbytes + size_t(p) * stride;
+    std::vector<DevPlan> plans;
+    RS_HIP(c.encode_plan().device_plans(&plans));
+    d.tabs = plans[0].tabs;
+    if (!rsamd::file_direct_ok(d)) return RS_OK;
+    *taken = true;
+    const bool pool = need > (size_t(2) << 20);  // (as run_zero_copy: the pool's wake-up costs more below)
+    auto copy = [&](const std::vector<rsamd::CopyJob> &jobs) {
+        if (pool) {
+            rsamd::CopyPool::get().copy(jobs);
+        } else {
+            for (const rsamd::CopyJob &j : jobs)
+                for (size_t r = 0; r < j.rows; ++r) {
+                    uint8_t *dst = static_cast<uint8_t *>(j.dst) + r * j.dst_stride;
+                    if (j.src)
+                        std::memcpy(dst, static_cast<const uint8_t *>(j.src) + r * j.src_stride, j.n);
+                    else
+                        std::memset(dst, 0, j.n);
+                }
+        }
+    };
+    std::vector<rsamd::CopyJob> jobs;
+    if (file_len) jobs.push_back({ctx->zc, file, file_len});
+    copy(jobs);
+    bounds::allow(d.file, file_len);
+    for (int p = 0; p < m; ++p) bounds::allow(d.out[k + p], S);
+    RS_HIP(rsamd::launch_file_encode_direct(d, ctx->stream));
+    jobs.clear();
+    split_jobs(file, file_len, blk, k, shards, nullptr, 0, 0, S / blk, &jobs);
+    copy(jobs);
+    RS_HIP(hipStreamSynchronize(ctx->stream));
+    jobs.clear();
+    for (int p = 0; p < m; ++p) jobs.push_back({shards[k + p], ctx->zc + fbytes + size_t(p) * stride, S});
+    copy(jobs);
+    return RS_OK;
+}
+
 // The staged form of the host file encode: chunks of block rows through
 // run_chunks.  file_len fills every row but the last (the padded layout).
 int file_encode_staged(const Codec &c, const uint8_t *file, size_t file_len, size_t blk, uint8_t *const *shards,
@@ -1491,6 +1554,8 @@ int rs_file_encode(const rs_codec *codec, const uint8_t *file, int64_t file_len,
         rc = file_encode_direct(*c, file, size_t(file_len), blk, shards_out, size_t(S), ctx, &taken);
     else if (big && size_t(S) >= mirror_min_bytes())
         rc = file_encode_mirrored(*c, file, size_t(file_len), blk, shards_out, size_t(S), ctx, &taken);
+    else
+        rc = file_encode_zc_split(*c, file, size_t(file_len), blk, shards_out, size_t(S), ctx, &taken);
     if (rc || taken) return rc;
     return file_encode_staged(*c, file, size_t(file_len), blk, shards_out, size_t(S), ctx, pinned);
 }

@@ -14,7 +14,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-FILE_SIZES = [1 << 20, 4 << 20, 16 << 20, 64 << 20]
+FILE_SIZES = [90_999, 256 << 10, 1 << 20, 3 << 20, 4 << 20, 16 << 20, 64 << 20]
 SIZES = [16 << 10, 32 << 10, 64 << 10, 128 << 10, 192 << 10, 256 << 10, 512 << 10, 1 << 20, 2 << 20, 4 << 20, 16 << 20, 64 << 20]
 
 
