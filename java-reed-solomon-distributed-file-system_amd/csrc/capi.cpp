@@ -596,8 +596,11 @@ int file_encode_direct(const Codec &c, const uint8_t *file, size_t file_len, siz
 // there (reading the file over the link, writing only the parity back), and
 // the host splits the data shards from the caller's file while it runs -- the
 // link carries the file and the parity instead of the file and every shard
-// (TUNING builds: RSAMD_FILE_ZC_SPLIT=0 keeps the all-GPU pass).  *taken =
-// false when the kernel cannot take the geometry (block % 8, k, m, size).
+// (TUNING builds: RSAMD_FILE_ZC_SPLIT=0 keeps the all-GPU pass).  4+2 encode
+// per call, all-GPU / split: 88 KB 39 / 36 us, 256 KiB 53 / 42-44, 1 MiB
+// 126 / 85-86, 3 MiB 254 / 175 (profiles/r5/host_sizes_tile8_r5zz.txt).
+// *taken = false when the kernel cannot take the geometry (block % 8, k, m,
+// size).
 int file_encode_zc_split(const Codec &c, const uint8_t *file, size_t file_len, size_t blk, uint8_t *const *shards,
                          size_t S, ThreadCtx *ctx, bool *taken) {
     *taken = false;

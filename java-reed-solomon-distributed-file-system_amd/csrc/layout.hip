@@ -871,8 +871,22 @@ __global__ void __launch_bounds__(kThreads) file_direct_tiled_kernel(FileDirect 
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint64_t r0 = t * a.tile_rows, nr = min(a.tile_rows, rows - r0);
         __syncthreads();  // the previous tile's LDS reads are done
-        for (uint64_t q = threadIdx.x; q < nr * kb / 8; q += kThreads)
-            tile[q] = load_run8(a.file, r0 * kb + q * 8, a.file_len);  // (zeros past the file: its padding)
+        // (zeros past the file: its padding); eight loads in flight per lane
+        // before their LDS stores, so a few workgroups still keep the link busy
+        const uint64_t nq = nr * kb / 8;
+        for (uint64_t q0 = threadIdx.x; q0 < nq; q0 += 8 * kThreads) {
+            uint64_t v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint64_t q = q0 + uint64_t(j) * kThreads;
+                v[j] = q < nq ? load_run8(a.file, r0 * kb + q * 8, a.file_len) : 0;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint64_t q = q0 + uint64_t(j) * kThreads;
+                if (q < nq) tile[q] = v[j];
+            }
+        }
         __syncthreads();
         for (uint64_t u = threadIdx.x; u < nr * a.block / 8; u += kThreads) {
             const uint64_t cl = u * 8, r = cl / a.block, w = cl - r * a.block, c = r0 * a.block + cl;
@@ -948,6 +962,15 @@ hipError_t launch_file_encode_direct(const FileDirect &d0, hipStream_t s) {
     FileDirect d = d0;
     d.rot = file_direct_rot(d);
     d.tile_rows = file_tile_rows(d.k, d.block);
+    // Few tiles leave most CUs idle: below 32 tiles (2 MiB of a 4+2 file) the
+    // column kernel spreads the file over every CU instead.  Small pageable
+    // files (the zero-copy split, capi.cpp file_encode_zc_split), encode per
+    // call, tiles / columns: 88 KB 45 / 36 us, 256 KiB 51 / 42-44, 1 MiB 90 /
+    // 85-86, 3 MiB 175 / 182-187; 256 MiB pinned 51.4-52.0 / 44.4 GiB/s
+    // (profiles/r5/host_sizes_tile8_r5zz.txt, pfile_tile8_r5zz.txt; TUNING
+    // builds: RSAMD_FILE_TILE_MIN tiles).
+    if (d.tile_rows && (d.units * 8 / d.block + d.tile_rows - 1) / d.tile_rows < tuning_size("RSAMD_FILE_TILE_MIN", 32))
+        d.tile_rows = 0;
     if (d.tile_rows) {
         const uint64_t rows = d.units * 8 / d.block, ntiles = (rows + d.tile_rows - 1) / d.tile_rows;
         const dim3 grid(unsigned(std::min<uint64_t>(ntiles, tuning_size("RSAMD_FILE_TILE_BLOCKS", 512))));
