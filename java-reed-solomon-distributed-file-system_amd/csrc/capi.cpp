@@ -799,6 +799,86 @@ size_t file_rows_needed(int k, size_t S, size_t blk, const std::vector<int> &mis
     return missing.empty() ? std::min(rows, (file_size + kb - 1) / kb) : rows;
 }
 
+// Small pageable file decodes (one zero-copy pass): the survivors are copied
+// into the context's device-mapped buffer, the direct kernels rebuild the
+// absent shards there, and the host merges the present data shards into the
+// file meanwhile; then the rebuilt shards are copied out, a rebuilt data
+// shard into the file in the same pass (tee_jobs).  Only the survivors and
+// the rebuilt shards cross the link; with nothing absent the call is the
+// merge alone, on the host (TUNING builds: RSAMD_FILE_ZC_SPLIT=0 keeps the
+// all-GPU pass).  *taken = false when the direct kernels cannot take the plan.
+int file_decode_zc_split(const Codec &c, uint8_t *const *shards, const uint8_t *present, const std::vector<int> &surv,
+                         const std::vector<int> &missing, size_t blk, uint8_t *file_out, size_t file_size,
+                         size_t rows_needed, ThreadCtx *ctx, bool *taken) {
+    *taken = false;
+    const int k = c.k(), T = c.total();
+    if (!rsamd::tuning_size("RSAMD_FILE_ZC_SPLIT", 1) || !direct_enabled() || k > rsamd::kMaxDirectIn) return RS_OK;
+    std::vector<const uint8_t *> src(shards, shards + k);
+    std::vector<bool> now(static_cast<size_t>(k), false);
+    for (int d = 0; d < k; ++d) now[d] = present[d] != 0;
+    std::vector<rsamd::CopyJob> jobs;
+    if (missing.empty()) {  // mergeShardsToFile alone
+        merge_jobs(k, blk, file_out, file_size, src.data(), now, 0, rows_needed, &jobs);
+        if (file_size > (size_t(2) << 20)) {
+            rsamd::CopyPool::get().copy(jobs);
+        } else {
+            for (const rsamd::CopyJob &j : jobs)
+                for (size_t r = 0; r < j.rows; ++r)
+                    std::memcpy(static_cast<uint8_t *>(j.dst) + r * j.dst_stride,
+                                static_cast<const uint8_t *>(j.src) + r * j.src_stride, j.n);
+        }
+        *taken = true;
+        return RS_OK;
+    }
+    std::shared_ptr<const Plan> plan;
+    int rc = c.decode_plan(present, &plan);
+    if (rc) return fail(rc, rc == RS_E_SINGULAR ? "Matrix is singular" : "Not enough shards present");
+    std::vector<DevPlan> plans;
+    RS_HIP(plan->device_plans(&plans));
+    for (const DevPlan &p : plans)
+        if (p.nin > rsamd::kMaxDirectIn) return RS_OK;
+    const size_t n = rows_needed * blk, ss = round_up(std::max<size_t>(n, 1), 256), need = ss * size_t(T);
+    if (need > (size_t(64) << 20)) return RS_OK;
+    rc = zero_copy_buffer(ctx, need);
+    if (rc) return rc;
+    *taken = true;
+    const bool pool = need > (size_t(2) << 20);  // (as run_zero_copy)
+    auto copy = [&](const std::vector<rsamd::CopyJob> &js) {
+        if (pool) {
+            rsamd::CopyPool::get().copy(js);
+            return;
+        }
+        for (const rsamd::CopyJob &j : js)
+            for (size_t r = 0; r < j.rows; ++r) {
+                uint8_t *dst = static_cast<uint8_t *>(j.dst) + r * j.dst_stride;
+                const uint8_t *sp = static_cast<const uint8_t *>(j.src) + r * j.src_stride;
+                std::memcpy(dst, sp, j.n);
+                if (j.dst2) std::memcpy(static_cast<uint8_t *>(j.dst2) + r * j.dst2_stride, sp, j.n);
+            }
+    };
+    for (int sidx : surv) jobs.push_back({ctx->zc + size_t(sidx) * ss, shards[sidx], n});
+    copy(jobs);
+    rc = code_slots(plans, plan->in_idx(), plan->out_idx(), ctx->zc_dev, ss, n, Mode::Code, nullptr, ctx->stream);
+    if (rc) {
+        (void)hipStreamSynchronize(ctx->stream);
+        return rc;
+    }
+    jobs.clear();
+    merge_jobs(k, blk, file_out, file_size, src.data(), now, 0, rows_needed, &jobs);
+    copy(jobs);
+    RS_HIP(hipStreamSynchronize(ctx->stream));
+    jobs.clear();
+    for (int sidx : missing) {
+        const uint8_t *slot = ctx->zc + size_t(sidx) * ss;
+        if (sidx < k)
+            tee_jobs(k, blk, file_out, file_size, sidx, slot, shards[sidx], 0, rows_needed, &jobs);
+        else
+            jobs.push_back({shards[sidx], slot, n});
+    }
+    copy(jobs);
+    return RS_OK;
+}
+
 // The staged form of the host file decode (rs_file_decode's whole-shard
 // case): chunks of block rows through run_chunks.
 int file_decode_staged(const Codec &c, uint8_t *const *shards, size_t S, const uint8_t *present,
@@ -942,6 +1022,9 @@ int file_decode_chunked(const Codec &c, uint8_t *const *shards, const int64_t *l
                                 &taken);
     } else if (big && size_t(S) >= mirror_min_bytes()) {
         rc = file_decode_mirrored(c, shards, present, surv, missing, blk, file_out, size_t(file_size), rows_needed,
+                                  ctx, &taken);
+    } else {
+        rc = file_decode_zc_split(c, shards, present, surv, missing, blk, file_out, size_t(file_size), rows_needed,
                                   ctx, &taken);
     }
     if (rc || taken) return rc;
