@@ -58,9 +58,14 @@ struct FileArgs {
 // non-temporal): IO_NT8 = 8-byte non-temporal, IO_PLAIN8 = 8-byte plain (the
 // two halves of a 16-byte column vector meet in L2), IO_PAIR16 = one 16-byte
 // access when both halves fall in the same block row (8-byte aligned), else
-// two 8-byte accesses.  Chosen at launch (RSAMD_LAYOUT_IO); default IO_PLAIN8,
-// measured best (profiles/r1/layout_io_sweep.txt: file encode 0.78 / decode 0.50
-// of HBM peak vs 0.68 / 0.38 non-temporal and 0.77 / 0.47 paired).
+// two 8-byte accesses.  Chosen at launch (RSAMD_LAYOUT_IO); default
+// IO_PLAIN8, measured best (profiles/r1/layout_io_sweep.txt: file encode 0.78 /
+// decode 0.50 of HBM peak vs 0.68 / 0.38 non-temporal and 0.77 / 0.47 paired).
+// Round 5, 1000-byte blocks, one process and one set of buffers: encode 0.745
+// plain 8-byte against 0.637 paired, 0.633 paired non-temporal -- every other
+// block row starts 8 bytes off a 16-byte boundary, and a 16-byte load there
+// costs far more than two 8-byte ones (tools/file_io_ab.py,
+// profiles/r5/file_io_ab_r6i.txt; the non-temporal form was deleted).
 enum FileIo { IO_NT8 = 0, IO_PLAIN8 = 1, IO_PAIR16 = 2 };
 
 // File byte runs of 8: [f, f+8) clipped to len, zero beyond (the padding).
@@ -578,11 +583,8 @@ __global__ void __launch_bounds__(kThreads) split_merge_kernel(CopyArgs a) {
 }
 
 int file_io_mode() {
-    static const int v = [] {
-        const char *e = tuning_env("RSAMD_LAYOUT_IO");
-        return e ? std::atoi(e) : int(IO_PLAIN8);
-    }();
-    return v;
+    const char *e = tuning_env("RSAMD_LAYOUT_IO");  // per launch (TUNING builds): A/B in one process
+    return e ? std::atoi(e) : int(IO_PLAIN8);
 }
 
 // XCD span for a file-kernel grid of n blocks (RSAMD_FILE_XCD=0 turns the
