@@ -817,8 +817,16 @@ int run_mirrored_impl(ThreadCtx *ctx, MirrorSet *ms, int nbuf, size_t n_chunks, 
 
 size_t mirror_chunk_bytes(size_t total, int nslots, size_t granule) {
     granule = std::max<size_t>(1, granule);
-    // 8 chunks per call when they fit the slot, never under 256 KiB per slot
-    size_t c = std::max<size_t>(size_t(256) << 10, total / 8);
+    // 8 chunks per call when they fit the slot, never under 2 MiB per slot:
+    // calls up to 3 MiB per shard then run as 4 equal chunks (ramp_bounds), 4
+    // MiB as 5.  Each chunk costs a pool batch, a launch and an event; against
+    // a 256 KiB floor (7-11 chunks) 4+2 calls of 1 / 2 / 4 MiB per shard took
+    // 196-198 / 309-320 / 495-507 us instead of 227-285 / 359-384 / 564-584,
+    // 4 and 16 MiB files 233-275 / 555-573 instead of 264-360 / 636-917; 64 MiB
+    // calls are unchanged (profiles/r5/host_sizes_chunkmin_r6k.txt).  TUNING
+    // builds: RSAMD_MIRROR_CHUNKS, RSAMD_MIRROR_CHUNK_MIN.
+    const size_t per = std::max<size_t>(1, rsamd::tuning_size("RSAMD_MIRROR_CHUNKS", 8));
+    size_t c = std::max<size_t>(rsamd::tuning_size("RSAMD_MIRROR_CHUNK_MIN", size_t(2) << 20), total / per);
     c = std::min(c, mirror_slot_bytes() / size_t(std::max(1, nslots)));
     c = std::max(granule, c / granule * granule);
     return c;
