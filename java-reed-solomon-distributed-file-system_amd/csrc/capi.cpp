@@ -747,10 +747,14 @@ int file_encode_mirrored(const Codec &c, const uint8_t *file, size_t file_len, s
 // Direct path of the host file decode on caller-pinned memory: the absent
 // shards rebuilt in place across the link by the shard direct kernels (the
 // survivors read, the rebuilt shards written: only coded bytes cross the
-// link), while the copy pool merges the present data shards into the file;
-// the rebuilt data shards are merged once the kernels are done.  *taken =
-// false, nothing enqueued, when the direct kernels cannot take the plan or a
-// shard has no device address.
+// link), while the copy pool merges the present data shards into the file.
+// When the file is device-mapped too (and everything 8-byte aligned, block %
+// 8 == 0) the kernels store each rebuilt data shard into the file as well
+// (kernels.hpp DirectTee): the extra bytes travel device-to-host, the
+// direction the survivors leave idle, and no merge waits for the kernels.
+// Otherwise the rebuilt data shards are merged once the kernels are done.
+// *taken = false, nothing enqueued, when the direct kernels cannot take the
+// plan or a shard has no device address.
 int file_decode_pinned(const Codec &c, uint8_t *const *shards, const uint8_t *present, const std::vector<int> &missing,
                        size_t blk, uint8_t *file_out, size_t file_size, size_t rows_needed, ThreadCtx *ctx,
                        bool *taken) {
@@ -768,10 +772,27 @@ int file_decode_pinned(const Codec &c, uint8_t *const *shards, const uint8_t *pr
             return RS_OK;
     }
     const size_t n = rows_needed * blk;
-    for (const rsamd::DirectPlan &d : dp) {
+    // TUNING builds: RSAMD_FILE_DEC_TEE=0 merges the rebuilt data shards on the host (A/B)
+    uint8_t *const fdev = dp.empty() ? nullptr : host_dev_addr(file_out);
+    const bool tee = fdev && rsamd::tuning_size("RSAMD_FILE_DEC_TEE", 1) && blk % 8 == 0 &&
+                     reinterpret_cast<uintptr_t>(fdev) % 8 == 0 && reinterpret_cast<uintptr_t>(dp[0].in[0]) % 8 == 0;
+    std::vector<rsamd::DirectTee> tees(dp.size());
+    for (size_t g = 0; g < dp.size(); ++g) {
+        tees[g].file = fdev;
+        tees[g].file_size = file_size;
+        tees[g].blk = blk;
+        tees[g].k = uint64_t(k);
+        for (int q = 0; q < dp[g].nout; ++q) {
+            const int sidx = plan->out_idx()[g * size_t(rsamd::kMaxOut) + size_t(q)];
+            tees[g].data[q] = sidx < k ? sidx : -1;
+        }
+    }
+    if (tee) bounds::allow(fdev, file_size);
+    for (size_t g = 0; g < dp.size(); ++g) {
+        const rsamd::DirectPlan &d = dp[g];
         for (int i = 0; i < d.nin; ++i) bounds::allow(d.in[i], n);
         for (int q = 0; q < d.nout; ++q) bounds::allow(d.out[q], n);
-        RS_HIP(rsamd::launch_gf_direct(d, n, Mode::Code, nullptr, ctx->stream));
+        RS_HIP(rsamd::launch_gf_direct(d, n, Mode::Code, nullptr, ctx->stream, tee ? &tees[g] : nullptr));
     }
     *taken = true;
     std::vector<const uint8_t *> src(shards, shards + k);
@@ -786,6 +807,7 @@ int file_decode_pinned(const Codec &c, uint8_t *const *shards, const uint8_t *pr
     merge_jobs(k, blk, file_out, file_size, src.data(), now, 0, rows_needed, &jobs);
     rsamd::CopyPool::get().copy(jobs);
     RS_HIP(hipStreamSynchronize(ctx->stream));
+    if (tee) return RS_OK;  // the kernels wrote the rebuilt data shards' file bytes
     jobs.clear();
     merge_jobs(k, blk, file_out, file_size, src.data(), later, 0, rows_needed, &jobs);
     rsamd::CopyPool::get().copy(jobs);

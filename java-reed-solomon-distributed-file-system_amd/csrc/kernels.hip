@@ -1175,7 +1175,38 @@ struct DirectArgs {
     uint64_t n;            // bytes per shard
     int nin;
     int *mismatch;
+    DirectTee tee;         // TEE kernels only
 };
+
+// The tee store of one 8-byte unit of data shard d at column c (unit-aligned,
+// so inside one block), clipped to the file (the padding's rows are not file
+// bytes).
+__device__ __forceinline__ void tee8(const DirectTee &t, int d, uint64_t c, uint32_t lo, uint32_t hi) {
+    const uint64_t r = c / t.blk;
+    const uint64_t f = r * t.k * t.blk + uint64_t(d) * t.blk + (c - r * t.blk);
+    if (f + 8 <= t.file_size) {
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        __builtin_nontemporal_store(u32x2{lo, hi}, reinterpret_cast<u32x2 *>(RSAMD_G(t.file + f, 8)));
+        return;
+    }
+    const uint64_t x = uint64_t(lo) | uint64_t(hi) << 32;
+    for (uint64_t b = f; b < t.file_size && b < f + 8; ++b) *RSAMD_G(t.file + b, 1) = uint8_t(x >> (8 * (b - f)));
+}
+
+// The same for a 16-byte vector at column c: one 16-byte store when both
+// halves lie in one block row and in the file (consecutive lanes then cover
+// whole lines with one instruction), else two 8-byte ones.
+__device__ __forceinline__ void tee16(const DirectTee &t, int d, uint64_t c, const u32x4 &y) {
+    const uint64_t r = c / t.blk, w = c - r * t.blk;
+    const uint64_t f = r * t.k * t.blk + uint64_t(d) * t.blk + w;
+    if (w + 16 <= t.blk && f + 16 <= t.file_size) {
+        typedef uint32_t u32x4_a8 __attribute__((ext_vector_type(4), aligned(8)));
+        __builtin_nontemporal_store(u32x4_a8{y[0], y[1], y[2], y[3]}, reinterpret_cast<u32x4_a8 *>(RSAMD_G(t.file + f, 16)));
+        return;
+    }
+    tee8(t, d, c, y[0], y[1]);
+    tee8(t, d, c + 8, y[2], y[3]);
+}
 
 template <int W>
 struct DirectVec;
@@ -1190,7 +1221,7 @@ struct DirectVec<8> {
     static constexpr int kDwords = 2;
 };
 
-template <int W, int M, bool VERIFY>
+template <int W, int M, bool VERIFY, bool TEE>
 __global__ void __launch_bounds__(kThreads) gf_direct_kernel(DirectArgs a) {
     typedef typename DirectVec<W>::T V;
     constexpr int D = DirectVec<W>::kDwords;
@@ -1235,6 +1266,12 @@ __global__ void __launch_bounds__(kThreads) gf_direct_kernel(DirectArgs a) {
                 if (!same) flag_mismatch(a.mismatch);
             } else {
                 __builtin_nontemporal_store(y, dst);
+                if (TEE && a.tee.data[p] >= 0) {
+                    if constexpr (W == 16)
+                        tee16(a.tee, a.tee.data[p], off, y);
+                    else
+                        tee8(a.tee, a.tee.data[p], off, y[0], y[1]);
+                }
             }
         }
     }
@@ -1259,6 +1296,11 @@ __global__ void __launch_bounds__(kThreads) gf_direct_kernel(DirectArgs a) {
                 if (*RSAMD_G(a.out[p] + b, 1) != uint8_t(acc[p])) flag_mismatch(a.mismatch);
             } else {
                 *RSAMD_G(a.out[p] + b, 1) = uint8_t(acc[p]);
+                if (TEE && a.tee.data[p] >= 0) {
+                    const uint64_t r = b / a.tee.blk;
+                    const uint64_t f = r * a.tee.k * a.tee.blk + uint64_t(a.tee.data[p]) * a.tee.blk + (b - r * a.tee.blk);
+                    if (f < a.tee.file_size) *RSAMD_G(a.tee.file + f, 1) = uint8_t(acc[p]);
+                }
             }
         }
     }
@@ -1947,9 +1989,11 @@ namespace {
 template <int W, int M>
 void launch_direct_t(const DirectArgs &a, unsigned grid, Mode mode, hipStream_t s) {
     if (mode == Mode::Verify)
-        hipLaunchKernelGGL((gf_direct_kernel<W, M, true>), dim3(grid), dim3(kThreads), 0, s, a);
+        hipLaunchKernelGGL((gf_direct_kernel<W, M, true, false>), dim3(grid), dim3(kThreads), 0, s, a);
+    else if (a.tee.file)
+        hipLaunchKernelGGL((gf_direct_kernel<W, M, false, true>), dim3(grid), dim3(kThreads), 0, s, a);
     else
-        hipLaunchKernelGGL((gf_direct_kernel<W, M, false>), dim3(grid), dim3(kThreads), 0, s, a);
+        hipLaunchKernelGGL((gf_direct_kernel<W, M, false, false>), dim3(grid), dim3(kThreads), 0, s, a);
 }
 template <int W>
 hipError_t dispatch_direct(const DirectArgs &a, int nout, unsigned grid, Mode mode, hipStream_t s) {
@@ -1972,8 +2016,12 @@ hipError_t dispatch_direct(const DirectArgs &a, int nout, unsigned grid, Mode mo
 //   anonymous mmap  47.3   51.6   52.4   51.1   47.5
 constexpr unsigned kDirectBlocks = 256;
 
-hipError_t launch_gf_direct(const DirectPlan &p, size_t n, Mode mode, int *mismatch, hipStream_t s) {
+hipError_t launch_gf_direct(const DirectPlan &p, size_t n, Mode mode, int *mismatch, hipStream_t s,
+                            const DirectTee *tee) {
     if (p.nin < 1 || p.nin > kMaxDirectIn || p.nout < 1 || p.nout > kMaxOut) return hipErrorInvalidValue;
+    if (tee && (mode != Mode::Code || !tee->file || tee->blk == 0 || tee->blk % 8 || tee->k < 1 ||
+                reinterpret_cast<uintptr_t>(tee->file) % 8 || reinterpret_cast<uintptr_t>(p.in[0]) % 8))
+        return hipErrorInvalidValue;  // (the shards share in[0]'s residue: checked below)
     if (n == 0) return hipSuccess;
     // The widest vector every shard's address agrees on (same residue).
     int W = 16;
@@ -2013,6 +2061,7 @@ hipError_t launch_gf_direct(const DirectPlan &p, size_t n, Mode mode, int *misma
     a.n = n;
     a.nin = p.nin;
     a.mismatch = mismatch;
+    if (tee) a.tee = *tee;  // (head % 8 == 0: in[0] is 8-byte aligned and align >= 8)
     const uint64_t blocks = tuning_size("RSAMD_DIRECT_BLOCKS", kDirectBlocks);  // per call in TUNING builds
     const unsigned grid = unsigned(std::max<uint64_t>(1, std::min<uint64_t>(blocks, (a.nvec + kThreads - 1) / kThreads)));
     return W == 16 ? dispatch_direct<16>(a, p.nout, grid, mode, s) : dispatch_direct<8>(a, p.nout, grid, mode, s);

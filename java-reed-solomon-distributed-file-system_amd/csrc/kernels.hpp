@@ -84,7 +84,20 @@ struct DirectPlan {
     const uint32_t *tabs = nullptr;
     int nin = 0, nout = 0;
 };
-hipError_t launch_gf_direct(const DirectPlan &p, size_t n, Mode mode, int *mismatch, hipStream_t s);
+// The file tee of a direct decode (capi.cpp file_decode_pinned): every output
+// that is data shard d < k is also stored into its blocks of the client's
+// file -- column c = r * blk + w of data shard d is file byte (r k + d) blk + w
+// (ReedSolomonDecoder.java:92-103), clipped to the file's size -- so a rebuilt
+// data shard reaches the file in the pass that writes it.  The shard
+// addresses and the file's must be 8-byte aligned and blk % 8 == 0 (every
+// 8-byte unit then lies in one block); the outputs start at column 0.
+struct DirectTee {
+    uint8_t *file = nullptr;  // device address
+    uint64_t file_size = 0, blk = 0, k = 0;
+    int data[kMaxOut] = {-1, -1, -1, -1};  // output q's data shard, or -1 (parity)
+};
+hipError_t launch_gf_direct(const DirectPlan &p, size_t n, Mode mode, int *mismatch, hipStream_t s,
+                            const DirectTee *tee = nullptr);
 
 hipError_t launch_fill_synthetic(uint8_t *base, int k, size_t n_stripes, size_t shard_len,
                                  size_t shard_stride, size_t stripe_stride, uint64_t seed,

@@ -163,7 +163,8 @@ def test_file_pinned_random(gpu, oracle_lib, case):
     encode's tiled kernel (layout.hip file_direct_tiled_kernel; 64 KiB of
     block rows per workgroup, one row when a row is larger, the column kernel
     past that) across k, m and block sizes, then a decode with random
-    erasures, against the oracle."""
+    erasures (rebuilt data shards teed into the file by the direct kernels
+    when block % 8 == 0), against the oracle."""
     import rsamd
     from rsamd.device import HostBuffer
     from rsamd.layout import file_decode_into, file_encode_into, file_layout
@@ -187,9 +188,13 @@ def test_file_pinned_random(gpu, oracle_lib, case):
     miss = sorted(int(x) for x in rng.choice(k + m, e, replace=False))
     for j in miss:
         views[j][:] = 0
-    out = HostBuffer(n)
-    file_decode_into(rs, views, [i not in miss for i in range(k + m)], S, out.array, block)
-    assert np.array_equal(out.array, f.array), (k, m, block, n, miss)
+    # the decode's kernels write rebuilt data shards straight into the file
+    # (kernels.hpp DirectTee): 4 KiB of sentinel past the file's end must stay
+    out = HostBuffer(n + 4096)
+    out.array[:] = 0x33
+    file_decode_into(rs, views, [i not in miss for i in range(k + m)], S, out.array[:n], block)
+    assert np.array_equal(out.array[:n], f.array), (k, m, block, n, miss)
+    assert (out.array[n:] == 0x33).all(), (k, m, block, n, miss)
     assert_same(views, list(ref), (k, m, block, n, miss))
     for b in sh + [f, out]:
         b.free()
