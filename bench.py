@@ -1409,12 +1409,14 @@ def host_inclusive(rsamd, k, m, link=None):
     rs = rsamd.ReedSolomon.create(k, m)
     out = {}
 
-    def rate(fn, user_bytes, reps=12):
+    def rate(fn, user_bytes, reps=24):
         # 3 untimed calls: the first allocates the staging buffers, and the
         # second of a fresh process still runs at a third of the rate (14.6 ms
         # against 5.6 ms for a 4+2 x 64 MiB encode, tools/host_trace.py).
-        # 12 timed calls: a single slow call moved a 5-call mean by 5%
-        # (profiles/r3/host_calls_r3zf.txt: pageable calls 5.56-5.65 ms)
+        # 24 timed calls: a single slow call moved a 5-call mean by 5%
+        # (profiles/r3/host_calls_r3zf.txt: pageable calls 5.56-5.65 ms), and
+        # the 12-call pinned encode read 0.917 of the link bound in one run
+        # against 1.00-1.01 in every other (profiles/r5/bench_r6q.json)
         for _ in range(3):
             fn()
         t0 = time.perf_counter()
