@@ -545,12 +545,18 @@ int run_chunks_impl(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinn
 // ---------------------------------------------------------------------------
 namespace {
 // Pinned bytes per slot (TUNING builds: RSAMD_MIRROR_BYTES).
-// 48 MiB: a direct kernel over a chunk costs ~70 us on top of its bytes, so
+// 64 MiB: a direct kernel over a chunk costs ~70 us on top of its bytes, so
 // larger chunks run closer to the link (4+2 x 64 MiB, no host copies: 0.893 of
 // the link bound at 24 MiB slots, 0.953 at 48 MiB; with the copies 0.853 /
-// 0.888; 16 MiB 0.832; profiles/r5/host_legs_r5d.txt, r5e).
+// 0.888; 16 MiB 0.832; profiles/r5/host_legs_r5d.txt, r5e).  With 6 chunks per
+// call (mirror_chunk_bytes) instead of 8 in 48 MiB slots, the bench's host legs
+// (encode / decode {0,1} / file encode / file decode {0,5}, mean of four child
+// processes alternated with the others) read 0.872 / 0.870 / 0.716 / 0.880 of
+// the link bound against 0.854 / 0.839 / 0.691 / 0.845; 96 MiB slots with 4
+// chunks and 128 MiB with 3 read the same as 64 MiB with 6 within a point
+// (profiles/r5/host_legs_bigchunks_r6r.txt, host_legs_bigchunks2_r6s.txt).
 size_t mirror_slot_bytes() {
-    static const size_t v = rsamd::tuning_size("RSAMD_MIRROR_BYTES", size_t(48) << 20);
+    static const size_t v = rsamd::tuning_size("RSAMD_MIRROR_BYTES", size_t(64) << 20);
     return v;
 }
 
@@ -817,7 +823,8 @@ int run_mirrored_impl(ThreadCtx *ctx, MirrorSet *ms, int nbuf, size_t n_chunks, 
 
 size_t mirror_chunk_bytes(size_t total, int nslots, size_t granule) {
     granule = std::max<size_t>(1, granule);
-    // 8 chunks per call when they fit the slot, never under 2 MiB per slot:
+    // 6 chunks per call when they fit the slot (mirror_slot_bytes), never
+    // under 2 MiB per slot:
     // calls up to 3 MiB per shard then run as 4 equal chunks (ramp_bounds), 4
     // MiB as 5.  Each chunk costs a pool batch, a launch and an event; against
     // a 256 KiB floor (7-11 chunks) 4+2 calls of 1 / 2 / 4 MiB per shard took
@@ -825,7 +832,7 @@ size_t mirror_chunk_bytes(size_t total, int nslots, size_t granule) {
     // 4 and 16 MiB files 233-275 / 555-573 instead of 264-360 / 636-917; 64 MiB
     // calls are unchanged (profiles/r5/host_sizes_chunkmin_r6k.txt).  TUNING
     // builds: RSAMD_MIRROR_CHUNKS, RSAMD_MIRROR_CHUNK_MIN.
-    const size_t per = std::max<size_t>(1, rsamd::tuning_size("RSAMD_MIRROR_CHUNKS", 8));
+    const size_t per = std::max<size_t>(1, rsamd::tuning_size("RSAMD_MIRROR_CHUNKS", 6));
     size_t c = std::max<size_t>(rsamd::tuning_size("RSAMD_MIRROR_CHUNK_MIN", size_t(2) << 20), total / per);
     c = std::min(c, mirror_slot_bytes() / size_t(std::max(1, nslots)));
     c = std::max(granule, c / granule * granule);

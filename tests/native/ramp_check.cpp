@@ -42,7 +42,7 @@ int main() {
         for (size_t total : {size_t(1000), size_t(1) << 20, size_t(64) << 20, size_t(1) << 30}) {
             const size_t c = rsamd::host::mirror_chunk_bytes(total, nslots, 4096);
             ++cases;
-            if (c == 0 || c % 4096 || c * size_t(nslots) > (size_t(48) << 20) + 4096 * size_t(nslots))
+            if (c == 0 || c % 4096 || c * size_t(nslots) > (size_t(64) << 20) + 4096 * size_t(nslots))
                 fail("mirror_chunk_bytes", total, size_t(nslots), 4096);
         }
     std::printf("%d cases, %d bad\n", cases, bad);
