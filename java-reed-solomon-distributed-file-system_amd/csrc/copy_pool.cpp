@@ -124,8 +124,13 @@ void copy_piece(const CopyJob &j) {
         return s && j.rows > 1 && dst_stride == j.n && j.n >= 32 && use_stream() && !tuning_size("RSAMD_COPY_ROWWISE", 0);
     };
     if (gathers(j.dst_stride) && (!d2 || gathers(j.dst2_stride))) {
+        // Two passes, the second reading the source again from this core's
+        // cache: one pass loading each 16 bytes once and streaming them to both
+        // destinations (16-byte stores; a caller's array and its slot agree only
+        // modulo 16) made the 256 MiB pageable file encode slower, 35.1-35.5
+        // GiB/s against 37.0-37.4 (profiles/r5/host_legs_dual_r6u.txt; deleted).
         gather_stream(d, s, j.n, j.rows, j.src_stride);
-        if (d2) gather_stream(d2, s, j.n, j.rows, j.src_stride);  // the source again, from this core's cache
+        if (d2) gather_stream(d2, s, j.n, j.rows, j.src_stride);
     } else if (s && d2 && j.rows > 1 && j.src_stride == j.n && j.dst_stride == j.n && use_stream()) {
         // a contiguous run teed into rows (a decode's data shard into its slot
         // and the file): the run in one stream, then the rows from this core's cache

@@ -20,6 +20,7 @@ int main() {  // copy_pool.cpp gathers, tees, zero fills: every byte against a p
         size_t n = 1 + rng() % 5000, rows = 1 + rng() % 300, sstride = n + rng() % 9000;
         if (it % 3 == 0) n = 1000, sstride = 4000;
         size_t doff = rng() % 64, soff = rng() % 64, d2off = rng() % 64;
+        if (it % 4 == 1) d2off = doff % 16 + 16 * (rng() % 3);  // destinations agreeing modulo 16
         std::vector<uint8_t> src(soff + sstride * rows + n), dst(doff + n * rows + 64, 0xEE), dst2(d2off + n * rows + 64, 0xDD);
         for (auto &b : src) b = uint8_t(rng());
         rsamd::CopyJob j{dst.data() + doff, src.data() + soff, n, rows, n, sstride};
@@ -37,6 +38,7 @@ int main() {  // copy_pool.cpp gathers, tees, zero fills: every byte against a p
             if (j.dst2 && memcmp(dst2.data() + d2off + r * n, src.data() + soff + r * sstride, n)) { ++bad; printf("bad2 n=%zu rows=%zu r=%zu\n", n, rows, r); break; }
         }
         if (dst[doff + n * rows] != 0xEE || (doff && dst[doff - 1] != 0xEE)) { ++bad; printf("overrun n=%zu\n", n); }
+        if (j.dst2 && (dst2[d2off + n * rows] != 0xDD || (d2off && dst2[d2off - 1] != 0xDD))) { ++bad; printf("overrun2 n=%zu\n", n); }
     }
     // a contiguous run teed into strided rows (a decode's data shard into its
     // slot and the file): every byte of both destinations, nothing past them
