@@ -8,7 +8,7 @@ knobs; each prints one JSON line.  The pageable encode is checked against the
 oracle.  --trace writes the mirrored pipeline's per-chunk timeline
 (RSAMD_TRACE, TUNING build) of the pageable encode calls to the given file.
   python tools/host_legs.py [--lib build/ab/tuning/librsamd.so]
-                            [--var RSAMD_MIRROR_BYTES=16777216,RSAMD_COPY_NT=0 ...] [--trace FILE]"""
+                            [--var RSAMD_MIRROR_BYTES=16777216,RSAMD_COPY_NT=0 ...] [--trace FILE] [--small]"""
 import argparse
 import json
 import os
@@ -36,6 +36,9 @@ def child(trace):
     with bench.gpu_numa_bound(torch, parallel, extra):
         link = bench.host_link(torch)
         out.update(bench.host_inclusive(rsamd, 4, 2, link))
+        if os.environ.get("HOST_LEGS_SMALL"):  # the bench's next legs: small calls after the large ones
+            out.update(bench.config0_single_stripe(rsamd, 4, 2))
+            out.update(bench.host_by_size(rsamd, 4, 2))
         # the pageable encode against the oracle (and, traced, a timeline of it)
         k, m, n = 4, 2, 64 << 20
         rng = np.random.default_rng(9)
@@ -68,12 +71,15 @@ def main():
     ap.add_argument("--lib", default=os.path.join(ROOT, "build/ab/tuning/librsamd.so"))
     ap.add_argument("--var", nargs="*", default=[""], help="comma-separated NAME=VALUE settings, one child each")
     ap.add_argument("--trace", default="")
+    ap.add_argument("--small", action="store_true", help="then the bench's small-call legs (configs[0], by size)")
     ap.add_argument("--child", action="store_true")
     a = ap.parse_args()
     if a.child:
         return child(a.trace)
     for var in a.var:
         env = dict(os.environ, RSAMD_TEST_LIB=a.lib)
+        if a.small:
+            env["HOST_LEGS_SMALL"] = "1"
         for kv in filter(None, var.split(",")):
             key, val = kv.split("=", 1)
             env[key] = val
