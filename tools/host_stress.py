@@ -1,12 +1,14 @@
 #!/usr/bin/env python3
 """Concurrency stress of the host paths (the process-wide copy pool with its
 polling threads, the mirrored pipeline's shared slot sets, the zero-copy
-path): T threads at once, each making random pageable calls -- encodeParity /
-decodeMissing at random sizes (4 KiB .. 24 MiB per shard) and offsets, and
-file encode / decode at random sizes and blocks -- for a fixed time, every
-result checked against the oracle.  Prints one JSON line per thread and a
-summary; exits 1 on any mismatch.
-  python tools/host_stress.py [--threads 8] [--seconds 60]"""
+path, and with --pinned P a share P of the calls on the library's pinned
+buffers: the in-place direct kernels, the pinned file decode's file tee): T
+threads at once, each making random calls -- encodeParity / decodeMissing at
+random sizes (4 KiB .. 24 MiB per shard) and offsets, and file encode / decode
+at random sizes and blocks (4 KiB of sentinel past the decoded file) -- for a
+fixed time, every result checked against the oracle.  Prints one JSON line
+per thread and a summary; exits 1 on any mismatch.
+  python tools/host_stress.py [--threads 8] [--seconds 60] [--pinned 0.3]"""
 import argparse
 import json
 import os
@@ -19,14 +21,32 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "java-reed-solomon-distributed-file-system_amd"))
 
 
-def worker(tid, seconds, oracle, res):
+def worker(tid, seconds, oracle, res, pinned_share=0.0):
     import numpy as np
     import rsamd
+    from rsamd.device import HostBuffer
     from rsamd.layout import file_decode_into, file_encode_into, file_layout
     rng = np.random.default_rng(1000 + tid)
-    calls = bad = 0
+    calls = bad = npinned = 0
     t_end = time.time() + seconds
     while time.time() < t_end:
+        pinned = rng.random() < pinned_share
+        held = []
+
+        def buf(size, fill=None):  # a pageable array, or one on rs_host_alloc memory
+            if pinned:
+                held.append(HostBuffer(size))
+                a = held[-1].array
+                if fill is not None:
+                    a[:] = fill
+                return a
+            return np.zeros(size, np.uint8) if fill is None else np.full(size, fill, np.uint8)
+
+        def rand(size):
+            a = buf(size)
+            a[:] = rng.integers(0, 256, size, dtype=np.uint8)
+            return a
+
         k = int(rng.choice([4, 4, 10, 3, 6]))
         m = int(rng.choice([2, 2, 4, 1, 3]))
         rs = rsamd.ReedSolomon.create(k, m)
@@ -36,7 +56,7 @@ def worker(tid, seconds, oracle, res):
             n += int(rng.integers(0, 4096))
             off = int(rng.integers(0, 64))
             cnt = n - off - int(rng.integers(0, 64))
-            sh = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)] + [np.zeros(n, np.uint8) for _ in range(m)]
+            sh = [rand(n) for _ in range(k)] + [buf(n, 0) for _ in range(m)]
             ref = [a.copy() for a in sh]
             oc.encode_parity(ref, off, cnt)
             rs.encodeParity(sh, off, cnt)
@@ -50,9 +70,9 @@ def worker(tid, seconds, oracle, res):
         else:
             block = int(rng.choice([1000, 1000, 4096, 520, 8]))
             n = int(rng.choice([90_999, 1 << 20, 5 << 20, 20 << 20])) + int(rng.integers(0, 5000))
-            data = rng.integers(0, 256, n, dtype=np.uint8)
+            data = rand(n)
             _, S = file_layout(rs, n, block)
-            sh = [np.full(S, 0xEE, np.uint8) for _ in range(k + m)]
+            sh = [buf(S, 0xEE) for _ in range(k + m)]
             file_encode_into(rs, data, sh, block)
             ref = oc.file_encode(data.tobytes(), block)
             ok = all(np.array_equal(a, b) for a, b in zip(sh, ref))
@@ -60,18 +80,23 @@ def worker(tid, seconds, oracle, res):
             miss = sorted(int(x) for x in rng.choice(k + m, e, replace=False))
             for j in miss:
                 sh[j][:] = 0
-            out = np.zeros(n, np.uint8)
-            file_decode_into(rs, sh, [i not in miss for i in range(k + m)], S, out, block)
-            ok = ok and np.array_equal(out, data) and all(np.array_equal(a, b) for a, b in zip(sh, ref))
+            out = buf(n + 4096, 0x33)
+            file_decode_into(rs, sh, [i not in miss for i in range(k + m)], S, out[:n], block)
+            ok = ok and np.array_equal(out[:n], data) and bool((out[n:] == 0x33).all()) and \
+                all(np.array_equal(a, b) for a, b in zip(sh, ref))
         calls += 1
+        npinned += int(pinned)
         bad += 0 if ok else 1
-    res[tid] = {"thread": tid, "calls": calls, "bad": bad}
+        for h in held:
+            h.free()
+    res[tid] = {"thread": tid, "calls": calls, "pinned_calls": npinned, "bad": bad}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--seconds", type=float, default=60)
+    ap.add_argument("--pinned", type=float, default=0.0, help="share of calls on rs_host_alloc buffers")
     a = ap.parse_args()
     from rsamd import _lib
     if os.environ.get("RSAMD_TEST_LIB"):  # e.g. the bounds-checking build
@@ -80,7 +105,7 @@ def main():
     torch.cuda.init()
     from oracle import c_ref
     res = {}
-    ts = [threading.Thread(target=worker, args=(t, a.seconds, c_ref, res)) for t in range(a.threads)]
+    ts = [threading.Thread(target=worker, args=(t, a.seconds, c_ref, res, a.pinned)) for t in range(a.threads)]
     for t in ts:
         t.start()
     for t in ts:
