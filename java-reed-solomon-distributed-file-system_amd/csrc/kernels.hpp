@@ -96,6 +96,7 @@ struct DirectTee {
     uint64_t file_size = 0, blk = 0, k = 0;
     int data[kMaxOut] = {-1, -1, -1, -1};  // output q's data shard, or -1 (parity)
 };
+static_assert(kMaxOut == 4, "DirectTee::data initialises kMaxOut entries");
 hipError_t launch_gf_direct(const DirectPlan &p, size_t n, Mode mode, int *mismatch, hipStream_t s,
                             const DirectTee *tee = nullptr);
 
