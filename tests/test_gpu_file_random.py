@@ -198,3 +198,38 @@ def test_file_pinned_random(gpu, oracle_lib, case):
     assert_same(views, list(ref), (k, m, block, n, miss))
     for b in sh + [f, out]:
         b.free()
+
+
+@pytest.mark.parametrize("block", [1000, 8, 520])
+def test_file_pinned_two_launch_groups(gpu, oracle_lib, block):
+    """A pinned file decode whose plan needs two direct launches (six absent
+    shards, at most four outputs per launch): the second launch's rebuilt data
+    shards reach the file through its own tee entries (kernels.hpp
+    DirectTee; block 520 is not a multiple of 8 and merges on the host)."""
+    import rsamd
+    from rsamd.device import HostBuffer
+    from rsamd.layout import file_decode_into, file_encode_into, file_layout
+    k, m = 8, 6
+    rng = np.random.default_rng(7100 + block)
+    n = k * block * 300 + int(rng.integers(1, k * block))
+    rs = rsamd.ReedSolomon.create(k, m)
+    oc = oracle_lib.Codec(k, m)
+    _, S = file_layout(rs, n, block)
+    f = HostBuffer(n)
+    f.array[:] = rng.integers(0, 256, n, dtype=np.uint8)
+    sh = [HostBuffer(S) for _ in range(k + m)]
+    views = [b.array for b in sh]
+    file_encode_into(rs, f.array, views, block)
+    ref = oc.file_encode(f.array.tobytes(), block)
+    assert_same(views, list(ref), (k, m, block, n))
+    miss = [0, 2, 3, 5, 7, 9]  # five data shards (over both launches) and a parity shard
+    for j in miss:
+        views[j][:] = 0
+    out = HostBuffer(n + 4096)
+    out.array[:] = 0x33
+    file_decode_into(rs, views, [i not in miss for i in range(k + m)], S, out.array[:n], block)
+    assert np.array_equal(out.array[:n], f.array), (block, n)
+    assert (out.array[n:] == 0x33).all(), (block, n)
+    assert_same(views, list(ref), (k, m, block, n, miss))
+    for b in sh + [f, out]:
+        b.free()
