@@ -304,13 +304,18 @@ def run(args, live_traffic=None):
             extra.update(granule_legs(torch, rsamd, rdev, dev, stream, headline_layout=args.layout))
             extra.update(chunk_group_legs(torch, rsamd, rdev, dev, stream))
             extra.update(layout_legs(torch, rsamd, dev, stream))
-            cpu = cpu_baseline(k, m, S, args.cpu_seconds)
-            extra["cpu_configs"] = cpu_configs()
+            # The host legs before the CPU baseline, small calls first: run
+            # after the baseline's 16 busy threads and the large host calls, the
+            # configs[0] and 64 KiB calls took 44-52 us against 37 in a process
+            # of their own (profiles/r5/bench_r6q.json, bench_r6x.json,
+            # host_sizes_slots_r6t.txt).
             with gpu_numa_bound(torch, parallel, extra):
                 link = host_link(torch)
-                extra.update(host_inclusive(rsamd, k, m, link))
                 extra.update(config0_single_stripe(rsamd, k, m))
                 extra.update(host_by_size(rsamd, k, m))
+                extra.update(host_inclusive(rsamd, k, m, link))
+            cpu = cpu_baseline(k, m, S, args.cpu_seconds)
+            extra["cpu_configs"] = cpu_configs()
         else:
             # every rank at once: the node's aggregate host <-> device rate
             with gpu_numa_bound(torch, parallel, extra):
