@@ -82,23 +82,26 @@ void gather_plain(uint8_t *dst, const uint8_t *src, size_t n, size_t src_stride,
 // instead leaves each short row's first and last line partly written by
 // streaming stores, which costs those lines a read-modify-write.  A vector
 // that straddles two rows is assembled from both.
-// With `prefetch`, each row's successor is prefetched as the row starts: the
-// rows are short runs src_stride apart (a file's 1000-byte blocks 4000 bytes
-// apart), where the hardware prefetchers restart at every row and each row's
-// first lines miss.
+// With `prefetch` = p > 0, the row p rows on is prefetched as each row
+// starts: the rows are short runs src_stride apart (a file's 1000-byte blocks
+// 4000 bytes apart), where the hardware prefetchers restart at every row and
+// each row's first lines miss.
 __attribute__((target("avx2"))) void gather_stream(uint8_t *dst, const uint8_t *src, size_t n, size_t rows,
-                                                   size_t src_stride, bool prefetch) {
+                                                   size_t src_stride, size_t prefetch) {
     const size_t total = n * rows;
     size_t x = std::min(total, (32 - reinterpret_cast<uintptr_t>(dst) % 32) % 32);
     gather_plain(dst, src, n, src_stride, 0, x);
     size_t r = x / n, c = x % n;
     const uint8_t *sp = src + r * src_stride + c;
-    auto ahead = [&](size_t row) {  // the row after `row`, line by line
-        if (!prefetch || row + 1 >= rows) return;
-        const char *p = reinterpret_cast<const char *>(src + (row + 1) * src_stride);
+    auto fetch = [&](size_t row) {  // one row, line by line
+        if (row >= rows) return;
+        const char *p = reinterpret_cast<const char *>(src + row * src_stride);
         for (size_t l = 0; l < n; l += 64) _mm_prefetch(p + l, _MM_HINT_T0);
     };
-    ahead(r);
+    auto ahead = [&](size_t row) {  // entering `row`: the row `prefetch` rows on
+        if (prefetch) fetch(row + prefetch);
+    };
+    for (size_t q = 1; q <= prefetch; ++q) fetch(r + q);
     for (; x + 32 <= total; x += 32) {
         __m256i v;
         if (c + 32 <= n) {
@@ -128,9 +131,13 @@ __attribute__((target("avx2"))) void gather_stream(uint8_t *dst, const uint8_t *
     gather_plain(dst, src, n, src_stride, x, total - x);
 }
 
-bool use_prefetch() {
-    static const bool on = tuning_size("RSAMD_COPY_PREFETCH", 1) != 0;
-    return on;
+// Rows ahead the gather prefetches (TUNING builds: RSAMD_COPY_PREFETCH, 0 = none).
+// 256 MiB pageable file encode, three alternated runs each: none 39.5-40.6
+// GiB/s; 1 row 44.4-45.5; 2 rows 44.9-45.5; 3 rows 43.4-45.4
+// (profiles/r5/host_legs_prefetch_r7d.txt, host_legs_pfdist_r7i.txt).
+size_t prefetch_rows() {
+    static const size_t v = tuning_size("RSAMD_COPY_PREFETCH", 2);
+    return v;
 }
 
 void copy_piece(const CopyJob &j) {
@@ -147,8 +154,8 @@ void copy_piece(const CopyJob &j) {
         // modulo 16) made the 256 MiB pageable file encode slower, 35.1-35.5
         // GiB/s against 37.0-37.4 (profiles/r5/host_legs_dual_r6u.txt; deleted).
         // (TUNING builds: RSAMD_COPY_PREFETCH=0 turns the row prefetch off, A/B)
-        gather_stream(d, s, j.n, j.rows, j.src_stride, use_prefetch());
-        if (d2) gather_stream(d2, s, j.n, j.rows, j.src_stride, false);
+        gather_stream(d, s, j.n, j.rows, j.src_stride, prefetch_rows());
+        if (d2) gather_stream(d2, s, j.n, j.rows, j.src_stride, 0);
     } else if (s && d2 && j.rows > 1 && j.src_stride == j.n && j.dst_stride == j.n && use_stream()) {
         // a contiguous run teed into rows (a decode's data shard into its slot
         // and the file): the run in one stream, then the rows from this core's cache
