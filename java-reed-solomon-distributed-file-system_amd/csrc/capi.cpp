@@ -202,6 +202,80 @@ int run_mirror_host(ThreadCtx *ctx, const std::vector<DevPlan> &plans, int nslot
     return run_mirrored(ctx, cb.size() - 1, slot_stride * size_t(nslots), io, code);
 }
 
+// Small calls (one zero-copy pass, one launch group): the inputs are copied
+// into the context's coherent, device-mapped buffer, ONE direct-kernel launch
+// codes it in place over the link -- 16-byte vectors, its head and tail bytes
+// in the same launch -- and signals its completion into host memory, where
+// this thread spins (kernels.hpp DirectSignal); then the outputs are copied
+// back.  Against the staged pass it replaces (the stripe kernels over the
+// buffer, then a stream synchronisation), measured from C on one MI355X
+// (tools/small_latency.hip, profiles/r6/small_latency_*.json): 4+2 x 1000 B
+// decodeMissing 18.6 -> see DESIGN.md 5.2 -- at 1000 B the stripe kernels had
+// no whole 1 KiB wave span and coded every byte in the byte kernel (8.7 us of
+// GPU time), and a stream synchronisation observes a finished kernel ~3 us
+// later than the spin does.  *taken = false (nothing done) for plans of more
+// than one launch group or wider than the direct kernels take.
+bool small_signal_enabled() { return rsamd::tuning_size("RSAMD_SMALL_SIGNAL", 1) != 0; }  // TUNING builds: A/B
+
+int run_small(ThreadCtx *ctx, const std::vector<DevPlan> &plans, int nslots, const std::vector<int> &in_slots,
+              const std::vector<int> &out_slots, uint8_t *const *host, size_t offset, size_t count, Mode mode,
+              int *result, bool *taken) {
+    *taken = false;
+    if (plans.size() != 1 || count == 0 || !small_signal_enabled()) return RS_OK;
+    const size_t ss = round_up(count, 256), bytes = ss * size_t(nslots);
+    if (bytes > zero_copy_limit()) return RS_OK;
+    int rc = zero_copy_buffer(ctx, bytes);
+    if (rc) return rc;
+    std::vector<rsamd::DirectPlan> dp;
+    if (!direct_plans(plans, in_slots, out_slots, [&](int sl) { return ctx->zc_dev + size_t(sl) * ss; }, &dp))
+        return RS_OK;
+    rsamd::DirectSignal sg;
+    rc = next_signal(ctx, &sg.flag, &sg.ctr, &sg.seq);
+    if (rc) return rc;
+    *taken = true;
+    // host copies on this thread; the copy pool only above 2 MiB (as run_zero_copy)
+    const bool use_pool = bytes > (size_t(2) << 20);
+    std::vector<rsamd::CopyJob> jobs;
+    auto copy = [&]() {
+        if (use_pool)
+            rsamd::CopyPool::get().copy(jobs);
+        else
+            for (const rsamd::CopyJob &j : jobs) std::memcpy(j.dst, j.src, j.n);
+        jobs.clear();
+    };
+    // The kernel codes whole 16-byte vectors: each slot's bytes past `count`
+    // up to the next 16 are zeroed (0 codes to 0, so a verify compares them
+    // equal) and coded too, no byte tail in the launch (at 1000-byte shards
+    // the tail's per-input byte loads cost several link round trips).
+    const size_t n16 = round_up(count, 16);
+    for (int s : in_slots) {
+        jobs.push_back({ctx->zc + size_t(s) * ss, host[s] + offset, count});
+        if (n16 > count) std::memset(ctx->zc + size_t(s) * ss + count, 0, n16 - count);
+    }
+    copy();
+    const rsamd::DirectPlan &d = dp[0];
+    for (int i = 0; i < d.nin; ++i) bounds::allow(d.in[i], n16);
+    for (int q = 0; q < d.nout; ++q) bounds::allow(d.out[q], n16);
+    const hipError_t e = rsamd::launch_gf_direct(d, n16, mode, ctx->flag, ctx->stream, nullptr, &sg);
+    if (e != hipSuccess) {
+        (void)hipStreamSynchronize(ctx->stream);
+        return hip_fail(e, "launch_gf_direct (small call)");
+    }
+    uint32_t mm = 0;
+    rc = wait_signal(ctx, sg.seq, &mm);
+    if (rc) {
+        (void)hipStreamSynchronize(ctx->stream);
+        return rc;
+    }
+    if (mode == Mode::Verify) {
+        *result = mm ? 0 : 1;
+        return RS_OK;
+    }
+    for (int s : out_slots) jobs.push_back({host[s] + offset, ctx->zc + size_t(s) * ss, count});
+    copy();
+    return RS_OK;
+}
+
 // Stage [offset, offset+count) of the host shards (slot-indexed), run every
 // launch group of `plans`, copy results back.
 //   in_slots:  slots copied host -> device (coding inputs, plus the checked
@@ -219,7 +293,24 @@ int run_host(const std::vector<DevPlan> &plans, int nslots, const std::vector<in
     // pipeline (or, for plans the direct kernels cannot take, the DMA pipeline).
     const size_t dmin = direct_min_bytes();
     const bool pinned = count >= std::min(dmin, size_t(1) << 20) && all_pinned(host, nslots);
-    if (mode == Mode::Verify) RS_HIP(hipMemsetAsync(ctx->flag, 0, sizeof(int), ctx->stream));
+    // The verify word (ctx->flag): a small call's signal leaves it zero
+    // (kernels.hpp DirectSignal); every other verify may leave it set, so the
+    // next verify zeroes it first (a memset is a dispatch of its own: ~4 us of
+    // a small call).
+    if (!pinned && count < mirror_min_bytes()) {
+        if (mode == Mode::Verify && ctx->flag_dirty) {
+            RS_HIP(hipMemsetAsync(ctx->flag, 0, sizeof(int), ctx->stream));
+            ctx->flag_dirty = false;
+        }
+        bool taken = false;
+        rc = run_small(ctx, plans, nslots, in_slots, out_slots, host, offset, count, mode, result, &taken);
+        if (rc) ctx->flag_dirty = true;
+        if (rc || taken) return rc;
+    }
+    if (mode == Mode::Verify) {
+        if (ctx->flag_dirty) RS_HIP(hipMemsetAsync(ctx->flag, 0, sizeof(int), ctx->stream));
+        ctx->flag_dirty = true;
+    }
     if (pinned || count >= mirror_min_bytes()) {
         bool taken = false;
         rc = pinned ? run_direct(ctx, plans, in_slots, out_slots, host, offset, count, mode, &taken)

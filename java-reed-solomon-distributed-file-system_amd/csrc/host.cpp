@@ -148,6 +148,7 @@ int thread_ctx(ThreadCtx **out) {
             if (e == hipSuccess) e = hipEventCreateWithFlags(&c->loaded[b], hipEventDisableTiming);
         }
         if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&c->flag), 256);
+        if (e == hipSuccess) e = hipMemset(c->flag, 0, 256);  // the verify word and the signal's block counter
         if (e != hipSuccess) {
             delete c;
             return hip_fail(e, "thread context");
@@ -176,6 +177,8 @@ void free_buffers(ThreadCtx *c) {
     if (c->plan) (void)hipFree(c->plan);
     if (c->file) (void)hipFree(c->file);
     if (c->zc) (void)hipHostFree(c->zc);
+    if (c->sig) (void)hipHostFree(c->sig);
+    c->sig = c->sig_dev = nullptr;
     c->mirror = c->stage = c->plan = c->file = c->zc = c->zc_dev = nullptr;
     c->mirror_cap = c->stage_cap = c->plan_cap = c->file_cap = c->zc_cap = 0;
 }
@@ -383,6 +386,14 @@ int run_chunks(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinned, c
     return rc;
 }
 
+size_t zero_copy_limit() {
+    static const size_t v = [] {
+        const char *e = tuning_env("RSAMD_ZC_BYTES");
+        return e ? size_t(std::strtoull(e, nullptr, 10)) : kZeroCopyBytes;
+    }();
+    return v;
+}
+
 int zero_copy_buffer(ThreadCtx *ctx, size_t buf_bytes) {
     if (ctx->zc_cap < buf_bytes) {
         if (ctx->zc) RS_HIP(hipHostFree(ctx->zc));
@@ -401,6 +412,44 @@ int zero_copy_buffer(ThreadCtx *ctx, size_t buf_bytes) {
     return RS_OK;
 }
 
+int next_signal(ThreadCtx *ctx, uint32_t **flag_dev, uint32_t **ctr, uint32_t *seq) {
+    if (!ctx->sig) {
+        RS_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->sig), 256, hipHostMallocMapped | hipHostMallocCoherent));
+        RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->sig_dev), ctx->sig, 0));
+        __atomic_store_n(&ctx->sig[0], 0u, __ATOMIC_RELEASE);
+        __atomic_store_n(&ctx->sig[1], 0u, __ATOMIC_RELEASE);
+    }
+    if (++ctx->sig_seq == 0) ctx->sig_seq = 1;
+    *flag_dev = ctx->sig_dev;
+    *ctr = reinterpret_cast<uint32_t *>(ctx->flag) + kSignalCtr;
+    *seq = ctx->sig_seq;
+    bounds::allow(ctx->sig_dev, 8);
+    return RS_OK;
+}
+
+int wait_signal(ThreadCtx *ctx, uint32_t seq, uint32_t *mismatch) {
+    // Spin: a small call's kernel ends a few microseconds after its launch, and
+    // the stream's own completion costs ~3 us more to observe.
+    // Past 100 us the stream is asked now and then whether it failed or went
+    // idle without the signal.
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spins = 1;; ++spins) {
+        if (__atomic_load_n(&ctx->sig[0], __ATOMIC_ACQUIRE) == seq) break;
+        if (spins % 64 != 0 || std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(100)) continue;
+        const hipError_t e = hipStreamQuery(ctx->stream);
+        if (e == hipErrorNotReady) {
+            (void)hipGetLastError();
+            std::this_thread::yield();
+            continue;
+        }
+        if (__atomic_load_n(&ctx->sig[0], __ATOMIC_ACQUIRE) == seq) break;
+        if (e != hipSuccess) return hip_fail(e, "small call (hipStreamQuery)");
+        return fail(RS_E_HIP, "small call: the stream is idle and the kernel's completion signal is missing");
+    }
+    if (mismatch) *mismatch = __atomic_load_n(&ctx->sig[1], __ATOMIC_ACQUIRE);
+    return RS_OK;
+}
+
 namespace {
 
 // Single-chunk calls (<= 4 MiB per shard) skip the DMA pipeline: the inputs
@@ -411,13 +460,6 @@ namespace {
 // pageable): 1000-B shards 130 -> 36 us, 64 KiB 180 -> 40 us, 1 MiB 390-500
 // -> 280-306 us, 4 MiB 810-1100 -> 660-725 us.  RSAMD_ZC_BYTES sets the size
 // limit of the staging buffer (0 disables).
-size_t zero_copy_limit() {
-    static const size_t v = [] {
-        const char *e = tuning_env("RSAMD_ZC_BYTES");
-        return e ? size_t(std::strtoull(e, nullptr, 10)) : kZeroCopyBytes;
-    }();
-    return v;
-}
 
 int run_zero_copy(ThreadCtx *ctx, size_t buf_bytes, const ChunkIo &io, const ChunkCode &code) {
     int zrc = zero_copy_buffer(ctx, buf_bytes);

@@ -74,6 +74,12 @@ struct ThreadCtx {
     uint8_t *zc = nullptr;      // small calls: coherent, device-mapped host buffer the kernels use directly
     uint8_t *zc_dev = nullptr;  // its device address
     size_t zc_cap = 0;
+    // Small calls' completion signal (kernels.hpp DirectSignal): two coherent,
+    // device-mapped host words the kernel stores into and the thread spins on;
+    // the block counter is a word of `flag` (kSignalCtr).
+    uint32_t *sig = nullptr, *sig_dev = nullptr;
+    uint32_t sig_seq = 0;
+    bool flag_dirty = true;  // the verify word may be nonzero (zeroed by a memset before the next verify)
     // rs_decode_batch_masked_dev: two staging slots used in turn, so a call's
     // host-side preparation overlaps the previous call's kernels.
     MaskedSlot masked[2];
@@ -91,6 +97,18 @@ int grow_pinned(uint8_t **buf, size_t *cap, size_t want);
 // The context's coherent, device-mapped host buffer (zc / zc_dev) with at
 // least buf_bytes.
 int zero_copy_buffer(ThreadCtx *ctx, size_t buf_bytes);
+// Largest staging buffer of a single zero-copy pass.
+size_t zero_copy_limit();
+
+// ---- small calls' completion signal ---------------------------------------
+constexpr size_t kSignalCtr = 16;  // int index into ThreadCtx::flag of the block counter
+// The context's signal words (allocated on first use) and the next call's
+// sequence number (never 0).
+int next_signal(ThreadCtx *ctx, uint32_t **flag_dev, uint32_t **ctr, uint32_t *seq);
+// Spins until the launch signalled `seq`; *mismatch (may be NULL) gets the
+// verify word.  A stream that went idle without the signal, or failed, is an
+// error (nothing then spins forever).
+int wait_signal(ThreadCtx *ctx, uint32_t seq, uint32_t *mismatch);
 
 // ---- the chunked pipeline --------------------------------------------------
 // Bytes per slot per chunk for a call of `total` bytes per slot and `nslots`

@@ -1176,7 +1176,25 @@ struct DirectArgs {
     int nin;
     int *mismatch;
     DirectTee tee;         // TEE kernels only
+    DirectSignal sig;      // sig.flag == nullptr: no completion signal
 };
+
+// The completion signal (kernels.hpp DirectSignal), after a block's last store.
+__device__ __forceinline__ void signal_done(const DirectSignal &sg, int *mismatch) {
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const uint32_t prev = __hip_atomic_fetch_add(RSAMD_G(sg.ctr, 4), 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev + 1 != gridDim.x) return;
+    __hip_atomic_store(RSAMD_G(sg.ctr, 4), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t mm = 0;
+    if (mismatch) {
+        mm = uint32_t(__hip_atomic_load(RSAMD_G(mismatch, 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        __hip_atomic_store(RSAMD_G(mismatch, 4), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __hip_atomic_store(RSAMD_G(sg.flag + 1, 4), mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(RSAMD_G(sg.flag, 4), sg.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // The tee store of one 8-byte unit of data shard d at column c (unit-aligned,
 // so inside one block), clipped to the file (the padding's rows are not file
@@ -1221,35 +1239,60 @@ struct DirectVec<8> {
     static constexpr int kDwords = 2;
 };
 
-template <int W, int M, bool VERIFY, bool TEE>
+// Input i's W bytes at `off` folded into acc.
+template <int W, int M>
+__device__ __forceinline__ void direct_fold(const DirectArgs &a, int i, const typename DirectVec<W>::T &x,
+                                            uint32_t (&acc)[M][DirectVec<W>::kDwords]) {
+    uint32_t T[M][5];
+#pragma unroll
+    for (int p = 0; p < M; ++p)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) T[p][j] = *RSAMD_G(a.tabs + ((i * M + p) * 5 + j), 4);
+#pragma unroll
+    for (int w = 0; w < DirectVec<W>::kDwords; ++w) {
+        const Sel s = selectors(x[w]);
+#pragma unroll
+        for (int p = 0; p < M; ++p) {
+            uint32_t t0, t1, t2;
+            terms(T[p], s, t0, t1, t2);
+            acc[p][w] = xor3(acc[p][w], t0, t1) ^ t2;
+        }
+    }
+}
+
+// PRE (small calls, kernels.hpp DirectSignal): the inputs are loaded eight at
+// a time before any is folded, so a thread waits for one link round trip per
+// eight inputs instead of one per input -- a small call has too few waves to
+// hide them.  The streaming form keeps one input in flight per thread (its
+// many waves hide the latency; its ISA is unchanged).
+template <int W, int M, bool VERIFY, bool TEE, bool PRE>
 __global__ void __launch_bounds__(kThreads) gf_direct_kernel(DirectArgs a) {
     typedef typename DirectVec<W>::T V;
     constexpr int D = DirectVec<W>::kDwords;
     const uint64_t step = uint64_t(gridDim.x) * kThreads;
     for (uint64_t v = uint64_t(blockIdx.x) * kThreads + threadIdx.x; v < a.nvec; v += step) {
-        if (VERIFY && mismatch_seen(a.mismatch)) return;
+        if (VERIFY && mismatch_seen(a.mismatch)) break;  // (the completion signal below still runs)
         const uint64_t off = a.head + v * W;
         uint32_t acc[M][D];
 #pragma unroll
         for (int p = 0; p < M; ++p)
 #pragma unroll
             for (int w = 0; w < D; ++w) acc[p][w] = 0;
-        for (int i = 0; i < a.nin; ++i) {
-            const V x = __builtin_nontemporal_load(reinterpret_cast<const V *>(RSAMD_G(a.in[i] + off, W)));
-            uint32_t T[M][5];
+        if constexpr (PRE) {
+            constexpr int kPre = 8;
+            for (int i0 = 0; i0 < a.nin; i0 += kPre) {
+                V x[kPre];
 #pragma unroll
-            for (int p = 0; p < M; ++p)
+                for (int j = 0; j < kPre; ++j)
+                    if (i0 + j < a.nin) x[j] = __builtin_nontemporal_load(reinterpret_cast<const V *>(RSAMD_G(a.in[i0 + j] + off, W)));
 #pragma unroll
-                for (int j = 0; j < 5; ++j) T[p][j] = *RSAMD_G(a.tabs + ((i * M + p) * 5 + j), 4);
-#pragma unroll
-            for (int w = 0; w < D; ++w) {
-                const Sel s = selectors(x[w]);
-#pragma unroll
-                for (int p = 0; p < M; ++p) {
-                    uint32_t t0, t1, t2;
-                    terms(T[p], s, t0, t1, t2);
-                    acc[p][w] = xor3(acc[p][w], t0, t1) ^ t2;
-                }
+                for (int j = 0; j < kPre; ++j)
+                    if (i0 + j < a.nin) direct_fold<W, M>(a, i0 + j, x[j], acc);
+            }
+        } else {
+            for (int i = 0; i < a.nin; ++i) {
+                const V x = __builtin_nontemporal_load(reinterpret_cast<const V *>(RSAMD_G(a.in[i] + off, W)));
+                direct_fold<W, M>(a, i, x, acc);
             }
         }
 #pragma unroll
@@ -1304,6 +1347,7 @@ __global__ void __launch_bounds__(kThreads) gf_direct_kernel(DirectArgs a) {
             }
         }
     }
+    if (a.sig.flag) signal_done(a.sig, VERIFY ? a.mismatch : nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -1988,12 +2032,17 @@ hipError_t launch_gf(const Geometry &g, const DevPlan &p, Mode mode, int *mismat
 namespace {
 template <int W, int M>
 void launch_direct_t(const DirectArgs &a, unsigned grid, Mode mode, hipStream_t s) {
-    if (mode == Mode::Verify)
-        hipLaunchKernelGGL((gf_direct_kernel<W, M, true, false>), dim3(grid), dim3(kThreads), 0, s, a);
+    const bool pre = a.sig.flag != nullptr;  // small calls (signalled)
+    if (mode == Mode::Verify && pre)
+        hipLaunchKernelGGL((gf_direct_kernel<W, M, true, false, true>), dim3(grid), dim3(kThreads), 0, s, a);
+    else if (mode == Mode::Verify)
+        hipLaunchKernelGGL((gf_direct_kernel<W, M, true, false, false>), dim3(grid), dim3(kThreads), 0, s, a);
     else if (a.tee.file)
-        hipLaunchKernelGGL((gf_direct_kernel<W, M, false, true>), dim3(grid), dim3(kThreads), 0, s, a);
+        hipLaunchKernelGGL((gf_direct_kernel<W, M, false, true, false>), dim3(grid), dim3(kThreads), 0, s, a);
+    else if (pre)
+        hipLaunchKernelGGL((gf_direct_kernel<W, M, false, false, true>), dim3(grid), dim3(kThreads), 0, s, a);
     else
-        hipLaunchKernelGGL((gf_direct_kernel<W, M, false, false>), dim3(grid), dim3(kThreads), 0, s, a);
+        hipLaunchKernelGGL((gf_direct_kernel<W, M, false, false, false>), dim3(grid), dim3(kThreads), 0, s, a);
 }
 template <int W>
 hipError_t dispatch_direct(const DirectArgs &a, int nout, unsigned grid, Mode mode, hipStream_t s) {
@@ -2017,12 +2066,13 @@ hipError_t dispatch_direct(const DirectArgs &a, int nout, unsigned grid, Mode mo
 constexpr unsigned kDirectBlocks = 256;
 
 hipError_t launch_gf_direct(const DirectPlan &p, size_t n, Mode mode, int *mismatch, hipStream_t s,
-                            const DirectTee *tee) {
+                            const DirectTee *tee, const DirectSignal *sig) {
     if (p.nin < 1 || p.nin > kMaxDirectIn || p.nout < 1 || p.nout > kMaxOut) return hipErrorInvalidValue;
     if (tee && (mode != Mode::Code || !tee->file || tee->blk == 0 || tee->blk % 8 || tee->k < 1 ||
                 reinterpret_cast<uintptr_t>(tee->file) % 8 || reinterpret_cast<uintptr_t>(p.in[0]) % 8))
         return hipErrorInvalidValue;  // (the shards share in[0]'s residue: checked below)
-    if (n == 0) return hipSuccess;
+    if (sig && (!sig->flag || !sig->ctr || (mode == Mode::Verify && !mismatch))) return hipErrorInvalidValue;
+    if (n == 0) return hipSuccess;  // (a signalled caller checks for n == 0 first)
     // The widest vector every shard's address agrees on (same residue).
     int W = 16;
     for (int wide : {16, 8}) {
@@ -2062,6 +2112,7 @@ hipError_t launch_gf_direct(const DirectPlan &p, size_t n, Mode mode, int *misma
     a.nin = p.nin;
     a.mismatch = mismatch;
     if (tee) a.tee = *tee;  // (head % 8 == 0: in[0] is 8-byte aligned and align >= 8)
+    if (sig) a.sig = *sig;
     const uint64_t blocks = tuning_size("RSAMD_DIRECT_BLOCKS", kDirectBlocks);  // per call in TUNING builds
     const unsigned grid = unsigned(std::max<uint64_t>(1, std::min<uint64_t>(blocks, (a.nvec + kThreads - 1) / kThreads)));
     return W == 16 ? dispatch_direct<16>(a, p.nout, grid, mode, s) : dispatch_direct<8>(a, p.nout, grid, mode, s);

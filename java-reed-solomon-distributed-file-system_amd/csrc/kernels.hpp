@@ -97,8 +97,19 @@ struct DirectTee {
     int data[kMaxOut] = {-1, -1, -1, -1};  // output q's data shard, or -1 (parity)
 };
 static_assert(kMaxOut == 4, "DirectTee::data initialises kMaxOut entries");
+// Completion signal of a small host call (capi.cpp run_small): every block
+// makes its stores visible system-wide and counts itself done on `ctr` (a
+// device word, zero between calls); the last block resets it, stores the
+// verify result (the device word `mismatch`, then zeroed) into flag[1] and
+// `seq` into flag[0] -- coherent host memory the calling thread spins on
+// instead of waiting for the stream (small calls).
+struct DirectSignal {
+    uint32_t *flag = nullptr;  // device address of the coherent host words
+    uint32_t *ctr = nullptr;
+    uint32_t seq = 0;
+};
 hipError_t launch_gf_direct(const DirectPlan &p, size_t n, Mode mode, int *mismatch, hipStream_t s,
-                            const DirectTee *tee = nullptr);
+                            const DirectTee *tee = nullptr, const DirectSignal *sig = nullptr);
 
 hipError_t launch_fill_synthetic(uint8_t *base, int k, size_t n_stripes, size_t shard_len,
                                  size_t shard_stride, size_t stripe_stride, uint64_t seed,
