@@ -14,7 +14,10 @@
  *    then holds the text the Java code would have put in its
  *    IllegalArgumentException (thread-local), so a JNI shim can ThrowNew.
  *  - Argument checks run in the reference's order
- *    (ReedSolomon.java:277-302) and nothing is written on an error path.
+ *    (ReedSolomon.java:277-302), all before anything is written: nothing is
+ *    written on an argument error.  A call that fails later (RS_E_HIP, or a
+ *    relocator's failed acquire) returns only once nothing of it is still in
+ *    flight, but may have written part of its outputs.
  *  - Host entry points are synchronous and use the calling thread's current
  *    HIP device.  *_dev entry points are asynchronous on `stream` (a
  *    hipStream_t passed as void*, NULL = the null stream).
@@ -65,8 +68,10 @@ typedef struct rs_codec rs_codec;
  *   4: rs_abi_version (this), rs_shard_stride_recommended.
  *   5: rs_set_host_register and rs_host_registry_state removed: the library
  *      no longer page-locks caller memory (round 5).
- *   6: rs_host_alloc / rs_host_free (caller-owned pinned buffers). */
-#define RS_AMD_ABI_VERSION 6
+ *   6: rs_host_alloc / rs_host_free (caller-owned pinned buffers).
+ *   7: rs_decode_groups_shard_major (the master's recovery on host arrays),
+ *      rs_set_relocator (movable caller arrays: one call per JNI call). */
+#define RS_AMD_ABI_VERSION 7
 RS_API int rs_abi_version(void);
 
 /* ---------------------------------------------------------------------------
@@ -89,7 +94,9 @@ RS_API int rs_codec_decode_matrix(const rs_codec *codec, const uint8_t *present,
                            int *survivors, int *missing, int *n_missing, uint8_t *rows);
 
 RS_API const char *rs_last_error_message(void);
-/* Free the calling thread's device contexts (streams, staging buffers). */
+/* Free the calling thread's device contexts (streams, staging buffers) and the
+ * process's idle pooled pinned slots of the pageable-call pipeline (at most
+ * four sets, 384 MiB, per device are kept idle between calls). */
 RS_API void rs_thread_release(void);
 /* Number of visible HIP devices (0 when none). */
 RS_API int rs_device_count(void);
@@ -137,6 +144,59 @@ RS_API int rs_is_parity_correct(const rs_codec *codec, uint8_t *const *shards, i
  * before copying anything. */
 RS_API int rs_check_buffers_and_sizes(const rs_codec *codec, int nshards, const int64_t *shard_lens,
                                       int64_t offset, int64_t byte_count);
+
+/* The master's recovery loop on HOST arrays (MasterImpl.recoverOfflineChunkserver,
+ * MasterImpl.java:733-743, 794-839, with ChunkserverDiskRecoveryMachine.java:
+ * 34-48 per chunk group), in the master's own layout: one array per server,
+ * the groups back to back -- chunk g of server s at servers[s] + g*chunk_len
+ * (server_lens[s] >= n_groups*chunk_len; bytes past that are untouched).
+ * present holds n_groups x (k+m) flags, group after group (nonzero: server s
+ * answered for group g); every absent chunk of every group is rebuilt in
+ * place from the group's first k present chunks (ReedSolomon.java:210-223),
+ * present chunks are not written.  The GPU form of the Java loop that calls
+ * decodeMissing once per 6 x 1000-B group: the offline set is the same for
+ * every group and only grows when a read fails mid-loop, so the groups form a
+ * few runs of one pattern, and a run of n groups is ONE decodeMissing of
+ * n*chunk_len-byte shards (rs_decode_missing's host paths: pageable arrays
+ * through the mirrored pipeline, the library's pinned buffers coded in place).
+ * Flags that form many runs (more than one per 128 MiB, at least 8) are
+ * decoded in chunks of groups by the per-stripe pattern kernels.  Checks, in
+ * this order, before anything is written: nservers != k+m ->
+ * RS_E_WRONG_NSHARDS; NULL arrays -> RS_E_INVALID; a server array shorter than
+ * n_groups*chunk_len -> RS_E_INVALID; a group with fewer than k present ->
+ * RS_E_NOT_ENOUGH ("Not enough shards present"). */
+RS_API int rs_decode_groups_shard_major(const rs_codec *codec, uint8_t *const *servers, int nservers,
+                                        const int64_t *server_lens, size_t chunk_len, size_t n_groups,
+                                        const uint8_t *present);
+
+/* Movable caller arrays (a JVM's heap byte[]s, reached through JNI): the
+ * library reads and writes caller memory only in copy batches -- a chunk's
+ * inputs into its pinned slots, outputs back, a file's rows split or merged --
+ * and never holds a caller address across one.  With a relocator set on the
+ * calling thread, every host entry point it calls brackets each batch with
+ * acquire(user, base) -- pin every array (GetPrimitiveArrayCritical) and store
+ * its current address into base[0..n) -- and release(user, base), and moves
+ * every address inside [keys[i], keys[i] + lens[i]] the call was given to the
+ * same offset from base[i].  Between batches (while the GPU codes) the arrays
+ * are unpinned and may move, so a caller needs no critical region across the
+ * call, and one call codes the whole range with no restart of the pipeline.
+ * The keys are stand-in addresses that are never dereferenced: pass them (or
+ * pointers made from them) as the call's array arguments; they must not
+ * overlap any real memory the call uses (non-canonical addresses do not).
+ * Caller arrays are never treated as pinned while a relocator is set.  An
+ * acquire that returns nonzero skips its batch and the call returns RS_E_INVALID
+ * ("relocator: acquire failed"; outputs may then be partly written).  The
+ * struct is copied; keys and lens must stay valid until the relocator is
+ * cleared with rs_set_relocator(NULL).  RS_E_INVALID for n < 1 or NULL members. */
+typedef struct rs_relocator {
+    void *user;
+    int n;
+    const uint8_t *const *keys;
+    const int64_t *lens;
+    int (*acquire)(void *user, uint8_t **base);
+    void (*release)(void *user, uint8_t **base);
+} rs_relocator;
+RS_API int rs_set_relocator(const rs_relocator *relocator);
 
 /* CodingLoop.codeSomeShards(matrixRows, inputs, inputCount, outputs, outputCount,
  * offset, byteCount) (CodingLoop.java:79-85; default impl
@@ -361,8 +421,10 @@ RS_API int rs_dev_free(void *ptr);
  * pages placed by the calling thread's NUMA policy.  Host calls on arrays in
  * it are coded in place across the link with no host copies (DESIGN.md 5.2:
  * 1.00 of the link bound for 4+2 x 64 MiB encodeParity, against 0.86-0.90
- * for pageable arrays).  Free with rs_host_free.  RS_E_NO_DEVICE without a
- * GPU, RS_E_HIP when the allocation fails.
+ * for pageable arrays).  Free with rs_host_free, which takes only a live
+ * rs_host_alloc pointer (a foreign or interior pointer, or a second free, is
+ * RS_E_INVALID and frees nothing).  RS_E_NO_DEVICE without a GPU, RS_E_HIP
+ * when the allocation fails.
  * ------------------------------------------------------------------------- */
 RS_API int rs_host_alloc(void **out, size_t bytes);
 RS_API int rs_host_free(void *ptr);

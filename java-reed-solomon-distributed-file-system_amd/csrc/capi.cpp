@@ -17,6 +17,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -240,7 +241,7 @@ int run_small(ThreadCtx *ctx, const std::vector<DevPlan> &plans, int nslots, con
         if (use_pool)
             rsamd::CopyPool::get().copy(jobs);
         else
-            for (const rsamd::CopyJob &j : jobs) std::memcpy(j.dst, j.src, j.n);
+            rsamd::CopyPool::copy_here(jobs);
         jobs.clear();
     };
     // The kernel codes whole 16-byte vectors: each slot's bytes past `count`
@@ -719,18 +720,10 @@ int file_encode_zc_split(const Codec &c, const uint8_t *file, size_t file_len, s
     *taken = true;
     const bool pool = need > (size_t(2) << 20);  // (as run_zero_copy: the pool's wake-up costs more below)
     auto copy = [&](const std::vector<rsamd::CopyJob> &jobs) {
-        if (pool) {
+        if (pool)
             rsamd::CopyPool::get().copy(jobs);
-        } else {
-            for (const rsamd::CopyJob &j : jobs)
-                for (size_t r = 0; r < j.rows; ++r) {
-                    uint8_t *dst = static_cast<uint8_t *>(j.dst) + r * j.dst_stride;
-                    if (j.src)
-                        std::memcpy(dst, static_cast<const uint8_t *>(j.src) + r * j.src_stride, j.n);
-                    else
-                        std::memset(dst, 0, j.n);
-                }
-        }
+        else
+            rsamd::CopyPool::copy_here(jobs);
     };
     std::vector<rsamd::CopyJob> jobs;
     if (file_len) jobs.push_back({ctx->zc, file, file_len});
@@ -883,7 +876,11 @@ int file_decode_pinned(const Codec &c, uint8_t *const *shards, const uint8_t *pr
         const rsamd::DirectPlan &d = dp[g];
         for (int i = 0; i < d.nin; ++i) bounds::allow(d.in[i], n);
         for (int q = 0; q < d.nout; ++q) bounds::allow(d.out[q], n);
-        RS_HIP(rsamd::launch_gf_direct(d, n, Mode::Code, nullptr, ctx->stream, tee ? &tees[g] : nullptr));
+        const hipError_t e = rsamd::launch_gf_direct(d, n, Mode::Code, nullptr, ctx->stream, tee ? &tees[g] : nullptr);
+        if (e != hipSuccess) {  // the groups already launched finish before the caller gets control
+            (void)hipStreamSynchronize(ctx->stream);
+            return hip_fail(e, "launch_gf_direct (file decode)");
+        }
     }
     *taken = true;
     std::vector<const uint8_t *> src(shards, shards + k);
@@ -932,14 +929,10 @@ int file_decode_zc_split(const Codec &c, uint8_t *const *shards, const uint8_t *
     std::vector<rsamd::CopyJob> jobs;
     if (missing.empty()) {  // mergeShardsToFile alone
         merge_jobs(k, blk, file_out, file_size, src.data(), now, 0, rows_needed, &jobs);
-        if (file_size > (size_t(2) << 20)) {
+        if (file_size > (size_t(2) << 20))
             rsamd::CopyPool::get().copy(jobs);
-        } else {
-            for (const rsamd::CopyJob &j : jobs)
-                for (size_t r = 0; r < j.rows; ++r)
-                    std::memcpy(static_cast<uint8_t *>(j.dst) + r * j.dst_stride,
-                                static_cast<const uint8_t *>(j.src) + r * j.src_stride, j.n);
-        }
+        else
+            rsamd::CopyPool::copy_here(jobs);
         *taken = true;
         return RS_OK;
     }
@@ -957,17 +950,10 @@ int file_decode_zc_split(const Codec &c, uint8_t *const *shards, const uint8_t *
     *taken = true;
     const bool pool = need > (size_t(2) << 20);  // (as run_zero_copy)
     auto copy = [&](const std::vector<rsamd::CopyJob> &js) {
-        if (pool) {
+        if (pool)
             rsamd::CopyPool::get().copy(js);
-            return;
-        }
-        for (const rsamd::CopyJob &j : js)
-            for (size_t r = 0; r < j.rows; ++r) {
-                uint8_t *dst = static_cast<uint8_t *>(j.dst) + r * j.dst_stride;
-                const uint8_t *sp = static_cast<const uint8_t *>(j.src) + r * j.src_stride;
-                std::memcpy(dst, sp, j.n);
-                if (j.dst2) std::memcpy(static_cast<uint8_t *>(j.dst2) + r * j.dst2_stride, sp, j.n);
-            }
+        else
+            rsamd::CopyPool::copy_here(js);
     };
     for (int sidx : surv) jobs.push_back({ctx->zc + size_t(sidx) * ss, shards[sidx], n});
     copy(jobs);
@@ -1358,7 +1344,140 @@ int granule_view(int total_shards, uint8_t *base, size_t n_stripes, size_t shard
     return RS_OK;
 }
 
+// rs_decode_groups_shard_major's form for flags that change every few groups
+// (not the master's loop): chunks of whole groups staged through the DMA
+// pipeline (host.hpp run_chunks), each chunk's slots laid out as the caller's
+// arrays ([server][groups * chunk_len]) and decoded in HBM by the per-stripe
+// pattern kernels, one launch group per output slot group -- the groups read
+// as stripes of chunk_len-byte shards (stripe stride chunk_len).  Every group
+// is checked (presence_bits) before anything is copied.  The servers with an
+// absent chunk in a chunk's groups are copied back whole over those groups
+// (their present chunks come back unchanged).
+int groups_host_per_group(const Codec &c, const rsamd::PatternTables &pt, uint8_t *const *servers, size_t cl,
+                          size_t n_groups, const uint8_t *present) {
+    const int T = c.total(), k = c.k();
+    MaskedSlot *sl = nullptr;
+    ThreadCtx *ctx = nullptr;
+    int rc = masked_slot(n_groups * sizeof(uint32_t), &sl, &ctx);
+    if (rc) return rc;
+    uint32_t *bits = reinterpret_cast<uint32_t *>(sl->host);
+    rc = presence_bits(present, n_groups, T, k, pt.host_mask_table, bits);
+    if (rc) return fail(rc, rc == RS_E_SINGULAR ? "Matrix is singular" : "Not enough shards present");
+    const bool pinned = all_pinned(servers, T);
+    const size_t G = std::min(n_groups, std::max<size_t>(1, chunk_bytes(n_groups * cl, T, pinned) / cl));
+    const size_t n_chunks = (n_groups + G - 1) / G, ss = round_up(G * cl, 256);
+    const uint32_t full = T >= 32 ? ~0u : (1u << T) - 1;
+    std::vector<uint32_t> absent(n_chunks, 0);  // per chunk: servers with an absent chunk
+    for (size_t g = 0; g < n_groups; ++g) absent[g / G] |= ~bits[g] & full;
+    rc = upload_slot(ctx, sl, n_groups * sizeof(uint32_t), ctx->stream);
+    if (rc) return rc;
+    const int32_t *dbits = reinterpret_cast<const int32_t *>(sl->dev);
+    auto io = [&](size_t j, std::vector<Xfer> *in, std::vector<Xfer> *out) {
+        const size_t g0 = j * G, n = std::min(G, n_groups - g0);
+        for (int s = 0; s < T; ++s) {
+            in->push_back({servers[s] + g0 * cl, size_t(s) * ss, n * cl});
+            if (absent[j] >> s & 1) out->push_back({servers[s] + g0 * cl, size_t(s) * ss, n * cl});
+        }
+    };
+    auto code = [&](size_t j, uint8_t *buf, hipStream_t st) -> int {
+        const size_t g0 = j * G, n = std::min(G, n_groups - g0);
+        const Geometry geo{buf, n, 0, cl, ss, cl, T};
+        return launch_pattern_groups(c, pt, geo, 0, dbits + g0, nullptr, st);
+    };
+    rc = run_chunks(ctx, n_chunks, ss * size_t(T), pinned, io, code);
+    RS_HIP(hipEventRecord(sl->done, ctx->stream));
+    return rc;
+}
+
+// Runs of consecutive chunk groups with one presence pattern (the master's
+// offline set only grows, MasterImpl.java:794-806: one or a few runs), each
+// with its decode plan (null: every shard present).  Every group of the runs
+// found is checked (RS_E_NOT_ENOUGH / RS_E_SINGULAR); past max_runs runs the
+// search stops with *per_group = true and the rest unchecked.
+struct GroupRun {
+    size_t g0, n;
+    std::shared_ptr<const Plan> plan;
+};
+
+size_t max_group_runs(size_t bytes_per_server, int total) {
+    return std::min<size_t>(4096, std::max<size_t>(8, (bytes_per_server >> 27) * size_t(total)));
+}
+
+int group_runs(const Codec &c, const uint8_t *present, size_t n_groups, size_t max_runs, std::vector<GroupRun> *runs,
+               bool *per_group) {
+    const int T = c.total(), k = c.k();
+    const size_t rowb = size_t(T);
+    *per_group = false;
+    runs->clear();
+    auto same_flags = [&](const uint8_t *a, const uint8_t *b) {
+        for (int i = 0; i < T; ++i)
+            if ((a[i] != 0) != (b[i] != 0)) return false;
+        return true;
+    };
+    for (size_t g = 0; g < n_groups;) {
+        if (runs->size() == max_runs) {
+            *per_group = true;
+            break;
+        }
+        const uint8_t *p = present + g * rowb;
+        int np = 0;
+        for (int i = 0; i < T; ++i) np += p[i] ? 1 : 0;
+        if (np < k) return fail(RS_E_NOT_ENOUGH, "Not enough shards present");
+        // Extend the run: byte-identical rows by memcmp blocks that double
+        // while they match and halve when they do not (rows [g, g+n) all equal
+        // row g, so rows [g+n, g+n+a) are compared with rows [g, g+a), a <= n:
+        // 4 M groups cost about one pass over the flags); from the first row
+        // that differs in bytes, row by row on the flags' meaning (nonzero).
+        size_t n = 1, a = 1;
+        bool exact = true;
+        while (g + n < n_groups) {
+            if (exact) {
+                a = std::min(a, n_groups - g - n);
+                if (std::memcmp(present + (g + n) * rowb, p, a * rowb) == 0) {
+                    n += a;
+                    a = n;
+                } else if (a > 1) {
+                    a /= 2;
+                } else {
+                    exact = false;
+                }
+            } else if (same_flags(present + (g + n) * rowb, p)) {
+                ++n;
+            } else {
+                break;
+            }
+        }
+        GroupRun r{g, n, nullptr};
+        if (np < T) {
+            int rc = c.decode_plan(p, &r.plan);
+            if (rc) return fail(rc, rc == RS_E_SINGULAR ? "Matrix is singular" : "Not enough shards present");
+        }
+        runs->push_back(r);
+        g += n;
+    }
+    return RS_OK;
+}
+
+// Live rs_host_alloc buffers: rs_host_free frees only these, so a foreign
+// pointer, a slice of a buffer or a second free is RS_E_INVALID instead of
+// undefined behaviour in the runtime.
+struct HostAllocs {
+    std::mutex mu;
+    std::set<void *> live;
+};
+HostAllocs &host_allocs() {
+    static HostAllocs *h = new HostAllocs;  // never destroyed: no teardown order at exit
+    return *h;
+}
+
 const Codec *impl(const rs_codec *c) { return c ? c->impl : nullptr; }
+
+// A host entry point's result, with a relocator's failed acquire (a batch
+// that was not copied, copy_pool.hpp) reported as RS_E_INVALID.
+int reloc_checked(int rc) {
+    if (rsamd::take_relocation_failure() && rc == RS_OK) return fail(RS_E_INVALID, "relocator: acquire failed");
+    return rc;
+}
 
 }  // namespace
 
@@ -1421,68 +1540,78 @@ int rs_device_count(void) {
 
 int rs_encode_parity(const rs_codec *codec, uint8_t *const *shards, int nshards, const int64_t *shard_lens,
                      int32_t offset, int32_t byte_count) {
-    bounds::Scope bs;
-    const Codec *c = impl(codec);
-    if (!c) return fail(RS_E_INVALID, "codec is NULL");
-    int rc = check_buffers_and_sizes(*c, shards, nshards, shard_lens, offset, byte_count);
-    if (rc) return rc;
-    if (byte_count == 0 || c->m() == 0) return RS_OK;
-    return code_with_plan(c->encode_plan(), c->total(), shards, size_t(offset), size_t(byte_count), Mode::Code,
-                          nullptr);
+    return reloc_checked([&]() -> int {
+        bounds::Scope bs;
+        const Codec *c = impl(codec);
+        if (!c) return fail(RS_E_INVALID, "codec is NULL");
+        int rc = check_buffers_and_sizes(*c, shards, nshards, shard_lens, offset, byte_count);
+        if (rc) return rc;
+        if (byte_count == 0 || c->m() == 0) return RS_OK;
+        return code_with_plan(c->encode_plan(), c->total(), shards, size_t(offset), size_t(byte_count), Mode::Code,
+                              nullptr);
+    }());
 }
 
 int rs_decode_missing(const rs_codec *codec, uint8_t *const *shards, int nshards, const int64_t *shard_lens,
                       const uint8_t *present, int32_t offset, int32_t byte_count) {
-    bounds::Scope bs;
-    const Codec *c = impl(codec);
-    if (!c) return fail(RS_E_INVALID, "codec is NULL");
-    int rc = check_buffers_and_sizes(*c, shards, nshards, shard_lens, offset, byte_count);
-    if (rc) return rc;
-    if (!present) return fail(RS_E_INVALID, "present must not be NULL");
-    int n_present = 0;
-    for (int i = 0; i < c->total(); ++i) n_present += present[i] ? 1 : 0;
-    if (n_present == c->total()) return RS_OK;  // ReedSolomon.java:190-194
-    if (n_present < c->k()) return fail(RS_E_NOT_ENOUGH, "Not enough shards present");
-    std::shared_ptr<const Plan> plan;
-    rc = c->decode_plan(present, &plan);
-    if (rc == RS_E_SINGULAR) return fail(rc, "Matrix is singular");
-    if (rc) return fail(rc, "Not enough shards present");
-    if (byte_count == 0) return RS_OK;
-    return code_with_plan(*plan, c->total(), shards, size_t(offset), size_t(byte_count), Mode::Code, nullptr);
+    return reloc_checked([&]() -> int {
+        bounds::Scope bs;
+        const Codec *c = impl(codec);
+        if (!c) return fail(RS_E_INVALID, "codec is NULL");
+        int rc = check_buffers_and_sizes(*c, shards, nshards, shard_lens, offset, byte_count);
+        if (rc) return rc;
+        if (!present) return fail(RS_E_INVALID, "present must not be NULL");
+        int n_present = 0;
+        for (int i = 0; i < c->total(); ++i) n_present += present[i] ? 1 : 0;
+        if (n_present == c->total()) return RS_OK;  // ReedSolomon.java:190-194
+        if (n_present < c->k()) return fail(RS_E_NOT_ENOUGH, "Not enough shards present");
+        std::shared_ptr<const Plan> plan;
+        rc = c->decode_plan(present, &plan);
+        if (rc == RS_E_SINGULAR) return fail(rc, "Matrix is singular");
+        if (rc) return fail(rc, "Not enough shards present");
+        if (byte_count == 0) return RS_OK;
+        return code_with_plan(*plan, c->total(), shards, size_t(offset), size_t(byte_count), Mode::Code, nullptr);
+    }());
 }
 
 int rs_is_parity_correct(const rs_codec *codec, uint8_t *const *shards, int nshards, const int64_t *shard_lens,
                          int32_t first_byte, int32_t byte_count, const uint8_t *temp, int64_t temp_len,
                          int *result) {
-    bounds::Scope bs;
-    const Codec *c = impl(codec);
-    if (!c || !result) return fail(RS_E_INVALID, "codec and result must not be NULL");
-    int rc = check_buffers_and_sizes(*c, shards, nshards, shard_lens, first_byte, byte_count);
-    if (rc) return rc;
-    if (temp && temp_len < int64_t(first_byte) + byte_count)
-        return fail(RS_E_TEMP_TOO_SMALL, "tempBuffer is not big enough");
-    if (byte_count == 0 || c->m() == 0) {
-        *result = 1;
-        return RS_OK;
-    }
-    return code_with_plan(c->verify_plan(), c->total(), shards, size_t(first_byte), size_t(byte_count),
-                          Mode::Verify, result);
+    return reloc_checked([&]() -> int {
+        bounds::Scope bs;
+        const Codec *c = impl(codec);
+        if (!c || !result) return fail(RS_E_INVALID, "codec and result must not be NULL");
+        int rc = check_buffers_and_sizes(*c, shards, nshards, shard_lens, first_byte, byte_count);
+        if (rc) return rc;
+        if (temp && temp_len < int64_t(first_byte) + byte_count)
+            return fail(RS_E_TEMP_TOO_SMALL, "tempBuffer is not big enough");
+        if (byte_count == 0 || c->m() == 0) {
+            *result = 1;
+            return RS_OK;
+        }
+        return code_with_plan(c->verify_plan(), c->total(), shards, size_t(first_byte), size_t(byte_count),
+                              Mode::Verify, result);
+    }());
 }
 
 int rs_code_some_shards(const uint8_t *const *matrix_rows, const uint8_t *const *inputs, int input_count,
                         uint8_t *const *outputs, int output_count, int32_t offset, int32_t byte_count) {
-    bounds::Scope bs;
-    return code_rows(matrix_rows, inputs, input_count, outputs, output_count, offset, byte_count, Mode::Code,
-                     nullptr);
+    return reloc_checked([&]() -> int {
+        bounds::Scope bs;
+        return code_rows(matrix_rows, inputs, input_count, outputs, output_count, offset, byte_count, Mode::Code,
+                         nullptr);
+    }());
 }
 
 int rs_check_some_shards(const uint8_t *const *matrix_rows, const uint8_t *const *inputs, int input_count,
                          const uint8_t *const *to_check, int check_count, int32_t offset, int32_t byte_count,
                          int *result) {
-    if (!result) return fail(RS_E_INVALID, "result must not be NULL");
-    bounds::Scope bs;
-    return code_rows(matrix_rows, inputs, input_count, const_cast<uint8_t *const *>(to_check), check_count, offset,
-                     byte_count, Mode::Verify, result);
+    return reloc_checked([&]() -> int {
+        if (!result) return fail(RS_E_INVALID, "result must not be NULL");
+        bounds::Scope bs;
+        return code_rows(matrix_rows, inputs, input_count, const_cast<uint8_t *const *>(to_check), check_count, offset,
+                         byte_count, Mode::Verify, result);
+    }());
 }
 
 int rs_encode_batch_dev(const rs_codec *codec, uint8_t *dev_base, size_t n_stripes, size_t shard_len,
@@ -1528,19 +1657,11 @@ int rs_decode_groups_shard_major_dev(const rs_codec *codec, uint8_t *dev_base, s
     if (!present) return fail(RS_E_INVALID, "present must not be NULL");
     if (n_groups == 0 || chunk_len == 0) return RS_OK;
     if (!dev_base) return fail(RS_E_INVALID, "NULL device base");
-    const int T = c->total(), k = c->k();
+    const int T = c->total();
     if (n_groups > SIZE_MAX / chunk_len || server_stride > SIZE_MAX / size_t(T))
         return fail(RS_E_INVALID, "n_groups * chunk_len or server_stride * total overflows");
     if (server_stride < n_groups * chunk_len)
         return fail(RS_E_INVALID, "server_stride " + std::to_string(server_stride) + " is smaller than n_groups * chunk_len");
-    // Runs of consecutive groups with one presence pattern (the master's
-    // offline set only grows, MasterImpl.java:794-806: one or a few runs).
-    // Every group is checked before anything is enqueued.
-    struct Run {
-        size_t g0, n;
-        std::shared_ptr<const Plan> plan;  // null: every shard present
-    };
-    std::vector<Run> runs;
     // Flags that change every few groups (not the master's loop) would make
     // many small launches: past max_runs runs the groups go to the per-stripe
     // pattern kernels instead, the layout read as n_groups stripes of
@@ -1550,55 +1671,10 @@ int rs_decode_groups_shard_major_dev(const rs_codec *codec, uint8_t *dev_base, s
     // pattern each: profiles/r4/shard_major_runs_r4zk.txt), and a run costs
     // about 15 us of launches, so runs pay while they number fewer than one
     // per ~160 MB of the batch: one per 128 MiB, at least 8.
-    const size_t max_runs = std::min<size_t>(4096, std::max<size_t>(8, ((n_groups * chunk_len) >> 27) * size_t(T)));
+    std::vector<GroupRun> runs;
     bool per_group = false;
-    const size_t rowb = size_t(T);
-    auto same_flags = [&](const uint8_t *a, const uint8_t *b) {
-        for (int i = 0; i < T; ++i)
-            if ((a[i] != 0) != (b[i] != 0)) return false;
-        return true;
-    };
-    for (size_t g = 0; g < n_groups;) {
-        if (runs.size() == max_runs) {
-            per_group = true;
-            break;
-        }
-        const uint8_t *p = present + g * rowb;
-        int np = 0;
-        for (int i = 0; i < T; ++i) np += p[i] ? 1 : 0;
-        if (np < k) return fail(RS_E_NOT_ENOUGH, "Not enough shards present");
-        // Extend the run: byte-identical rows by memcmp blocks that double
-        // while they match and halve when they do not (rows [g, g+n) all equal
-        // row g, so rows [g+n, g+n+a) are compared with rows [g, g+a), a <= n:
-        // 4 M groups cost about one pass over the flags); from the first row
-        // that differs in bytes, row by row on the flags' meaning (nonzero).
-        size_t n = 1, a = 1;
-        bool exact = true;
-        while (g + n < n_groups) {
-            if (exact) {
-                a = std::min(a, n_groups - g - n);
-                if (std::memcmp(present + (g + n) * rowb, p, a * rowb) == 0) {
-                    n += a;
-                    a = n;
-                } else if (a > 1) {
-                    a /= 2;
-                } else {
-                    exact = false;
-                }
-            } else if (same_flags(present + (g + n) * rowb, p)) {
-                ++n;
-            } else {
-                break;
-            }
-        }
-        Run r{g, n, nullptr};
-        if (np < T) {
-            int rc = c->decode_plan(p, &r.plan);
-            if (rc) return fail(rc, rc == RS_E_SINGULAR ? "Matrix is singular" : "Not enough shards present");
-        }
-        runs.push_back(r);
-        g += n;
-    }
+    int rc0 = group_runs(*c, present, n_groups, max_group_runs(n_groups * chunk_len, T), &runs, &per_group);
+    if (rc0) return rc0;
     if (per_group && n_groups > size_t(INT32_MAX)) return fail(RS_E_INVALID, "too many groups");
     int rc = need_device();
     if (rc) return rc;
@@ -1608,7 +1684,7 @@ int rs_decode_groups_shard_major_dev(const rs_codec *codec, uint8_t *dev_base, s
         const Geometry geo{dev_base, n_groups, 0, chunk_len, server_stride, chunk_len, T};
         return decode_masked_dev(*c, present, n_groups, geo, 0, static_cast<hipStream_t>(stream));
     }
-    for (const Run &r : runs) {
+    for (const GroupRun &r : runs) {
         if (!r.plan) continue;
         std::vector<DevPlan> plans;
         RS_HIP(r.plan->device_plans(&plans));
@@ -1617,6 +1693,65 @@ int rs_decode_groups_shard_major_dev(const rs_codec *codec, uint8_t *dev_base, s
         for (const DevPlan &p : plans)
             RS_HIP(rsamd::launch_gf(g, p, Mode::Code, nullptr, static_cast<hipStream_t>(stream)));
     }
+    return RS_OK;
+}
+
+int rs_decode_groups_shard_major(const rs_codec *codec, uint8_t *const *servers, int nservers,
+                                 const int64_t *server_lens, size_t chunk_len, size_t n_groups, const uint8_t *present) {
+    return reloc_checked([&]() -> int {
+        bounds::Scope bs;
+        const Codec *c = impl(codec);
+        if (!c) return fail(RS_E_INVALID, "codec is NULL");
+        const int T = c->total();
+        if (nservers != T) return fail(RS_E_WRONG_NSHARDS, "wrong number of shards: " + std::to_string(nservers));
+        if (!servers || !server_lens || !present) return fail(RS_E_INVALID, "servers, server_lens and present must not be NULL");
+        if (n_groups == 0 || chunk_len == 0) return RS_OK;
+        if (n_groups > size_t(INT64_MAX) / chunk_len) return fail(RS_E_INVALID, "n_groups * chunk_len overflows");
+        const size_t span = n_groups * chunk_len;
+        for (int s = 0; s < T; ++s) {
+            if (!servers[s]) return fail(RS_E_INVALID, "server " + std::to_string(s) + " is NULL");
+            if (server_lens[s] < 0 || size_t(server_lens[s]) < span)
+                return fail(RS_E_INVALID, "server " + std::to_string(s) + " holds " + std::to_string(server_lens[s]) +
+                                              " bytes; n_groups * chunk_len is " + std::to_string(span));
+        }
+        std::vector<GroupRun> runs;
+        bool per_group = false;
+        int rc = group_runs(*c, present, n_groups, max_group_runs(span, T), &runs, &per_group);
+        if (rc) return rc;
+        rsamd::PatternTables pt;
+        std::string err;
+        if (per_group && c->pattern_tables(&pt, &err) != RS_OK) {  // wide codes: every run, one by one
+            rc = group_runs(*c, present, n_groups, SIZE_MAX, &runs, &per_group);
+            if (rc) return rc;
+        }
+        rc = need_device();
+        if (rc) return rc;
+        if (per_group) return groups_host_per_group(*c, pt, servers, chunk_len, n_groups, present);
+        // each run: ONE decodeMissing of n * chunk_len-byte shards at offset g0 * chunk_len
+        for (const GroupRun &r : runs) {
+            if (!r.plan) continue;
+            rc = code_with_plan(*r.plan, T, servers, r.g0 * chunk_len, r.n * chunk_len, Mode::Code, nullptr);
+            if (rc) return rc;
+        }
+        return RS_OK;
+    }());
+}
+
+int rs_set_relocator(const rs_relocator *r) {
+    if (!r) {
+        rsamd::set_thread_relocator(nullptr);
+        return RS_OK;
+    }
+    if (r->n < 1 || !r->keys || !r->lens || !r->acquire || !r->release)
+        return fail(RS_E_INVALID, "relocator: n >= 1 and keys, lens, acquire, release are required");
+    rsamd::Relocator rr;
+    rr.user = r->user;
+    rr.n = r->n;
+    rr.keys = r->keys;
+    rr.lens = r->lens;
+    rr.acquire = r->acquire;
+    rr.release = r->release;
+    rsamd::set_thread_relocator(&rr);
     return RS_OK;
 }
 
@@ -1727,75 +1862,71 @@ int rs_file_decode_dev(const rs_codec *codec, uint8_t *dev_shards, size_t shard_
 
 int rs_file_encode(const rs_codec *codec, const uint8_t *file, int64_t file_len, int32_t block,
                    uint8_t *const *shards_out, int nshards, const int64_t *shard_lens) {
-    bounds::Scope bs;
-    const Codec *c = impl(codec);
-    if (!c) return fail(RS_E_INVALID, "codec is NULL");
-    int64_t padded = 0, S = 0;
-    int rc = file_layout(*c, file_len, block, &padded, &S);
-    if (rc) return rc;
-    if (nshards != c->total()) return fail(RS_E_WRONG_NSHARDS, "wrong number of shards: " + std::to_string(nshards));
-    if (!shards_out || !shard_lens || (!file && file_len)) return fail(RS_E_INVALID, "NULL argument");
-    for (int i = 0; i < nshards; ++i)
-        if (shard_lens[i] < S || (!shards_out[i] && S)) return fail(RS_E_INVALID, "shard " + std::to_string(i) + " is shorter than " + std::to_string(S));
-    if (S == 0) return RS_OK;
-    rc = need_device();
-    if (rc) return rc;
-    ThreadCtx *ctx = nullptr;
-    rc = thread_ctx(&ctx);
-    if (rc) return rc;
-    const size_t blk = size_t(block);
-    std::vector<const uint8_t *> bufs(shards_out, shards_out + nshards);
-    bufs.push_back(file);
-    const bool pinned = all_pinned(bufs.data(), int(bufs.size()));
-    const bool big = file_chunks(c->k(), c->total(), size_t(S), blk, false).n > 1 || size_t(S) >= direct_min_bytes();
-    bool taken = false;
-    if (pinned)
-        rc = file_encode_direct(*c, file, size_t(file_len), blk, shards_out, size_t(S), ctx, &taken);
-    else if (big && size_t(S) >= mirror_min_bytes())
-        rc = file_encode_mirrored(*c, file, size_t(file_len), blk, shards_out, size_t(S), ctx, &taken);
-    else
-        rc = file_encode_zc_split(*c, file, size_t(file_len), blk, shards_out, size_t(S), ctx, &taken);
-    if (rc || taken) return rc;
-    return file_encode_staged(*c, file, size_t(file_len), blk, shards_out, size_t(S), ctx, pinned);
+    return reloc_checked([&]() -> int {
+        bounds::Scope bs;
+        const Codec *c = impl(codec);
+        if (!c) return fail(RS_E_INVALID, "codec is NULL");
+        int64_t padded = 0, S = 0;
+        int rc = file_layout(*c, file_len, block, &padded, &S);
+        if (rc) return rc;
+        if (nshards != c->total()) return fail(RS_E_WRONG_NSHARDS, "wrong number of shards: " + std::to_string(nshards));
+        if (!shards_out || !shard_lens || (!file && file_len)) return fail(RS_E_INVALID, "NULL argument");
+        for (int i = 0; i < nshards; ++i)
+            if (shard_lens[i] < S || (!shards_out[i] && S)) return fail(RS_E_INVALID, "shard " + std::to_string(i) + " is shorter than " + std::to_string(S));
+        if (S == 0) return RS_OK;
+        rc = need_device();
+        if (rc) return rc;
+        ThreadCtx *ctx = nullptr;
+        rc = thread_ctx(&ctx);
+        if (rc) return rc;
+        const size_t blk = size_t(block);
+        std::vector<const uint8_t *> bufs(shards_out, shards_out + nshards);
+        bufs.push_back(file);
+        const bool pinned = all_pinned(bufs.data(), int(bufs.size()));
+        const bool big = file_chunks(c->k(), c->total(), size_t(S), blk, false).n > 1 || size_t(S) >= direct_min_bytes();
+        bool taken = false;
+        if (pinned)
+            rc = file_encode_direct(*c, file, size_t(file_len), blk, shards_out, size_t(S), ctx, &taken);
+        else if (big && size_t(S) >= mirror_min_bytes())
+            rc = file_encode_mirrored(*c, file, size_t(file_len), blk, shards_out, size_t(S), ctx, &taken);
+        else
+            rc = file_encode_zc_split(*c, file, size_t(file_len), blk, shards_out, size_t(S), ctx, &taken);
+        if (rc || taken) return rc;
+        return file_encode_staged(*c, file, size_t(file_len), blk, shards_out, size_t(S), ctx, pinned);
+    }());
 }
 
 int rs_file_decode(const rs_codec *codec, uint8_t *const *shards, int nshards, const int64_t *shard_lens,
                    const uint8_t *present, int32_t byte_cnt_in_shard, int32_t block, uint8_t *file_out,
                    int64_t file_size) {
-    bounds::Scope bs;
-    const Codec *c = impl(codec);
-    if (!c) return fail(RS_E_INVALID, "codec is NULL");
-    if (nshards == c->total() && shards && shard_lens && present && byte_cnt_in_shard == shard_lens[0] &&
-        block >= 1 && shard_lens[0] % block == 0)
-        return file_decode_chunked(*c, shards, shard_lens, present, block, file_out, file_size);
-    // decodeMissing(shards, shardPresent, 0, byteCntInShard)  (ReedSolomonDecoder.java:36)
-    int rc = rs_decode_missing(codec, shards, nshards, shard_lens, present, 0, byte_cnt_in_shard);
-    if (rc) return rc;
-    // mergeShardsToFile + trimPadding (ReedSolomonDecoder.java:92-103, 62-66) over shards[0].length
-    const int64_t S = shard_lens[0];
-    if (block < 1 || S % block) return fail(RS_E_INVALID, "shard length " + std::to_string(S) + " is not a multiple of the block size");
-    if (file_size < 0 || file_size > S * c->k()) return fail(RS_E_INVALID, "file size exceeds k * shard length");
-    if (file_size == 0) return RS_OK;
-    if (!file_out) return fail(RS_E_INVALID, "file_out is NULL");
-    rc = need_device();
-    if (rc) return rc;
-    ThreadCtx *ctx = nullptr;
-    rc = thread_ctx(&ctx);
-    if (rc) return rc;
-    const size_t stride = round_up(size_t(S), 256);
-    const size_t file_bytes = round_up(size_t(file_size), 256);
-    rc = grow(&ctx->file, &ctx->file_cap, file_bytes + stride * size_t(c->total()));
-    if (rc) return rc;
-    uint8_t *dfile = ctx->file, *dsh = ctx->file + file_bytes;
-    for (int i = 0; i < c->k(); ++i)
-        RS_HIP(hipMemcpyAsync(dsh + size_t(i) * stride, shards[i], size_t(S), hipMemcpyHostToDevice, ctx->stream));
-    std::vector<uint8_t> all(c->total(), 1);  // shards are complete now: merge only
-    rc = file_decode_dev(*c, dsh, size_t(S), stride, all.data(), size_t(block), dfile, size_t(file_size), false,
-                         ctx->stream);
-    if (rc) return rc;
-    RS_HIP(hipMemcpyAsync(file_out, dfile, size_t(file_size), hipMemcpyDeviceToHost, ctx->stream));
-    RS_HIP(hipStreamSynchronize(ctx->stream));
-    return RS_OK;
+    return reloc_checked([&]() -> int {
+        bounds::Scope bs;
+        const Codec *c = impl(codec);
+        if (!c) return fail(RS_E_INVALID, "codec is NULL");
+        if (nshards == c->total() && shards && shard_lens && present && byte_cnt_in_shard == shard_lens[0] &&
+            block >= 1 && shard_lens[0] % block == 0)
+            return file_decode_chunked(*c, shards, shard_lens, present, block, file_out, file_size);
+        // decodeMissing(shards, shardPresent, 0, byteCntInShard)  (ReedSolomonDecoder.java:36)
+        int rc = rs_decode_missing(codec, shards, nshards, shard_lens, present, 0, byte_cnt_in_shard);
+        if (rc) return rc;
+        // mergeShardsToFile + trimPadding (ReedSolomonDecoder.java:92-103, 62-66) over shards[0].length
+        const int64_t S = shard_lens[0];
+        if (block < 1 || S % block) return fail(RS_E_INVALID, "shard length " + std::to_string(S) + " is not a multiple of the block size");
+        if (file_size < 0 || file_size > S * c->k()) return fail(RS_E_INVALID, "file size exceeds k * shard length");
+        if (file_size == 0) return RS_OK;
+        if (!file_out) return fail(RS_E_INVALID, "file_out is NULL");
+        // The shards are complete now: the merge is a pure byte permutation, done
+        // on the host (copy jobs, as every other host path moves caller bytes).
+        std::vector<const uint8_t *> src(shards, shards + c->k());
+        const std::vector<bool> every(size_t(c->k()), true);
+        std::vector<rsamd::CopyJob> jobs;
+        merge_jobs(c->k(), size_t(block), file_out, size_t(file_size), src.data(), every, 0, size_t(S / block), &jobs);
+        if (file_size > (int64_t(2) << 20))
+            rsamd::CopyPool::get().copy(jobs);
+        else
+            rsamd::CopyPool::copy_here(jobs);
+        return RS_OK;
+    }());
 }
 
 int rs_fill_synthetic_dev(uint8_t *dev_base, int data_shards, size_t n_stripes, size_t shard_len, size_t shard_stride,
@@ -1842,11 +1973,21 @@ int rs_host_alloc(void **out, size_t bytes) {
     int rc = need_device();
     if (rc) return rc;
     RS_HIP(hipHostMalloc(out, std::max<size_t>(bytes, 1), hipHostMallocMapped | hipHostMallocNumaUser));
+    HostAllocs &h = host_allocs();
+    std::lock_guard<std::mutex> lock(h.mu);
+    h.live.insert(*out);
     return RS_OK;
 }
 
 int rs_host_free(void *ptr) {
-    if (ptr) RS_HIP(hipHostFree(ptr));
+    if (!ptr) return RS_OK;
+    {
+        HostAllocs &h = host_allocs();
+        std::lock_guard<std::mutex> lock(h.mu);
+        if (!h.live.erase(ptr))  // a foreign pointer, an interior one (a slice), or freed twice
+            return fail(RS_E_INVALID, "rs_host_free: not a live rs_host_alloc buffer");
+    }
+    RS_HIP(hipHostFree(ptr));
     return RS_OK;
 }
 

@@ -172,6 +172,83 @@ void copy_piece(const CopyJob &j) {
 }
 }  // namespace
 
+// ---- relocation (copy_pool.hpp Relocator) ----------------------------------
+namespace {
+thread_local Relocator t_reloc;
+thread_local bool t_reloc_on = false;
+thread_local bool t_reloc_failed = false;
+
+// The batch's jobs with every address inside a key range moved to its array's
+// current base.
+template <class P>
+P rebase(P p, uint8_t *const *base) {
+    if (!p) return p;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    for (int i = 0; i < t_reloc.n; ++i) {
+        const uintptr_t k = reinterpret_cast<uintptr_t>(t_reloc.keys[i]);
+        if (a >= k && a - k <= uintptr_t(t_reloc.lens[i]))
+            return reinterpret_cast<P>(reinterpret_cast<uintptr_t>(base[i]) + (a - k));
+    }
+    return p;
+}
+
+// Runs `fn` over the jobs, relocated when this thread has a relocator: false
+// (nothing copied, the failure recorded) when its acquire fails.
+template <class Fn>
+void with_relocation(const std::vector<CopyJob> &jobs, Fn fn) {
+    if (!t_reloc_on || jobs.empty()) {
+        fn(jobs);
+        return;
+    }
+    std::vector<uint8_t *> base(size_t(std::max(1, t_reloc.n)), nullptr);
+    if (t_reloc.acquire(t_reloc.user, base.data()) != 0) {
+        t_reloc_failed = true;
+        return;
+    }
+    std::vector<CopyJob> moved(jobs);
+    for (CopyJob &j : moved) {
+        j.dst = rebase(j.dst, base.data());
+        j.src = rebase(j.src, base.data());
+        j.dst2 = rebase(j.dst2, base.data());
+    }
+    fn(moved);
+    t_reloc.release(t_reloc.user, base.data());
+}
+}  // namespace
+
+void set_thread_relocator(const Relocator *r) {
+    t_reloc_on = r != nullptr;
+    t_reloc = r ? *r : Relocator{};
+    t_reloc_failed = false;
+}
+bool thread_relocating() { return t_reloc_on; }
+bool take_relocation_failure() {
+    const bool f = t_reloc_failed;
+    t_reloc_failed = false;
+    return f;
+}
+
+void CopyPool::copy_here(const std::vector<CopyJob> &jobs) {
+    with_relocation(jobs, [](const std::vector<CopyJob> &js) {
+        for (const CopyJob &j : js)
+            for (size_t r = 0; r < j.rows; ++r) {
+                uint8_t *dst = static_cast<uint8_t *>(j.dst) + r * j.dst_stride;
+                const uint8_t *src = j.src ? static_cast<const uint8_t *>(j.src) + r * j.src_stride : nullptr;
+                if (src)
+                    std::memcpy(dst, src, j.n);
+                else
+                    std::memset(dst, 0, j.n);
+                if (j.dst2) {
+                    uint8_t *d2 = static_cast<uint8_t *>(j.dst2) + r * j.dst2_stride;
+                    if (src)
+                        std::memcpy(d2, src, j.n);
+                    else
+                        std::memset(d2, 0, j.n);
+                }
+            }
+    });
+}
+
 CopyPool &CopyPool::get() {
     static CopyPool *pool = [] {
         const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
@@ -222,6 +299,10 @@ void CopyPool::run() {
 }
 
 void CopyPool::copy(const std::vector<CopyJob> &jobs) {
+    with_relocation(jobs, [this](const std::vector<CopyJob> &js) { copy_batch(js); });
+}
+
+void CopyPool::copy_batch(const std::vector<CopyJob> &jobs) {
     std::atomic<size_t> pending{0};
     {
         std::lock_guard<std::mutex> lock(mu_);

@@ -34,6 +34,31 @@ struct CopyJob {
     size_t dst2_stride = 0;
 };
 
+// Caller arrays that may move between copy batches (a JVM's heap arrays;
+// rs_amd.h rs_set_relocator).  The library touches caller memory only by
+// copy jobs -- CopyPool::copy and CopyPool::copy_here -- so the arrays need
+// to stay put only while one batch runs: with a relocator set on the calling
+// thread, each batch first calls acquire (which pins every array and writes
+// its current address into base[i]), rewrites every job address inside
+// [keys[i], keys[i] + lens[i]) to the same offset from base[i], copies, then
+// calls release.  The keys are stand-ins the call's pointers were made from;
+// they are never dereferenced.
+struct Relocator {
+    void *user = nullptr;
+    int n = 0;
+    const uint8_t *const *keys = nullptr;
+    const int64_t *lens = nullptr;
+    int (*acquire)(void *user, uint8_t **base) = nullptr;
+    void (*release)(void *user, uint8_t **base) = nullptr;
+};
+// The calling thread's relocator (nullptr: none; the struct is copied, the
+// key and length arrays it points to must outlive the setting).
+void set_thread_relocator(const Relocator *r);
+bool thread_relocating();
+// True, and cleared, when an acquire failed on this thread since the last
+// call (that batch was not copied).
+bool take_relocation_failure();
+
 class CopyPool {
 public:
     // The process-wide pool (created on first use, never destroyed: its
@@ -44,12 +69,16 @@ public:
     // thread; returns when all bytes are copied.  Safe to call from several
     // threads at once.
     void copy(const std::vector<CopyJob> &jobs);
+    // The same on the calling thread alone with plain memcpy / memset (small
+    // calls: the pool's wake-up costs more than their bytes).
+    static void copy_here(const std::vector<CopyJob> &jobs);
 
     int workers() const { return int(threads_.size()); }
 
 private:
     explicit CopyPool(int n);
     void run();
+    void copy_batch(const std::vector<CopyJob> &jobs);
 
     struct Piece {
         CopyJob job;

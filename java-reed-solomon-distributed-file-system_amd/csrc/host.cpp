@@ -281,7 +281,10 @@ void orphan(std::map<int, ThreadCtx *> &&ctx) {
 }
 }  // namespace
 
-void release_thread_contexts() { release_all(t_ctx.m); }
+void release_thread_contexts() {
+    release_all(t_ctx.m);
+    release_idle_mirror_sets();
+}
 
 int grow(uint8_t **buf, size_t *cap, size_t want) {
     if (*cap >= want) {
@@ -353,6 +356,7 @@ size_t chunk_bytes(size_t total, int nslots, bool pinned) {
 // pinned by the caller (torch pin_memory, hipHostMalloc, a pooled direct
 // buffer).  The library itself never page-locks caller memory.
 bool all_pinned(const uint8_t *const *ptrs, int n) {
+    if (rsamd::thread_relocating()) return false;  // movable arrays (rs_set_relocator): stand-in addresses
     for (int i = 0; i < n; ++i) {
         if (!ptrs[i]) continue;
         hipPointerAttribute_t attr;
@@ -472,11 +476,10 @@ int run_zero_copy(ThreadCtx *ctx, size_t buf_bytes, const ChunkIo &io, const Chu
     // profiles/r5/host_sizes_r5v.txt.)
     const bool use_pool = buf_bytes > tuning_size("RSAMD_ZC_POOL_MIN", size_t(2) << 20);
     auto copy = [&](const std::vector<rsamd::CopyJob> &jobs) {
-        if (use_pool) {
+        if (use_pool)
             rsamd::CopyPool::get().copy(jobs);
-        } else {
-            for (const rsamd::CopyJob &j : jobs) std::memcpy(j.dst, j.src, j.n);
-        }
+        else
+            rsamd::CopyPool::copy_here(jobs);
     };
     std::vector<rsamd::CopyJob> jobs;
     for (const Xfer &x : in) jobs.push_back({ctx->zc + x.off, x.host, x.n});
@@ -622,6 +625,10 @@ struct MirrorSet {
 };
 
 constexpr size_t kIdleSets = 4;
+// Pinned bytes idle sets may hold per device (a set of three 64 MiB slots is
+// 192 MiB): beyond it a returned set is freed.  rs_thread_release frees every
+// idle set (release_idle_mirror_sets).
+constexpr size_t kIdleBytes = size_t(384) << 20;
 
 struct MirrorPool {
     std::mutex mu;
@@ -696,13 +703,38 @@ void release_set(MirrorSet *s) {
         MirrorPool &p = mirror_pool();
         std::lock_guard<std::mutex> lock(p.mu);
         std::vector<MirrorSet *> &v = p.idle[s->dev];
-        if (v.size() < kIdleSets || process_exiting()) {
+        size_t held = s->cap;
+        for (const MirrorSet *x : v) held += x->cap;
+        if ((v.size() < kIdleSets && held <= kIdleBytes) || process_exiting()) {
             v.push_back(s);
             return;
         }
     }
     free_set(s);
 }
+}  // namespace
+
+void release_idle_mirror_sets() {
+    if (process_exiting()) return;
+    std::vector<MirrorSet *> drop;
+    {
+        MirrorPool &p = mirror_pool();
+        std::lock_guard<std::mutex> lock(p.mu);
+        for (auto &kv : p.idle) {
+            drop.insert(drop.end(), kv.second.begin(), kv.second.end());
+            kv.second.clear();
+        }
+    }
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (MirrorSet *s : drop) {
+        (void)hipSetDevice(s->dev);
+        free_set(s);
+    }
+    (void)hipSetDevice(cur);
+}
+
+namespace {
 
 // TUNING builds: RSAMD_TRACE=<file> appends one JSON line per mirrored call
 // with every chunk's copy batch (host ns from the call's start), launch, and

@@ -89,8 +89,11 @@ struct ThreadCtx {
 int need_device();
 // The calling thread's context on its current device (created on first use).
 int thread_ctx(ThreadCtx **out);
-// Frees every context of the calling thread (rs_thread_release).
+// Frees every context of the calling thread and every idle pooled slot set
+// (rs_thread_release).
 void release_thread_contexts();
+// Frees the process's idle mirrored-pipeline slot sets (pinned host memory).
+void release_idle_mirror_sets();
 // Device / pinned-host buffers that only grow.
 int grow(uint8_t **buf, size_t *cap, size_t want);
 int grow_pinned(uint8_t **buf, size_t *cap, size_t want);

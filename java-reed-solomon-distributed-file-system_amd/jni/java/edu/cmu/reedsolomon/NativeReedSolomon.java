@@ -142,7 +142,7 @@ public final class NativeReedSolomon implements AutoCloseable {
      * asynchronous on the HIP stream handle `stream` (0 = default).  Stripes
      * with fewer than k present shards are skipped and counted into the device
      * int at devBad when it is not 0.  For services that keep chunk groups in
-     * GPU memory; the master's host-side loop uses decodeMissing per group.
+     * GPU memory; the master's host-side loop uses recoverGroupsShardMajor.
      */
     public void decodeMaskedBitsDevice(long devBase, long devBits, long nStripes, long shardLen, long shardStride,
                                        long stripeStride, long devBad, long stream) {
@@ -162,6 +162,30 @@ public final class NativeReedSolomon implements AutoCloseable {
     public void recoverGroupsShardMajorDevice(long devBase, long serverStride, int chunkLen, long nGroups,
                                               byte[] present, long stream) {
         nativeRecoverGroupsShardMajorDevice(handle, devBase, serverStride, chunkLen, nGroups, present, stream);
+    }
+
+    /**
+     * MasterImpl.recoverOfflineChunkserver's loop (MasterImpl.java:733-743,
+     * 794-839; ChunkserverDiskRecoveryMachine.java:34-48 per chunk group) on
+     * the master's own host arrays, batched: servers[s] holds server s's chunks
+     * of nGroups groups back to back (chunk g at g * chunkLen; arrays may be
+     * longer), present holds nGroups * getTotalShardCount() flags, group after
+     * group (nonzero: the server answered for that group).  Every absent chunk
+     * of every group is rebuilt in place from the group's first k present
+     * chunks; present chunks are not written.  Instead of one decodeMissing per
+     * 6 x 1000-B group, each run of groups with one offline set is ONE decode of
+     * run-long shards on the GPU, the arrays pinned only around the library's
+     * copy batches.  Throws IllegalArgumentException ("Not enough shards
+     * present") before anything is written when a group has fewer than k
+     * present.
+     */
+    public void recoverGroupsShardMajor(byte[][] servers, int chunkLen, int nGroups, byte[] present) {
+        nativeRecoverGroupsShardMajor(handle, servers, chunkLen, nGroups, present);
+    }
+
+    /** The same over direct buffers (allocatePinned ones are coded in place across the link). */
+    public void recoverGroupsShardMajor(ByteBuffer[] servers, int chunkLen, int nGroups, byte[] present) {
+        nativeRecoverGroupsShardMajorDirect(handle, servers, chunkLen, nGroups, present);
     }
 
     /**
@@ -205,4 +229,8 @@ public final class NativeReedSolomon implements AutoCloseable {
     private static native void nativeRecoverGroupsShardMajorDevice(long h, long devBase, long serverStride,
                                                                    int chunkLen, long nGroups, byte[] present,
                                                                    long stream);
+    private static native void nativeRecoverGroupsShardMajor(long h, byte[][] servers, int chunkLen, int nGroups,
+                                                             byte[] present);
+    private static native void nativeRecoverGroupsShardMajorDirect(long h, ByteBuffer[] servers, int chunkLen,
+                                                                   int nGroups, byte[] present);
 }

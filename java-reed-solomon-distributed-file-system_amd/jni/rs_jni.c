@@ -10,9 +10,12 @@
  *
  * Java side: jni/java/edu/cmu/reedsolomon/{NativeReedSolomon,GpuCodingLoop}.java.
  * This file only adapts JNIEnv to the rsj_env interface of rs_jni_core.h; the
- * marshalling (argument checks, exceptions, local references, slice-by-slice
- * pinning, the copying fallback) lives in rs_jni_core.c, which
- * tests/test_jni_core.py compiles and exercises against mock Java arrays.
+ * marshalling (argument checks, exceptions, local references, movable arrays
+ * pinned around the library's copy batches, the copying fallback) lives in
+ * rs_jni_core.c, which tests/test_jni_core.py compiles and exercises against
+ * mock Java arrays.  tests/test_jni_adapter.py compiles this file against a
+ * declarations-only jni.h written from the JNI specification
+ * (tests/jni_spec/jni.h), so its types and calls are checked without a JDK.
  */
 #include <jni.h>
 #include <stdint.h>
@@ -233,4 +236,21 @@ JNIEXPORT void JNICALL Java_edu_cmu_reedsolomon_NativeReedSolomon_nativeRecoverG
     jenv je;
     rsj_recover_groups_shard_major(wrap(&je, env), rsj_librsamd_backend(), CODEC(h), devBase, serverStride, chunkLen,
                                    nGroups, present, stream);
+}
+
+/* The master's recovery loop on its host arrays (rs_decode_groups_shard_major):
+ * byte[][] (movable, pinned around the library's copy batches) or direct
+ * ByteBuffer[] servers. */
+JNIEXPORT void JNICALL Java_edu_cmu_reedsolomon_NativeReedSolomon_nativeRecoverGroupsShardMajor(
+        JNIEnv *env, jclass cls, jlong h, jobjectArray servers, jint chunkLen, jint nGroups, jbyteArray present) {
+    jenv je;
+    rsj_recover_groups_shard_major_host(wrap(&je, env), rsj_librsamd_backend(), CODEC(h), servers, chunkLen, nGroups,
+                                        present);
+}
+
+JNIEXPORT void JNICALL Java_edu_cmu_reedsolomon_NativeReedSolomon_nativeRecoverGroupsShardMajorDirect(
+        JNIEnv *env, jclass cls, jlong h, jobjectArray servers, jint chunkLen, jint nGroups, jbyteArray present) {
+    jenv je;
+    rsj_recover_groups_shard_major_direct(wrap(&je, env), rsj_librsamd_backend(), CODEC(h), servers, chunkLen,
+                                          nGroups, present);
 }

@@ -1,22 +1,27 @@
 /*
  * rs_jni_core.c -- see rs_jni_core.h.
  *
- * How a call reaches the GPU: the range [offset, offset + count) is coded in
- * slices of RSJ_SLICE_BYTES per shard.  For each slice every Java array is
- * pinned with GetPrimitiveArrayCritical, librsamd codes the slice from and to
- * those arrays (pageable memory: its mirrored pipeline; the
- * library never page-locks them), and the arrays are released -- outputs with
- * mode 0 (commit), inputs with JNI_ABORT -- before the next slice.  So no
- * critical region lasts longer than one slice (a few ms), the garbage
- * collector can run between slices, and the shim itself copies no byte.
- * Calls of more than one slice are validated up front (same checks
- * and order as the reference), so a later slice never fails after an earlier
- * one was written.  If the JVM answers a critical get with a COPY of the array
- * (isCopy), pinning per slice would copy whole arrays each time: the call then
- * copies each slice through C buffers with Get/SetByteArrayRegion instead.
- * No JNI call is made while a critical region is open.  Element references of
- * the byte[][] arrays are local references: capacity is ensured up front and
- * each one is deleted before returning.
+ * How a call reaches the GPU: ONE library call per Java call, with the Java
+ * arrays movable (rs_set_relocator, include/rs_amd.h).  The library touches
+ * caller memory only in copy batches (a chunk's inputs into its pinned slots,
+ * outputs back, a file's rows split or merged), and brackets each batch with
+ * this shim's acquire -- every array pinned with GetPrimitiveArrayCritical,
+ * its current address handed over -- and release (outputs with mode 0, inputs
+ * with JNI_ABORT).  So no critical region lasts longer than one batch's host
+ * copies (about a millisecond; the GPU codes between batches with every array
+ * released, and the GC may move them then), the library's pipeline runs the
+ * whole range without a restart, and the shim itself copies no byte.  The
+ * call's array arguments are stand-in keys (non-canonical addresses the
+ * library never dereferences).
+ *
+ * If the JVM answers a critical get with a COPY (isCopy, seen by one probing
+ * pin before the call), pinning per batch would copy whole arrays each time:
+ * the call then copies slices of RSJ_SLICE_BYTES through C buffers with
+ * Get/SetByteArrayRegion instead, validated up front (same checks and order
+ * as the reference) so a later slice never fails after an earlier one was
+ * written.  No JNI call is made while a critical region is open.  Element
+ * references of the byte[][] arrays are local references: capacity is ensured
+ * up front and each one is deleted before returning.
  */
 #include "rs_jni_core.h"
 
@@ -34,7 +39,8 @@ const rsj_backend *rsj_librsamd_backend(void) {
                                   rs_code_some_shards,        rs_check_some_shards,      rs_check_buffers_and_sizes,
                                   rs_codec_total_shard_count, rs_codec_data_shard_count, rs_last_error_message,
                                   rs_decode_groups_shard_major_dev, rs_file_layout,          rs_file_encode,
-                                  rs_file_decode,             rs_host_alloc,             rs_host_free};
+                                  rs_file_decode,             rs_host_alloc,             rs_host_free,
+                                  rs_decode_groups_shard_major, rs_set_relocator};
     return &b;
 }
 
@@ -55,7 +61,6 @@ typedef struct {
     int n;
     rsj_obj arr[RSJ_MAX_SHARDS];
     int64_t len[RSJ_MAX_SHARDS];
-    uint8_t *ptr[RSJ_MAX_SHARDS];
 } arrays;
 
 static void drop_refs(rsj_env *e, arrays *a) {
@@ -69,7 +74,6 @@ static void drop_refs(rsj_env *e, arrays *a) {
  * dereference it).  Returns 0, or -1 with an exception pending. */
 static int take(rsj_env *e, rsj_obj outer, int n, arrays *a) {
     a->n = 0;
-    memset(a->ptr, 0, sizeof a->ptr);
     if (n > RSJ_MAX_SHARDS) n = RSJ_MAX_SHARDS;
     if (n > 0 && e->ensure_local_capacity(e, n + 4) < 0) return -1;
     for (int i = 0; i < n; i++) {
@@ -90,37 +94,106 @@ static int take(rsj_env *e, rsj_obj outer, int n, arrays *a) {
     return 0;
 }
 
-/* Returns whether any array came back as a copy. */
-static int pin(rsj_env *e, arrays *a) {
-    int any_copy = 0;
-    for (int i = 0; i < a->n; i++) {
-        int is_copy = 0;
-        a->ptr[i] = e->critical_get(e, a->arr[i], &is_copy);
-        any_copy |= is_copy;
-    }
-    return any_copy;
-}
-
-/* mode_of[i] (or `mode` for all when NULL), in reverse order of pinning. */
-static void unpin(rsj_env *e, arrays *a, const int *mode_of, int mode) {
-    for (int i = a->n - 1; i >= 0; i--)
-        if (a->ptr[i]) {
-            e->critical_release(e, a->arr[i], a->ptr[i], mode_of ? mode_of[i] : mode);
-            a->ptr[i] = NULL;
-        }
-}
-
-static int pinned_ok(const arrays *a) {
-    for (int i = 0; i < a->n; i++)
-        if (!a->ptr[i] && a->len[i] > 0) return 0;
-    return 1;
-}
-
 /* Slice buffers for the copying path: one RSJ_SLICE_BYTES buffer per array. */
 static uint8_t *slice_buffers(int n, uint8_t **ptrs) {
     uint8_t *mem = (uint8_t *)malloc((size_t)(n > 0 ? n : 1) * RSJ_SLICE_BYTES);
     for (int i = 0; mem && i < n; i++) ptrs[i] = mem + (size_t)i * RSJ_SLICE_BYTES;
     return mem;
+}
+
+/* ---- movable arrays (rs_set_relocator) ---- */
+
+/* Stand-in address of array i: non-canonical on x86-64 and aarch64, so never
+ * real memory; a Java array holds < 2^31 bytes < 2^36. */
+#define RSJ_KEY(i) ((uint8_t *)(uintptr_t)(0x4000000000000000ull + ((uint64_t)(i) << 36)))
+#define RSJ_MAX_ARRAYS (2 * RSJ_MAX_SHARDS + 1)
+
+typedef struct {
+    rsj_env *e;
+    int n;
+    rsj_obj arr[RSJ_MAX_ARRAYS];
+    int64_t len[RSJ_MAX_ARRAYS];
+    int mode[RSJ_MAX_ARRAYS];  /* release mode after a batch: RSJ_COMMIT for written arrays */
+    const uint8_t *key[RSJ_MAX_ARRAYS];
+    int acquire_failed;
+} movable;
+
+static void mv_init(movable *mv, rsj_env *e) {
+    mv->e = e;
+    mv->n = 0;
+    mv->acquire_failed = 0;
+}
+
+static void mv_add(movable *mv, rsj_obj arr, int64_t len, int mode) {
+    mv->arr[mv->n] = arr;
+    mv->len[mv->n] = len;
+    mv->mode[mv->n] = mode;
+    mv->key[mv->n] = RSJ_KEY(mv->n);
+    mv->n++;
+}
+
+/* Pins every array into base[] (is_copy: whether any came back as a copy).
+ * On a failed get the ones pinned are released and -1 returned. */
+static int mv_pin(movable *mv, uint8_t **base, int *is_copy) {
+    *is_copy = 0;
+    for (int i = 0; i < mv->n; i++) {
+        int c = 0;
+        base[i] = mv->e->critical_get(mv->e, mv->arr[i], &c);
+        *is_copy |= c;
+        if (!base[i] && mv->len[i] > 0) {
+            for (int j = i - 1; j >= 0; j--)
+                if (base[j]) mv->e->critical_release(mv->e, mv->arr[j], base[j], RSJ_ABORT);
+            return -1;
+        }
+    }
+    return 0;
+}
+
+static void mv_unpin(movable *mv, uint8_t **base, const int *mode) {
+    for (int i = mv->n - 1; i >= 0; i--)
+        if (base[i]) mv->e->critical_release(mv->e, mv->arr[i], base[i], mode ? mode[i] : RSJ_ABORT);
+}
+
+static int mv_acquire(void *user, uint8_t **base) {
+    movable *mv = (movable *)user;
+    int c;
+    if (mv_pin(mv, base, &c)) {
+        mv->acquire_failed = 1;
+        return -1;
+    }
+    return 0;
+}
+
+static void mv_release(void *user, uint8_t **base) {
+    movable *mv = (movable *)user;
+    mv_unpin(mv, base, mv->mode);
+}
+
+/* The probe before a call: 0 with *copies set, or -1 with OutOfMemoryError
+ * pending (a critical get failed). */
+static int mv_probe(movable *mv, int *copies) {
+    uint8_t *base[RSJ_MAX_ARRAYS];
+    if (mv_pin(mv, base, copies)) {
+        mv->e->throw_new(mv->e, "java/lang/OutOfMemoryError", "GetPrimitiveArrayCritical failed");
+        return -1;
+    }
+    mv_unpin(mv, base, NULL);
+    return 0;
+}
+
+static rs_relocator mv_relocator(movable *mv) {
+    rs_relocator r = {mv, mv->n, mv->key, mv->len, mv_acquire, mv_release};
+    return r;
+}
+
+/* After a relocated backend call: 0, or -1 with the exception pending. */
+static int mv_result(rsj_env *e, const rsj_backend *b, movable *mv, int rc) {
+    if (!rc) return 0;
+    if (mv->acquire_failed)
+        e->throw_new(e, "java/lang/OutOfMemoryError", "GetPrimitiveArrayCritical failed");
+    else
+        e->throw_new(e, (rc == RS_E_HIP || rc == RS_E_NO_DEVICE) ? ISE : IAE, b->last_error());
+    return -1;
 }
 
 /* ---- ReedSolomon (codec-level) natives ---- */
@@ -139,79 +212,88 @@ static int shard_slice(const rsj_backend *b, const rs_codec *c, int op, uint8_t 
     return b->is_parity_correct(c, ptr, n_arr, len, off, n, temp, temp_len, part);
 }
 
-/* The shard-array call, slice by slice.  role[i] says whether shard i is read
- * and/or written.  Returns 0 (result in *result) or -1 with an exception pending. */
-static int shard_call(rsj_env *e, const rsj_backend *b, const rs_codec *c, arrays *s, const int *role, int op,
-                      const uint8_t *present, int32_t offset, int32_t count, const uint8_t *temp, int64_t temp_len,
-                      int *result) {
-    int rc;
-    *result = 1;
-    const int multi = count > (int32_t)RSJ_SLICE_BYTES;
-    if (multi || (op == OP_VERIFY && temp)) {
-        rc = b->check_buffers_and_sizes(c, s->n, s->len, offset, count);
-        if (rc) {
-            throw_rc(e, b, rc);
-            return -1;
-        }
-        if (op == OP_VERIFY && temp && temp_len < (int64_t)offset + count) {  /* ReedSolomon.java:147-151 */
-            e->throw_new(e, IAE, "tempBuffer is not big enough");
-            return -1;
-        }
+/* The copying fallback (a JVM whose critical gets return copies): validated
+ * up front, then slice by slice through C buffers with Get/SetByteArrayRegion
+ * (only the arrays role[] says are read are copied in, only those written
+ * copied out).  Returns 0 (result in *result) or -1 with an exception pending. */
+static int shard_call_copying(rsj_env *e, const rsj_backend *b, const rs_codec *c, arrays *s, const int *role, int op,
+                              const uint8_t *present, int32_t offset, int32_t count, const uint8_t *temp,
+                              int64_t temp_len, int *result) {
+    int rc = b->check_buffers_and_sizes(c, s->n, s->len, offset, count);
+    if (rc) {
+        throw_rc(e, b, rc);
+        return -1;
     }
-    int mode_of[RSJ_MAX_SHARDS];
-    for (int i = 0; i < s->n; i++) mode_of[i] = (role[i] & ROLE_OUT) ? RSJ_COMMIT : RSJ_ABORT;
-    uint8_t *mem = NULL, *buf[RSJ_MAX_SHARDS];
+    if (op == OP_VERIFY && temp && temp_len < (int64_t)offset + count) {  /* ReedSolomon.java:147-151 */
+        e->throw_new(e, IAE, "tempBuffer is not big enough");
+        return -1;
+    }
+    uint8_t *buf[RSJ_MAX_SHARDS];
+    uint8_t *mem = slice_buffers(s->n, buf);
+    if (!mem) {
+        e->throw_new(e, "java/lang/OutOfMemoryError", "slice buffers");
+        return -1;
+    }
     int64_t lens[RSJ_MAX_SHARDS];
     int32_t done = 0;
     do {  /* at least once: a zero-byte call still gets the backend's checks */
-        /* a one-slice call hands its count to the backend as is (a negative one is its error to report) */
         const int32_t left = count - done;
-        const int32_t n = (!multi || left < (int32_t)RSJ_SLICE_BYTES) ? left : (int32_t)RSJ_SLICE_BYTES;
+        const int32_t n = left < (int32_t)RSJ_SLICE_BYTES ? left : (int32_t)RSJ_SLICE_BYTES;
         int part = 1;
-        if (!mem) {
-            const int copied = pin(e, s);
-            if (!pinned_ok(s)) {
-                unpin(e, s, NULL, RSJ_ABORT);
-                e->throw_new(e, "java/lang/OutOfMemoryError", "GetPrimitiveArrayCritical failed");
-                return -1;
-            }
-            if (copied && multi && done == 0) {  /* the JVM copies: slice through C buffers instead */
-                unpin(e, s, NULL, RSJ_ABORT);
-                mem = slice_buffers(s->n, buf);
-                if (!mem) {
-                    e->throw_new(e, "java/lang/OutOfMemoryError", "slice buffers");
-                    return -1;
-                }
-                continue;
-            }
-            rc = shard_slice(b, c, op, s->ptr, s->n, s->len, present, offset + done, n, temp, temp_len, &part);
-            unpin(e, s, rc ? NULL : mode_of, RSJ_ABORT);  /* on an error nothing was written */
-        } else {
-            for (int i = 0; i < s->n; i++) {
-                lens[i] = n;
-                if (role[i] & ROLE_IN) e->byte_region_get(e, s->arr[i], offset + done, n, buf[i]);
-            }
-            if (e->exception_pending(e)) {
-                free(mem);
-                return -1;
-            }
-            rc = shard_slice(b, c, op, buf, s->n, lens, present, 0, n, temp ? buf[0] : NULL, temp ? n : 0, &part);
-            for (int i = 0; !rc && i < s->n; i++)
-                if (role[i] & ROLE_OUT) e->byte_region_set(e, s->arr[i], offset + done, n, buf[i]);
+        for (int i = 0; i < s->n; i++) {
+            lens[i] = n;
+            if (role[i] & ROLE_IN) e->byte_region_get(e, s->arr[i], offset + done, n, buf[i]);
         }
+        if (e->exception_pending(e)) break;
+        rc = shard_slice(b, c, op, buf, s->n, lens, present, 0, n, temp ? buf[0] : NULL, temp ? n : 0, &part);
         if (rc) {
-            free(mem);
             throw_rc(e, b, rc);
-            return -1;
+            break;
         }
-        if (mem && e->exception_pending(e)) {
-            free(mem);
-            return -1;
-        }
+        for (int i = 0; i < s->n; i++)
+            if (role[i] & ROLE_OUT) e->byte_region_set(e, s->arr[i], offset + done, n, buf[i]);
+        if (e->exception_pending(e)) break;
         if (!part) *result = 0; /* isParityCorrect: false at the first mismatch */
         done += n;
     } while (done < count && *result);
     free(mem);
+    return e->exception_pending(e) ? -1 : 0;
+}
+
+/* The shard-array call: role[i] says whether shard i is read and/or written.
+ * One backend call over the whole range with the arrays movable (the file
+ * header); the copying fallback when the JVM copies.  Returns 0 (result in
+ * *result) or -1 with an exception pending. */
+static int shard_call(rsj_env *e, const rsj_backend *b, const rs_codec *c, arrays *s, const int *role, int op,
+                      const uint8_t *present, int32_t offset, int32_t count, const uint8_t *temp, int64_t temp_len,
+                      int *result) {
+    *result = 1;
+    if (op == OP_VERIFY && temp) {  /* checkBuffersAndSizes, then the tempBuffer (ReedSolomon.java:147-151) */
+        const int rc = b->check_buffers_and_sizes(c, s->n, s->len, offset, count);
+        if (rc) {
+            throw_rc(e, b, rc);
+            return -1;
+        }
+        if (temp_len < (int64_t)offset + count) {
+            e->throw_new(e, IAE, "tempBuffer is not big enough");
+            return -1;
+        }
+    }
+    movable mv;
+    mv_init(&mv, e);
+    for (int i = 0; i < s->n; i++) mv_add(&mv, s->arr[i], s->len[i], (role[i] & ROLE_OUT) ? RSJ_COMMIT : RSJ_ABORT);
+    int copies = 0;
+    if (mv_probe(&mv, &copies)) return -1;
+    if (copies && count > 0)
+        return shard_call_copying(e, b, c, s, role, op, present, offset, count, temp, temp_len, result);
+    const rs_relocator r = mv_relocator(&mv);
+    b->set_relocator(&r);
+    int part = 1;
+    const int rc = shard_slice(b, c, op, (uint8_t *const *)mv.key, s->n, s->len, present, offset, count, temp,
+                               temp_len, &part);
+    b->set_relocator(NULL);
+    if (mv_result(e, b, &mv, rc)) return -1;
+    *result = part;
     return 0;
 }
 
@@ -397,62 +479,61 @@ static int loop_call(rsj_env *e, const rsj_backend *b, rsj_obj rows, rsj_obj ins
     }
     int rc = 0;
     /* nothing is coded when count <= 0 or nin == 0 (the Java loops do no byte iterations) */
-    uint8_t *ib[RSJ_MAX_SHARDS], *ob[RSJ_MAX_SHARDS], *mi = NULL, *mo = NULL;
-    for (int32_t done = 0; !rc && nin > 0 && done < count && result;) {
-        const int32_t n = (count - done) < (int32_t)RSJ_SLICE_BYTES ? (count - done) : (int32_t)RSJ_SLICE_BYTES;
-        int part = 1;
-        if (!mi) {
-            const int copied = pin(e, &in) | pin(e, &out);
-            if (!pinned_ok(&in) || !pinned_ok(&out)) {
-                unpin(e, &out, NULL, RSJ_ABORT);
-                unpin(e, &in, NULL, RSJ_ABORT);
-                e->throw_new(e, "java/lang/OutOfMemoryError", "GetPrimitiveArrayCritical failed");
+    if (nin > 0 && count > 0) {
+        movable mv;
+        mv_init(&mv, e);
+        for (int i = 0; i < nin; i++) mv_add(&mv, in.arr[i], in.len[i], RSJ_ABORT);
+        for (int i = 0; i < nout; i++) mv_add(&mv, out.arr[i], out.len[i], verify ? RSJ_ABORT : RSJ_COMMIT);
+        int copies = 0;
+        rc = mv_probe(&mv, &copies);
+        if (!rc && !copies) {
+            const rs_relocator r = mv_relocator(&mv);
+            b->set_relocator(&r);
+            int part = 1;
+            const uint8_t *const *ik = mv.key, *const *ok = mv.key + nin;
+            const int brc = verify ? b->check_some_shards(rp, ik, nin, ok, nout, offset, count, &part)
+                                   : b->code_some_shards(rp, ik, nin, (uint8_t *const *)ok, nout, offset, count);
+            b->set_relocator(NULL);
+            rc = mv_result(e, b, &mv, brc);
+            if (!rc && !part) result = 0;
+        } else if (!rc) {  /* the JVM copies: slices through C buffers */
+            uint8_t *ib[RSJ_MAX_SHARDS], *ob[RSJ_MAX_SHARDS];
+            uint8_t *mi = slice_buffers(nin, ib), *mo = slice_buffers(nout, ob);
+            if (!mi || !mo) {
+                e->throw_new(e, "java/lang/OutOfMemoryError", "slice buffers");
                 rc = -1;
-                break;
             }
-            if (copied && count > (int32_t)RSJ_SLICE_BYTES && done == 0) {  /* the JVM copies: C buffers */
-                unpin(e, &out, NULL, RSJ_ABORT);
-                unpin(e, &in, NULL, RSJ_ABORT);
-                mi = slice_buffers(nin, ib);
-                mo = slice_buffers(nout, ob);
-                if (!mi || !mo) {
-                    e->throw_new(e, "java/lang/OutOfMemoryError", "slice buffers");
+            for (int32_t done = 0; !rc && done < count && result;) {
+                const int32_t n = (count - done) < (int32_t)RSJ_SLICE_BYTES ? (count - done) : (int32_t)RSJ_SLICE_BYTES;
+                int part = 1;
+                for (int i = 0; i < nin; i++) e->byte_region_get(e, in.arr[i], offset + done, n, ib[i]);
+                if (verify)
+                    for (int i = 0; i < nout; i++) e->byte_region_get(e, out.arr[i], offset + done, n, ob[i]);
+                if (e->exception_pending(e)) {
                     rc = -1;
+                    break;
                 }
-                continue;
+                const int brc = verify ? b->check_some_shards(rp, (const uint8_t *const *)ib, nin,
+                                                              (const uint8_t *const *)ob, nout, 0, n, &part)
+                                       : b->code_some_shards(rp, (const uint8_t *const *)ib, nin, ob, nout, 0, n);
+                if (brc) {
+                    throw_rc(e, b, brc);
+                    rc = -1;
+                    break;
+                }
+                if (!verify)
+                    for (int i = 0; i < nout; i++) e->byte_region_set(e, out.arr[i], offset + done, n, ob[i]);
+                if (e->exception_pending(e)) {
+                    rc = -1;
+                    break;
+                }
+                if (!part) result = 0;
+                done += n;
             }
-            rc = verify ? b->check_some_shards(rp, (const uint8_t *const *)in.ptr, nin, (const uint8_t *const *)out.ptr,
-                                               nout, offset + done, n, &part)
-                        : b->code_some_shards(rp, (const uint8_t *const *)in.ptr, nin, out.ptr, nout, offset + done, n);
-            unpin(e, &out, NULL, (verify || rc) ? RSJ_ABORT : RSJ_COMMIT);
-            unpin(e, &in, NULL, RSJ_ABORT);
-        } else {
-            for (int i = 0; i < nin; i++) e->byte_region_get(e, in.arr[i], offset + done, n, ib[i]);
-            if (verify)
-                for (int i = 0; i < nout; i++) e->byte_region_get(e, out.arr[i], offset + done, n, ob[i]);
-            if (e->exception_pending(e)) {
-                rc = -1;
-                break;
-            }
-            rc = verify ? b->check_some_shards(rp, (const uint8_t *const *)ib, nin, (const uint8_t *const *)ob, nout, 0,
-                                               n, &part)
-                        : b->code_some_shards(rp, (const uint8_t *const *)ib, nin, ob, nout, 0, n);
-            if (!rc && !verify)
-                for (int i = 0; i < nout; i++) e->byte_region_set(e, out.arr[i], offset + done, n, ob[i]);
-            if (!rc && e->exception_pending(e)) {
-                rc = -1;
-                break;
-            }
+            free(mi);
+            free(mo);
         }
-        if (rc) {
-            throw_rc(e, b, rc);
-            break;
-        }
-        if (!part) result = 0;
-        done += n;
     }
-    free(mi);
-    free(mo);
     drop_refs(e, &out);
     drop_refs(e, &in);
     free(flat);
@@ -514,6 +595,98 @@ void rsj_recover_groups_shard_major(rsj_env *e, const rsj_backend *b, const rs_c
     if (rc) throw_rc(e, b, rc);
 }
 
+/* present (byte[] of n_groups * total flags) copied out, validated; NULL
+ * with an exception pending on failure (the caller frees the result). */
+static uint8_t *take_group_flags(rsj_env *e, rsj_obj present, int total, int64_t n_groups, int *nflags) {
+    static uint8_t none;
+    if (!present) {
+        e->throw_new(e, NPE, "present is null");
+        return NULL;
+    }
+    const int n = e->array_length(e, present);
+    if (total <= 0 || n_groups < 0 || n_groups > INT32_MAX / total || (int64_t)n != n_groups * total) {
+        char msg[128];
+        snprintf(msg, sizeof msg, "present has %d flags; nGroups * total shards is %lld", n,
+                 (long long)n_groups * (total > 0 ? total : 0));
+        e->throw_new(e, IAE, msg);
+        return NULL;
+    }
+    *nflags = n;
+    if (!n) return &none;
+    uint8_t *flags = (uint8_t *)malloc((size_t)n);
+    if (!flags) {
+        e->throw_new(e, "java/lang/OutOfMemoryError", "present flags");
+        return NULL;
+    }
+    e->byte_region_get(e, present, 0, n, flags);
+    if (e->exception_pending(e)) {
+        free(flags);
+        return NULL;
+    }
+    return flags;
+}
+
+void rsj_recover_groups_shard_major_host(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj servers,
+                                         int32_t chunk_len, int32_t n_groups, rsj_obj present) {
+    arrays s;
+    if (take_shards(e, b, c, servers, &s)) return;
+    if (chunk_len < 0 || n_groups < 0) {
+        e->throw_new(e, IAE, "negative size");
+        drop_refs(e, &s);
+        return;
+    }
+    int nflags = 0;
+    uint8_t *flags = take_group_flags(e, present, s.n, n_groups, &nflags);
+    if (!flags) {
+        drop_refs(e, &s);
+        return;
+    }
+    /* every server array is read (its present chunks) and written (its absent ones) */
+    movable mv;
+    mv_init(&mv, e);
+    for (int i = 0; i < s.n; i++) mv_add(&mv, s.arr[i], s.len[i], RSJ_COMMIT);
+    int copies = 0;
+    if (!mv_probe(&mv, &copies)) {
+        if (copies) {
+            /* the JVM copies: the whole call through C buffers (the master's
+             * arrays are one chunk per group per server: a few MB at most) */
+            const int64_t span = (int64_t)chunk_len * n_groups;
+            uint8_t *buf[RSJ_MAX_SHARDS];
+            uint8_t *mem = span > 0 ? (uint8_t *)malloc((size_t)(span * s.n)) : NULL;
+            int64_t lens[RSJ_MAX_SHARDS];
+            if (span > 0 && !mem) {
+                e->throw_new(e, "java/lang/OutOfMemoryError", "group buffers");
+            } else {
+                for (int i = 0; i < s.n; i++) {
+                    buf[i] = mem ? mem + (size_t)(span * i) : NULL;
+                    lens[i] = span;
+                    if (span > s.len[i]) {
+                        throw_index(e, s.len[i], s.len[i]);
+                        break;
+                    }
+                    if (span) e->byte_region_get(e, s.arr[i], 0, (int)span, buf[i]);
+                }
+                const int rc = e->exception_pending(e) ? 0
+                               : b->decode_groups_shard_major_host(c, buf, s.n, lens, (size_t)chunk_len,
+                                                                    (size_t)n_groups, flags);
+                if (rc) throw_rc(e, b, rc);
+                for (int i = 0; !e->exception_pending(e) && span && i < s.n; i++)
+                    e->byte_region_set(e, s.arr[i], 0, (int)span, buf[i]);
+            }
+            free(mem);
+        } else {
+            const rs_relocator r = mv_relocator(&mv);
+            b->set_relocator(&r);
+            const int rc = b->decode_groups_shard_major_host(c, (uint8_t *const *)mv.key, s.n, s.len,
+                                                             (size_t)chunk_len, (size_t)n_groups, flags);
+            b->set_relocator(NULL);
+            (void)mv_result(e, b, &mv, rc);
+        }
+    }
+    if (nflags) free(flags);
+    drop_refs(e, &s);
+}
+
 /* ---- client file layout natives (ReedSolomonEncoder / ReedSolomonDecoder) ---- */
 
 typedef struct {
@@ -526,9 +699,10 @@ typedef struct {
 
 /* The whole call: the arrays as Java holds them, every argument passed on, so
  * the library makes every check itself. */
-static int file_whole(const rsj_backend *b, const rs_codec *c, const file_op *op, arrays *s, uint8_t *f) {
-    if (op->op == OP_ENCODE) return b->file_encode(c, f, op->file_len, op->block, s->ptr, s->n, s->len);
-    return b->file_decode(c, s->ptr, s->n, s->len, op->present, op->byte_cnt, op->block, f, op->file_len);
+static int file_whole(const rsj_backend *b, const rs_codec *c, const file_op *op, uint8_t *const *sh, int n,
+                      const int64_t *len, uint8_t *f) {
+    if (op->op == OP_ENCODE) return b->file_encode(c, f, op->file_len, op->block, sh, n, len);
+    return b->file_decode(c, sh, n, len, op->present, op->byte_cnt, op->block, f, op->file_len);
 }
 
 /* Block rows [r0, r1) of a sliced call: row r0 of every shard at sh[i], the
@@ -552,82 +726,57 @@ static int64_t slice_rows(int32_t block) {
 }
 
 /* Runs a file call over the shard arrays s (roles: what each is) and the file
- * array f (f_role: read for encode, written for decode), whole when rows fit
- * one slice, else slice by slice (pinned, or copied through C buffers when
- * the JVM copies).  Leaves an exception pending on failure. */
+ * array f (f_role: read for encode, written for decode): one library call
+ * with every array movable (the file header); when the JVM copies and the
+ * rows exceed one slice, slice by slice through C buffers (validated up
+ * front by the callers).  Leaves an exception pending on failure. */
 static void file_call(rsj_env *e, const rsj_backend *b, const rs_codec *c, const file_op *op, arrays *s,
                       const int *role, rsj_obj f, int f_role, int64_t rows) {
     const int64_t blk = op->block, kb = (int64_t)b->data_shards(c) * blk, per = slice_rows(op->block);
-    const int multi = rows > per;
-    int mode_of[RSJ_MAX_SHARDS];
-    for (int i = 0; i < s->n; i++) mode_of[i] = (role[i] & ROLE_OUT) ? RSJ_COMMIT : RSJ_ABORT;
-    const int f_mode = f_role == ROLE_OUT ? RSJ_COMMIT : RSJ_ABORT;
     const int64_t f_len = e->array_length(e, f);
-    uint8_t *mem = NULL, *fbuf = NULL, *buf[RSJ_MAX_SHARDS], *at[RSJ_MAX_SHARDS];
-    int64_t r0 = 0;
-    do {  /* at least once: a call with no rows still gets the library's checks */
-        const int64_t r1 = !multi ? rows : (r0 + per < rows ? r0 + per : rows);
-        int rc;
-        if (!mem) {
-            int f_copy = 0;
-            const int copied = pin(e, s);
-            uint8_t *fp = e->critical_get(e, f, &f_copy);
-            if (!pinned_ok(s) || (!fp && f_len > 0)) {
-                if (fp) e->critical_release(e, f, fp, RSJ_ABORT);
-                unpin(e, s, NULL, RSJ_ABORT);
-                e->throw_new(e, "java/lang/OutOfMemoryError", "GetPrimitiveArrayCritical failed");
-                return;
-            }
-            if ((copied || f_copy) && multi && r0 == 0) {  /* the JVM copies: slice through C buffers instead */
-                e->critical_release(e, f, fp, RSJ_ABORT);
-                unpin(e, s, NULL, RSJ_ABORT);
-                mem = (uint8_t *)malloc((size_t)(s->n * per * blk + per * kb));
-                if (!mem) {
-                    e->throw_new(e, "java/lang/OutOfMemoryError", "slice buffers");
-                    return;
-                }
-                for (int i = 0; i < s->n; i++) buf[i] = mem + (size_t)(i * per * blk);
-                fbuf = mem + (size_t)(s->n * per * blk);
-                continue;
-            }
-            if (!multi) {
-                rc = file_whole(b, c, op, s, fp);
-            } else {
-                for (int i = 0; i < s->n; i++) at[i] = s->ptr[i] + r0 * blk;
-                rc = file_rows(b, c, op, at, s->n, (fp && r0 * kb < f_len) ? fp + r0 * kb : NULL, r0, r1);
-            }
-            if (fp) e->critical_release(e, f, fp, rc ? RSJ_ABORT : f_mode);
-            unpin(e, s, rc ? NULL : mode_of, RSJ_ABORT);  /* on an error nothing was written */
-        } else {
-            const int32_t len = (int32_t)((r1 - r0) * blk);
-            int64_t fl = op->file_len - r0 * kb;
-            if (fl < 0) fl = 0;
-            if (fl > (r1 - r0) * kb) fl = (r1 - r0) * kb;
-            for (int i = 0; i < s->n; i++)
-                if (role[i] & ROLE_IN) e->byte_region_get(e, s->arr[i], (int)(r0 * blk), len, buf[i]);
-            if (f_role == ROLE_IN && fl) e->byte_region_get(e, f, (int)(r0 * kb), (int)fl, fbuf);
-            if (e->exception_pending(e)) {
-                free(mem);
-                return;
-            }
-            rc = file_rows(b, c, op, buf, s->n, fbuf, r0, r1);
-            if (!rc) {
-                for (int i = 0; i < s->n; i++)
-                    if (role[i] & ROLE_OUT) e->byte_region_set(e, s->arr[i], (int)(r0 * blk), len, buf[i]);
-                if (f_role == ROLE_OUT && fl) e->byte_region_set(e, f, (int)(r0 * kb), (int)fl, fbuf);
-            }
-        }
+    movable mv;
+    mv_init(&mv, e);
+    for (int i = 0; i < s->n; i++) mv_add(&mv, s->arr[i], s->len[i], (role[i] & ROLE_OUT) ? RSJ_COMMIT : RSJ_ABORT);
+    mv_add(&mv, f, f_len, f_role == ROLE_OUT ? RSJ_COMMIT : RSJ_ABORT);
+    int copies = 0;
+    if (mv_probe(&mv, &copies)) return;
+    if (!copies || rows <= per) {
+        const rs_relocator r = mv_relocator(&mv);
+        b->set_relocator(&r);
+        const int rc = file_whole(b, c, op, (uint8_t *const *)mv.key, s->n, s->len, (uint8_t *)mv.key[s->n]);
+        b->set_relocator(NULL);
+        (void)mv_result(e, b, &mv, rc);
+        return;
+    }
+    /* the JVM copies: slices of whole block rows through C buffers */
+    uint8_t *mem = (uint8_t *)malloc((size_t)(s->n * per * blk + per * kb));
+    if (!mem) {
+        e->throw_new(e, "java/lang/OutOfMemoryError", "slice buffers");
+        return;
+    }
+    uint8_t *buf[RSJ_MAX_SHARDS], *fbuf = mem + (size_t)(s->n * per * blk);
+    for (int i = 0; i < s->n; i++) buf[i] = mem + (size_t)(i * per * blk);
+    for (int64_t r0 = 0; r0 < rows;) {
+        const int64_t r1 = r0 + per < rows ? r0 + per : rows;
+        const int32_t len = (int32_t)((r1 - r0) * blk);
+        int64_t fl = op->file_len - r0 * kb;
+        if (fl < 0) fl = 0;
+        if (fl > (r1 - r0) * kb) fl = (r1 - r0) * kb;
+        for (int i = 0; i < s->n; i++)
+            if (role[i] & ROLE_IN) e->byte_region_get(e, s->arr[i], (int)(r0 * blk), len, buf[i]);
+        if (f_role == ROLE_IN && fl) e->byte_region_get(e, f, (int)(r0 * kb), (int)fl, fbuf);
+        if (e->exception_pending(e)) break;
+        const int rc = file_rows(b, c, op, buf, s->n, fbuf, r0, r1);
         if (rc) {
-            free(mem);
             throw_rc(e, b, rc);
-            return;
+            break;
         }
-        if (mem && e->exception_pending(e)) {
-            free(mem);
-            return;
-        }
+        for (int i = 0; i < s->n; i++)
+            if (role[i] & ROLE_OUT) e->byte_region_set(e, s->arr[i], (int)(r0 * blk), len, buf[i]);
+        if (f_role == ROLE_OUT && fl) e->byte_region_set(e, f, (int)(r0 * kb), (int)fl, fbuf);
+        if (e->exception_pending(e)) break;
         r0 = r1;
-    } while (r0 < rows);
+    }
     free(mem);
 }
 
@@ -877,5 +1026,23 @@ void rsj_file_decode_direct(rsj_env *e, const rsj_backend *b, const rs_codec *c,
         return;
     }
     rc = b->file_decode(c, ptr, n, len, pres, byte_cnt, block, f, file_size);
+    if (rc) throw_rc(e, b, rc);
+}
+
+void rsj_recover_groups_shard_major_direct(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj servers,
+                                           int32_t chunk_len, int32_t n_groups, rsj_obj present) {
+    uint8_t *ptr[RSJ_MAX_SHARDS];
+    int64_t len[RSJ_MAX_SHARDS];
+    int n = 0;
+    if (take_direct_shards(e, b, c, servers, ptr, len, &n)) return;
+    if (chunk_len < 0 || n_groups < 0) {
+        e->throw_new(e, IAE, "negative size");
+        return;
+    }
+    int nflags = 0;
+    uint8_t *flags = take_group_flags(e, present, n, n_groups, &nflags);
+    if (!flags) return;
+    const int rc = b->decode_groups_shard_major_host(c, ptr, n, len, (size_t)chunk_len, (size_t)n_groups, flags);
+    if (nflags) free(flags);
     if (rc) throw_rc(e, b, rc);
 }

@@ -5,7 +5,7 @@
  * rs_jni.c implements rsj_env over a JNIEnv and exports the Java natives;
  * tests/jni_mock/ implements it over mock Java arrays, so the marshalling --
  * argument checks and the exceptions they raise, local-reference accounting,
- * slice-by-slice critical-region pinning, the copying fallback -- is compiled
+ * per-batch critical-region pinning of movable arrays, the copying fallback -- is compiled
  * and tested without a JDK.
  *
  * Semantics follow the reference Java code the natives replace:
@@ -34,11 +34,11 @@ extern "C" {
 #define RSJ_COMMIT 0 /* JNI release mode: copy back and free */
 #define RSJ_ABORT 2  /* JNI_ABORT: free without copying back */
 
-/* Calls are coded in slices of this many bytes per shard, each with the Java
- * arrays pinned (GetPrimitiveArrayCritical) only for that slice: a critical
- * region lasts one slice's GPU round trip (4+2: about 3 ms at 32 MiB), and
- * the GC may run between slices.  When the JVM hands out copies instead of
- * pinning, the slices are copied through C buffers (Get/SetByteArrayRegion). */
+/* A call is ONE library call with the Java arrays movable: pinned
+ * (GetPrimitiveArrayCritical) only around each of the library's copy batches
+ * (rs_set_relocator).  When the JVM hands out copies instead of pinning,
+ * calls are copied through C buffers (Get/SetByteArrayRegion) in slices of
+ * this many bytes per shard. */
 #define RSJ_SLICE_BYTES (32u << 20)
 
 typedef void *rsj_obj; /* a jobject (jarray) */
@@ -84,6 +84,9 @@ typedef struct rsj_backend {
                        uint8_t *, int64_t);
     int (*host_alloc)(void **, size_t);
     int (*host_free)(void *);
+    int (*decode_groups_shard_major_host)(const rs_codec *, uint8_t *const *, int, const int64_t *, size_t, size_t,
+                                          const uint8_t *);
+    int (*set_relocator)(const rs_relocator *);
 } rsj_backend;
 
 const rsj_backend *rsj_librsamd_backend(void);
@@ -112,6 +115,19 @@ void rsj_recover_groups_shard_major(rsj_env *e, const rsj_backend *b, const rs_c
                                     int64_t server_stride, int32_t chunk_len, int64_t n_groups, rsj_obj present,
                                     int64_t stream);
 
+/* The same loop on the master's HOST arrays (rs_decode_groups_shard_major):
+ * servers is a byte[][] of k+m arrays, server s's chunks of n_groups groups
+ * back to back (chunk g at g * chunk_len); present as above.  Every absent
+ * chunk is rebuilt in place.  One library call with the arrays movable
+ * (critical regions only around the library's copy batches); argument errors
+ * (short arrays, a group with fewer than k present) are thrown before any
+ * array is written.  The _direct form takes a ByteBuffer[] of direct buffers
+ * (allocatePinned ones are coded in place across the link). */
+void rsj_recover_groups_shard_major_host(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj servers,
+                                         int32_t chunk_len, int32_t n_groups, rsj_obj present);
+void rsj_recover_groups_shard_major_direct(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj servers,
+                                           int32_t chunk_len, int32_t n_groups, rsj_obj present);
+
 /* The client's file layout (ReedSolomonEncoder.java:56-85,
  * ReedSolomonDecoder.java:33-39, 62-66, 92-103) through rs_file_encode /
  * rs_file_decode, so only coded bytes cross the link and the split / merge
@@ -123,10 +139,10 @@ void rsj_recover_groups_shard_major(rsj_env *e, const rsj_backend *b, const rs_c
  *   decode: decodeMissing(shards, present, 0, byte_cnt) in place, then the
  *     data shards merged and trimmed to file_size into file_out (a byte[] of
  *     at least file_size bytes).
- * Large calls are coded in slices of whole block rows (RSJ_SLICE_BYTES of
- * each shard, rounded down to the block), pinned slice by slice like the
- * shard calls and validated up front, so a later slice never fails after an
- * earlier one was written. */
+ * One library call with the file and the shards movable, like the shard
+ * calls; when the JVM copies, slices of whole block rows (RSJ_SLICE_BYTES of
+ * each shard, rounded down to the block) through C buffers, validated up
+ * front, so a later slice never fails after an earlier one was written. */
 void rsj_file_encode(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj file, int32_t block, rsj_obj shards);
 void rsj_file_decode(rsj_env *e, const rsj_backend *b, const rs_codec *c, rsj_obj shards, rsj_obj present,
                      int32_t byte_cnt, int32_t block, rsj_obj file_out, int32_t file_size);

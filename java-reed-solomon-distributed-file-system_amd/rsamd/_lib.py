@@ -13,7 +13,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_ROOT, "lib", "librsamd.so")
 CSRC = os.path.join(PKG_ROOT, "csrc")
 
-ABI_VERSION = 6  # include/rs_amd.h RS_AMD_ABI_VERSION, which SIGNATURES follows
+ABI_VERSION = 7  # include/rs_amd.h RS_AMD_ABI_VERSION, which SIGNATURES follows
 u8p = C.POINTER(C.c_uint8)
 u8pp = C.POINTER(u8p)
 
@@ -54,6 +54,9 @@ SIGNATURES = {
                                                     C.c_size_t, C.c_void_p, C.c_void_p]),
     "rs_decode_groups_shard_major_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t, u8p,
                                                    C.c_void_p]),
+    "rs_decode_groups_shard_major": (C.c_int, [C.c_void_p, u8pp, C.c_int, C.POINTER(C.c_int64), C.c_size_t,
+                                               C.c_size_t, u8p]),
+    "rs_set_relocator": (C.c_int, [C.c_void_p]),
     "rs_shard_stride_recommended": (C.c_size_t, [C.c_int, C.c_size_t]),
     "rs_verify_batch_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t,
                                       C.c_void_p, C.c_void_p]),

@@ -275,15 +275,19 @@ class HostBuffer:
     """Pinned host memory from rs_host_alloc (page-locked, mapped for the
     device, placed by the calling thread's NUMA policy): shards and files kept
     here are coded in place across the link by the host calls, with no host
-    copies.  `.array` is a NumPy uint8 view (valid while the buffer lives);
-    freed by free() or when collected."""
+    copies.  `.array` is a NumPy uint8 view that keeps the buffer alive (its
+    base holds a reference to this object, so `HostBuffer(n).array` and its
+    slices stay valid); freed by free() -- after which every view dangles --
+    or when the buffer and every view are collected."""
 
     def __init__(self, nbytes: int):
         import numpy as np
         p = C.c_void_p()
         check(_lib.load().rs_host_alloc(C.byref(p), nbytes))
         self._ptr, self.nbytes = p.value, nbytes
-        self.array = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(max(nbytes, 1),))[:nbytes]
+        raw = (C.c_uint8 * max(nbytes, 1)).from_address(p.value)
+        raw._owner = self  # the view's base (raw) keeps this buffer from being collected
+        self.array = np.frombuffer(raw, dtype=np.uint8)[:nbytes]
 
     def data_ptr(self) -> int:
         return self._ptr

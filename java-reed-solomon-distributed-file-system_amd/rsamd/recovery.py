@@ -9,7 +9,9 @@ launch, each group with its own presence pattern (rs_decode_batch_masked_dev),
 in the group-major layout [group][server][chunk]; recover_groups_shard_major_dev
 takes the layout the master's loop itself implies -- one array per server,
 groups back to back -- where a run of groups with one pattern is one long
-stripe (rs_decode_groups_shard_major_dev).
+stripe (rs_decode_groups_shard_major_dev), and recover_groups_shard_major is
+the same on host arrays, the form the master holds them in after its reads
+(rs_decode_groups_shard_major; NativeReedSolomon.recoverGroupsShardMajor).
 """
 from __future__ import annotations
 
@@ -18,7 +20,7 @@ import numpy as np
 import ctypes as C
 
 from . import _lib
-from .codec import IllegalArgumentException, RS_E_INVALID, RS_E_NOT_ENOUGH, check
+from .codec import IllegalArgumentException, RS_E_INVALID, RS_E_NOT_ENOUGH, _Buffers, check
 from .device import StripeLayout, _stream_handle, decode_masked
 from .layout import DATA_SHARD_COUNT, PARITY_SHARD_COUNT, TOTAL_SHARD_COUNT, _codec
 
@@ -97,3 +99,21 @@ def recover_groups_shard_major_dev(dev_base: int, server_stride: int, present, c
     check(_lib.load().rs_decode_groups_shard_major_dev(
         _codec(data_shards, parity_shards).handle, C.c_void_p(dev_base), server_stride, chunk_len, p.shape[0],
         p.ctypes.data_as(_lib.u8p), C.c_void_p(_stream_handle(stream))))
+
+
+def recover_groups_shard_major(servers, present, chunk_len: int = 1000, data_shards: int = DATA_SHARD_COUNT,
+                               parity_shards: int = PARITY_SHARD_COUNT) -> None:
+    """MasterImpl.recoverOfflineChunkserver's loop (MasterImpl.java:733-743,
+    794-839) on HOST arrays: servers[s] holds server s's chunks of n_groups
+    groups back to back (chunk g at byte g*chunk_len; a NumPy uint8 array,
+    pageable or from rsamd.device.HostBuffer), present is (n_groups, k+m).
+    Every absent chunk is rebuilt in place (ChunkserverDiskRecoveryMachine.java:
+    34-48 per group); a run of groups with one pattern is one decodeMissing of
+    run-long shards (rs_decode_groups_shard_major)."""
+    p = np.ascontiguousarray(np.asarray(present, dtype=bool)).view(np.uint8)
+    T = data_shards + parity_shards
+    if p.ndim != 2 or p.shape[1] != T:
+        raise ValueError(f"present must be (n_groups, {T}), got {p.shape}")
+    b = _Buffers(servers)
+    check(_lib.load().rs_decode_groups_shard_major(_codec(data_shards, parity_shards).handle, b.ptrs, len(servers),
+                                                   b.lens, chunk_len, p.shape[0], p.ctypes.data_as(_lib.u8p)))

@@ -10,13 +10,20 @@
  *   - a pending exception: class and message; JNI calls other than
  *     ExceptionCheck / DeleteLocalRef / releases with one pending are counted
  *     as violations too;
- *   - region copies in and out (bytes), to tell the pinned and staged paths apart.
+ *   - region copies in and out (bytes), to tell the pinned and staged paths apart;
+ *   - with mock_moving(1), a compacting GC: every critical get of an array
+ *     no region holds moves it to a fresh mapping and unmaps the old one, so
+ *     an access through an address from an earlier region faults.
  * It also provides a fake coding backend (codes out[p][b] = XOR_i in[i][b] ^
- * (p + 1), checks nothing but pointers) so the CPU tests see data movement.
+ * (p + 1), checks nothing but pointers) so the CPU tests see data movement;
+ * it honours a relocator (rs_set_relocator) as librsamd does, pinning the
+ * arrays once around each fake call.
  */
+#define _DEFAULT_SOURCE /* MAP_ANONYMOUS under -std=c11 */
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 
 #include "rs_jni_core.h"
 
@@ -24,8 +31,9 @@ enum { K_BYTES = 1, K_BOOLS = 2, K_OBJECTS = 3, K_DIRECT = 4 };
 
 typedef struct mobj {
     int kind, len;
-    uint8_t *data;        /* bytes / booleans */
+    uint8_t *data;        /* bytes / booleans (mapped: alloc_data) */
     struct mobj **elems;  /* objects */
+    int pins;             /* open critical regions on it */
 } mobj;
 
 typedef struct {
@@ -37,17 +45,25 @@ typedef struct {
     long long bytes_in, bytes_out, critical_gets, commits, aborts;
     int fail_critical;     /* critical_get returns NULL when set */
     int force_copy;        /* critical_get reports isCopy (the data is still the array's) */
+    int moving;            /* critical_get moves an unpinned array first */
+    long long moves;
 } mstate;
 
 static mstate S;
 
 /* ---- objects (exported to the Python test) ---- */
 
+static size_t map_bytes(int len) { return ((size_t)(len > 0 ? len : 1) + 4095) & ~(size_t)4095; }
+static uint8_t *alloc_data(int len) {  /* zeroed */
+    void *p = mmap(NULL, map_bytes(len), PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    return p == MAP_FAILED ? NULL : (uint8_t *)p;
+}
+
 mobj *mock_new_bytes(int len) {
     mobj *o = (mobj *)calloc(1, sizeof *o);
     o->kind = K_BYTES;
     o->len = len;
-    o->data = (uint8_t *)calloc((size_t)(len > 0 ? len : 1), 1);
+    o->data = alloc_data(len);
     return o;
 }
 mobj *mock_new_bools(int len) {
@@ -72,9 +88,16 @@ mobj *mock_new_direct(uint8_t *p, int cap) {
 }
 void mock_set(mobj *outer, int i, mobj *inner) { outer->elems[i] = inner; }
 uint8_t *mock_data(mobj *o) { return o->data; }
-void mock_reset(void) { memset(&S, 0, sizeof S); S.capacity = 16; }
+void mock_reset(void) {
+    const int moving = S.moving;
+    memset(&S, 0, sizeof S);
+    S.capacity = 16;
+    S.moving = moving;
+}
 void mock_fail_critical(int on) { S.fail_critical = on; }
 void mock_force_copy(int on) { S.force_copy = on; }
+void mock_moving(int on) { S.moving = on; }
+long long mock_moves(void) { return S.moves; }
 const char *mock_exc_class(void) { return S.exc ? S.exc_cls : ""; }
 const char *mock_exc_message(void) { return S.exc ? S.exc_msg : ""; }
 void mock_stats(long long *out) {
@@ -130,12 +153,25 @@ static uint8_t *m_critical_get(rsj_env *e, rsj_obj a, int *is_copy) {
     if (S.exc) S.violations++;
     *is_copy = S.force_copy;
     if (S.fail_critical) return NULL;
+    mobj *o = (mobj *)a;
+    if (S.moving && o->kind != K_DIRECT && o->pins == 0) {  /* the GC moved it since the last region */
+        uint8_t *to = alloc_data(o->len);
+        if (!to) return NULL;
+        memcpy(to, o->data, (size_t)(o->len > 0 ? o->len : 0));
+        munmap(o->data, map_bytes(o->len));
+        o->data = to;
+        S.moves++;
+    }
+    o->pins++;
     S.critical_open++;
     S.critical_gets++;
     if (S.critical_open > S.max_critical_open) S.max_critical_open = S.critical_open;
-    return ((mobj *)a)->data;
+    return o->data;
 }
 static void m_critical_release(rsj_env *e, rsj_obj a, uint8_t *p, int mode) {
+    mobj *o = (mobj *)a;
+    if (p != o->data) S.violations++;  /* released with an address it no longer has */
+    o->pins--;
     S.critical_open--;
     if (mode == RSJ_COMMIT) S.commits++;
     else S.aborts++;
@@ -201,23 +237,52 @@ static rsj_env ENV = {NULL,           m_array_length,    m_object_element,   m_d
 
 static int fake_data_shards(const rs_codec *c) { return rs_codec_data_shard_count(c); }
 
-static int fake_encode(const rs_codec *c, uint8_t *const *sh, int n, const int64_t *lens, int32_t off, int32_t cnt) {
-    int rc = rs_check_buffers_and_sizes(c, n, lens, off, cnt);
-    if (rc) return rc;
-    const int k = rs_codec_data_shard_count(c);
+/* A relocator set on the fake backend (as librsamd keeps one per thread): the
+ * fake calls pin the arrays once around their work and use the addresses the
+ * acquire gave, moving every argument that lies in a key range. */
+static struct {
+    int on;
+    rs_relocator r;
+    uint8_t *base[2 * RSJ_MAX_SHARDS + 1];
+    int failed;
+} REL;
+static int fake_set_relocator(const rs_relocator *r) {
+    REL.on = r != NULL;
+    if (r) REL.r = *r;
+    return 0;
+}
+static int rel_begin(void) {
+    if (!REL.on) return 0;
+    if (REL.r.acquire(REL.r.user, REL.base)) return RS_E_INVALID;
+    return 0;
+}
+static void rel_end(void) {
+    if (REL.on) REL.r.release(REL.r.user, REL.base);
+}
+static uint8_t *rel(const uint8_t *p) {
+    if (!REL.on || !p) return (uint8_t *)p;
+    for (int i = 0; i < REL.r.n; i++) {
+        const uintptr_t k = (uintptr_t)REL.r.keys[i], a = (uintptr_t)p;
+        if (a >= k && a - k <= (uintptr_t)REL.r.lens[i]) return REL.base[i] + (a - k);
+    }
+    return (uint8_t *)p;
+}
+/* sh[0..n) moved into out[] */
+static uint8_t **rel_all(const uint8_t *const *sh, int n, uint8_t **out) {
+    for (int i = 0; i < n; i++) out[i] = rel(sh[i]);
+    return out;
+}
+
+static void enc_raw(int k, uint8_t *const *sh, int n, int32_t off, int32_t cnt) {
     for (int p = k; p < n; p++)
         for (int32_t b = off; b < off + cnt; b++) {
             uint8_t x = (uint8_t)(p - k + 1);
             for (int i = 0; i < k; i++) x ^= sh[i][b];
             sh[p][b] = x;
         }
-    return 0;
 }
-static int fake_decode(const rs_codec *c, uint8_t *const *sh, int n, const int64_t *lens, const uint8_t *pres,
-                       int32_t off, int32_t cnt) {
-    int rc = rs_check_buffers_and_sizes(c, n, lens, off, cnt);
-    if (rc) return rc;
-    /* missing shard j := XOR of the present shards ^ 0x80 ^ j (data movement only) */
+/* missing shard j := XOR of the present shards ^ 0x80 ^ j (data movement only) */
+static void dec_raw(uint8_t *const *sh, int n, const uint8_t *pres, int32_t off, int32_t cnt) {
     for (int j = 0; j < n; j++) {
         if (pres[j]) continue;
         for (int32_t b = off; b < off + cnt; b++) {
@@ -227,44 +292,81 @@ static int fake_decode(const rs_codec *c, uint8_t *const *sh, int n, const int64
             sh[j][b] = x;
         }
     }
+}
+
+static int fake_encode(const rs_codec *c, uint8_t *const *sh, int n, const int64_t *lens, int32_t off, int32_t cnt) {
+    int rc = rs_check_buffers_and_sizes(c, n, lens, off, cnt);
+    if (rc || cnt <= 0) return rc;
+    if ((rc = rel_begin())) return rc;
+    uint8_t *p[RSJ_MAX_SHARDS];
+    enc_raw(rs_codec_data_shard_count(c), rel_all((const uint8_t *const *)sh, n, p), n, off, cnt);
+    rel_end();
+    return 0;
+}
+static int fake_decode(const rs_codec *c, uint8_t *const *sh, int n, const int64_t *lens, const uint8_t *pres,
+                       int32_t off, int32_t cnt) {
+    int rc = rs_check_buffers_and_sizes(c, n, lens, off, cnt);
+    if (rc || cnt <= 0) return rc;
+    if ((rc = rel_begin())) return rc;
+    uint8_t *p[RSJ_MAX_SHARDS];
+    dec_raw(rel_all((const uint8_t *const *)sh, n, p), n, pres, off, cnt);
+    rel_end();
     return 0;
 }
 static int fake_verify(const rs_codec *c, uint8_t *const *sh, int n, const int64_t *lens, int32_t off, int32_t cnt,
                        const uint8_t *temp, int64_t temp_len, int *result) {
     int rc = rs_check_buffers_and_sizes(c, n, lens, off, cnt);
     if (rc) return rc;
-    const int k = rs_codec_data_shard_count(c);
+    if (temp && temp_len < (int64_t)off + cnt) return RS_E_TEMP_TOO_SMALL;
     *result = 1;
+    if (cnt <= 0) return 0;
+    if ((rc = rel_begin())) return rc;
+    uint8_t *q[RSJ_MAX_SHARDS];
+    uint8_t *const *v = rel_all((const uint8_t *const *)sh, n, q);
+    const int k = rs_codec_data_shard_count(c);
     for (int p = k; p < n && *result; p++)
         for (int32_t b = off; b < off + cnt; b++) {
             uint8_t x = (uint8_t)(p - k + 1);
-            for (int i = 0; i < k; i++) x ^= sh[i][b];
-            if (sh[p][b] != x) {
+            for (int i = 0; i < k; i++) x ^= v[i][b];
+            if (v[p][b] != x) {
                 *result = 0;
                 break;
             }
         }
+    rel_end();
     return 0;
 }
 static int fake_code(const uint8_t *const *rows, const uint8_t *const *in, int nin, uint8_t *const *out, int nout,
                      int32_t off, int32_t cnt) {
+    int rc = rel_begin();
+    if (rc) return rc;
+    uint8_t *ip[RSJ_MAX_SHARDS], *op[RSJ_MAX_SHARDS];
+    rel_all(in, nin, ip);
+    rel_all((const uint8_t *const *)out, nout, op);
     for (int p = 0; p < nout; p++)
         for (int32_t b = off; b < off + cnt; b++) {
             uint8_t x = 0;
-            for (int i = 0; i < nin; i++) x ^= (uint8_t)(in[i][b] + rows[p][i]);
-            out[p][b] = x;
+            for (int i = 0; i < nin; i++) x ^= (uint8_t)(ip[i][b] + rows[p][i]);
+            op[p][b] = x;
         }
+    rel_end();
     return 0;
 }
 static int fake_check(const uint8_t *const *rows, const uint8_t *const *in, int nin, const uint8_t *const *chk,
                       int nchk, int32_t off, int32_t cnt, int *result) {
+    int rc = rel_begin();
+    if (rc) return rc;
+    uint8_t *ip[RSJ_MAX_SHARDS], *cp[RSJ_MAX_SHARDS];
+    rel_all(in, nin, ip);
+    rel_all(chk, nchk, cp);
     *result = 1;
     for (int p = 0; p < nchk; p++)
         for (int32_t b = off; b < off + cnt; b++) {
             uint8_t x = 0;
-            for (int i = 0; i < nin; i++) x ^= (uint8_t)(in[i][b] + rows[p][i]);
-            if (chk[p][b] != x) *result = 0;
+            for (int i = 0; i < nin; i++) x ^= (uint8_t)(ip[i][b] + rows[p][i]);
+            if (cp[p][b] != x) *result = 0;
         }
+    rel_end();
     return 0;
 }
 
@@ -309,13 +411,21 @@ static int fake_file_encode(const rs_codec *c, const uint8_t *file, int64_t flen
     int rc = rs_file_layout(c, flen, block, &padded, &S);
     if (rc) return rc;
     file_record(flen, n ? lens[0] : -1);
+    rc = rs_check_buffers_and_sizes(c, n, lens, 0, S);
+    if (rc) return rc;
+    if ((rc = rel_begin())) return rc;
+    uint8_t *p[RSJ_MAX_SHARDS];
+    uint8_t *const *v = rel_all((const uint8_t *const *)sh, n, p);
+    const uint8_t *f = rel(file);
     const int k = rs_codec_data_shard_count(c);
     for (int64_t blk = 0; blk < padded / block; blk++)
         for (int32_t i = 0; i < block; i++) {
             const int64_t at = blk * block + i;
-            sh[blk % k][(blk / k) * block + i] = at < flen ? file[at] : 0;
+            v[blk % k][(blk / k) * block + i] = at < flen ? f[at] : 0;
         }
-    return fake_encode(c, sh, n, lens, 0, (int32_t)S);
+    enc_raw(k, v, n, 0, (int32_t)S);
+    rel_end();
+    return 0;
 }
 static int fake_file_decode(const rs_codec *c, uint8_t *const *sh, int n, const int64_t *lens, const uint8_t *pres,
                             int32_t cnt, int32_t block, uint8_t *out, int64_t fsize) {
@@ -327,11 +437,41 @@ static int fake_file_decode(const rs_codec *c, uint8_t *const *sh, int n, const 
     if (np < k) return RS_E_NOT_ENOUGH;
     if (block < 1 || lens[0] % block || fsize < 0 || fsize > k * lens[0]) return RS_E_INVALID;
     file_record(fsize, lens[0]);
-    if (np < n) fake_decode(c, sh, n, lens, pres, 0, cnt);
+    if ((rc = rel_begin())) return rc;
+    uint8_t *p[RSJ_MAX_SHARDS];
+    uint8_t *const *v = rel_all((const uint8_t *const *)sh, n, p);
+    uint8_t *o = rel(out);
+    if (np < n && cnt > 0) dec_raw(v, n, pres, 0, cnt);
     for (int64_t at = 0; at < fsize; at++) {
         const int64_t blk = at / block;
-        out[at] = sh[blk % k][(blk / k) * block + at % block];
+        o[at] = v[blk % k][(blk / k) * block + at % block];
     }
+    rel_end();
+    return 0;
+}
+/* the master's host arrays: every absent chunk of group g := the fake decode
+ * of that group's chunks (checks as librsamd: count, lengths, >= k present) */
+static int fake_shard_major_host(const rs_codec *c, uint8_t *const *sv, int n, const int64_t *lens, size_t chunk,
+                                 size_t groups, const uint8_t *pres) {
+    const int T = rs_codec_total_shard_count(c), k = rs_codec_data_shard_count(c);
+    if (n != T) return RS_E_WRONG_NSHARDS;
+    for (int s = 0; s < n; s++)
+        if (lens[s] < (int64_t)(chunk * groups)) return RS_E_INVALID;
+    for (size_t g = 0; g < groups; g++) {
+        int np = 0;
+        for (int s = 0; s < n; s++) np += pres[g * n + s] ? 1 : 0;
+        if (np < k) return RS_E_NOT_ENOUGH;
+    }
+    int rc = rel_begin();
+    if (rc) return rc;
+    uint8_t *p[RSJ_MAX_SHARDS];
+    uint8_t *const *v = rel_all((const uint8_t *const *)sv, n, p);
+    for (size_t g = 0; g < groups; g++) {
+        uint8_t *at[RSJ_MAX_SHARDS];
+        for (int s = 0; s < n; s++) at[s] = v[s] + g * chunk;
+        dec_raw(at, n, pres + g * n, 0, (int32_t)chunk);
+    }
+    rel_end();
     return 0;
 }
 /* pinned host memory: plain malloc, counted */
@@ -361,7 +501,8 @@ static const rsj_backend FAKE = {fake_encode,       fake_decode,         fake_ve
                                  fake_code,         fake_check,          rs_check_buffers_and_sizes,
                                  rs_codec_total_shard_count, fake_data_shards, rs_last_error_message,
                                  fake_shard_major,  rs_file_layout,      fake_file_encode,
-                                 fake_file_decode,  fake_host_alloc,     fake_host_free};
+                                 fake_file_decode,  fake_host_alloc,     fake_host_free,
+                                 fake_shard_major_host, fake_set_relocator};
 
 static const rsj_backend *backend(int real) { return real ? rsj_librsamd_backend() : &FAKE; }
 
@@ -421,4 +562,12 @@ void mock_file_encode_direct(int real, const rs_codec *c, mobj *file, int32_t fl
 void mock_file_decode_direct(int real, const rs_codec *c, mobj *shards, mobj *present, int32_t cnt, int32_t block,
                              mobj *out, int32_t fsize) {
     rsj_file_decode_direct(&ENV, backend(real), c, shards, present, cnt, block, out, fsize);
+}
+void mock_recover_groups_shard_major_host(int real, const rs_codec *c, mobj *servers, int32_t chunk, int32_t n,
+                                          mobj *present) {
+    rsj_recover_groups_shard_major_host(&ENV, backend(real), c, servers, chunk, n, present);
+}
+void mock_recover_groups_shard_major_direct(int real, const rs_codec *c, mobj *servers, int32_t chunk, int32_t n,
+                                            mobj *present) {
+    rsj_recover_groups_shard_major_direct(&ENV, backend(real), c, servers, chunk, n, present);
 }

@@ -1,9 +1,11 @@
 """The JNI shim's marshalling (jni/rs_jni_core.c) over the real librsamd
 backend on the GPU, through the mock JNI environment of test_jni_core.py:
 Java-array in, Java-array out, compared with the oracle byte for byte, for
-single-slice calls and for calls pinned slice by slice (more than SLICE bytes
-per shard), with the reference's offsets and erasure patterns
-(ReedSolomon.java:90-104, 175-272; ReedSolomonTest.java:77-93's {0, 5}).
+small calls and calls of more than SLICE bytes per shard (one library call
+either way, the arrays pinned only around the library's copy batches), with
+the reference's offsets and erasure patterns (ReedSolomon.java:90-104,
+175-272; ReedSolomonTest.java:77-93's {0, 5}); and with the mock as a
+compacting GC that moves every array between batches.
 """
 import ctypes as C
 
@@ -240,6 +242,161 @@ def test_pageable_direct_buffers_through_shim(gpu, oracle_lib, native, jvm):
                                         jvm.bools([j != 2 for j in range(6)]), S, 1000, jvm.direct(out), flen)
         assert jvm.exception() == ("", "")
         assert np.array_equal(out, f[:flen])
+        jvm.assert_clean()
+    finally:
+        native.rs_codec_destroy(h)
+
+
+@pytest.fixture
+def moving(jvm):
+    """The mock as a compacting GC: every critical get of an unpinned array
+    moves it and unmaps the old mapping (an address kept past a region faults)."""
+    jvm.lib.mock_moving(1)
+    yield jvm
+    jvm.lib.mock_moving(0)
+
+
+@pytest.mark.parametrize("S", [100_000, (3 << 20) + 4099, (70 << 20) + 8])
+def test_moving_arrays_shard_calls(gpu, oracle_lib, native, moving, S):
+    """One library call per Java call with the arrays moving between the
+    library's copy batches (the small-call pass; the mirrored pipeline's many
+    batches): encode, verify, decode {0,5} against the oracle."""
+    jvm = moving
+    k, m = 4, 2
+    h = C.c_void_p()
+    assert native.rs_codec_create(k, m, C.byref(h)) == 0
+    try:
+        rng = np.random.default_rng(S)
+        data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
+        ref = [d.copy() for d in data]
+        oracle_lib.Codec(k, m).encode_parity(ref, 0, S)
+        arrs = [jvm.bytes(d) for d in data]
+        jvm.lib.mock_encode_parity(1, h, jvm.objects(arrs), 0, S)
+        assert jvm.exception() == ("", "")
+        assert all(np.array_equal(jvm.read(a, S), r) for a, r in zip(arrs, ref))
+        moves = jvm.lib.mock_moves()
+        assert moves >= 2 * (k + m)  # the probe and at least one batch each moved every array
+        assert jvm.lib.mock_is_parity_correct(1, h, jvm.objects(arrs), 0, S, None) == 1
+        for j in (0, 5):
+            arrs[j] = jvm.bytes(np.full(S, 0x5A, np.uint8))
+        jvm.lib.mock_decode_missing(1, h, jvm.objects(arrs), jvm.bools([i not in (0, 5) for i in range(6)]), 0, S)
+        assert jvm.exception() == ("", "")
+        assert all(np.array_equal(jvm.read(a, S), r) for a, r in zip(arrs, ref))
+        jvm.assert_clean()
+    finally:
+        native.rs_codec_destroy(h)
+
+
+@pytest.mark.parametrize("flen", [90_999, 9 << 20])
+def test_moving_arrays_file_calls(gpu, oracle_lib, native, moving, flen):
+    jvm = moving
+    k, m = 4, 2
+    h = C.c_void_p()
+    assert native.rs_codec_create(k, m, C.byref(h)) == 0
+    try:
+        data = np.random.default_rng(flen).integers(0, 256, flen, dtype=np.uint8)
+        ref = oracle_lib.Codec(k, m).file_encode(data.tobytes(), 1000)
+        S = ref.shape[1]
+        arrs = [jvm.bytes(np.full(S, 0xA5, np.uint8)) for _ in range(k + m)]
+        jvm.lib.mock_file_encode(1, h, jvm.bytes(data), 1000, jvm.objects(arrs))
+        assert jvm.exception() == ("", "")
+        assert all(np.array_equal(jvm.read(a, S), r) for a, r in zip(arrs, ref))
+        for i in (0, 5):
+            arrs[i] = jvm.bytes(np.zeros(S, np.uint8))
+        out = jvm.bytes(np.full(flen, 0x11, np.uint8))
+        jvm.lib.mock_file_decode(1, h, jvm.objects(arrs), jvm.bools([i not in (0, 5) for i in range(6)]), S, 1000,
+                                 out, flen)
+        assert jvm.exception() == ("", "")
+        assert np.array_equal(jvm.read(out, flen), data)
+        assert all(np.array_equal(jvm.read(a, S), r) for a, r in zip(arrs, ref))
+        jvm.assert_clean()
+    finally:
+        native.rs_codec_destroy(h)
+
+
+def test_moving_arrays_code_some_shards(gpu, oracle_lib, moving):
+    jvm = moving
+    rng = np.random.default_rng(12)
+    nin, nout, off, cnt = 6, 2, 3, (2 << 20) + 5
+    S = off + cnt + 1
+    rows = rng.integers(0, 256, (nout, nin), dtype=np.uint8)
+    ins = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(nin)]
+    want = [np.zeros(S, np.uint8) for _ in range(nout)]
+    oracle_lib.code_some_shards(0, rows, ins, want, off, cnt)
+    outs = [jvm.bytes(np.zeros(S, np.uint8)) for _ in range(nout)]
+    R = jvm.objects([jvm.bytes(r) for r in rows])
+    I = jvm.objects([jvm.bytes(a) for a in ins])
+    jvm.lib.mock_code_some_shards(1, R, I, nin, jvm.objects(outs), nout, off, cnt)
+    assert jvm.exception() == ("", "")
+    assert all(np.array_equal(jvm.read(o, S), w) for o, w in zip(outs, want))
+    jvm.assert_clean()
+
+
+@pytest.mark.parametrize("move,N,grow", [(0, 2049, 1001), (1, 2049, 1001), (1, 600, None), (0, 3001, "many")])
+def test_recover_groups_shard_major_host_through_shim(gpu, oracle_lib, native, jvm, move, N, grow):
+    """NativeReedSolomon.recoverGroupsShardMajor(byte[][] ...) over the real
+    entry point: the master's host arrays (one per server, padded past the
+    groups), the offline set growing mid-loop (or changing every other group),
+    the arrays moving between batches; every byte as the oracle encoded it."""
+    k, m, chunk = 4, 2, 1000
+    T, L = k + m, N * chunk
+    h = C.c_void_p()
+    assert native.rs_codec_create(k, m, C.byref(h)) == 0
+    try:
+        rng = np.random.default_rng(N + move)
+        rows = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(T)]
+        oracle_lib.Codec(k, m).encode_parity(rows, 0, L)
+        want = [np.concatenate([r, np.full(77, 0xD7, np.uint8)]) for r in rows]
+        flags = np.ones((N, T), np.uint8)
+        if grow == "many":
+            for g in range(0, N, 2):
+                flags[g, int(rng.integers(0, T))] = 0
+        elif grow is None:
+            flags[:, 2] = 0
+        else:
+            flags[:grow, 1] = 0
+            flags[grow:, [1, 4]] = 0
+        arrs = [jvm.bytes(np.concatenate([np.where(np.repeat(flags[:, s], chunk).astype(bool), rows[s], 0x3C)
+                                          .astype(np.uint8), np.full(77, 0xD7, np.uint8)])) for s in range(T)]
+        jvm.lib.mock_moving(move)
+        jvm.lib.mock_recover_groups_shard_major_host(1, h, jvm.objects(arrs), chunk, N, jvm.bytes(flags.ravel()))
+        jvm.lib.mock_moving(0)
+        assert jvm.exception() == ("", "")
+        for s in range(T):
+            assert np.array_equal(jvm.read(arrs[s], L + 77), want[s]), s
+        jvm.assert_clean()
+    finally:
+        native.rs_codec_destroy(h)
+
+
+def test_recover_groups_shard_major_direct_through_shim(gpu, oracle_lib, native, jvm):
+    """The ByteBuffer[] overload: the master's arrays in the shim's pinned
+    buffers (allocatePinned), coded in place across the link."""
+    k, m, chunk, N = 4, 2, 1000, 2049
+    T, L = k + m, N * chunk
+    h = C.c_void_p()
+    assert native.rs_codec_create(k, m, C.byref(h)) == 0
+
+    def view(buf, size):
+        return np.ctypeslib.as_array(C.cast(jvm.lib.mock_data(buf), C.POINTER(C.c_uint8)), shape=(size,))
+
+    try:
+        rng = np.random.default_rng(77)
+        rows = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(T)]
+        oracle_lib.Codec(k, m).encode_parity(rows, 0, L)
+        bufs = [jvm.lib.mock_alloc_pinned(1, L) for _ in range(T)]
+        for b, r in zip(bufs, rows):
+            view(b, L)[:] = r
+        flags = np.ones((N, T), np.uint8)
+        flags[:, [0, 5]] = 0
+        for s in (0, 5):
+            view(bufs[s], L)[:] = 0
+        jvm.lib.mock_recover_groups_shard_major_direct(1, h, jvm.objects(bufs), chunk, N, jvm.bytes(flags.ravel()))
+        assert jvm.exception() == ("", "")
+        assert all(np.array_equal(view(b, L), r) for b, r in zip(bufs, rows))
+        for b in bufs:
+            jvm.lib.mock_drop_local()
+            jvm.lib.mock_free_pinned(1, b)
         jvm.assert_clean()
     finally:
         native.rs_codec_destroy(h)

@@ -8,6 +8,13 @@ text (ReedSolomon.java:277-302 and :175-272, InputOutputByteTableCodingLoop
 regions vs copying large ones slice by slice, which arrays are committed --
 is checked here.  A fake coding backend (data movement only) stands in for the
 GPU; test_gpu_jni_core.py runs the same marshalling over librsamd on a GPU.
+
+A call is one backend call with the Java arrays movable (rs_set_relocator):
+one probing pin of every array (released without copy-back), then the
+backend's own pins around its copy batches (the fake pins once per call).
+With mock_moving(1) the mock is a compacting GC -- every critical get of an
+unpinned array moves it and unmaps the old copy -- so an address kept past a
+critical region faults.
 """
 import ctypes as C
 import os
@@ -44,6 +51,9 @@ def build_mock():
         ("mock_new_bytes", P, [C.c_int]), ("mock_new_bools", P, [C.c_int]), ("mock_new_objects", P, [C.c_int]),
         ("mock_set", None, [P, C.c_int, P]), ("mock_data", P, [P]), ("mock_reset", None, []),
         ("mock_fail_critical", None, [C.c_int]), ("mock_force_copy", None, [C.c_int]),
+        ("mock_moving", None, [C.c_int]), ("mock_moves", C.c_longlong, []),
+        ("mock_recover_groups_shard_major_host", None, [C.c_int, P, P, C.c_int32, C.c_int32, P]),
+        ("mock_recover_groups_shard_major_direct", None, [C.c_int, P, P, C.c_int32, C.c_int32, P]),
         ("mock_exc_class", C.c_char_p, []), ("mock_exc_message", C.c_char_p, []),
         ("mock_stats", None, [C.POINTER(C.c_longlong)]),
         ("mock_encode_parity", None, [C.c_int, P, P, C.c_int32, C.c_int32]),
@@ -161,10 +171,11 @@ def slices(cnt):
 
 @pytest.mark.parametrize("off,cnt,copy", [(100, 500, 0), (0, SLICE, 0), (7, SLICE + 1, 0), (3, 2 * SLICE + 12345, 0),
                                           (7, SLICE + 1, 1), (100, 500, 1)])
-def test_encode_slices(jvm, codec42, off, cnt, copy):
-    """Per-slice pinning: each slice pins all 6 arrays, commits the 2 parity
+def test_encode_one_call(jvm, codec42, off, cnt, copy):
+    """One backend call whatever the size: the probe pins all 6 arrays and
+    releases them without copy-back, the backend's pin commits the 2 parity
     arrays and aborts the 4 data arrays, no byte copied on the host; when the
-    JVM reports copies, a multi-slice call copies slices through C buffers."""
+    JVM reports copies, the call copies slices through C buffers."""
     S = off + cnt + 50
     data, arrs = shard_set(jvm, 4, 2, S, seed=cnt)
     jvm.lib.mock_force_copy(copy)
@@ -175,12 +186,11 @@ def test_encode_slices(jvm, codec42, off, cnt, copy):
     for i in range(6):
         assert np.array_equal(jvm.read(arrs[i], S), want[i]), i
     st = jvm.assert_clean()
-    n = slices(cnt)
-    if copy and n > 1:  # one probing pin, then slices copied in and out
+    if copy:  # one probing pin, then slices copied in and out
         assert st["critical_gets"] == 6 and st["aborts"] == 6 and st["commits"] == 0
         assert st["bytes_in"] == 4 * cnt and st["bytes_out"] == 2 * cnt
     else:
-        assert st["critical_gets"] == 6 * n and st["commits"] == 2 * n and st["aborts"] == 4 * n
+        assert st["critical_gets"] == 12 and st["commits"] == 2 and st["aborts"] == 10
         assert st["bytes_in"] == 0 and st["bytes_out"] == 0 and st["max_critical_open"] == 6
 
 
@@ -248,11 +258,10 @@ def test_decode_roles_and_commit(jvm, codec42, cnt, copy):
     for i in range(6):
         assert np.array_equal(jvm.read(arrs[i], S), want[i]), i
     st = jvm.assert_clean()
-    n = slices(cnt)
     if copy:  # (+6: the shardPresent booleans)
         assert st["bytes_in"] == 4 * cnt + 6 and st["bytes_out"] == 2 * cnt
-    else:  # the missing shards are committed, the survivors released without copy-back
-        assert st["commits"] == 2 * n and st["aborts"] == 4 * n and st["bytes_out"] == 0
+    else:  # the missing shards are committed, the survivors released without copy-back (+6: the probe)
+        assert st["commits"] == 2 and st["aborts"] == 4 + 6 and st["bytes_out"] == 0
 
 
 def test_decode_present_array_checks(jvm, codec42):
@@ -325,11 +334,10 @@ def test_code_some_shards_extra_entries_ignored(jvm, cnt, copy):
         assert (got[:off] == 0xEE).all() and (got[off + cnt:] == 0xEE).all()
     assert (jvm.read(oa[nout], S) == 0xEE).all()
     st = jvm.assert_clean()
-    n = slices(cnt)
-    if copy and n > 1:  # (+ nout * nin: the matrix rows)
+    if copy:  # (+ nout * nin: the matrix rows)
         assert st["bytes_in"] == nin * cnt + nout * nin and st["bytes_out"] == nout * cnt
-    else:
-        assert st["critical_gets"] == (nin + nout) * n and st["commits"] == nout * n
+    else:  # the probe, then the backend's pin
+        assert st["critical_gets"] == (nin + nout) * 2 and st["commits"] == nout
         assert st["bytes_in"] == nout * nin and st["bytes_out"] == 0
     # checkSomeShards on what was just written: true, then false after a flip
     chk = [jvm.bytes(jvm.read(o, S)) for o in oa[:nout]]
@@ -500,8 +508,9 @@ FILE_CASES = [(4, 2, 1000, 90999, 0), (4, 2, 1000, 92000, 0), (4, 2, 1000, 0, 0)
 @pytest.mark.parametrize("k,m,block,flen,copy", FILE_CASES)
 def test_file_encode_marshalling(jvm, codec42, codec21, k, m, block, flen, copy):
     """The whole file in, every shard out (data split + parity), committed;
-    a file of more than one slice of block rows per shard goes to the library
-    in slices of whole rows, the last one holding the ragged end."""
+    one library call whatever the size; when the JVM copies, a file of more
+    than one slice of block rows per shard goes to the library in slices of
+    whole rows through C buffers, the last one holding the ragged end."""
     codec = codec42 if k == 4 else codec21
     data = np.random.default_rng(flen).integers(0, 256, flen, dtype=np.uint8)
     want = split_file(data, k, m, block)
@@ -517,17 +526,16 @@ def test_file_encode_marshalling(jvm, codec42, codec21, k, m, block, flen, copy)
     st = jvm.assert_clean()
     rows, per = S // block, max(1, SLICE // block)
     calls = file_calls(jvm)
-    if rows <= per:
+    if rows <= per or not copy:
         assert calls == [(flen, S)]  # one call, with the arrays' own lengths
+        if not copy:  # the probe, then the backend's pin: shards committed, the file aborted
+            assert st["critical_gets"] == (k + m + 1) * 2 and st["commits"] == k + m
+            assert st["bytes_in"] == 0 and st["bytes_out"] == 0
     else:
         n = -(-rows // per)
         assert [c[1] for c in calls] == [per * block] * (n - 1) + [(rows - (n - 1) * per) * block]
         assert sum(c[0] for c in calls) == flen
-        if copy:
-            assert st["bytes_in"] == flen and st["bytes_out"] == (k + m) * S
-        else:
-            assert st["critical_gets"] == (k + m + 1) * n and st["commits"] == (k + m) * n
-            assert st["bytes_in"] == 0 and st["bytes_out"] == 0
+        assert st["bytes_in"] == flen and st["bytes_out"] == (k + m) * S
 
 
 @pytest.mark.parametrize("k,m,block,flen,copy", FILE_CASES)
@@ -555,13 +563,13 @@ def test_file_decode_marshalling(jvm, codec42, codec21, k, m, block, flen, copy)
     st = jvm.assert_clean()
     rows, per = S // block, max(1, SLICE // block)
     calls = file_calls(jvm)
-    if rows > per:
+    if rows > per and copy:
         n = -(-rows // per)
         assert len(calls) == n and sum(c[0] for c in calls) == flen
-        if copy:
-            assert st["bytes_in"] == (k + m - 1) * S + k + m and st["bytes_out"] == S + flen
-        else:
-            assert st["commits"] == 2 * n and st["aborts"] == (k + m - 1) * n
+        assert st["bytes_in"] == (k + m - 1) * S + k + m and st["bytes_out"] == S + flen
+    elif not copy:  # one call: the rebuilt shard and the file committed (+ k + m + 1: the probe)
+        assert calls == [(flen, S)]
+        assert st["commits"] == 2 and st["aborts"] == (k + m - 1) + (k + m + 1)
 
 
 def test_file_argument_errors(jvm, codec42):
@@ -712,10 +720,12 @@ def test_alloc_free_pinned(jvm, native):
     jvm.assert_clean()
 
 
-def test_file_decode_sliced_short_file(jvm, codec21):
-    """A sliced decode whose fileSize ends in the first slice: every slice
-    still rebuilds the absent shard (the reference decodes all byteCntInShard
-    bytes before it trims), the later slices write no file bytes."""
+@pytest.mark.parametrize("copy", [0, 1])
+def test_file_decode_sliced_short_file(jvm, codec21, copy):
+    """A decode of shards longer than a slice whose fileSize ends in the
+    first block rows: the absent shard is still rebuilt whole (the reference
+    decodes all byteCntInShard bytes before it trims) -- in one call, or when
+    the JVM copies in slices, the later ones writing no file bytes."""
     k, m, block = 2, 1, 4096
     S = 2 * SLICE + 3 * block
     rng = np.random.default_rng(8)
@@ -724,12 +734,166 @@ def test_file_decode_sliced_short_file(jvm, codec21):
     present = [True, False, True]
     arrs = [jvm.bytes(s if p else np.zeros(S, np.uint8)) for s, p in zip(shards, present)]
     out = jvm.bytes(np.full(10, 0x77, np.uint8))
+    jvm.lib.mock_force_copy(copy)
     jvm.lib.mock_file_decode(0, codec21, jvm.objects(arrs), jvm.bools(present), S, block, out, 5)
+    jvm.lib.mock_force_copy(0)
     assert jvm.exception() == ("", "")
     want = fake_decode(shards, present, 0, S)
     assert np.array_equal(jvm.read(arrs[1], S), want[1])
     got = jvm.read(out, 10)
     assert np.array_equal(got[:5], want[0][:5]) and (got[5:] == 0x77).all()
     calls = file_calls(jvm)
-    assert [c[0] for c in calls] == [5, 0, 0] and sum(c[1] for c in calls) == S
+    if copy:
+        assert [c[0] for c in calls] == [5, 0, 0] and sum(c[1] for c in calls) == S
+    else:
+        assert calls == [(5, S)]
     jvm.assert_clean()
+
+
+# ---- movable arrays: the mock as a compacting GC ----
+
+@pytest.fixture
+def moving(jvm):
+    jvm.lib.mock_moving(1)
+    yield jvm
+    jvm.lib.mock_moving(0)
+
+
+def test_moving_gc_shard_calls(moving, codec42):
+    """Every critical get moves the array (the old mapping unmapped): encode,
+    verify, decode and codeSomeShards still land every byte in the arrays'
+    current places, and every release names the address its get returned."""
+    jvm = moving
+    S, off, cnt = 70_000, 5, 60_000
+    data, arrs = shard_set(jvm, 4, 2, S, seed=21)
+    jvm.lib.mock_encode_parity(0, codec42, jvm.objects(arrs), off, cnt)
+    assert jvm.exception() == ("", "")
+    want = fake_parity(data, 4, 2, off, cnt)
+    assert all(np.array_equal(jvm.read(a, S), w) for a, w in zip(arrs, want))
+    assert jvm.lib.mock_is_parity_correct(0, codec42, jvm.objects(arrs), off, cnt, None) == 1
+    present = [True, False, True, True, False, True]
+    jvm.lib.mock_decode_missing(0, codec42, jvm.objects(arrs), jvm.bools(present), off, cnt)
+    assert jvm.exception() == ("", "")
+    want = fake_decode(want, present, off, cnt)
+    assert all(np.array_equal(jvm.read(a, S), w) for a, w in zip(arrs, want))
+    rows = [np.arange(3, dtype=np.uint8) + r for r in range(2)]
+    outs = [jvm.bytes(np.zeros(S, np.uint8)) for _ in range(2)]
+    jvm.lib.mock_code_some_shards(0, jvm.objects([jvm.bytes(r) for r in rows]), jvm.objects(arrs[:3]), 3,
+                                  jvm.objects(outs), 2, off, cnt)
+    assert jvm.exception() == ("", "")
+    got = fake_code(rows, want[:3], off, cnt)
+    assert all(np.array_equal(jvm.read(o, S)[off:off + cnt], g) for o, g in zip(outs, got))
+    st = jvm.assert_clean()
+    assert jvm.lib.mock_moves() >= 4 * 6  # every call moved every array at least twice
+    assert st["violations"] == 0
+
+
+def test_moving_gc_file_calls(moving, codec42):
+    jvm = moving
+    k, m, block, flen = 4, 2, 1000, 90_999
+    data = np.random.default_rng(22).integers(0, 256, flen, dtype=np.uint8)
+    want = fake_parity(split_file(data, k, m, block), k, m, 0, 23_000)
+    arrs = [jvm.bytes(np.zeros(23_000, np.uint8)) for _ in range(k + m)]
+    jvm.lib.mock_file_encode(0, codec42, jvm.bytes(data), block, jvm.objects(arrs))
+    assert jvm.exception() == ("", "")
+    assert all(np.array_equal(jvm.read(a, 23_000), w) for a, w in zip(arrs, want))
+    out = jvm.bytes(np.zeros(flen, np.uint8))
+    present = [False, True, True, True, True, False]
+    jvm.lib.mock_file_decode(0, codec42, jvm.objects(arrs), jvm.bools(present), 23_000, block, out, flen)
+    assert jvm.exception() == ("", "")
+    dec = fake_decode(want, present, 0, 23_000)
+    assert np.array_equal(jvm.read(out, flen), merge_file(dec, k, block, flen))
+    jvm.assert_clean()
+    assert jvm.lib.mock_moves() > 0
+
+
+# ---- recoverGroupsShardMajor on host arrays (rs_decode_groups_shard_major) ----
+
+def fake_groups(servers, present, chunk):
+    """The fake backend's per-group decode over the master's host arrays."""
+    out = [s.copy() for s in servers]
+    N, T = present.shape
+    for g in range(N):
+        at = [s[g * chunk:(g + 1) * chunk] for s in servers]
+        dec = fake_decode(at, list(present[g]), 0, chunk)
+        for s in range(T):
+            out[s][g * chunk:(g + 1) * chunk] = dec[s]
+    return out
+
+
+@pytest.mark.parametrize("move", [0, 1])
+def test_shard_major_host_marshalling(jvm, codec42, move):
+    """byte[][] servers (one per server, groups back to back, padded past the
+    groups) and byte[] flags: one backend call over movable arrays, every
+    server committed (present chunks are read, absent ones written), the flags
+    copied out; the ByteBuffer[] form reaches the same call by address."""
+    N, chunk = 9, 100
+    rng = np.random.default_rng(40 + move)
+    servers = [rng.integers(0, 256, N * chunk + 37, dtype=np.uint8) for _ in range(6)]
+    present = np.ones((N, 6), bool)
+    present[:5, 0] = False
+    present[5:, [0, 3]] = False
+    want = fake_groups(servers, present, chunk)
+    arrs = [jvm.bytes(s) for s in servers]
+    jvm.lib.mock_moving(move)
+    jvm.lib.mock_recover_groups_shard_major_host(0, codec42, jvm.objects(arrs), chunk, N,
+                                                 jvm.bytes(present.astype(np.uint8).ravel()))
+    jvm.lib.mock_moving(0)
+    assert jvm.exception() == ("", "")
+    for a, w in zip(arrs, want):
+        assert np.array_equal(jvm.read(a, N * chunk + 37), w)
+    st = jvm.assert_clean()
+    assert st["commits"] == 6 and st["critical_gets"] == 12 and st["bytes_in"] == N * 6
+    bufs = [s.copy() for s in servers]
+    jvm.lib.mock_recover_groups_shard_major_direct(0, codec42, jvm.objects([jvm.direct(b) for b in bufs]), chunk, N,
+                                                   jvm.bytes(present.astype(np.uint8).ravel()))
+    assert jvm.exception() == ("", "")
+    assert all(np.array_equal(b, w) for b, w in zip(bufs, want))
+    jvm.assert_clean()
+
+
+def test_shard_major_host_copying_jvm(jvm, codec42):
+    """A JVM that copies: the groups go through C buffers, same results."""
+    N, chunk = 5, 64
+    rng = np.random.default_rng(44)
+    servers = [rng.integers(0, 256, N * chunk, dtype=np.uint8) for _ in range(6)]
+    present = np.ones((N, 6), bool)
+    present[:, 2] = False
+    want = fake_groups(servers, present, chunk)
+    arrs = [jvm.bytes(s) for s in servers]
+    jvm.lib.mock_force_copy(1)
+    jvm.lib.mock_recover_groups_shard_major_host(0, codec42, jvm.objects(arrs), chunk, N,
+                                                 jvm.bytes(present.astype(np.uint8).ravel()))
+    jvm.lib.mock_force_copy(0)
+    assert jvm.exception() == ("", "")
+    assert all(np.array_equal(jvm.read(a, N * chunk), w) for a, w in zip(arrs, want))
+    jvm.assert_clean()
+
+
+def test_shard_major_host_argument_errors(jvm, codec42):
+    """Java-side checks (null flags, a flag count that is not nGroups x 6,
+    negative sizes, the shard count) and the library's (a short server, a
+    group with fewer than k present: real backend, no device needed), none
+    writing any array."""
+    N, chunk = 4, 100
+    servers = [np.full(N * chunk, i, np.uint8) for i in range(6)]
+    arrs = [jvm.bytes(s) for s in servers]
+    ok = jvm.bytes(np.ones(N * 6, np.uint8))
+
+    def call(objs, flags, chunk_len=chunk, n=N, real=0):
+        jvm.lib.mock_reset()
+        jvm.lib.mock_recover_groups_shard_major_host(real, codec42, objs, chunk_len, n, flags)
+        jvm.assert_clean()
+        return jvm.exception()
+
+    assert call(jvm.objects(arrs), None) == (NPE, "present is null")
+    assert call(jvm.objects(arrs), jvm.bytes(np.ones(23, np.uint8))) == (
+        IAE, "present has 23 flags; nGroups * total shards is 24")
+    assert call(jvm.objects(arrs), ok, chunk_len=-1) == (IAE, "negative size")
+    assert call(jvm.objects(arrs[:5]), ok) == (IAE, "wrong number of shards: 5")
+    short = arrs[:5] + [jvm.bytes(np.zeros(N * chunk - 1, np.uint8))]
+    assert call(jvm.objects(short), ok, real=1)[0] == IAE
+    flags = np.ones((N, 6), np.uint8)
+    flags[2, :3] = 0
+    assert call(jvm.objects(arrs), jvm.bytes(flags.ravel()), real=1) == (IAE, "Not enough shards present")
+    assert all(np.array_equal(jvm.read(a, N * chunk), s) for a, s in zip(arrs, servers))
