@@ -312,8 +312,11 @@ def run(args, live_traffic=None):
             with gpu_numa_bound(torch, parallel, extra):
                 link = host_link(torch)
                 extra.update(config0_single_stripe(rsamd, k, m))
+                extra.update(host_small_calls(rsamd, k, m))
                 extra.update(host_by_size(rsamd, k, m))
                 extra.update(host_inclusive(rsamd, k, m, link))
+                extra.update(host_groups_leg(rsamd, k, m, link))
+                extra.update(host_jni_legs(rsamd, k, m, link))
             cpu = cpu_baseline(k, m, S, args.cpu_seconds)
             extra["cpu_configs"] = cpu_configs()
         else:
@@ -363,33 +366,8 @@ def run(args, live_traffic=None):
             "rank_avg_launch_ms_min": fast_ms,
             "rank_avg_launch_ms_max": slow_ms,
             "host_link": link,
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": traffic,
-                "traffic_source": traffic_source,
-                "traffic_live": live_traffic,
-                "kernel": f"gf_vec_kernel<{k},{m},false> (rs_encode_batch_dev)",
-                "alg_bytes_per_launch": alg_bytes,
-                "achieved_basis": ("the slowest rank's mean HIP-event launch time; per GPU" if world > 1
-                                   else "mean HIP-event launch time"),
-                "frac_per_gpu_min": round(alg_bytes / (slow_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                "frac_per_gpu_max": round(alg_bytes / (fast_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                "aggregate_achieved": round(world * alg_bytes / (slow_ms * 1e-3) / 1e9, 1),
-                "aggregate_peak": world * HBM_PEAK_GBPS,
-                "avg_launch_ms": round(launch_ms, 4),
-                "median_launch_ms": round(median_ms, 4),  # SURVEY 8(d) asks for the median too
-                # also as a fraction of the measured device copy kernel
-                "frac_of_copy_kernel": (round(achieved / extra["copy_kernel_GBps"], 4)
-                                        if extra.get("copy_kernel_GBps") else None),
-                # north_star's decode target (configs[2], >= 0.50 on 2 erasures) and the
-                # other configs, here so a record that keeps only this object has them
-                # (ReedSolomon.java:175-272; full legs in `extra`)
-                **decode_summary(extra),
-            },
+            "roofline": roofline_object(world, achieved, traffic, traffic_source, live_traffic, k, m, alg_bytes,
+                                        slow_ms, fast_ms, launch_ms, median_ms, extra),
             "cpu_baseline": cpu,
             "extra": extra,
         }
@@ -403,23 +381,62 @@ def run(args, live_traffic=None):
     return 0
 
 
+# The driver keeps the first 23 keys of `roofline` (BENCH_r05): the contract's
+# six first, then the legs' fractions that matter most at this N, the rest
+# after them, the bookkeeping last.
+FIRST_N1 = ["c2_dec2_frac", "c3_enc_frac", "c3_enc_granule_frac", "c4_enc_frac", "c4_enc_granule_frac",
+            "file_enc_frac", "file_dec_frac", "shard_major_dec01_frac", "group_major_bits_frac", "host_enc_link_frac",
+            "host_file_enc_link_frac", "host_groups_link_frac", "host_jni_enc_link_frac",
+            "host_jni_file_enc_link_frac", "host_dec_1000B_us", "host_enc_4K_us", "verify_frac"]
+FIRST_NN = ["c2_dec2_frac", "c3_enc_frac", "c3_enc_granule_frac", "c3_dec4_frac", "c3_dec4_granule_frac",
+            "sustained_frac", "host_pinned_all_ranks_frac_of_N_links", "host_pageable_all_ranks_frac_of_N_links",
+            "host_pageable_all_ranks_GiBps", "host_pinned_all_ranks_GiBps"]
+
+
+def roofline_object(world, achieved, traffic, traffic_source, live_traffic, k, m, alg_bytes, slow_ms, fast_ms,
+                    launch_ms, median_ms, extra):
+    head = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic}
+    summary = decode_summary(extra)
+    first = FIRST_N1 if world == 1 else FIRST_NN
+    obj = dict(head)
+    obj.update({key: summary.get(key) for key in first})
+    obj.update({key: v for key, v in summary.items() if key not in obj})
+    obj.update({
+        "kernel": f"gf_vec_kernel<{k},{m},false> (rs_encode_batch_dev)",
+        "alg_bytes_per_launch": alg_bytes,
+        "avg_launch_ms": round(launch_ms, 4),
+        # also as a fraction of the measured device copy kernel
+        "frac_of_copy_kernel": (round(achieved / extra["copy_kernel_GBps"], 4)
+                                if extra.get("copy_kernel_GBps") else None),
+        "traffic_live": live_traffic,
+        "traffic_source": traffic_source,
+        "achieved_basis": ("the slowest rank's mean HIP-event launch time; per GPU" if world > 1
+                           else "mean HIP-event launch time"),
+        "frac_per_gpu_min": round(alg_bytes / (slow_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+        "frac_per_gpu_max": round(alg_bytes / (fast_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+        "aggregate_achieved": round(world * alg_bytes / (slow_ms * 1e-3) / 1e9, 1),
+        "aggregate_peak": world * HBM_PEAK_GBPS,
+        "median_launch_ms": round(median_ms, 4),  # SURVEY 8(d) asks for the median too
+    })
+    return obj
+
+
 def decode_summary(extra):
-    """Short roofline keys for the decode legs and configs[2]-[4] (fractions of
-    8 TB/s; None where the leg did not run, e.g. at N > 1)."""
+    """Short roofline keys for every leg: fractions of 8 TB/s for the device
+    legs, of the measured link bound for the host legs, microseconds for the
+    small calls (None where the leg did not run, e.g. at N > 1)."""
     g = extra.get
     d01 = g("decode_0_1_hbm_frac") or g("decode_0_1_all_ranks_hbm_frac_per_gpu")
     return {
-        "decode_0_frac": g("decode_0_hbm_frac"),
-        "decode_0_1_frac": d01,
+        "c2_dec1_frac": g("decode_0_hbm_frac"), "c2_dec2_frac": d01,
         "decode_0_5_frac": g("decode_0_5_hbm_frac"),
         "decode_patterns_min": g("decode_patterns_min"),
         "decode_2_erasures_target_0_50_met": (d01 >= 0.50 and (g("decode_0_5_hbm_frac") or 1) >= 0.50)
         if d01 is not None else None,
-        # every config and caller leg as a scalar key (a record that keeps only
-        # the scalar keys of this object keeps them all): configs[2]-[4]
-        # (BASELINE.json), the master's recovery (f2), the fused file layout
-        # (f1), verify (f3), and the host-inclusive legs against the link bound
-        "c2_dec1_frac": g("decode_0_hbm_frac"), "c2_dec2_frac": d01,
+        # configs[2]-[4] (BASELINE.json), the master's recovery (f2), the fused
+        # file layout (f1), verify (f3), and the host-inclusive legs against the
+        # link bound
         "c3_enc_frac": g("cfg3_strong_encode_hbm_frac_per_gpu"),
         "c3_dec4_frac": g("cfg3_strong_decode_hbm_frac_per_gpu"),
         "c3_enc_pad_frac": g("cfg3_strong_stride_rec_encode_hbm_frac_per_gpu"),
@@ -454,8 +471,26 @@ def decode_summary(extra):
         "host_pinned_enc_link_frac": g("host_inclusive_pinned_encode_frac_of_link_bound"),
         "host_pinned_file_enc_link_frac": g("host_inclusive_pinned_file_encode_frac_of_link_bound"),
         "host_pinned_file_dec_link_frac": g("host_inclusive_pinned_file_decode_0_5_frac_of_link_bound"),
+        # the master's recovery on its host arrays (NativeReedSolomon.recoverGroupsShardMajor)
+        "host_groups_GiBps": g("host_groups_dec0_GiBps"),
+        "host_groups_link_frac": g("host_groups_dec0_frac_of_link_bound"),
+        "host_groups_grows_link_frac": g("host_groups_grows_frac_of_link_bound"),
+        # a JVM caller: the JNI core over the mock JNIEnv
+        "host_jni_enc_link_frac": g("host_jni_encode_frac_of_link_bound"),
+        "host_jni_dec01_link_frac": g("host_jni_decode_0_1_frac_of_link_bound"),
+        "host_jni_file_enc_link_frac": g("host_jni_file_encode_frac_of_link_bound"),
+        "host_jni_file_dec_link_frac": g("host_jni_file_decode_0_5_frac_of_link_bound"),
+        # small calls, microseconds per call from C
+        "host_dec_1000B_us": g("host_dec_1000B_us"), "host_enc_4K_us": g("host_enc_4K_us"),
+        "host_jni_dec_1000B_us": g("host_jni_dec_1000B_us"), "host_jni_enc_4K_us": g("host_jni_enc_4K_us"),
+        "cpu_port_dec_1000B_us": g("cpu_port_dec_1000B_us"),
         "host_enc_64K_us": g("host_enc_64K_us"), "host_enc_1M_us": g("host_enc_1024K_us"),
         "host_enc_4M_us": g("host_enc_4096K_us"),
+        # N > 1: every rank calling the host API at once
+        "host_pinned_all_ranks_GiBps": g("host_inclusive_pinned_encode_all_ranks_GiBps"),
+        "host_pageable_all_ranks_GiBps": g("host_inclusive_pageable_encode_all_ranks_GiBps"),
+        "host_pinned_all_ranks_frac_of_N_links": g("host_inclusive_pinned_encode_all_ranks_frac_of_N_links"),
+        "host_pageable_all_ranks_frac_of_N_links": g("host_inclusive_pageable_encode_all_ranks_frac_of_N_links"),
     }
 
 
@@ -1502,6 +1537,234 @@ def host_inclusive(rsamd, k, m, link=None):
     return out
 
 
+def _mockjni():
+    """The mock JNIEnv over librsamd (tests/jni_mock, built by build()): a C
+    caller for the small-call and JNI legs."""
+    d = os.path.join(ROOT, "tests", "jni_mock")
+    if d not in sys.path:
+        sys.path.insert(0, d)
+    import mockjni
+    return mockjni.load()
+
+
+def _mock_array(mj, a):
+    """A mock Java byte[] holding a copy of NumPy array a."""
+    import ctypes as C
+    o = mj.mock_new_bytes(len(a))
+    if len(a):
+        C.memmove(mj.mock_data(o), a.ctypes.data, len(a))
+    return o
+
+
+def _mock_view(mj, o, n):
+    import ctypes as C
+    import numpy as np
+    return np.ctypeslib.as_array(C.cast(mj.mock_data(o), C.POINTER(C.c_uint8)), shape=(n,))
+
+
+def _mock_objects(mj, arrs):
+    objs = mj.mock_new_objects(len(arrs))
+    for i, o in enumerate(arrs):
+        mj.mock_set(objs, i, o)
+    return objs
+
+
+def host_small_calls(rsamd, k, m, reps=2000):
+    """Small host calls per call, median microseconds of `reps` calls from a C
+    caller (no Python per call; tests/jni_mock's timing loops): 4+2 x 1000-B
+    decodeMissing {0} -- the recovery machine's call per chunk group
+    (ChunkserverDiskRecoveryMachine.java:44) -- and 4+2 x 4 KiB encodeParity
+    (configs[4]'s stripe), through the C-ABI and through the JNI core over the
+    mock JNIEnv (the path a JVM caller takes, minus the JVM's own JNI cost);
+    every output checked against the oracle afterwards.  Beside them the
+    scalar port's time for the same decode (1 thread, a bounded batch)."""
+    import ctypes as C
+    import numpy as np
+    from rsamd import _lib
+    from oracle import c_ref
+    mj = _mockjni()
+    rs = rsamd.ReedSolomon.create(k, m)
+    oc = c_ref.Codec(k, m)
+    out, ok = {}, True
+    T = k + m
+    for S, kind, key in ((1000, 1, "dec_1000B"), (4096, 0, "enc_4K")):
+        rng = np.random.default_rng(S)
+        want = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
+        oc.encode_parity(want, 0, S)
+        sh = [a.copy() for a in want]
+        if kind == 1:
+            sh[0][:] = 0x3C
+        else:
+            for p in range(k, T):
+                sh[p][:] = 0
+        present = np.array([0] + [1] * (T - 1), np.uint8)
+        ptrs = (_lib.u8p * T)(*[a.ctypes.data_as(_lib.u8p) for a in sh])
+        lens = (C.c_int64 * T)(*[S] * T)
+        us = mj.mock_time_capi(kind, rs.handle, ptrs, T, lens, present.ctypes.data_as(_lib.u8p), S, reps)
+        ok = ok and us > 0 and all(np.array_equal(a, b) for a, b in zip(sh, want))
+        mj.mock_reset()
+        arrs = [_mock_array(mj, a) for a in sh]
+        if kind == 1:
+            _mock_view(mj, arrs[0], S)[:] = 0x3C
+        else:
+            for p in range(k, T):
+                _mock_view(mj, arrs[p], S)[:] = 0
+        pres = mj.mock_new_bools(T)
+        C.memmove(mj.mock_data(pres), present.ctypes.data, T)
+        usj = mj.mock_time_jni(kind, rs.handle, _mock_objects(mj, arrs), pres, S, reps)
+        ok = ok and usj > 0 and all(np.array_equal(_mock_view(mj, o, S), b) for o, b in zip(arrs, want))
+        out[f"host_{key}_us"] = round(us, 2)
+        out[f"host_jni_{key}_us"] = round(usj, 2)
+    rate, n, el = cpu_rate(oc, k, m, 1000, [False] + [True] * (T - 1), 1, 1.0, 100_000)
+    out["cpu_port_dec_1000B_us"] = round(k * 1000 / (rate * 2**30) * 1e6, 3)
+    out["host_small_calls_bit_exact"] = bool(ok)
+    out["host_small_calls_note"] = (
+        f"{k}+{m}, one stripe per call, pageable host arrays; median of {reps} calls from C "
+        f"(tests/jni_mock timing loops): host_* through the C-ABI, host_jni_* through jni/rs_jni_core.c over the "
+        f"mock JNIEnv; the small-call pass is one signalled direct-kernel launch (DESIGN.md 5.2); "
+        f"cpu_port_dec_1000B_us: the oracle's scalar decodeMissing per 1000-B group, 1 thread, {n} groups in "
+        f"{el:.1f} s")
+    return out
+
+
+def host_groups_leg(rsamd, k, m, link=None, N=1 << 20, chunk=1000, reps=5):
+    """The master's recovery loop on its pageable host arrays
+    (rs_decode_groups_shard_major = NativeReedSolomon.recoverGroupsShardMajor;
+    MasterImpl.java:733-743, 794-839 with ChunkserverDiskRecoveryMachine.java:
+    34-48 per group): k+m arrays of N 1000-B chunks, one per server; offline
+    {0} for every group (one run), then a set that grows to {0, k+m-1} at group
+    N/2 + 1 (two runs).  GiB/s of user data (k chunks per group) against the
+    link bound of the bytes each call moves (the k survivors up, the rebuilt
+    chunks down); the rebuilt chunks checked against the oracle on sampled
+    groups.  Beside it: the same groups through one decodeMissing per group
+    (host_dec_1000B_us) and the scalar port."""
+    import numpy as np
+    from oracle import c_ref
+    from rsamd.recovery import recover_groups_shard_major
+    T, L = k + m, N * chunk
+    rng = np.random.default_rng(11)
+    blk = rng.integers(0, 256, 64 << 20, dtype=np.uint8)
+    servers = []
+    for i in range(T):
+        a = np.empty(L, np.uint8)
+        if i < k:
+            for o in range(0, L, len(blk)):
+                n = min(len(blk), L - o)
+                a[o:o + n] = np.roll(blk, 4099 * i)[:n]
+        servers.append(a)
+    rs = rsamd.ReedSolomon.create(k, m)
+    rs.encodeParity(servers, 0, L)
+    sample = rng.choice(N, 64, replace=False)
+    oc = c_ref.Codec(k, m)
+    ok = True
+    for g in sample:  # the encode itself, per group, against the oracle
+        grp = [s[g * chunk:(g + 1) * chunk].copy() for s in servers]
+        ref = [x.copy() for x in grp[:k]] + [np.zeros(chunk, np.uint8) for _ in range(m)]
+        oc.encode_parity(ref, 0, chunk)
+        ok = ok and all(np.array_equal(x, y) for x, y in zip(grp, ref))
+    saved = {s: servers[s].copy() for s in (0, T - 1)}
+    out = {}
+    j = N // 2 + 1
+    for name, down in (("dec0", 1.0 / k), ("grows", (1.0 + (N - j) / N) / k)):
+        present = np.ones((N, T), bool)
+        present[:, 0] = False
+        if name == "grows":
+            present[j:, T - 1] = False
+        servers[0][:] = 0x3C
+        if name == "grows":
+            servers[T - 1][j * chunk:] = 0x3C
+        for _ in range(2):
+            recover_groups_shard_major(servers, present, chunk, k, m)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            recover_groups_shard_major(servers, present, chunk, k, m)
+        t = (time.perf_counter() - t0) / reps
+        ok = ok and all(np.array_equal(servers[s], saved[s]) for s in saved)
+        key = f"host_groups_{name}_GiBps"
+        out[key] = round(k * L / t / 2**30, 3)
+        bound = link_bound_GiBps(link, 1.0, down)
+        if bound:
+            out[key.replace("_GiBps", "_link_bound_GiBps")] = bound
+            out[key.replace("_GiBps", "_frac_of_link_bound")] = round(out[key] / bound, 4)
+    out["host_groups_bit_exact"] = bool(ok)
+    out["host_groups_note"] = (f"{k}+{m} x {chunk}-B chunk groups x {N}, one pageable array per server "
+                               f"({L / 1e9:.2f} GB each); one call = every group (runs of one offline set, each "
+                               f"one decodeMissing of run-long shards through the mirrored pipeline); {reps} calls "
+                               f"timed per leg; dec0: offline {{0}}; grows: {{0}} then {{0,{T - 1}}} from group "
+                               f"{j}; GiB/s of k chunks per group")
+    del servers, saved
+    return out
+
+
+def host_jni_legs(rsamd, k, m, link=None, n=64 << 20, fbytes=256 << 20, reps=12):
+    """What a JVM caller gets: the JNI core (jni/rs_jni_core.c, the marshalling
+    NativeReedSolomon's natives run) over the mock JNIEnv and librsamd, Java
+    byte[] arrays in and out -- one library call per Java call with the arrays
+    pinned only around the library's copy batches.  encodeParity and
+    decodeMissing {0,1} of 4+2 x 64 MiB, encodeFile / decodeFile {0,5} of a
+    256 MiB file, against the link bound of the bytes each moves; outputs
+    checked against the numpy-array calls' (themselves oracle-checked)."""
+    import numpy as np
+    mj = _mockjni()
+    mj.mock_reset()
+    rs = rsamd.ReedSolomon.create(k, m)
+    T = k + m
+    rng = np.random.default_rng(17)
+    data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
+    ref = data + [np.zeros(n, np.uint8) for _ in range(m)]
+    rs.encodeParity(ref, 0, n)
+    arrs = [_mock_array(mj, a) for a in ref[:k]] + [mj.mock_new_bytes(n) for _ in range(m)]
+    objs = _mock_objects(mj, arrs)
+    out = {}
+
+    def rate(fn, user_bytes):
+        for _ in range(3):
+            fn()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        return round(user_bytes / ((time.perf_counter() - t0) / reps) / 2**30, 3)
+
+    out["host_jni_encode_GiBps"] = rate(lambda: mj.mock_encode_parity(1, rs.handle, objs, 0, n), k * n)
+    ok = all(np.array_equal(_mock_view(mj, o, n), r) for o, r in zip(arrs, ref))
+    present = mj.mock_new_bools(T)
+    _mock_view(mj, present, T)[:] = [0, 0] + [1] * (T - 2)
+    _mock_view(mj, arrs[0], n)[:] = 0
+    _mock_view(mj, arrs[1], n)[:] = 0
+    out["host_jni_decode_0_1_GiBps"] = rate(lambda: mj.mock_decode_missing(1, rs.handle, objs, present, 0, n), k * n)
+    ok = ok and all(np.array_equal(_mock_view(mj, o, n), r) for o, r in zip(arrs, ref))
+    from rsamd.layout import file_encode_into, file_layout
+    fdata = rng.integers(0, 256, fbytes, dtype=np.uint8)
+    _, S = file_layout(rs, fbytes)
+    fref = [np.zeros(S, np.uint8) for _ in range(T)]
+    file_encode_into(rs, fdata, fref)
+    farr = _mock_array(mj, fdata)
+    fsh = [mj.mock_new_bytes(S) for _ in range(T)]
+    fobjs = _mock_objects(mj, fsh)
+    out["host_jni_file_encode_GiBps"] = rate(lambda: mj.mock_file_encode(1, rs.handle, farr, 1000, fobjs), fbytes)
+    ok = ok and all(np.array_equal(_mock_view(mj, o, S), r) for o, r in zip(fsh, fref))
+    fpres = mj.mock_new_bools(T)
+    _mock_view(mj, fpres, T)[:] = [0] + [1] * (T - 2) + [0]
+    fout = mj.mock_new_bytes(fbytes)
+    out["host_jni_file_decode_0_%d_GiBps" % (T - 1)] = rate(
+        lambda: mj.mock_file_decode(1, rs.handle, fobjs, fpres, S, 1000, fout, fbytes), fbytes)
+    ok = ok and np.array_equal(_mock_view(mj, fout, fbytes), fdata)
+    ok = ok and all(np.array_equal(_mock_view(mj, o, S), r) for o, r in zip(fsh, fref))
+    exc = mj.mock_exc_class().decode()
+    out["host_jni_bit_exact"] = bool(ok and not exc)
+    legs = {"host_jni_encode_GiBps": (1.0, m / k), "host_jni_decode_0_1_GiBps": (1.0, 2 / k),
+            "host_jni_file_encode_GiBps": (1.0, m / k), "host_jni_file_decode_0_%d_GiBps" % (T - 1): (1.0, 2.0 / k)}
+    for key, (up, down) in legs.items():
+        bound = link_bound_GiBps(link, up, down)
+        if bound:
+            out[key.replace("_GiBps", "_frac_of_link_bound")] = round(out[key] / bound, 4)
+    out["host_jni_note"] = (f"jni/rs_jni_core.c over the mock JNIEnv (tests/jni_mock) and librsamd: Java byte[] "
+                            f"arrays ({k}+{m} x {n >> 20} MiB; a {fbytes >> 20} MiB file, 1000-B blocks), one library "
+                            f"call per Java call with the arrays movable (pinned only around the library's copy "
+                            f"batches, rs_set_relocator); {reps} calls timed per leg")
+    return out
+
+
 def config0_single_stripe(rsamd, k, m, S=64 << 10, reps=200):
     """BASELINE configs[0]: one 4+2 stripe of 64 KiB shards, encode then a
     1-erasure decode, through the JNI-facing host API (H2D + kernel + D2H per
@@ -1601,8 +1864,9 @@ def host_inclusive_all_ranks(rsamd, parallel, r, k, m, link=None, n=64 << 20, re
     bound = link_bound_GiBps(link, 1.0, m / k)  # rank 0's own link, measured alone
     if bound:
         out["host_inclusive_rank0_link_bound_GiBps"] = bound
-        out["host_inclusive_pinned_encode_all_ranks_frac_of_N_links"] = round(
-            out["host_inclusive_pinned_encode_all_ranks_GiBps"] / (r.world * bound), 4)
+        for name in ("pinned", "pageable"):
+            out[f"host_inclusive_{name}_encode_all_ranks_frac_of_N_links"] = round(
+                out[f"host_inclusive_{name}_encode_all_ranks_GiBps"] / (r.world * bound), 4)
     del pin, pageable
     for b in held:
         b.free()

@@ -571,3 +571,63 @@ void mock_recover_groups_shard_major_direct(int real, const rs_codec *c, mobj *s
                                             mobj *present) {
     rsj_recover_groups_shard_major_direct(&ENV, backend(real), c, servers, chunk, n, present);
 }
+
+/* ---- timing loops for bench.py's host legs (a C caller: no Python per call) ----
+ * Median microseconds per call over `reps` calls after 20 warm-up calls.
+ * kind: 0 encodeParity, 1 decodeMissing.  mock_time_jni goes through the JNI
+ * core (rsj_* over this mock JNIEnv, the real backend), mock_time_capi calls
+ * the C-ABI directly. */
+#include <time.h>
+
+static double now_us(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec * 1e6 + t.tv_nsec * 1e-3;
+}
+
+static int cmp_double(const void *a, const void *b) {
+    const double x = *(const double *)a, y = *(const double *)b;
+    return (x > y) - (x < y);
+}
+
+static double median_of(double *t, int n) {
+    qsort(t, (size_t)n, sizeof *t, cmp_double);
+    return t[n / 2];
+}
+
+double mock_time_jni(int kind, const rs_codec *c, mobj *shards, mobj *present, int32_t cnt, int reps) {
+    double *t = (double *)malloc(sizeof(double) * (size_t)(reps > 0 ? reps : 1));
+    for (int i = -20; i < reps; i++) {
+        const double t0 = now_us();
+        if (kind == 0)
+            rsj_encode_parity(&ENV, rsj_librsamd_backend(), c, shards, 0, cnt);
+        else
+            rsj_decode_missing(&ENV, rsj_librsamd_backend(), c, shards, present, 0, cnt);
+        if (S.exc) {
+            free(t);
+            return -1.0;
+        }
+        if (i >= 0) t[i] = now_us() - t0;
+    }
+    const double m = median_of(t, reps);
+    free(t);
+    return m;
+}
+
+double mock_time_capi(int kind, const rs_codec *c, uint8_t *const *sh, int n, const int64_t *lens,
+                      const uint8_t *present, int32_t cnt, int reps) {
+    double *t = (double *)malloc(sizeof(double) * (size_t)(reps > 0 ? reps : 1));
+    for (int i = -20; i < reps; i++) {
+        const double t0 = now_us();
+        const int rc = kind == 0 ? rs_encode_parity(c, sh, n, lens, 0, cnt)
+                                 : rs_decode_missing(c, sh, n, lens, present, 0, cnt);
+        if (rc) {
+            free(t);
+            return -1.0;
+        }
+        if (i >= 0) t[i] = now_us() - t0;
+    }
+    const double m = median_of(t, reps);
+    free(t);
+    return m;
+}

@@ -201,7 +201,7 @@ def test_decode_summary_keys():
           "decode_patterns_min": 0.84, "cfg3_strong_encode_hbm_frac_per_gpu": 0.77,
           "granule_4p2_4KiB_x1M_encode_hbm_frac": 0.87}
     s = bench.decode_summary(ex)
-    assert (s["decode_0_frac"], s["decode_0_1_frac"], s["decode_0_5_frac"], s["decode_patterns_min"]) == \
+    assert (s["c2_dec1_frac"], s["c2_dec2_frac"], s["decode_0_5_frac"], s["decode_patterns_min"]) == \
         (0.87, 0.86, 0.85, 0.84)
     assert s["decode_2_erasures_target_0_50_met"] is True
     assert s["c3_enc_frac"] == 0.77 and s["c4_enc_granule_frac"] == 0.87
@@ -209,6 +209,27 @@ def test_decode_summary_keys():
     # every key is a scalar: a record that drops nested objects keeps them all
     assert all(not isinstance(v, (dict, list)) for v in s.values())
     n8 = bench.decode_summary({"decode_0_1_all_ranks_hbm_frac_per_gpu": 0.45})
-    assert n8["decode_0_1_frac"] == 0.45 and n8["decode_0_frac"] is None
+    assert n8["c2_dec2_frac"] == 0.45 and n8["c2_dec1_frac"] is None
     assert n8["decode_2_erasures_target_0_50_met"] is False
     assert bench.decode_summary({})["decode_2_erasures_target_0_50_met"] is None
+
+
+def test_roofline_first_keys():
+    """The driver keeps the first 23 keys of `roofline`: the contract's six,
+    then configs[2]-[4], f1, f2 and the host legs at N = 1 (the multi-GPU legs
+    at N > 1); the bookkeeping keys come last."""
+    sys.path.insert(0, ROOT)
+    import bench
+    for world, first in ((1, bench.FIRST_N1), (8, bench.FIRST_NN)):
+        obj = bench.roofline_object(world, 6900.0, 1.0, "src", None, 4, 2, 100, 3.7, 3.6, 3.7, 3.7, {})
+        keys = list(obj)
+        assert keys[:6] == ["bound", "achieved", "peak", "unit", "frac", "traffic"]
+        assert keys[6:6 + len(first)] == first and 6 + len(first) <= 23
+        assert keys[-1] == "median_launch_ms" and "traffic_source" not in keys[:23]
+        assert all(not isinstance(obj[key], (dict, list)) for key in keys[:23])
+    for key in ("c3_enc_frac", "c3_enc_granule_frac", "c4_enc_frac", "c4_enc_granule_frac", "file_enc_frac",
+                "file_dec_frac", "shard_major_dec01_frac", "group_major_bits_frac", "host_enc_link_frac",
+                "host_file_enc_link_frac", "host_groups_link_frac", "host_jni_enc_link_frac",
+                "host_jni_file_enc_link_frac", "host_dec_1000B_us", "host_enc_4K_us"):
+        assert key in bench.FIRST_N1
+    assert "host_pageable_all_ranks_frac_of_N_links" in bench.FIRST_NN

@@ -18,16 +18,12 @@ critical region faults.
 """
 import ctypes as C
 import os
-import subprocess
 
 import numpy as np
 import pytest
 
-from conftest import PKG_DIR, ROOT
+from conftest import ROOT
 
-BUILD = os.path.join(ROOT, "build", "jni_mock")
-SRC = [os.path.join(PKG_DIR, "jni", "rs_jni_core.c"), os.path.join(ROOT, "tests", "jni_mock", "mock_env.c")]
-LIBDIR = os.path.join(PKG_DIR, "lib")
 SLICE = 32 << 20  # RSJ_SLICE_BYTES
 
 NPE = "java/lang/NullPointerException"
@@ -37,47 +33,10 @@ AIOOBE = "java/lang/ArrayIndexOutOfBoundsException"
 
 
 def build_mock():
-    from rsamd import _lib
-    _lib.load()  # the HIP runtime and librsamd first (see _lib.load)
-    os.makedirs(BUILD, exist_ok=True)
-    so = os.path.join(BUILD, "libmockjni.so")
-    if not os.path.exists(so) or any(os.path.getmtime(s) > os.path.getmtime(so) for s in SRC):
-        subprocess.run(["gcc", "-std=c11", "-O1", "-g", "-Wall", "-Wextra", "-Werror", "-Wno-unused-parameter",
-                        "-shared", "-fPIC", "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(PKG_DIR, "jni"),
-                        *SRC, "-L" + LIBDIR, "-lrsamd", "-Wl,-rpath," + LIBDIR, "-o", so], check=True)
-    lib = C.CDLL(so)
-    P = C.c_void_p
-    for name, res, args in [
-        ("mock_new_bytes", P, [C.c_int]), ("mock_new_bools", P, [C.c_int]), ("mock_new_objects", P, [C.c_int]),
-        ("mock_set", None, [P, C.c_int, P]), ("mock_data", P, [P]), ("mock_reset", None, []),
-        ("mock_fail_critical", None, [C.c_int]), ("mock_force_copy", None, [C.c_int]),
-        ("mock_moving", None, [C.c_int]), ("mock_moves", C.c_longlong, []),
-        ("mock_recover_groups_shard_major_host", None, [C.c_int, P, P, C.c_int32, C.c_int32, P]),
-        ("mock_recover_groups_shard_major_direct", None, [C.c_int, P, P, C.c_int32, C.c_int32, P]),
-        ("mock_exc_class", C.c_char_p, []), ("mock_exc_message", C.c_char_p, []),
-        ("mock_stats", None, [C.POINTER(C.c_longlong)]),
-        ("mock_encode_parity", None, [C.c_int, P, P, C.c_int32, C.c_int32]),
-        ("mock_decode_missing", None, [C.c_int, P, P, P, C.c_int32, C.c_int32]),
-        ("mock_is_parity_correct", C.c_int, [C.c_int, P, P, C.c_int32, C.c_int32, P]),
-        ("mock_code_some_shards", None, [C.c_int, P, P, C.c_int32, P, C.c_int32, C.c_int32, C.c_int32]),
-        ("mock_check_some_shards", C.c_int, [C.c_int, P, P, C.c_int32, P, C.c_int32, C.c_int32, C.c_int32]),
-        ("mock_recover_groups_shard_major", None,
-         [C.c_int, P, C.c_int64, C.c_int64, C.c_int32, C.c_int64, P, C.c_int64]),
-        ("mock_shard_major_record", None, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint8), C.c_int]),
-        ("mock_shard_major_rc", None, [C.c_int]),
-        ("mock_file_encode", None, [C.c_int, P, P, C.c_int32, P]),
-        ("mock_file_decode", None, [C.c_int, P, P, P, C.c_int32, C.c_int32, P, C.c_int32]),
-        ("mock_file_record", None, [C.POINTER(C.c_int64), C.c_int]),
-        ("mock_new_direct", P, [P, C.c_int]), ("mock_host_live", C.c_int, []), ("mock_drop_local", None, []),
-        ("mock_alloc_pinned", P, [C.c_int, C.c_int32]), ("mock_free_pinned", None, [C.c_int, P]),
-        ("mock_encode_parity_direct", None, [C.c_int, P, P, C.c_int32, C.c_int32]),
-        ("mock_decode_missing_direct", None, [C.c_int, P, P, P, C.c_int32, C.c_int32]),
-        ("mock_file_encode_direct", None, [C.c_int, P, P, C.c_int32, C.c_int32, P]),
-        ("mock_file_decode_direct", None, [C.c_int, P, P, P, C.c_int32, C.c_int32, P, C.c_int32]),
-    ]:
-        fn = getattr(lib, name)
-        fn.restype, fn.argtypes = res, args
-    return lib
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "jni_mock"))
+    import mockjni
+    return mockjni.load()
 
 
 class Jvm:
