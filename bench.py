@@ -315,8 +315,8 @@ def run(args, live_traffic=None):
                 extra.update(host_small_calls(rsamd, k, m))
                 extra.update(host_by_size(rsamd, k, m))
                 extra.update(host_inclusive(rsamd, k, m, link))
-                extra.update(host_groups_leg(rsamd, k, m, link))
                 extra.update(host_jni_legs(rsamd, k, m, link))
+                extra.update(host_groups_leg(rsamd, k, m, link))
             cpu = cpu_baseline(k, m, S, args.cpu_seconds)
             extra["cpu_configs"] = cpu_configs()
         else:
@@ -1696,7 +1696,7 @@ def host_groups_leg(rsamd, k, m, link=None, N=1 << 20, chunk=1000, reps=5):
     return out
 
 
-def host_jni_legs(rsamd, k, m, link=None, n=64 << 20, fbytes=256 << 20, reps=12):
+def host_jni_legs(rsamd, k, m, link=None, n=64 << 20, fbytes=256 << 20, reps=24, huge=1):
     """What a JVM caller gets: the JNI core (jni/rs_jni_core.c, the marshalling
     NativeReedSolomon's natives run) over the mock JNIEnv and librsamd, Java
     byte[] arrays in and out -- one library call per Java call with the arrays
@@ -1707,6 +1707,7 @@ def host_jni_legs(rsamd, k, m, link=None, n=64 << 20, fbytes=256 << 20, reps=12)
     import numpy as np
     mj = _mockjni()
     mj.mock_reset()
+    mj.mock_hugepages(huge)
     rs = rsamd.ReedSolomon.create(k, m)
     T = k + m
     rng = np.random.default_rng(17)
@@ -1759,9 +1760,11 @@ def host_jni_legs(rsamd, k, m, link=None, n=64 << 20, fbytes=256 << 20, reps=12)
         if bound:
             out[key.replace("_GiBps", "_frac_of_link_bound")] = round(out[key] / bound, 4)
     out["host_jni_note"] = (f"jni/rs_jni_core.c over the mock JNIEnv (tests/jni_mock) and librsamd: Java byte[] "
-                            f"arrays ({k}+{m} x {n >> 20} MiB; a {fbytes >> 20} MiB file, 1000-B blocks), one library "
-                            f"call per Java call with the arrays movable (pinned only around the library's copy "
-                            f"batches, rs_set_relocator); {reps} calls timed per leg")
+                            f"arrays ({k}+{m} x {n >> 20} MiB; a {fbytes >> 20} MiB file, 1000-B blocks) on "
+                            f"{'transparent huge pages (a JVM run with -XX:+UseTransparentHugePages, INTEGRATION.md)' if huge else '4 KiB pages'}, "
+                            f"one library call per Java call with the arrays movable (pinned only around the "
+                            f"library's copy batches, rs_set_relocator); {reps} calls timed per leg")
+    mj.mock_hugepages(0)
     return out
 
 

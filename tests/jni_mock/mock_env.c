@@ -53,10 +53,17 @@ static mstate S;
 
 /* ---- objects (exported to the Python test) ---- */
 
+/* Java arrays' pages: 4 KiB (a JVM heap by default) or, with
+ * mock_hugepages(1), transparent huge pages (-XX:+UseTransparentHugePages). */
+static int huge_pages;
+void mock_hugepages(int on) { huge_pages = on; }
+
 static size_t map_bytes(int len) { return ((size_t)(len > 0 ? len : 1) + 4095) & ~(size_t)4095; }
 static uint8_t *alloc_data(int len) {  /* zeroed */
     void *p = mmap(NULL, map_bytes(len), PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-    return p == MAP_FAILED ? NULL : (uint8_t *)p;
+    if (p == MAP_FAILED) return NULL;
+    madvise(p, map_bytes(len), huge_pages ? MADV_HUGEPAGE : MADV_NOHUGEPAGE);
+    return (uint8_t *)p;
 }
 
 mobj *mock_new_bytes(int len) {

@@ -14,7 +14,7 @@ SIGNATURES = [
     ("mock_new_bytes", P, [C.c_int]), ("mock_new_bools", P, [C.c_int]), ("mock_new_objects", P, [C.c_int]),
     ("mock_set", None, [P, C.c_int, P]), ("mock_data", P, [P]), ("mock_reset", None, []),
     ("mock_fail_critical", None, [C.c_int]), ("mock_force_copy", None, [C.c_int]),
-    ("mock_moving", None, [C.c_int]), ("mock_moves", C.c_longlong, []),
+    ("mock_moving", None, [C.c_int]), ("mock_moves", C.c_longlong, []), ("mock_hugepages", None, [C.c_int]),
     ("mock_exc_class", C.c_char_p, []), ("mock_exc_message", C.c_char_p, []),
     ("mock_stats", None, [C.POINTER(C.c_longlong)]),
     ("mock_encode_parity", None, [C.c_int, P, P, C.c_int32, C.c_int32]),

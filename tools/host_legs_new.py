@@ -23,6 +23,8 @@ def main():
         extra.update(bench.host_small_calls(rsamd, 4, 2))
         extra.update(bench.host_groups_leg(rsamd, 4, 2, link))
         extra.update(bench.host_jni_legs(rsamd, 4, 2, link))
+        small = bench.host_jni_legs(rsamd, 4, 2, link, huge=0)  # the same on 4 KiB pages
+        extra.update({k.replace("host_jni_", "host_jni4k_"): v for k, v in small.items()})
         if "--inclusive" in sys.argv:
             extra.update(bench.host_inclusive(rsamd, 4, 2, link))
     extra["host_link"] = link
