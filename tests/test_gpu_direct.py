@@ -377,3 +377,45 @@ def test_host_buffer_shards_and_file(gpu, oracle_lib):
     assert np.array_equal(out.array, fbuf.array)
     for b in bufs + fsh + [fbuf, out]:
         b.free()
+
+
+def test_host_buffer_view_keeps_its_owner(gpu, oracle_lib):
+    """HostBuffer(n).array with the HostBuffer itself dropped: the view keeps
+    the pinned allocation alive (its base holds the owner), and the host
+    calls still code it in place."""
+    import gc
+    import rsamd
+    from rsamd.device import HostBuffer
+    k, m, n = 4, 2, 1 << 20
+    views = [HostBuffer(n).array for _ in range(k + m)]
+    gc.collect()
+    rng = np.random.default_rng(31)
+    for v in views[:k]:
+        v[:] = rng.integers(0, 256, n, dtype=np.uint8)
+    ref = [v.copy() for v in views[:k]] + [np.zeros(n, np.uint8) for _ in range(m)]
+    oracle_lib.Codec(k, m).encode_parity(ref, 0, n)
+    rsamd.ReedSolomon.create(k, m).encodeParity(views, 0, n)
+    assert all(np.array_equal(v, r) for v, r in zip(views, ref))
+    half = views[0][n // 2:]  # a slice keeps the owner alive too
+    del views
+    gc.collect()
+    assert np.array_equal(half, ref[0][n // 2:])
+
+
+def test_host_free_takes_only_live_allocations(gpu):
+    """rs_host_free: a foreign pointer, an interior one (a slice) and a second
+    free are RS_E_INVALID and free nothing; the allocation itself frees once."""
+    import ctypes as C
+    from rsamd import _lib
+    from rsamd.codec import RS_E_INVALID
+    lib = _lib.load()
+    p = C.c_void_p()
+    assert lib.rs_host_alloc(C.byref(p), 1 << 16) == 0
+    foreign = np.zeros(4096, np.uint8)
+    assert lib.rs_host_free(C.c_void_p(foreign.ctypes.data)) == RS_E_INVALID
+    assert "not a live rs_host_alloc buffer" in _lib.last_error()
+    assert lib.rs_host_free(C.c_void_p(p.value + 4096)) == RS_E_INVALID
+    C.memset(p, 0x5A, 1 << 16)  # still allocated and mapped
+    assert lib.rs_host_free(p) == 0
+    assert lib.rs_host_free(p) == RS_E_INVALID
+    assert lib.rs_host_free(None) == 0

@@ -400,3 +400,24 @@ def test_recover_groups_shard_major_direct_through_shim(gpu, oracle_lib, native,
         jvm.assert_clean()
     finally:
         native.rs_codec_destroy(h)
+
+
+def test_free_pinned_rejects_foreign_buffers(gpu, native, jvm):
+    """NativeReedSolomon.freePinned on a direct buffer the shim did not
+    allocate, on a slice of one, and twice: IllegalArgumentException each
+    time (rs_host_free's check), the real allocation freed exactly once."""
+    buf = jvm.lib.mock_alloc_pinned(1, 8192)
+    assert buf and jvm.exception() == ("", "")
+    jvm.lib.mock_drop_local()
+    other = np.zeros(4096, np.uint8)
+    jvm.lib.mock_free_pinned(1, jvm.direct(other))
+    assert jvm.exception() == ("java/lang/IllegalArgumentException", "rs_host_free: not a live rs_host_alloc buffer")
+    jvm.lib.mock_reset()
+    inner = jvm.lib.mock_new_direct(C.c_void_p(jvm.lib.mock_data(buf) + 4096), 4096)
+    jvm.lib.mock_free_pinned(1, inner)
+    assert jvm.exception()[0] == "java/lang/IllegalArgumentException"
+    jvm.lib.mock_reset()
+    jvm.lib.mock_free_pinned(1, buf)
+    assert jvm.exception() == ("", "")
+    jvm.lib.mock_free_pinned(1, buf)
+    assert jvm.exception()[0] == "java/lang/IllegalArgumentException"
