@@ -78,5 +78,26 @@ __device__ __forceinline__ void flag_mismatch(int *mismatch) {
 // (252 VGPRs and 2 waves per SIMD for the 10+4 verify kernel).
 __device__ __forceinline__ bool mismatch_seen(const int *mismatch) { return *RSAMD_G(mismatch, 4) != 0; }
 
+// A small host call's completion signal (kernels.hpp DirectSignal), after a
+// block's last store: the block's stores are made visible system-wide and it
+// counts itself done on `ctr`; the last block resets `ctr`, moves the verify
+// word (if any) into flag[1] and releases `seq` into flag[0].  Vector atomics
+// on global memory only.
+__device__ __forceinline__ void signal_done(uint32_t *flag, uint32_t *ctr, uint32_t seq, int *mismatch) {
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const uint32_t prev = __hip_atomic_fetch_add(RSAMD_G(ctr, 4), 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev + 1 != gridDim.x) return;
+    __hip_atomic_store(RSAMD_G(ctr, 4), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t mm = 0;
+    if (mismatch) {
+        mm = uint32_t(__hip_atomic_load(RSAMD_G(mismatch, 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        __hip_atomic_store(RSAMD_G(mismatch, 4), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __hip_atomic_store(RSAMD_G(flag + 1, 4), mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(RSAMD_G(flag, 4), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace dev
 }  // namespace rsamd

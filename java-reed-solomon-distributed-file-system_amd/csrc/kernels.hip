@@ -1181,19 +1181,7 @@ struct DirectArgs {
 
 // The completion signal (kernels.hpp DirectSignal), after a block's last store.
 __device__ __forceinline__ void signal_done(const DirectSignal &sg, int *mismatch) {
-    __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    const uint32_t prev = __hip_atomic_fetch_add(RSAMD_G(sg.ctr, 4), 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev + 1 != gridDim.x) return;
-    __hip_atomic_store(RSAMD_G(sg.ctr, 4), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t mm = 0;
-    if (mismatch) {
-        mm = uint32_t(__hip_atomic_load(RSAMD_G(mismatch, 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        __hip_atomic_store(RSAMD_G(mismatch, 4), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __hip_atomic_store(RSAMD_G(sg.flag + 1, 4), mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(RSAMD_G(sg.flag, 4), sg.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    dev::signal_done(sg.flag, sg.ctr, sg.seq, mismatch);
 }
 
 // The tee store of one 8-byte unit of data shard d at column c (unit-aligned,

@@ -853,6 +853,7 @@ __global__ void __launch_bounds__(kThreads) file_direct_encode_kernel(FileDirect
     const uint64_t step = uint64_t(gridDim.x) * kThreads;
     for (uint64_t u = uint64_t(blockIdx.x) * kThreads + threadIdx.x; u < a.units; u += step)
         file_direct_unit<M>(a, rotated_column(u, a));
+    if (a.sig.flag) signal_done(a.sig.flag, a.sig.ctr, a.sig.seq, nullptr);
 }
 
 // Tiled form: a workgroup takes tile_rows block rows, loads their file bytes
@@ -905,6 +906,7 @@ __global__ void __launch_bounds__(kThreads) file_direct_tiled_kernel(FileDirect 
                                             reinterpret_cast<uint64_t *>(RSAMD_G(a.out[a.k + p] + c, 8)));
         }
     }
+    if (a.sig.flag) signal_done(a.sig.flag, a.sig.ctr, a.sig.seq, nullptr);
 }
 
 // 128 x 256 threads.  256 MiB file, 4+2, GiB/s (tools/direct_file_probe.py,

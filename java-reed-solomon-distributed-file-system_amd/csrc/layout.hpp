@@ -60,6 +60,7 @@ struct FileDirect {
     int k = 0, nout = 0;
     uint64_t rot = 0;        // set by the launcher (layout.hip rotated_column)
     uint64_t tile_rows = 0;  // set by the launcher: block rows per workgroup of the tiled kernel
+    DirectSignal sig;        // sig.flag == nullptr: no completion signal (capi.cpp file_encode_zc_split)
 };
 bool file_direct_ok(const FileDirect &d);
 hipError_t launch_file_encode_direct(const FileDirect &d, hipStream_t s);

@@ -7,6 +7,9 @@
 //   lib_dec1000_05  the same, {0,5} absent
 //   lib_enc4k       rs_encode_parity 4+2 x 4 KiB
 //   lib_enc64k      rs_encode_parity 4+2 x 64 KiB
+//   lib_fencF, lib_fdecF_0, lib_fdecF_05
+//                   rs_file_encode / rs_file_decode ({0}, {0,5} absent) of an
+//                   F-byte file, 1000-byte blocks (the client's small files)
 // and the pieces such a call is made of, on this process's own stream:
 //   launch_only     hipLaunchKernelGGL of an empty kernel, no wait (host cost)
 //   empty_sync      empty kernel + hipStreamSynchronize
@@ -140,6 +143,36 @@ int main(int argc, char **argv) {
             std::fprintf(stderr, "library call failed: %s\n", rs_last_error_message());
             return 1;
         }
+    }
+    // the client's file calls on small files (1000-byte blocks): encode, and
+    // decode with {0} and {0,5} absent
+    for (size_t F : {size_t(90999), size_t(256) << 10, size_t(1) << 20}) {
+        const size_t blk = 1000, S = (F + 4 * blk - 1) / (4 * blk) * blk;
+        std::vector<uint8_t> file(F), back(F);
+        for (size_t b = 0; b < F; ++b) file[b] = uint8_t(b * 31 + (b >> 9));
+        std::vector<std::vector<uint8_t>> sh(6, std::vector<uint8_t>(S));
+        uint8_t *p[6];
+        int64_t lens[6];
+        for (int i = 0; i < 6; ++i) {
+            p[i] = sh[i].data();
+            lens[i] = int64_t(S);
+        }
+        int rc = 0;
+        const double e = median_us(reps / 4, [&] {
+            rc |= rs_file_encode(codec, file.data(), int64_t(F), int32_t(blk), p, 6, lens);
+        });
+        const uint8_t pres0[6] = {0, 1, 1, 1, 1, 1}, pres05[6] = {0, 1, 1, 1, 1, 0};
+        const double d0 = median_us(reps / 4, [&] {
+            rc |= rs_file_decode(codec, p, 6, lens, pres0, int32_t(S), int32_t(blk), back.data(), int64_t(F));
+        });
+        const double d05 = median_us(reps / 4, [&] {
+            rc |= rs_file_decode(codec, p, 6, lens, pres05, int32_t(S), int32_t(blk), back.data(), int64_t(F));
+        });
+        if (rc || back != file) {
+            std::fprintf(stderr, "file call failed or wrong: %s\n", rs_last_error_message());
+            return 1;
+        }
+        std::printf(", \"lib_fenc%zu\": %.2f, \"lib_fdec%zu_0\": %.2f, \"lib_fdec%zu_05\": %.2f", F, e, F, d0, F, d05);
     }
     rs_codec_destroy(codec);
     if (mode == "lib200") {
