@@ -23,7 +23,7 @@ from typing import Sequence
 import numpy as np
 
 from . import _lib
-from .codec import RS_E_INVALID, IllegalArgumentException, ReedSolomon, _bools, _Buffers, check
+from .codec import RS_E_INVALID, IllegalArgumentException, ReedSolomon, _bools, _Buffers, _flag_array, check
 from .device import _stream_handle
 
 BLOCK_SIZE = 1000         # ConfigVariables.BLOCK_SIZE
@@ -51,10 +51,10 @@ def file_layout(codec: ReedSolomon, file_len: int, block: int = BLOCK_SIZE):
 
 def file_encode_into(codec: ReedSolomon, file_data: np.ndarray, shards_out: Sequence, block: int = BLOCK_SIZE) -> None:
     """rs_file_encode into caller-provided shard buffers (no allocation)."""
-    src = file_data if len(file_data) else np.zeros(1, np.uint8)
+    src = _Buffers([file_data if len(file_data) else np.zeros(1, np.uint8)], writable=False)
     b = _Buffers(shards_out)
-    check(_lib.load().rs_file_encode(codec.handle, src.ctypes.data_as(_lib.u8p), len(file_data), block, b.ptrs,
-                                     len(shards_out), b.lens))
+    check(_lib.load().rs_file_encode(codec.handle, src.ptrs[0], len(file_data), block, b.ptrs, len(shards_out),
+                                     b.lens))
 
 
 def _is_path(x) -> bool:
@@ -130,9 +130,9 @@ def file_decode_into(codec: ReedSolomon, shards: Sequence, shardPresent: Sequenc
     if not (isinstance(file_out, np.ndarray) and file_out.dtype == np.uint8 and file_out.flags.c_contiguous):
         raise TypeError("file_out must be a C-contiguous uint8 numpy array")
     b = _Buffers(shards)
-    p = _bools(shardPresent)
-    check(_lib.load().rs_file_decode(codec.handle, b.ptrs, len(shards), b.lens, p.ctypes.data_as(_lib.u8p),
-                                     byteCntInShard, block, file_out.ctypes.data_as(_lib.u8p), len(file_out)))
+    out = _Buffers([file_out])
+    check(_lib.load().rs_file_decode(codec.handle, b.ptrs, len(shards), b.lens, _flag_array(shardPresent),
+                                     byteCntInShard, block, out.ptrs[0], len(file_out)))
 
 
 class ReedSolomonDecoder:
