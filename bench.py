@@ -484,6 +484,7 @@ def decode_summary(extra):
         "host_dec_1000B_us": g("host_dec_1000B_us"), "host_enc_4K_us": g("host_enc_4K_us"),
         "host_jni_dec_1000B_us": g("host_jni_dec_1000B_us"), "host_jni_enc_4K_us": g("host_jni_enc_4K_us"),
         "cpu_port_dec_1000B_us": g("cpu_port_dec_1000B_us"),
+        "host_file_enc_88K_us": g("host_file_enc_88K_us"), "host_file_dec05_88K_us": g("host_file_dec05_88K_us"),
         "host_enc_64K_us": g("host_enc_64K_us"), "host_enc_1M_us": g("host_enc_1024K_us"),
         "host_enc_4M_us": g("host_enc_4096K_us"),
         # N > 1: every rank calling the host API at once
@@ -1615,6 +1616,29 @@ def host_small_calls(rsamd, k, m, reps=2000):
         ok = ok and usj > 0 and all(np.array_equal(_mock_view(mj, o, S), b) for o, b in zip(arrs, want))
         out[f"host_{key}_us"] = round(us, 2)
         out[f"host_jni_{key}_us"] = round(usj, 2)
+    # the client's file calls on the reference's own fixture file (90,999 B,
+    # tests/golden/reference_test.txt; ClientCLI.java:177 -> ReedSolomonEncoder
+    # / ReedSolomonDecoder), 1000-B blocks: encode, and decode with {0,5} absent
+    blk = 1000
+    with open(os.path.join(ROOT, "tests", "golden", "reference_test.txt"), "rb") as f:
+        fdata = np.frombuffer(f.read(), np.uint8).copy()
+    fref = oc.file_encode(fdata.tobytes(), blk)
+    S = fref.shape[1]
+    fsh = [np.zeros(S, np.uint8) for _ in range(T)]
+    fptrs = (_lib.u8p * T)(*[a.ctypes.data_as(_lib.u8p) for a in fsh])
+    flens = (C.c_int64 * T)(*[S] * T)
+    fout = np.zeros(len(fdata), np.uint8)
+    src = fdata.ctypes.data_as(_lib.u8p)
+    us = mj.mock_time_capi_file(0, rs.handle, src, len(fdata), blk, fptrs, T, flens, None, None, reps)
+    ok = ok and us > 0 and np.array_equal(np.stack(fsh), fref)
+    out["host_file_enc_88K_us"] = round(us, 2)
+    fpres = np.array([0] + [1] * (T - 2) + [0], np.uint8)
+    fsh[0][:] = 0x3C
+    fsh[T - 1][:] = 0x3C
+    us = mj.mock_time_capi_file(1, rs.handle, src, len(fdata), blk, fptrs, T, flens,
+                                fpres.ctypes.data_as(_lib.u8p), fout.ctypes.data_as(_lib.u8p), reps)
+    ok = ok and us > 0 and np.array_equal(fout, fdata) and np.array_equal(np.stack(fsh), fref)
+    out["host_file_dec05_88K_us"] = round(us, 2)
     rate, n, el = cpu_rate(oc, k, m, 1000, [False] + [True] * (T - 1), 1, 1.0, 100_000)
     out["cpu_port_dec_1000B_us"] = round(k * 1000 / (rate * 2**30) * 1e6, 3)
     out["host_small_calls_bit_exact"] = bool(ok)
@@ -1622,6 +1646,8 @@ def host_small_calls(rsamd, k, m, reps=2000):
         f"{k}+{m}, one stripe per call, pageable host arrays; median of {reps} calls from C "
         f"(tests/jni_mock timing loops): host_* through the C-ABI, host_jni_* through jni/rs_jni_core.c over the "
         f"mock JNIEnv; the small-call pass is one signalled direct-kernel launch (DESIGN.md 5.2); "
+        f"host_file_*_88K_us: rs_file_encode / rs_file_decode {{0,5}} of the reference's 90,999-B fixture file, "
+        f"1000-B blocks; "
         f"cpu_port_dec_1000B_us: the oracle's scalar decodeMissing per 1000-B group, 1 thread, {n} groups in "
         f"{el:.1f} s")
     return out

@@ -638,3 +638,25 @@ double mock_time_capi(int kind, const rs_codec *c, uint8_t *const *sh, int n, co
     free(t);
     return m;
 }
+
+/* The client's file calls on a small file: kind 0 rs_file_encode (file ->
+ * shards), 1 rs_file_decode (shards with `present` -> out, byteCntInShard =
+ * the shard length). */
+double mock_time_capi_file(int kind, const rs_codec *c, const uint8_t *file, int64_t flen, int32_t block,
+                           uint8_t *const *sh, int n, const int64_t *lens, const uint8_t *present, uint8_t *out,
+                           int reps) {
+    double *t = (double *)malloc(sizeof(double) * (size_t)(reps > 0 ? reps : 1));
+    for (int i = -20; i < reps; i++) {
+        const double t0 = now_us();
+        const int rc = kind == 0 ? rs_file_encode(c, file, flen, block, sh, n, lens)
+                                 : rs_file_decode(c, sh, n, lens, present, (int32_t)lens[0], block, out, flen);
+        if (rc) {
+            free(t);
+            return -1.0;
+        }
+        if (i >= 0) t[i] = now_us() - t0;
+    }
+    const double m = median_of(t, reps);
+    free(t);
+    return m;
+}

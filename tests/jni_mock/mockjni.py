@@ -38,6 +38,7 @@ SIGNATURES = [
     ("mock_file_decode_direct", None, [C.c_int, P, P, P, C.c_int32, C.c_int32, P, C.c_int32]),
     ("mock_time_jni", C.c_double, [C.c_int, P, P, P, C.c_int32, C.c_int]),
     ("mock_time_capi", C.c_double, [C.c_int, P, P, C.c_int, P, P, C.c_int32, C.c_int]),
+    ("mock_time_capi_file", C.c_double, [C.c_int, P, P, C.c_int64, C.c_int32, P, C.c_int, P, P, P, C.c_int]),
 ]
 
 _lib = None

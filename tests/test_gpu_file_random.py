@@ -233,3 +233,33 @@ def test_file_pinned_two_launch_groups(gpu, oracle_lib, block):
     assert_same(views, list(ref), (k, m, block, n, miss))
     for b in sh + [f, out]:
         b.free()
+
+
+@pytest.mark.parametrize("block", [1000, 8, 520, 1])
+def test_file_small_pageable_two_launch_groups(gpu, oracle_lib, block):
+    """The small pageable file decode (capi.cpp file_decode_zc_split: the
+    survivors staged in the zero-copy buffer, padded to whole 16-byte vectors)
+    with a plan of two direct launches, the second signalling completion for
+    both (kernels.hpp DirectSignal), then the same file again with one launch.
+    Shard lengths that are and are not multiples of 16."""
+    from rsamd.layout import file_decode_into, file_encode_into, file_layout
+    import rsamd
+    k, m = 8, 6
+    rng = np.random.default_rng(7300 + block)
+    for n in (k * block * 37 + int(rng.integers(1, k * block + 1)), k * block * 5):
+        rs = rsamd.ReedSolomon.create(k, m)
+        oc = oracle_lib.Codec(k, m)
+        data = rng.integers(0, 256, n, dtype=np.uint8)
+        _, S = file_layout(rs, n, block)
+        sh = [np.zeros(S, np.uint8) for _ in range(k + m)]
+        file_encode_into(rs, data, sh, block)
+        ref = oc.file_encode(data.tobytes(), block)
+        assert_same(sh, list(ref), (block, n))
+        for miss in ([0, 2, 3, 5, 7, 9], [1, 12]):
+            for j in miss:
+                sh[j][:] = 0x5A
+            out = np.full(n + 64, 0x33, np.uint8)
+            file_decode_into(rs, sh, [i not in miss for i in range(k + m)], S, out[:n], block)
+            assert np.array_equal(out[:n], data), (block, n, miss)
+            assert (out[n:] == 0x33).all(), (block, n, miss)
+            assert_same(sh, list(ref), (block, n, miss))
