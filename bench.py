@@ -1831,10 +1831,25 @@ def config0_single_stripe(rsamd, k, m, S=64 << 10, reps=200):
 
     out["cfg0_gpu_host_api_decode_0_us"] = per_call_us(gpu_decode)
     out["cfg0_cpu_port_decode_0_us"] = per_call_us(cpu_decode)
-    out["cfg0_bit_exact"] = ok and all(np.array_equal(a, b) for a, b in zip(sh, ref)) and \
-        np.array_equal(sh[0], data[0])
+    ok = ok and all(np.array_equal(a, b) for a, b in zip(sh, ref)) and np.array_equal(sh[0], data[0])
+    # the same two calls from C (tests/jni_mock timing loops: median of 2000,
+    # no Python per call), the latency a JNI or C caller sees
+    import ctypes as C
+    from rsamd import _lib
+    mj = _mockjni()
+    T = k + m
+    ptrs = (_lib.u8p * T)(*[a.ctypes.data_as(_lib.u8p) for a in sh])
+    lens = (C.c_int64 * T)(*[S] * T)
+    pres = np.array([0] + [1] * (T - 1), np.uint8)
+    out["cfg0_gpu_capi_encode_us"] = round(mj.mock_time_capi(0, rs.handle, ptrs, T, lens, None, S, 2000), 2)
+    sh[0][:] = 0
+    out["cfg0_gpu_capi_decode_0_us"] = round(
+        mj.mock_time_capi(1, rs.handle, ptrs, T, lens, pres.ctypes.data_as(_lib.u8p), S, 2000), 2)
+    out["cfg0_bit_exact"] = bool(ok and out["cfg0_gpu_capi_encode_us"] > 0 and out["cfg0_gpu_capi_decode_0_us"] > 0
+                                 and all(np.array_equal(a, b) for a, b in zip(sh, ref)))
     out["cfg0_note"] = (f"one {k}+{m} stripe of {S >> 10} KiB shards per call, host buffers; GPU = host API "
-                        f"(H2D + kernel + D2H), CPU = oracle scalar port, 1 thread")
+                        f"(H2D + kernel + D2H) through the Python binding (cfg0_gpu_host_api_*) and from C "
+                        f"(cfg0_gpu_capi_*: median of 2000 calls), CPU = oracle scalar port, 1 thread")
     return out
 
 
