@@ -235,7 +235,7 @@ int run_small(ThreadCtx *ctx, const std::vector<DevPlan> &plans, int nslots, con
     if (rc) return rc;
     *taken = true;
     // host copies on this thread; the copy pool only above 2 MiB (as run_zero_copy)
-    const bool use_pool = bytes > (size_t(2) << 20);
+    const bool use_pool = bytes > zc_pool_min();
     std::vector<rsamd::CopyJob> jobs;
     auto copy = [&]() {
         if (use_pool)
@@ -727,7 +727,7 @@ int file_encode_zc_split(const Codec &c, const uint8_t *file, size_t file_len, s
         if (rc) return rc;
     }
     *taken = true;
-    const bool pool = need > (size_t(2) << 20);  // (as run_zero_copy: the pool's wake-up costs more below)
+    const bool pool = need > zc_pool_min();  // (as run_zero_copy: the pool's wake-up costs more below)
     auto copy = [&](const std::vector<rsamd::CopyJob> &jobs) {
         if (pool)
             rsamd::CopyPool::get().copy(jobs);
@@ -953,7 +953,7 @@ int file_decode_zc_split(const Codec &c, uint8_t *const *shards, const uint8_t *
     std::vector<rsamd::CopyJob> jobs;
     if (missing.empty()) {  // mergeShardsToFile alone
         merge_jobs(k, blk, file_out, file_size, src.data(), now, 0, rows_needed, &jobs);
-        if (file_size > (size_t(2) << 20))
+        if (file_size > zc_pool_min())
             rsamd::CopyPool::get().copy(jobs);
         else
             rsamd::CopyPool::copy_here(jobs);
@@ -972,7 +972,7 @@ int file_decode_zc_split(const Codec &c, uint8_t *const *shards, const uint8_t *
     rc = zero_copy_buffer(ctx, need);
     if (rc) return rc;
     *taken = true;
-    const bool pool = need > (size_t(2) << 20);  // (as run_zero_copy)
+    const bool pool = need > zc_pool_min();  // (as run_zero_copy)
     auto copy = [&](const std::vector<rsamd::CopyJob> &js) {
         if (pool)
             rsamd::CopyPool::get().copy(js);
@@ -1970,7 +1970,7 @@ int rs_file_decode(const rs_codec *codec, uint8_t *const *shards, int nshards, c
         const std::vector<bool> every(size_t(c->k()), true);
         std::vector<rsamd::CopyJob> jobs;
         merge_jobs(c->k(), size_t(block), file_out, size_t(file_size), src.data(), every, 0, size_t(S / block), &jobs);
-        if (file_size > (int64_t(2) << 20))
+        if (size_t(file_size) > zc_pool_min())
             rsamd::CopyPool::get().copy(jobs);
         else
             rsamd::CopyPool::copy_here(jobs);

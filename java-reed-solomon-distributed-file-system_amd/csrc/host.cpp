@@ -390,6 +390,13 @@ int run_chunks(ThreadCtx *ctx, size_t n_chunks, size_t buf_bytes, bool pinned, c
     return rc;
 }
 
+// Bytes above which a zero-copy pass's host copies go to the copy pool
+// (TUNING builds: RSAMD_ZC_POOL_MIN).
+size_t zc_pool_min() {
+    static const size_t v = tuning_size("RSAMD_ZC_POOL_MIN", size_t(2) << 20);
+    return v;
+}
+
 size_t zero_copy_limit() {
     static const size_t v = [] {
         const char *e = tuning_env("RSAMD_ZC_BYTES");
@@ -474,7 +481,7 @@ int run_zero_copy(ThreadCtx *ctx, size_t buf_bytes, const ChunkIo &io, const Chu
     // wake-up costs more than a small memcpy; TUNING builds: RSAMD_ZC_POOL_MIN).
     // (Streaming stores on the calling thread instead of memcpy: no better,
     // profiles/r5/host_sizes_r5v.txt.)
-    const bool use_pool = buf_bytes > tuning_size("RSAMD_ZC_POOL_MIN", size_t(2) << 20);
+    const bool use_pool = buf_bytes > zc_pool_min();
     auto copy = [&](const std::vector<rsamd::CopyJob> &jobs) {
         if (use_pool)
             rsamd::CopyPool::get().copy(jobs);

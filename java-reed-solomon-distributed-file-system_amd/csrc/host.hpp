@@ -102,6 +102,9 @@ int grow_pinned(uint8_t **buf, size_t *cap, size_t want);
 int zero_copy_buffer(ThreadCtx *ctx, size_t buf_bytes);
 // Largest staging buffer of a single zero-copy pass.
 size_t zero_copy_limit();
+// Bytes above which a zero-copy pass copies with the copy pool (below, on the
+// calling thread: the pool's hand-off costs more than a small memcpy).
+size_t zc_pool_min();
 
 // ---- small calls' completion signal ---------------------------------------
 constexpr size_t kSignalCtr = 16;  // int index into ThreadCtx::flag of the block counter
