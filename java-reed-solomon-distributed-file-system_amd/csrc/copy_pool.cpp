@@ -258,23 +258,13 @@ CopyPool &CopyPool::get() {
     return *pool;
 }
 
-// An idle thread (a worker with nothing queued, a caller waiting for its
-// batch's last pieces) polls for this long before it sleeps on a condition
-// variable: the mirrored pipeline hands the pool a batch per chunk, and a
-// sleeping thread's wake-up costs more than a small chunk's copy.  4+2
+// spin_us_: an idle thread (a worker with nothing to claim, a caller waiting
+// for its batch's last pieces) polls for this long before it sleeps (a
+// caller: yields): the mirrored pipeline hands the pool a batch per chunk, and
+// a sleeping thread's wake-up costs more than a small chunk's copy.  4+2
 // pageable encodeParity per call, 0 -> 50 us (profiles/r5/host_sizes_r5v.txt):
 // 1 MiB shards 309-378 -> 235-269 us, 2 MiB 465-547 -> 354-394, 4 MiB
 // 620-656 -> 556-567; 200 us is no better (TUNING builds: RSAMD_POOL_SPIN_US).
-template <class Ready>
-void spin_until(int us, Ready ready) {
-    if (us <= 0) return;
-    const auto end = std::chrono::steady_clock::now() + std::chrono::microseconds(us);
-    while (!ready()) {
-        for (int i = 0; i < 32; ++i) _mm_pause();
-        if (std::chrono::steady_clock::now() > end) return;
-    }
-}
-
 CopyPool::CopyPool(int n) {
     spin_us_ = int(tuning_size("RSAMD_POOL_SPIN_US", 50));
     for (int i = 0; i < n; ++i) {
@@ -283,18 +273,55 @@ CopyPool::CopyPool(int n) {
     }
 }
 
+// Claims and copies pieces of slot s's batch while any are left; true if it
+// copied one.  A worker holds a reference while it may touch the slot's
+// batch, so the batch's owner returns (and its pieces go) only after every
+// claimant has let go; the slots themselves live as long as the pool.
+bool CopyPool::work_on(Slot &s) {
+    if (s.state.load(std::memory_order_acquire) != kActive) return false;
+    s.refs.fetch_add(1, std::memory_order_acq_rel);
+    bool did = false;
+    if (s.state.load(std::memory_order_acquire) == kActive) {
+        for (;;) {
+            const size_t i = s.next.fetch_add(1, std::memory_order_acq_rel);
+            if (i >= s.n) break;
+            copy_piece(s.pieces[i]);
+            s.done.fetch_add(1, std::memory_order_acq_rel);
+            did = true;
+        }
+    }
+    s.refs.fetch_sub(1, std::memory_order_acq_rel);
+    return did;
+}
+
+// Workers poll the slots; one sleeps only after spin_us_ of continuous
+// idleness, and a caller posting a batch wakes the sleepers.  Pieces are
+// claimed with an atomic counter, not under a lock: with a mutex-guarded queue
+// the 15 workers polling for a batch met at the mutex, and a small batch cost
+// 17 us more through the pool than on the calling thread alone (4 x 64 KiB;
+// tools/pool_batch_probe.cpp, profiles/r6/pool_probe_r6y.txt).
 void CopyPool::run() {
+    using clock = std::chrono::steady_clock;
+    auto idle_since = clock::now();
     for (;;) {
-        spin_until(spin_us_, [this] { return queued_.load(std::memory_order_acquire) != 0; });
+        bool did = false;
+        for (Slot &s : slots_) did = work_on(s) || did;
+        if (did) {
+            idle_since = clock::now();
+            continue;
+        }
+        if (clock::now() - idle_since < std::chrono::microseconds(spin_us_)) {
+            for (int i = 0; i < 32; ++i) _mm_pause();
+            continue;
+        }
         std::unique_lock<std::mutex> lock(mu_);
-        work_cv_.wait(lock, [this] { return !queue_.empty(); });
-        Piece p = queue_.front();
-        queue_.pop_front();
-        queued_.fetch_sub(1, std::memory_order_relaxed);
-        lock.unlock();
-        copy_piece(p.job);
-        lock.lock();
-        if (p.pending->fetch_sub(1, std::memory_order_acq_rel) == 1) done_cv_.notify_all();
+        const uint64_t seen = posted_.load(std::memory_order_seq_cst);
+        sleepers_.fetch_add(1, std::memory_order_seq_cst);
+        bool any = false;
+        for (Slot &s : slots_) any = any || s.state.load(std::memory_order_seq_cst) == kActive;
+        if (!any) work_cv_.wait(lock, [&] { return posted_.load(std::memory_order_seq_cst) != seen; });
+        sleepers_.fetch_sub(1, std::memory_order_seq_cst);
+        idle_since = clock::now();
     }
 }
 
@@ -303,56 +330,66 @@ void CopyPool::copy(const std::vector<CopyJob> &jobs) {
 }
 
 void CopyPool::copy_batch(const std::vector<CopyJob> &jobs) {
-    std::atomic<size_t> pending{0};
-    {
-        std::lock_guard<std::mutex> lock(mu_);
-        for (const CopyJob &j : jobs) {
-            if (j.n == 0 || j.rows == 0) continue;
-            const uint8_t *src = static_cast<const uint8_t *>(j.src);
-            uint8_t *dst = static_cast<uint8_t *>(j.dst);
-            uint8_t *dst2 = static_cast<uint8_t *>(j.dst2);
-            if (j.rows == 1) {
-                for (size_t off = 0; off < j.n; off += kPiece) {
-                    CopyJob piece{dst + off, src ? src + off : nullptr, std::min(kPiece, j.n - off)};
-                    piece.dst2 = dst2 ? dst2 + off : nullptr;
-                    queue_.push_back({piece, &pending});
-                    pending.fetch_add(1, std::memory_order_relaxed);
-                }
-                continue;
+    std::vector<CopyJob> pieces;
+    for (const CopyJob &j : jobs) {
+        if (j.n == 0 || j.rows == 0) continue;
+        const uint8_t *src = static_cast<const uint8_t *>(j.src);
+        uint8_t *dst = static_cast<uint8_t *>(j.dst);
+        uint8_t *dst2 = static_cast<uint8_t *>(j.dst2);
+        if (j.rows == 1) {
+            for (size_t off = 0; off < j.n; off += kPiece) {
+                CopyJob piece{dst + off, src ? src + off : nullptr, std::min(kPiece, j.n - off)};
+                piece.dst2 = dst2 ? dst2 + off : nullptr;
+                pieces.push_back(piece);
             }
-            // rows: pieces of about kPiece bytes of whole rows
-            const size_t per = std::max<size_t>(1, kPiece / j.n);
-            for (size_t r = 0; r < j.rows; r += per) {
-                CopyJob piece{dst + r * j.dst_stride, src ? src + r * j.src_stride : nullptr, j.n,
-                              std::min(per, j.rows - r), j.dst_stride, j.src_stride,
-                              dst2 ? dst2 + r * j.dst2_stride : nullptr, j.dst2_stride};
-                queue_.push_back({piece, &pending});
-                pending.fetch_add(1, std::memory_order_relaxed);
-            }
-        }
-        queued_.store(queue_.size(), std::memory_order_release);
-    }
-    if (pending.load(std::memory_order_relaxed) == 0) return;
-    work_cv_.notify_all();
-    // The caller works too: take this batch's pieces (or anyone's) until the
-    // queue is empty, then wait for the pieces still being copied.
-    std::unique_lock<std::mutex> lock(mu_);
-    while (pending.load(std::memory_order_acquire) > 0) {
-        if (!queue_.empty()) {
-            Piece p = queue_.front();
-            queue_.pop_front();
-            queued_.fetch_sub(1, std::memory_order_relaxed);
-            lock.unlock();
-            copy_piece(p.job);
-            lock.lock();
-            if (p.pending->fetch_sub(1, std::memory_order_acq_rel) == 1) done_cv_.notify_all();
             continue;
         }
-        lock.unlock();
-        spin_until(spin_us_, [&] { return pending.load(std::memory_order_acquire) == 0; });
-        lock.lock();
-        done_cv_.wait(lock, [&] { return pending.load(std::memory_order_acquire) == 0 || !queue_.empty(); });
+        // rows: pieces of about kPiece bytes of whole rows
+        const size_t per = std::max<size_t>(1, kPiece / j.n);
+        for (size_t r = 0; r < j.rows; r += per)
+            pieces.push_back({dst + r * j.dst_stride, src ? src + r * j.src_stride : nullptr, j.n,
+                              std::min(per, j.rows - r), j.dst_stride, j.src_stride,
+                              dst2 ? dst2 + r * j.dst2_stride : nullptr, j.dst2_stride});
     }
+    if (pieces.empty()) return;
+    // A free slot (every slot taken by other callers' batches: this thread copies alone)
+    Slot *slot = nullptr;
+    for (Slot &s : slots_) {
+        uint32_t free = kFree;
+        if (s.state.compare_exchange_strong(free, kFilling, std::memory_order_acq_rel)) {
+            slot = &s;
+            break;
+        }
+    }
+    if (!slot || pieces.size() == 1) {
+        if (slot) slot->state.store(kFree, std::memory_order_release);
+        for (const CopyJob &p : pieces) copy_piece(p);
+        return;
+    }
+    slot->pieces = pieces.data();
+    slot->n = pieces.size();
+    slot->next.store(0, std::memory_order_relaxed);
+    slot->done.store(0, std::memory_order_relaxed);
+    slot->state.store(kActive, std::memory_order_seq_cst);
+    posted_.fetch_add(1, std::memory_order_seq_cst);
+    if (sleepers_.load(std::memory_order_seq_cst) > 0) {
+        { std::lock_guard<std::mutex> lock(mu_); }
+        work_cv_.notify_all();
+    }
+    // The caller works too, then waits for the pieces others still copy.
+    work_on(*slot);
+    const auto t0 = std::chrono::steady_clock::now();
+    while (slot->done.load(std::memory_order_acquire) < slot->n) {
+        if (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(spin_us_))
+            for (int i = 0; i < 32; ++i) _mm_pause();
+        else
+            std::this_thread::yield();
+    }
+    // Retire the batch: no new claimant after this, and the last one gone
+    // before the pieces (this frame's vector) go.
+    slot->state.store(kDraining, std::memory_order_seq_cst);
+    while (slot->refs.load(std::memory_order_acquire) != 0) _mm_pause();
+    slot->state.store(kFree, std::memory_order_release);
 }
 
 }  // namespace rsamd

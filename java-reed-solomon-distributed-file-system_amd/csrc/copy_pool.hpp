@@ -80,15 +80,26 @@ private:
     void run();
     void copy_batch(const std::vector<CopyJob> &jobs);
 
-    struct Piece {
-        CopyJob job;
-        std::atomic<size_t> *pending;  // the batch's counter (decremented under mu_)
+    // One posted batch: its pieces (the caller's), claimed one at a time by
+    // an atomic counter.  kSlots batches (callers) at once; a caller that
+    // finds none free copies alone.
+    enum : uint32_t { kFree = 0, kFilling = 1, kActive = 2, kDraining = 3 };
+    struct Slot {
+        std::atomic<uint32_t> state{kFree};
+        const CopyJob *pieces = nullptr;
+        size_t n = 0;
+        std::atomic<size_t> next{0}, done{0};
+        std::atomic<int> refs{0};  // threads that may touch the batch
     };
-    std::mutex mu_;
-    std::condition_variable work_cv_, done_cv_;
-    std::deque<Piece> queue_;
-    std::atomic<size_t> queued_{0};  // queue_.size(), readable without mu_ (the spinners poll it)
-    int spin_us_ = 0;                // how long an idle thread polls before it sleeps
+    static constexpr int kSlots = 16;
+    bool work_on(Slot &s);
+
+    Slot slots_[kSlots];
+    std::atomic<uint64_t> posted_{0};  // batches posted so far (a sleeper's wake-up condition)
+    std::atomic<int> sleepers_{0};
+    std::mutex mu_;                    // sleeping workers only
+    std::condition_variable work_cv_;
+    int spin_us_ = 0;                  // how long an idle thread polls before it sleeps
     std::vector<std::thread> threads_;
 };
 

@@ -4,7 +4,8 @@
 // tee into the pinned slots), random row lengths, strides and alignments;
 // every byte is compared with a plain copy and nothing past the destination
 // may be written.  Then several threads hand the pool batches at once (the
-// process-wide pool serves every concurrent call), each batch checked.  Built
+// process-wide pool serves every concurrent call), more of them than it has
+// batch slots, each batch checked.  Built
 // and run by tests/test_copy_pool.py, with and without idle spinning.
 #include "copy_pool.hpp"
 #include <atomic>
@@ -61,13 +62,16 @@ int main() {  // copy_pool.cpp gathers, tees, zero fills: every byte against a p
             if (r + 1 < rows && d2stride > n && dst2[d2off + r * d2stride + n] != 0xDD) { ++bad; printf("tee gap n=%zu\n", n); break; }
         }
     }
-    // concurrent callers: 6 threads x 300 batches of 1-6 jobs, 1 B to 3 MiB each
+    // concurrent callers: 6 threads x 300 batches of 1-6 jobs, 1 B to 3 MiB
+    // each; then 24 threads x 60 batches, more callers than the pool has batch
+    // slots (those copy alone)
     std::atomic<int> cbad{0}, ccases{0};
+    for (const int nt : {6, 24}) {
     std::vector<std::thread> ts;
-    for (int t = 0; t < 6; ++t)
-        ts.emplace_back([&, t] {
-            std::mt19937_64 r(100 + t);
-            for (int it = 0; it < 300; ++it) {
+    for (int t = 0; t < nt; ++t)
+        ts.emplace_back([&, t, nt] {
+            std::mt19937_64 r(100 + t + 1000 * nt);
+            for (int it = 0; it < (nt == 6 ? 300 : 60); ++it) {
                 const int nj = 1 + int(r() % 6);
                 std::vector<std::vector<uint8_t>> srcs(nj), dsts(nj);
                 std::vector<rsamd::CopyJob> jobs;
@@ -85,6 +89,7 @@ int main() {  // copy_pool.cpp gathers, tees, zero fills: every byte against a p
             }
         });
     for (auto &th : ts) th.join();
+    }
     printf("%d concurrent batches, %d bad\n", ccases.load(), cbad.load());
     bad += cbad.load();
     printf("%d cases, %d bad\n", cases, bad);
