@@ -2020,7 +2020,9 @@ hipError_t launch_gf(const Geometry &g, const DevPlan &p, Mode mode, int *mismat
 namespace {
 template <int W, int M>
 void launch_direct_t(const DirectArgs &a, unsigned grid, Mode mode, hipStream_t s) {
-    const bool pre = a.sig.flag != nullptr;  // small calls (signalled)
+    // small calls (signalled); TUNING builds: RSAMD_DIRECT_PRE=0 keeps the streaming form (A/B)
+    static const bool pre_on = tuning_size("RSAMD_DIRECT_PRE", 1) != 0;
+    const bool pre = a.sig.flag != nullptr && pre_on;
     if (mode == Mode::Verify && pre)
         hipLaunchKernelGGL((gf_direct_kernel<W, M, true, false, true>), dim3(grid), dim3(kThreads), 0, s, a);
     else if (mode == Mode::Verify)

@@ -21,6 +21,7 @@
 //   xor_flag_S      the same, the kernel's last block storing the flag
 //   graph_sync      the xor kernel as a one-node hipGraph + hipStreamSynchronize
 // argv[1] == "spin": hipSetDeviceFlags(hipDeviceScheduleSpin) first.
+// SL_SIZES=a,b,... replaces the encode / verify shard sizes 4096 and 65536.
 // argv[1] == "lib200": only 200 calls of each library call (for a rocprofv3
 // --kernel-trace --memory-copy-trace --hip-runtime-trace of exactly those).
 //
@@ -112,7 +113,19 @@ int main(int argc, char **argv) {
     // ---- library calls -------------------------------------------------------
     rs_codec *codec = nullptr;
     if (rs_codec_create(4, 2, &codec)) return 1;
-    for (size_t S : {size_t(1000), size_t(4096), size_t(65536)}) {
+    // SL_SIZES=a,b,...: the encode / verify shard sizes instead of 4096 and 65536
+    std::vector<size_t> sizes{1000, 4096, 65536};
+    if (const char *e = std::getenv("SL_SIZES")) {
+        sizes.assign(1, 1000);
+        for (const char *p = e; *p;) {
+            char *end = nullptr;
+            const size_t v = std::strtoull(p, &end, 10);
+            if (end == p) break;
+            if (v && v != 1000) sizes.push_back(v);
+            p = *end == ',' ? end + 1 : end;
+        }
+    }
+    for (size_t S : sizes) {
         std::vector<std::vector<uint8_t>> sh(6, std::vector<uint8_t>(S));
         for (int i = 0; i < 6; ++i)
             for (size_t b = 0; b < S; ++b) sh[i][b] = uint8_t(b * 7 + i * 13 + (b >> 8));
