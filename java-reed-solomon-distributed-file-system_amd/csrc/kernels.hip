@@ -2019,10 +2019,7 @@ hipError_t launch_gf(const Geometry &g, const DevPlan &p, Mode mode, int *mismat
 
 namespace {
 template <int W, int M>
-void launch_direct_t(const DirectArgs &a, unsigned grid, Mode mode, hipStream_t s) {
-    // small calls (signalled); TUNING builds: RSAMD_DIRECT_PRE=0 keeps the streaming form (A/B)
-    static const bool pre_on = tuning_size("RSAMD_DIRECT_PRE", 1) != 0;
-    const bool pre = a.sig.flag != nullptr && pre_on;
+void launch_direct_t(const DirectArgs &a, unsigned grid, Mode mode, bool pre, hipStream_t s) {
     if (mode == Mode::Verify && pre)
         hipLaunchKernelGGL((gf_direct_kernel<W, M, true, false, true>), dim3(grid), dim3(kThreads), 0, s, a);
     else if (mode == Mode::Verify)
@@ -2035,12 +2032,12 @@ void launch_direct_t(const DirectArgs &a, unsigned grid, Mode mode, hipStream_t 
         hipLaunchKernelGGL((gf_direct_kernel<W, M, false, false, false>), dim3(grid), dim3(kThreads), 0, s, a);
 }
 template <int W>
-hipError_t dispatch_direct(const DirectArgs &a, int nout, unsigned grid, Mode mode, hipStream_t s) {
+hipError_t dispatch_direct(const DirectArgs &a, int nout, unsigned grid, Mode mode, bool pre, hipStream_t s) {
     switch (nout) {
-    case 1: launch_direct_t<W, 1>(a, grid, mode, s); break;
-    case 2: launch_direct_t<W, 2>(a, grid, mode, s); break;
-    case 3: launch_direct_t<W, 3>(a, grid, mode, s); break;
-    case 4: launch_direct_t<W, 4>(a, grid, mode, s); break;
+    case 1: launch_direct_t<W, 1>(a, grid, mode, pre, s); break;
+    case 2: launch_direct_t<W, 2>(a, grid, mode, pre, s); break;
+    case 3: launch_direct_t<W, 3>(a, grid, mode, pre, s); break;
+    case 4: launch_direct_t<W, 4>(a, grid, mode, pre, s); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -2105,7 +2102,17 @@ hipError_t launch_gf_direct(const DirectPlan &p, size_t n, Mode mode, int *misma
     if (sig) a.sig = *sig;
     const uint64_t blocks = tuning_size("RSAMD_DIRECT_BLOCKS", kDirectBlocks);  // per call in TUNING builds
     const unsigned grid = unsigned(std::max<uint64_t>(1, std::min<uint64_t>(blocks, (a.nvec + kThreads - 1) / kThreads)));
-    return W == 16 ? dispatch_direct<16>(a, p.nout, grid, mode, s) : dispatch_direct<8>(a, p.nout, grid, mode, s);
+    // The PRE form (inputs loaded eight at a time) for signalled launches of
+    // small shards; from 512 KiB the streaming form is as fast or faster
+    // (4+2 encode kernel, 1 MiB shards: 131 against 145 us; 256 KiB 39.8 /
+    // 39.0; 64 KiB and less PRE 2-5 us faster; profiles/r6/
+    // zc_mid_kernels_r6af_r6ag.txt).  Whole calls, PRE at every size / only
+    // up to 256 KiB: 512 KiB encode 139-154 / 135-136 us, 768 KiB 198-213 /
+    // 194-196 (pre_max_ab_r6ao.txt).  TUNING builds: RSAMD_DIRECT_PRE_MAX.
+    static const uint64_t pre_max = tuning_size("RSAMD_DIRECT_PRE_MAX", uint64_t(256) << 10);
+    const bool pre = sig && n <= pre_max;
+    return W == 16 ? dispatch_direct<16>(a, p.nout, grid, mode, pre, s)
+                   : dispatch_direct<8>(a, p.nout, grid, mode, pre, s);
 }
 
 hipError_t launch_fill_synthetic(uint8_t *base, int k, size_t n_stripes, size_t shard_len, size_t shard_stride,
