@@ -2101,7 +2101,7 @@ hipError_t launch_gf_direct(const DirectPlan &p, size_t n, Mode mode, int *misma
     if (tee) a.tee = *tee;  // (head % 8 == 0: in[0] is 8-byte aligned and align >= 8)
     if (sig) a.sig = *sig;
     const uint64_t blocks = tuning_size("RSAMD_DIRECT_BLOCKS", kDirectBlocks);  // per call in TUNING builds
-    const unsigned grid = unsigned(std::max<uint64_t>(1, std::min<uint64_t>(blocks, (a.nvec + kThreads - 1) / kThreads)));
+    unsigned grid = unsigned(std::max<uint64_t>(1, std::min<uint64_t>(blocks, (a.nvec + kThreads - 1) / kThreads)));
     // The PRE form (inputs loaded eight at a time) for signalled launches of
     // small shards; from 512 KiB the streaming form is as fast or faster
     // (4+2 encode kernel, 1 MiB shards: 131 against 145 us; 256 KiB 39.8 /
@@ -2111,6 +2111,19 @@ hipError_t launch_gf_direct(const DirectPlan &p, size_t n, Mode mode, int *misma
     // 194-196 (pre_max_ab_r6ao.txt).  TUNING builds: RSAMD_DIRECT_PRE_MAX.
     static const uint64_t pre_max = tuning_size("RSAMD_DIRECT_PRE_MAX", uint64_t(256) << 10);
     const bool pre = sig && n <= pre_max;
+    // The streaming form in mid-size launches: a thread that codes one vector
+    // loads, codes and stores once, so a launch's reads all come before its
+    // writes and the link's two directions take turns; with several vectors
+    // per thread one vector's stores overlap the next one's loads.  At least
+    // kDirectIters vectors per thread (not under 32 workgroups): 4+2 x 1 MiB
+    // shards, 16 / 32 / 64 / 128 / 256 workgroups: 129 / 112 / 116 / 114 /
+    // 131 us per kernel (profiles/r6/direct_grid_r6at.txt).  Large launches
+    // keep 256 (kDirectBlocks).  TUNING builds: RSAMD_DIRECT_ITERS (1: off).
+    static const uint64_t iters = std::max<uint64_t>(1, tuning_size("RSAMD_DIRECT_ITERS", 8));
+    if (!pre && iters > 1) {
+        const uint64_t want = (a.nvec + kThreads * iters - 1) / (kThreads * iters);
+        grid = unsigned(std::min<uint64_t>(grid, std::max<uint64_t>(want, 32)));
+    }
     return W == 16 ? dispatch_direct<16>(a, p.nout, grid, mode, pre, s)
                    : dispatch_direct<8>(a, p.nout, grid, mode, pre, s);
 }
