@@ -222,16 +222,41 @@ int run_small(ThreadCtx *ctx, const std::vector<DevPlan> &plans, int nslots, con
               int *result, bool *taken) {
     *taken = false;
     if (plans.size() != 1 || count == 0 || !small_signal_enabled()) return RS_OK;
-    const size_t ss = round_up(count, 256), bytes = ss * size_t(nslots);
+    // The kernel codes whole 16-byte vectors: each slot's bytes past `count`
+    // up to the next 16 are zeroed (0 codes to 0, so a verify compares them
+    // equal) and coded too, no byte tail in the launch (at 1000-byte shards
+    // the tail's per-input byte loads cost several link round trips).
+    const size_t n16 = round_up(count, 16);
+    // From 128 KiB per shard a coding call runs as two launches over two
+    // column ranges, each signalling: the second range's copy-in overlaps the
+    // first range's kernel, the first range's copy-out the second's.  4+2
+    // encodeParity per call, from C (profiles/r6/small_parts_ab_r6ay.txt):
+    // 256 KiB 77 -> 64 us, 512 KiB 130-137 -> 113-117, 768 KiB 171-198 -> 141-148.
+    // The cut is on a page boundary: cuts inside a page (the CPU copying into
+    // the page whose other half the GPU is reading) made each later launch
+    // 25-50 us slower.  Three or four ranges are no better than two; a verify
+    // stays one launch (one mismatch word per launch).  TUNING builds:
+    // RSAMD_SMALL_PARTS, RSAMD_SMALL_PARTS_MIN, RSAMD_SMALL_PARTS_ALIGN.
+    static const size_t parts_want = std::max<size_t>(1, rsamd::tuning_size("RSAMD_SMALL_PARTS", 2));
+    static const size_t parts_min = rsamd::tuning_size("RSAMD_SMALL_PARTS_MIN", size_t(128) << 10);
+    const size_t parts = mode == Mode::Code && count >= parts_min ? std::min<size_t>(parts_want, 8) : 1;
+    static const size_t cut_align = std::max<size_t>(256, rsamd::tuning_size("RSAMD_SMALL_PARTS_ALIGN", 4096));
+    std::vector<size_t> cut(parts + 1, n16);
+    cut[0] = 0;
+    for (size_t j = 1; j < parts; ++j) cut[j] = std::min(n16, round_up(n16 * j / parts, cut_align));
+    // (split: the slots on page boundaries too, so no page holds bytes of two ranges)
+    const size_t ss = round_up(count, parts > 1 ? cut_align : 256), bytes = ss * size_t(nslots);
     if (bytes > zero_copy_limit()) return RS_OK;
     int rc = zero_copy_buffer(ctx, bytes);
     if (rc) return rc;
     std::vector<rsamd::DirectPlan> dp;
     if (!direct_plans(plans, in_slots, out_slots, [&](int sl) { return ctx->zc_dev + size_t(sl) * ss; }, &dp))
         return RS_OK;
-    rsamd::DirectSignal sg;
-    rc = next_signal(ctx, &sg.flag, &sg.ctr, &sg.seq);
-    if (rc) return rc;
+    std::vector<rsamd::DirectSignal> sg(parts);
+    for (rsamd::DirectSignal &g : sg) {
+        rc = next_signal(ctx, &g.flag, &g.ctr, &g.seq);
+        if (rc) return rc;
+    }
     *taken = true;
     // host copies on this thread; the copy pool only above 2 MiB (as run_zero_copy)
     const bool use_pool = bytes > zc_pool_min();
@@ -243,36 +268,44 @@ int run_small(ThreadCtx *ctx, const std::vector<DevPlan> &plans, int nslots, con
             rsamd::CopyPool::copy_here(jobs);
         jobs.clear();
     };
-    // The kernel codes whole 16-byte vectors: each slot's bytes past `count`
-    // up to the next 16 are zeroed (0 codes to 0, so a verify compares them
-    // equal) and coded too, no byte tail in the launch (at 1000-byte shards
-    // the tail's per-input byte loads cost several link round trips).
-    const size_t n16 = round_up(count, 16);
-    for (int s : in_slots) {
-        jobs.push_back({ctx->zc + size_t(s) * ss, host[s] + offset, count});
-        if (n16 > count) std::memset(ctx->zc + size_t(s) * ss + count, 0, n16 - count);
-    }
-    copy();
     const rsamd::DirectPlan &d = dp[0];
     for (int i = 0; i < d.nin; ++i) bounds::allow(d.in[i], n16);
     for (int q = 0; q < d.nout; ++q) bounds::allow(d.out[q], n16);
-    const hipError_t e = rsamd::launch_gf_direct(d, n16, mode, ctx->flag, ctx->stream, nullptr, &sg);
-    if (e != hipSuccess) {
-        (void)hipStreamSynchronize(ctx->stream);
-        return hip_fail(e, "launch_gf_direct (small call)");
+    for (size_t j = 0; j < parts; ++j) {
+        const size_t lo = cut[j], hi = cut[j + 1];
+        if (lo == hi) continue;
+        const size_t end = std::min(hi, count);
+        for (int s : in_slots) {
+            if (end > lo) jobs.push_back({ctx->zc + size_t(s) * ss + lo, host[s] + offset + lo, end - lo});
+            if (hi > count) std::memset(ctx->zc + size_t(s) * ss + count, 0, hi - count);
+        }
+        copy();
+        rsamd::DirectPlan dj = d;
+        for (int i = 0; i < dj.nin; ++i) dj.in[i] += lo;
+        for (int q = 0; q < dj.nout; ++q) dj.out[q] += lo;
+        const hipError_t e = rsamd::launch_gf_direct(dj, hi - lo, mode, ctx->flag, ctx->stream, nullptr, &sg[j]);
+        if (e != hipSuccess) {
+            (void)hipStreamSynchronize(ctx->stream);
+            return hip_fail(e, "launch_gf_direct (small call)");
+        }
     }
-    uint32_t mm = 0;
-    rc = wait_signal(ctx, sg.seq, &mm);
-    if (rc) {
-        (void)hipStreamSynchronize(ctx->stream);
-        return rc;
+    for (size_t j = 0; j < parts; ++j) {
+        const size_t lo = cut[j], end = std::min(cut[j + 1], count);
+        if (cut[j] == cut[j + 1]) continue;
+        uint32_t mm = 0;
+        rc = wait_signal(ctx, sg[j].seq, &mm);
+        if (rc) {
+            (void)hipStreamSynchronize(ctx->stream);
+            return rc;
+        }
+        if (mode == Mode::Verify) {
+            *result = mm ? 0 : 1;
+            return RS_OK;
+        }
+        if (end > lo)
+            for (int s : out_slots) jobs.push_back({host[s] + offset + lo, ctx->zc + size_t(s) * ss + lo, end - lo});
+        copy();
     }
-    if (mode == Mode::Verify) {
-        *result = mm ? 0 : 1;
-        return RS_OK;
-    }
-    for (int s : out_slots) jobs.push_back({host[s] + offset, ctx->zc + size_t(s) * ss, count});
-    copy();
     return RS_OK;
 }
 

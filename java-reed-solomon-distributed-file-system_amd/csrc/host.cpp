@@ -443,17 +443,21 @@ int wait_signal(ThreadCtx *ctx, uint32_t seq, uint32_t *mismatch) {
     // the stream's own completion costs ~3 us more to observe.
     // Past 100 us the stream is asked now and then whether it failed or went
     // idle without the signal.
+    // A later launch of the same stream may already have signalled past seq
+    // (the sequence numbers only grow, modulo 2^32).
+    auto reached = [&] { return int32_t(__atomic_load_n(&ctx->sig[0], __ATOMIC_ACQUIRE) - seq) >= 0; };
+    static const auto query_after = std::chrono::microseconds(tuning_size("RSAMD_SIGNAL_QUERY_US", 100));
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t spins = 1;; ++spins) {
-        if (__atomic_load_n(&ctx->sig[0], __ATOMIC_ACQUIRE) == seq) break;
-        if (spins % 64 != 0 || std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(100)) continue;
+        if (reached()) break;
+        if (spins % 64 != 0 || std::chrono::steady_clock::now() - t0 < query_after) continue;
         const hipError_t e = hipStreamQuery(ctx->stream);
         if (e == hipErrorNotReady) {
             (void)hipGetLastError();
             std::this_thread::yield();
             continue;
         }
-        if (__atomic_load_n(&ctx->sig[0], __ATOMIC_ACQUIRE) == seq) break;
+        if (reached()) break;
         if (e != hipSuccess) return hip_fail(e, "small call (hipStreamQuery)");
         return fail(RS_E_HIP, "small call: the stream is idle and the kernel's completion signal is missing");
     }

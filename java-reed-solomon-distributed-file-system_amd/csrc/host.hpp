@@ -111,7 +111,8 @@ constexpr size_t kSignalCtr = 16;  // int index into ThreadCtx::flag of the bloc
 // The context's signal words (allocated on first use) and the next call's
 // sequence number (never 0).
 int next_signal(ThreadCtx *ctx, uint32_t **flag_dev, uint32_t **ctr, uint32_t *seq);
-// Spins until the launch signalled `seq`; *mismatch (may be NULL) gets the
+// Spins until the launch signalled `seq` (or a later launch on the stream its
+// own, higher number); *mismatch (may be NULL) gets the
 // verify word.  A stream that went idle without the signal, or failed, is an
 // error (nothing then spins forever).
 int wait_signal(ThreadCtx *ctx, uint32_t seq, uint32_t *mismatch);

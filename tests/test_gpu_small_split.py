@@ -1,0 +1,88 @@
+"""GPU tests of the split small-call pass (capi.cpp run_small): pageable
+coding calls from 128 KiB to just under 1 MiB per shard run as two signalled
+launches over two page-aligned column ranges of the zero-copy buffer.  The
+cut, the page-aligned slot stride and the zeroed 16-byte tail must never
+change a byte: ragged sizes either side of the threshold, offsets into larger
+arrays, several codes, decodes of every kind of absent set, and threads
+alternating split and one-launch calls (each thread's signal sequence)."""
+import threading
+
+import numpy as np
+import pytest
+from bytes_report import assert_same
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [(128 << 10) - 16, 128 << 10, (128 << 10) + 5, 200_003, 262_151, 777_777, (1 << 20) - 1]
+CODES = [(4, 2), (10, 4), (6, 3), (3, 1)]
+
+
+@pytest.mark.parametrize("k,m", CODES)
+@pytest.mark.parametrize("S", SIZES)
+def test_split_encode_decode(gpu, oracle_lib, k, m, S):
+    import rsamd
+    rng = np.random.default_rng(S * 31 + k * 7 + m)
+    off = int(rng.integers(0, 5000))
+    n = S + off + int(rng.integers(0, 300))
+    sh = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k + m)]
+    ref = [a.copy() for a in sh]
+    rs = rsamd.ReedSolomon.create(k, m)
+    oc = oracle_lib.Codec(k, m)
+    rs.encodeParity(sh, off, S)
+    oc.encode_parity(ref, off, S)
+    assert_same(sh, ref, f"encode k={k} m={m} S={S} off={off}")
+    assert rs.isParityCorrect(sh, off, S)
+    for absent in ({0}, {k + m - 1}, set(range(m)), set(range(k, k + m)) if m else set()):
+        present = [i not in absent for i in range(k + m)]
+        got = [a.copy() for a in sh]
+        for i in absent:
+            got[i][off:off + S] = rng.integers(0, 256, S, dtype=np.uint8)
+        rs.decodeMissing(got, present, off, S)
+        assert_same(got, sh, f"decode {sorted(absent)} k={k} m={m} S={S} off={off}")
+
+
+def test_split_calls_alternate_with_small_ones_in_threads(gpu, oracle_lib):
+    """Four threads, each alternating split calls and one-launch calls (1000 B,
+    64 KiB) on its own shards: every call waits on its own signal numbers."""
+    import rsamd
+    rs = rsamd.ReedSolomon.create(4, 2)
+    oc = oracle_lib.Codec(4, 2)
+    errors = []
+
+    def work(t):
+        try:
+            rng = np.random.default_rng(700 + t)
+            for it in range(6):
+                S = [1000, 300_001 + t, 65536, 524_288 + 17 * t][it % 4]
+                sh = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(6)]
+                ref = [a.copy() for a in sh]
+                oc.encode_parity(ref, 0, S)
+                rs.encodeParity(sh, 0, S)
+                assert_same(sh, ref, f"thread {t} encode S={S}")
+                sh[t % 6][:] = 0
+                rs.decodeMissing(sh, [i != t % 6 for i in range(6)], 0, S)
+                assert_same(sh, ref, f"thread {t} decode S={S}")
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    ts = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+    for th in ts:
+        th.start()
+    for th in ts:
+        th.join()
+    assert not errors, errors
+
+
+def test_split_code_some_shards(gpu, oracle_lib):
+    """The CodingLoop-level call on a split size, one input passed twice."""
+    import rsamd
+    rng = np.random.default_rng(41)
+    S = 333_333
+    a = rng.integers(0, 256, S, dtype=np.uint8)
+    b = rng.integers(0, 256, S, dtype=np.uint8)
+    rows = np.array([[3, 7, 11], [1, 2, 250]], dtype=np.uint8)
+    out = [np.zeros(S, np.uint8), np.full(S, 9, np.uint8)]
+    ref = [np.zeros(S, np.uint8), np.zeros(S, np.uint8)]
+    oracle_lib.code_some_shards(7, rows, [a, b, a], ref, 0, S)
+    rsamd.codeSomeShards(rows, [a, b, a], 3, out, 2, 0, S)
+    assert_same(out, ref, '')
