@@ -216,6 +216,20 @@ int run_mirror_host(ThreadCtx *ctx, const std::vector<DevPlan> &plans, int nslot
 // later than the spin does.  *taken = false (nothing done) for plans of more
 // than one launch group or wider than the direct kernels take.
 bool small_signal_enabled() { return rsamd::tuning_size("RSAMD_SMALL_SIGNAL", 1) != 0; }  // TUNING builds: A/B
+// Launches of a split small call (run_small), the bytes per shard from which
+// calls split, and the alignment of the cuts (TUNING builds: A/B knobs).
+size_t small_parts() {
+    static const size_t v = std::min<size_t>(8, std::max<size_t>(1, rsamd::tuning_size("RSAMD_SMALL_PARTS", 2)));
+    return v;
+}
+size_t small_parts_min() {
+    static const size_t v = rsamd::tuning_size("RSAMD_SMALL_PARTS_MIN", size_t(128) << 10);
+    return v;
+}
+size_t small_parts_align() {
+    static const size_t v = std::max<size_t>(256, rsamd::tuning_size("RSAMD_SMALL_PARTS_ALIGN", 4096));
+    return v;
+}
 
 int run_small(ThreadCtx *ctx, const std::vector<DevPlan> &plans, int nslots, const std::vector<int> &in_slots,
               const std::vector<int> &out_slots, uint8_t *const *host, size_t offset, size_t count, Mode mode,
@@ -237,10 +251,8 @@ int run_small(ThreadCtx *ctx, const std::vector<DevPlan> &plans, int nslots, con
     // 25-50 us slower.  Three or four ranges are no better than two; a verify
     // stays one launch (one mismatch word per launch).  TUNING builds:
     // RSAMD_SMALL_PARTS, RSAMD_SMALL_PARTS_MIN, RSAMD_SMALL_PARTS_ALIGN.
-    static const size_t parts_want = std::max<size_t>(1, rsamd::tuning_size("RSAMD_SMALL_PARTS", 2));
-    static const size_t parts_min = rsamd::tuning_size("RSAMD_SMALL_PARTS_MIN", size_t(128) << 10);
-    const size_t parts = mode == Mode::Code && count >= parts_min ? std::min<size_t>(parts_want, 8) : 1;
-    static const size_t cut_align = std::max<size_t>(256, rsamd::tuning_size("RSAMD_SMALL_PARTS_ALIGN", 4096));
+    const size_t parts = mode == Mode::Code && count >= small_parts_min() ? small_parts() : 1;
+    const size_t cut_align = small_parts_align();
     std::vector<size_t> cut(parts + 1, n16);
     cut[0] = 0;
     for (size_t j = 1; j < parts; ++j) cut[j] = std::min(n16, round_up(n16 * j / parts, cut_align));
@@ -725,6 +737,87 @@ int file_encode_direct(const Codec &c, const uint8_t *file, size_t file_len, siz
 // 126 / 85-86, 3 MiB 254 / 175 (profiles/r5/host_sizes_tile8_r5zz.txt).
 // *taken = false when the kernel cannot take the geometry (block % 8, k, m,
 // size).
+// The same pass as two launches over two halves of the block rows (as
+// run_small's split, from 128 KiB per shard): the second half of the file is
+// copied in while the first half is coded, the first half's parity copied out
+// while the second half is coded.  Each half's file bytes and parity sit on
+// pages of their own in the staging buffer.  *taken = false when the kernel
+// refuses the halves' geometry.
+int file_encode_zc_halves(const Codec &c, const uint8_t *file, size_t file_len, size_t blk, uint8_t *const *shards,
+                          size_t S, ThreadCtx *ctx, bool *taken) {
+    *taken = false;
+    const int k = c.k(), m = c.m();
+    const size_t A = small_parts_align(), rows = S / blk, kb = size_t(k) * blk;
+    const size_t r[3] = {0, rows / 2, rows};
+    size_t at = 0, fo[2], flen[2], po[2][rsamd::kMaxOut];
+    for (int h = 0; h < 2; ++h) {
+        const size_t b0 = r[h] * kb;
+        flen[h] = file_len > b0 ? std::min(file_len - b0, (r[h + 1] - r[h]) * kb) : 0;
+        fo[h] = at;
+        at += round_up(std::max<size_t>(flen[h], 1), A);
+    }
+    for (int h = 0; h < 2; ++h)
+        for (int p = 0; p < m; ++p) {
+            po[h][p] = at;
+            at += round_up(std::max<size_t>((r[h + 1] - r[h]) * blk, 1), A);
+        }
+    if (at > (size_t(64) << 20)) return RS_OK;
+    int rc = zero_copy_buffer(ctx, at);
+    if (rc) return rc;
+    std::vector<DevPlan> plans;
+    RS_HIP(c.encode_plan().device_plans(&plans));
+    rsamd::FileDirect d[2];
+    for (int h = 0; h < 2; ++h) {
+        d[h].k = k;
+        d[h].nout = m;
+        d[h].block = blk;
+        d[h].units = (r[h + 1] - r[h]) * blk / 8;
+        d[h].file_len = flen[h];
+        d[h].file = ctx->zc_dev + fo[h];
+        for (int p = 0; p < m; ++p) d[h].out[k + p] = ctx->zc_dev + po[h][p];
+        d[h].tabs = plans[0].tabs;
+        if (!rsamd::file_direct_ok(d[h]) || d[h].units == 0) return RS_OK;
+    }
+    for (int h = 0; h < 2; ++h) {
+        rc = next_signal(ctx, &d[h].sig.flag, &d[h].sig.ctr, &d[h].sig.seq);
+        if (rc) return rc;
+    }
+    *taken = true;
+    const bool pool = at > zc_pool_min();  // (as run_zero_copy)
+    auto copy = [&](std::vector<rsamd::CopyJob> &jobs) {
+        if (pool)
+            rsamd::CopyPool::get().copy(jobs);
+        else
+            rsamd::CopyPool::copy_here(jobs);
+        jobs.clear();
+    };
+    std::vector<rsamd::CopyJob> jobs;
+    for (int h = 0; h < 2; ++h) {
+        if (flen[h]) jobs.push_back({ctx->zc + fo[h], file + r[h] * kb, flen[h]});
+        copy(jobs);
+        bounds::allow(d[h].file, std::max<size_t>(flen[h], 1));
+        for (int p = 0; p < m; ++p) bounds::allow(d[h].out[k + p], d[h].units * 8);
+        const hipError_t e = rsamd::launch_file_encode_direct(d[h], ctx->stream);
+        if (e != hipSuccess) {
+            (void)hipStreamSynchronize(ctx->stream);
+            return hip_fail(e, "launch_file_encode_direct (small file, halves)");
+        }
+    }
+    split_jobs(file, file_len, blk, k, shards, nullptr, 0, 0, rows, &jobs);
+    copy(jobs);
+    for (int h = 0; h < 2; ++h) {
+        rc = wait_signal(ctx, d[h].sig.seq, nullptr);
+        if (rc) {
+            (void)hipStreamSynchronize(ctx->stream);
+            return rc;
+        }
+        for (int p = 0; p < m; ++p)
+            jobs.push_back({shards[k + p] + r[h] * blk, ctx->zc + po[h][p], (r[h + 1] - r[h]) * blk});
+        copy(jobs);
+    }
+    return RS_OK;
+}
+
 int file_encode_zc_split(const Codec &c, const uint8_t *file, size_t file_len, size_t blk, uint8_t *const *shards,
                          size_t S, ThreadCtx *ctx, bool *taken) {
     *taken = false;
@@ -732,6 +825,10 @@ int file_encode_zc_split(const Codec &c, const uint8_t *file, size_t file_len, s
     if (!rsamd::tuning_size("RSAMD_FILE_ZC_SPLIT", 1) || !direct_enabled() || m < 1 || m > rsamd::kMaxOut ||
         k > rsamd::kMaxDirectIn || blk % 8 || S % 8)
         return RS_OK;
+    if (small_signal_enabled() && small_parts() > 1 && S >= small_parts_min() && S % blk == 0 && S / blk >= 2) {
+        int rc = file_encode_zc_halves(c, file, file_len, blk, shards, S, ctx, taken);
+        if (rc || *taken) return rc;
+    }
     const size_t fbytes = round_up(std::max<size_t>(file_len, 1), 256), stride = round_up(S, 256);
     const size_t need = fbytes + size_t(m) * stride;
     if (need > (size_t(64) << 20)) return RS_OK;
@@ -999,6 +1096,72 @@ int file_decode_zc_split(const Codec &c, uint8_t *const *shards, const uint8_t *
     RS_HIP(plan->device_plans(&plans));
     for (const DevPlan &p : plans)
         if (p.nin > rsamd::kMaxDirectIn) return RS_OK;
+    // From 128 KiB per shard: two signalled passes over two halves of the
+    // block rows (as file_encode_zc_halves), each half's slots on pages of
+    // their own; the second half's survivors are copied in while the first
+    // half is coded, the first half's rebuilt shards copied out (and teed into
+    // the file) while the second half is coded.
+    if (small_signal_enabled() && small_parts() > 1 && rows_needed >= 2 && rows_needed * blk >= small_parts_min()) {
+        const size_t A = small_parts_align(), r[3] = {0, rows_needed / 2, rows_needed};
+        size_t base[2], st[2], nh[2], at = 0;
+        for (int h = 0; h < 2; ++h) {
+            nh[h] = (r[h + 1] - r[h]) * blk;
+            st[h] = round_up(round_up(nh[h], 16), A);
+            base[h] = at;
+            at += st[h] * size_t(T);
+        }
+        if (at <= (size_t(64) << 20)) {
+            rc = zero_copy_buffer(ctx, at);
+            if (rc) return rc;
+            rsamd::DirectSignal sg[2];
+            for (rsamd::DirectSignal &g : sg) {
+                rc = next_signal(ctx, &g.flag, &g.ctr, &g.seq);
+                if (rc) return rc;
+            }
+            *taken = true;
+            const bool pool = at > zc_pool_min();  // (as run_zero_copy)
+            auto copy = [&]() {
+                if (pool)
+                    rsamd::CopyPool::get().copy(jobs);
+                else
+                    rsamd::CopyPool::copy_here(jobs);
+                jobs.clear();
+            };
+            for (int h = 0; h < 2; ++h) {
+                const size_t n16 = round_up(nh[h], 16);
+                for (int sidx : surv) {
+                    jobs.push_back({ctx->zc + base[h] + size_t(sidx) * st[h], shards[sidx] + r[h] * blk, nh[h]});
+                    if (n16 > nh[h]) std::memset(ctx->zc + base[h] + size_t(sidx) * st[h] + nh[h], 0, n16 - nh[h]);
+                }
+                copy();
+                rc = code_slots(plans, plan->in_idx(), plan->out_idx(), ctx->zc_dev + base[h], st[h], n16, Mode::Code,
+                                nullptr, ctx->stream, &sg[h]);
+                if (rc) {
+                    (void)hipStreamSynchronize(ctx->stream);
+                    return rc;
+                }
+            }
+            merge_jobs(k, blk, file_out, file_size, src.data(), now, 0, rows_needed, &jobs);
+            copy();
+            for (int h = 0; h < 2; ++h) {
+                rc = wait_signal(ctx, sg[h].seq, nullptr);
+                if (rc) {
+                    (void)hipStreamSynchronize(ctx->stream);
+                    return rc;
+                }
+                for (int sidx : missing) {
+                    const uint8_t *slot = ctx->zc + base[h] + size_t(sidx) * st[h];
+                    if (sidx < k)
+                        tee_jobs(k, blk, file_out, file_size, sidx, slot, shards[sidx] + r[h] * blk, r[h], r[h + 1],
+                                 &jobs);
+                    else
+                        jobs.push_back({shards[sidx] + r[h] * blk, slot, nh[h]});
+                }
+                copy();
+            }
+            return RS_OK;
+        }
+    }
     const size_t n = rows_needed * blk, ss = round_up(std::max<size_t>(n, 1), 256), need = ss * size_t(T);
     if (need > (size_t(64) << 20)) return RS_OK;
     rc = zero_copy_buffer(ctx, need);

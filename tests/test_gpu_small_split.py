@@ -86,3 +86,34 @@ def test_split_code_some_shards(gpu, oracle_lib):
     oracle_lib.code_some_shards(7, rows, [a, b, a], ref, 0, S)
     rsamd.codeSomeShards(rows, [a, b, a], 3, out, 2, 0, S)
     assert_same(out, ref, '')
+
+
+FILES = [(4, 2, 1000, 524_288), (4, 2, 1000, 1_000_003), (4, 2, 1000, 3_999_999), (6, 3, 4096, 2_000_000),
+         (10, 4, 1000, 1_400_000), (3, 1, 8, 600_001), (4, 2, 520, 700_000), (2, 2, 1000, 262_000),
+         (2, 2, 1000, 263_001), (5, 3, 999, 900_000), (1, 1, 1000, 131_072)]
+
+
+@pytest.mark.parametrize("k,m,block,F", FILES)
+def test_split_file_encode(gpu, oracle_lib, k, m, block, F):
+    """The client's file encode on pageable memory at sizes whose shards reach
+    128 KiB (capi.cpp file_encode_zc_halves: two launches over two halves of
+    the block rows), then file decodes (capi.cpp file_decode_zc_split, halves from 128 KiB)
+    of {0}, of the m parity shards and of a data and a parity shard."""
+    import rsamd
+    from rsamd.layout import file_decode_into, file_encode_into, file_layout
+    rng = np.random.default_rng(F + 97 * k + m)
+    data = rng.integers(0, 256, F, dtype=np.uint8)
+    rs = rsamd.ReedSolomon.create(k, m)
+    _, S = file_layout(rs, F, block)
+    sh = [np.full(S, 0xA5, np.uint8) for _ in range(k + m)]
+    file_encode_into(rs, data, sh, block)
+    ref = oracle_lib.Codec(k, m).file_encode(data.tobytes(), block)
+    assert_same([np.stack(sh)], [ref], (k, m, block, F))
+    for absent in ({0}, set(range(k, k + m)), {k - 1, k + m - 1} if m >= 2 else {k - 1}):
+        pres = [i not in absent for i in range(k + m)]
+        got = [a.copy() for a in sh]
+        for i in absent:
+            got[i][:] = 0x3C
+        out = np.zeros(F, np.uint8)
+        file_decode_into(rs, got, pres, S, out, block)
+        assert np.array_equal(out, data), (k, m, block, F, sorted(absent))
