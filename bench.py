@@ -485,8 +485,10 @@ def decode_summary(extra):
         "host_jni_dec_1000B_us": g("host_jni_dec_1000B_us"), "host_jni_enc_4K_us": g("host_jni_enc_4K_us"),
         "cpu_port_dec_1000B_us": g("cpu_port_dec_1000B_us"),
         "host_file_enc_88K_us": g("host_file_enc_88K_us"), "host_file_dec05_88K_us": g("host_file_dec05_88K_us"),
-        "host_enc_64K_us": g("host_enc_64K_us"), "host_enc_1M_us": g("host_enc_1024K_us"),
+        "host_enc_64K_us": g("host_enc_64K_us"), "host_enc_256K_us": g("host_enc_256K_us"),
+        "host_enc_1M_us": g("host_enc_1024K_us"),
         "host_enc_4M_us": g("host_enc_4096K_us"),
+        "host_file_enc_1M_us": g("host_file_enc_1M_us"), "host_file_dec05_1M_us": g("host_file_dec05_1M_us"),
         # N > 1: every rank calling the host API at once
         "host_pinned_all_ranks_GiBps": g("host_inclusive_pinned_encode_all_ranks_GiBps"),
         "host_pageable_all_ranks_GiBps": g("host_inclusive_pageable_encode_all_ranks_GiBps"),
@@ -1853,7 +1855,7 @@ def config0_single_stripe(rsamd, k, m, S=64 << 10, reps=200):
     return out
 
 
-def host_by_size(rsamd, k, m, sizes=(64 << 10, 1 << 20, 4 << 20, 16 << 20)):
+def host_by_size(rsamd, k, m, sizes=(64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20)):
     """Pageable encodeParity per call by shard size (the mid sizes a DFS
     client's files give: the shards are a quarter of the file), microseconds
     per call, each result checked against the oracle (tools/host_sizes.py is
@@ -1875,6 +1877,24 @@ def host_by_size(rsamd, k, m, sizes=(64 << 10, 1 << 20, 4 << 20, 16 << 20)):
         ref = [a.copy() for a in sh[:k]] + [np.zeros(S, np.uint8) for _ in range(m)]
         c_ref.Codec(k, m).encode_parity(ref, 0, S)
         ok = ok and all(np.array_equal(a, b) for a, b in zip(sh, ref))
+    # the client's 1 MiB file (1000-byte blocks): encodeFile, then decodeFile with {0, k+m-1} absent
+    from rsamd.layout import file_decode_into, file_encode_into, file_layout
+    F = 1 << 20
+    data = np.random.default_rng(F).integers(0, 256, F, dtype=np.uint8)
+    _, S = file_layout(rs, F)
+    fsh = [np.zeros(S, np.uint8) for _ in range(k + m)]
+    fout = np.zeros(F, np.uint8)
+    pres = [i not in (0, k + m - 1) for i in range(k + m)]
+    for name, fn in (("host_file_enc_1M_us", lambda: file_encode_into(rs, data, fsh)),
+                     ("host_file_dec05_1M_us", lambda: file_decode_into(rs, fsh, pres, S, fout))):
+        for _ in range(3):
+            fn()
+        t0 = time.perf_counter()
+        for _ in range(50):
+            fn()
+        out[name] = round((time.perf_counter() - t0) / 50 * 1e6, 1)
+    ref = c_ref.Codec(k, m).file_encode(data.tobytes(), 1000)
+    ok = ok and np.array_equal(np.stack(fsh), ref) and np.array_equal(fout, data)
     out["host_by_size_bit_exact"] = bool(ok)
     return out
 
