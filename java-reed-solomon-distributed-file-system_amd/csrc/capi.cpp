@@ -248,10 +248,14 @@ int run_small(ThreadCtx *ctx, const std::vector<DevPlan> &plans, int nslots, con
     // 256 KiB 77 -> 64 us, 512 KiB 130-137 -> 113-117, 768 KiB 171-198 -> 141-148.
     // The cut is on a page boundary: cuts inside a page (the CPU copying into
     // the page whose other half the GPU is reading) made each later launch
-    // 25-50 us slower.  Three or four ranges are no better than two; a verify
-    // stays one launch (one mismatch word per launch).  TUNING builds:
-    // RSAMD_SMALL_PARTS, RSAMD_SMALL_PARTS_MIN, RSAMD_SMALL_PARTS_ALIGN.
-    const size_t parts = mode == Mode::Code && count >= small_parts_min() ? small_parts() : 1;
+    // 25-50 us slower.  Three or four ranges are no better than two.  A
+    // verify splits too, only its last launch signalling: the launches before
+    // leave their mismatches in the device word, which the last one's signal
+    // reports and zeroes.  TUNING builds: RSAMD_SMALL_PARTS,
+    // RSAMD_SMALL_PARTS_MIN, RSAMD_SMALL_PARTS_ALIGN, RSAMD_SMALL_PARTS_VERIFY.
+    static const bool split_verify = rsamd::tuning_size("RSAMD_SMALL_PARTS_VERIFY", 1) != 0;
+    const size_t parts =
+        (mode == Mode::Code || split_verify) && count >= small_parts_min() ? small_parts() : 1;
     const size_t cut_align = small_parts_align();
     std::vector<size_t> cut(parts + 1, n16);
     cut[0] = 0;
@@ -269,6 +273,9 @@ int run_small(ThreadCtx *ctx, const std::vector<DevPlan> &plans, int nslots, con
         rc = next_signal(ctx, &g.flag, &g.ctr, &g.seq);
         if (rc) return rc;
     }
+    size_t last = 0;  // the last non-empty range
+    for (size_t j = 0; j < parts; ++j)
+        if (cut[j] < cut[j + 1]) last = j;
     *taken = true;
     // host copies on this thread; the copy pool only above 2 MiB (as run_zero_copy)
     const bool use_pool = bytes > zc_pool_min();
@@ -295,7 +302,8 @@ int run_small(ThreadCtx *ctx, const std::vector<DevPlan> &plans, int nslots, con
         rsamd::DirectPlan dj = d;
         for (int i = 0; i < dj.nin; ++i) dj.in[i] += lo;
         for (int q = 0; q < dj.nout; ++q) dj.out[q] += lo;
-        const hipError_t e = rsamd::launch_gf_direct(dj, hi - lo, mode, ctx->flag, ctx->stream, nullptr, &sg[j]);
+        const rsamd::DirectSignal *sj = mode == Mode::Verify && j != last ? nullptr : &sg[j];
+        const hipError_t e = rsamd::launch_gf_direct(dj, hi - lo, mode, ctx->flag, ctx->stream, nullptr, sj);
         if (e != hipSuccess) {
             (void)hipStreamSynchronize(ctx->stream);
             return hip_fail(e, "launch_gf_direct (small call)");
@@ -303,7 +311,7 @@ int run_small(ThreadCtx *ctx, const std::vector<DevPlan> &plans, int nslots, con
     }
     for (size_t j = 0; j < parts; ++j) {
         const size_t lo = cut[j], end = std::min(cut[j + 1], count);
-        if (cut[j] == cut[j + 1]) continue;
+        if (cut[j] == cut[j + 1] || (mode == Mode::Verify && j != last)) continue;
         uint32_t mm = 0;
         rc = wait_signal(ctx, sg[j].seq, &mm);
         if (rc) {

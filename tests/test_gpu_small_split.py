@@ -117,3 +117,26 @@ def test_split_file_encode(gpu, oracle_lib, k, m, block, F):
         out = np.zeros(F, np.uint8)
         file_decode_into(rs, got, pres, S, out, block)
         assert np.array_equal(out, data), (k, m, block, F, sorted(absent))
+
+
+@pytest.mark.parametrize("S", [128 << 10, 200_003, 777_777, (1 << 20) - 1])
+def test_split_verify(gpu, oracle_lib, S):
+    """isParityCorrect split in two launches (only the last one signals): a
+    wrong byte in either half, at either side of the cut or at the very end,
+    is found; a correct call after a failed one reads true (the mismatch word
+    the first launch leaves set is reported and zeroed by the last)."""
+    import rsamd
+    rng = np.random.default_rng(S + 5)
+    k, m = 4, 2
+    sh = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
+    oracle_lib.Codec(k, m).encode_parity(sh, 0, S)
+    rs = rsamd.ReedSolomon.create(k, m)
+    assert rs.isParityCorrect(sh, 0, S)
+    n16 = (S + 15) // 16 * 16
+    cut = min(n16, (n16 // 2 + 4095) // 4096 * 4096)
+    for pos in sorted({0, cut - 1, cut, S - 1, S // 3}):
+        for shard in (1, k, k + m - 1):
+            sh[shard][pos] ^= 0x41
+            assert not rs.isParityCorrect(sh, 0, S), (pos, shard)
+            sh[shard][pos] ^= 0x41
+            assert rs.isParityCorrect(sh, 0, S), (pos, shard)
