@@ -226,6 +226,17 @@ size_t small_parts_min() {
     static const size_t v = rsamd::tuning_size("RSAMD_SMALL_PARTS_MIN", size_t(128) << 10);
     return v;
 }
+// Staging bytes above which the small file passes (file_encode_zc_split,
+// file_decode_zc_split) copy with the copy pool: 8 MiB, against 2 MiB for the
+// shard calls (zc_pool_min).  4+2, 3 MiB file, calling thread / pool,
+// alternated: encode 170-174 / 176-187 us, decode {0,5} 151-169 / 170-186;
+// 10+4 3 MiB file 154-156 / 184-200.  The shard calls keep 2 MiB: at 10+4
+// the calling thread lost from 192 KiB per shard (profiles/r6/zcpool_*_r6bk.txt, zcpool2_42_r6bk.txt).
+// TUNING builds: RSAMD_FILE_ZC_POOL_MIN.
+size_t file_zc_pool_min() {
+    static const size_t v = rsamd::tuning_size("RSAMD_FILE_ZC_POOL_MIN", size_t(8) << 20);
+    return v;
+}
 size_t small_parts_align() {
     static const size_t v = std::max<size_t>(256, rsamd::tuning_size("RSAMD_SMALL_PARTS_ALIGN", 4096));
     return v;
@@ -791,7 +802,7 @@ int file_encode_zc_halves(const Codec &c, const uint8_t *file, size_t file_len, 
         if (rc) return rc;
     }
     *taken = true;
-    const bool pool = at > zc_pool_min();  // (as run_zero_copy)
+    const bool pool = at > file_zc_pool_min();
     auto copy = [&](std::vector<rsamd::CopyJob> &jobs) {
         if (pool)
             rsamd::CopyPool::get().copy(jobs);
@@ -864,7 +875,7 @@ int file_encode_zc_split(const Codec &c, const uint8_t *file, size_t file_len, s
         if (rc) return rc;
     }
     *taken = true;
-    const bool pool = need > zc_pool_min();  // (as run_zero_copy: the pool's wake-up costs more below)
+    const bool pool = need > file_zc_pool_min();
     auto copy = [&](const std::vector<rsamd::CopyJob> &jobs) {
         if (pool)
             rsamd::CopyPool::get().copy(jobs);
@@ -1127,7 +1138,7 @@ int file_decode_zc_split(const Codec &c, uint8_t *const *shards, const uint8_t *
                 if (rc) return rc;
             }
             *taken = true;
-            const bool pool = at > zc_pool_min();  // (as run_zero_copy)
+            const bool pool = at > file_zc_pool_min();
             auto copy = [&]() {
                 if (pool)
                     rsamd::CopyPool::get().copy(jobs);
@@ -1175,7 +1186,7 @@ int file_decode_zc_split(const Codec &c, uint8_t *const *shards, const uint8_t *
     rc = zero_copy_buffer(ctx, need);
     if (rc) return rc;
     *taken = true;
-    const bool pool = need > zc_pool_min();  // (as run_zero_copy)
+    const bool pool = need > file_zc_pool_min();
     auto copy = [&](const std::vector<rsamd::CopyJob> &js) {
         if (pool)
             rsamd::CopyPool::get().copy(js);

@@ -5,7 +5,8 @@ files (the DFS client's files are split into shards of a quarter of the
 file, so mid sizes are the common case), GiB/s of data shards and us per
 call, bound to the GPU's NUMA node as bench.py binds its host legs.  One child
 process per TUNING variant; each prints one JSON line.
-  python tools/host_sizes.py [--lib build/ab/tuning/librsamd.so] [--var RSAMD_MIRROR_MIN=1048576 ...]"""
+  python tools/host_sizes.py [--lib build/ab/tuning/librsamd.so] [--var RSAMD_MIRROR_MIN=1048576 ...]
+  (HS_CODE=10,4 in the environment: another code than 4+2)"""
 import argparse
 import json
 import os
@@ -31,7 +32,7 @@ def child():
     import bench
     from oracle import c_ref
     torch.cuda.init()
-    k, m = 4, 2
+    k, m = (int(x) for x in os.environ.get("HS_CODE", "4,2").split(","))
     rs = rsamd.ReedSolomon.create(k, m)
     out, extra = {}, {}
     with bench.gpu_numa_bound(torch, parallel, extra):
